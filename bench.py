@@ -1,0 +1,180 @@
+#!/usr/bin/env python3
+"""UP-Retinex hot-path benchmark (BASELINE.json metric: images/s at 512x512 bs=32).
+
+One step = one MultiScaleUP_Retinex forward over one resident batch of 32
+synthetic 512x512 images per GPU (configs[1]: random-init plain model, fp32;
+--precision fp16 --variant preact_aspp gives configs[2]).  Multi-GPU: one
+process per GPU (torch.distributed.run), each rank processes its own 32-image
+shard with no data-path collective (weak scaling); barrier + synchronize
+bracket the timed region and rank 0 reports the max over ranks.
+
+Extra objects on the JSON line:
+  roofline      the implicit-GEMM conv kernel family (conv_igemm_kernel<*>),
+                timed live with HIP events around every launch on the model's
+                stream inside the timed region (upr_model_profile)
+  cpu_baseline  the CPU oracle forward (oracle/net.py, torch-CPU fp32) on the
+                host cores, rank 0 only, on a bounded sample
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "retinex-image-enhancement_amd")
+for _p in (PKG, REPO):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+
+PEAK_TFLOPS = {"fp32": 157.3, "fp16": 2516.6}   # MI355X dense MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+REF_GFLOP_PER_IMG = {"plain": 105.6, "preact_aspp": 123.4}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32, help="images per GPU")
+    ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--precision", choices=["fp32", "fp16"], default="fp32")
+    ap.add_argument("--variant", choices=["plain", "preact_aspp"], default="plain")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline budget (0 = skip)")
+    ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events")
+    ap.add_argument("--breakdown", action="store_true", help="print per-layer stats to stderr")
+    return ap.parse_args()
+
+
+def cpu_baseline(sd, pre, aspp, size, budget_s):
+    """Oracle forward on host cores, one image at a time, until the budget is spent."""
+    from oracle import net as onet  # checker / baseline only
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    x = torch.rand(1, 3, size, size, generator=torch.Generator().manual_seed(99))
+    with torch.no_grad():
+        onet.forward(sd, x, pre, aspp)  # warm-up
+        n, t0 = 0, time.perf_counter()
+        while True:
+            onet.forward(sd, x, pre, aspp)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= budget_s or n >= 64:
+                break
+    return {"value": n / el, "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{n} x 1x3x{size}x{size} fp32 forwards of oracle/net.py (torch-CPU), {el:.1f}s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from models.model import UP_Retinex
+    pre = aspp = args.variant == "preact_aspp"
+    torch.manual_seed(0)
+    model = UP_Retinex(use_preact=pre, use_aspp=aspp).eval()
+    sd_cpu = {k: v.clone() for k, v in model.state_dict().items()}
+    dt = torch.float16 if args.precision == "fp16" else torch.float32
+    model = model.to(dev)
+    if args.precision == "fp16":
+        model = model.half()
+    B, S = args.batch, args.size
+    g = torch.Generator().manual_seed(1 + rank)
+    x = torch.rand(B, 3, S, S, generator=g).to(dev, dt)
+
+    def step():
+        with torch.no_grad():
+            return model(x)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    handle = next(iter(model.__dict__["_upr_cache"].values()))[1]
+    if not args.no_profile:
+        handle.profile(True)
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    stats = handle.profile_read() if not args.no_profile else []
+    handle.profile(False)
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+
+    total_imgs = world * B * args.steps
+    out = {
+        "metric": "images/sec at 512x512 bs=32 (UP-Retinex forward)",
+        "value": total_imgs / elapsed,
+        "unit": "images/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1000.0 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32" if args.precision == "fp32" else "f16 (fp32 accumulate)",
+        "data": "synthetic torch.rand inputs, random-init weights (torch.manual_seed(0))",
+        "config": {"workload": f"configs[{1 if args.precision == 'fp32' else 2}]: bs={B}/GPU {S}x{S} "
+                               f"{args.variant} forward, {args.precision}",
+                   "global_batch": world * B, "image_size": S, "variant": args.variant,
+                   "parallelism": f"batch-shard x{world} (no data-path collective)"},
+    }
+    if stats:
+        gemm = [s for s in stats if s["kind"] == "conv_igemm"]
+        g_ms = sum(s["ms"] for s in gemm)
+        g_calls = sum(s["calls"] for s in gemm)
+        g_flops = sum(s["flops"] for s in gemm)
+        g_bytes = sum(s["bytes"] for s in gemm)
+        all_ms = sum(s["ms"] for s in stats)
+        achieved = g_flops / (g_ms * 1e-3) / 1e12 if g_ms > 0 else 0.0
+        peak = PEAK_TFLOPS[args.precision]
+        out["roofline"] = {
+            "bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
+            "traffic": None,
+            "kernel": "conv_igemm_kernel<*> (all launches of the step)",
+            "launches_per_step": g_calls / args.steps,
+            "avg_launch_us": 1000.0 * g_ms / max(g_calls, 1),
+            "gemm_gflop_per_img": g_flops / (args.steps * B) / 1e9,
+            "gemm_alg_GB_per_img": g_bytes / (args.steps * B) / 1e9,
+            "gemm_share_of_device_time": g_ms / all_ms if all_ms else None,
+            "ref_equiv_tflops": REF_GFLOP_PER_IMG[args.variant] * total_imgs / world / elapsed / 1e3,
+        }
+        if args.breakdown and rank == 0:
+            for s in stats:
+                tf = s["flops"] / (s["ms"] * 1e-3) / 1e12 if s["ms"] else 0
+                gbs = s["bytes"] / (s["ms"] * 1e-3) / 1e9 if s["ms"] else 0
+                print(f"{s['name']:44s} {s['kind']:10s} {s['ms'] / max(s['calls'], 1):9.3f} ms "
+                      f"{tf:8.1f} TF/s {gbs:8.1f} GB/s", file=sys.stderr)
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        out["cpu_baseline"] = cpu_baseline(sd_cpu, pre, aspp, S, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out))
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,149 @@
+/*
+ * upr.h — C ABI of libupr.so, the MI355X (gfx950) UP-Retinex kernel library.
+ *
+ * The reference (xh92117/Retinex-image-Enhancement) has no native code and no
+ * FFI: its hot path is the Python/PyTorch surface below.  Each entry point
+ * names the reference interface it replaces (file:line, relative to the
+ * reference root).  Conventions:
+ *   - every buffer is caller-allocated device memory unless stated otherwise
+ *     (params of upr_model_create are HOST fp32 arrays); the library never
+ *     frees caller memory;
+ *   - `stream` is a hipStream_t passed as void*; launches are stream-ordered
+ *     and never synchronise internally;
+ *   - images are NCHW with C = 3 (the reference's tensor layout), dtype
+ *     UPR_F32 (float) or UPR_F16 (IEEE half);
+ *   - return 0 on success, a hipError_t value (> 0) passed through, or a
+ *     negative UPR_ERR_* code; upr_status_string() describes either.
+ * Thread safety: distinct models / streams may be used concurrently; one model
+ * handle must not be used on two streams at once.
+ */
+#ifndef UPR_H_
+#define UPR_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { UPR_F32 = 0, UPR_F16 = 1 };
+
+enum {
+  UPR_OK = 0,
+  UPR_ERR_ARG = -1,
+  UPR_ERR_SHAPE = -2,
+  UPR_ERR_MISSING_PARAM = -3,
+  UPR_ERR_WORKSPACE = -4,
+  UPR_ERR_UNSUPPORTED = -5
+};
+
+/* model flags */
+enum { UPR_MODEL_IENET_ONLY = 1 };
+
+typedef struct UprModel UprModel;
+
+/* One state_dict entry: reference key name (e.g. "ie_net.enc1.conv1.weight"),
+ * host fp32 data, shape. */
+typedef struct {
+  const char* name;
+  const float* data;
+  int ndim;
+  int64_t shape[4];
+} UprTensorDesc;
+
+/* Replaces constructing + .to(device) + .eval() of MultiScaleUP_Retinex
+ * (models/model.py:375-403) / ResidualIENet (:289-331, flag
+ * UPR_MODEL_IENET_ONLY): packs an eval-mode state_dict (BatchNorm folded,
+ * linear 1x1 chains composed, weights laid out [N][K] in `dtype`) into device
+ * memory owned by the handle.  Keys follow the reference state_dict
+ * (ResidualIENet keys carry the "ie_net." prefix). */
+int upr_model_create(const UprTensorDesc* params, int n_params, int use_preact, int use_aspp, int dtype,
+                     int flags, UprModel** out);
+
+/* Device bytes of workspace upr_model_forward needs for a B x 3 x H x W batch. */
+size_t upr_model_workspace(const UprModel* model, int B, int H, int W);
+
+/* Replaces MultiScaleUP_Retinex.forward (models/model.py:445-455):
+ * x [B,3,H,W] in [0,1], H and W multiples of 8 (>= 16)  ->
+ * enh [B,3,H,W], refl [B,3,H,W], illu [B,1,H,W] (all `dtype` of the model).
+ * With UPR_MODEL_IENET_ONLY (ResidualIENet.forward, :333-360) only `illu` is
+ * written and enh/refl may be NULL. */
+int upr_model_forward(UprModel* model, const void* x, int B, int H, int W, void* enh, void* refl, void* illu,
+                      void* workspace, size_t workspace_bytes, void* stream);
+
+void upr_model_destroy(UprModel* model);
+
+/* Per-op profiling of upr_model_forward (no reference counterpart: the
+ * reference only brackets whole calls with time.time(), simple_enhance.py:165-179).
+ * enable != 0 records a hipEvent pair around every op of every later forward
+ * (stream-ordered, no synchronisation); enable == 0 stops and clears.
+ * upr_model_profile_read waits for the recorded events and returns, per op in
+ * launch order, the calls, summed device milliseconds, summed GEMM flops
+ * (2*M*N*K of the launch) and summed algorithmic bytes. */
+enum { UPR_OP_CONV_IGEMM = 0, UPR_OP_OTHER = 1 };
+typedef struct {
+  char name[64];
+  int kind;
+  int calls;
+  double ms;
+  double flops;
+  double bytes;
+} UprOpStat;
+int upr_model_profile(UprModel* model, int enable);
+int upr_model_profile_read(UprModel* model, UprOpStat* out, int max_ops, int* n_ops);
+
+const char* upr_status_string(int status);
+
+/* Generic NHWC convolution (op-level hook used by the parity tests and by
+ * callers composing their own graphs): y = act(conv(x, w) + bias [+ residual]).
+ * x [B,H,W,Cin] (Cin % 32 == 0), w packed [Cout][kh*kw*Cin] (tap-major, then
+ * channel), bias fp32 [Cout] or NULL, residual [B,Ho,Wo,Cout] or NULL (added
+ * before the ReLU), y [B,Ho,Wo,Cout] with Cout % 32 == 0. */
+int upr_conv2d_nhwc(const void* x, int B, int H, int W, int Cin, const void* w, const float* bias, int Cout, int kh,
+                    int kw, int stride, int pad, int dil, const void* residual, int relu, void* y, int dtype,
+                    void* stream);
+
+/* float -> uint8 exactly as `(x * 255).astype(np.uint8)` on float32
+ * (enhancers/adaptive_params.py:142, letterbox.py:93): truncation, wrap mod
+ * 256, NaN / |x*255| >= 2^31 -> 0.  n elements, any layout. */
+int upr_quantize_u8(const void* x, uint8_t* out, size_t n, int dtype, void* stream);
+
+/* cv2.cvtColor(..., COLOR_RGB2LAB) / (..., COLOR_LAB2RGB) on 8-bit interleaved
+ * pixels (adaptive_params.py:142-145, :158-161 — the reference goes through
+ * BGR, which is the same arithmetic). */
+int upr_rgb2lab_u8(const uint8_t* rgb, uint8_t* lab, size_t npix, void* stream);
+int upr_lab2rgb_u8(const uint8_t* lab, uint8_t* rgb, size_t npix, void* stream);
+
+/* cv2.createCLAHE(clip, (tiles_x, tiles_y)).apply on B planar 8-bit images
+ * [B,H,W] (adaptive_params.py:149-152).  lut_ws: B*tiles_x*tiles_y*256 bytes. */
+int upr_clahe_u8(const uint8_t* src, uint8_t* dst, uint8_t* lut_ws, int B, int H, int W, float clip, int tiles_x,
+                 int tiles_y, void* stream);
+
+/* Fused AdaptiveParameterAdjuster.apply_clahe_enhancement
+ * (adaptive_params.py:121-169) on a batch: enh [B,3,H,W] float -> quantise ->
+ * Lab -> CLAHE(clip, tiles) on L -> RGB -> /255 -> out [B,3,H,W].
+ * Workspace: upr_clahe_enhance_workspace() bytes. */
+size_t upr_clahe_enhance_workspace(int B, int H, int W, int tiles_x, int tiles_y);
+int upr_clahe_enhance(const void* enh, void* out, void* workspace, int B, int H, int W, float clip, int tiles_x,
+                      int tiles_y, int dtype, void* stream);
+
+/* 256-bin histogram of the 8-bit BGR2GRAY image of each x [B,3,H,W] float
+ * (calculate_brightness_features, adaptive_params.py:24-68): hist int32 [B,256]. */
+int upr_gray_hist(const void* x, int32_t* hist, int B, int H, int W, int dtype, void* stream);
+
+/* MultiScaleEnhancer (enhancers/multi_scale.py:17-115) per image:
+ * sums fp64 [B,3] = per-scale feature sums; factor fp64 [B] (nullable);
+ * when enh/out are non-NULL, out = clamp(enh * factor, 0, 1). */
+int upr_multiscale(const void* x, const void* enh, void* out, double* sums, double* factor, int B, int H, int W,
+                   int dtype, void* stream);
+
+/* Host copies of the 8-bit Lab integer tables (for CPU-side verification):
+ * gamma[256], cbrt[3072], yf[512], invgamma[4096] (uint16), rgb2xyz[9], xyz2rgb[9]. */
+void upr_lab_tables(uint16_t* gamma, uint16_t* cbrt, uint16_t* yf, uint16_t* invgamma, int32_t* rgb2xyz,
+                    int32_t* xyz2rgb);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* UPR_H_ */

@@ -1,0 +1,89 @@
+// C ABI of the enhancer kernels (see include/upr.h for the contract of each).
+#include <cstring>
+
+#include "upr_common.h"
+#include "lab_tables.h"
+#include "../../include/upr.h"
+
+namespace upr {
+int launch_clahe_pipeline(const void* enh, void* out, uint8_t* ws, int B, int H, int W, float clip, int tilesX,
+                          int tilesY, int dtype, hipStream_t st);
+size_t clahe_pipeline_ws(int B, int H, int W, int tilesX, int tilesY);
+int launch_clahe_u8(const uint8_t* src, uint8_t* dst, uint8_t* lut, int B, int H, int W, float clip, int tilesX,
+                    int tilesY, hipStream_t st);
+int launch_rgb2lab(const uint8_t* rgb, uint8_t* lab, size_t npix, hipStream_t st);
+int launch_lab2rgb(const uint8_t* lab, uint8_t* rgb, size_t npix, hipStream_t st);
+int launch_quantize(const void* x, uint8_t* out, size_t n, int dtype, hipStream_t st);
+int launch_gray_hist(const void* img, int* hist, int B, int H, int W, int dtype, hipStream_t st);
+int launch_multiscale(const void* x, const void* enh, void* out, double* sums, double* factor, int B, int H, int W,
+                      int dtype, hipStream_t st);
+}  // namespace upr
+
+using namespace upr;
+
+static bool dtype_ok(int dt) { return dt == UPR_F32 || dt == UPR_F16; }
+
+extern "C" {
+
+int upr_quantize_u8(const void* x, uint8_t* out, size_t n, int dtype, void* stream) {
+  if (!x || !out || !dtype_ok(dtype)) return UPR_ERR_ARG;
+  if (n == 0) return UPR_OK;
+  return launch_quantize(x, out, n, dtype, (hipStream_t)stream);
+}
+
+int upr_rgb2lab_u8(const uint8_t* rgb, uint8_t* lab, size_t npix, void* stream) {
+  if (!rgb || !lab) return UPR_ERR_ARG;
+  if (npix == 0) return UPR_OK;
+  return launch_rgb2lab(rgb, lab, npix, (hipStream_t)stream);
+}
+
+int upr_lab2rgb_u8(const uint8_t* lab, uint8_t* rgb, size_t npix, void* stream) {
+  if (!rgb || !lab) return UPR_ERR_ARG;
+  if (npix == 0) return UPR_OK;
+  return launch_lab2rgb(lab, rgb, npix, (hipStream_t)stream);
+}
+
+int upr_clahe_u8(const uint8_t* src, uint8_t* dst, uint8_t* lut_ws, int B, int H, int W, float clip, int tiles_x,
+                 int tiles_y, void* stream) {
+  if (!src || !dst || !lut_ws || B <= 0 || H <= 0 || W <= 0 || tiles_x <= 0 || tiles_y <= 0) return UPR_ERR_ARG;
+  if (tiles_x > W || tiles_y > H) return UPR_ERR_SHAPE;
+  return launch_clahe_u8(src, dst, lut_ws, B, H, W, clip, tiles_x, tiles_y, (hipStream_t)stream);
+}
+
+size_t upr_clahe_enhance_workspace(int B, int H, int W, int tiles_x, int tiles_y) {
+  if (B <= 0 || H <= 0 || W <= 0 || tiles_x <= 0 || tiles_y <= 0) return 0;
+  return clahe_pipeline_ws(B, H, W, tiles_x, tiles_y);
+}
+
+int upr_clahe_enhance(const void* enh, void* out, void* workspace, int B, int H, int W, float clip, int tiles_x,
+                      int tiles_y, int dtype, void* stream) {
+  if (!enh || !out || !workspace || B <= 0 || H <= 0 || W <= 0 || !dtype_ok(dtype)) return UPR_ERR_ARG;
+  if (tiles_x <= 0 || tiles_y <= 0 || tiles_x > W || tiles_y > H) return UPR_ERR_SHAPE;
+  return launch_clahe_pipeline(enh, out, (uint8_t*)workspace, B, H, W, clip, tiles_x, tiles_y, dtype,
+                               (hipStream_t)stream);
+}
+
+int upr_gray_hist(const void* x, int32_t* hist, int B, int H, int W, int dtype, void* stream) {
+  if (!x || !hist || B <= 0 || H <= 0 || W <= 0 || !dtype_ok(dtype)) return UPR_ERR_ARG;
+  return launch_gray_hist(x, hist, B, H, W, dtype, (hipStream_t)stream);
+}
+
+int upr_multiscale(const void* x, const void* enh, void* out, double* sums, double* factor, int B, int H, int W,
+                   int dtype, void* stream) {
+  if (!x || !sums || B <= 0 || H <= 0 || W <= 0 || !dtype_ok(dtype)) return UPR_ERR_ARG;
+  if (H < 8 || W < 8) return UPR_ERR_SHAPE;  // torch.gradient needs >= 2 samples at the 1/4 scale
+  return launch_multiscale(x, enh, out, sums, factor, B, H, W, dtype, (hipStream_t)stream);
+}
+
+void upr_lab_tables(uint16_t* gamma, uint16_t* cbrt, uint16_t* yf, uint16_t* invgamma, int32_t* rgb2xyz,
+                    int32_t* xyz2rgb) {
+  const LabTables& t = lab_tables();
+  if (gamma) memcpy(gamma, t.gamma_b, sizeof(t.gamma_b));
+  if (cbrt) memcpy(cbrt, t.cbrt_b, sizeof(t.cbrt_b));
+  if (yf) memcpy(yf, t.yf_b, sizeof(t.yf_b));
+  if (invgamma) memcpy(invgamma, t.invgamma_b, sizeof(t.invgamma_b));
+  if (rgb2xyz) memcpy(rgb2xyz, t.rgb2xyz, sizeof(t.rgb2xyz));
+  if (xyz2rgb) memcpy(xyz2rgb, t.xyz2rgb, sizeof(t.xyz2rgb));
+}
+
+}  // extern "C"

@@ -1,0 +1,367 @@
+// Implicit-GEMM convolution for gfx950 (CDNA4), NHWC activations.
+//
+// One kernel covers every conv of the UP-Retinex graph that has >= 32 input
+// channels (models/model.py: ResBlock/PreActResBlock convs :106-118/:149-162,
+// ASPP :196-229, UpBlock :261-269, residual head :324-328, EnhancedFAM
+// :29-44) plus ConvTranspose2d(k2,s2) as a pixel-shuffled GEMM.
+//
+//   M = B*Ho*Wo pixels (rows), N = output channels (cols), K = virtual concat of
+//   up to 4 segments, each a kh x kw window over C channels of an NHWC source.
+//
+// Tile: 256 threads = 4 waves of 64.  BM x BN output tile, BK = 32 channels per
+// K step.  A (pixels x channels) and B (weights, [N][K]) are staged through LDS
+// with a register prefetch of the next K step (issue-early / write-late).
+//
+// MFMA: each lane's fragment is 8 consecutive k of one row at k-offset
+// 8*(lane>>4).  fp32 consumes it as 8 x v_mfma_f32_16x16x4_f32 (exact fp32),
+// fp16 as 1 x v_mfma_f32_16x16x32_f16 (fp32 accumulate).  The permutation of k
+// across MFMA k-slots is the same for A and B, so the sum is unchanged.
+#include "upr_common.h"
+
+namespace upr {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+template <typename T> struct Frag;
+template <> struct Frag<float> {
+  static constexpr int EPC = 4;  // elements per 16-byte chunk
+};
+template <> struct Frag<half_t> {
+  static constexpr int EPC = 8;
+};
+
+__device__ __forceinline__ float to_f(float v) { return v; }
+__device__ __forceinline__ float to_f(half_t v) { return (float)v; }
+template <typename T> __device__ __forceinline__ T from_f(float v);
+template <> __device__ __forceinline__ float from_f<float>(float v) { return v; }
+template <> __device__ __forceinline__ half_t from_f<half_t>(float v) { return (half_t)v; }
+
+// XCD-aware bijective remap: consecutive logical tiles land on one XCD (blocks
+// b and b+8 share an XCD under round-robin dispatch; speed only).
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  int q = nwg >> 3, r = nwg & 7;
+  int xcd = bid & 7, idx = bid >> 3;
+  int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + idx;
+}
+
+template <typename T, int WAVES_M, int WAVES_N, int WM, int WN>
+__global__ __launch_bounds__(256) void conv_igemm_kernel(ConvOp op) {
+  constexpr int BK = 32;
+  constexpr int EPC = Frag<T>::EPC;
+  constexpr int CH = BK / EPC;              // 16-byte chunks per row of a K step
+  constexpr int ROWS_PASS = 256 / CH;
+  constexpr int BM = WAVES_M * WM * 16;
+  constexpr int BN = WAVES_N * WN * 16;
+  constexpr int A_IT = BM / ROWS_PASS;
+  constexpr int B_IT = (BN * CH + 255) / 256;
+  constexpr int LDS_ROW = BK + EPC;         // +16 B pad per row
+  static_assert(A_IT >= 1, "tile too small");
+
+  __shared__ __attribute__((aligned(16))) T As[BM * LDS_ROW];
+  __shared__ __attribute__((aligned(16))) T Bs[BN * LDS_ROW];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave % WAVES_M;
+  const int wn = wave / WAVES_M;
+
+  const int M = op.B * op.Ho * op.Wo;
+  const int HW = op.Ho * op.Wo;
+  const int mtiles = (M + BM - 1) / BM;
+  const int ntiles = op.N / BN;
+  const int L = xcd_remap(blockIdx.x, mtiles * ntiles);
+  const int ntile = L % ntiles;
+  const int mtile = L / ntiles;
+  const int m0 = mtile * BM;
+  const int n0 = ntile * BN;
+
+  // ---- per-thread A-load rows ------------------------------------------
+  const int a_chunk = tid % CH;
+  const int a_row0 = tid / CH;
+  int pb[A_IT], py[A_IT], px[A_IT];
+#pragma unroll
+  for (int i = 0; i < A_IT; ++i) {
+    int m = m0 + a_row0 + i * ROWS_PASS;
+    if (m < M) {
+      int b = m / HW, r = m - b * HW;
+      pb[i] = b;
+      py[i] = r / op.Wo;
+      px[i] = r - py[i] * op.Wo;
+    } else {
+      pb[i] = -1; py[i] = 0; px[i] = 0;
+    }
+  }
+
+  // ---- K-step cursor ------------------------------------------------------
+  int total_steps = 0;
+  for (int s = 0; s < op.nseg; ++s) total_steps += op.seg[s].kh * op.seg[s].kw * (op.seg[s].C / BK);
+
+  uint4 ra[A_IT];
+  uint4 rb[B_IT];
+
+  int cur_seg = 0, cur_tap = 0, cur_c0 = 0;
+
+  auto load_step = [&](int seg_i, int tap, int c0) {
+    const ConvSeg& sg = op.seg[seg_i];
+    const int r = tap / sg.kw, s = tap - r * sg.kw;
+    const int cbase = c0 + a_chunk * EPC;
+    const T* src = (const T*)sg.src;
+    float psc[EPC], psh[EPC];
+    if (sg.pre == kPreAffineRelu) {
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) { psc[e] = sg.pre_scale[cbase + e]; psh[e] = sg.pre_shift[cbase + e]; }
+    }
+#pragma unroll
+    for (int i = 0; i < A_IT; ++i) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (pb[i] >= 0) {
+        const int iy = py[i] * sg.stride - sg.pad + r * sg.dil;
+        const int ix = px[i] * sg.stride - sg.pad + s * sg.dil;
+        if (iy >= 0 && iy < sg.Hin && ix >= 0 && ix < sg.Win) {
+          const size_t pix = ((size_t)pb[i] * sg.Hin + iy) * sg.Win + ix;
+          if (sg.pre == kPreMaxPool3) {
+            float mx[EPC];
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) mx[e] = -INFINITY;
+            for (int dy = -1; dy <= 1; ++dy) {
+              const int yy = iy + dy;
+              if (yy < 0 || yy >= sg.Hin) continue;
+              for (int dx = -1; dx <= 1; ++dx) {
+                const int xx = ix + dx;
+                if (xx < 0 || xx >= sg.Win) continue;
+                const size_t p2 = ((size_t)pb[i] * sg.Hin + yy) * sg.Win + xx;
+                uint4 w = *(const uint4*)(src + p2 * sg.cs + sg.coff + cbase);
+                const T* wv = (const T*)&w;
+#pragma unroll
+                for (int e = 0; e < EPC; ++e) mx[e] = fmaxf(mx[e], to_f(wv[e]));
+              }
+            }
+            T* vv = (T*)&v;
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) vv[e] = from_f<T>(mx[e]);
+          } else {
+            v = *(const uint4*)(src + pix * sg.cs + sg.coff + cbase);
+            if (sg.pre == kPreAffineRelu) {
+              T* vv = (T*)&v;
+#pragma unroll
+              for (int e = 0; e < EPC; ++e) vv[e] = from_f<T>(fmaxf(to_f(vv[e]) * psc[e] + psh[e], 0.f));
+            }
+          }
+        }
+      }
+      ra[i] = v;
+    }
+    const int kb = sg.kbase + tap * sg.C + c0;
+    const T* W = (const T*)op.W;
+#pragma unroll
+    for (int j = 0; j < B_IT; ++j) {
+      const int idx = tid + j * 256;
+      if (idx < BN * CH) {
+        const int nrow = idx / CH, ch = idx % CH;
+        rb[j] = *(const uint4*)(W + (size_t)(n0 + nrow) * op.Kpad + kb + ch * EPC);
+      }
+    }
+  };
+  auto advance = [&]() {
+    const ConvSeg& sg = op.seg[cur_seg];
+    cur_c0 += BK;
+    if (cur_c0 >= sg.C) {
+      cur_c0 = 0;
+      if (++cur_tap >= sg.kh * sg.kw) { cur_tap = 0; ++cur_seg; }
+    }
+  };
+
+  f32x4 acc[WM][WN];
+#pragma unroll
+  for (int a = 0; a < WM; ++a)
+#pragma unroll
+    for (int b = 0; b < WN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (total_steps > 0) { load_step(cur_seg, cur_tap, cur_c0); advance(); }
+
+  const int fr = lane & 15;
+  const int fk = (lane >> 4) * 8;
+
+  for (int step = 0; step < total_steps; ++step) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < A_IT; ++i)
+      *(uint4*)(As + (a_row0 + i * ROWS_PASS) * LDS_ROW + a_chunk * EPC) = ra[i];
+#pragma unroll
+    for (int j = 0; j < B_IT; ++j) {
+      const int idx = tid + j * 256;
+      if (idx < BN * CH) *(uint4*)(Bs + (idx / CH) * LDS_ROW + (idx % CH) * EPC) = rb[j];
+    }
+    __syncthreads();
+    if (step + 1 < total_steps) { load_step(cur_seg, cur_tap, cur_c0); advance(); }
+
+    if constexpr (sizeof(T) == 4) {
+      f32x4 af[WM][2], bf[WN][2];
+#pragma unroll
+      for (int a = 0; a < WM; ++a) {
+        const float* p = (const float*)As + (wm * WM * 16 + a * 16 + fr) * LDS_ROW + fk;
+        af[a][0] = *(const f32x4*)p;
+        af[a][1] = *(const f32x4*)(p + 4);
+      }
+#pragma unroll
+      for (int b = 0; b < WN; ++b) {
+        const float* p = (const float*)Bs + (wn * WN * 16 + b * 16 + fr) * LDS_ROW + fk;
+        bf[b][0] = *(const f32x4*)p;
+        bf[b][1] = *(const f32x4*)(p + 4);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int a = 0; a < WM; ++a)
+#pragma unroll
+          for (int b = 0; b < WN; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[a][j >> 2][j & 3], bf[b][j >> 2][j & 3],
+                                                            acc[a][b], 0, 0, 0);
+    } else {
+      f16x8 af[WM], bf[WN];
+#pragma unroll
+      for (int a = 0; a < WM; ++a)
+        af[a] = *(const f16x8*)((const half_t*)As + (wm * WM * 16 + a * 16 + fr) * LDS_ROW + fk);
+#pragma unroll
+      for (int b = 0; b < WN; ++b)
+        bf[b] = *(const f16x8*)((const half_t*)Bs + (wn * WN * 16 + b * 16 + fr) * LDS_ROW + fk);
+#pragma unroll
+      for (int a = 0; a < WM; ++a)
+#pragma unroll
+        for (int b = 0; b < WN; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a], bf[b], acc[a][b], 0, 0, 0);
+    }
+  }
+
+  // ---- epilogue -------------------------------------------------------------
+  const int rq = (lane >> 4) * 4;  // first of this lane's 4 accumulator rows
+  if (op.store == kStoreHeadIllu) {
+    // residual head (models/model.py:324-328, :351-358): per pixel
+    // r = sum_c relu(conv3x3(d1)+b)_c * w2_c + b2 ; illu = sigmoid(mean_c(x) + r)
+#pragma unroll
+    for (int a = 0; a < WM; ++a) {
+      float part[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int b = 0; b < WN; ++b) {
+        const int n = n0 + wn * WN * 16 + b * 16 + fr;
+        const float sc = op.scale ? op.scale[n] : 1.f;
+        const float bi = op.bias ? op.bias[n] : 0.f;
+        const float w2 = op.head_w[n];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) part[i] += fmaxf(acc[a][b][i] * sc + bi, 0.f) * w2;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float v = part[i];
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        v += __shfl_xor(v, 4);
+        v += __shfl_xor(v, 8);
+        part[i] = v;
+      }
+      if (fr == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = m0 + wm * WM * 16 + a * 16 + rq + i;
+          if (m >= M) continue;
+          const int b = m / HW, p = m - b * HW;
+          float x0, x1, x2;
+          if (op.x_f16) {
+            const half_t* x = (const half_t*)op.x_nchw + (size_t)b * 3 * HW + p;
+            x0 = (float)x[0]; x1 = (float)x[HW]; x2 = (float)x[2 * HW];
+          } else {
+            const float* x = op.x_nchw + (size_t)b * 3 * HW + p;
+            x0 = x[0]; x1 = x[HW]; x2 = x[2 * HW];
+          }
+          const float z = (x0 + x1 + x2) / 3.f + (part[i] + op.head_b);
+          const float il = 1.f / (1.f + expf(-z));
+          if (op.illu_f16) ((half_t*)op.illu)[m] = (half_t)il;
+          else op.illu[m] = il;
+        }
+      }
+    }
+    return;
+  }
+
+  const bool one_image = (m0 / HW) == (min(m0 + BM, M) - 1) / HW;
+  T* out = (T*)op.out;
+  const T* res1 = (const T*)op.res1;
+  const T* res2 = (const T*)op.res2;
+#pragma unroll
+  for (int b = 0; b < WN; ++b) {
+    const int n = n0 + wn * WN * 16 + b * 16 + fr;
+    const float sc = op.scale ? op.scale[n] : 1.f;
+    const float bi = op.bias ? op.bias[n] : 0.f;
+    float psum = 0.f;
+#pragma unroll
+    for (int a = 0; a < WM; ++a) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + wm * WM * 16 + a * 16 + rq + i;
+        if (m >= M) continue;
+        float v = acc[a][b][i] * sc + bi;
+        const int img = m / HW;
+        if (op.img_bias) v += op.img_bias[img * op.N + n];
+        if (res1) v += to_f(res1[(size_t)m * op.res1_cs + n]);
+        if (op.relu) v = fmaxf(v, 0.f);
+        if (res2) v += to_f(res2[(size_t)m * op.res2_cs + n]);
+        if (op.store == kStoreConvT2x2) {
+          const int cout = op.N >> 2;
+          const int q = n / cout, co = n - q * cout;
+          const int p = m - img * HW;
+          const int oy = p / op.Wo, ox = p - oy * op.Wo;
+          const int Y = 2 * oy + (q >> 1), X = 2 * ox + (q & 1);
+          const size_t opix = ((size_t)img * 2 * op.Ho + Y) * (2 * op.Wo) + X;
+          out[opix * op.out_cs + op.out_coff + co] = from_f<T>(v);
+        } else {
+          const T tv = from_f<T>(v);
+          out[(size_t)m * op.out_cs + op.out_coff + n] = tv;
+          if (op.pool) {
+            if (one_image) psum += to_f(tv);
+            else atomicAdd(op.pool + img * op.N + n, to_f(tv));
+          }
+        }
+      }
+    }
+    if (op.pool && one_image) {
+      psum += __shfl_xor(psum, 16);
+      psum += __shfl_xor(psum, 32);
+      if (lane < 16) atomicAdd(op.pool + (m0 / HW) * op.N + n, psum);
+    }
+  }
+}
+
+template <typename T, int WAVES_M, int WAVES_N, int WM, int WN>
+static int launch_cfg(const ConvOp& op, hipStream_t stream) {
+  constexpr int BM = WAVES_M * WM * 16;
+  constexpr int BN = WAVES_N * WN * 16;
+  const int M = op.B * op.Ho * op.Wo;
+  if (op.N % BN) return kErrShape;
+  const int grid = ((M + BM - 1) / BM) * (op.N / BN);
+  hipLaunchKernelGGL((conv_igemm_kernel<T, WAVES_M, WAVES_N, WM, WN>), dim3(grid), dim3(256), 0, stream, op);
+  return (int)hipGetLastError();
+}
+
+template <typename T>
+static int launch_t(const ConvOp& op, hipStream_t stream) {
+  if (op.store == kStoreHeadIllu) {
+    if (op.N != 32) return kErrShape;
+    return launch_cfg<T, 4, 1, 4, 2>(op, stream);
+  }
+  if (op.N % 128 == 0 && op.N >= 256) return launch_cfg<T, 2, 2, 4, 4>(op, stream);
+  if (op.N % 64 == 0) return launch_cfg<T, 2, 2, 4, 2>(op, stream);
+  if (op.N % 32 == 0) return launch_cfg<T, 4, 1, 4, 2>(op, stream);
+  return kErrShape;
+}
+
+int launch_conv(const ConvOp& op, int dtype, hipStream_t stream) {
+  if (op.nseg < 1 || op.nseg > 4 || op.B <= 0 || op.Ho <= 0 || op.Wo <= 0) return kErrArg;
+  for (int s = 0; s < op.nseg; ++s)
+    if (op.seg[s].C % 32 || op.seg[s].src == nullptr) return kErrShape;
+  return dtype == kF16 ? launch_t<half_t>(op, stream) : launch_t<float>(op, stream);
+}
+
+}  // namespace upr

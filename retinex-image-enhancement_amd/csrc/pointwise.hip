@@ -1,0 +1,326 @@
+// Small fused kernels around the implicit-GEMM convs (gfx950).
+//
+//  prep_pyramid   bilinear x0.5 / x0.25 (align_corners=False) + MaxPool2 / MaxPool4
+//                 inputs of scale2 / scale3 (models/model.py:388,395,421-422)
+//  conv3_direct   3->32 3x3 conv + bias + ReLU on a planar 3-channel image
+//                 (ie_net.input_layer :298/:335, scale{1,2,3} first conv :382-396)
+//  fam_ca         EnhancedFAM channel attention MLP on pooled sums (:47-53, :88)
+//  fam_mix        y*ca -> [mean_c, max_c] map + 3-channel head projection (:89-93)
+//  fam_sa         7x7 spatial attention conv + sigmoid, scales the projection (:56-59, :94-95)
+//  retinex_tail   sigmoid(head) , R = x/(I+1e-6), R*E + (1-R)*E^2 (:411-412, :430-442)
+#include "upr_common.h"
+
+namespace upr {
+
+__device__ __forceinline__ float ldf(const float* p, size_t i) { return p[i]; }
+__device__ __forceinline__ float ldf(const half_t* p, size_t i) { return (float)p[i]; }
+__device__ __forceinline__ void stf(float* p, size_t i, float v) { p[i] = v; }
+__device__ __forceinline__ void stf(half_t* p, size_t i, float v) { p[i] = (half_t)v; }
+__device__ __forceinline__ float sigmoidf_(float z) { return 1.f / (1.f + expf(-z)); }
+
+// ---------------------------------------------------------------------------
+// prep_pyramid: one thread per (b, c, y, x) of the H/16 image?  No: one thread
+// per pixel of the H/4 image; it writes the H/4 pixel and, when (y,x) % 4 == 0
+// and in range, also the H/16 pixel.
+//   x2  = bilinear(x, 0.5)  -> x2[Y][X]  = mean of x[2Y..2Y+1][2X..2X+1]
+//   x2p = MaxPool2(x2)      (H2 = floor(H/2), H4 = floor(H2/2))
+//   x3  = bilinear(x, 0.25) -> x3[Y][X]  = mean of x[4Y+1..4Y+2][4X+1..4X+2]
+//   x3p = MaxPool4(x3)      (H3 = floor(H/4), H16 = floor(H3/4))
+// ---------------------------------------------------------------------------
+template <typename TI, typename TO>
+__global__ void prep_pyramid_kernel(const TI* __restrict__ x, TO* __restrict__ x2p, TO* __restrict__ x3p,
+                                    int B, int H, int W) {
+  const int H4 = (H / 2) / 2, W4 = (W / 2) / 2;
+  const int H16 = (H / 4) / 4, W16 = (W / 4) / 4;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  const int total = B * 3 * H4 * W4;
+  if (idx >= total) return;
+  const int X = idx % W4;
+  const int Y = (idx / W4) % H4;
+  const int bc = idx / (W4 * H4);
+  const TI* img = x + (size_t)bc * H * W;
+  float m = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int y2 = 2 * Y + i, x2 = 2 * X + j;  // coords in the H/2 image
+      const float a = ldf(img, (size_t)(2 * y2) * W + 2 * x2), b = ldf(img, (size_t)(2 * y2) * W + 2 * x2 + 1);
+      const float c = ldf(img, (size_t)(2 * y2 + 1) * W + 2 * x2), d = ldf(img, (size_t)(2 * y2 + 1) * W + 2 * x2 + 1);
+      const float v = 0.5f * (0.5f * a + 0.5f * b) + 0.5f * (0.5f * c + 0.5f * d);
+      m = fmaxf(m, v);
+    }
+  stf(x2p, idx, m);
+  if ((Y & 3) == 0 && (X & 3) == 0 && (Y >> 2) < H16 && (X >> 2) < W16) {
+    const int Ys = Y >> 2, Xs = X >> 2;
+    float m3 = -INFINITY;
+    for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < 4; ++j) {
+        const int y3 = 4 * Ys + i, x3 = 4 * Xs + j;  // coords in the H/4 image
+        const int r = 4 * y3 + 1, c = 4 * x3 + 1;
+        const float a = ldf(img, (size_t)r * W + c), b = ldf(img, (size_t)r * W + c + 1);
+        const float cc = ldf(img, (size_t)(r + 1) * W + c), d = ldf(img, (size_t)(r + 1) * W + c + 1);
+        const float v = 0.5f * (0.5f * a + 0.5f * b) + 0.5f * (0.5f * cc + 0.5f * d);
+        m3 = fmaxf(m3, v);
+      }
+    stf(x3p, ((size_t)bc * H16 + Ys) * W16 + Xs, m3);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// conv3_direct: planar [B,3,h,w] input -> up to two NHWC [B,h,w,32] outputs,
+// each relu(conv3x3(x; w_k) + b_k).  Weights [nout*32][27] fp32 in (c,ky,kx)
+// order, read as wave-uniform scalars.
+// ---------------------------------------------------------------------------
+template <typename TI, typename TO, int NOUT>
+__global__ __launch_bounds__(256) void conv3_direct_kernel(const TI* __restrict__ x, const float* __restrict__ w,
+                                                           const float* __restrict__ bias, TO* __restrict__ out0,
+                                                           TO* __restrict__ out1, int B, int h, int wd) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  const int total = B * h * wd;
+  if (idx >= total) return;
+  const int ox = idx % wd, oy = (idx / wd) % h, b = idx / (wd * h);
+  float in[27];
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int iy = oy + ky - 1, ix = ox + kx - 1;
+        in[c * 9 + ky * 3 + kx] = (iy >= 0 && iy < h && ix >= 0 && ix < wd)
+                                      ? ldf(x, (((size_t)b * 3 + c) * h + iy) * wd + ix) : 0.f;
+      }
+#pragma unroll
+  for (int o = 0; o < NOUT; ++o) {
+    TO* out = o == 0 ? out0 : out1;
+    TO* dst = out + (size_t)idx * 32;
+#pragma unroll
+    for (int g = 0; g < 32; g += 4) {
+      float r[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int oc = o * 32 + g + j;
+        float s = bias[oc];
+#pragma unroll
+        for (int k = 0; k < 27; ++k) s += in[k] * w[oc * 27 + k];
+        r[j] = fmaxf(s, 0.f);
+      }
+      if constexpr (sizeof(TO) == 4) {
+        *(float4*)(dst + g) = make_float4(r[0], r[1], r[2], r[3]);
+      } else {
+        dst[g] = (TO)r[0]; dst[g + 1] = (TO)r[1]; dst[g + 2] = (TO)r[2]; dst[g + 3] = (TO)r[3];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// fam_ca: ca[b][c] = sigmoid(W2 relu(W1 (pool[b]/HW) + b1) + b2), 32 -> 2 -> 32
+// ---------------------------------------------------------------------------
+__global__ void fam_ca_kernel(const float* __restrict__ pool, const float* __restrict__ w1,
+                              const float* __restrict__ b1, const float* __restrict__ w2,
+                              const float* __restrict__ b2, float* __restrict__ ca, int B, float inv_hw) {
+  const int b = blockIdx.x;
+  const int c = threadIdx.x;  // 32 threads
+  if (b >= B || c >= 32) return;
+  __shared__ float g[32];
+  __shared__ float hdn[2];
+  g[c] = pool[b * 32 + c] * inv_hw;
+  __syncthreads();
+  if (c < 2) {
+    float s = b1[c];
+    for (int k = 0; k < 32; ++k) s += w1[c * 32 + k] * g[k];
+    hdn[c] = fmaxf(s, 0.f);
+  }
+  __syncthreads();
+  ca[b * 32 + c] = sigmoidf_(b2[c] + w2[c * 2 + 0] * hdn[0] + w2[c * 2 + 1] * hdn[1]);
+}
+
+// ---------------------------------------------------------------------------
+// fam_mix: per pixel o = y * ca[b]; mm = [mean_c o, max_c o]; p = P o (3 ch)
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void fam_mix_kernel(const T* __restrict__ y, const float* __restrict__ ca,
+                                                      const float* __restrict__ P, float* __restrict__ mm,
+                                                      float* __restrict__ p, int B, int HW) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= B * HW) return;
+  const int b = idx / HW;
+  const T* yp = y + (size_t)idx * 32;
+  const float* cab = ca + b * 32;
+  float s = 0.f, mx = -INFINITY, p0 = 0.f, p1 = 0.f, p2 = 0.f;
+#pragma unroll
+  for (int c = 0; c < 32; ++c) {
+    const float o = ldf(yp, c) * cab[c];
+    s += o;
+    mx = fmaxf(mx, o);
+    p0 += P[c] * o;
+    p1 += P[32 + c] * o;
+    p2 += P[64 + c] * o;
+  }
+  mm[(size_t)idx * 2] = s / 32.f;
+  mm[(size_t)idx * 2 + 1] = mx;
+  p[(size_t)idx * 3] = p0;
+  p[(size_t)idx * 3 + 1] = p1;
+  p[(size_t)idx * 3 + 2] = p2;
+}
+
+// ---------------------------------------------------------------------------
+// fam_sa: sa = sigmoid(conv7x7([mean,max]) + b), q = sa * p   (zero padding 3)
+// weights w[2][7][7] (channel 0 = mean, 1 = max)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void fam_sa_kernel(const float* __restrict__ mm, const float* __restrict__ p,
+                                                     const float* __restrict__ w, float bias,
+                                                     float* __restrict__ q, int B, int h, int wd) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= B * h * wd) return;
+  const int ox = idx % wd, oy = (idx / wd) % h, b = idx / (wd * h);
+  float s = bias;
+  for (int ky = 0; ky < 7; ++ky) {
+    const int iy = oy + ky - 3;
+    if (iy < 0 || iy >= h) continue;
+    for (int kx = 0; kx < 7; ++kx) {
+      const int ix = ox + kx - 3;
+      if (ix < 0 || ix >= wd) continue;
+      const size_t pi = ((size_t)b * h + iy) * wd + ix;
+      s += w[ky * 7 + kx] * mm[pi * 2] + w[49 + ky * 7 + kx] * mm[pi * 2 + 1];
+    }
+  }
+  const float sa = sigmoidf_(s);
+  q[(size_t)idx * 3] = sa * p[(size_t)idx * 3];
+  q[(size_t)idx * 3 + 1] = sa * p[(size_t)idx * 3 + 1];
+  q[(size_t)idx * 3 + 2] = sa * p[(size_t)idx * 3 + 2];
+}
+
+// bilinear source coordinate, align_corners=False, size-based (in/out ratio)
+__device__ __forceinline__ void src_idx(int d, int in, float scale, int& i0, int& i1, float& l1) {
+  float s = scale * (d + 0.5f) - 0.5f;
+  if (s < 0.f) s = 0.f;
+  i0 = (int)s;
+  if (i0 > in - 1) i0 = in - 1;
+  i1 = i0 + ((i0 < in - 1) ? 1 : 0);
+  l1 = s - (float)i0;
+}
+
+__device__ __forceinline__ float bilerp3(const float* q, int b, int h, int wd, int c, int y0, int y1, float ly,
+                                         int x0, int x1, float lx) {
+  const float* base = q + (size_t)b * h * wd * 3 + c;
+  const float v00 = base[((size_t)y0 * wd + x0) * 3], v01 = base[((size_t)y0 * wd + x1) * 3];
+  const float v10 = base[((size_t)y1 * wd + x0) * 3], v11 = base[((size_t)y1 * wd + x1) * 3];
+  return (1.f - ly) * ((1.f - lx) * v00 + lx * v01) + ly * ((1.f - lx) * v10 + lx * v11);
+}
+
+// ---------------------------------------------------------------------------
+// retinex_tail: per output pixel and channel.
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void retinex_tail_kernel(const T* __restrict__ x, const float* __restrict__ illu_f32,
+                                                           const T* __restrict__ illu_t,
+                                                           const float* __restrict__ q1, const float* __restrict__ q2,
+                                                           const float* __restrict__ q3, const float* __restrict__ cst,
+                                                           T* __restrict__ enh, T* __restrict__ refl,
+                                                           int B, int H, int W, int h2, int w2, int h3, int w3) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= B * H * W) return;
+  const int ox = idx % W, oy = (idx / W) % H, b = idx / (W * H);
+  int ay0, ay1, ax0, ax1, by0, by1, bx0, bx1;
+  float aly, alx, bly, blx;
+  src_idx(oy, h2, (float)h2 / (float)H, ay0, ay1, aly);
+  src_idx(ox, w2, (float)w2 / (float)W, ax0, ax1, alx);
+  src_idx(oy, h3, (float)h3 / (float)H, by0, by1, bly);
+  src_idx(ox, w3, (float)w3 / (float)W, bx0, bx1, blx);
+  const float il = illu_t ? ldf(illu_t, idx) : illu_f32[idx];
+  const size_t HW = (size_t)H * W;
+  const size_t pix = (size_t)oy * W + ox;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    float z = q1[(size_t)idx * 3 + c] + bilerp3(q2, b, h2, w2, c, ay0, ay1, aly, ax0, ax1, alx) +
+              bilerp3(q3, b, h3, w3, c, by0, by1, bly, bx0, bx1, blx) + cst[c];
+    const float e = sigmoidf_(z);
+    const size_t o = ((size_t)b * 3 + c) * HW + pix;
+    const float xv = ldf(x, o);
+    const float r = xv / (il + 1e-6f);
+    stf(refl, o, r);
+    stf(enh, o, r * e + (1.f - r) * (e * e));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host launchers
+// ---------------------------------------------------------------------------
+static inline int grid1d(size_t n) { return (int)((n + 255) / 256); }
+
+int launch_prep(const void* x, void* x2p, void* x3p, int B, int H, int W, int dtype, hipStream_t st) {
+  const int n = B * 3 * ((H / 2) / 2) * ((W / 2) / 2);
+  if (n <= 0) return kErrShape;
+  if (dtype == kF16)
+    hipLaunchKernelGGL((prep_pyramid_kernel<half_t, half_t>), dim3(grid1d(n)), dim3(256), 0, st,
+                       (const half_t*)x, (half_t*)x2p, (half_t*)x3p, B, H, W);
+  else
+    hipLaunchKernelGGL((prep_pyramid_kernel<float, float>), dim3(grid1d(n)), dim3(256), 0, st,
+                       (const float*)x, (float*)x2p, (float*)x3p, B, H, W);
+  return (int)hipGetLastError();
+}
+
+int launch_conv3(const void* x, const float* w, const float* bias, void* out0, void* out1, int B, int h, int wd,
+                 int dtype, hipStream_t st) {
+  const int n = B * h * wd;
+  if (n <= 0) return kErrShape;
+  if (dtype == kF16) {
+    if (out1)
+      hipLaunchKernelGGL((conv3_direct_kernel<half_t, half_t, 2>), dim3(grid1d(n)), dim3(256), 0, st,
+                         (const half_t*)x, w, bias, (half_t*)out0, (half_t*)out1, B, h, wd);
+    else
+      hipLaunchKernelGGL((conv3_direct_kernel<half_t, half_t, 1>), dim3(grid1d(n)), dim3(256), 0, st,
+                         (const half_t*)x, w, bias, (half_t*)out0, (half_t*)nullptr, B, h, wd);
+  } else {
+    if (out1)
+      hipLaunchKernelGGL((conv3_direct_kernel<float, float, 2>), dim3(grid1d(n)), dim3(256), 0, st,
+                         (const float*)x, w, bias, (float*)out0, (float*)out1, B, h, wd);
+    else
+      hipLaunchKernelGGL((conv3_direct_kernel<float, float, 1>), dim3(grid1d(n)), dim3(256), 0, st,
+                         (const float*)x, w, bias, (float*)out0, (float*)nullptr, B, h, wd);
+  }
+  return (int)hipGetLastError();
+}
+
+int launch_fam_ca(const float* pool, const float* w1, const float* b1, const float* w2, const float* b2, float* ca,
+                  int B, int HW, hipStream_t st) {
+  hipLaunchKernelGGL(fam_ca_kernel, dim3(B), dim3(32), 0, st, pool, w1, b1, w2, b2, ca, B, 1.f / (float)HW);
+  return (int)hipGetLastError();
+}
+
+int launch_fam_mix(const void* y, const float* ca, const float* P, float* mm, float* p, int B, int HW, int dtype,
+                   hipStream_t st) {
+  const int n = B * HW;
+  if (dtype == kF16)
+    hipLaunchKernelGGL((fam_mix_kernel<half_t>), dim3(grid1d(n)), dim3(256), 0, st, (const half_t*)y, ca, P, mm, p, B,
+                       HW);
+  else
+    hipLaunchKernelGGL((fam_mix_kernel<float>), dim3(grid1d(n)), dim3(256), 0, st, (const float*)y, ca, P, mm, p, B,
+                       HW);
+  return (int)hipGetLastError();
+}
+
+int launch_fam_sa(const float* mm, const float* p, const float* w, float bias, float* q, int B, int h, int wd,
+                  hipStream_t st) {
+  const int n = B * h * wd;
+  hipLaunchKernelGGL(fam_sa_kernel, dim3(grid1d(n)), dim3(256), 0, st, mm, p, w, bias, q, B, h, wd);
+  return (int)hipGetLastError();
+}
+
+int launch_tail(const void* x, const float* illu_f32, const void* illu_t, const float* q1, const float* q2,
+                const float* q3, const float* cst, void* enh, void* refl, int B, int H, int W, int h2, int w2, int h3,
+                int w3, int dtype, hipStream_t st) {
+  const int n = B * H * W;
+  if (dtype == kF16)
+    hipLaunchKernelGGL((retinex_tail_kernel<half_t>), dim3(grid1d(n)), dim3(256), 0, st, (const half_t*)x, illu_f32,
+                       (const half_t*)illu_t, q1, q2, q3, cst, (half_t*)enh, (half_t*)refl, B, H, W, h2, w2, h3, w3);
+  else
+    hipLaunchKernelGGL((retinex_tail_kernel<float>), dim3(grid1d(n)), dim3(256), 0, st, (const float*)x, illu_f32,
+                       (const float*)illu_t, q1, q2, q3, cst, (float*)enh, (float*)refl, B, H, W, h2, w2, h3, w3);
+  return (int)hipGetLastError();
+}
+
+}  // namespace upr

@@ -1,0 +1,96 @@
+// Shared definitions for the UP-Retinex gfx950 kernel library (libupr.so).
+//
+// Activations live in HBM as NHWC (channels innermost) in the model's storage
+// type T (float or _Float16); accumulation is always fp32.  The C ABI itself
+// (include/upr.h) exposes only plain pointers, sizes and a stream handle.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#define UPR_CHECK_HIP(expr)                                  \
+  do {                                                       \
+    hipError_t _e = (expr);                                  \
+    if (_e != hipSuccess) return (int)_e;                    \
+  } while (0)
+
+namespace upr {
+
+typedef _Float16 half_t;
+
+// Status codes (mirrored in include/upr.h).
+enum : int {
+  kOk = 0,
+  kErrArg = -1,
+  kErrShape = -2,
+  kErrMissingParam = -3,
+  kErrWorkspace = -4,
+  kErrUnsupported = -5,
+};
+
+enum DType : int { kF32 = 0, kF16 = 1 };
+
+// ---------------------------------------------------------------------------
+// Implicit-GEMM convolution descriptor.
+//
+// GEMM view: M = B*Ho*Wo output pixels, N = output channels, K = sum over
+// segments of (kh*kw*C_seg).  A segment is one operand of a "virtual concat":
+// it reads C channels of an NHWC source at channel offset coff (pixel stride
+// cs), through a kh x kw window with its own stride / padding / dilation.  The
+// packed weight matrix is [N][Kpad] (k contiguous), K ordered (segment, tap,
+// channel).
+// ---------------------------------------------------------------------------
+enum SegPre : int {
+  kPreNone = 0,
+  kPreAffineRelu = 1,  // v = max(v*pre_scale[c] + pre_shift[c], 0), in-bounds taps only
+  kPreMaxPool3 = 2,    // 3x3/s1/p1 max-pool of the source (padding ignored), then the tap
+};
+
+struct ConvSeg {
+  const void* src;
+  int C, cs, coff;      // channels read, source pixel stride, channel offset
+  int Hin, Win;
+  int kh, kw, stride, pad, dil;
+  int pre;
+  const float* pre_scale;
+  const float* pre_shift;
+  int kbase;            // first k row of this segment in the packed weights
+};
+
+enum StoreMode : int {
+  kStoreNHWC = 0,       // out[m*out_cs + out_coff + n]
+  kStoreConvT2x2 = 1,   // ConvTranspose2d k2 s2 pixel shuffle: n = (dy*2+dx)*Cout + co
+  kStoreHeadIllu = 2,   // residual head: illu = sigmoid(mean_c(x) + relu(v).w2 + b2) (N == 32)
+};
+
+struct ConvOp {
+  int nseg;
+  ConvSeg seg[4];
+  int B, Ho, Wo, N;
+  int Kpad;
+  const void* W;          // packed weights [N][Kpad], type T
+  const float* scale;     // per output channel (nullable => 1)
+  const float* bias;      // per output channel (nullable => 0)
+  const float* img_bias;  // per (image, channel) [B][N] (nullable)
+  const void* res1; int res1_cs;  // added before ReLU (nullable)
+  int relu;
+  const void* res2; int res2_cs;  // added after ReLU (nullable)
+  void* out; int out_cs, out_coff;
+  int store;
+  float* pool;            // per (image, channel) sum of the stored value (nullable)
+  // kStoreConvT2x2: Cout = N/4, out is [B, 2Ho, 2Wo, out_cs]
+  // kStoreHeadIllu:
+  const float* head_w;    // [32] 1x1 weights
+  float head_b;
+  const float* x_nchw;    // network input (fp32 or T per x_f16), [B,3,Ho,Wo]
+  int x_f16;
+  float* illu;            // [B,1,Ho,Wo] fp32 output (or T when illu_f16)
+  int illu_f16;
+};
+
+int launch_conv(const ConvOp& op, int dtype, hipStream_t stream);
+
+inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+}  // namespace upr

@@ -1,0 +1,82 @@
+"""Drop-in surface of models/model.py (reference models/model.py:11-464):
+state_dict keys/order/values under seeded construction (G1), parameter counts,
+and the no-fallback guarantees of the HIP-only forward."""
+import json
+import os
+
+import pytest
+import torch
+
+from conftest import GOLDEN
+from models import model as M
+
+VARIANTS = [(False, False), (True, False), (False, True), (True, True)]
+
+
+@pytest.fixture(scope="module")
+def g1():
+    with open(os.path.join(GOLDEN, "g1_state_dict.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("pre,aspp", VARIANTS)
+@pytest.mark.parametrize("seed", [0, 1])
+def test_state_dict_g1(g1, pre, aspp, seed):
+    rec = g1[f"pre{int(pre)}_aspp{int(aspp)}_seed{seed}"]
+    torch.manual_seed(seed)
+    m = M.UP_Retinex(use_preact=pre, use_aspp=aspp)
+    sd = m.state_dict()
+    assert list(sd.keys()) == rec["keys"]
+    assert M.count_parameters(m) == rec["n_params"]
+    for k, v in sd.items():
+        r = rec["tensors"][k]
+        assert list(v.shape) == r["shape"], k
+        assert str(v.dtype).replace("torch.", "") == r["dtype"], k
+        t = v.double().reshape(-1)
+        assert abs(float(t.sum()) - r["sum"]) <= 1e-9 * max(1.0, abs(r["sum"])) + 1e-9, k
+        assert abs(float((t * t).sum()) - r["sumsq"]) <= 1e-9 * max(1.0, r["sumsq"]), k
+        assert [float(a) for a in t[:4]] == r["first"], k
+
+
+def test_defaults_and_alias():
+    assert M.UP_Retinex is M.MultiScaleUP_Retinex
+    m = M.UP_Retinex()  # reference default: use_preact=True, use_aspp=True (model.py:375)
+    assert "ie_net.bottleneck.1.aspp_branches.2.0.weight" in m.state_dict()
+    assert m.ie_net.enc1.bn1.num_features == 32  # pre-activation block
+    ie = M.ResidualIENet()
+    assert ie.use_aspp is False and "bottleneck.1.conv1.weight" in ie.state_dict()
+
+
+def test_load_state_dict_roundtrip():
+    torch.manual_seed(3)
+    a = M.UP_Retinex(use_preact=False, use_aspp=True)
+    b = M.UP_Retinex(use_preact=False, use_aspp=True)
+    b.load_state_dict(a.state_dict(), strict=True)
+    for (ka, va), (kb, vb) in zip(a.state_dict().items(), b.state_dict().items()):
+        assert ka == kb and torch.equal(va, vb)
+
+
+def test_cpu_forward_raises_no_fallback():
+    m = M.UP_Retinex(use_preact=False, use_aspp=False).eval()
+    with pytest.raises(RuntimeError, match="ROCm"):
+        m(torch.rand(1, 3, 32, 32))
+    with pytest.raises(RuntimeError, match="ROCm"):
+        m.ie_net(torch.rand(1, 3, 32, 32))
+
+
+def test_fused_submodules_raise():
+    fam = M.EnhancedFAM(32, 32)
+    with pytest.raises(NotImplementedError):
+        fam(torch.rand(1, 32, 8, 8))
+    with pytest.raises(NotImplementedError):
+        M.ResBlock(32, 64, 2)(torch.rand(1, 32, 8, 8))
+    m = M.UP_Retinex()
+    with pytest.raises(NotImplementedError):
+        m.retinex_decompose(torch.rand(1, 3, 8, 8), torch.rand(1, 1, 8, 8))
+
+
+def test_training_mode_raises():
+    m = M.UP_Retinex(use_preact=False, use_aspp=False)  # .train() by default
+    x = torch.rand(1, 3, 32, 32)
+    with pytest.raises((NotImplementedError, RuntimeError)):
+        m(x)

@@ -1,0 +1,253 @@
+"""HIP path vs CPU oracle on the MI355X (run with `-m gpu`).
+
+Tolerances: fp32 model outputs |d| <= 1e-3 per pixel (BASELINE.json north_star);
+integer/byte enhancer stages bit-exact given the same input; fp16 storage +
+fp16 MFMA (fp32 accumulate) reported against the fp32 oracle with its own bound.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import has_gpu
+from oracle import cv_u8
+from oracle import enhancers as oenh
+from oracle import net as onet
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not has_gpu(), reason="needs a ROCm device")]
+
+DEV = "cuda:0"
+VARIANTS = [(False, False), (True, False), (False, True), (True, True)]
+FP32_TOL = 1e-3
+FP16_TOL = 3e-2
+
+
+def vname(pre, aspp):
+    return f"pre{int(pre)}_aspp{int(aspp)}"
+
+
+def make_model(pre, aspp, seed=0):
+    from models.model import UP_Retinex
+    torch.manual_seed(seed)
+    return UP_Retinex(use_preact=pre, use_aspp=aspp).eval()
+
+
+def maxdiff(a, b):
+    return (a.detach().float().cpu() - b.detach().float().cpu()).abs().max().item()
+
+
+# ---------------------------------------------------------------------------
+# op level: implicit-GEMM conv vs torch CPU fp32 conv
+# ---------------------------------------------------------------------------
+CONV_CASES = [
+    # B, H, W, Cin, Cout, k, stride, pad, dil, relu, residual
+    (2, 16, 16, 32, 32, 3, 1, 1, 1, True, False),
+    (2, 16, 24, 32, 64, 3, 2, 1, 1, False, True),
+    (1, 20, 12, 64, 128, 3, 1, 2, 2, True, True),
+    (2, 8, 8, 256, 256, 3, 1, 6, 6, True, False),
+    (1, 16, 16, 128, 256, 1, 2, 0, 1, False, False),
+    (3, 7, 9, 32, 96, 1, 1, 0, 1, True, False),
+    (1, 9, 11, 96, 32, 3, 1, 1, 1, False, True),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_conv2d_nhwc(case, dtype):
+    from upr import runtime
+    B, H, W, Cin, Cout, k, s, p, d, relu, res = case
+    g = torch.Generator().manual_seed(hash(case) & 0xffff)
+    x = torch.randn(B, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, k, k, generator=g) / (Cin * k * k) ** 0.5
+    b = torch.randn(Cout, generator=g)
+    ref = F.conv2d(x, w, b, s, p, d)
+    r = torch.randn_like(ref) if res else None
+    if res:
+        ref = ref + r
+    if relu:
+        ref = F.relu(ref)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV, dtype)
+    wd = runtime.pack_conv_weight(w).to(DEV, dtype)
+    rd = r.permute(0, 2, 3, 1).contiguous().to(DEV, dtype) if res else None
+    y = runtime.conv2d_nhwc(xd, wd, b.to(DEV), k, k, s, p, d, residual=rd, relu=relu)
+    torch.cuda.synchronize()
+    err = maxdiff(y.permute(0, 3, 1, 2), ref)
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+    assert err <= tol, f"conv {case} {dtype}: max|d| {err}"
+
+
+# ---------------------------------------------------------------------------
+# model level: 4 variants at the golden 64x64 B=2 inputs, rect, real crop
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("pre,aspp", VARIANTS)
+def test_model_forward_fp32(golden, pre, aspp):
+    gd = golden(f"g2_forward_{vname(pre, aspp)}.npz")
+    m = make_model(pre, aspp)
+    x = torch.from_numpy(gd["x"])
+    m = m.to(DEV)
+    with torch.no_grad():
+        e, r, i = m(x.to(DEV))
+    torch.cuda.synchronize()
+    assert e.shape == (2, 3, 64, 64) and r.shape == (2, 3, 64, 64) and i.shape == (2, 1, 64, 64)
+    assert e.dtype == torch.float32
+    for name, a in (("enh", e), ("refl", r), ("illu", i)):
+        err = maxdiff(a, torch.from_numpy(gd[name]))
+        assert err <= FP32_TOL, f"{vname(pre, aspp)} {name}: {err}"
+    if "x_low" in gd:
+        with torch.no_grad():
+            e, r, i = m(torch.from_numpy(gd["x_low"]).to(DEV))
+        assert maxdiff(e, torch.from_numpy(gd["enh_low"])) <= FP32_TOL
+        assert maxdiff(i, torch.from_numpy(gd["illu_low"])) <= FP32_TOL
+
+
+def test_model_forward_rect(golden):
+    gd = golden("g2_forward_rect_pre1_aspp1.npz")
+    m = make_model(True, True).to(DEV)
+    with torch.no_grad():
+        e, r, i = m(torch.from_numpy(gd["x"]).to(DEV))
+    assert maxdiff(e, torch.from_numpy(gd["enh"])) <= FP32_TOL
+    assert maxdiff(r, torch.from_numpy(gd["refl"])) <= FP32_TOL
+    assert maxdiff(i, torch.from_numpy(gd["illu"])) <= FP32_TOL
+
+
+def test_model_real_crop(golden):
+    gd = golden("g4_real_crop.npz")
+    x = torch.from_numpy(gd["img_u8"].astype(np.float32) / 255.0).permute(2, 0, 1)[None].contiguous()
+    m = make_model(False, False).to(DEV)
+    with torch.no_grad():
+        e, r, i = m(x.to(DEV))
+    assert maxdiff(e, torch.from_numpy(gd["enh"])) <= FP32_TOL
+    assert maxdiff(i, torch.from_numpy(gd["illu"])) <= FP32_TOL
+
+
+@pytest.mark.parametrize("pre,aspp", [(False, False), (True, True)])
+def test_model_forward_fp16(pre, aspp):
+    m = make_model(pre, aspp)
+    x = torch.rand(2, 3, 96, 128, generator=torch.Generator().manual_seed(4))
+    with torch.no_grad():
+        ref = onet.forward(m.state_dict(), x, pre, aspp)
+        m = m.to(DEV)
+        out = m(x.to(DEV).half())
+    torch.cuda.synchronize()
+    for name, a, b in zip(("enh", "refl", "illu"), out, ref):
+        assert a.dtype == torch.float16
+        err = maxdiff(a, b) / (1.0 if name != "refl" else max(1.0, b.abs().max().item()))
+        print(f"fp16 {vname(pre, aspp)} {name} max|d| = {err:.3e}")
+        assert err <= FP16_TOL, f"fp16 {name}: {err}"
+
+
+def test_ienet_standalone_matches_full():
+    m = make_model(True, True).to(DEV)
+    x = torch.rand(1, 3, 64, 96, generator=torch.Generator().manual_seed(5)).to(DEV)
+    with torch.no_grad():
+        _, _, illu = m(x)
+        illu2 = m.ie_net(x)
+    assert maxdiff(illu, illu2) <= 1e-6
+
+
+def test_batch_independence():
+    """Eval forward is per-image independent (the property batch sharding relies on)."""
+    m = make_model(True, True).to(DEV)
+    x = torch.rand(4, 3, 64, 64, generator=torch.Generator().manual_seed(6)).to(DEV)
+    with torch.no_grad():
+        full = m(x)
+        parts = [m(x[i:i + 1]) for i in range(4)]
+    for k in range(3):
+        cat = torch.cat([p[k] for p in parts])
+        assert maxdiff(full[k], cat) <= 1e-6
+
+
+def test_state_change_repacks():
+    m = make_model(False, False).to(DEV)
+    x = torch.rand(1, 3, 32, 32, generator=torch.Generator().manual_seed(7)).to(DEV)
+    with torch.no_grad():
+        a = m(x)[0].clone()
+        m.output_layer.bias.add_(0.5)
+        b = m(x)[0]
+        ref = onet.forward({k: v.cpu() for k, v in m.state_dict().items()}, x.cpu(), False, False)[0]
+    assert maxdiff(a, b) > 1e-3
+    assert maxdiff(b, ref) <= FP32_TOL
+
+
+def test_bad_shapes_raise():
+    m = make_model(False, False).to(DEV)
+    with pytest.raises(RuntimeError):
+        m(torch.rand(1, 3, 36, 32, device=DEV))  # H % 8 != 0 (reference fails on the skip add too)
+    with pytest.raises(RuntimeError):
+        m(torch.rand(1, 4, 32, 32, device=DEV))
+
+
+# ---------------------------------------------------------------------------
+# enhancer kernels: bit-exact vs the numpy restatement
+# ---------------------------------------------------------------------------
+def test_quantize_u8(golden):
+    from upr import runtime
+    gd = golden("g8_cast_u8.npz")
+    q = runtime.quantize_u8(torch.from_numpy(gd["x"]).to(DEV)).cpu().numpy()
+    np.testing.assert_array_equal(q, gd["u8"])
+    x = torch.randn(100003, generator=torch.Generator().manual_seed(8)) * 3
+    q = runtime.quantize_u8(x.to(DEV)).cpu().numpy()
+    np.testing.assert_array_equal(q, cv_u8.quantize_u8(x.numpy()))
+
+
+def test_lab_roundtrip_kernels():
+    from upr import runtime
+    rng = np.random.default_rng(9)
+    rgb = rng.integers(0, 256, (1 << 20, 3)).astype(np.uint8)
+    rgb[:8] = [[0, 0, 0], [255, 255, 255], [255, 0, 0], [0, 255, 0], [0, 0, 255], [1, 2, 3], [254, 1, 128],
+               [128, 128, 128]]
+    lab = runtime.rgb2lab_u8(torch.from_numpy(rgb).to(DEV)).cpu().numpy()
+    np.testing.assert_array_equal(lab, cv_u8.rgb2lab_u8(rgb))
+    labs = rng.integers(0, 256, (1 << 20, 3)).astype(np.uint8)
+    back = runtime.lab2rgb_u8(torch.from_numpy(labs).to(DEV)).cpu().numpy()
+    np.testing.assert_array_equal(back, cv_u8.lab2rgb_u8(labs))
+
+
+@pytest.mark.parametrize("hw", [(64, 64), (256, 256), (100, 75), (31, 45), (512, 384)])
+def test_clahe_u8(hw):
+    from upr import runtime
+    rng = np.random.default_rng(hw[0] * 1000 + hw[1])
+    H, W = hw
+    imgs = [rng.integers(0, 256, (H, W)).astype(np.uint8),
+            np.clip(rng.normal(60, 20, (H, W)), 0, 255).astype(np.uint8),  # low-light, clipping active
+            np.full((H, W), 100, np.uint8)]
+    src = np.stack(imgs)
+    out = runtime.clahe_u8(torch.from_numpy(src).to(DEV)).cpu().numpy()
+    for b in range(len(imgs)):
+        np.testing.assert_array_equal(out[b], cv_u8.clahe_apply(src[b]), err_msg=f"image {b} {hw}")
+
+
+def test_clahe_enhance_pipeline():
+    from upr import runtime
+    g = torch.Generator().manual_seed(10)
+    x = torch.rand(2, 3, 64, 80, generator=g) * 0.6
+    x[0, :, :4, :4] = 1.2  # wrap-around values
+    out = runtime.clahe_enhance(x.to(DEV)).cpu()
+    ref = oenh.clahe_enhancement(x)
+    assert torch.equal(out, ref), f"max|d| {maxdiff(out, ref)}"
+
+
+def test_gray_hist():
+    from upr import runtime
+    x = torch.rand(3, 3, 50, 70, generator=torch.Generator().manual_seed(11))
+    h = runtime.gray_hist(x.to(DEV)).cpu().numpy()
+    for b in range(3):
+        gray = cv_u8.rgb_to_gray_u8(cv_u8.quantize_u8(x[b].permute(1, 2, 0).numpy()))
+        np.testing.assert_array_equal(h[b], np.bincount(gray.reshape(-1), minlength=256))
+
+
+def test_multiscale_kernel(golden):
+    from upr import runtime
+    gd = golden("g5_multiscale.npz")
+    for tag in ("a", "b"):
+        x = torch.from_numpy(gd[f"{tag}_x"]).to(DEV)
+        _, factor, _ = runtime.multiscale(x)
+        assert abs(factor.item() - float(gd[f"{tag}_factor"])) < 1e-6
+    x = torch.rand(3, 3, 64, 48, generator=torch.Generator().manual_seed(12))
+    enh = torch.rand_like(x)
+    out, factor, _ = runtime.multiscale(x.to(DEV), enh.to(DEV))
+    fac = oenh.multiscale_factor(x)
+    for b in range(3):
+        assert abs(factor[b].item() - fac[b]) < 1e-6
+        ref = torch.clamp(enh[b] * fac[b], 0, 1)
+        assert maxdiff(out[b], ref) <= 1e-6
