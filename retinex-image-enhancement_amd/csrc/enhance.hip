@@ -360,20 +360,33 @@ __global__ __launch_bounds__(256) void ms_sums_kernel(const T* __restrict__ x, d
   if (threadIdx.x == 0) atomicAdd(&sums[b * 3 + scale_idx], red[0]);
 }
 
-// factor[b] = 1 + sum_i w_i * 0.1 * sums[b][i] / (7*h_i*w_i); then clamp(enh*factor, 0, 1)
+// factor[b] = 1 + sum_i w_i * mean_i * 0.1, mean_i = float32(sums[b][i] / (7*h_i*w_i))
+// (torch.mean returns a float32 tensor; .item() widens it; Python accumulates in
+// double, multi_scale.py:310-314)
+__device__ __forceinline__ double ms_factor(const double* sums, int b, double n0, double n1, double n2) {
+  double f = 1.0;
+  f += 0.5 * (double)(float)(sums[b * 3 + 0] / n0) * 0.1;
+  f += 0.3 * (double)(float)(sums[b * 3 + 1] / n1) * 0.1;
+  f += 0.2 * (double)(float)(sums[b * 3 + 2] / n2) * 0.1;
+  return f;
+}
+
+__global__ void ms_factor_kernel(const double* __restrict__ sums, double* __restrict__ factor, int B, double n0,
+                                 double n1, double n2) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) factor[b] = ms_factor(sums, b, n0, n1, n2);
+}
+
+// clamp(enh * float(factor), 0, 1)   (multi_scale.py:317-318)
 template <typename T>
 __global__ __launch_bounds__(256) void scale_clamp_kernel(const T* __restrict__ enh, T* __restrict__ out,
                                                           const double* __restrict__ sums, double n0, double n1,
-                                                          double n2, int CHW, int B, double* __restrict__ factor_out) {
+                                                          double n2, int CHW, int B) {
   const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (size_t)B * CHW) return;
   const int b = (int)(idx / CHW);
-  double f = 1.0;
-  f += 0.5 * (sums[b * 3 + 0] / n0) * 0.1;
-  f += 0.3 * (sums[b * 3 + 1] / n1) * 0.1;
-  f += 0.2 * (sums[b * 3 + 2] / n2) * 0.1;
-  if (factor_out && (idx % CHW) == 0) factor_out[b] = f;
-  const float v = __fmul_rn(ldf(enh, idx), (float)f);
+  const float f = (float)ms_factor(sums, b, n0, n1, n2);
+  const float v = __fmul_rn(ldf(enh, idx), f);
   stf(out, idx, fminf(fmaxf(v, 0.f), 1.f));
 }
 
@@ -492,15 +505,18 @@ int launch_multiscale(const void* x, const void* enh, void* out, double* sums, d
       hipLaunchKernelGGL((ms_sums_kernel<float>), dim3(gx, B), dim3(256), 0, st, (const float*)x, sums, H, W, hs[s],
                          wsz[s], s);
   }
+  const double n0 = 7.0 * hs[0] * wsz[0], n1 = 7.0 * hs[1] * wsz[1], n2 = 7.0 * hs[2] * wsz[2];
+  if (factor)
+    hipLaunchKernelGGL(ms_factor_kernel, dim3((B + 63) / 64), dim3(64), 0, st, (const double*)sums, factor, B, n0, n1,
+                       n2);
   if (enh && out) {
     const size_t n = (size_t)B * 3 * H * W;
-    const double n0 = 7.0 * hs[0] * wsz[0], n1 = 7.0 * hs[1] * wsz[1], n2 = 7.0 * hs[2] * wsz[2];
     if (dtype == kF16)
       hipLaunchKernelGGL((scale_clamp_kernel<half_t>), dim3(g1(n)), dim3(256), 0, st, (const half_t*)enh,
-                         (half_t*)out, sums, n0, n1, n2, 3 * H * W, B, factor);
+                         (half_t*)out, sums, n0, n1, n2, 3 * H * W, B);
     else
       hipLaunchKernelGGL((scale_clamp_kernel<float>), dim3(g1(n)), dim3(256), 0, st, (const float*)enh, (float*)out,
-                         sums, n0, n1, n2, 3 * H * W, B, factor);
+                         sums, n0, n1, n2, 3 * H * W, B);
   }
   return (int)hipGetLastError();
 }
