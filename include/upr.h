@@ -138,6 +138,21 @@ int upr_gray_hist(const void* x, int32_t* hist, int B, int H, int W, int dtype, 
 int upr_multiscale(const void* x, const void* enh, void* out, double* sums, double* factor, int B, int H, int W,
                    int dtype, void* stream);
 
+/* MultiScaleEnhancer.extract_multi_scale_features (multi_scale.py:17-60), one
+ * scale (0: x1, 1: x0.5, 2: x0.25, size int(h*s) x int(w*s)):
+ * out [B,7,hs,ws] = [bilinear image (3), luminance, gradient magnitude (3)]. */
+int upr_multiscale_features(const void* x, void* out, int B, int H, int W, int scale_idx, int dtype, void* stream);
+
+/* ContentAwareEnhancer (enhancers/content_aware.py:19-122) per image of
+ * x [B,3,H,W]: saliency fp32 [B,H,W] (compute_saliency_map, nullable),
+ * attention fp32 [B,H,W] (compute_attention_map, nullable) and, when enh/out
+ * are non-NULL, out = clamp(enh * (1 + 0.2 * attention), 0, 1)
+ * (apply_content_aware_enhancement :93-122, all on the device — the
+ * reference's saliency stays on the CPU, :56-57). */
+size_t upr_content_aware_workspace(int B, int H, int W);
+int upr_content_aware(const void* x, const void* enh, void* out, float* saliency, float* attention, void* workspace,
+                      size_t workspace_bytes, int B, int H, int W, int dtype, void* stream);
+
 /* Host copies of the 8-bit Lab integer tables (for CPU-side verification):
  * gamma[256], cbrt[3072], yf[512], invgamma[4096] (uint16), rgb2xyz[9], xyz2rgb[9]. */
 void upr_lab_tables(uint16_t* gamma, uint16_t* cbrt, uint16_t* yf, uint16_t* invgamma, int32_t* rgb2xyz,

@@ -277,20 +277,27 @@ def laplacian_k1_f64(gray):
 def gaussian_kernel_f64(ksize, sigma):
     if sigma <= 0:
         sigma = ((ksize - 1) * 0.5 - 1) * 0.3 + 0.8
-    x = np.arange(ksize, dtype=np.float64) - (ksize - 1) * 0.5
-    k = np.exp(-0.5 / (sigma * sigma) * x * x)
-    return k / k.sum()
+    scale2x = -0.5 / (sigma * sigma)
+    k = np.zeros(ksize, np.float64)
+    s = 0.0
+    for i in range(ksize):  # getGaussianKernel: t = exp(scale2X*x*x); sum; cd *= 1/sum
+        x = i - (ksize - 1) * 0.5
+        k[i] = np.exp(scale2x * x * x)
+        s += k[i]
+    return k * (1.0 / s)
 
 
 def gaussian_blur_f64(img, ksize=15, sigma=0.0):
+    """sepFilter2D order: RowFilter (taps left to right), then SymmColumnFilter
+    (centre tap first, then k[c+j] * (S[y+j] + S[y-j]))."""
     k = gaussian_kernel_f64(ksize, sigma)
     p = ksize // 2
     a = _pad101(np.asarray(img, np.float64), p)
     H, W = np.asarray(img).shape
-    tmp = np.zeros((H + 2 * p, W), np.float64)
-    for j in range(ksize):
-        tmp += k[j] * a[:, j:j + W]
-    out = np.zeros((H, W), np.float64)
-    for i in range(ksize):
-        out += k[i] * tmp[i:i + H, :]
+    tmp = k[0] * a[:, 0:W]
+    for j in range(1, ksize):
+        tmp = tmp + k[j] * a[:, j:j + W]
+    out = k[p] * tmp[p:p + H, :] + 0.0
+    for j in range(1, p + 1):
+        out = out + k[p + j] * (tmp[p + j:p + j + H, :] + tmp[p - j:p - j + H, :])
     return out

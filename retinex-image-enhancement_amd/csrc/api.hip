@@ -17,6 +17,10 @@ int launch_quantize(const void* x, uint8_t* out, size_t n, int dtype, hipStream_
 int launch_gray_hist(const void* img, int* hist, int B, int H, int W, int dtype, hipStream_t st);
 int launch_multiscale(const void* x, const void* enh, void* out, double* sums, double* factor, int B, int H, int W,
                       int dtype, hipStream_t st);
+int launch_ms_features(const void* x, void* out, int B, int H, int W, int scale_idx, int dtype, hipStream_t st);
+size_t content_aware_ws(int B, int H, int W);
+int launch_content_aware(const void* x, const void* enh, void* out, float* sal_out, float* att_out, uint8_t* ws,
+                         int B, int H, int W, int dtype, hipStream_t st);
 }  // namespace upr
 
 using namespace upr;
@@ -73,6 +77,26 @@ int upr_multiscale(const void* x, const void* enh, void* out, double* sums, doub
   if (!x || !sums || B <= 0 || H <= 0 || W <= 0 || !dtype_ok(dtype)) return UPR_ERR_ARG;
   if (H < 8 || W < 8) return UPR_ERR_SHAPE;  // torch.gradient needs >= 2 samples at the 1/4 scale
   return launch_multiscale(x, enh, out, sums, factor, B, H, W, dtype, (hipStream_t)stream);
+}
+
+int upr_multiscale_features(const void* x, void* out, int B, int H, int W, int scale_idx, int dtype, void* stream) {
+  if (!x || !out || B <= 0 || H <= 0 || W <= 0 || scale_idx < 0 || scale_idx > 2 || !dtype_ok(dtype))
+    return UPR_ERR_ARG;
+  return launch_ms_features(x, out, B, H, W, scale_idx, dtype, (hipStream_t)stream);
+}
+
+size_t upr_content_aware_workspace(int B, int H, int W) {
+  if (B <= 0 || H <= 0 || W <= 0) return 0;
+  return content_aware_ws(B, H, W);
+}
+
+int upr_content_aware(const void* x, const void* enh, void* out, float* saliency, float* attention, void* workspace,
+                      size_t workspace_bytes, int B, int H, int W, int dtype, void* stream) {
+  if (!x || !workspace || B <= 0 || H <= 0 || W <= 0 || !dtype_ok(dtype)) return UPR_ERR_ARG;
+  if ((enh == nullptr) != (out == nullptr)) return UPR_ERR_ARG;
+  if (workspace_bytes < content_aware_ws(B, H, W)) return UPR_ERR_WORKSPACE;
+  return launch_content_aware(x, enh, out, saliency, attention, (uint8_t*)workspace, B, H, W, dtype,
+                              (hipStream_t)stream);
 }
 
 void upr_lab_tables(uint16_t* gamma, uint16_t* cbrt, uint16_t* yf, uint16_t* invgamma, int32_t* rgb2xyz,

@@ -1,0 +1,245 @@
+// Content-aware enhancer kernels (gfx950), enhancers/content_aware.py:19-122.
+//
+//   gray (cv2 BGR2GRAY 8U) -> |Laplacian ksize=1| (CV_64F, BORDER_REFLECT_101)
+//   -> GaussianBlur 15x15 sigma 0 (=> 2.6), CV_64F, REFLECT_101, separable
+//   -> min-max normalise (fp64) -> float32 saliency
+//   attention = saliency * (1 / (luminance + 0.1)), min-max normalised (fp32)
+//   out = clamp(enh * (1 + 0.2 * attention), 0, 1)
+// Per image (the reference runs B = 1 and normalises over the whole tensor).
+// Built with -ffp-contract=off so the fp64/fp32 operation order follows
+// OpenCV's RowFilter / SymmColumnFilter and torch's CPU elementwise ops.
+#include <cfloat>
+#include <cmath>
+
+#include "upr_common.h"
+
+namespace upr {
+
+__device__ __forceinline__ float ldf(const float* p, size_t i) { return p[i]; }
+__device__ __forceinline__ float ldf(const half_t* p, size_t i) { return (float)p[i]; }
+__device__ __forceinline__ void stf(float* p, size_t i, float v) { p[i] = v; }
+__device__ __forceinline__ void stf(half_t* p, size_t i, float v) { p[i] = (half_t)v; }
+
+__device__ __forceinline__ int quant_u8c(float v) {
+  const float t = v * 255.f;
+  if (!(fabsf(t) < 2147483648.f)) return 0;
+  return ((int)t) & 255;
+}
+
+__device__ __forceinline__ int refl101(int i, int n) {
+  if (n == 1) return 0;
+  while (i < 0 || i >= n) i = i < 0 ? -i : 2 * (n - 1) - i;
+  return i;
+}
+
+template <typename T>
+__device__ __forceinline__ int gray_at(const T* img, int H, int W, int y, int x) {
+  const size_t HW = (size_t)H * W, p = (size_t)y * W + x;
+  const int r = quant_u8c(ldf(img, p)), g = quant_u8c(ldf(img, HW + p)), b = quant_u8c(ldf(img, 2 * HW + p));
+  return (b * 1868 + g * 9617 + r * 4899 + (1 << 13)) >> 14;
+}
+
+// |Laplacian| of the 8-bit gray image, fp64
+template <typename T>
+__global__ __launch_bounds__(256) void ca_lap_kernel(const T* __restrict__ x, double* __restrict__ lap, int B, int H,
+                                                     int W) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= B * H * W) return;
+  const int b = idx / (H * W), p = idx - b * H * W;
+  const int y = p / W, xx = p - y * W;
+  const T* img = x + (size_t)b * 3 * H * W;
+  const int c = gray_at(img, H, W, y, xx);
+  const int u = gray_at(img, H, W, refl101(y - 1, H), xx), d = gray_at(img, H, W, refl101(y + 1, H), xx);
+  const int l = gray_at(img, H, W, y, refl101(xx - 1, W)), r = gray_at(img, H, W, y, refl101(xx + 1, W));
+  lap[idx] = fabs((double)(u + l - 4 * c + r + d));
+}
+
+struct GaussK {
+  double k[15];
+};
+
+// RowFilter: s = k0*S[x-7] + k1*S[x-6] + ... (tap order)
+__global__ __launch_bounds__(256) void ca_gauss_rows(const double* __restrict__ in, double* __restrict__ out, int B,
+                                                     int H, int W, GaussK g) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= B * H * W) return;
+  const int row = idx / W, x = idx - row * W;
+  const double* s = in + (size_t)row * W;
+  double acc = g.k[0] * s[refl101(x - 7, W)];
+  for (int k = 1; k < 15; ++k) acc += g.k[k] * s[refl101(x - 7 + k, W)];
+  out[idx] = acc;
+}
+
+// SymmColumnFilter: s = ky[c]*S[y] + 0.0; s += ky[c+k]*(S[y+k] + S[y-k]); + per-block min/max
+__global__ __launch_bounds__(256) void ca_gauss_cols(const double* __restrict__ in, double* __restrict__ out, int H,
+                                                     int W, GaussK g, double* __restrict__ part, int nblk) {
+  const int b = blockIdx.y;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  double mn = DBL_MAX, mx = -DBL_MAX;
+  if (p < H * W) {
+    const int y = p / W, x = p - y * W;
+    const double* img = in + (size_t)b * H * W;
+    double acc = g.k[7] * img[(size_t)y * W + x] + 0.0;
+    for (int k = 1; k <= 7; ++k)
+      acc += g.k[7 + k] * (img[(size_t)refl101(y + k, H) * W + x] + img[(size_t)refl101(y - k, H) * W + x]);
+    out[(size_t)b * H * W + p] = acc;
+    mn = mx = acc;
+  }
+  __shared__ double smn[256], smx[256];
+  smn[threadIdx.x] = mn;
+  smx[threadIdx.x] = mx;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      smn[threadIdx.x] = fmin(smn[threadIdx.x], smn[threadIdx.x + s]);
+      smx[threadIdx.x] = fmax(smx[threadIdx.x], smx[threadIdx.x + s]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    part[((size_t)b * nblk + blockIdx.x) * 2] = smn[0];
+    part[((size_t)b * nblk + blockIdx.x) * 2 + 1] = smx[0];
+  }
+}
+
+template <typename F>
+__global__ void reduce_minmax(const F* __restrict__ part, F* __restrict__ res, int nblk) {
+  const int b = blockIdx.x;
+  __shared__ F smn[256], smx[256];
+  F mn = part[(size_t)b * nblk * 2], mx = part[(size_t)b * nblk * 2 + 1];
+  for (int i = threadIdx.x; i < nblk; i += blockDim.x) {
+    mn = part[((size_t)b * nblk + i) * 2] < mn ? part[((size_t)b * nblk + i) * 2] : mn;
+    mx = part[((size_t)b * nblk + i) * 2 + 1] > mx ? part[((size_t)b * nblk + i) * 2 + 1] : mx;
+  }
+  smn[threadIdx.x] = mn;
+  smx[threadIdx.x] = mx;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      if (smn[threadIdx.x + s] < smn[threadIdx.x]) smn[threadIdx.x] = smn[threadIdx.x + s];
+      if (smx[threadIdx.x + s] > smx[threadIdx.x]) smx[threadIdx.x] = smx[threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) { res[2 * b] = smn[0]; res[2 * b + 1] = smx[0]; }
+}
+
+// saliency (normalised, fp32) and raw attention + per-block fp32 min/max
+template <typename T>
+__global__ __launch_bounds__(256) void ca_att_kernel(const T* __restrict__ x, const double* __restrict__ sal,
+                                                     const double* __restrict__ mm, float* __restrict__ sal_out,
+                                                     float* __restrict__ att, float* __restrict__ part, int H, int W,
+                                                     int nblk) {
+  const int b = blockIdx.y;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  float mn = FLT_MAX, mx = -FLT_MAX;
+  if (p < H * W) {
+    const size_t HW = (size_t)H * W;
+    const double smin = mm[2 * b], smax = mm[2 * b + 1];
+    const float s = (float)((sal[(size_t)b * HW + p] - smin) / (smax - smin + 1e-8));
+    if (sal_out) sal_out[(size_t)b * HW + p] = s;
+    const T* img = x + (size_t)b * 3 * HW;
+    const float lum = 0.299f * ldf(img, p) + 0.587f * ldf(img, HW + p) + 0.114f * ldf(img, 2 * HW + p);
+    const float a = s * (1.0f / (lum + 0.1f));
+    att[(size_t)b * HW + p] = a;
+    mn = mx = a;
+  }
+  __shared__ float smn[256], smx[256];
+  smn[threadIdx.x] = mn;
+  smx[threadIdx.x] = mx;
+  __syncthreads();
+  for (int s2 = 128; s2 > 0; s2 >>= 1) {
+    if (threadIdx.x < s2) {
+      smn[threadIdx.x] = fminf(smn[threadIdx.x], smn[threadIdx.x + s2]);
+      smx[threadIdx.x] = fmaxf(smx[threadIdx.x], smx[threadIdx.x + s2]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    part[((size_t)b * nblk + blockIdx.x) * 2] = smn[0];
+    part[((size_t)b * nblk + blockIdx.x) * 2 + 1] = smx[0];
+  }
+}
+
+// attention normalisation (+ optional enhancement)
+template <typename T>
+__global__ __launch_bounds__(256) void ca_apply_kernel(const float* __restrict__ att, const float* __restrict__ mm,
+                                                       float* __restrict__ att_out, const T* __restrict__ enh,
+                                                       T* __restrict__ out, int B, int HW) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (size_t)B * HW) return;
+  const int b = (int)(idx / HW);
+  const size_t p = idx - (size_t)b * HW;
+  const float mn = mm[2 * b], mx = mm[2 * b + 1];
+  const float a = (att[idx] - mn) / (mx - mn + 1e-8f);
+  if (att_out) att_out[idx] = a;
+  if (enh && out) {
+    const float f = 1.0f + 0.2f * a;
+    for (int c = 0; c < 3; ++c) {
+      const size_t o = ((size_t)b * 3 + c) * HW + p;
+      stf(out, o, fminf(fmaxf(ldf(enh, o) * f, 0.f), 1.f));
+    }
+  }
+}
+
+static inline int gd(size_t n) { return (int)((n + 255) / 256); }
+
+size_t content_aware_ws(int B, int H, int W) {
+  const size_t HW = (size_t)H * W;
+  const size_t nblk = (HW + 255) / 256;
+  return align_up(2 * (size_t)B * HW * 8, 256) + align_up((size_t)B * HW * 4, 256) +
+         align_up((size_t)B * nblk * 2 * 8, 256) + align_up((size_t)B * 2 * 8, 256) + align_up((size_t)B * 2 * 4, 256);
+}
+
+int launch_content_aware(const void* x, const void* enh, void* out, float* sal_out, float* att_out, uint8_t* ws,
+                         int B, int H, int W, int dtype, hipStream_t st) {
+  const size_t HW = (size_t)H * W;
+  const int nblk = (int)((HW + 255) / 256);
+  double* lap = (double*)ws;
+  double* tmp = lap + (size_t)B * HW;
+  uint8_t* p = ws + align_up(2 * (size_t)B * HW * 8, 256);
+  float* att = (float*)p;
+  p += align_up((size_t)B * HW * 4, 256);
+  double* part64 = (double*)p;
+  float* part32 = (float*)p;
+  p += align_up((size_t)B * nblk * 2 * 8, 256);
+  double* mm64 = (double*)p;
+  p += align_up((size_t)B * 2 * 8, 256);
+  float* mm32 = (float*)p;
+  // Gaussian kernel: getGaussianKernel(15, 0 -> 2.6, CV_64F)
+  GaussK g;
+  const double sigma = ((15 - 1) * 0.5 - 1) * 0.3 + 0.8;
+  const double scale2X = -0.5 / (sigma * sigma);
+  double sum = 0.0;
+  for (int i = 0; i < 15; ++i) {
+    const double xx = i - (15 - 1) * 0.5;
+    g.k[i] = std::exp(scale2X * xx * xx);
+    sum += g.k[i];
+  }
+  sum = 1. / sum;
+  for (int i = 0; i < 15; ++i) g.k[i] *= sum;
+  const size_t n = (size_t)B * HW;
+  if (dtype == kF16)
+    hipLaunchKernelGGL((ca_lap_kernel<half_t>), dim3(gd(n)), dim3(256), 0, st, (const half_t*)x, lap, B, H, W);
+  else
+    hipLaunchKernelGGL((ca_lap_kernel<float>), dim3(gd(n)), dim3(256), 0, st, (const float*)x, lap, B, H, W);
+  hipLaunchKernelGGL(ca_gauss_rows, dim3(gd(n)), dim3(256), 0, st, lap, tmp, B, H, W, g);
+  hipLaunchKernelGGL(ca_gauss_cols, dim3(nblk, B), dim3(256), 0, st, tmp, lap, H, W, g, part64, nblk);
+  hipLaunchKernelGGL((reduce_minmax<double>), dim3(B), dim3(256), 0, st, part64, mm64, nblk);
+  if (dtype == kF16)
+    hipLaunchKernelGGL((ca_att_kernel<half_t>), dim3(nblk, B), dim3(256), 0, st, (const half_t*)x, lap, mm64, sal_out,
+                       att, part32, H, W, nblk);
+  else
+    hipLaunchKernelGGL((ca_att_kernel<float>), dim3(nblk, B), dim3(256), 0, st, (const float*)x, lap, mm64, sal_out,
+                       att, part32, H, W, nblk);
+  hipLaunchKernelGGL((reduce_minmax<float>), dim3(B), dim3(256), 0, st, part32, mm32, nblk);
+  if (dtype == kF16)
+    hipLaunchKernelGGL((ca_apply_kernel<half_t>), dim3(gd(n)), dim3(256), 0, st, att, mm32, att_out,
+                       (const half_t*)enh, (half_t*)out, B, (int)HW);
+  else
+    hipLaunchKernelGGL((ca_apply_kernel<float>), dim3(gd(n)), dim3(256), 0, st, att, mm32, att_out,
+                       (const float*)enh, (float*)out, B, (int)HW);
+  return (int)hipGetLastError();
+}
+
+}  // namespace upr

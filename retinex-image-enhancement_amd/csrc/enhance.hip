@@ -521,4 +521,51 @@ int launch_multiscale(const void* x, const void* enh, void* out, double* sums, d
   return (int)hipGetLastError();
 }
 
+// Feature maps of one scale: out [B,7,hs,ws] = [img_s (3), luminance, |grad| (3)]
+// (MultiScaleEnhancer.extract_multi_scale_features, multi_scale.py:17-60)
+template <typename T>
+__global__ __launch_bounds__(256) void ms_features_kernel(const T* __restrict__ x, T* __restrict__ out, int B, int H,
+                                                          int W, int hs, int ws) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= B * hs * ws) return;
+  const int b = idx / (hs * ws), p = idx - b * hs * ws;
+  const int y = p / ws, xx = p - y * ws;
+  const T* img = x + (size_t)b * 3 * H * W;
+  const float sy = (float)H / (float)hs, sx = (float)W / (float)ws;
+  T* o = out + (size_t)b * 7 * hs * ws + p;
+  const size_t plane = (size_t)hs * ws;
+  float c3[3];
+  for (int c = 0; c < 3; ++c) {
+    const T* ch = img + (size_t)c * H * W;
+    const float v = sample_s(ch, H, W, hs, ws, sy, sx, y, xx);
+    c3[c] = v;
+    float gx, gy;
+    if (ws < 2) gx = 0.f;
+    else if (xx == 0) gx = sample_s(ch, H, W, hs, ws, sy, sx, y, 1) - v;
+    else if (xx == ws - 1) gx = v - sample_s(ch, H, W, hs, ws, sy, sx, y, ws - 2);
+    else gx = (sample_s(ch, H, W, hs, ws, sy, sx, y, xx + 1) - sample_s(ch, H, W, hs, ws, sy, sx, y, xx - 1)) / 2.f;
+    if (hs < 2) gy = 0.f;
+    else if (y == 0) gy = sample_s(ch, H, W, hs, ws, sy, sx, 1, xx) - v;
+    else if (y == hs - 1) gy = v - sample_s(ch, H, W, hs, ws, sy, sx, hs - 2, xx);
+    else gy = (sample_s(ch, H, W, hs, ws, sy, sx, y + 1, xx) - sample_s(ch, H, W, hs, ws, sy, sx, y - 1, xx)) / 2.f;
+    stf(o, c * plane, v);
+    stf(o, (4 + c) * plane, sqrtf(gx * gx + gy * gy));
+  }
+  stf(o, 3 * plane, 0.299f * c3[0] + 0.587f * c3[1] + 0.114f * c3[2]);
+}
+
+int launch_ms_features(const void* x, void* out, int B, int H, int W, int scale_idx, int dtype, hipStream_t st) {
+  const double sc = scale_idx == 0 ? 1.0 : (scale_idx == 1 ? 0.5 : 0.25);
+  const int hs = scale_idx == 0 ? H : (int)(H * sc), wsz = scale_idx == 0 ? W : (int)(W * sc);
+  if (hs < 1 || wsz < 1) return kErrShape;
+  const size_t n = (size_t)B * hs * wsz;
+  if (dtype == kF16)
+    hipLaunchKernelGGL((ms_features_kernel<half_t>), dim3(g1(n)), dim3(256), 0, st, (const half_t*)x, (half_t*)out, B,
+                       H, W, hs, wsz);
+  else
+    hipLaunchKernelGGL((ms_features_kernel<float>), dim3(g1(n)), dim3(256), 0, st, (const float*)x, (float*)out, B,
+                       H, W, hs, wsz);
+  return (int)hipGetLastError();
+}
+
 }  // namespace upr

@@ -1,0 +1,129 @@
+"""Enhance harness (drop-in for reference enhancers/simple_enhance.py).
+
+Image decode/encode stays on the host (PIL), everything between load and save
+runs on the device.  Intentional divergences, each a reference bug:
+  * enhance_single_image accepts and ignores `adjuster=` so main.py's
+    single-file branch works (reference main.py:240-249 vs simple_enhance.py:135
+    raises TypeError);
+  * enhance_batch_images takes optional use_preact/use_aspp/seed (defaults keep
+    the reference behaviour: UP_Retinex() defaults, unseeded init).
+"""
+import os
+import time
+
+import numpy as np
+import torch
+from PIL import Image
+
+from models.model import UP_Retinex
+from enhancers.adaptive_params import AdaptiveParameterAdjuster
+from enhancers.multi_scale import MultiScaleEnhancer
+from enhancers.content_aware import ContentAwareEnhancer
+from utils.letterbox import letterbox_tensor
+
+VALID_EXTENSIONS = {'.jpg', '.jpeg', '.png', '.bmp', '.tif', '.tiff'}
+
+
+def _to_tensor(img):
+    """torchvision ToTensor for an RGB PIL image: uint8 HWC -> float32 CHW / 255."""
+    a = np.asarray(img, dtype=np.uint8)
+    return torch.from_numpy(np.ascontiguousarray(a.transpose(2, 0, 1))).float().div(255)
+
+
+def load_image(image_path, max_size=None):
+    """Decode, letterbox (reference :23-62) -> ([1,3,H,W] float32, (W, H))."""
+    img = Image.open(image_path).convert('RGB')
+    original_size = img.size
+    t = _to_tensor(img)
+    new_shape = max_size if max_size is not None else tuple(t.shape[1:])
+    t, _, _ = letterbox_tensor(t, new_shape=new_shape, auto=True, scaleup=False)
+    return t.unsqueeze(0), original_size
+
+
+def _to_u8_hwc(t):
+    a = t.detach().float().cpu().numpy()
+    if a.shape[0] == 1:
+        a = np.clip(a[0], 0, 1)
+        a = (a * 255).astype(np.uint8)
+        return np.stack([a, a, a], axis=2)
+    a = np.clip(np.transpose(a, (1, 2, 0)), 0, 1)
+    return (a * 255).astype(np.uint8)
+
+
+def save_image(tensor, save_path):
+    """[1,C,H,W] or [C,H,W] -> PNG; 1-channel maps are replicated to RGB (reference :65-99)."""
+    if tensor.dim() == 4:
+        tensor = tensor.squeeze(0)
+    Image.fromarray(_to_u8_hwc(tensor)).save(save_path)
+    print(f"已保存: {save_path}")
+
+
+def create_comparison(img_low, img_enhanced, save_path):
+    """[input | enhanced] side by side (reference :102-132)."""
+    a = _to_u8_hwc(img_low.squeeze(0))
+    b = _to_u8_hwc(img_enhanced.squeeze(0))
+    Image.fromarray(np.concatenate([a, b], axis=1)).save(save_path)
+    print(f"已保存对比图像: {save_path}")
+
+
+def enhance_single_image(model, image_path, output_dir, device, max_size=None, enable_multi_scale=False,
+                         enable_content_aware=False, adjuster=None, precision="fp32"):
+    """Enhance one file and write {name}_enhanced/_illumination/_comparison.png (reference :135-199).
+    precision="fp16" runs the fp16 storage / fp16-MFMA graph (input cast to half)."""
+    print(f"正在处理: {os.path.basename(image_path)}")
+    img_low, _ = load_image(image_path, max_size)
+    if precision == "fp16":
+        img_low = img_low.half()
+    adjuster = AdaptiveParameterAdjuster()
+    multi_scale_enhancer = MultiScaleEnhancer()
+    content_aware_enhancer = ContentAwareEnhancer()
+    start = time.time()
+    if enable_content_aware:
+        img_enhanced, illu_map = content_aware_enhancer.apply_content_aware_enhancement(model, img_low, device)
+    elif enable_multi_scale:
+        img_enhanced, illu_map = multi_scale_enhancer.enhance_with_pyramid(model, img_low, device)
+    else:
+        img_enhanced, illu_map = adjuster.apply_adaptive_enhancement(model, img_low, device)
+    if torch.cuda.is_available() and img_enhanced.is_cuda:
+        torch.cuda.synchronize(img_enhanced.device)
+    print(f"增强耗时: {time.time() - start:.4f}s")
+    os.makedirs(output_dir, exist_ok=True)
+    name = os.path.splitext(os.path.basename(image_path))[0]
+    save_image(img_enhanced, os.path.join(output_dir, f"{name}_enhanced.png"))
+    save_image(illu_map, os.path.join(output_dir, f"{name}_illumination.png"))
+    create_comparison(img_low, img_enhanced, os.path.join(output_dir, f"{name}_comparison.png"))
+    print("图像增强完成！")
+    return img_enhanced, illu_map
+
+
+def list_images(input_dir):
+    files = [os.path.join(input_dir, f) for f in os.listdir(input_dir)
+             if os.path.splitext(f)[1].lower() in VALID_EXTENSIONS]
+    return sorted(files)
+
+
+def enhance_batch_images(input_dir, output_dir, device, max_size=None, use_preact=True, use_aspp=True, seed=None,
+                         precision="fp32"):
+    """Enhance every image of a directory (reference :202-250)."""
+    print("正在加载模型...")
+    if seed is not None:
+        torch.manual_seed(seed)
+    model = UP_Retinex(use_preact=use_preact, use_aspp=use_aspp).to(device).eval()
+    image_files = list_images(input_dir)
+    if not image_files:
+        print(f"在目录 '{input_dir}' 中未找到有效图像文件")
+        return
+    print(f"找到 {len(image_files)} 个图像文件")
+    print("=" * 50)
+    total = 0.0
+    for i, path in enumerate(image_files, 1):
+        print(f"[{i}/{len(image_files)}]")
+        t0 = time.time()
+        enhance_single_image(model, path, output_dir, device, max_size, precision=precision)
+        total += time.time() - t0
+        print("-" * 50)
+    print("=" * 50)
+    print(f"总共处理了 {len(image_files)} 张图像")
+    print(f"总耗时: {total:.2f}s")
+    print(f"平均每张图像耗时: {total / len(image_files):.4f}s")
+    print("=" * 50)

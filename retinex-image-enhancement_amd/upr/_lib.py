@@ -66,6 +66,10 @@ SIGNATURES = {
     "upr_gray_hist": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "upr_multiscale": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                c_void_p]),
+    "upr_multiscale_features": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
+    "upr_content_aware_workspace": (c_size_t, [c_int, c_int, c_int]),
+    "upr_content_aware": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_int,
+                                  c_int, c_int, c_void_p]),
     "upr_lab_tables": (None, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
 }
 

@@ -267,3 +267,42 @@ def lab_tables():
     L.lib().upr_lab_tables(g.ctypes.data, c.ctypes.data, yf.ctypes.data, ig.ctypes.data, m1.ctypes.data,
                            m2.ctypes.data)
     return {"gamma": g, "cbrt": c, "yf": yf, "invgamma": ig, "rgb2xyz": m1, "xyz2rgb": m2}
+
+
+def multiscale_features(x, scale_idx):
+    """[B,3,H,W] -> [B,7,hs,ws] feature maps of scale 0 (x1), 1 (x0.5) or 2 (x0.25)."""
+    _require_device(x)
+    x = x.contiguous()
+    B, C, H, W = x.shape
+    s = (1.0, 0.5, 0.25)[scale_idx]
+    hs, ws = (H, W) if scale_idx == 0 else (int(H * s), int(W * s))
+    out = torch.empty((B, 7, hs, ws), dtype=x.dtype, device=x.device)
+    with torch.cuda.device(x.device):
+        rc = L.lib().upr_multiscale_features(_ptr(x), _ptr(out), B, H, W, int(scale_idx), dtype_code(x.dtype),
+                                             _stream(x.device))
+    L.check(rc, "upr_multiscale_features")
+    return out
+
+
+def content_aware(x, enh=None, saliency=False, attention=False):
+    """Returns (out or None, saliency [B,H,W] f32 or None, attention [B,H,W] f32 or None)."""
+    _require_device(x)
+    x = x.contiguous()
+    B, C, H, W = x.shape
+    dev = x.device
+    out = None
+    if enh is not None:
+        enh = enh.contiguous()
+        if enh.shape != x.shape or enh.dtype != x.dtype:
+            raise RuntimeError("content_aware: enhanced image must match the input's shape and dtype")
+        out = torch.empty_like(enh)
+    sal = torch.empty((B, H, W), dtype=torch.float32, device=dev) if saliency else None
+    att = torch.empty((B, H, W), dtype=torch.float32, device=dev) if attention else None
+    lib = L.lib()
+    with torch.cuda.device(dev):
+        nbytes = lib.upr_content_aware_workspace(B, H, W)
+        ws = _WS.get(dev, nbytes)
+        rc = lib.upr_content_aware(_ptr(x), _ptr(enh), _ptr(out), _ptr(sal), _ptr(att), _ptr(ws),
+                                   ctypes.c_size_t(ws.numel()), B, H, W, dtype_code(x.dtype), _stream(dev))
+    L.check(rc, "upr_content_aware")
+    return out, sal, att

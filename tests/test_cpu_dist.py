@@ -1,0 +1,52 @@
+"""Batch-shard logic of upr/dist.py over a world_size-2 gloo group on CPU."""
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from upr.dist import shard_bounds, gather_shards
+
+
+def test_shard_bounds_cover_exactly():
+    for total in (1, 7, 32, 256, 257):
+        for world in (1, 2, 4, 8):
+            spans = [shard_bounds(total, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == total
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+            sizes = [b - a for a, b in spans]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, total, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    full = torch.arange(total * 6, dtype=torch.float32).reshape(total, 2, 3)
+    a, b = shard_bounds(total, world, rank)
+    got = gather_shards(full[a:b] * 1.0, total)
+    q.put((rank, bool(torch.equal(got, full))))
+    dist.destroy_process_group()
+
+
+def test_gloo_gather_world2():
+    ctx = mp.get_context("spawn")
+    for total in (8, 5):
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_worker, args=(r, 2, port, total, q)) for r in range(2)]
+        for p in procs:
+            p.start()
+        res = [q.get(timeout=120) for _ in procs]
+        for p in procs:
+            p.join(timeout=60)
+        assert sorted(res) == [(0, True), (1, True)]
