@@ -16,6 +16,9 @@
 // 8*(lane>>4).  fp32 consumes it as 8 x v_mfma_f32_16x16x4_f32 (exact fp32),
 // fp16 as 1 x v_mfma_f32_16x16x32_f16 (fp32 accumulate).  The permutation of k
 // across MFMA k-slots is the same for A and B, so the sum is unchanged.
+#include <cstdlib>
+#include <cstring>
+
 #include "upr_common.h"
 
 namespace upr {
@@ -357,10 +360,27 @@ static int launch_t(const ConvOp& op, hipStream_t stream) {
   return kErrShape;
 }
 
+int launch_conv_halo(const ConvOp& op, int dtype, hipStream_t st);
+
+// UPR_CONV_IMPL=generic forces the implicit-GEMM kernel everywhere (A/B tests);
+// default: halo-tiled kernel where the shape allows, implicit GEMM otherwise.
+static int conv_impl_mode() {
+  static int mode = -1;
+  if (mode < 0) {
+    const char* e = getenv("UPR_CONV_IMPL");
+    mode = (e && strcmp(e, "generic") == 0) ? 1 : 0;
+  }
+  return mode;
+}
+
 int launch_conv(const ConvOp& op, int dtype, hipStream_t stream) {
   if (op.nseg < 1 || op.nseg > 4 || op.B <= 0 || op.Ho <= 0 || op.Wo <= 0) return kErrArg;
   for (int s = 0; s < op.nseg; ++s)
     if (op.seg[s].C % 32 || op.seg[s].src == nullptr) return kErrShape;
+  if (conv_impl_mode() == 0) {
+    const int rc = launch_conv_halo(op, dtype, stream);
+    if (rc != kErrUnsupported) return rc;
+  }
   return dtype == kF16 ? launch_t<half_t>(op, stream) : launch_t<float>(op, stream);
 }
 

@@ -48,6 +48,13 @@ CONV_CASES = [
     (1, 16, 16, 128, 256, 1, 2, 0, 1, False, False),
     (3, 7, 9, 32, 96, 1, 1, 0, 1, True, False),
     (1, 9, 11, 96, 32, 3, 1, 1, 1, False, True),
+    # shapes routed to the halo-tiled kernel (stride 1, Wo >= 24, Ho >= 8), incl. partial tiles
+    (2, 24, 40, 32, 32, 3, 1, 1, 1, True, True),
+    (1, 17, 70, 32, 64, 3, 1, 2, 2, False, True),
+    (2, 12, 33, 64, 64, 3, 1, 1, 1, True, False),
+    (1, 9, 48, 32, 128, 1, 1, 0, 1, False, False),
+    (1, 16, 64, 128, 64, 3, 1, 1, 1, True, True),
+    (1, 8, 32, 256, 256, 3, 1, 1, 1, False, False),
 ]
 
 
