@@ -9,9 +9,11 @@ shard with no data-path collective (weak scaling); barrier + synchronize
 bracket the timed region and rank 0 reports the max over ranks.
 
 Extra objects on the JSON line:
-  roofline      the implicit-GEMM conv kernel family (conv_igemm_kernel<*>),
-                timed live with HIP events around every launch on the model's
-                stream inside the timed region (upr_model_profile)
+  roofline      the conv kernel family (conv_halo_kernel<*>, conv_igemm_kernel<*>,
+                ~97% of device time), timed live with HIP events around every
+                launch on the model's stream inside the timed region
+                (upr_model_profile); traffic from rocprofv3 FETCH_SIZE/WRITE_SIZE
+                child passes run before this process touches the GPU
   cpu_baseline  the CPU oracle forward (oracle/net.py, torch-CPU fp32) on the
                 host cores, rank 0 only, on a bounded sample
 """
@@ -46,6 +48,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline budget (0 = skip)")
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events")
     ap.add_argument("--breakdown", action="store_true", help="print per-layer stats to stderr")
+    ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     return ap.parse_args()
 
 
@@ -68,11 +71,71 @@ def cpu_baseline(sd, pre, aspp, size, budget_s):
             "sample": f"{n} x 1x3x{size}x{size} fp32 forwards of oracle/net.py (torch-CPU), {el:.1f}s"}
 
 
+CONV_KERNELS = ("conv_halo_kernel", "conv_igemm_kernel")
+
+
+def pmc_traffic(args):
+    """HBM bytes of the conv kernels per forward from rocprofv3 PMC counters.
+
+    Runs BEFORE this process touches the GPU: two child passes of this script
+    (one forward of warm-up + one timed) under `rocprofv3 --pmc FETCH_SIZE` and
+    `--pmc WRITE_SIZE` (separate passes: they do not fit one pass on gfx950).
+    FETCH_SIZE (KB) reports half the bytes of wide coalesced reads on gfx950, so
+    it is doubled (MI355X_MICROARCH.md, HBM section).  Returns None on failure."""
+    import csv
+    import shutil
+    import subprocess
+    import tempfile
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        return None
+    out = {}
+    base = [sys.executable, os.path.abspath(__file__), "--steps", "1", "--warmup", "1", "--cpu-seconds", "0",
+            "--no-profile", "--no-traffic", "--batch", str(args.batch), "--size", str(args.size),
+            "--precision", args.precision, "--variant", args.variant]
+    env = dict(os.environ, TMPDIR="/tmp")
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="upr_pmc_", dir="/tmp")
+        cmd = [exe, "--pmc", ctr, "--kernel-trace", "-T", "-d", d, "-o", "p", "--output-format", "csv", "--"] + base
+        try:
+            subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                           timeout=300, check=True)
+            path = None
+            for root, _, files in os.walk(d):
+                for f in files:
+                    if f.endswith("counter_collection.csv"):
+                        path = os.path.join(root, f)
+            if path is None:
+                return None
+            tot, n = 0.0, 0
+            with open(path) as f:
+                for r in csv.DictReader(f):
+                    if r["Counter_Name"] == ctr and r["Kernel_Name"].startswith(CONV_KERNELS):
+                        tot += float(r["Counter_Value"])
+                        n += 1
+            out[ctr] = (tot, n)
+        except Exception:
+            return None
+        finally:
+            shutil.rmtree(d, ignore_errors=True)
+    fetch_kb, n_launch = out["FETCH_SIZE"]
+    write_kb, _ = out["WRITE_SIZE"]
+    if n_launch == 0:
+        return None
+    per_fwd = (2.0 * fetch_kb + write_kb) * 1024.0 / 2.0  # 2 forwards (1 warm-up + 1 timed)
+    return {"bytes_per_launch": per_fwd / (n_launch / 2.0), "bytes_per_forward": per_fwd,
+            "read_bytes_per_forward": 2.0 * fetch_kb * 1024.0 / 2.0, "write_bytes_per_forward": write_kb * 1024.0 / 2.0,
+            "launches_per_forward": n_launch / 2.0}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    traffic = None
+    if world == 1 and not args.no_traffic and not any(k.startswith("ROCPROF") for k in os.environ):
+        traffic = pmc_traffic(args)  # child processes, before this process initialises the GPU
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
@@ -153,8 +216,11 @@ def main():
         peak = PEAK_TFLOPS[args.precision]
         out["roofline"] = {
             "bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
-            "traffic": None,
-            "kernel": "conv_igemm_kernel<*> (all launches of the step)",
+            "traffic": traffic["bytes_per_launch"] if traffic else None,
+            "traffic_unit": "bytes per conv launch (rocprofv3 FETCH_SIZE*2 + WRITE_SIZE)",
+            "traffic_per_img_GB": traffic["bytes_per_forward"] / B / 1e9 if traffic else None,
+            "alg_bytes_per_launch": g_bytes / max(g_calls, 1),
+            "kernel": "conv_halo_kernel<*> + conv_igemm_kernel<*> (all conv launches of the step)",
             "launches_per_step": g_calls / args.steps,
             "avg_launch_us": 1000.0 * g_ms / max(g_calls, 1),
             "gemm_gflop_per_img": g_flops / (args.steps * B) / 1e9,
