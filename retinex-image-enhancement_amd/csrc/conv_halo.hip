@@ -1,21 +1,33 @@
 // Halo-tiled direct convolution for gfx950 (stride-1 3x3 / 1x1 segments).
 //
 // The generic implicit-GEMM kernel (conv.hip) re-reads the A operand once per
-// filter tap.  Here a block owns an 8 x 32 output-pixel tile of one image and
+// filter tap.  Here a block owns a TH x 32 output-pixel tile of one image and
 // stages, per K step (= one segment x 32-channel chunk), the input REGION the
 // tile needs (tile + (k-1)*dil halo) into LDS once; every tap then reads its A
 // fragments from LDS at shifted offsets.  The step's weights for all taps sit
 // next to it (staged once per block when the whole K is one step).
 //
-// Pipeline: blocks loop over tiles (persistent grid).  The region of the NEXT
-// step (possibly of the next tile) is loaded into registers — prologue
-// (pre-activation BN+ReLU, 3x3 max-pool) applied there — while the current
-// step's MFMAs run; fragments of tap t+1 are read from LDS while tap t's MFMAs
-// issue.  Epilogue goes through LDS so every global store / residual load is a
-// full 16-byte chunk of consecutive channels (NHWC rows are contiguous).
+// * Blocks loop over tiles (persistent grid).  With PREF the region of the NEXT
+//   step (possibly of the next tile) is loaded into registers while the
+//   current step's MFMAs run; the prologue (pre-activation BN+ReLU) is applied
+//   when the registers are written to LDS; a 1x1 max-pool segment is pooled
+//   synchronously (EnhancedFAM branch2 only).
+// * Region geometry is a compile-time function of the step kind (1x1, 3x3 d1,
+//   3x3 d2), so every index division is by a constant.
+// * LDS pixel / weight-row strides are chosen so the 16-byte fragment reads of
+//   the MFMA operands are bank-conflict free (fp32: 10 chunks per row with the
+//   k-permutation {g, g+4}; fp16: 6 chunks per row) — brute-forced against
+//   the ds_read_b128 lane groups of MI355X_MICROARCH.md §LDS.
+// * Epilogue goes through LDS: residual chunks are all requested before the
+//   first is used, and every global store is a full 16-byte chunk of
+//   consecutive channels (NHWC rows are contiguous).
 //
-// MFMA fragment convention as in conv.hip: lane (r = lane&15, g = lane>>4)
-// owns 8 consecutive channels [8g, 8g+8) of pixel / weight row r.
+// MFMA fragments: lane (r = lane&15, g = lane>>4) owns 8 channels of pixel /
+// weight row r: fp16 [8g, 8g+8) -> one v_mfma_f32_16x16x32_f16;
+// fp32 [4g, 4g+4) u [16+4g, 16+4g+4) -> 8 x v_mfma_f32_16x16x4_f32 (exact fp32).
+// The same channel permutation is applied to A and B, so the sum is unchanged.
+#include <cstdio>
+#include <cstdlib>
 #include <type_traits>
 
 #include "upr_common.h"
@@ -32,49 +44,214 @@ template <> __device__ __forceinline__ float hfrom_f<float>(float v) { return v;
 template <> __device__ __forceinline__ half_t hfrom_f<half_t>(float v) { return (half_t)v; }
 
 constexpr int HALO_TW = 32;
-constexpr int HALO_MAXPAD = 2;  // 3x3 with dilation <= 2
+constexpr int HALO_MAXEXT = 4;  // 3x3 with dilation <= 2
 
 template <typename T, int NB, int TH>
 struct HaloCfg {
   static constexpr int EPC = 16 / sizeof(T);   // elements per 16-byte chunk
   static constexpr int CCH = 32 / EPC;         // chunks per 32-channel slice
-  static constexpr int PSTR = 32 + EPC;        // LDS pixel stride (elements): odd # of 16-B chunks
-  static constexpr int HH = TH + 2 * HALO_MAXPAD;
-  static constexpr int HWX = HALO_TW + 2 * HALO_MAXPAD;
-  static constexpr int HALO_ELEMS = HH * HWX * PSTR;
+  static constexpr int PSTR = sizeof(T) == 4 ? 40 : 48;  // row stride (elements): 10 / 6 chunks
+  static constexpr int HALO_ELEMS = (TH + HALO_MAXEXT) * (HALO_TW + HALO_MAXEXT) * PSTR;
   static constexpr int CSTR = NB + 4;          // fp32 epilogue staging stride
   static constexpr int EPI_BYTES = TH * HALO_TW * CSTR * 4;
   static constexpr int REGION_BYTES =
       HALO_ELEMS * (int)sizeof(T) > EPI_BYTES ? HALO_ELEMS * (int)sizeof(T) : EPI_BYTES;
   static constexpr int B_ELEMS = 9 * NB * PSTR;
   static constexpr int BYTES = REGION_BYTES + B_ELEMS * (int)sizeof(T);
-  static constexpr int PF = (HH * HWX * CCH + 255) / 256;  // prefetch registers (uint4) per thread
+  static constexpr int PF = ((TH + HALO_MAXEXT) * (HALO_TW + HALO_MAXEXT) * CCH + 255) / 256;
+  static constexpr int CHN = NB / EPC;         // epilogue chunks per pixel
+  static constexpr int PPP = 256 / CHN;        // epilogue pixels per pass
+  static constexpr int PASSES = TH * HALO_TW / PPP;
 };
 
+// step kind: 0 = 1x1, 1 = 3x3 dil 1, 2 = 3x3 dil 2  ->  EXT = 0, 2, 4
+__device__ __forceinline__ int step_kind(const ConvSeg& s) { return s.kh == 1 ? 0 : (s.dil == 1 ? 1 : 2); }
+
+template <typename T, int NB, int TH, int EXT>
+__device__ __forceinline__ void halo_load(uint4* pf, const ConvSeg& sg, int b, int oy0,
+                                          int ox0, int c0, int tid) {
+  using C = HaloCfg<T, NB, TH>;
+  constexpr int HW = HALO_TW + EXT, HH = TH + EXT, NCH = HH * HW * C::CCH;
+  constexpr int PAD = EXT / 2;
+  const T* base = (const T*)sg.src + (size_t)b * sg.Hin * sg.Win * sg.cs + sg.coff + c0;
+  // Every step kind writes EVERY pf[] entry at a constant index: when the kinds
+  // write different subsets, the compiler merges their stores through a phi'd
+  // address and demotes pf[] to scratch (each prefetch then waits on vmcnt(0)).
+#pragma unroll
+  for (int j = 0; j < C::PF; ++j) {
+    const int q = tid + j * 256;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (j * 256 < NCH) {
+      const int px = q / C::CCH, ch = q % C::CCH;
+      const int hy = px / HW, hx = px % HW;
+      const int iy = oy0 - PAD + hy, ix = ox0 - PAD + hx;
+      const bool ok = q < NCH && iy >= 0 && iy < sg.Hin && ix >= 0 && ix < sg.Win;
+      if (ok) v = *(const uint4*)(base + ((size_t)iy * sg.Win + ix) * sg.cs + ch * C::EPC);
+    }
+    pf[j] = v;
+  }
+}
+
+template <typename T, int NB, int TH, int EXT>
+__device__ __forceinline__ void halo_store(const uint4* pf, const ConvSeg& sg, int oy0,
+                                           int ox0, int c0, int tid, T* halo) {
+  using C = HaloCfg<T, NB, TH>;
+  constexpr int HW = HALO_TW + EXT, HH = TH + EXT, NCH = HH * HW * C::CCH;
+  constexpr int PAD = EXT / 2;
+  const bool aff = sg.pre == kPreAffineRelu;
+#pragma unroll
+  for (int j = 0; j < C::PF; ++j) {
+    const int q = tid + j * 256;
+    if (j * 256 < NCH && q < NCH) {
+      const int px = q / C::CCH, ch = q % C::CCH;
+      uint4 v = pf[j];
+      if (aff) {
+        const int hy = px / HW, hx = px % HW;
+        const int iy = oy0 - PAD + hy, ix = ox0 - PAD + hx;
+        if (iy >= 0 && iy < sg.Hin && ix >= 0 && ix < sg.Win) {  // zero padding stays zero
+          const int cb = c0 + ch * C::EPC;
+          T* vv = (T*)&v;
+#pragma unroll
+          for (int e = 0; e < C::EPC; ++e)
+            vv[e] = hfrom_f<T>(fmaxf(hto_f(vv[e]) * sg.pre_scale[cb + e] + sg.pre_shift[cb + e], 0.f));
+        }
+      }
+      *(uint4*)(halo + px * C::PSTR + ch * C::EPC) = v;
+    }
+  }
+}
+
+// 3x3/s1/p1 max-pool of the source for a 1x1 segment (EnhancedFAM branch2, model.py:32,69)
 template <typename T, int NB, int TH>
-__global__ __launch_bounds__(256) void conv_halo_kernel(ConvOp op, int tiles_x, int tiles_y, int ntiles) {
+__device__ void halo_pool(const ConvSeg& sg, int b, int oy0, int ox0, int c0, int tid, T* halo) {
+  using C = HaloCfg<T, NB, TH>;
+  const T* src = (const T*)sg.src;
+  for (int q = tid; q < TH * HALO_TW * C::CCH; q += 256) {
+    const int px = q / C::CCH, ch = q % C::CCH;
+    const int iy = oy0 + px / HALO_TW, ix = ox0 + px % HALO_TW;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (iy < sg.Hin && ix < sg.Win) {
+      float mx[C::EPC];
+#pragma unroll
+      for (int e = 0; e < C::EPC; ++e) mx[e] = -INFINITY;
+      for (int dy = -1; dy <= 1; ++dy) {
+        const int yy = iy + dy;
+        if (yy < 0 || yy >= sg.Hin) continue;
+        for (int dx = -1; dx <= 1; ++dx) {
+          const int xx = ix + dx;
+          if (xx < 0 || xx >= sg.Win) continue;
+          const uint4 w4 =
+              *(const uint4*)(src + (((size_t)b * sg.Hin + yy) * sg.Win + xx) * sg.cs + sg.coff + c0 + ch * C::EPC);
+          const T* wv = (const T*)&w4;
+#pragma unroll
+          for (int e = 0; e < C::EPC; ++e) mx[e] = fmaxf(mx[e], hto_f(wv[e]));
+        }
+      }
+      T* vv = (T*)&v;
+#pragma unroll
+      for (int e = 0; e < C::EPC; ++e) vv[e] = hfrom_f<T>(mx[e]);
+    }
+    *(uint4*)(halo + px * C::PSTR + ch * C::EPC) = v;
+  }
+}
+
+// all taps of one step
+template <typename T, int NB, int TH, int K, int D>
+__device__ __forceinline__ void halo_taps(f32x4_h (&acc)[TH / 2][NB / 16], const T* halo, const T* Bs, int wave,
+                                          int fr, int fg) {
+  using C = HaloCfg<T, NB, TH>;
+  constexpr int PSTR = C::PSTR;
+  constexpr int RPW = TH / 4;
+  constexpr int MT = 2 * RPW;
+  constexpr int NT = NB / 16;
+  constexpr int HW = HALO_TW + (K - 1) * D;
+  constexpr int NTAP = K * K;
+  if constexpr (sizeof(T) == 2) {
+#pragma unroll
+    for (int tap = 0; tap < NTAP; ++tap) {
+      const int r = tap / K, c = tap % K;
+      f16x8_h bf[NT], af[MT];
+#pragma unroll
+      for (int j = 0; j < NT; ++j) bf[j] = *(const f16x8_h*)(Bs + (tap * NB + j * 16 + fr) * PSTR + fg * 8);
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const int py = wave * RPW + (i >> 1) + r * D, pxx = (i & 1) * 16 + fr + c * D;
+        af[i] = *(const f16x8_h*)(halo + (py * HW + pxx) * PSTR + fg * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+  } else {
+#pragma unroll
+    for (int tap = 0; tap < NTAP; ++tap) {
+      const int r = tap / K, c = tap % K;
+      f32x4_h bf[NT][2], af[MT][2];
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const float* p = (const float*)Bs + (tap * NB + j * 16 + fr) * PSTR + fg * 4;
+        bf[j][0] = *(const f32x4_h*)p;
+        bf[j][1] = *(const f32x4_h*)(p + 16);
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const int py = wave * RPW + (i >> 1) + r * D, pxx = (i & 1) * 16 + fr + c * D;
+        const float* p = (const float*)halo + (py * HW + pxx) * PSTR + fg * 4;
+        af[i][0] = *(const f32x4_h*)p;
+        af[i][1] = *(const f32x4_h*)(p + 16);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int j = 0; j < NT; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][e >> 2][e & 3], bf[j][e >> 2][e & 3], acc[i][j],
+                                                            0, 0, 0);
+    }
+  }
+}
+
+// The next step's region (possibly of the next tile) is loaded into registers
+// during the current step's MFMAs.  OCC = waves per SIMD the register
+// allocation must allow (= co-resident 256-thread blocks per CU): above 1 the
+// compiler stops hoisting every tap's fragment reads and a second block's
+// MFMAs overlap this block's staging / epilogue.  KM = bitmask of the step
+// kinds the op contains (1: 1x1, 2: 3x3 d1, 4: 3x3 d2); a single-kind op gets
+// a kernel with only that kind's region / tap code (fewer live registers).
+template <typename T, int NB, int TH, int OCC, int KM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void conv_halo_kernel(
+    ConvOp op, int tiles_x, int tiles_y, int ntiles, int region_bytes) {
+  constexpr bool PREF = true;
   using C = HaloCfg<T, NB, TH>;
   constexpr int EPC = C::EPC, CCH = C::CCH, PSTR = C::PSTR;
   constexpr int TW = HALO_TW;
   constexpr int RPW = TH / 4;  // tile rows per wave
   constexpr int MT = 2 * RPW;  // 16-pixel M tiles per wave
   constexpr int NT = NB / 16;  // 16-channel N tiles
-  __shared__ __attribute__((aligned(16))) unsigned char smem[C::BYTES];
+  constexpr int CHN = C::CHN, PPP = C::PPP, PASSES = C::PASSES;
+  // dynamic LDS sized per op on the host: [region | epilogue staging] then weights
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   T* halo = (T*)smem;
   float* Cs = (float*)smem;
-  T* Bs = (T*)(smem + C::REGION_BYTES);
+  T* Bs = (T*)(smem + region_bytes);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
   const int nblk_n = op.N / NB;
   const int HWo = op.Ho * op.Wo;
   const T* W = (const T*)op.W;
+  // at most one residual per op (launch_conv_halo checks): added before (res1) or after (res2) the ReLU
+  const T* resp = (const T*)(op.res1 ? op.res1 : op.res2);
+  const int res_cs = op.res1 ? op.res1_cs : op.res2_cs;
+  const bool res_pre = op.res1 != nullptr;
 
   int nsteps = 0;
   for (int s = 0; s < op.nseg; ++s) nsteps += op.seg[s].C / 32;
-  const bool b_resident = nsteps == 1;
+  const bool b_keep = nsteps == 1 && nblk_n == 1;  // weights identical for every tile of the block
 
-  // tile index -> (b, oy0, ox0, n0)
   auto tile_coords = [&](int tile, int& b, int& oy0, int& ox0, int& n0) {
     int t = tile;
     const int nb = t % nblk_n; t /= nblk_n;
@@ -82,113 +259,38 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(ConvOp op, int tiles_x, 
     const int ty = t % tiles_y; t /= tiles_y;
     b = t; oy0 = ty * TH; ox0 = tx * TW; n0 = nb * NB;
   };
-  // K step -> (segment, first channel)
   auto step_seg = [&](int step, int& si, int& c0) {
     si = 0;
     int s = step;
     while (s >= op.seg[si].C / 32) { s -= op.seg[si].C / 32; ++si; }
     c0 = s * 32;
   };
-
+  auto kind_of = [&](const ConvSeg& sg) -> int {
+    if constexpr (KM == 1) return 0;
+    if constexpr (KM == 2) return 1;
+    if constexpr (KM == 4) return 2;
+    return step_kind(sg);
+  };
   uint4 pf[C::PF];
-  auto load_region = [&](int step, int tile) {
+  auto load = [&](int step, int tile) {
     int b, oy0, ox0, n0, si, c0;
     tile_coords(tile, b, oy0, ox0, n0);
     step_seg(step, si, c0);
     const ConvSeg& sg = op.seg[si];
-    const int ext = (sg.kh - 1) * sg.dil;
-    const int hh = TH + ext, hw = TW + ext;
-    const int nch = hh * hw * CCH;
-    const T* src = (const T*)sg.src;
-    if (sg.pre == kPreMaxPool3) return;  // pooled synchronously in store_region (rare, 1x1 only)
-    const T* base = src + (size_t)b * sg.Hin * sg.Win * sg.cs + sg.coff + c0;
-#pragma unroll
-    for (int j = 0; j < C::PF; ++j) {
-      const int q = tid + j * 256;
-      const int px = q / CCH, ch = q - px * CCH;
-      const int hy = px / hw, hx = px - hy * hw;
-      const int iy = oy0 - sg.pad + hy, ix = ox0 - sg.pad + hx;
-      const bool ok = q < nch && iy >= 0 && iy < sg.Hin && ix >= 0 && ix < sg.Win;
-      const T* p = base + ((size_t)iy * sg.Win + ix) * sg.cs + ch * EPC;
-      pf[j] = ok ? *(const uint4*)p : make_uint4(0, 0, 0, 0);
+    const int kind = kind_of(sg);
+    if ((KM & 1) && kind == 0) {
+      if (sg.pre != kPreMaxPool3) halo_load<T, NB, TH, 0>(pf, sg, b, oy0, ox0, c0, tid);
+    } else if ((KM & 2) && kind == 1) {
+      halo_load<T, NB, TH, 2>(pf, sg, b, oy0, ox0, c0, tid);
+    } else if (KM & 4) {
+      halo_load<T, NB, TH, 4>(pf, sg, b, oy0, ox0, c0, tid);
     }
   };
-  // 3x3/s1/p1 max-pool of the source for a 1x1 segment (EnhancedFAM branch2, model.py:32,69)
-  auto pool_region = [&](int si, int c0, int b, int oy0, int ox0) {
-    const ConvSeg& sg = op.seg[si];
-    const T* src = (const T*)sg.src;
-    for (int q = tid; q < TH * TW * CCH; q += 256) {
-      const int px = q / CCH, ch = q - px * CCH;
-      const int hy = px / TW, hx = px - hy * TW;
-      const int iy = oy0 + hy, ix = ox0 + hx;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (iy < sg.Hin && ix < sg.Win) {
-        float mx[EPC];
-#pragma unroll
-        for (int e = 0; e < EPC; ++e) mx[e] = -INFINITY;
-        for (int dy = -1; dy <= 1; ++dy) {
-          const int yy = iy + dy;
-          if (yy < 0 || yy >= sg.Hin) continue;
-          for (int dx = -1; dx <= 1; ++dx) {
-            const int xx = ix + dx;
-            if (xx < 0 || xx >= sg.Win) continue;
-            const uint4 w4 = *(const uint4*)(src + (((size_t)b * sg.Hin + yy) * sg.Win + xx) * sg.cs + sg.coff + c0 +
-                                             ch * EPC);
-            const T* wv = (const T*)&w4;
-#pragma unroll
-            for (int e = 0; e < EPC; ++e) mx[e] = fmaxf(mx[e], hto_f(wv[e]));
-          }
-        }
-        T* vv = (T*)&v;
-#pragma unroll
-        for (int e = 0; e < EPC; ++e) vv[e] = hfrom_f<T>(mx[e]);
-      }
-      *(uint4*)(halo + px * PSTR + ch * EPC) = v;
-    }
-  };
-  // prologue transform + write to LDS (same q -> slot mapping as load_region)
-  auto store_region = [&](int step, int tile) {
-    int si, c0;
-    step_seg(step, si, c0);
-    const ConvSeg& sg = op.seg[si];
-    const int ext = (sg.kh - 1) * sg.dil;
-    const int hh = TH + ext, hw = TW + ext;
-    const int nch = hh * hw * CCH;
-    int b, oy0, ox0, n0;
-    tile_coords(tile, b, oy0, ox0, n0);
-    if (sg.pre == kPreMaxPool3) {
-      pool_region(si, c0, b, oy0, ox0);
-      return;
-    }
-#pragma unroll
-    for (int j = 0; j < C::PF; ++j) {
-      const int q = tid + j * 256;
-      if (q < nch) {
-        const int px = q / CCH, ch = q - px * CCH;
-        uint4 v = pf[j];
-        if (sg.pre == kPreAffineRelu) {
-          const int hy = px / hw, hx = px - hy * hw;
-          const int iy = oy0 - sg.pad + hy, ix = ox0 - sg.pad + hx;
-          if (iy >= 0 && iy < sg.Hin && ix >= 0 && ix < sg.Win) {  // zero padding stays zero
-            const int cb = c0 + ch * EPC;
-            T* vv = (T*)&v;
-#pragma unroll
-            for (int e = 0; e < EPC; ++e)
-              vv[e] = hfrom_f<T>(fmaxf(hto_f(vv[e]) * sg.pre_scale[cb + e] + sg.pre_shift[cb + e], 0.f));
-          }
-        }
-        *(uint4*)(halo + px * PSTR + ch * EPC) = v;
-      }
-    }
-  };
-  auto stage_b = [&](int step, int n0) {
-    int si, c0;
-    step_seg(step, si, c0);
-    const ConvSeg& sg = op.seg[si];
+  auto stage_b = [&](const ConvSeg& sg, int c0, int n0) {
     const int nbq = sg.kh * sg.kw * NB * CCH;
     for (int q = tid; q < nbq; q += 256) {
-      const int row = q / CCH, ch = q - row * CCH;  // row = tap*NB + n
-      const int tap = row / NB, n = row - tap * NB;
+      const int row = q / CCH, ch = q % CCH;  // row = tap*NB + n
+      const int tap = row / NB, n = row % NB;
       *(uint4*)(Bs + row * PSTR + ch * EPC) =
           *(const uint4*)(W + (size_t)(n0 + n) * op.Kpad + sg.kbase + tap * sg.C + c0 + ch * EPC);
     }
@@ -196,13 +298,13 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(ConvOp op, int tiles_x, 
 
   int tile = blockIdx.x;
   if (tile >= ntiles) return;
-  if (b_resident) {
-    int b, oy0, ox0, n0;
+  if (b_keep) {
+    int b, oy0, ox0, n0, si, c0;
     tile_coords(tile, b, oy0, ox0, n0);
-    // all tiles of this block share n0 only if nblk_n == 1; otherwise restage per tile (below)
-    if (nblk_n == 1) stage_b(0, n0);
+    step_seg(0, si, c0);
+    stage_b(op.seg[si], c0, n0);
   }
-  load_region(0, tile);
+  if constexpr (PREF) load(0, tile);
 
   for (; tile < ntiles; tile += gridDim.x) {
     int b, oy0, ox0, n0;
@@ -214,80 +316,52 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(ConvOp op, int tiles_x, 
 #pragma unroll
       for (int j = 0; j < NT; ++j) acc[i][j] = f32x4_h{0.f, 0.f, 0.f, 0.f};
 
+    const int ch = tid % CHN;
+    const int nb0 = ch * EPC;  // first channel (within the block slice) of this thread in the epilogue
+    uint4 rr[PASSES];
     for (int step = 0; step < nsteps; ++step) {
-      __syncthreads();  // LDS free (previous step's compute / previous tile's epilogue)
-      store_region(step, tile);
-      if (!(b_resident && nblk_n == 1)) stage_b(step, n0);
-      __syncthreads();
-      // prefetch the next step's region (next tile after the last step)
-      {
-        const int nstep = step + 1 < nsteps ? step + 1 : 0;
-        const int ntile = step + 1 < nsteps ? tile : tile + gridDim.x;
-        if (ntile < ntiles) load_region(nstep, ntile);
-      }
       int si, c0;
       step_seg(step, si, c0);
       const ConvSeg& sg = op.seg[si];
-      const int d = sg.dil;
-      auto run_taps = [&](auto kc) {
-        constexpr int k = decltype(kc)::value;
-        constexpr int ntap = k * k;
-        const int hw = TW + (k - 1) * d;
-        if constexpr (sizeof(T) == 2) {
-          f16x8_h af[2][MT], bf[2][NT];
+      const int kind = kind_of(sg);
+      if constexpr (!PREF) load(step, tile);
+      __syncthreads();  // LDS free (previous step's MFMAs / previous tile's epilogue)
+      if ((KM & 1) && kind == 0) {
+        if (sg.pre == kPreMaxPool3)
+          halo_pool<T, NB, TH>(sg, b, oy0, ox0, c0, tid, halo);
+        else
+          halo_store<T, NB, TH, 0>(pf, sg, oy0, ox0, c0, tid, halo);
+      } else if ((KM & 2) && kind == 1) {
+        halo_store<T, NB, TH, 2>(pf, sg, oy0, ox0, c0, tid, halo);
+      } else if (KM & 4) {
+        halo_store<T, NB, TH, 4>(pf, sg, oy0, ox0, c0, tid, halo);
+      }
+      if (!b_keep) stage_b(sg, c0, n0);
+      __syncthreads();
+      if constexpr (PREF) {
+        const int nstep = step + 1 < nsteps ? step + 1 : 0;
+        const int ntile = step + 1 < nsteps ? tile : tile + gridDim.x;
+        if (ntile < ntiles) load(nstep, ntile);
+      }
+      if (step == nsteps - 1 && resp) {
+        // residual chunks of this tile, requested before the last step's MFMAs
 #pragma unroll
-          for (int tap = 0; tap < ntap; ++tap) {
-            const int r = tap / k, c = tap % k;
-            const int cur = tap & 1;
-#pragma unroll
-            for (int j = 0; j < NT; ++j)
-              bf[cur][j] = *(const f16x8_h*)(Bs + ((tap * NB) + j * 16 + fr) * PSTR + fg * 8);
-#pragma unroll
-            for (int i = 0; i < MT; ++i) {
-              const int py = wave * RPW + (i >> 1) + r * d, pxx = (i & 1) * 16 + fr + c * d;
-              af[cur][i] = *(const f16x8_h*)(halo + (py * hw + pxx) * PSTR + fg * 8);
-            }
-#pragma unroll
-            for (int i = 0; i < MT; ++i)
-#pragma unroll
-              for (int j = 0; j < NT; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[cur][i], bf[cur][j], acc[i][j], 0, 0, 0);
-          }
-        } else {
-          f32x4_h af[2][MT][2], bf[2][NT][2];
-#pragma unroll
-          for (int tap = 0; tap < ntap; ++tap) {
-            const int r = tap / k, c = tap % k;
-            const int cur = tap & 1;
-#pragma unroll
-            for (int j = 0; j < NT; ++j) {
-              const float* p = (const float*)Bs + ((tap * NB) + j * 16 + fr) * PSTR + fg * 8;
-              bf[cur][j][0] = *(const f32x4_h*)p;
-              bf[cur][j][1] = *(const f32x4_h*)(p + 4);
-            }
-#pragma unroll
-            for (int i = 0; i < MT; ++i) {
-              const int py = wave * RPW + (i >> 1) + r * d, pxx = (i & 1) * 16 + fr + c * d;
-              const float* p = (const float*)halo + (py * hw + pxx) * PSTR + fg * 8;
-              af[cur][i][0] = *(const f32x4_h*)p;
-              af[cur][i][1] = *(const f32x4_h*)(p + 4);
-            }
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-#pragma unroll
-              for (int i = 0; i < MT; ++i)
-#pragma unroll
-                for (int j = 0; j < NT; ++j)
-                  acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[cur][i][e >> 2][e & 3], bf[cur][j][e >> 2][e & 3],
-                                                                  acc[i][j], 0, 0, 0);
-          }
+        for (int ps = 0; ps < PASSES; ++ps) {
+          const int p = tid / CHN + ps * PPP;
+          const int oy = oy0 + p / TW, ox = ox0 + p % TW;
+          const size_t m = ((size_t)b * op.Ho + oy) * op.Wo + ox;
+          rr[ps] = (oy < op.Ho && ox < op.Wo) ? *(const uint4*)(resp + m * res_cs + n0 + nb0) : make_uint4(0, 0, 0, 0);
         }
-      };
-      if (sg.kh == 3) run_taps(std::integral_constant<int, 3>{});
-      else run_taps(std::integral_constant<int, 1>{});
+      }
+      if ((KM & 1) && kind == 0)
+        halo_taps<T, NB, TH, 1, 1>(acc, halo, Bs, wave, fr, fg);
+      else if ((KM & 2) && kind == 1)
+        halo_taps<T, NB, TH, 3, 1>(acc, halo, Bs, wave, fr, fg);
+      else if (KM & 4)
+        halo_taps<T, NB, TH, 3, 2>(acc, halo, Bs, wave, fr, fg);
     }
 
-    // ---- epilogue: stage fp32 accumulators, then coalesced 16-byte passes ----
+    // ---- epilogue ------------------------------------------------------------
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
@@ -299,11 +373,7 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(ConvOp op, int tiles_x, 
     }
     __syncthreads();
 
-    constexpr int CHN = NB / EPC;   // 16-byte chunks per pixel of the block's channel slice
-    constexpr int PPP = 256 / CHN;  // pixels per pass
-    const int ch = tid % CHN;
-    const int nb0 = ch * EPC;       // first channel (within the block slice) of this thread
-    float bias_v[EPC], scale_v[EPC];
+    float bias_v[EPC];
     if (op.bias) {
       const f32x4_h* bp = (const f32x4_h*)(op.bias + n0 + nb0);
 #pragma unroll
@@ -315,25 +385,26 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(ConvOp op, int tiles_x, 
 #pragma unroll
       for (int e = 0; e < EPC; ++e) bias_v[e] = 0.f;
     }
-    if (op.scale) {
-#pragma unroll
-      for (int e = 0; e < EPC; ++e) scale_v[e] = op.scale[n0 + nb0 + e];
-    } else {
-#pragma unroll
-      for (int e = 0; e < EPC; ++e) scale_v[e] = 1.f;
-    }
     float psum[EPC];
 #pragma unroll
     for (int e = 0; e < EPC; ++e) psum[e] = 0.f;
     T* out = (T*)op.out;
-    for (int p = tid / CHN; p < TH * TW; p += PPP) {
-      const int py = p / TW, pxx = p - py * TW;
-      const int oy = oy0 + py, ox = ox0 + pxx;
+#pragma unroll
+    for (int ps = 0; ps < PASSES; ++ps) {
+      const int p = tid / CHN + ps * PPP;
+      const int oy = oy0 + p / TW, ox = ox0 + p % TW;
       const bool valid = oy < op.Ho && ox < op.Wo;
       const size_t m = ((size_t)b * op.Ho + oy) * op.Wo + ox;
       float v[EPC];
+      {
+        const f32x4_h* cp = (const f32x4_h*)(Cs + p * C::CSTR + nb0);
 #pragma unroll
-      for (int e = 0; e < EPC; ++e) v[e] = Cs[p * C::CSTR + nb0 + e] * scale_v[e] + bias_v[e];
+        for (int e = 0; e < EPC; e += 4) {
+          const f32x4_h t4 = cp[e / 4];
+          v[e] = t4[0] + bias_v[e]; v[e + 1] = t4[1] + bias_v[e + 1];
+          v[e + 2] = t4[2] + bias_v[e + 2]; v[e + 3] = t4[3] + bias_v[e + 3];
+        }
+      }
       if (op.store == kStoreHeadIllu) {
         // residual head (models/model.py:324-328, :351-358); NB == N == 32
         float part = 0.f;
@@ -361,9 +432,8 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(ConvOp op, int tiles_x, 
 #pragma unroll
         for (int e = 0; e < EPC; ++e) v[e] += op.img_bias[b * op.N + n0 + nb0 + e];
       }
-      if (op.res1) {
-        const uint4 rr = *(const uint4*)((const T*)op.res1 + m * op.res1_cs + n0 + nb0);
-        const T* rv = (const T*)&rr;
+      if (resp && res_pre) {
+        const T* rv = (const T*)&rr[ps];
 #pragma unroll
         for (int e = 0; e < EPC; ++e) v[e] += hto_f(rv[e]);
       }
@@ -371,9 +441,8 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(ConvOp op, int tiles_x, 
 #pragma unroll
         for (int e = 0; e < EPC; ++e) v[e] = fmaxf(v[e], 0.f);
       }
-      if (op.res2) {
-        const uint4 rr = *(const uint4*)((const T*)op.res2 + m * op.res2_cs + n0 + nb0);
-        const T* rv = (const T*)&rr;
+      if (resp && !res_pre) {
+        const T* rv = (const T*)&rr[ps];
 #pragma unroll
         for (int e = 0; e < EPC; ++e) v[e] += hto_f(rv[e]);
       }
@@ -382,10 +451,8 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(ConvOp op, int tiles_x, 
 #pragma unroll
       for (int e = 0; e < EPC; ++e) ov[e] = hfrom_f<T>(v[e]);
       *(uint4*)(out + m * op.out_cs + op.out_coff + n0 + nb0) = o;
-      if (op.pool) {
 #pragma unroll
-        for (int e = 0; e < EPC; ++e) psum[e] += hto_f(ov[e]);
-      }
+      for (int e = 0; e < EPC; ++e) psum[e] += hto_f(ov[e]);
     }
     if (op.pool) {
       // per-channel tile sums -> one atomic per channel
@@ -403,16 +470,79 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(ConvOp op, int tiles_x, 
   }
 }
 
-template <typename T, int NB, int TH>
+template <typename T, int NB, int TH, int OCC, int KM>
 static int launch_halo_cfg(const ConvOp& op, hipStream_t st) {
   const int tiles_x = cdiv(op.Wo, HALO_TW), tiles_y = cdiv(op.Ho, TH);
   const int ntiles = op.B * tiles_x * tiles_y * (op.N / NB);
   using C = HaloCfg<T, NB, TH>;
-  const int per_cu = C::BYTES > 80 * 1024 ? 1 : (C::BYTES > 53 * 1024 ? 2 : 3);
-  int grid = 256 * per_cu;  // persistent: one wave of resident blocks
+  // LDS: region for the largest halo extent / tap count among this op's segments
+  int ext = 0, taps = 1;
+  for (int s = 0; s < op.nseg; ++s) {
+    const int e = (op.seg[s].kh - 1) * op.seg[s].dil;
+    ext = e > ext ? e : ext;
+    taps = op.seg[s].kh * op.seg[s].kw > taps ? op.seg[s].kh * op.seg[s].kw : taps;
+  }
+  const int halo_bytes = (TH + ext) * (HALO_TW + ext) * C::PSTR * (int)sizeof(T);
+  const int region = (int)align_up((size_t)(halo_bytes > C::EPI_BYTES ? halo_bytes : C::EPI_BYTES), 16);
+  const int lds = region + taps * NB * C::PSTR * (int)sizeof(T);
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)conv_halo_kernel<T, NB, TH, OCC, KM>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  // Persistent grid = blocks that are actually co-resident (registers AND LDS);
+  // an oversized grid leaves a second, partial wave of blocks (tail).  Speed only.
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)conv_halo_kernel<T, NB, TH, OCC, KM>, 256,
+                                                   lds) != hipSuccess || per_cu < 1)
+    per_cu = 1;
+  const int lds_cap = (160 * 1024) / lds;
+  if (per_cu > lds_cap) per_cu = lds_cap < 1 ? 1 : lds_cap;
+  int grid = 256 * per_cu;
   if (grid > ntiles) grid = ntiles;
-  hipLaunchKernelGGL((conv_halo_kernel<T, NB, TH>), dim3(grid), dim3(256), 0, st, op, tiles_x, tiles_y, ntiles);
+  hipLaunchKernelGGL((conv_halo_kernel<T, NB, TH, OCC, KM>), dim3(grid), dim3(256), lds, st, op, tiles_x, tiles_y,
+                     ntiles, region);
   return (int)hipGetLastError();
+}
+
+template <typename T, int NB, int KM>
+static int launch_halo_th(const ConvOp& op, int th, int occ, hipStream_t st) {
+  if constexpr (KM == 2) {  // single-kind ops: registers leave room for 2-3 blocks per CU
+    if (th == 4) {
+      if (occ >= 3) return launch_halo_cfg<T, NB, 4, 3, KM>(op, st);
+      return occ == 2 ? launch_halo_cfg<T, NB, 4, 2, KM>(op, st) : launch_halo_cfg<T, NB, 4, 1, KM>(op, st);
+    }
+    return occ >= 2 ? launch_halo_cfg<T, NB, 8, 2, KM>(op, st) : launch_halo_cfg<T, NB, 8, 1, KM>(op, st);
+  }
+  return th == 4 ? launch_halo_cfg<T, NB, 4, 1, KM>(op, st) : launch_halo_cfg<T, NB, 8, 1, KM>(op, st);
+}
+
+template <typename T, int NB>
+static int launch_halo_km(const ConvOp& op, int km, int th, int occ, hipStream_t st) {
+  if (km == 2) return launch_halo_th<T, NB, 2>(op, th, occ, st);
+  return launch_halo_th<T, NB, 7>(op, th, occ, st);
+}
+
+// Tile rows / occupancy per layer class; UPR_HALO="<th>,<occ>" overrides (experiments).
+// Measured on MI355X (tools/halo_sweep.sh, UP-Retinex layer shapes, bs 32):
+// single-kind 3x3 ops run 2 blocks per CU — fp16 with 8-row tiles, fp32 with
+// 4-row tiles (8-row fp32 tiles need > 256 registers); mixed-kind ops (the
+// FAM fusion GEMM, dilated convs) 8-row tiles, 1 block per CU.
+static void halo_choice(int dtype, int N, int km, int& th, int& occ) {
+  (void)N;
+  if (km == 2) {
+    th = dtype == kF16 ? 8 : 4;
+    occ = 2;
+  } else {
+    th = 8;
+    occ = 1;
+  }
+  const char* e = getenv("UPR_HALO");
+  if (e) {
+    int a = 0, b = 0;
+    if (sscanf(e, "%d,%d", &a, &b) == 2 && (a == 4 || a == 8) && b >= 1 && b <= 3) { th = a; occ = b; }
+  }
 }
 
 // Returns kErrUnsupported when the op is not a halo-kernel shape (caller falls back).
@@ -423,9 +553,10 @@ int launch_conv_halo(const ConvOp& op, int dtype, hipStream_t st) {
     const ConvSeg& g = op.seg[s];
     if (g.stride != 1 || g.kh != g.kw) return kErrUnsupported;
     if (g.kh == 3) {
-      if (g.dil < 1 || g.dil > HALO_MAXPAD || g.pad != g.dil) return kErrUnsupported;
+      if (g.dil < 1 || g.dil > HALO_MAXEXT / 2 || g.pad != g.dil) return kErrUnsupported;
     } else if (g.kh == 1) {
       if (g.pad != 0) return kErrUnsupported;
+      if (g.pre == kPreMaxPool3 && g.dil != 1) return kErrUnsupported;
     } else {
       return kErrUnsupported;
     }
@@ -433,12 +564,21 @@ int launch_conv_halo(const ConvOp& op, int dtype, hipStream_t st) {
   }
   const int elt = dtype == kF16 ? 2 : 4;
   if (op.out && ((op.out_cs * elt) % 16 || (op.out_coff * elt) % 16)) return kErrUnsupported;
+  if (op.res1 && (op.res1_cs * elt) % 16) return kErrUnsupported;
+  if (op.res2 && (op.res2_cs * elt) % 16) return kErrUnsupported;
+  if (op.res1 && op.res2) return kErrUnsupported;
   if (op.store == kStoreHeadIllu && op.N != 32) return kErrUnsupported;
+  if (op.bias && ((uintptr_t)op.bias % 16)) return kErrUnsupported;
+  if (op.scale) return kErrUnsupported;  // the graph folds every scale into the weights
+  int km = 0;
+  for (int s = 0; s < op.nseg; ++s) km |= 1 << (op.seg[s].kh == 1 ? 0 : (op.seg[s].dil == 1 ? 1 : 2));
+  int th, occ;
+  halo_choice(dtype, op.N, km, th, occ);
   if (dtype == kF16) {
-    if (op.N == 32) return launch_halo_cfg<half_t, 32, 8>(op, st);
-    if (op.N % 64 == 0) return launch_halo_cfg<half_t, 64, 8>(op, st);
+    if (op.N == 32) return launch_halo_km<half_t, 32>(op, km, th, occ, st);
+    if (op.N % 64 == 0) return launch_halo_km<half_t, 64>(op, km, th, occ, st);
   } else {
-    if (op.N % 32 == 0 && op.N <= 64) return launch_halo_cfg<float, 32, 8>(op, st);
+    if (op.N % 32 == 0) return launch_halo_km<float, 32>(op, km, th, occ, st);
   }
   return kErrUnsupported;
 }
