@@ -1,4 +1,5 @@
-// Halo-tiled direct convolution for gfx950 (stride-1 3x3 / 1x1 segments).
+// Halo-tiled direct convolution for gfx950 (stride-1 3x3 / 1x1 segments, plus
+// the 1x1 stride-2 ResBlock shortcut and the EnhancedFAM max-pool branch).
 //
 // The generic implicit-GEMM kernel (conv.hip) re-reads the A operand once per
 // filter tap.  Here a block owns a TH x 32 output-pixel tile of one image and
@@ -7,20 +8,31 @@
 // fragments from LDS at shifted offsets.  The step's weights for all taps sit
 // next to it (staged once per block when the whole K is one step).
 //
-// * Blocks loop over tiles (persistent grid).  With PREF the region of the NEXT
-//   step (possibly of the next tile) is loaded into registers while the
-//   current step's MFMAs run; the prologue (pre-activation BN+ReLU) is applied
-//   when the registers are written to LDS; a 1x1 max-pool segment is pooled
-//   synchronously (EnhancedFAM branch2 only).
-// * Region geometry is a compile-time function of the step kind (1x1, 3x3 d1,
-//   3x3 d2), so every index division is by a constant.
-// * LDS pixel / weight-row strides are chosen so the 16-byte fragment reads of
-//   the MFMA operands are bank-conflict free (fp32: 10 chunks per row with the
-//   k-permutation {g, g+4}; fp16: 6 chunks per row) — brute-forced against
-//   the ds_read_b128 lane groups of MI355X_MICROARCH.md §LDS.
-// * Epilogue goes through LDS: residual chunks are all requested before the
-//   first is used, and every global store is a full 16-byte chunk of
-//   consecutive channels (NHWC rows are contiguous).
+// * Step kinds (compile-time region geometry, so every index division is by a
+//   constant):
+//     1x1        region = tile
+//     3x3        region = tile + 1-pixel halo
+//     3x3 d2     region = tile + 2-pixel halo
+//     pair       EnhancedFAM branch1 + branch2 (models/model.py:29-32,66-69):
+//                x (1x1) and maxpool3x3(x) (1x1) from ONE region with a 1-pixel
+//                -inf halo — tap 0 reads the centre, tap 1 the 3x3 max
+//     1x1 s2     ResBlock projecting shortcut (model.py:114-118): region =
+//                every other input pixel of the tile's 2x footprint
+// * An op's segments form a PROGRAM: up to three phases of one kind each
+//   (e.g. FAM fusion = [3x3, 3x3 d2, pair]; ResBlock conv2 = [3x3, 1x1 s2]);
+//   the kernel is instantiated per program, so each phase is straight-line
+//   code and only one kind's registers are live at a time.
+// * Blocks loop over tiles (persistent grid, sized to co-resident blocks).
+//   The NEXT step's region (possibly of the next tile) is loaded into
+//   registers while the current step's MFMAs run; the pre-activation
+//   prologue (BN + ReLU) is applied when the registers are written to LDS.
+// * LDS pixel / weight-row strides make the 16-byte fragment reads of the MFMA
+//   operands bank-conflict free (fp32: 10 chunks per row with the
+//   k-permutation {g, g+4}; fp16: 6 chunks per row).
+// * Epilogue goes through LDS: residual chunks are requested before the last
+//   step's MFMAs, and every global store is a full 16-byte chunk of
+//   consecutive channels (NHWC rows are contiguous; the ConvTranspose 2x2
+//   pixel shuffle keeps each chunk inside one output pixel).
 //
 // MFMA fragments: lane (r = lane&15, g = lane>>4) owns 8 channels of pixel /
 // weight row r: fp16 [8g, 8g+8) -> one v_mfma_f32_16x16x32_f16;
@@ -44,47 +56,89 @@ template <> __device__ __forceinline__ float hfrom_f<float>(float v) { return v;
 template <> __device__ __forceinline__ half_t hfrom_f<half_t>(float v) { return (half_t)v; }
 
 constexpr int HALO_TW = 32;
-constexpr int HALO_MAXEXT = 4;  // 3x3 with dilation <= 2
+constexpr int HALO_MAXSTEPS = 64;
+
+// ---- step kinds and programs ------------------------------------------------
+enum HaloKind : int { kK1x1 = 0, kK3x3 = 1, kK3x3D2 = 2, kKPair = 3, kK1x1S2 = 4 };
+
+constexpr int kind_ext(int k) { return k == kK3x3 || k == kKPair ? 2 : (k == kK3x3D2 ? 4 : 0); }
+constexpr int kind_taps(int k) { return k == kK3x3 || k == kK3x3D2 ? 9 : (k == kKPair ? 2 : 1); }
+// program = up to 3 phases, kind+1 per 3-bit digit (0 terminates)
+constexpr int prog1(int a) { return a + 1; }
+constexpr int prog2(int a, int b) { return (a + 1) | (b + 1) << 3; }
+constexpr int prog3(int a, int b, int c) { return (a + 1) | (b + 1) << 3 | (c + 1) << 6; }
+constexpr int prog_len(int p) { return p == 0 ? 0 : 1 + prog_len(p >> 3); }
+constexpr int prog_kind(int p, int i) { return ((p >> (3 * i)) & 7) - 1; }
+
+// host-built step table: step -> (segment, 32-channel chunk); phase p = steps [end[p-1], end[p])
+struct HaloSteps {
+  int n;
+  int phase_end[3];
+  unsigned char si[HALO_MAXSTEPS];
+  unsigned char cq[HALO_MAXSTEPS];
+};
+
+// The whole kernel argument.  The kernel reads it through the kernarg segment
+// pointer: indexing op.seg[] / hs.si[] with a runtime step then compiles to
+// scalar loads, instead of the compiler copying the by-value argument to
+// scratch to make it addressable.
+struct HaloArgs {
+  ConvOp op;
+  HaloSteps hs;
+  int tiles_x, tiles_y, ntiles, region_bytes;
+};
 
 template <typename T, int NB, int TH>
 struct HaloCfg {
   static constexpr int EPC = 16 / sizeof(T);   // elements per 16-byte chunk
   static constexpr int CCH = 32 / EPC;         // chunks per 32-channel slice
   static constexpr int PSTR = sizeof(T) == 4 ? 40 : 48;  // row stride (elements): 10 / 6 chunks
-  static constexpr int HALO_ELEMS = (TH + HALO_MAXEXT) * (HALO_TW + HALO_MAXEXT) * PSTR;
   static constexpr int CSTR = NB + 4;          // fp32 epilogue staging stride
   static constexpr int EPI_BYTES = TH * HALO_TW * CSTR * 4;
-  static constexpr int REGION_BYTES =
-      HALO_ELEMS * (int)sizeof(T) > EPI_BYTES ? HALO_ELEMS * (int)sizeof(T) : EPI_BYTES;
-  static constexpr int B_ELEMS = 9 * NB * PSTR;
-  static constexpr int BYTES = REGION_BYTES + B_ELEMS * (int)sizeof(T);
-  static constexpr int PF = ((TH + HALO_MAXEXT) * (HALO_TW + HALO_MAXEXT) * CCH + 255) / 256;
   static constexpr int CHN = NB / EPC;         // epilogue chunks per pixel
   static constexpr int PPP = 256 / CHN;        // epilogue pixels per pass
   static constexpr int PASSES = TH * HALO_TW / PPP;
+  static constexpr int pf_of(int ext) { return ((TH + ext) * (HALO_TW + ext) * CCH + 255) / 256; }
 };
 
-// step kind: 0 = 1x1, 1 = 3x3 dil 1, 2 = 3x3 dil 2  ->  EXT = 0, 2, 4
-__device__ __forceinline__ int step_kind(const ConvSeg& s) { return s.kh == 1 ? 0 : (s.dil == 1 ? 1 : 2); }
+template <typename T, int NB, int TH, int PROG>
+struct ProgCfg {
+  static constexpr int NPH = prog_len(PROG);
+  static constexpr int K0 = prog_kind(PROG, 0);
+  static constexpr int K1 = NPH > 1 ? prog_kind(PROG, 1) : K0;
+  static constexpr int K2 = NPH > 2 ? prog_kind(PROG, 2) : K0;
+  static constexpr int MAXEXT = kind_ext(K0) > kind_ext(K1) ? (kind_ext(K0) > kind_ext(K2) ? kind_ext(K0) : kind_ext(K2))
+                                                            : (kind_ext(K1) > kind_ext(K2) ? kind_ext(K1) : kind_ext(K2));
+  static constexpr int PF = HaloCfg<T, NB, TH>::pf_of(MAXEXT);
+  static constexpr int MAXTAPS = kind_taps(K0) > kind_taps(K1)
+                                     ? (kind_taps(K0) > kind_taps(K2) ? kind_taps(K0) : kind_taps(K2))
+                                     : (kind_taps(K1) > kind_taps(K2) ? kind_taps(K1) : kind_taps(K2));
+  static constexpr int PW = (MAXTAPS * NB * HaloCfg<T, NB, TH>::CCH + 255) / 256;  // weight chunks per thread
+};
 
-template <typename T, int NB, int TH, int EXT>
-__device__ __forceinline__ void halo_load(uint4* pf, const ConvSeg& sg, int b, int oy0,
-                                          int ox0, int c0, int tid) {
+// Region of one step -> registers.  Every kind writes EVERY pf[] entry at a
+// constant index: when code paths write different subsets, the compiler merges
+// their stores through a phi'd address and demotes pf[] to scratch (each
+// prefetch then waits on vmcnt(0)).
+template <typename T, int NB, int TH, int KIND, int PFN>
+__device__ __forceinline__ void halo_load(uint4 (&pf)[PFN], const ConvSeg& sg, int b, int oy0, int ox0, int c0,
+                                          int tid) {
   using C = HaloCfg<T, NB, TH>;
-  constexpr int HW = HALO_TW + EXT, HH = TH + EXT, NCH = HH * HW * C::CCH;
-  constexpr int PAD = EXT / 2;
+  constexpr int EXT = kind_ext(KIND), HW = HALO_TW + EXT, HH = TH + EXT, NCH = HH * HW * C::CCH;
+  constexpr int PAD = EXT / 2, S = KIND == kK1x1S2 ? 2 : 1;
+  constexpr unsigned FILL = KIND != kKPair ? 0u : (sizeof(T) == 2 ? 0xFC00FC00u : 0xFF800000u);  // -inf
+  // opaque copy of tid: stops the per-entry offsets (tile-invariant) from being
+  // hoisted out of the tile loop and held in registers for every step kind
+  asm volatile("" : "+v"(tid));
   const T* base = (const T*)sg.src + (size_t)b * sg.Hin * sg.Win * sg.cs + sg.coff + c0;
-  // Every step kind writes EVERY pf[] entry at a constant index: when the kinds
-  // write different subsets, the compiler merges their stores through a phi'd
-  // address and demotes pf[] to scratch (each prefetch then waits on vmcnt(0)).
 #pragma unroll
-  for (int j = 0; j < C::PF; ++j) {
+  for (int j = 0; j < PFN; ++j) {
     const int q = tid + j * 256;
-    uint4 v = make_uint4(0, 0, 0, 0);
+    uint4 v = make_uint4(FILL, FILL, FILL, FILL);
     if (j * 256 < NCH) {
       const int px = q / C::CCH, ch = q % C::CCH;
       const int hy = px / HW, hx = px % HW;
-      const int iy = oy0 - PAD + hy, ix = ox0 - PAD + hx;
+      const int iy = S * (oy0 + hy) - PAD, ix = S * (ox0 + hx) - PAD;
       const bool ok = q < NCH && iy >= 0 && iy < sg.Hin && ix >= 0 && ix < sg.Win;
       if (ok) v = *(const uint4*)(base + ((size_t)iy * sg.Win + ix) * sg.cs + ch * C::EPC);
     }
@@ -92,22 +146,23 @@ __device__ __forceinline__ void halo_load(uint4* pf, const ConvSeg& sg, int b, i
   }
 }
 
-template <typename T, int NB, int TH, int EXT>
-__device__ __forceinline__ void halo_store(const uint4* pf, const ConvSeg& sg, int oy0,
-                                           int ox0, int c0, int tid, T* halo) {
+template <typename T, int NB, int TH, int KIND, int PFN>
+__device__ __forceinline__ void halo_store(const uint4 (&pf)[PFN], const ConvSeg& sg, int oy0, int ox0, int c0,
+                                           int tid, T* halo) {
   using C = HaloCfg<T, NB, TH>;
-  constexpr int HW = HALO_TW + EXT, HH = TH + EXT, NCH = HH * HW * C::CCH;
-  constexpr int PAD = EXT / 2;
-  const bool aff = sg.pre == kPreAffineRelu;
+  constexpr int EXT = kind_ext(KIND), HW = HALO_TW + EXT, HH = TH + EXT, NCH = HH * HW * C::CCH;
+  constexpr int PAD = EXT / 2, S = KIND == kK1x1S2 ? 2 : 1;
+  const bool aff = KIND != kKPair && sg.pre == kPreAffineRelu;
+  asm volatile("" : "+v"(tid));  // see halo_load
 #pragma unroll
-  for (int j = 0; j < C::PF; ++j) {
+  for (int j = 0; j < PFN; ++j) {
     const int q = tid + j * 256;
     if (j * 256 < NCH && q < NCH) {
       const int px = q / C::CCH, ch = q % C::CCH;
       uint4 v = pf[j];
       if (aff) {
         const int hy = px / HW, hx = px % HW;
-        const int iy = oy0 - PAD + hy, ix = ox0 - PAD + hx;
+        const int iy = S * (oy0 + hy) - PAD, ix = S * (ox0 + hx) - PAD;
         if (iy >= 0 && iy < sg.Hin && ix >= 0 && ix < sg.Win) {  // zero padding stays zero
           const int cb = c0 + ch * C::EPC;
           T* vv = (T*)&v;
@@ -121,42 +176,90 @@ __device__ __forceinline__ void halo_store(const uint4* pf, const ConvSeg& sg, i
   }
 }
 
-// 3x3/s1/p1 max-pool of the source for a 1x1 segment (EnhancedFAM branch2, model.py:32,69)
-template <typename T, int NB, int TH>
-__device__ void halo_pool(const ConvSeg& sg, int b, int oy0, int ox0, int c0, int tid, T* halo) {
+// Weights of one step (all taps x NB rows x 32 channels) -> registers; same
+// every-entry rule as halo_load.  Pair: tap t is segment si + t (both 1x1).
+template <typename T, int NB, int TH, int KIND, int PWN>
+__device__ __forceinline__ void wts_load(uint4 (&pw)[PWN], const ConvOp& op, int si, int c0, int n0, int tid) {
   using C = HaloCfg<T, NB, TH>;
-  const T* src = (const T*)sg.src;
-  for (int q = tid; q < TH * HALO_TW * C::CCH; q += 256) {
-    const int px = q / C::CCH, ch = q % C::CCH;
-    const int iy = oy0 + px / HALO_TW, ix = ox0 + px % HALO_TW;
+  constexpr int NBQ = kind_taps(KIND) * NB * C::CCH;
+  const T* W = (const T*)op.W;
+  asm volatile("" : "+v"(tid));  // see halo_load
+#pragma unroll
+  for (int j = 0; j < PWN; ++j) {
+    const int q = tid + j * 256;
     uint4 v = make_uint4(0, 0, 0, 0);
-    if (iy < sg.Hin && ix < sg.Win) {
-      float mx[C::EPC];
-#pragma unroll
-      for (int e = 0; e < C::EPC; ++e) mx[e] = -INFINITY;
-      for (int dy = -1; dy <= 1; ++dy) {
-        const int yy = iy + dy;
-        if (yy < 0 || yy >= sg.Hin) continue;
-        for (int dx = -1; dx <= 1; ++dx) {
-          const int xx = ix + dx;
-          if (xx < 0 || xx >= sg.Win) continue;
-          const uint4 w4 =
-              *(const uint4*)(src + (((size_t)b * sg.Hin + yy) * sg.Win + xx) * sg.cs + sg.coff + c0 + ch * C::EPC);
-          const T* wv = (const T*)&w4;
-#pragma unroll
-          for (int e = 0; e < C::EPC; ++e) mx[e] = fmaxf(mx[e], hto_f(wv[e]));
-        }
-      }
-      T* vv = (T*)&v;
-#pragma unroll
-      for (int e = 0; e < C::EPC; ++e) vv[e] = hfrom_f<T>(mx[e]);
+    if (j * 256 < NBQ && q < NBQ) {
+      const int row = q / C::CCH, ch = q % C::CCH;  // row = tap*NB + n
+      const int tap = row / NB, n = row % NB;
+      const ConvSeg& sg = op.seg[KIND == kKPair ? si + tap : si];
+      const int koff = KIND == kKPair ? 0 : tap * sg.C;
+      v = *(const uint4*)(W + (size_t)(n0 + n) * op.Kpad + sg.kbase + koff + c0 + ch * C::EPC);
     }
-    *(uint4*)(halo + px * C::PSTR + ch * C::EPC) = v;
+    pw[j] = v;
   }
 }
 
+template <typename T, int NB, int TH, int KIND, int PWN>
+__device__ __forceinline__ void wts_store(const uint4 (&pw)[PWN], int tid, T* Bs) {
+  using C = HaloCfg<T, NB, TH>;
+  constexpr int NBQ = kind_taps(KIND) * NB * C::CCH;
+  asm volatile("" : "+v"(tid));
+#pragma unroll
+  for (int j = 0; j < PWN; ++j) {
+    const int q = tid + j * 256;
+    if (j * 256 < NBQ && q < NBQ) {
+      const int row = q / C::CCH, ch = q % C::CCH;
+      *(uint4*)(Bs + row * C::PSTR + ch * C::EPC) = pw[j];
+    }
+  }
+}
+
+// A fragments of one M tile (16 pixels starting at region pixel `pix`)
+template <typename T, int PSTR>
+struct Frag;
+template <int PSTR>
+struct Frag<half_t, PSTR> {
+  f16x8_h v;
+  __device__ __forceinline__ void ld(const half_t* s, int pix, int fg) { v = *(const f16x8_h*)(s + pix * PSTR + fg * 8); }
+  __device__ __forceinline__ void max_with(const Frag& o) { v = __builtin_elementwise_max(v, o.v); }
+};
+template <int PSTR>
+struct Frag<float, PSTR> {
+  f32x4_h v[2];
+  __device__ __forceinline__ void ld(const float* s, int pix, int fg) {
+    const float* p = s + pix * PSTR + fg * 4;
+    v[0] = *(const f32x4_h*)p;
+    v[1] = *(const f32x4_h*)(p + 16);
+  }
+  __device__ __forceinline__ void max_with(const Frag& o) {
+    v[0] = __builtin_elementwise_max(v[0], o.v[0]);
+    v[1] = __builtin_elementwise_max(v[1], o.v[1]);
+  }
+};
+
+template <int MT, int NT, int PSTR>
+__device__ __forceinline__ void frag_mma(f32x4_h (&acc)[MT][NT], const Frag<half_t, PSTR> (&af)[MT],
+                                         const Frag<half_t, PSTR> (&bf)[NT]) {
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i].v, bf[j].v, acc[i][j], 0, 0, 0);
+}
+template <int MT, int NT, int PSTR>
+__device__ __forceinline__ void frag_mma(f32x4_h (&acc)[MT][NT], const Frag<float, PSTR> (&af)[MT],
+                                         const Frag<float, PSTR> (&bf)[NT]) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i].v[e >> 2][e & 3], bf[j].v[e >> 2][e & 3], acc[i][j],
+                                                        0, 0, 0);
+}
+
 // all taps of one step
-template <typename T, int NB, int TH, int K, int D>
+template <typename T, int NB, int TH, int KIND>
 __device__ __forceinline__ void halo_taps(f32x4_h (&acc)[TH / 2][NB / 16], const T* halo, const T* Bs, int wave,
                                           int fr, int fg) {
   using C = HaloCfg<T, NB, TH>;
@@ -164,69 +267,62 @@ __device__ __forceinline__ void halo_taps(f32x4_h (&acc)[TH / 2][NB / 16], const
   constexpr int RPW = TH / 4;
   constexpr int MT = 2 * RPW;
   constexpr int NT = NB / 16;
-  constexpr int HW = HALO_TW + (K - 1) * D;
-  constexpr int NTAP = K * K;
-  if constexpr (sizeof(T) == 2) {
+  constexpr int EXT = kind_ext(KIND);
+  constexpr int HW = HALO_TW + EXT;
+  using F = Frag<T, PSTR>;
+  auto pix = [&](int i, int r, int c) { return (wave * RPW + (i >> 1) + r) * HW + (i & 1) * 16 + fr + c; };
+  if constexpr (KIND == kKPair) {
+    F bf[NT], af[MT];
 #pragma unroll
-    for (int tap = 0; tap < NTAP; ++tap) {
-      const int r = tap / K, c = tap % K;
-      f16x8_h bf[NT], af[MT];
+    for (int j = 0; j < NT; ++j) bf[j].ld(Bs, j * 16 + fr, fg);
 #pragma unroll
-      for (int j = 0; j < NT; ++j) bf[j] = *(const f16x8_h*)(Bs + (tap * NB + j * 16 + fr) * PSTR + fg * 8);
+    for (int i = 0; i < MT; ++i) af[i].ld(halo, pix(i, 1, 1), fg);
+    frag_mma<MT, NT, PSTR>(acc, af, bf);
 #pragma unroll
-      for (int i = 0; i < MT; ++i) {
-        const int py = wave * RPW + (i >> 1) + r * D, pxx = (i & 1) * 16 + fr + c * D;
-        af[i] = *(const f16x8_h*)(halo + (py * HW + pxx) * PSTR + fg * 8);
+    for (int j = 0; j < NT; ++j) bf[j].ld(Bs, NB + j * 16 + fr, fg);
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        if (t == 4) continue;  // centre already in af[i]
+        F o;
+        o.ld(halo, pix(i, t / 3, t % 3), fg);
+        af[i].max_with(o);
       }
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
+    frag_mma<MT, NT, PSTR>(acc, af, bf);
   } else {
+    constexpr int K = kind_taps(KIND) == 9 ? 3 : 1;
+    constexpr int D = KIND == kK3x3D2 ? 2 : 1;
 #pragma unroll
-    for (int tap = 0; tap < NTAP; ++tap) {
+    for (int tap = 0; tap < K * K; ++tap) {
       const int r = tap / K, c = tap % K;
-      f32x4_h bf[NT][2], af[MT][2];
+      F bf[NT], af[MT];
 #pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const float* p = (const float*)Bs + (tap * NB + j * 16 + fr) * PSTR + fg * 4;
-        bf[j][0] = *(const f32x4_h*)p;
-        bf[j][1] = *(const f32x4_h*)(p + 16);
-      }
+      for (int j = 0; j < NT; ++j) bf[j].ld(Bs, tap * NB + j * 16 + fr, fg);
 #pragma unroll
-      for (int i = 0; i < MT; ++i) {
-        const int py = wave * RPW + (i >> 1) + r * D, pxx = (i & 1) * 16 + fr + c * D;
-        const float* p = (const float*)halo + (py * HW + pxx) * PSTR + fg * 4;
-        af[i][0] = *(const f32x4_h*)p;
-        af[i][1] = *(const f32x4_h*)(p + 16);
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e)
-#pragma unroll
-        for (int i = 0; i < MT; ++i)
-#pragma unroll
-          for (int j = 0; j < NT; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][e >> 2][e & 3], bf[j][e >> 2][e & 3], acc[i][j],
-                                                            0, 0, 0);
+      for (int i = 0; i < MT; ++i) af[i].ld(halo, pix(i, r * D, c * D), fg);
+      frag_mma<MT, NT, PSTR>(acc, af, bf);
     }
   }
 }
 
-// The next step's region (possibly of the next tile) is loaded into registers
-// during the current step's MFMAs.  OCC = waves per SIMD the register
-// allocation must allow (= co-resident 256-thread blocks per CU): above 1 the
-// compiler stops hoisting every tap's fragment reads and a second block's
-// MFMAs overlap this block's staging / epilogue.  KM = bitmask of the step
-// kinds the op contains (1: 1x1, 2: 3x3 d1, 4: 3x3 d2); a single-kind op gets
-// a kernel with only that kind's region / tap code (fewer live registers).
-template <typename T, int NB, int TH, int OCC, int KM>
+template <int V>
+using IC = std::integral_constant<int, V>;
+
+// OCC = waves per SIMD the register allocation must allow (= co-resident
+// 256-thread blocks per CU): at 2 a second block's MFMAs overlap this block's
+// staging / epilogue.
+template <typename T, int NB, int TH, int OCC, int PROG>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void conv_halo_kernel(
-    ConvOp op, int tiles_x, int tiles_y, int ntiles, int region_bytes) {
-  constexpr bool PREF = true;
+    HaloArgs args) {
+  const HaloArgs& A = *(const HaloArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  const ConvOp& op = A.op;
+  const HaloSteps& hs = A.hs;
+  const int tiles_x = A.tiles_x, tiles_y = A.tiles_y, ntiles = A.ntiles, region_bytes = A.region_bytes;
   using C = HaloCfg<T, NB, TH>;
-  constexpr int EPC = C::EPC, CCH = C::CCH, PSTR = C::PSTR;
+  using P = ProgCfg<T, NB, TH, PROG>;
+  constexpr int EPC = C::EPC;
   constexpr int TW = HALO_TW;
   constexpr int RPW = TH / 4;  // tile rows per wave
   constexpr int MT = 2 * RPW;  // 16-pixel M tiles per wave
@@ -242,14 +338,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
   const int fr = lane & 15, fg = lane >> 4;
   const int nblk_n = op.N / NB;
   const int HWo = op.Ho * op.Wo;
-  const T* W = (const T*)op.W;
   // at most one residual per op (launch_conv_halo checks): added before (res1) or after (res2) the ReLU
   const T* resp = (const T*)(op.res1 ? op.res1 : op.res2);
   const int res_cs = op.res1 ? op.res1_cs : op.res2_cs;
   const bool res_pre = op.res1 != nullptr;
-
-  int nsteps = 0;
-  for (int s = 0; s < op.nseg; ++s) nsteps += op.seg[s].C / 32;
+  const int nsteps = hs.n;
   const bool b_keep = nsteps == 1 && nblk_n == 1;  // weights identical for every tile of the block
 
   auto tile_coords = [&](int tile, int& b, int& oy0, int& ox0, int& n0) {
@@ -259,52 +352,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     const int ty = t % tiles_y; t /= tiles_y;
     b = t; oy0 = ty * TH; ox0 = tx * TW; n0 = nb * NB;
   };
-  auto step_seg = [&](int step, int& si, int& c0) {
-    si = 0;
-    int s = step;
-    while (s >= op.seg[si].C / 32) { s -= op.seg[si].C / 32; ++si; }
-    c0 = s * 32;
-  };
-  auto kind_of = [&](const ConvSeg& sg) -> int {
-    if constexpr (KM == 1) return 0;
-    if constexpr (KM == 2) return 1;
-    if constexpr (KM == 4) return 2;
-    return step_kind(sg);
-  };
-  uint4 pf[C::PF];
-  auto load = [&](int step, int tile) {
-    int b, oy0, ox0, n0, si, c0;
+  // the next step's region and (unless resident) weights, in registers
+  uint4 pf[P::PF];
+  uint4 pw[P::PW];
+  auto load = [&](auto kc, int step, int tile) {
+    constexpr int K = decltype(kc)::value;
+    int b, oy0, ox0, n0;
     tile_coords(tile, b, oy0, ox0, n0);
-    step_seg(step, si, c0);
-    const ConvSeg& sg = op.seg[si];
-    const int kind = kind_of(sg);
-    if ((KM & 1) && kind == 0) {
-      if (sg.pre != kPreMaxPool3) halo_load<T, NB, TH, 0>(pf, sg, b, oy0, ox0, c0, tid);
-    } else if ((KM & 2) && kind == 1) {
-      halo_load<T, NB, TH, 2>(pf, sg, b, oy0, ox0, c0, tid);
-    } else if (KM & 4) {
-      halo_load<T, NB, TH, 4>(pf, sg, b, oy0, ox0, c0, tid);
-    }
-  };
-  auto stage_b = [&](const ConvSeg& sg, int c0, int n0) {
-    const int nbq = sg.kh * sg.kw * NB * CCH;
-    for (int q = tid; q < nbq; q += 256) {
-      const int row = q / CCH, ch = q % CCH;  // row = tap*NB + n
-      const int tap = row / NB, n = row % NB;
-      *(uint4*)(Bs + row * PSTR + ch * EPC) =
-          *(const uint4*)(W + (size_t)(n0 + n) * op.Kpad + sg.kbase + tap * sg.C + c0 + ch * EPC);
-    }
+    halo_load<T, NB, TH, K>(pf, op.seg[hs.si[step]], b, oy0, ox0, hs.cq[step] * 32, tid);
+    if (!b_keep) wts_load<T, NB, TH, K>(pw, op, hs.si[step], hs.cq[step] * 32, n0, tid);
   };
 
   int tile = blockIdx.x;
   if (tile >= ntiles) return;
-  if (b_keep) {
-    int b, oy0, ox0, n0, si, c0;
+  if (b_keep) {  // one step, one N block: weights staged once per block
+    int b, oy0, ox0, n0;
     tile_coords(tile, b, oy0, ox0, n0);
-    step_seg(0, si, c0);
-    stage_b(op.seg[si], c0, n0);
+    wts_load<T, NB, TH, P::K0>(pw, op, hs.si[0], hs.cq[0] * 32, n0, tid);
+    wts_store<T, NB, TH, P::K0>(pw, tid, Bs);
   }
-  if constexpr (PREF) load(0, tile);
+  load(IC<P::K0>{}, 0, tile);
 
   for (; tile < ntiles; tile += gridDim.x) {
     int b, oy0, ox0, n0;
@@ -319,47 +386,49 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     const int ch = tid % CHN;
     const int nb0 = ch * EPC;  // first channel (within the block slice) of this thread in the epilogue
     uint4 rr[PASSES];
-    for (int step = 0; step < nsteps; ++step) {
-      int si, c0;
-      step_seg(step, si, c0);
-      const ConvSeg& sg = op.seg[si];
-      const int kind = kind_of(sg);
-      if constexpr (!PREF) load(step, tile);
-      __syncthreads();  // LDS free (previous step's MFMAs / previous tile's epilogue)
-      if ((KM & 1) && kind == 0) {
-        if (sg.pre == kPreMaxPool3)
-          halo_pool<T, NB, TH>(sg, b, oy0, ox0, c0, tid, halo);
-        else
-          halo_store<T, NB, TH, 0>(pf, sg, oy0, ox0, c0, tid, halo);
-      } else if ((KM & 2) && kind == 1) {
-        halo_store<T, NB, TH, 2>(pf, sg, oy0, ox0, c0, tid, halo);
-      } else if (KM & 4) {
-        halo_store<T, NB, TH, 4>(pf, sg, oy0, ox0, c0, tid, halo);
-      }
-      if (!b_keep) stage_b(sg, c0, n0);
-      __syncthreads();
-      if constexpr (PREF) {
-        const int nstep = step + 1 < nsteps ? step + 1 : 0;
-        const int ntile = step + 1 < nsteps ? tile : tile + gridDim.x;
-        if (ntile < ntiles) load(nstep, ntile);
-      }
-      if (step == nsteps - 1 && resp) {
-        // residual chunks of this tile, requested before the last step's MFMAs
-#pragma unroll
-        for (int ps = 0; ps < PASSES; ++ps) {
-          const int p = tid / CHN + ps * PPP;
-          const int oy = oy0 + p / TW, ox = ox0 + p % TW;
-          const size_t m = ((size_t)b * op.Ho + oy) * op.Wo + ox;
-          rr[ps] = (oy < op.Ho && ox < op.Wo) ? *(const uint4*)(resp + m * res_cs + n0 + nb0) : make_uint4(0, 0, 0, 0);
+    int step = 0;
+    // one phase: steps [step, pend) of kind K; the step after the phase is of kind KN
+    auto phase = [&](auto kc, auto knc, int pend) {
+      constexpr int K = decltype(kc)::value;
+      for (; step < pend; ++step) {
+        const int si = hs.si[step], c0 = hs.cq[step] * 32;
+        const ConvSeg& sg = op.seg[si];
+        __syncthreads();  // LDS free (previous step's MFMAs / previous tile's epilogue)
+        halo_store<T, NB, TH, K>(pf, sg, oy0, ox0, c0, tid, halo);
+        if (!b_keep) wts_store<T, NB, TH, K>(pw, tid, Bs);
+        __syncthreads();
+        {
+          // next step: this tile's, or the first of the block's next tile
+          int ns = step + 1, nt = tile;
+          if (ns == nsteps) { ns = 0; nt = tile + (int)gridDim.x; }
+          // the step after a phase is the next phase's first (kind KN) or, after
+          // the last phase, the next tile's first (KN == K0): at most 2 call sites
+          if (nt < ntiles) {
+            if constexpr (K == decltype(knc)::value)
+              load(kc, ns, nt);
+            else if (ns > 0 && ns < pend)
+              load(kc, ns, nt);
+            else
+              load(knc, ns, nt);
+          }
         }
+        if (step == nsteps - 1 && resp) {
+          // residual chunks of this tile, requested before the last step's MFMAs
+#pragma unroll
+          for (int ps = 0; ps < PASSES; ++ps) {
+            const int p = tid / CHN + ps * PPP;
+            const int oy = oy0 + p / TW, ox = ox0 + p % TW;
+            const size_t m = ((size_t)b * op.Ho + oy) * op.Wo + ox;
+            rr[ps] = (oy < op.Ho && ox < op.Wo) ? *(const uint4*)(resp + m * res_cs + n0 + nb0)
+                                                : make_uint4(0, 0, 0, 0);
+          }
+        }
+        halo_taps<T, NB, TH, K>(acc, halo, Bs, wave, fr, fg);
       }
-      if ((KM & 1) && kind == 0)
-        halo_taps<T, NB, TH, 1, 1>(acc, halo, Bs, wave, fr, fg);
-      else if ((KM & 2) && kind == 1)
-        halo_taps<T, NB, TH, 3, 1>(acc, halo, Bs, wave, fr, fg);
-      else if (KM & 4)
-        halo_taps<T, NB, TH, 3, 2>(acc, halo, Bs, wave, fr, fg);
-    }
+    };
+    phase(IC<P::K0>{}, IC<P::K1>{}, hs.phase_end[0]);
+    if constexpr (P::NPH > 1) phase(IC<P::K1>{}, IC<P::K2>{}, hs.phase_end[1]);
+    if constexpr (P::NPH > 2) phase(IC<P::K2>{}, IC<P::K0>{}, hs.phase_end[2]);
 
     // ---- epilogue ------------------------------------------------------------
     __syncthreads();
@@ -423,7 +492,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
             x0 = x[0]; x1 = x[HWo]; x2 = x[2 * HWo];
           }
           const float z = (x0 + x1 + x2) / 3.f + (part + op.head_b);
-          op.illu[m] = 1.f / (1.f + expf(-z));
+          const float il = 1.f / (1.f + expf(-z));
+          if (op.illu_f16) ((half_t*)op.illu)[m] = (half_t)il;
+          else op.illu[m] = il;
         }
         continue;
       }
@@ -450,7 +521,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
       T* ov = (T*)&o;
 #pragma unroll
       for (int e = 0; e < EPC; ++e) ov[e] = hfrom_f<T>(v[e]);
-      *(uint4*)(out + m * op.out_cs + op.out_coff + n0 + nb0) = o;
+      if (op.store == kStoreConvT2x2) {
+        // ConvTranspose2d(2, 2) pixel shuffle (model.py:167): n = (dy*2+dx)*Cout + co
+        const int cout = op.N >> 2;
+        const int n = n0 + nb0, q = n / cout, co = n - q * cout;
+        const size_t opix = ((size_t)b * 2 * op.Ho + 2 * oy + (q >> 1)) * (2 * op.Wo) + 2 * ox + (q & 1);
+        *(uint4*)(out + opix * op.out_cs + op.out_coff + co) = o;
+      } else {
+        *(uint4*)(out + m * op.out_cs + op.out_coff + n0 + nb0) = o;
+      }
 #pragma unroll
       for (int e = 0; e < EPC; ++e) psum[e] += hto_f(ov[e]);
     }
@@ -470,73 +549,121 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
   }
 }
 
-template <typename T, int NB, int TH, int OCC, int KM>
-static int launch_halo_cfg(const ConvOp& op, hipStream_t st) {
+// ---- host side ------------------------------------------------------------------
+
+template <typename T, int NB, int TH, int OCC, int PROG>
+static int launch_halo_cfg(const ConvOp& op, const HaloSteps& hs, hipStream_t st) {
   const int tiles_x = cdiv(op.Wo, HALO_TW), tiles_y = cdiv(op.Ho, TH);
   const int ntiles = op.B * tiles_x * tiles_y * (op.N / NB);
   using C = HaloCfg<T, NB, TH>;
-  // LDS: region for the largest halo extent / tap count among this op's segments
-  int ext = 0, taps = 1;
-  for (int s = 0; s < op.nseg; ++s) {
-    const int e = (op.seg[s].kh - 1) * op.seg[s].dil;
-    ext = e > ext ? e : ext;
-    taps = op.seg[s].kh * op.seg[s].kw > taps ? op.seg[s].kh * op.seg[s].kw : taps;
-  }
-  const int halo_bytes = (TH + ext) * (HALO_TW + ext) * C::PSTR * (int)sizeof(T);
-  const int region = (int)align_up((size_t)(halo_bytes > C::EPI_BYTES ? halo_bytes : C::EPI_BYTES), 16);
-  const int lds = region + taps * NB * C::PSTR * (int)sizeof(T);
+  using P = ProgCfg<T, NB, TH, PROG>;
+  // LDS: region for the largest halo extent, weights for the largest tap count of the program
+  constexpr int taps = kind_taps(P::K0) > kind_taps(P::K1)
+                           ? (kind_taps(P::K0) > kind_taps(P::K2) ? kind_taps(P::K0) : kind_taps(P::K2))
+                           : (kind_taps(P::K1) > kind_taps(P::K2) ? kind_taps(P::K1) : kind_taps(P::K2));
+  constexpr int halo_bytes = (TH + P::MAXEXT) * (HALO_TW + P::MAXEXT) * C::PSTR * (int)sizeof(T);
+  constexpr int region = ((halo_bytes > C::EPI_BYTES ? halo_bytes : C::EPI_BYTES) + 15) / 16 * 16;
+  constexpr int lds = region + taps * NB * C::PSTR * (int)sizeof(T);
+  static_assert(lds <= 160 * 1024, "halo LDS budget");
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)conv_halo_kernel<T, NB, TH, OCC, KM>,
+    (void)hipFuncSetAttribute((const void*)conv_halo_kernel<T, NB, TH, OCC, PROG>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
   // Persistent grid = blocks that are actually co-resident (registers AND LDS);
   // an oversized grid leaves a second, partial wave of blocks (tail).  Speed only.
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)conv_halo_kernel<T, NB, TH, OCC, KM>, 256,
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)conv_halo_kernel<T, NB, TH, OCC, PROG>, 256,
                                                    lds) != hipSuccess || per_cu < 1)
     per_cu = 1;
   const int lds_cap = (160 * 1024) / lds;
   if (per_cu > lds_cap) per_cu = lds_cap < 1 ? 1 : lds_cap;
   int grid = 256 * per_cu;
   if (grid > ntiles) grid = ntiles;
-  hipLaunchKernelGGL((conv_halo_kernel<T, NB, TH, OCC, KM>), dim3(grid), dim3(256), lds, st, op, tiles_x, tiles_y,
-                     ntiles, region);
+  HaloArgs args;
+  args.op = op;
+  args.hs = hs;
+  args.tiles_x = tiles_x;
+  args.tiles_y = tiles_y;
+  args.ntiles = ntiles;
+  args.region_bytes = region;
+  hipLaunchKernelGGL((conv_halo_kernel<T, NB, TH, OCC, PROG>), dim3(grid), dim3(256), lds, st, args);
   return (int)hipGetLastError();
 }
 
-template <typename T, int NB, int KM>
-static int launch_halo_th(const ConvOp& op, int th, int occ, hipStream_t st) {
-  if constexpr (KM == 2) {  // single-kind ops: registers leave room for 2-3 blocks per CU
-    if (th == 4) {
-      if (occ >= 3) return launch_halo_cfg<T, NB, 4, 3, KM>(op, st);
-      return occ == 2 ? launch_halo_cfg<T, NB, 4, 2, KM>(op, st) : launch_halo_cfg<T, NB, 4, 1, KM>(op, st);
-    }
-    return occ >= 2 ? launch_halo_cfg<T, NB, 8, 2, KM>(op, st) : launch_halo_cfg<T, NB, 8, 1, KM>(op, st);
-  }
-  return th == 4 ? launch_halo_cfg<T, NB, 4, 1, KM>(op, st) : launch_halo_cfg<T, NB, 8, 1, KM>(op, st);
+template <typename T, int NB, int PROG>
+static int launch_halo_prog(const ConvOp& op, const HaloSteps& hs, int th, int occ, hipStream_t st) {
+  if (th == 4) return occ >= 3 ? launch_halo_cfg<T, NB, 4, 3, PROG>(op, hs, st) : launch_halo_cfg<T, NB, 4, 2, PROG>(op, hs, st);
+  return occ >= 2 ? launch_halo_cfg<T, NB, 8, 2, PROG>(op, hs, st) : launch_halo_cfg<T, NB, 8, 1, PROG>(op, hs, st);
 }
+
+// the programs instantiated (any other segment mix runs on the generic kernel)
+constexpr int kProg3x3 = prog1(kK3x3);
+constexpr int kProg1x1 = prog1(kK1x1);
+constexpr int kProgD2 = prog1(kK3x3D2);
+constexpr int kProgFam = prog3(kK3x3, kK3x3D2, kKPair);  // EnhancedFAM fusion GEMM
+constexpr int kProgResS2 = prog2(kK3x3, kK1x1S2);        // ResBlock conv2 + projecting shortcut
 
 template <typename T, int NB>
-static int launch_halo_km(const ConvOp& op, int km, int th, int occ, hipStream_t st) {
-  if (km == 2) return launch_halo_th<T, NB, 2>(op, th, occ, st);
-  return launch_halo_th<T, NB, 7>(op, th, occ, st);
+static int launch_halo_nb(const ConvOp& op, const HaloSteps& hs, int prog, int th, int occ, hipStream_t st) {
+  switch (prog) {
+    case kProg3x3: return launch_halo_prog<T, NB, kProg3x3>(op, hs, th, occ, st);
+    case kProg1x1: return launch_halo_prog<T, NB, kProg1x1>(op, hs, th, occ, st);
+    case kProgD2: return launch_halo_prog<T, NB, kProgD2>(op, hs, th, occ, st);
+    case kProgFam: return launch_halo_prog<T, NB, kProgFam>(op, hs, th, occ, st);
+    case kProgResS2: return launch_halo_prog<T, NB, kProgResS2>(op, hs, th, occ, st);
+    default: return kErrUnsupported;
+  }
 }
 
-// Tile rows / occupancy per layer class; UPR_HALO="<th>,<occ>" overrides (experiments).
-// Measured on MI355X (tools/halo_sweep.sh, UP-Retinex layer shapes, bs 32):
-// single-kind 3x3 ops run 2 blocks per CU — fp16 with 8-row tiles, fp32 with
-// 4-row tiles (8-row fp32 tiles need > 256 registers); mixed-kind ops (the
-// FAM fusion GEMM, dilated convs) 8-row tiles, 1 block per CU.
-static void halo_choice(int dtype, int N, int km, int& th, int& occ) {
-  (void)N;
-  if (km == 2) {
-    th = dtype == kF16 ? 8 : 4;
-    occ = 2;
-  } else {
+// Segment kind of the halo kernel, or -1.  `pair` = segment s+1 is the max-pool
+// twin of s (same source slice), consumed together.
+static int seg_kind(const ConvOp& op, int s, int Ho, int Wo, bool& pair) {
+  const ConvSeg& g = op.seg[s];
+  pair = false;
+  if (g.C % 32 || g.kh != g.kw) return -1;
+  if (g.stride == 2) {
+    if (g.kh != 1 || g.pad != 0 || g.pre != kPreNone) return -1;
+    if ((g.Hin - 1) / 2 + 1 != Ho || (g.Win - 1) / 2 + 1 != Wo) return -1;
+    return kK1x1S2;
+  }
+  if (g.stride != 1 || g.Hin != Ho || g.Win != Wo) return -1;
+  if (g.kh == 3) {
+    if (g.dil == 1 && g.pad == 1) return kK3x3;
+    if (g.dil == 2 && g.pad == 2) return kK3x3D2;
+    return -1;
+  }
+  if (g.kh != 1 || g.pad != 0) return -1;
+  if (g.pre == kPreMaxPool3) return -1;  // only as the twin of a plain 1x1
+  if (s + 1 < op.nseg) {
+    const ConvSeg& h = op.seg[s + 1];
+    if (h.pre == kPreMaxPool3 && g.pre == kPreNone && h.kh == 1 && h.kw == 1 && h.stride == 1 && h.pad == 0 &&
+        h.src == g.src && h.C == g.C && h.cs == g.cs && h.coff == g.coff && h.Hin == g.Hin && h.Win == g.Win) {
+      pair = true;
+      return kKPair;
+    }
+  }
+  return kK1x1;
+}
+
+// Tile rows / occupancy per program, from per-layer sweeps of the whole forward
+// on MI355X (tools/layer_sweep.sh + tools/layer_table.py, bs 32, 512^2):
+//   fp32: 4-row tiles at 2 blocks/CU; 8-row tiles for the 1x1 (ConvT) and the
+//         FAM fusion program (1 block/CU: it restages weights every step)
+//   fp16: 8-row tiles; 2 blocks/CU for one-step ops, the FAM fusion and 1x1,
+//         1 block/CU for multi-step ops; the residual head 4-row at 3 blocks/CU
+// UPR_HALO="<th>,<occ>" overrides (experiments).
+static void halo_choice(int dtype, int prog, int store, int nsteps, int& th, int& occ) {
+  if (dtype == kF16) {
     th = 8;
-    occ = 1;
+    occ = nsteps > 1 && prog != kProgFam && prog != kProg1x1 ? 1 : 2;
+    if (store == kStoreHeadIllu) { th = 4; occ = 3; }
+  } else {
+    th = 4;
+    occ = 2;
+    if (prog == kProg1x1) th = 8;
+    if (prog == kProgFam) { th = 8; occ = 1; }
   }
   const char* e = getenv("UPR_HALO");
   if (e) {
@@ -547,38 +674,51 @@ static void halo_choice(int dtype, int N, int km, int& th, int& occ) {
 
 // Returns kErrUnsupported when the op is not a halo-kernel shape (caller falls back).
 int launch_conv_halo(const ConvOp& op, int dtype, hipStream_t st) {
-  if (op.store == kStoreConvT2x2) return kErrUnsupported;
   if (op.Wo < 24 || op.Ho < 8) return kErrUnsupported;
-  for (int s = 0; s < op.nseg; ++s) {
-    const ConvSeg& g = op.seg[s];
-    if (g.stride != 1 || g.kh != g.kw) return kErrUnsupported;
-    if (g.kh == 3) {
-      if (g.dil < 1 || g.dil > HALO_MAXEXT / 2 || g.pad != g.dil) return kErrUnsupported;
-    } else if (g.kh == 1) {
-      if (g.pad != 0) return kErrUnsupported;
-      if (g.pre == kPreMaxPool3 && g.dil != 1) return kErrUnsupported;
-    } else {
-      return kErrUnsupported;
-    }
-    if (g.Hin != op.Ho || g.Win != op.Wo) return kErrUnsupported;
-  }
   const int elt = dtype == kF16 ? 2 : 4;
   if (op.out && ((op.out_cs * elt) % 16 || (op.out_coff * elt) % 16)) return kErrUnsupported;
   if (op.res1 && (op.res1_cs * elt) % 16) return kErrUnsupported;
   if (op.res2 && (op.res2_cs * elt) % 16) return kErrUnsupported;
   if (op.res1 && op.res2) return kErrUnsupported;
   if (op.store == kStoreHeadIllu && op.N != 32) return kErrUnsupported;
+  if (op.store == kStoreConvT2x2 && ((op.N / 4) % 16 || op.pool)) return kErrUnsupported;
   if (op.bias && ((uintptr_t)op.bias % 16)) return kErrUnsupported;
   if (op.scale) return kErrUnsupported;  // the graph folds every scale into the weights
-  int km = 0;
-  for (int s = 0; s < op.nseg; ++s) km |= 1 << (op.seg[s].kh == 1 ? 0 : (op.seg[s].dil == 1 ? 1 : 2));
+  // step table + program
+  HaloSteps hs;
+  hs.n = 0;
+  int kinds[3], nph = 0;
+  for (int s = 0; s < op.nseg; ++s) {
+    bool pair = false;
+    const int k = seg_kind(op, s, op.Ho, op.Wo, pair);
+    if (k < 0) return kErrUnsupported;
+    if (nph == 0 || kinds[nph - 1] != k) {
+      if (nph == 3) return kErrUnsupported;
+      if (nph > 0) hs.phase_end[nph - 1] = hs.n;
+      kinds[nph++] = k;
+    }
+    for (int cq = 0; cq < op.seg[s].C / 32; ++cq) {
+      if (hs.n == HALO_MAXSTEPS) return kErrUnsupported;
+      hs.si[hs.n] = (unsigned char)s;
+      hs.cq[hs.n] = (unsigned char)cq;
+      ++hs.n;
+    }
+    if (pair) ++s;
+  }
+  if (nph == 0) return kErrUnsupported;
+  hs.phase_end[nph - 1] = hs.n;
+  for (int p = nph; p < 3; ++p) hs.phase_end[p] = hs.n;
+  const int prog = nph == 1 ? prog1(kinds[0]) : (nph == 2 ? prog2(kinds[0], kinds[1]) : prog3(kinds[0], kinds[1], kinds[2]));
   int th, occ;
-  halo_choice(dtype, op.N, km, th, occ);
+  halo_choice(dtype, prog, op.store, hs.n, th, occ);
+  if (getenv("UPR_HALO_DEBUG"))
+    fprintf(stderr, "[halo] prog %d (%d phases, %d steps) N=%d %dx%d th=%d occ=%d\n", prog, nph, hs.n, op.N, op.Ho,
+            op.Wo, th, occ);
   if (dtype == kF16) {
-    if (op.N == 32) return launch_halo_km<half_t, 32>(op, km, th, occ, st);
-    if (op.N % 64 == 0) return launch_halo_km<half_t, 64>(op, km, th, occ, st);
+    if (op.N == 32) return launch_halo_nb<half_t, 32>(op, hs, prog, th, occ, st);
+    if (op.N % 64 == 0) return launch_halo_nb<half_t, 64>(op, hs, prog, th, occ, st);
   } else {
-    if (op.N % 32 == 0) return launch_halo_km<float, 32>(op, km, th, occ, st);
+    if (op.N % 32 == 0) return launch_halo_nb<float, 32>(op, hs, prog, th, occ, st);
   }
   return kErrUnsupported;
 }
