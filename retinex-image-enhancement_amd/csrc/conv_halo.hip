@@ -456,6 +456,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 
     const int ch = tid % CHN;
     const int nb0 = ch * EPC;  // first channel (within the block slice) of this thread in the epilogue
+    const bool tile_full = oy0 + TH <= op.Ho && ox0 + TW <= op.Wo;  // uniform: no per-pixel validity checks
     uint4 rr[PASSES];
     int step = 0;
     // one phase: steps [step, pend) of kind K; the step after the phase is of kind KN
@@ -487,13 +488,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
         }
         if (step == nsteps - 1 && resp) {
           // residual chunks of this tile, requested before the last step's MFMAs
+          const char* rb = (const char*)(resp + (((size_t)b * op.Ho + oy0) * op.Wo + ox0) * res_cs + n0);
+          const unsigned rrow = (unsigned)(op.Wo * res_cs * (int)sizeof(T)), rcol = (unsigned)(res_cs * (int)sizeof(T));
 #pragma unroll
           for (int ps = 0; ps < PASSES; ++ps) {
-            const int p = tid / CHN + ps * PPP;
-            const int oy = oy0 + p / TW, ox = ox0 + p % TW;
-            const size_t m = ((size_t)b * op.Ho + oy) * op.Wo + ox;
-            rr[ps] = (oy < op.Ho && ox < op.Wo) ? *(const uint4*)(resp + m * res_cs + n0 + nb0)
-                                                : make_uint4(0, 0, 0, 0);
+            const unsigned p = (unsigned)tid / CHN + ps * PPP;
+            const unsigned off = (p / TW) * rrow + (p % TW) * rcol + (unsigned)nb0 * sizeof(T);
+            const bool ok = tile_full || (oy0 + (int)(p / TW) < op.Ho && ox0 + (int)(p % TW) < op.Wo);
+            rr[ps] = ok ? *(const uint4*)(rb + off) : make_uint4(0, 0, 0, 0);
           }
         }
         halo_taps<T, NB, TH, K>(acc, halo, Bs, wave, fr, fg);
@@ -540,11 +542,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 #pragma unroll
     for (int e = 0; e < EPC; ++e) psum[e] = 0.f;
     T* out = (T*)op.out;
+    // uniform tile base + 32-bit per-lane byte offsets (NHWC store)
+    char* ob = (char*)(out + (((size_t)b * op.Ho + oy0) * op.Wo + ox0) * op.out_cs + op.out_coff + n0);
+    const unsigned orow = (unsigned)(op.Wo * op.out_cs * (int)sizeof(T)), ocol = (unsigned)(op.out_cs * (int)sizeof(T));
 #pragma unroll
     for (int ps = 0; ps < PASSES; ++ps) {
       const int p = tid / CHN + ps * PPP;
       const int oy = oy0 + p / TW, ox = ox0 + p % TW;
-      const bool valid = oy < op.Ho && ox < op.Wo;
+      const bool valid = tile_full || (oy < op.Ho && ox < op.Wo);
       const size_t m = ((size_t)b * op.Ho + oy) * op.Wo + ox;
       float v[EPC];
       {
@@ -610,7 +615,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
         const size_t opix = ((size_t)b * 2 * op.Ho + 2 * oy + (q >> 1)) * (2 * op.Wo) + 2 * ox + (q & 1);
         *(uint4*)(out + opix * op.out_cs + op.out_coff + co) = o;
       } else {
-        *(uint4*)(out + m * op.out_cs + op.out_coff + n0 + nb0) = o;
+        *(uint4*)(ob + ((unsigned)(p / TW) * orow + (unsigned)(p % TW) * ocol + (unsigned)nb0 * sizeof(T))) = o;
       }
 #pragma unroll
       for (int e = 0; e < EPC; ++e) psum[e] += hto_f(ov[e]);
