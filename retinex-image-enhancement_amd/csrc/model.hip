@@ -248,6 +248,16 @@ enum BufId : int {
   B_COUNT
 };
 
+// [nout][3*3*3] (c, ky, kx) conv weights -> k-major [27][nout]: the direct 3->32
+// kernel reads channel pairs of one tap as adjacent scalars (packed FMAs)
+static std::vector<double> conv3_kmajor(const std::vector<double>& w) {
+  const size_t nout = w.size() / 27;
+  std::vector<double> t(w.size());
+  for (size_t o = 0; o < nout; ++o)
+    for (size_t k = 0; k < 27; ++k) t[k * nout + o] = w[o * 27 + k];
+  return t;
+}
+
 enum OpKind { OP_GEMM, OP_CONV3, OP_PREP, OP_FAM_CA, OP_FAM_MIX, OP_FAM_SA, OP_ASPP_G, OP_TAIL };
 
 struct Op {
@@ -626,7 +636,7 @@ static int build_model(UprModel* m, ParamSet& P) {
       b.insert(b.end(), bs->v.begin(), bs->v.end());
       o.out1 = B_S1IN;
     }
-    o.w = blob.add_f32(w); o.b = blob.add_f32(b);
+    o.w = blob.add_f32(conv3_kmajor(w)); o.b = blob.add_f32(b);
     m->ops.push_back(o);
   }
   (void)pre;
@@ -686,7 +696,7 @@ static int build_model(UprModel* m, ParamSet& P) {
       Op o;
       o.kind = OP_CONV3; o.name = p; o.in = k == 1 ? B_X2P : B_X3P; o.out = k == 1 ? B_S2IN : B_S3IN;
       o.lvl_shift = k == 1 ? 2 : 4;
-      o.w = blob.add_f32(w->v); o.b = blob.add_f32(b->v);
+      o.w = blob.add_f32(conv3_kmajor(w->v)); o.b = blob.add_f32(b->v);
       m->ops.push_back(o);
     }
     bd.fam("scale1.2", 0, B_S1IN, B_H1, B_Y1, B_MM1, B_P1, B_Q1, 0, Whead);

@@ -69,49 +69,71 @@ __global__ void prep_pyramid_kernel(const TI* __restrict__ x, TO* __restrict__ x
 
 // ---------------------------------------------------------------------------
 // conv3_direct: planar [B,3,h,w] input -> up to two NHWC [B,h,w,32] outputs,
-// each relu(conv3x3(x; w_k) + b_k).  Weights [nout*32][27] fp32 in (c,ky,kx)
-// order, read as wave-uniform scalars.
+// each relu(conv3x3(x; w_k) + b_k).  Weights k-major [27][nout*32] fp32, tap k
+// in (c,ky,kx) order, read as wave-uniform scalars; channel pairs accumulate with packed
+// FMAs.  A block owns 256 consecutive output pixels, whose NHWC rows form one
+// contiguous span: results go through LDS and leave as coalesced 16-byte
+// chunks (a per-thread 32-channel row store would scatter 16-byte pieces at a
+// 64/128-byte lane stride).
 // ---------------------------------------------------------------------------
+typedef float f2v __attribute__((ext_vector_type(2)));
+
 template <typename TI, typename TO, int NOUT>
 __global__ __launch_bounds__(256) void conv3_direct_kernel(const TI* __restrict__ x, const float* __restrict__ w,
                                                            const float* __restrict__ bias, TO* __restrict__ out0,
                                                            TO* __restrict__ out1, int B, int h, int wd) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  constexpr int CPP = 32 * (int)sizeof(TO) / 16;  // 16-byte chunks per output pixel
+  constexpr int RS = 9;                           // LDS row stride in 16-byte slots (conflict-free writes)
+  __shared__ uint4 stage[256 * RS];
   const int total = B * h * wd;
-  if (idx >= total) return;
-  const int ox = idx % wd, oy = (idx / wd) % h, b = idx / (wd * h);
+  const int base = blockIdx.x * 256;
+  const int idx = base + threadIdx.x;
+  const int npx = total - base < 256 ? total - base : 256;
   float in[27];
+  if (idx < total) {
+    const int ox = idx % wd, oy = (idx / wd) % h, b = idx / (wd * h);
 #pragma unroll
-  for (int c = 0; c < 3; ++c)
+    for (int c = 0; c < 3; ++c)
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
+      for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const int iy = oy + ky - 1, ix = ox + kx - 1;
-        in[c * 9 + ky * 3 + kx] = (iy >= 0 && iy < h && ix >= 0 && ix < wd)
-                                      ? ldf(x, (((size_t)b * 3 + c) * h + iy) * wd + ix) : 0.f;
-      }
+        for (int kx = 0; kx < 3; ++kx) {
+          const int iy = oy + ky - 1, ix = ox + kx - 1;
+          in[c * 9 + ky * 3 + kx] = (iy >= 0 && iy < h && ix >= 0 && ix < wd)
+                                        ? ldf(x, (((size_t)b * 3 + c) * h + iy) * wd + ix) : 0.f;
+        }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 27; ++k) in[k] = 0.f;
+  }
 #pragma unroll
   for (int o = 0; o < NOUT; ++o) {
-    TO* out = o == 0 ? out0 : out1;
-    TO* dst = out + (size_t)idx * 32;
+    float r[32];
 #pragma unroll
-    for (int g = 0; g < 32; g += 4) {
-      float r[4];
+    for (int g = 0; g < 32; g += 2) {
+      const int oc = o * 32 + g;
+      f2v acc2 = {bias[oc], bias[oc + 1]};
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int oc = o * 32 + g + j;
-        float s = bias[oc];
-#pragma unroll
-        for (int k = 0; k < 27; ++k) s += in[k] * w[oc * 27 + k];
-        r[j] = fmaxf(s, 0.f);
+      for (int k = 0; k < 27; ++k) {
+        const f2v w2 = *(const f2v*)(w + k * (NOUT * 32) + oc);  // k-major weights
+        acc2 = __builtin_elementwise_fma((f2v){in[k], in[k]}, w2, acc2);
       }
-      if constexpr (sizeof(TO) == 4) {
-        *(float4*)(dst + g) = make_float4(r[0], r[1], r[2], r[3]);
-      } else {
-        dst[g] = (TO)r[0]; dst[g + 1] = (TO)r[1]; dst[g + 2] = (TO)r[2]; dst[g + 3] = (TO)r[3];
-      }
+      r[g] = fmaxf(acc2[0], 0.f);
+      r[g + 1] = fmaxf(acc2[1], 0.f);
     }
+    uint4* row = stage + threadIdx.x * RS;
+#pragma unroll
+    for (int c = 0; c < CPP; ++c) {
+      uint4 v;
+      TO* vv = (TO*)&v;
+#pragma unroll
+      for (int e = 0; e < 16 / (int)sizeof(TO); ++e) vv[e] = (TO)r[c * (16 / (int)sizeof(TO)) + e];
+      row[c] = v;
+    }
+    __syncthreads();
+    uint4* dst = (uint4*)((o == 0 ? out0 : out1) + (size_t)base * 32);
+    for (int q = threadIdx.x; q < npx * CPP; q += 256) dst[q] = stage[(q / CPP) * RS + q % CPP];
+    __syncthreads();
   }
 }
 
@@ -144,23 +166,29 @@ template <typename T>
 __global__ __launch_bounds__(256) void fam_mix_kernel(const T* __restrict__ y, const float* __restrict__ ca,
                                                       const float* __restrict__ P, float* __restrict__ mm,
                                                       float* __restrict__ p, int B, int HW) {
+  constexpr int EPC = 16 / (int)sizeof(T);  // channels per 16-byte load
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= B * HW) return;
   const int b = idx / HW;
-  const T* yp = y + (size_t)idx * 32;
+  const uint4* yp = (const uint4*)(y + (size_t)idx * 32);
   const float* cab = ca + b * 32;
   float s = 0.f, mx = -INFINITY, p0 = 0.f, p1 = 0.f, p2 = 0.f;
 #pragma unroll
-  for (int c = 0; c < 32; ++c) {
-    const float o = ldf(yp, c) * cab[c];
-    s += o;
-    mx = fmaxf(mx, o);
-    p0 += P[c] * o;
-    p1 += P[32 + c] * o;
-    p2 += P[64 + c] * o;
+  for (int k = 0; k < 32 / EPC; ++k) {
+    const uint4 v4 = yp[k];
+    const T* v = (const T*)&v4;
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) {
+      const int c = k * EPC + e;
+      const float o = (float)v[e] * cab[c];
+      s += o;
+      mx = fmaxf(mx, o);
+      p0 += P[c] * o;
+      p1 += P[32 + c] * o;
+      p2 += P[64 + c] * o;
+    }
   }
-  mm[(size_t)idx * 2] = s / 32.f;
-  mm[(size_t)idx * 2 + 1] = mx;
+  *(float2*)(mm + (size_t)idx * 2) = make_float2(s / 32.f, mx);
   p[(size_t)idx * 3] = p0;
   p[(size_t)idx * 3 + 1] = p1;
   p[(size_t)idx * 3 + 2] = p2;
@@ -170,27 +198,37 @@ __global__ __launch_bounds__(256) void fam_mix_kernel(const T* __restrict__ y, c
 // fam_sa: sa = sigmoid(conv7x7([mean,max]) + b), q = sa * p   (zero padding 3)
 // weights w[2][7][7] (channel 0 = mean, 1 = max)
 // ---------------------------------------------------------------------------
+constexpr int SA_TW = 32, SA_TH = 8;
 __global__ __launch_bounds__(256) void fam_sa_kernel(const float* __restrict__ mm, const float* __restrict__ p,
                                                      const float* __restrict__ w, float bias,
                                                      float* __restrict__ q, int B, int h, int wd) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= B * h * wd) return;
-  const int ox = idx % wd, oy = (idx / wd) % h, b = idx / (wd * h);
-  float s = bias;
-  for (int ky = 0; ky < 7; ++ky) {
-    const int iy = oy + ky - 3;
-    if (iy < 0 || iy >= h) continue;
-    for (int kx = 0; kx < 7; ++kx) {
-      const int ix = ox + kx - 3;
-      if (ix < 0 || ix >= wd) continue;
-      const size_t pi = ((size_t)b * h + iy) * wd + ix;
-      s += w[ky * 7 + kx] * mm[pi * 2] + w[49 + ky * 7 + kx] * mm[pi * 2 + 1];
-    }
+  // one block = a 32 x 8 output tile; the [mean,max] map of the tile + 3-pixel
+  // halo is staged in LDS (zero outside the image = the conv's zero padding)
+  constexpr int RW = SA_TW + 6, RH = SA_TH + 6;
+  __shared__ float2 reg[RH * RW];
+  const int b = blockIdx.z, oy0 = blockIdx.y * SA_TH, ox0 = blockIdx.x * SA_TW;
+  const float2* mmb = (const float2*)mm + (size_t)b * h * wd;
+  for (int i = threadIdx.x; i < RH * RW; i += 256) {
+    const int iy = oy0 - 3 + i / RW, ix = ox0 - 3 + i % RW;
+    reg[i] = (iy >= 0 && iy < h && ix >= 0 && ix < wd) ? mmb[(size_t)iy * wd + ix] : make_float2(0.f, 0.f);
   }
+  __syncthreads();
+  const int ty = threadIdx.x / SA_TW, tx = threadIdx.x % SA_TW;
+  const int oy = oy0 + ty, ox = ox0 + tx;
+  if (oy >= h || ox >= wd) return;
+  float s = bias;
+#pragma unroll
+  for (int ky = 0; ky < 7; ++ky)
+#pragma unroll
+    for (int kx = 0; kx < 7; ++kx) {
+      const float2 v = reg[(ty + ky) * RW + tx + kx];
+      s += w[ky * 7 + kx] * v.x + w[49 + ky * 7 + kx] * v.y;
+    }
   const float sa = sigmoidf_(s);
-  q[(size_t)idx * 3] = sa * p[(size_t)idx * 3];
-  q[(size_t)idx * 3 + 1] = sa * p[(size_t)idx * 3 + 1];
-  q[(size_t)idx * 3 + 2] = sa * p[(size_t)idx * 3 + 2];
+  const size_t idx = ((size_t)b * h + oy) * wd + ox;
+  q[idx * 3] = sa * p[idx * 3];
+  q[idx * 3 + 1] = sa * p[idx * 3 + 1];
+  q[idx * 3 + 2] = sa * p[idx * 3 + 2];
 }
 
 // bilinear source coordinate, align_corners=False, size-based (in/out ratio)
@@ -295,8 +333,8 @@ int launch_fam_mix(const void* y, const float* ca, const float* P, float* mm, fl
                    hipStream_t st) {
   const int n = B * HW;
   if (dtype == kF16)
-    hipLaunchKernelGGL((fam_mix_kernel<half_t>), dim3(grid1d(n)), dim3(256), 0, st, (const half_t*)y, ca, P, mm, p, B,
-                       HW);
+    hipLaunchKernelGGL((fam_mix_kernel<half_t>), dim3(grid1d(n)), dim3(256), 0, st, (const half_t*)y, ca, P, mm, p,
+                       B, HW);
   else
     hipLaunchKernelGGL((fam_mix_kernel<float>), dim3(grid1d(n)), dim3(256), 0, st, (const float*)y, ca, P, mm, p, B,
                        HW);
@@ -305,8 +343,9 @@ int launch_fam_mix(const void* y, const float* ca, const float* P, float* mm, fl
 
 int launch_fam_sa(const float* mm, const float* p, const float* w, float bias, float* q, int B, int h, int wd,
                   hipStream_t st) {
-  const int n = B * h * wd;
-  hipLaunchKernelGGL(fam_sa_kernel, dim3(grid1d(n)), dim3(256), 0, st, mm, p, w, bias, q, B, h, wd);
+  if (B <= 0 || h <= 0 || wd <= 0) return kErrShape;
+  hipLaunchKernelGGL(fam_sa_kernel, dim3(cdiv(wd, SA_TW), cdiv(h, SA_TH), B), dim3(256), 0, st, mm, p, w, bias, q, B,
+                     h, wd);
   return (int)hipGetLastError();
 }
 
