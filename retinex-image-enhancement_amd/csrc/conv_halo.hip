@@ -458,6 +458,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     const int nb0 = ch * EPC;  // first channel (within the block slice) of this thread in the epilogue
     const bool tile_full = oy0 + TH <= op.Ho && ox0 + TW <= op.Wo;  // uniform: no per-pixel validity checks
     uint4 rr[PASSES];
+    float xs[sizeof(T) == 4 ? PASSES : 1][3];  // fp32 residual head: network-input pixels of this tile, prefetched
     int step = 0;
     // one phase: steps [step, pend) of kind K; the step after the phase is of kind KN
     auto phase = [&](auto kc, auto knc, int pend) {
@@ -496,6 +497,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
             const unsigned off = (p / TW) * rrow + (p % TW) * rcol + (unsigned)nb0 * sizeof(T);
             const bool ok = tile_full || (oy0 + (int)(p / TW) < op.Ho && ox0 + (int)(p % TW) < op.Wo);
             rr[ps] = ok ? *(const uint4*)(rb + off) : make_uint4(0, 0, 0, 0);
+          }
+        }
+        // fp32 (2 blocks/CU) exposes the epilogue's x-read latency; fp16's head runs
+        // 3 blocks/CU, where the early loads only cost (measured)
+        if constexpr (sizeof(T) == 4) if (step == nsteps - 1 && op.store == kStoreHeadIllu) {
+#pragma unroll
+          for (int ps = 0; ps < PASSES; ++ps) {
+            const int p = tid / CHN + ps * PPP;
+            const int oy = oy0 + p / TW, ox = ox0 + p % TW;
+            const bool ok = tile_full || (oy < op.Ho && ox < op.Wo);
+            const size_t pp = (size_t)b * 3 * HWo + (size_t)oy * op.Wo + ox;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+              float xv = 0.f;
+              if (ok) xv = op.x_f16 ? (float)((const half_t*)op.x_nchw)[pp + (size_t)c * HWo] : op.x_nchw[pp + (size_t)c * HWo];
+              xs[ps][c] = xv;
+            }
           }
         }
         halo_taps<T, NB, TH, K>(acc, halo, Bs, wave, fr, fg);
@@ -541,6 +559,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     float psum[EPC];
 #pragma unroll
     for (int e = 0; e < EPC; ++e) psum[e] = 0.f;
+    // residual-head 1x1 weights in registers: read once, not per pass (the illu
+    // stores may alias them as far as the compiler knows)
+    float hw_v[EPC];
+    if (op.store == kStoreHeadIllu) {
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) hw_v[e] = op.head_w[nb0 + e];
+    }
     T* out = (T*)op.out;
     // uniform tile base + 32-bit per-lane byte offsets (NHWC store)
     char* ob = (char*)(out + (((size_t)b * op.Ho + oy0) * op.Wo + ox0) * op.out_cs + op.out_coff + n0);
@@ -565,18 +590,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
         // residual head (models/model.py:324-328, :351-358); NB == N == 32
         float part = 0.f;
 #pragma unroll
-        for (int e = 0; e < EPC; ++e) part += fmaxf(v[e], 0.f) * op.head_w[nb0 + e];
+        for (int e = 0; e < EPC; ++e) part += fmaxf(v[e], 0.f) * hw_v[e];
 #pragma unroll
         for (int s = 1; s < CHN; s <<= 1) part += __shfl_xor(part, s);
         if (ch == 0 && valid) {
           float x0, x1, x2;
-          const size_t pp = (size_t)oy * op.Wo + ox;
-          if (op.x_f16) {
-            const half_t* x = (const half_t*)op.x_nchw + (size_t)b * 3 * HWo + pp;
-            x0 = (float)x[0]; x1 = (float)x[HWo]; x2 = (float)x[2 * HWo];
+          if constexpr (sizeof(T) == 4) {
+            x0 = xs[ps][0]; x1 = xs[ps][1]; x2 = xs[ps][2];
           } else {
-            const float* x = op.x_nchw + (size_t)b * 3 * HWo + pp;
-            x0 = x[0]; x1 = x[HWo]; x2 = x[2 * HWo];
+            const size_t pp = (size_t)oy * op.Wo + ox;
+            if (op.x_f16) {
+              const half_t* x = (const half_t*)op.x_nchw + (size_t)b * 3 * HWo + pp;
+              x0 = (float)x[0]; x1 = (float)x[HWo]; x2 = (float)x[2 * HWo];
+            } else {
+              const float* x = op.x_nchw + (size_t)b * 3 * HWo + pp;
+              x0 = x[0]; x1 = x[HWo]; x2 = x[2 * HWo];
+            }
           }
           const float z = (x0 + x1 + x2) / 3.f + (part + op.head_b);
           const float il = 1.f / (1.f + expf(-z));
