@@ -12,9 +12,9 @@
 // K step.  A (pixels x channels) and B (weights, [N][K]) are staged through LDS
 // with a register prefetch of the next K step (issue-early / write-late).
 //
-// MFMA: each lane's fragment is 8 consecutive k of one row at k-offset
-// 8*(lane>>4).  fp32 consumes it as 8 x v_mfma_f32_16x16x4_f32 (exact fp32),
-// fp16 as 1 x v_mfma_f32_16x16x32_f16 (fp32 accumulate).  The permutation of k
+// MFMA: each lane's fragment is 8 k of one row: fp16 [8g, 8g+8) as 1 x
+// v_mfma_f32_16x16x32_f16 (fp32 accumulate), fp32 [4g, 4g+4) u [16+4g, 16+4g+4)
+// as 8 x v_mfma_f32_16x16x4_f32 (exact fp32), g = lane>>4.  The permutation of k
 // across MFMA k-slots is the same for A and B, so the sum is unchanged.
 #include <cstdlib>
 #include <cstring>
@@ -59,7 +59,10 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvOp op) {
   constexpr int BN = WAVES_N * WN * 16;
   constexpr int A_IT = BM / ROWS_PASS;
   constexpr int B_IT = (BN * CH + 255) / 256;
-  constexpr int LDS_ROW = BK + EPC;         // +16 B pad per row
+  // LDS row stride: fp32 10 x 16 B with the k-permutation {g, g+4} below, fp16
+  // 6 x 16 B: the fragment reads (16 rows x 4 chunks per ds_read_b128) are then
+  // bank-conflict free (same analysis as conv_halo.hip)
+  constexpr int LDS_ROW = sizeof(T) == 4 ? 40 : 48;
   static_assert(A_IT >= 1, "tile too small");
 
   __shared__ __attribute__((aligned(16))) T As[BM * LDS_ROW];
@@ -186,7 +189,9 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvOp op) {
   if (total_steps > 0) { load_step(cur_seg, cur_tap, cur_c0); advance(); }
 
   const int fr = lane & 15;
-  const int fk = (lane >> 4) * 8;
+  const int fg = lane >> 4;
+  // fp16: lane reads k [8g, 8g+8); fp32: k [4g, 4g+4) u [16+4g, 16+4g+4)
+  const int fk = sizeof(T) == 4 ? fg * 4 : fg * 8;
 
   for (int step = 0; step < total_steps; ++step) {
     __syncthreads();
@@ -207,13 +212,13 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvOp op) {
       for (int a = 0; a < WM; ++a) {
         const float* p = (const float*)As + (wm * WM * 16 + a * 16 + fr) * LDS_ROW + fk;
         af[a][0] = *(const f32x4*)p;
-        af[a][1] = *(const f32x4*)(p + 4);
+        af[a][1] = *(const f32x4*)(p + 16);
       }
 #pragma unroll
       for (int b = 0; b < WN; ++b) {
         const float* p = (const float*)Bs + (wn * WN * 16 + b * 16 + fr) * LDS_ROW + fk;
         bf[b][0] = *(const f32x4*)p;
-        bf[b][1] = *(const f32x4*)(p + 4);
+        bf[b][1] = *(const f32x4*)(p + 16);
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j)

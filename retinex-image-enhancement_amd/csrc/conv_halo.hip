@@ -90,8 +90,11 @@ constexpr int prog_kind(int p, int i) { return ((p >> (3 * i)) & 7) - 1; }
 struct HaloSteps {
   int n;
   int phase_end[3];
+  int wtaps;  // taps over all steps (weights of the whole program = wtaps x NB rows)
+  int res;    // 1: the whole program's weights stay resident in LDS (set per launch)
   unsigned char si[HALO_MAXSTEPS];
   unsigned char cq[HALO_MAXSTEPS];
+  unsigned short wtap0[HALO_MAXSTEPS];  // first tap of each step in the resident weight image
 };
 
 // The whole kernel argument.  The kernel reads it through the kernarg segment
@@ -134,6 +137,14 @@ struct ProgCfg {
   static constexpr int MAXTAPS = cmax3(kind_taps(K0), kind_taps(K1), kind_taps(K2));
   static constexpr int PW = (MAXTAPS * NB * HaloCfg<T, NB, TH>::CCH + 255) / 256;  // weight chunks per thread
 };
+
+// Weight rows in LDS are unpadded (32 channels) with the 16-byte chunk index
+// XOR-swizzled by the row: fp16 c ^ ((row >> 1) & 3), fp32 c ^ (row & 7).  B
+// fragment reads start at rows that are multiples of 16, so the swizzle is a
+// per-lane constant (of fr); reads and the staging writes are bank-conflict
+// free (checked against the ds_read_b128 / ds_write_b128 lane groups).
+template <typename T>
+__device__ __forceinline__ int bswz(int row) { return sizeof(T) == 2 ? ((row >> 1) & 3) : (row & 7); }
 
 // Region of one step -> registers.  Every kind writes EVERY pf[] entry at a
 // constant index: when code paths write different subsets, the compiler merges
@@ -244,7 +255,7 @@ __device__ __forceinline__ void wts_store(const uint4 (&pw)[PWN], int tid, T* Bs
     const unsigned q = (unsigned)tid + j * 256u;
     if (j * 256 < NBQ && ((j + 1) * 256 <= NBQ || q < (unsigned)NBQ)) {
       const unsigned row = q / C::CCH, ch = q % C::CCH;
-      *(uint4*)(Bs + row * C::PSTR + ch * C::EPC) = pw[j];
+      *(uint4*)(Bs + row * 32 + (ch ^ (unsigned)bswz<T>((int)row)) * C::EPC) = pw[j];
     }
   }
 }
@@ -256,6 +267,10 @@ template <int PSTR>
 struct Frag<half_t, PSTR> {
   f16x8_h v;
   __device__ __forceinline__ void ld(const half_t* s, int pix, int fg) { v = *(const f16x8_h*)(s + pix * PSTR + fg * 8); }
+  // weight row (row = 16-aligned base + fr) of the swizzled B image
+  __device__ __forceinline__ void ldb(const half_t* s, int row, int fr, int fg) {
+    v = *(const f16x8_h*)(s + row * 32 + ((fg ^ bswz<half_t>(fr)) * 8));
+  }
   __device__ __forceinline__ void max_with(const Frag& o) { v = __builtin_elementwise_max(v, o.v); }
 };
 template <int PSTR>
@@ -265,6 +280,10 @@ struct Frag<float, PSTR> {
     const float* p = s + pix * PSTR + fg * 4;
     v[0] = *(const f32x4_h*)p;
     v[1] = *(const f32x4_h*)(p + 16);
+  }
+  __device__ __forceinline__ void ldb(const float* s, int row, int fr, int fg) {
+    v[0] = *(const f32x4_h*)(s + row * 32 + ((fg ^ bswz<float>(fr)) * 4));
+    v[1] = *(const f32x4_h*)(s + row * 32 + (((fg + 4) ^ bswz<float>(fr)) * 4));
   }
   __device__ __forceinline__ void max_with(const Frag& o) {
     v[0] = __builtin_elementwise_max(v[0], o.v[0]);
@@ -315,12 +334,12 @@ __device__ __forceinline__ void halo_taps(f32x4_h (&acc)[TH / 2][NB / 16], const
   if constexpr (KIND == kKPair) {
     F bf[NT], af[MT];
 #pragma unroll
-    for (int j = 0; j < NT; ++j) bf[j].ld(Bs, j * 16 + fr, fg);
+    for (int j = 0; j < NT; ++j) bf[j].ldb(Bs, j * 16 + fr, fr, fg);
 #pragma unroll
     for (int i = 0; i < MT; ++i) af[i].ld(halo, pix(i, 1, 1), fg);
     frag_mma<MT, NT, PSTR>(acc, af, bf);
 #pragma unroll
-    for (int j = 0; j < NT; ++j) bf[j].ld(Bs, NB + j * 16 + fr, fg);
+    for (int j = 0; j < NT; ++j) bf[j].ldb(Bs, NB + j * 16 + fr, fr, fg);
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
 #pragma unroll
@@ -340,7 +359,7 @@ __device__ __forceinline__ void halo_taps(f32x4_h (&acc)[TH / 2][NB / 16], const
     auto rd = [&](int tap, F (&a)[MT], F (&b)[NT]) {
       const int r = tap / K, c = tap % K;
 #pragma unroll
-      for (int j = 0; j < NT; ++j) b[j].ld(Bs, tap * NB + j * 16 + fr, fg);
+      for (int j = 0; j < NT; ++j) b[j].ldb(Bs, tap * NB + j * 16 + fr, fr, fg);
 #pragma unroll
       for (int i = 0; i < MT; ++i) a[i].ld(halo, pix(i, r * D, c * D), fg);
     };
@@ -406,10 +425,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
   const int res_cs = op.res1 ? op.res1_cs : op.res2_cs;
   const bool res_pre = op.res1 != nullptr;
   const int nsteps = hs.n;
-  // weights identical for every tile of the block: one step, and the block's N
-  // slice never changes (tile t has nb = t % nblk_n and the block strides by the
-  // grid size, a multiple of nblk_n — launch_halo_cfg guarantees it)
-  const bool b_keep = nsteps == 1 && gridDim.x % nblk_n == 0;
+  // weights resident for the whole kernel: the host found LDS room for every
+  // step's weights (hs.res), and the block's N slice never changes (tile t has
+  // nb = t % nblk_n and the block strides by the grid size, a multiple of
+  // nblk_n — launch_halo_cfg guarantees it)
+  const bool b_keep = hs.res && gridDim.x % nblk_n == 0;
 
   auto tile_coords = [&](int tile, int& b, int& oy0, int& ox0, int& n0) {
     int t = tile;
@@ -436,11 +456,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     if (A.sched & 2)
       for (int i = 0; i < (A.sched >> 8); ++i) __builtin_amdgcn_s_sleep(127);
   }
-  if (b_keep) {  // one step, one N block: weights staged once per block
+  if (b_keep) {  // every step's weights, staged once per block
     int b, oy0, ox0, n0;
     tile_coords(tile, b, oy0, ox0, n0);
-    wts_load<T, NB, TH, P::K0>(pw, op, hs.si[0], hs.cq[0] * 32, n0, tid);
-    wts_store<T, NB, TH, P::K0>(pw, tid, Bs);
+    auto stage_phase = [&](auto kc, int s0, int s1) {
+      constexpr int K = decltype(kc)::value;
+      for (int st = s0; st < s1; ++st) {
+        wts_load<T, NB, TH, K>(pw, op, hs.si[st], hs.cq[st] * 32, n0, tid);
+        wts_store<T, NB, TH, K>(pw, tid, Bs + hs.wtap0[st] * NB * 32);
+      }
+    };
+    stage_phase(IC<P::K0>{}, 0, hs.phase_end[0]);
+    if constexpr (P::NPH > 1) stage_phase(IC<P::K1>{}, hs.phase_end[0], hs.phase_end[1]);
+    if constexpr (P::NPH > 2) stage_phase(IC<P::K2>{}, hs.phase_end[1], hs.phase_end[2]);
   }
   load(IC<P::K0>{}, 0, tile);
 
@@ -463,7 +491,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     // one phase: steps [step, pend) of kind K; the step after the phase is of kind KN
     auto phase = [&](auto kc, auto knc, int pend) {
       constexpr int K = decltype(kc)::value;
-      for (; step < pend; ++step) {
+      // resident weight image of this phase's steps: consecutive, taps(K)*NB rows apart
+      const T* bstep = Bs + (b_keep && step < pend ? hs.wtap0[step] * NB * 32 : 0);
+      for (; step < pend; ++step, bstep += b_keep ? kind_taps(K) * NB * 32 : 0) {
         const int si = hs.si[step], c0 = hs.cq[step] * 32;
         const ConvSeg& sg = op.seg[si];
         __syncthreads();  // LDS free (previous step's MFMAs / previous tile's epilogue)
@@ -516,7 +546,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
             }
           }
         }
-        halo_taps<T, NB, TH, K>(acc, halo, Bs, wave, fr, fg);
+        halo_taps<T, NB, TH, K>(acc, halo, bstep, wave, fr, fg);
       }
     };
     phase(IC<P::K0>{}, IC<P::K1>{}, hs.phase_end[0]);
@@ -673,32 +703,41 @@ static int launch_halo_cfg(const ConvOp& op, const HaloSteps& hs, hipStream_t st
   const int ntiles = op.B * tiles_x * tiles_y * (op.N / NB);
   using C = HaloCfg<T, NB, TH>;
   using P = ProgCfg<T, NB, TH, PROG>;
-  // LDS: region for the largest halo extent, weights for the largest tap count of the program
+  // LDS: region (largest over the program's kinds; the epilogue staging reuses
+  // it) + weights: one step's (largest tap count) staged per step, or every
+  // step's resident for the whole kernel when that costs no co-resident block
   constexpr int region = ((P::REGION > C::EPI_BYTES ? P::REGION : C::EPI_BYTES) + 15) / 16 * 16;
-  constexpr int lds = region + P::MAXTAPS * NB * C::PSTR * (int)sizeof(T);
-  static_assert(lds <= 160 * 1024, "halo LDS budget");
+  constexpr int row_bytes = 32 * (int)sizeof(T);  // unpadded, swizzled weight rows
+  constexpr int lds_step = region + P::MAXTAPS * NB * row_bytes;
+  static_assert(lds_step <= 160 * 1024, "halo LDS budget");
+  const int lds_res = region + hs.wtaps * NB * row_bytes;
   static bool attr_set = false;
+  static int reg_cap = 0;  // co-resident blocks per CU allowed by registers
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)conv_halo_kernel<T, NB, TH, OCC, PROG>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&reg_cap, (const void*)conv_halo_kernel<T, NB, TH, OCC, PROG>,
+                                                     256, 0) != hipSuccess || reg_cap < 1)
+      reg_cap = 1;
     attr_set = true;
   }
+  auto blocks = [&](int l) { const int c = (160 * 1024) / l; return c < reg_cap ? c : reg_cap; };
+  const bool res = lds_res <= 160 * 1024 && blocks(lds_res) >= blocks(lds_step);
+  const int lds = res ? lds_res : lds_step;
   // Persistent grid = blocks that are actually co-resident (registers AND LDS);
   // an oversized grid leaves a second, partial wave of blocks (tail).  Speed only.
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)conv_halo_kernel<T, NB, TH, OCC, PROG>, 256,
-                                                   lds) != hipSuccess || per_cu < 1)
-    per_cu = 1;
-  const int lds_cap = (160 * 1024) / lds;
-  if (per_cu > lds_cap) per_cu = lds_cap < 1 ? 1 : lds_cap;
+  int per_cu = blocks(lds);
+  if (per_cu < 1) per_cu = 1;
   int grid = 256 * per_cu;
   if (grid > ntiles) grid = ntiles;
   grid -= grid % (op.N / NB);  // a whole number of N slices per grid stride (resident weights)
   if (getenv("UPR_HALO_DEBUG"))
-    fprintf(stderr, "[halo]   lds %d B, %d blocks/CU (occupancy API), grid %d, tiles %d\n", lds, per_cu, grid, ntiles);
+    fprintf(stderr, "[halo]   lds %d B (%s weights), %d blocks/CU, grid %d, tiles %d\n", lds,
+            res ? "resident" : "per-step", per_cu, grid, ntiles);
   HaloArgs args;
   args.op = op;
   args.hs = hs;
+  args.hs.res = res ? 1 : 0;
   args.tiles_x = tiles_x;
   args.tiles_y = tiles_y;
   args.ntiles = ntiles;
@@ -784,14 +823,15 @@ static int seg_kind(const ConvOp& op, int s, int Ho, int Wo, bool& pair) {
 // Tile rows / occupancy per program, from per-layer sweeps of the whole forward
 // on MI355X (tools/layer_sweep.sh + tools/layer_table.py, bs 32, 512^2):
 //   fp32: 4-row tiles at 2 blocks/CU; 8-row tiles for the 1x1 (ConvT) and the
-//         FAM fusion program (1 block/CU: it restages weights every step)
-//   fp16: 8-row tiles; 2 blocks/CU for one-step ops, the FAM fusion and 1x1,
-//         1 block/CU for multi-step ops; the residual head 4-row at 3 blocks/CU
+//         FAM fusion program (1 block/CU, all 20 taps of weights resident)
+//   fp16: 4-row tiles at 2 blocks/CU for N >= 64 (64-wide N blocks) and the FAM
+//         fusion (weights resident); 8-row tiles at 2 blocks/CU for N = 32 and
+//         1x1; the residual head 4-row at 3 blocks/CU
 // UPR_HALO="<th>,<occ>" overrides (experiments).
-static void halo_choice(int dtype, int prog, int store, int nsteps, int& th, int& occ) {
+static void halo_choice(int dtype, int prog, int store, int N, int& th, int& occ) {
   if (dtype == kF16) {
-    th = 8;
-    occ = nsteps > 1 && prog != kProgFam && prog != kProg1x1 ? 1 : 2;
+    th = N >= 64 || prog == kProgFam ? 4 : 8;
+    occ = 2;
     if (store == kStoreHeadIllu) { th = 4; occ = 3; }
   } else {
     th = 4;
@@ -822,6 +862,8 @@ int launch_conv_halo(const ConvOp& op, int dtype, hipStream_t st) {
   // step table + program
   HaloSteps hs;
   hs.n = 0;
+  hs.wtaps = 0;
+  hs.res = 0;
   int kinds[3], nph = 0;
   for (int s = 0; s < op.nseg; ++s) {
     bool pair = false;
@@ -836,6 +878,8 @@ int launch_conv_halo(const ConvOp& op, int dtype, hipStream_t st) {
       if (hs.n == HALO_MAXSTEPS) return kErrUnsupported;
       hs.si[hs.n] = (unsigned char)s;
       hs.cq[hs.n] = (unsigned char)cq;
+      hs.wtap0[hs.n] = (unsigned short)hs.wtaps;
+      hs.wtaps += kind_taps(k);
       ++hs.n;
     }
     if (pair) ++s;
@@ -847,7 +891,7 @@ int launch_conv_halo(const ConvOp& op, int dtype, hipStream_t st) {
   for (int p = nph; p < 3; ++p) hs.phase_end[p] = hs.n;
   const int prog = nph == 1 ? prog1(kinds[0]) : (nph == 2 ? prog2(kinds[0], kinds[1]) : prog3(kinds[0], kinds[1], kinds[2]));
   int th, occ;
-  halo_choice(dtype, prog, op.store, hs.n, th, occ);
+  halo_choice(dtype, prog, op.store, op.N, th, occ);
   if (getenv("UPR_HALO_DEBUG"))
     fprintf(stderr, "[halo] prog %d (%d phases, %d steps) N=%d %dx%d th=%d occ=%d\n", prog, nph, hs.n, op.N, op.Ho,
             op.Wo, th, occ);
