@@ -11,12 +11,28 @@ import torch
 import torch.nn.functional as F
 
 BN_EPS = 1e-5  # nn.BatchNorm2d default
+BN_MOMENTUM = 0.1
+
+# Training mode (oracle/train.py switches it): BatchNorm uses batch statistics
+# and updates the running buffers in place, Dropout draws its mask from
+# MODE["dropout_mask"] (a callable shape -> {0,1} mask, so the checker can
+# replay the product's mask) — nn.BatchNorm2d / nn.Dropout train semantics.
+MODE = {"train": False, "dropout_mask": None}
 
 
 def _bn(sd, p, x):
     # nn.BatchNorm2d eval: (x - rm) / sqrt(rv + eps) * w + b
+    # train: batch mean / biased var normalise; running stats updated with the
+    # unbiased var, momentum 0.1
     return F.batch_norm(x, sd[p + ".running_mean"], sd[p + ".running_var"],
-                        sd[p + ".weight"], sd[p + ".bias"], False, 0.0, BN_EPS)
+                        sd[p + ".weight"], sd[p + ".bias"], MODE["train"], BN_MOMENTUM, BN_EPS)
+
+
+def _dropout(x, p=0.1):
+    if not MODE["train"] or p == 0.0:
+        return x
+    mask = MODE["dropout_mask"](x.shape)
+    return x * mask / (1.0 - p)
 
 
 def _conv(sd, p, x, stride=1, padding=0, dilation=1):
@@ -76,7 +92,7 @@ def aspp(sd, p, x, dilations=(1, 6, 12, 18)):
     g = F.relu(_bn(sd, p + ".global_pool.2", _conv(sd, p + ".global_pool.1", g)))
     feats.append(F.interpolate(g, size=x.shape[2:], mode="bilinear", align_corners=False))
     o = _conv(sd, p + ".fusion.0", torch.cat(feats, 1))
-    return F.relu(_bn(sd, p + ".fusion.1", o))
+    return _dropout(F.relu(_bn(sd, p + ".fusion.1", o)), 0.1)
 
 
 def upblock(sd, p, x):
