@@ -1,0 +1,217 @@
+/*
+ * upr_train.h — C ABI of the UP-Retinex TRAINING kernels in libupr.so (gfx950).
+ *
+ * The reference trains with PyTorch autograd (trainers/train.py:63-103:
+ * forward -> losses/loss.py TotalLoss -> loss.backward() -> clip_grad_norm_ ->
+ * Adam.step()).  It has no native code, so every entry below replaces a piece
+ * of that Python/PyTorch path; each names the reference code it stands for.
+ * The host side (retinex-image-enhancement_amd/upr/train.py) strings these
+ * kernels into an explicit forward + backward of MultiScaleUP_Retinex and of
+ * TotalLoss — there is no autograd tape inside.
+ *
+ * Conventions (as upr.h): caller-allocated device buffers, fp32 unless stated,
+ * `stream` = hipStream_t as void*, stream-ordered, no internal synchronisation;
+ * return 0, a hipError_t (> 0) or a negative UPR_ERR_* code.
+ *
+ * Activations are described by UprView: element strides of the four logical
+ * axes (batch, row, column, channel), so one kernel reads NCHW network
+ * inputs, NHWC activations and channel slices of concat buffers alike.
+ * "Accumulate" arguments add into the destination instead of overwriting —
+ * the gradient of a tensor consumed by several ops is summed in place.
+ */
+#ifndef UPR_TRAIN_H_
+#define UPR_TRAIN_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+  void* data;
+  int64_t sb, sh, sw, sc;
+} UprView;
+
+/* hipMemsetAsync(p, 0, bytes) on the stream (zero a gradient / accumulator). */
+int upr_t_zero(void* p, size_t bytes, void* stream);
+
+/* ---- convolution ------------------------------------------------------- */
+
+/* nn.Conv2d.forward for any channel count (model.py:29-62 small convs:
+ * input/scale 3->32, output_layer 32->3, residual_head.2 32->1, channel /
+ * spatial attention; VGG conv1_1 of loss.py:198-211): direct FMA kernel,
+ * weights in PyTorch layout [Cout][Cin][kh][kw]. */
+int upr_t_conv_direct(const UprView* x, int B, int H, int W, int Cin, const float* w, const float* bias, int Cout,
+                      int kh, int kw, int stride, int pad, int dil, const UprView* y, int Ho, int Wo, int relu,
+                      int accumulate, void* stream);
+/* d(loss)/d(input) of the same conv (autograd of F.conv2d). */
+int upr_t_conv_direct_dgrad(const UprView* dy, int Ho, int Wo, const float* w, int B, int H, int W, int Cin, int Cout,
+                            int kh, int kw, int stride, int pad, int dil, const UprView* dx, int accumulate,
+                            void* stream);
+/* d(loss)/d(weight) [Cout][Cin][kh][kw] and d(loss)/d(bias) [Cout] (nullable),
+ * both ACCUMULATED (fp32 atomics). */
+int upr_t_conv_direct_wgrad(const UprView* x, const UprView* dy, int B, int H, int W, int Cin, int Ho, int Wo,
+                            int Cout, int kh, int kw, int stride, int pad, int dil, float* dw, float* dbias,
+                            void* stream);
+
+/* MFMA implicit-GEMM conv (the inference kernels of conv.hip/conv_halo.hip) on
+ * NHWC sources with channel stride/offset; Cin, Cout multiples of 32.
+ * wp: packed [N][kh*kw*Cin] (upr_t_pack_weight).  res (nullable) is added
+ * before the ReLU — with res == y it accumulates.  store 1 = ConvTranspose2d
+ * k2 s2 pixel shuffle (N = 4*Cout rows, y is [B,2Ho,2Wo]). */
+int upr_t_conv_mfma(const float* x, int B, int H, int W, int Cin, int x_cs, int x_coff, const float* wp,
+                    const float* bias, int N, int kh, int kw, int stride, int pad, int dil, const float* res,
+                    int res_cs, int relu, float* y, int y_cs, int y_coff, int store, void* stream);
+/* Weight gradient of an NHWC conv as an MFMA GEMM over pixels:
+ * dwp[co][(ky,kx,ci)] += sum_p dy[p][co] * x[window(p, ky, kx)][ci]
+ * (packed layout of upr_t_pack_weight mode 0).  Cin, Cout multiples of 32. */
+int upr_t_conv_wgrad(const float* x, int B, int H, int W, int Cin, int x_cs, int x_coff, const float* dy, int Ho,
+                     int Wo, int Cout, int dy_cs, int dy_coff, int kh, int kw, int stride, int pad, int dil,
+                     float* dwp, void* stream);
+/* Weight layout transforms.  mode 0: [Co][Ci][kh][kw] -> [Co][(ky,kx,ci)];
+ * mode 1: -> [Ci][(ky,kx,co)] spatially flipped (stride-1 dgrad as a conv);
+ * mode 2: ConvTranspose [Ci][Co][2][2] -> [(a,b,co)][ci] (forward GEMM);
+ * mode 3: ConvTranspose [Ci][Co][2][2] -> [ci][(a,b,co)] (dgrad = k2 s2 conv). */
+int upr_t_pack_weight(const float* w, float* out, int Co, int Ci, int kh, int kw, int mode, void* stream);
+/* Inverse of pack modes 0 and 3 for gradients; accumulate != 0 adds. */
+int upr_t_unpack_grad(const float* gp, float* g, int Co, int Ci, int kh, int kw, int mode, int accumulate,
+                      void* stream);
+/* z[B,2Ho,2Wo,C] = dy scattered to even positions, zeros elsewhere (dgrad of
+ * a stride-2 conv as a stride-1 conv over z). */
+int upr_t_zero_upsample(const float* dy, int B, int Ho, int Wo, int C, int dy_cs, int dy_coff, float* z,
+                        void* stream);
+
+/* ---- BatchNorm2d, training mode (nn.BatchNorm2d, model.py:106-162,196-229) -- */
+/* acc[2C] (fp64, zeroed by the caller) += (sum x, sum x^2) per channel of x[M][cs]. */
+int upr_t_bn_stats(const float* x, int M, int C, int cs, int coff, double* acc, void* stream);
+/* batch mean / 1/sqrt(var_biased + eps); running stats updated with the
+ * unbiased variance and momentum; *nbt += 1 (num_batches_tracked). */
+int upr_t_bn_finalize(const double* acc, int M, int C, float momentum, float eps, float* running_mean,
+                      float* running_var, int64_t* nbt, float* mean, float* invstd, void* stream);
+/* y = [relu](gamma*(x-mean)*invstd + beta + res_pre) + res_post  (res nullable). */
+int upr_t_bn_apply(const float* x, int M, int C, int x_cs, int x_coff, const float* mean, const float* invstd,
+                   const float* gamma, const float* beta, const float* res, int res_cs, int res_coff, int res_post,
+                   int relu, float* y, int y_cs, int y_coff, void* stream);
+/* acc[2C] (zeroed) += (sum g, sum g*xhat) per channel. */
+int upr_t_bn_bwd_reduce(const float* g, int g_cs, int g_coff, const float* x, int x_cs, int x_coff, const float* mean,
+                        const float* invstd, int M, int C, double* acc, void* stream);
+/* dx = gamma*invstd*(g - sum_g/M - xhat*sum_gx/M); dgamma/dbeta (nullable) += sums. */
+int upr_t_bn_bwd_apply(const float* g, int g_cs, int g_coff, const float* x, int x_cs, int x_coff, const float* mean,
+                       const float* invstd, const float* gamma, const double* acc, int M, int C, float* dgamma,
+                       float* dbeta, float* dx, int dx_cs, int dx_coff, int accumulate, void* stream);
+/* out[C] (+)= per-channel sum of g[M][cs] (conv bias gradients). */
+int upr_t_chan_sum(const float* g, int M, int C, int cs, int coff, float* out, int accumulate, void* stream);
+
+/* ---- elementwise / layout ---------------------------------------------- */
+/* g[m][c] *= (y[m][c] > 0)  (ReLU backward from the ReLU's output). */
+int upr_t_relu_mask(float* g, int g_cs, int g_coff, const float* y, int y_cs, int y_coff, int M, int C,
+                    void* stream);
+/* dst (+)= src, any layouts (NCHW <-> NHWC, concat slices). */
+int upr_t_copy(const UprView* src, const UprView* dst, int B, int H, int W, int C, int accumulate, void* stream);
+/* n contiguous elements.  op 0: out = sigmoid(a); op 1: out = a*b*(1-b)
+ * (sigmoid backward, b = sigmoid output); op 2: out = a*mask/(1-p) with
+ * mask_out[i] = hash(seed, i) >= p (nn.Dropout(p) train); op 3: out =
+ * a*mask_in/(1-p) (its backward); op 4: out = a + b; op 5: out = a * b[0]
+ * (scale by a device scalar, e.g. autograd's incoming loss gradient).
+ * out may alias a. */
+int upr_t_pointwise(const float* a, const float* b, float* out, size_t n, int op, const uint8_t* mask_in,
+                    uint8_t* mask_out, float p, uint64_t seed, void* stream);
+
+/* ---- pooling / resampling ---------------------------------------------- */
+/* nn.MaxPool2d(k, s, p) forward / backward (backward recomputes the argmax,
+ * first maximum in scan order, and scatters with atomics; dx accumulated). */
+int upr_t_maxpool(const UprView* x, int B, int H, int W, int C, int k, int s, int p, const UprView* y, int Ho, int Wo,
+                  void* stream);
+int upr_t_maxpool_bwd(const UprView* x, const UprView* dy, int B, int H, int W, int C, int k, int s, int p, int Ho,
+                      int Wo, const UprView* dx, void* stream);
+/* F.interpolate(mode='bilinear', align_corners=False) H x W -> Ho x Wo
+ * (scale = in/out per axis) and its backward (dx accumulated, atomics). */
+int upr_t_bilinear(const UprView* x, int B, int H, int W, int C, const UprView* y, int Ho, int Wo, int accumulate,
+                   void* stream);
+int upr_t_bilinear_bwd(const UprView* dy, int B, int H, int W, int C, int Ho, int Wo, const UprView* dx,
+                       void* stream);
+/* out[B][C] (+)= scale * sum over pixels (AdaptiveAvgPool2d(1) with scale = 1/HW). */
+int upr_t_pixel_sum(const float* x, int B, int HW, int C, int cs, int coff, float scale, float* out, int accumulate,
+                    void* stream);
+/* y[b][p][c] (+)= v[b][c] * scale  (broadcast of a per-image vector). */
+int upr_t_broadcast(const float* v, int B, int HW, int C, float scale, float* y, int y_cs, int y_coff, int accumulate,
+                    void* stream);
+
+/* ---- EnhancedFAM attention (model.py:47-59, 84-97) ---------------------- */
+/* o2 = o*ca[b][c]; m[b][p] = (mean_c o2, max_c o2).  o [B,HW,C] contiguous. */
+int upr_t_fam_ca_apply(const float* o, const float* ca, int B, int HW, int C, float* o2, float* m, void* stream);
+/* sa = sigmoid(s_pre); out = o2*sa. */
+int upr_t_fam_sa_apply(const float* o2, const float* s_pre, int B, int HW, int C, float* sa, float* out,
+                       void* stream);
+/* g_o2 = g*sa; g_spre = sum_c(g*o2) * sa*(1-sa). */
+int upr_t_fam_sa_bwd(const float* g, const float* o2, const float* sa, int B, int HW, int C, float* g_o2,
+                     float* g_spre, void* stream);
+/* g_o2 += g_m (mean/max routes); g_o = g_o2*ca; g_ca[b][c] += sum_p g_o2*o. */
+int upr_t_fam_ca_bwd(const float* g_o2, const float* g_m, const float* o, const float* o2, const float* ca, int B,
+                     int HW, int C, float* g_o, float* g_ca, void* stream);
+/* g_o = (g_o + g_pool[b][c]/HW) * (o > 0). */
+int upr_t_fam_pool_bwd(float* g_o, const float* g_pool, const float* o, int B, int HW, int C, void* stream);
+
+/* ---- network tail (model.py:351-358, 405-413, 439-455) ------------------ */
+/* illu = sigmoid(mean_c x + r): x [B,3,H,W], r [B,H,W] (1 channel), illu [B,1,H,W]. */
+int upr_t_head_fwd(const float* x, const float* r, float* illu, int B, int H, int W, void* stream);
+/* e = sigmoid(o) (o NHWC [B,H,W,3]); refl = x/(illu+1e-6); enh = refl*e + (1-refl)*e^2 (NCHW). */
+int upr_t_retinex_fwd(const float* x, const float* illu, const float* o, float* e, float* refl, float* enh, int B,
+                      int H, int W, void* stream);
+/* Backward of the two above from (g_enh, g_refl, g_illu) (NCHW; g_refl /
+ * g_illu nullable): g_o NHWC [B,H,W,3], g_r [B,H,W]. */
+int upr_t_retinex_bwd(const float* x, const float* illu, const float* e, const float* refl, const float* g_enh,
+                      const float* g_refl, const float* g_illu, float* g_o, float* g_r, int B, int H, int W,
+                      void* stream);
+
+/* ---- TotalLoss (losses/loss.py:586-753) -------------------------------- */
+/* Loss workspace bytes for a B x 3 x H x W batch (H, W multiples of 16). */
+size_t upr_t_loss_workspace(int B, int H, int W);
+/* Every non-perceptual, non-frequency term: exposure (:29-58), edge-aware
+ * smoothness (:138-176), colour (:351-371), spatial (:408-427), decoupling
+ * (:275-334), texture complexity 'tv' (:523-548) and the dynamic smooth weight
+ * (:704-720).  terms (device fp32, layout of upr_t_loss_total) receives
+ * [0..4] and [8];
+ * with grads != 0, g_enh / g_illu / g_refl (NCHW) are OVERWRITTEN with the
+ * weighted gradient of those terms. */
+int upr_t_loss_pixel(const float* low, const float* enh, const float* illu, const float* refl, int B, int H, int W,
+                     void* ws, float* terms, float* g_enh, float* g_illu, float* g_refl, int grads, float w_exp,
+                     float w_col, float w_spa, float w_dec, void* stream);
+/* Perceptual MSE level (F.mse_loss): acc (fp64) += sum (a-b)^2 / n; with
+ * g != NULL, g = scale*2*(a-b) (scale = weight/n). */
+int upr_t_mse(const float* a, const float* b, size_t n, double* acc, float* g, float scale, void* stream);
+/* (x NCHW - mean) / std -> NHWC [B,H,W,3]; bwd: g_x (NCHW) += g_y / std. */
+int upr_t_vgg_norm(const float* x, float* y, int B, int H, int W, void* stream);
+int upr_t_vgg_norm_bwd(const float* g_y, float* g_x, int B, int H, int W, void* stream);
+/* FrequencyLoss (:447-487) on complex spectra Ze, Zl (interleaved re/im,
+ * [B*3][H][W]): acc[1] += sum w*(|Ze|-|Zl|)^2 with w = 1 (dist > r) / 0.5;
+ * with G != NULL, G = scale*2*w*(|Ze|-|Zl|) * Ze/|Ze| (0 where |Ze| = 0). */
+int upr_t_freq(const float* Ze, const float* Zl, int BC, int H, int W, double* acc, float* G, float scale,
+               void* stream);
+/* g (+)= scale * Re(z) (z interleaved complex, n elements). */
+int upr_t_add_real(const float* z, float* g, size_t n, float scale, void* stream);
+/* out[i] = scale * acc[i], i < n (device-side finalisation of a reduction). */
+int upr_t_scale_acc(const double* acc, int n, float scale, float* out, void* stream);
+/* terms[9] = [exposure, smoothness, color, spatial, decouple, perceptual,
+ * frequency, total, smooth_weight]: terms[7] = the weighted sum of
+ * TotalLoss.forward (loss.py:722-729) with the fixed weights w[7] and
+ * terms[8] as the smoothness weight. */
+int upr_t_loss_total(float* terms, float w_exp, float w_col, float w_spa, float w_dec, float w_per, float w_freq,
+                     void* stream);
+
+/* ---- optimiser (torch.nn.utils.clip_grad_norm_ + torch.optim.Adam) ------ */
+/* acc (fp64, zeroed) += sum g^2 over n elements. */
+int upr_t_sqsum(const float* g, size_t n, double* acc, void* stream);
+/* One Adam step over a flat parameter buffer with the clip_grad_norm_(max_norm)
+ * coefficient computed on the device from sqsum: g' = g*min(1, max_norm/(sqrt(sqsum)+1e-6))
+ * + wd*p; m,v moments; bias-corrected update (train.py:84-103, Adam L2 decay).
+ * norm_out (nullable) receives sqrt(sqsum). */
+int upr_t_adam(float* p, const float* g, float* m, float* v, size_t n, const double* sqsum, float max_norm, float lr,
+               float beta1, float beta2, float eps, float weight_decay, int step, float* norm_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* UPR_TRAIN_H_ */

@@ -1,0 +1,1593 @@
+// Training kernels for gfx950: the backward pass of MultiScaleUP_Retinex, the
+// TotalLoss terms with their gradients, and the clip + Adam optimiser step
+// (reference trainers/train.py:63-103, losses/loss.py:12-753, models/model.py).
+// Contract of every entry: include/upr_train.h.
+//
+// Layout: activations are addressed through UprView strides (NCHW inputs,
+// NHWC activations, channel slices of concat buffers).  Everything computes in
+// fp32; per-channel / per-image reductions accumulate in fp64 (block partials
+// in registers + LDS, one fp64 atomic per block and channel).
+#include <cmath>
+#include <cstring>
+
+#include "upr_common.h"
+#include "../../include/upr.h"
+#include "../../include/upr_train.h"
+
+namespace upr {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct V {
+  float* d;
+  long long sb, sh, sw, sc;
+  __device__ __forceinline__ long long at(int b, int y, int x, int c) const {
+    return b * sb + y * sh + x * sw + c * sc;
+  }
+};
+
+static V mkv(const UprView* u) {
+  V v;
+  v.d = (float*)u->data;
+  v.sb = u->sb; v.sh = u->sh; v.sw = u->sw; v.sc = u->sc;
+  return v;
+}
+
+static inline int grid_for(long long n, int per = 256, int cap = 65536) {
+  long long g = (n + per - 1) / per;
+  if (g < 1) g = 1;
+  return (int)(g > cap ? cap : g);
+}
+
+#define GSTRIDE(i, n) for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < (n); \
+                           i += (long long)gridDim.x * blockDim.x)
+
+#define LAUNCH_CHECK() return (int)hipGetLastError()
+
+// ---------------------------------------------------------------------------
+// Direct convolution (small channel counts): forward / dgrad / wgrad
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void conv_direct_kernel(V x, int B, int H, int W, int Cin, const float* __restrict__ w,
+                                                          const float* __restrict__ bias, int Cout, int kh, int kw,
+                                                          int s, int p, int d, V y, int Ho, int Wo, int relu,
+                                                          int accum) {
+  const long long n = (long long)B * Ho * Wo * Cout;
+  GSTRIDE(i, n) {
+    const int co = (int)(i % Cout);
+    long long r = i / Cout;
+    const int ox = (int)(r % Wo); r /= Wo;
+    const int oy = (int)(r % Ho);
+    const int b = (int)(r / Ho);
+    float a = bias ? bias[co] : 0.f;
+    const float* wc = w + (size_t)co * Cin * kh * kw;
+    for (int ci = 0; ci < Cin; ++ci) {
+      for (int ky = 0; ky < kh; ++ky) {
+        const int iy = oy * s - p + ky * d;
+        if (iy < 0 || iy >= H) continue;
+        for (int kx = 0; kx < kw; ++kx) {
+          const int ix = ox * s - p + kx * d;
+          if (ix < 0 || ix >= W) continue;
+          a = fmaf(x.d[x.at(b, iy, ix, ci)], wc[(ci * kh + ky) * kw + kx], a);
+        }
+      }
+    }
+    float* yp = y.d + y.at(b, oy, ox, co);
+    if (accum) a += *yp;
+    if (relu) a = fmaxf(a, 0.f);
+    *yp = a;
+  }
+}
+
+__global__ __launch_bounds__(256) void conv_direct_dgrad_kernel(V dy, int Ho, int Wo, const float* __restrict__ w,
+                                                                int B, int H, int W, int Cin, int Cout, int kh,
+                                                                int kw, int s, int p, int d, V dx, int accum) {
+  const long long n = (long long)B * H * W * Cin;
+  GSTRIDE(i, n) {
+    const int ci = (int)(i % Cin);
+    long long r = i / Cin;
+    const int ix = (int)(r % W); r /= W;
+    const int iy = (int)(r % H);
+    const int b = (int)(r / H);
+    float a = 0.f;
+    for (int ky = 0; ky < kh; ++ky) {
+      const int yn = iy + p - ky * d;
+      if (yn < 0 || yn % s) continue;
+      const int oy = yn / s;
+      if (oy >= Ho) continue;
+      for (int kx = 0; kx < kw; ++kx) {
+        const int xn = ix + p - kx * d;
+        if (xn < 0 || xn % s) continue;
+        const int ox = xn / s;
+        if (ox >= Wo) continue;
+        for (int co = 0; co < Cout; ++co)
+          a = fmaf(dy.d[dy.at(b, oy, ox, co)], w[(((size_t)co * Cin + ci) * kh + ky) * kw + kx], a);
+      }
+    }
+    float* xp = dx.d + dx.at(b, iy, ix, ci);
+    if (accum) a += *xp;
+    *xp = a;
+  }
+}
+
+// Weight gradient of a small conv: a chunk of CH output pixels is staged in
+// LDS as dy[CH][Cout] and its im2col rows col[CH][taps*Cin]; each thread owns
+// weight entries (co, ci, tap) (+ a bias entry) and sums over the chunk.
+// Blocks loop over chunks (grid-stride) and issue their atomics once.
+__global__ __launch_bounds__(256) void conv_direct_wgrad_kernel(V x, V dy, int B, int H, int W, int Cin, int Ho,
+                                                                int Wo, int Cout, int kh, int kw, int s, int p,
+                                                                int d, int CH, float* __restrict__ dw,
+                                                                float* __restrict__ dbias) {
+  extern __shared__ float sm[];
+  const int taps = kh * kw;
+  const int KC = taps * Cin;
+  float* sdy = sm;              // [CH][Cout]
+  float* scol = sm + CH * Cout;  // [CH][KC]
+  const long long P = (long long)B * Ho * Wo;
+  const int nW = Cout * KC;
+  const int nE = nW + (dbias ? Cout : 0);
+  constexpr int MAXE = 16;
+  float acc[MAXE];
+#pragma unroll
+  for (int k = 0; k < MAXE; ++k) acc[k] = 0.f;
+  for (long long c0 = (long long)blockIdx.x * CH; c0 < P; c0 += (long long)gridDim.x * CH) {
+    __syncthreads();
+    for (int t = threadIdx.x; t < CH * Cout; t += blockDim.x) {
+      const int pp = t / Cout, co = t - pp * Cout;
+      const long long pix = c0 + pp;
+      float v = 0.f;
+      if (pix < P) {
+        const int ox = (int)(pix % Wo);
+        const long long r = pix / Wo;
+        const int oy = (int)(r % Ho), b = (int)(r / Ho);
+        v = dy.d[dy.at(b, oy, ox, co)];
+      }
+      sdy[t] = v;
+    }
+    for (int t = threadIdx.x; t < CH * KC; t += blockDim.x) {
+      const int pp = t / KC, k = t - pp * KC;
+      const int tap = k / Cin, ci = k - tap * Cin;
+      const int ky = tap / kw, kx = tap - ky * kw;
+      const long long pix = c0 + pp;
+      float v = 0.f;
+      if (pix < P) {
+        const int ox = (int)(pix % Wo);
+        const long long r = pix / Wo;
+        const int oy = (int)(r % Ho), b = (int)(r / Ho);
+        const int iy = oy * s - p + ky * d, ix = ox * s - p + kx * d;
+        if (iy >= 0 && iy < H && ix >= 0 && ix < W) v = x.d[x.at(b, iy, ix, ci)];
+      }
+      scol[t] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < MAXE; ++k) {
+      const int e = threadIdx.x + k * 256;
+      if (e >= nE) break;
+      float a = acc[k];
+      if (e < nW) {
+        const int co = e / KC, kk = e - co * KC;
+        for (int pp = 0; pp < CH; ++pp) a = fmaf(sdy[pp * Cout + co], scol[pp * KC + kk], a);
+      } else {
+        const int co = e - nW;
+        for (int pp = 0; pp < CH; ++pp) a += sdy[pp * Cout + co];
+      }
+      acc[k] = a;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < MAXE; ++k) {
+    const int e = threadIdx.x + k * 256;
+    if (e >= nE) break;
+    if (e < nW) {
+      // e = co*KC + tap*Cin + ci -> PyTorch [co][ci][ky][kx]
+      const int co = e / KC, kk = e - co * KC;
+      const int tap = kk / Cin, ci = kk - tap * Cin;
+      atomicAdd(dw + ((size_t)co * Cin + ci) * taps + tap, acc[k]);
+    } else {
+      atomicAdd(dbias + (e - nW), acc[k]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// MFMA weight gradient (C % 32 == 0): block tile 32 co x 32 ci of one tap,
+// 4 waves each summing interleaved groups of 4 pixels with
+// v_mfma_f32_16x16x4_f32 (A = dy[p][co], B = x[window(p)][ci], k = pixel).
+// ---------------------------------------------------------------------------
+constexpr int WG_PPB = 1024;  // pixels per block
+
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(const float* __restrict__ x, int B, int H, int W, int Cin,
+                                                         int x_cs, int x_coff, const float* __restrict__ dy, int Ho,
+                                                         int Wo, int Cout, int dy_cs, int dy_coff, int kh, int kw,
+                                                         int s, int p, int d, float* __restrict__ dwp) {
+  __shared__ float red[4][32 * 32];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int co0 = blockIdx.y * 32;
+  const int cblocks = Cin / 32;
+  const int tap = blockIdx.z / cblocks;
+  const int ci0 = (blockIdx.z - tap * cblocks) * 32;
+  const int ky = tap / kw, kx = tap - ky * kw;
+  const long long P = (long long)B * Ho * Wo;
+  const long long p0 = (long long)blockIdx.x * WG_PPB;
+  const int kk = lane >> 4, r = lane & 15;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int g = wave; g < WG_PPB / 4; g += 4) {
+    const long long pix = p0 + g * 4 + kk;
+    float a0 = 0.f, a1 = 0.f, b0 = 0.f, b1 = 0.f;
+    if (pix < P) {
+      const float* dp = dy + pix * dy_cs + dy_coff + co0 + r;
+      a0 = dp[0];
+      a1 = dp[16];
+      const int ox = (int)(pix % Wo);
+      const long long rr = pix / Wo;
+      const int oy = (int)(rr % Ho), b = (int)(rr / Ho);
+      const int iy = oy * s - p + ky * d, ix = ox * s - p + kx * d;
+      if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
+        const float* xp = x + (((long long)b * H + iy) * W + ix) * x_cs + x_coff + ci0 + r;
+        b0 = xp[0];
+        b1 = xp[16];
+      }
+    }
+    acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
+    acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
+    acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
+    acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
+  }
+  // C[row][col]: lane holds rows 4*(lane>>4)+q, col lane&15 of each 16x16 tile
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = i * 16 + kk * 4 + q, col = j * 16 + r;
+        red[wave][row * 32 + col] = acc[i][j][q];
+      }
+  __syncthreads();
+  const int KT = kh * kw * Cin;
+  for (int e = threadIdx.x; e < 1024; e += 256) {
+    const float v = red[0][e] + red[1][e] + red[2][e] + red[3][e];
+    const int row = e >> 5, col = e & 31;
+    atomicAdd(dwp + (size_t)(co0 + row) * KT + tap * Cin + ci0 + col, v);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// weight layout transforms
+// ---------------------------------------------------------------------------
+__global__ void pack_weight_kernel(const float* __restrict__ w, float* __restrict__ o, int Co, int Ci, int kh, int kw,
+                                   int mode) {
+  const int taps = kh * kw;
+  const long long n = (long long)Co * Ci * taps;
+  GSTRIDE(i, n) {
+    // i enumerates the SOURCE layout
+    if (mode == 0 || mode == 1) {
+      const int tap = (int)(i % taps);
+      const long long r = i / taps;
+      const int ci = (int)(r % Ci), co = (int)(r / Ci);
+      if (mode == 0) {
+        o[((size_t)co * taps + tap) * Ci + ci] = w[i];
+      } else {
+        const int ft = taps - 1 - tap;  // (kh-1-ky, kw-1-kx)
+        o[((size_t)ci * taps + ft) * Co + co] = w[i];
+      }
+    } else {
+      // ConvTranspose weight [Ci][Co][2][2] with Co, Ci as named in the call
+      // (Ci = in_channels, Co = out_channels), q = a*2+b
+      const int q = (int)(i % 4);
+      const long long r = i / 4;
+      const int co = (int)(r % Co), ci = (int)(r / Co);
+      if (mode == 2) o[((size_t)q * Co + co) * Ci + ci] = w[i];
+      else o[((size_t)ci * 4 + q) * Co + co] = w[i];
+    }
+  }
+}
+
+__global__ void unpack_grad_kernel(const float* __restrict__ gp, float* __restrict__ g, int Co, int Ci, int kh, int kw,
+                                   int mode, int accum) {
+  const int taps = kh * kw;
+  const long long n = (long long)Co * Ci * taps;
+  GSTRIDE(i, n) {
+    float v;
+    if (mode == 0) {
+      const int tap = (int)(i % taps);
+      const long long r = i / taps;
+      const int ci = (int)(r % Ci), co = (int)(r / Ci);
+      v = gp[((size_t)co * taps + tap) * Ci + ci];
+    } else {
+      const int q = (int)(i % 4);
+      const long long r = i / 4;
+      const int co = (int)(r % Co), ci = (int)(r / Co);
+      v = gp[((size_t)ci * 4 + q) * Co + co];
+    }
+    g[i] = accum ? g[i] + v : v;
+  }
+}
+
+__global__ void zero_upsample_kernel(const float* __restrict__ dy, int B, int Ho, int Wo, int C, int cs, int coff,
+                                     float* __restrict__ z) {
+  const long long n = (long long)B * 2 * Ho * 2 * Wo * C;
+  GSTRIDE(i, n) {
+    const int c = (int)(i % C);
+    long long r = i / C;
+    const int X = (int)(r % (2 * Wo)); r /= 2 * Wo;
+    const int Y = (int)(r % (2 * Ho));
+    const int b = (int)(r / (2 * Ho));
+    float v = 0.f;
+    if (!(X & 1) && !(Y & 1)) v = dy[(((long long)b * Ho + (Y >> 1)) * Wo + (X >> 1)) * cs + coff + c];
+    z[i] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// per-channel reductions over M rows: mode 0 (x, x^2), mode 1 (g, g*xhat),
+// mode 2 (g) -> float out via atomics
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void chan_reduce_kernel(const float* __restrict__ a, int a_cs, int a_coff,
+                                                          const float* __restrict__ x, int x_cs, int x_coff,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ invstd, int M, int C, int mode,
+                                                          double* __restrict__ acc, float* __restrict__ fout) {
+  __shared__ double s1[256], s2[256];
+  const int rows_per_block = (M + gridDim.x - 1) / gridDim.x;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(M, r0 + rows_per_block);
+  for (int cb = 0; cb < C; cb += 256) {
+    const int cw = min(256, C - cb);
+    const int R = 256 / cw;
+    const int c = threadIdx.x % cw, rg = threadIdx.x / cw;
+    double u = 0.0, v = 0.0;
+    if (rg < R) {
+      const int cc = cb + c;
+      float mu = 0.f, is = 0.f;
+      if (mode == 1) { mu = mean[cc]; is = invstd[cc]; }
+      for (int r = r0 + rg; r < r1; r += R) {
+        const float av = a[(size_t)r * a_cs + a_coff + cc];
+        if (mode == 0) { u += av; v += (double)av * av; }
+        else if (mode == 1) { u += av; v += (double)av * ((x[(size_t)r * x_cs + x_coff + cc] - mu) * is); }
+        else u += av;
+      }
+    }
+    s1[threadIdx.x] = u;
+    s2[threadIdx.x] = v;
+    __syncthreads();
+    if (threadIdx.x < cw) {
+      double t1 = 0.0, t2 = 0.0;
+      for (int k = 0; k < R; ++k) { t1 += s1[k * cw + threadIdx.x]; t2 += s2[k * cw + threadIdx.x]; }
+      const int cc = cb + threadIdx.x;
+      if (mode == 2) atomicAdd(fout + cc, (float)t1);
+      else { atomicAdd(acc + cc, t1); atomicAdd(acc + C + cc, t2); }
+    }
+    __syncthreads();
+  }
+}
+
+static int reduce_grid(int M) { return grid_for(M, 512, 2048); }
+
+__global__ void bn_finalize_kernel(const double* __restrict__ acc, int M, int C, float momentum, float eps,
+                                   float* __restrict__ rm, float* __restrict__ rv, long long* nbt,
+                                   float* __restrict__ mean, float* __restrict__ invstd) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 && nbt) *nbt += 1;
+  if (c >= C) return;
+  const double mu = acc[c] / M;
+  double var = acc[C + c] / M - mu * mu;
+  if (var < 0) var = 0;
+  mean[c] = (float)mu;
+  invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (rm) rm[c] = (1.f - momentum) * rm[c] + momentum * (float)mu;
+  if (rv) {
+    const double unb = M > 1 ? var * M / (M - 1) : var;
+    rv[c] = (1.f - momentum) * rv[c] + momentum * (float)unb;
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__ x, int M, int C, int x_cs,
+                                                       int x_coff, const float* __restrict__ mean,
+                                                       const float* __restrict__ invstd,
+                                                       const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, const float* res, int res_cs,
+                                                       int res_coff, int res_post, int relu, float* y, int y_cs,
+                                                       int y_coff) {
+  const long long n = (long long)M * C;
+  GSTRIDE(i, n) {
+    const int c = (int)(i % C);
+    const long long m = i / C;
+    float v = (x[m * x_cs + x_coff + c] - mean[c]) * invstd[c] * gamma[c] + beta[c];
+    const float rv = res ? res[m * res_cs + res_coff + c] : 0.f;
+    if (!res_post) v += rv;
+    if (relu) v = fmaxf(v, 0.f);
+    if (res_post) v += rv;
+    y[m * y_cs + y_coff + c] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restrict__ g, int g_cs, int g_coff,
+                                                           const float* __restrict__ x, int x_cs, int x_coff,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd,
+                                                           const float* __restrict__ gamma,
+                                                           const double* __restrict__ acc, int M, int C,
+                                                           float* dgamma, float* dbeta, float* dx, int dx_cs,
+                                                           int dx_coff, int accum) {
+  if (blockIdx.x == 0) {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      if (dgamma) dgamma[c] += (float)acc[C + c];
+      if (dbeta) dbeta[c] += (float)acc[c];
+    }
+  }
+  const long long n = (long long)M * C;
+  GSTRIDE(i, n) {
+    const int c = (int)(i % C);
+    const long long m = i / C;
+    const float is = invstd[c];
+    const float xh = (x[m * x_cs + x_coff + c] - mean[c]) * is;
+    const float sg = (float)(acc[c] / M), sgx = (float)(acc[C + c] / M);
+    float v = gamma[c] * is * (g[m * g_cs + g_coff + c] - sg - xh * sgx);
+    float* o = dx + m * dx_cs + dx_coff + c;
+    if (accum) v += *o;
+    *o = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// elementwise
+// ---------------------------------------------------------------------------
+__global__ void relu_mask_kernel(float* g, int g_cs, int g_coff, const float* __restrict__ y, int y_cs, int y_coff,
+                                 int M, int C) {
+  const long long n = (long long)M * C;
+  GSTRIDE(i, n) {
+    const int c = (int)(i % C);
+    const long long m = i / C;
+    if (!(y[m * y_cs + y_coff + c] > 0.f)) g[m * g_cs + g_coff + c] = 0.f;
+  }
+}
+
+__global__ void copy_kernel(V s, V d, int B, int H, int W, int C, int accum) {
+  const long long n = (long long)B * H * W * C;
+  GSTRIDE(i, n) {
+    const int c = (int)(i % C);
+    long long r = i / C;
+    const int x = (int)(r % W); r /= W;
+    const int y = (int)(r % H);
+    const int b = (int)(r / H);
+    const float v = s.d[s.at(b, y, x, c)];
+    float* o = d.d + d.at(b, y, x, c);
+    *o = accum ? *o + v : v;
+  }
+}
+
+__device__ __forceinline__ float hash_uniform(unsigned long long seed, unsigned long long i) {
+  // splitmix64 of (seed, index) -> [0, 1)
+  unsigned long long z = seed + 0x9E3779B97F4A7C15ull * (i + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.0f / 16777216.0f);
+}
+
+__global__ void pointwise_kernel(const float* a, const float* b, float* out, long long n, int op,
+                                 const uint8_t* __restrict__ mask_in, uint8_t* __restrict__ mask_out, float p,
+                                 unsigned long long seed) {
+  GSTRIDE(i, n) {
+    const float av = a[i];
+    float v;
+    switch (op) {
+      case 0: v = 1.f / (1.f + expf(-av)); break;
+      case 1: { const float s = b[i]; v = av * s * (1.f - s); } break;
+      case 2: {
+        const uint8_t m = hash_uniform(seed, (unsigned long long)i) >= p ? 1 : 0;
+        mask_out[i] = m;
+        v = m ? av * (1.f / (1.f - p)) : 0.f;
+      } break;
+      case 3: v = mask_in[i] ? av * (1.f / (1.f - p)) : 0.f; break;
+      case 4: v = av + b[i]; break;
+      default: v = av * b[0]; break;
+    }
+    out[i] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// pooling / resampling
+// ---------------------------------------------------------------------------
+__global__ void maxpool_kernel(V x, int B, int H, int W, int C, int k, int s, int p, V y, int Ho, int Wo) {
+  const long long n = (long long)B * Ho * Wo * C;
+  GSTRIDE(i, n) {
+    const int c = (int)(i % C);
+    long long r = i / C;
+    const int ox = (int)(r % Wo); r /= Wo;
+    const int oy = (int)(r % Ho);
+    const int b = (int)(r / Ho);
+    float m = -INFINITY;
+    for (int ky = 0; ky < k; ++ky) {
+      const int iy = oy * s - p + ky;
+      if (iy < 0 || iy >= H) continue;
+      for (int kx = 0; kx < k; ++kx) {
+        const int ix = ox * s - p + kx;
+        if (ix < 0 || ix >= W) continue;
+        const float v = x.d[x.at(b, iy, ix, c)];
+        if (v > m || isnan(v)) m = v;
+      }
+    }
+    y.d[y.at(b, oy, ox, c)] = m;
+  }
+}
+
+__global__ void maxpool_bwd_kernel(V x, V dy, int B, int H, int W, int C, int k, int s, int p, int Ho, int Wo, V dx) {
+  const long long n = (long long)B * Ho * Wo * C;
+  GSTRIDE(i, n) {
+    const int c = (int)(i % C);
+    long long r = i / C;
+    const int ox = (int)(r % Wo); r /= Wo;
+    const int oy = (int)(r % Ho);
+    const int b = (int)(r / Ho);
+    float m = -INFINITY;
+    int by = -1, bx = -1;
+    for (int ky = 0; ky < k; ++ky) {
+      const int iy = oy * s - p + ky;
+      if (iy < 0 || iy >= H) continue;
+      for (int kx = 0; kx < k; ++kx) {
+        const int ix = ox * s - p + kx;
+        if (ix < 0 || ix >= W) continue;
+        const float v = x.d[x.at(b, iy, ix, c)];
+        if (v > m || isnan(v) || by < 0) { m = v; by = iy; bx = ix; }
+        if (isnan(v)) break;
+      }
+    }
+    if (by >= 0) atomicAdd(dx.d + dx.at(b, by, bx, c), dy.d[dy.at(b, oy, ox, c)]);
+  }
+}
+
+__device__ __forceinline__ void bilin_src(int o, int in, float scale, int& i0, int& i1, float& l) {
+  float sr = ((float)o + 0.5f) * scale - 0.5f;
+  if (sr < 0.f) sr = 0.f;
+  i0 = (int)sr;
+  if (i0 > in - 1) i0 = in - 1;
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  l = sr - (float)i0;
+}
+
+__global__ void bilinear_kernel(V x, int B, int H, int W, int C, V y, int Ho, int Wo, float sh, float sw, int accum) {
+  const long long n = (long long)B * Ho * Wo * C;
+  GSTRIDE(i, n) {
+    const int c = (int)(i % C);
+    long long r = i / C;
+    const int ox = (int)(r % Wo); r /= Wo;
+    const int oy = (int)(r % Ho);
+    const int b = (int)(r / Ho);
+    int y0, y1, x0, x1;
+    float ly, lx;
+    bilin_src(oy, H, sh, y0, y1, ly);
+    bilin_src(ox, W, sw, x0, x1, lx);
+    const float v = (1.f - ly) * ((1.f - lx) * x.d[x.at(b, y0, x0, c)] + lx * x.d[x.at(b, y0, x1, c)]) +
+                    ly * ((1.f - lx) * x.d[x.at(b, y1, x0, c)] + lx * x.d[x.at(b, y1, x1, c)]);
+    float* o = y.d + y.at(b, oy, ox, c);
+    *o = accum ? *o + v : v;
+  }
+}
+
+__global__ void bilinear_bwd_kernel(V dy, int B, int H, int W, int C, int Ho, int Wo, float sh, float sw, V dx) {
+  const long long n = (long long)B * Ho * Wo * C;
+  GSTRIDE(i, n) {
+    const int c = (int)(i % C);
+    long long r = i / C;
+    const int ox = (int)(r % Wo); r /= Wo;
+    const int oy = (int)(r % Ho);
+    const int b = (int)(r / Ho);
+    int y0, y1, x0, x1;
+    float ly, lx;
+    bilin_src(oy, H, sh, y0, y1, ly);
+    bilin_src(ox, W, sw, x0, x1, lx);
+    const float g = dy.d[dy.at(b, oy, ox, c)];
+    atomicAdd(dx.d + dx.at(b, y0, x0, c), g * (1.f - ly) * (1.f - lx));
+    atomicAdd(dx.d + dx.at(b, y0, x1, c), g * (1.f - ly) * lx);
+    atomicAdd(dx.d + dx.at(b, y1, x0, c), g * ly * (1.f - lx));
+    atomicAdd(dx.d + dx.at(b, y1, x1, c), g * ly * lx);
+  }
+}
+
+// per-(image, channel) pixel sums: grid (chunks, B)
+__global__ __launch_bounds__(256) void pixel_sum_kernel(const float* __restrict__ x, int HW, int C, int cs, int coff,
+                                                        float scale, float* __restrict__ out) {
+  __shared__ float sm[256];
+  const int b = blockIdx.y;
+  const int per = (HW + gridDim.x - 1) / gridDim.x;
+  const int p0 = blockIdx.x * per, p1 = min(HW, p0 + per);
+  for (int cb = 0; cb < C; cb += 256) {
+    const int cw = min(256, C - cb);
+    const int R = 256 / cw;
+    const int c = threadIdx.x % cw, rg = threadIdx.x / cw;
+    float u = 0.f;
+    if (rg < R)
+      for (int q = p0 + rg; q < p1; q += R) u += x[((size_t)b * HW + q) * cs + coff + cb + c];
+    sm[threadIdx.x] = u;
+    __syncthreads();
+    if (threadIdx.x < cw) {
+      float t = 0.f;
+      for (int k = 0; k < R; ++k) t += sm[k * cw + threadIdx.x];
+      atomicAdd(out + (size_t)b * C + cb + threadIdx.x, t * scale);
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void broadcast_kernel(const float* __restrict__ v, int B, int HW, int C, float scale, float* y, int y_cs,
+                                 int y_coff, int accum) {
+  const long long n = (long long)B * HW * C;
+  GSTRIDE(i, n) {
+    const int c = (int)(i % C);
+    const long long m = i / C;
+    const int b = (int)(m / HW);
+    float* o = y + m * y_cs + y_coff + c;
+    const float val = v[(size_t)b * C + c] * scale;
+    *o = accum ? *o + val : val;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// EnhancedFAM attention (one thread per pixel, C channels contiguous)
+// ---------------------------------------------------------------------------
+__global__ void fam_ca_apply_kernel(const float* __restrict__ o, const float* __restrict__ ca, int B, int HW, int C,
+                                    float* __restrict__ o2, float* __restrict__ m) {
+  const long long n = (long long)B * HW;
+  GSTRIDE(i, n) {
+    const int b = (int)(i / HW);
+    const float* op = o + i * C;
+    float* q = o2 + i * C;
+    float s = 0.f, mx = -INFINITY;
+    for (int c = 0; c < C; ++c) {
+      const float v = op[c] * ca[(size_t)b * C + c];
+      q[c] = v;
+      s += v;
+      if (v > mx || isnan(v)) mx = v;
+    }
+    m[i * 2] = s / (float)C;
+    m[i * 2 + 1] = mx;
+  }
+}
+
+__global__ void fam_sa_apply_kernel(const float* __restrict__ o2, const float* __restrict__ s_pre, int B, int HW, int C,
+                                    float* __restrict__ sa, float* __restrict__ out) {
+  const long long n = (long long)B * HW;
+  GSTRIDE(i, n) {
+    const float a = 1.f / (1.f + expf(-s_pre[i]));
+    sa[i] = a;
+    for (int c = 0; c < C; ++c) out[i * C + c] = o2[i * C + c] * a;
+  }
+}
+
+__global__ void fam_sa_bwd_kernel(const float* __restrict__ g, const float* __restrict__ o2,
+                                  const float* __restrict__ sa, int B, int HW, int C, float* __restrict__ g_o2,
+                                  float* __restrict__ g_spre) {
+  const long long n = (long long)B * HW;
+  GSTRIDE(i, n) {
+    const float a = sa[i];
+    float t = 0.f;
+    for (int c = 0; c < C; ++c) {
+      const float gv = g[i * C + c];
+      t += gv * o2[i * C + c];
+      g_o2[i * C + c] = gv * a;
+    }
+    g_spre[i] = t * a * (1.f - a);
+  }
+}
+
+// g_ca[b][c] partials go through LDS: a block covers a pixel range of one image
+__global__ __launch_bounds__(256) void fam_ca_bwd_kernel(const float* __restrict__ g_o2, const float* __restrict__ g_m,
+                                                         const float* __restrict__ o, const float* __restrict__ o2,
+                                                         const float* __restrict__ ca, int HW, int C,
+                                                         float* __restrict__ g_o, float* __restrict__ g_ca) {
+  __shared__ float sm[256][33];
+  const int b = blockIdx.y;
+  const int per = (HW + gridDim.x - 1) / gridDim.x;
+  const int p0 = blockIdx.x * per, p1 = min(HW, p0 + per);
+  float part[32];
+#pragma unroll
+  for (int c = 0; c < 32; ++c) part[c] = 0.f;
+  for (int q = p0 + threadIdx.x; q < p1; q += 256) {
+    const size_t i = (size_t)b * HW + q;
+    const float gm0 = g_m[i * 2] / (float)C, gm1 = g_m[i * 2 + 1];
+    // argmax over channels of o2 (first maximum, torch.max semantics)
+    int am = 0;
+    float mx = o2[i * C];
+    for (int c = 1; c < C; ++c) {
+      const float v = o2[i * C + c];
+      if (v > mx || (isnan(v) && !isnan(mx))) { mx = v; am = c; }
+    }
+#pragma unroll
+    for (int c = 0; c < 32; ++c) {
+      if (c >= C) break;
+      const float gt = g_o2[i * C + c] + gm0 + (c == am ? gm1 : 0.f);
+      g_o[i * C + c] = gt * ca[(size_t)b * C + c];
+      part[c] += gt * o[i * C + c];
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 32; ++c) sm[threadIdx.x][c] = part[c];
+  __syncthreads();
+  if (threadIdx.x < C) {
+    float t = 0.f;
+    for (int k = 0; k < 256; ++k) t += sm[k][threadIdx.x];
+    atomicAdd(g_ca + (size_t)b * C + threadIdx.x, t);
+  }
+}
+
+__global__ void fam_pool_bwd_kernel(float* g_o, const float* __restrict__ g_pool, const float* __restrict__ o, int B,
+                                    int HW, int C) {
+  const long long n = (long long)B * HW * C;
+  GSTRIDE(i, n) {
+    const int c = (int)(i % C);
+    const int b = (int)(i / ((long long)HW * C));
+    const float v = g_o[i] + g_pool[(size_t)b * C + c] / (float)HW;
+    g_o[i] = o[i] > 0.f ? v : 0.f;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// network tail
+// ---------------------------------------------------------------------------
+__global__ void head_fwd_kernel(const float* __restrict__ x, const float* __restrict__ r, float* __restrict__ illu,
+                                int B, int HW) {
+  const long long n = (long long)B * HW;
+  GSTRIDE(i, n) {
+    const int b = (int)(i / HW), p = (int)(i - (long long)b * HW);
+    const float* xb = x + (size_t)b * 3 * HW + p;
+    const float z = (xb[0] + xb[HW] + xb[2 * HW]) / 3.f + r[i];
+    illu[i] = 1.f / (1.f + expf(-z));
+  }
+}
+
+__global__ void retinex_fwd_kernel(const float* __restrict__ x, const float* __restrict__ illu,
+                                   const float* __restrict__ o, float* __restrict__ e, float* __restrict__ refl,
+                                   float* __restrict__ enh, int B, int HW) {
+  const long long n = (long long)B * HW;
+  GSTRIDE(i, n) {
+    const int b = (int)(i / HW), p = (int)(i - (long long)b * HW);
+    const float den = illu[i] + 1e-6f;
+    for (int c = 0; c < 3; ++c) {
+      const size_t k = ((size_t)b * 3 + c) * HW + p;
+      const float ev = 1.f / (1.f + expf(-o[i * 3 + c]));
+      const float rv = x[k] / den;
+      e[i * 3 + c] = ev;
+      refl[k] = rv;
+      enh[k] = rv * ev + (1.f - rv) * (ev * ev);
+    }
+  }
+}
+
+__global__ void retinex_bwd_kernel(const float* __restrict__ x, const float* __restrict__ illu,
+                                   const float* __restrict__ e, const float* __restrict__ refl,
+                                   const float* __restrict__ g_enh, const float* __restrict__ g_refl,
+                                   const float* __restrict__ g_illu, float* __restrict__ g_o, float* __restrict__ g_r,
+                                   int B, int HW) {
+  const long long n = (long long)B * HW;
+  GSTRIDE(i, n) {
+    const int b = (int)(i / HW), p = (int)(i - (long long)b * HW);
+    const float il = illu[i];
+    const float den = il + 1e-6f;
+    float gi = g_illu ? g_illu[i] : 0.f;
+    for (int c = 0; c < 3; ++c) {
+      const size_t k = ((size_t)b * 3 + c) * HW + p;
+      const float ev = e[i * 3 + c], rv = refl[k], ge = g_enh[k];
+      // enh = r*e + (1-r)*e^2
+      const float gev = ge * (rv + 2.f * ev * (1.f - rv));
+      const float grv = ge * (ev - ev * ev) + (g_refl ? g_refl[k] : 0.f);
+      g_o[i * 3 + c] = gev * ev * (1.f - ev);
+      // r = x / (illu + 1e-6)
+      gi -= grv * x[k] / (den * den);
+    }
+    g_r[i] = gi * il * (1.f - il);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// TotalLoss pixel terms (loss.py): workspace of fp64 accumulators
+// ---------------------------------------------------------------------------
+enum {
+  LA_COL = 0,      // 3: sum enh_c
+  LA_SPA_H = 3, LA_SPA_V = 4,
+  LA_SM_H = 5, LA_SM_V = 6,
+  LA_TV_H = 7, LA_TV_V = 8,
+  LA_GLOW = 9,
+  LA_FIXED = 16,   // then per image: [sum illu, sum r_j (3), sum illu*r_j (3)]
+};
+
+struct LossWS {
+  double* acc;     // LA_FIXED + 7B
+  double* patch;   // B * (H/16) * (W/16) sums of gray(enh)
+  double* rowsum;  // B*H   sum_{x<W-1} edge
+  double* colsum;  // B*W   sum_{y<H-1} edge
+  float* scal;     // finalised scalars for the gradient pass
+};
+
+static LossWS loss_ws(void* ws, int B, int H, int W) {
+  LossWS l;
+  char* p = (char*)ws;
+  l.acc = (double*)p; p += align_up(sizeof(double) * (LA_FIXED + 7 * B), 256);
+  l.patch = (double*)p; p += align_up(sizeof(double) * B * (H / 16) * (W / 16), 256);
+  l.rowsum = (double*)p; p += align_up(sizeof(double) * B * H, 256);
+  l.colsum = (double*)p; p += align_up(sizeof(double) * B * W, 256);
+  l.scal = (float*)p;
+  return l;
+}
+static size_t loss_ws_bytes(int B, int H, int W) {
+  return align_up(sizeof(double) * (LA_FIXED + 7 * B), 256) + align_up(sizeof(double) * B * (H / 16) * (W / 16), 256) +
+         align_up(sizeof(double) * B * H, 256) + align_up(sizeof(double) * B * W, 256) +
+         align_up(sizeof(float) * (64 + 8 * B), 256);
+}
+
+// scalar slots
+enum { LS_T = 0, LS_NPATCH = 1, LS_WS = 2, LS_MU = 3 /*3*/, LS_NH = 6, LS_NV = 7, LS_DEC = 8 /* per image 5 */ };
+
+__device__ __forceinline__ float gray_at(const float* img, size_t base, int HW, int p) {
+  return (img[base + p] + img[base + HW + p] + img[base + 2 * HW + p]) / 3.f;
+}
+
+// Sobel edge magnitude of gray(low) with reflect padding (loss.py:110-136)
+__device__ float edge_at(const float* low, size_t base, int H, int W, int y, int x) {
+  const int HW = H * W;
+  float g[3][3];
+  for (int dy = -1; dy <= 1; ++dy) {
+    int yy = y + dy;
+    yy = yy < 0 ? -yy : (yy >= H ? 2 * H - 2 - yy : yy);
+    for (int dx = -1; dx <= 1; ++dx) {
+      int xx = x + dx;
+      xx = xx < 0 ? -xx : (xx >= W ? 2 * W - 2 - xx : xx);
+      g[dy + 1][dx + 1] = gray_at(low, base, HW, yy * W + xx);
+    }
+  }
+  const float gx = -g[0][0] + g[0][2] - 2.f * g[1][0] + 2.f * g[1][2] - g[2][0] + g[2][2];
+  const float gy = -g[0][0] - 2.f * g[0][1] - g[0][2] + g[2][0] + 2.f * g[2][1] + g[2][2];
+  return sqrtf(gx * gx + gy * gy);
+}
+
+template <int NV>
+__device__ __forceinline__ void block_sum_atomic(double (&v)[NV], double* dst[NV]) {
+  __shared__ double sm[NV][256];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) sm[k][threadIdx.x] = v[k];
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) sm[k][threadIdx.x] += sm[k][threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+      if (dst[k]) atomicAdd(dst[k], sm[k][0]);
+  }
+  __syncthreads();
+}
+
+// pass 1: grid (chunks, B)
+__global__ __launch_bounds__(256) void loss_pass1_kernel(const float* __restrict__ low, const float* __restrict__ enh,
+                                                         const float* __restrict__ illu,
+                                                         const float* __restrict__ refl, int H, int W, LossWS ws) {
+  const int b = blockIdx.y;
+  const int HW = H * W;
+  const size_t base = (size_t)b * 3 * HW;
+  const int per = (HW + gridDim.x - 1) / gridDim.x;
+  const int p0 = blockIdx.x * per, p1 = min(HW, p0 + per);
+  double v[17];
+#pragma unroll
+  for (int k = 0; k < 17; ++k) v[k] = 0.0;
+  const int PW = W / 16;
+  for (int q = p0 + threadIdx.x; q < p1; q += 256) {
+    const int y = q / W, x = q - y * W;
+    float le[3], ll[3];
+    for (int c = 0; c < 3; ++c) { le[c] = enh[base + c * HW + q]; ll[c] = low[base + c * HW + q]; }
+    for (int c = 0; c < 3; ++c) v[c] += le[c];
+    v[9] += (ll[0] + ll[1] + ll[2]) / 3.f;
+    if (x < W - 1) {
+      for (int c = 0; c < 3; ++c) {
+        const float de = le[c] - enh[base + c * HW + q + 1], dl = ll[c] - low[base + c * HW + q + 1];
+        v[3] += (double)(de - dl) * (de - dl);
+        v[7] += fabsf(dl);
+      }
+    }
+    if (y < H - 1) {
+      for (int c = 0; c < 3; ++c) {
+        const float de = le[c] - enh[base + c * HW + q + W], dl = ll[c] - low[base + c * HW + q + W];
+        v[4] += (double)(de - dl) * (de - dl);
+        v[8] += fabsf(dl);
+      }
+    }
+    const float il = illu[(size_t)b * HW + q];
+    v[10] += il;
+    for (int c = 0; c < 3; ++c) {
+      const float r = refl[base + c * HW + q];
+      v[11 + c] += r;
+      v[14 + c] += (double)il * r;
+    }
+    // exposure patches, edge row / column sums (per-pixel atomics on small arrays)
+    const float ge = (le[0] + le[1] + le[2]) / 3.f;
+    atomicAdd(ws.patch + ((size_t)b * (H / 16) + y / 16) * PW + x / 16, (double)ge);
+    const float ed = edge_at(low, base, H, W, y, x);
+    if (x < W - 1) atomicAdd(ws.rowsum + (size_t)b * H + y, (double)ed);
+    if (y < H - 1) atomicAdd(ws.colsum + (size_t)b * W + x, (double)ed);
+  }
+  double* dst[17];
+  for (int k = 0; k < 10; ++k) dst[k] = ws.acc + k;
+  for (int k = 10; k < 17; ++k) dst[k] = nullptr;
+  for (int k = 0; k < 7; ++k) dst[10 + k] = ws.acc + LA_FIXED + b * 7 + k;
+  block_sum_atomic<17>(v, dst);
+}
+
+// pass 2: edge-aware smoothness sums (needs the row / column edge means)
+__global__ __launch_bounds__(256) void loss_pass2_kernel(const float* __restrict__ low, const float* __restrict__ illu,
+                                                         int H, int W, LossWS ws) {
+  const int b = blockIdx.y;
+  const int HW = H * W;
+  const size_t base = (size_t)b * 3 * HW;
+  const int per = (HW + gridDim.x - 1) / gridDim.x;
+  const int p0 = blockIdx.x * per, p1 = min(HW, p0 + per);
+  double v[2] = {0.0, 0.0};
+  for (int q = p0 + threadIdx.x; q < p1; q += 256) {
+    const int y = q / W, x = q - y * W;
+    const float il = illu[(size_t)b * HW + q];
+    if (x < W - 1) {
+      float s = 0.f;
+      for (int c = 0; c < 3; ++c) s += fabsf(low[base + c * HW + q] - low[base + c * HW + q + 1]);
+      const float wh = expf(-10.f * (s / 3.f));
+      const float ef = 1.f + (float)(ws.rowsum[(size_t)b * H + y] / (W - 1));
+      v[0] += wh * ef * fabsf(il - illu[(size_t)b * HW + q + 1]);
+    }
+    if (y < H - 1) {
+      float s = 0.f;
+      for (int c = 0; c < 3; ++c) s += fabsf(low[base + c * HW + q] - low[base + c * HW + q + W]);
+      const float wv = expf(-10.f * (s / 3.f));
+      const float ef = 1.f + (float)(ws.colsum[(size_t)b * W + x] / (H - 1));
+      v[1] += wv * ef * fabsf(il - illu[(size_t)b * HW + q + W]);
+    }
+  }
+  double* dst[2] = {ws.acc + LA_SM_H, ws.acc + LA_SM_V};
+  block_sum_atomic<2>(v, dst);
+}
+
+// finalise: one block
+__global__ void loss_final_kernel(int B, int H, int W, LossWS ws, float* __restrict__ terms) {
+  __shared__ double ex[256];
+  const int HW = H * W;
+  const double N = (double)B * HW;
+  const double T = 0.6 + 0.2 * (1.0 - ws.acc[LA_GLOW] / N);
+  const int NP = B * (H / 16) * (W / 16);
+  double e = 0.0;
+  for (int k = threadIdx.x; k < NP; k += blockDim.x) e += fabs(ws.patch[k] / 256.0 - T);
+  ex[threadIdx.x] = e;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) ex[threadIdx.x] += ex[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  const double nh = (double)B * 3 * H * (W - 1), nv = (double)B * 3 * (H - 1) * W;
+  const double nh1 = (double)B * H * (W - 1), nv1 = (double)B * (H - 1) * W;
+  const double mu0 = ws.acc[0] / N, mu1 = ws.acc[1] / N, mu2 = ws.acc[2] / N;
+  const double col = (mu0 - mu1) * (mu0 - mu1) + (mu0 - mu2) * (mu0 - mu2) + (mu1 - mu2) * (mu1 - mu2);
+  const double spa = ws.acc[LA_SPA_H] / nh + ws.acc[LA_SPA_V] / nv;
+  const double smo = ws.acc[LA_SM_H] / nh1 + ws.acc[LA_SM_V] / nv1;
+  const double tc = ws.acc[LA_TV_H] / nh + ws.acc[LA_TV_V] / nv;
+  double wsm = 1.0 * (1.0 - tc * 0.8);
+  wsm = wsm < 0.1 ? 0.1 : (wsm > 5.0 ? 5.0 : wsm);
+  double frob = 0.0, md = 0.0;
+  for (int b = 0; b < B; ++b) {
+    const double* a = ws.acc + LA_FIXED + b * 7;
+    const double im = a[0] / HW;
+    double rmm = 0.0;
+    for (int j = 0; j < 3; ++j) {
+      const double cov = (a[4 + j] - a[1 + j] * a[0] / HW) / (HW - 1);
+      frob += 3.0 * cov * cov;
+      ws.scal[LS_DEC + b * 5 + j] = (float)cov;
+      rmm += a[1 + j] / HW / 3.0;
+    }
+    md += (im - rmm) * (im - rmm) / B;
+    ws.scal[LS_DEC + b * 5 + 3] = (float)(im - rmm);
+    ws.scal[LS_DEC + b * 5 + 4] = (float)im;
+  }
+  const double dec = frob + 0.1 * md;
+  terms[0] = (float)(ex[0] / NP);
+  terms[1] = (float)smo;
+  terms[2] = (float)col;
+  terms[3] = (float)spa;
+  terms[4] = (float)dec;
+  terms[8] = (float)wsm;
+  ws.scal[LS_T] = (float)T;
+  ws.scal[LS_NPATCH] = (float)NP;
+  ws.scal[LS_WS] = (float)wsm;
+  ws.scal[LS_MU + 0] = (float)mu0;
+  ws.scal[LS_MU + 1] = (float)mu1;
+  ws.scal[LS_MU + 2] = (float)mu2;
+}
+
+// gradient pass: one thread per pixel, overwrites g_enh / g_illu / g_refl
+__global__ __launch_bounds__(256) void loss_grad_kernel(const float* __restrict__ low, const float* __restrict__ enh,
+                                                        const float* __restrict__ illu,
+                                                        const float* __restrict__ refl, int B, int H, int W,
+                                                        LossWS ws, float* __restrict__ g_enh,
+                                                        float* __restrict__ g_illu, float* __restrict__ g_refl,
+                                                        float w_exp, float w_col, float w_spa, float w_dec) {
+  const int HW = H * W;
+  const long long n = (long long)B * HW;
+  const float T = ws.scal[LS_T];
+  const float NP = ws.scal[LS_NPATCH];
+  const float wsm = ws.scal[LS_WS];
+  const float mu0 = ws.scal[LS_MU], mu1 = ws.scal[LS_MU + 1], mu2 = ws.scal[LS_MU + 2];
+  const float N = (float)n;
+  const float dcol[3] = {2.f * (mu0 - mu1) + 2.f * (mu0 - mu2), -2.f * (mu0 - mu1) + 2.f * (mu1 - mu2),
+                         -2.f * (mu0 - mu2) - 2.f * (mu1 - mu2)};
+  const float nh = (float)B * 3 * H * (W - 1), nv = (float)B * 3 * (H - 1) * W;
+  const float nh1 = (float)B * H * (W - 1), nv1 = (float)B * (H - 1) * W;
+  const int PW = W / 16;
+  GSTRIDE(i, n) {
+    const int b = (int)(i / HW), q = (int)(i - (long long)b * HW);
+    const int y = q / W, x = q - y * W;
+    const size_t base = (size_t)b * 3 * HW;
+    // exposure: sign(P - T) / NP / 256 / 3
+    const float P = (float)(ws.patch[((size_t)b * (H / 16) + y / 16) * PW + x / 16] / 256.0);
+    const float dp = P - T;
+    const float gexp = w_exp * (dp > 0.f ? 1.f : (dp < 0.f ? -1.f : 0.f)) / NP / 256.f / 3.f;
+    for (int c = 0; c < 3; ++c) {
+      const size_t k = base + c * HW + q;
+      float g = gexp + w_col * dcol[c] / N;
+      // spatial: d/de of mean((De - Dl)^2), horizontal and vertical
+      const float e0 = enh[k], l0 = low[k];
+      if (x < W - 1) g += w_spa * 2.f * ((e0 - enh[k + 1]) - (l0 - low[k + 1])) / nh;
+      if (x > 0) g -= w_spa * 2.f * ((enh[k - 1] - e0) - (low[k - 1] - l0)) / nh;
+      if (y < H - 1) g += w_spa * 2.f * ((e0 - enh[k + W]) - (l0 - low[k + W])) / nv;
+      if (y > 0) g -= w_spa * 2.f * ((enh[k - W] - e0) - (low[k - W] - l0)) / nv;
+      g_enh[k] = g;
+    }
+    // smoothness on illumination (weight wsm)
+    const size_t ii = (size_t)b * HW + q;
+    const float il = illu[ii];
+    float gi = 0.f;
+    auto sgn = [](float v) { return v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f); };
+    auto wgt = [&](int qa, int qb) {
+      float s = 0.f;
+      for (int c = 0; c < 3; ++c) s += fabsf(low[base + c * HW + qa] - low[base + c * HW + qb]);
+      return expf(-10.f * (s / 3.f));
+    };
+    const float efh = 1.f + (float)(ws.rowsum[(size_t)b * H + y] / (W - 1));
+    if (x < W - 1) gi += wgt(q, q + 1) * efh * sgn(il - illu[ii + 1]) / nh1;
+    if (x > 0) gi -= wgt(q - 1, q) * efh * sgn(illu[ii - 1] - il) / nh1;
+    if (y < H - 1) gi += wgt(q, q + W) * (1.f + (float)(ws.colsum[(size_t)b * W + x] / (H - 1))) *
+                         sgn(il - illu[ii + W]) / nv1;
+    if (y > 0) gi -= wgt(q - W, q) * (1.f + (float)(ws.colsum[(size_t)b * W + x] / (H - 1))) *
+                     sgn(illu[ii - W] - il) / nv1;
+    gi *= wsm;
+    // decoupling: 3*sum_j cov_j^2 + 0.1*(imean - rmean)^2 / B
+    const float* sc = ws.scal + LS_DEC + b * 5;
+    const float md = sc[3], imean = sc[4];
+    const float inv = 1.f / (float)(HW - 1);
+    const double* a = ws.acc + LA_FIXED + b * 7;
+    float gd = 0.f;
+    for (int j = 0; j < 3; ++j) {
+      const float rmj = (float)(a[1 + j] / HW);
+      const float r = refl[base + j * HW + q];
+      gd += 6.f * sc[j] * (r - rmj) * inv;
+      g_refl[base + j * HW + q] = w_dec * (6.f * sc[j] * (il - imean) * inv - 0.1f * 2.f * md / (B * 3.f * HW));
+    }
+    gd += 0.1f * 2.f * md / ((float)B * HW);
+    g_illu[ii] = gi + w_dec * gd;
+  }
+}
+
+__global__ void loss_total_kernel(float* t, float we, float wc, float wsp, float wd, float wp, float wf) {
+  if (threadIdx.x == 0)
+    t[7] = we * t[0] + t[8] * t[1] + wc * t[2] + wsp * t[3] + wd * t[4] + wp * t[5] + wf * t[6];
+}
+
+__global__ __launch_bounds__(256) void mse_kernel(const float* __restrict__ a, const float* __restrict__ b, long long n,
+                                                  double* acc, float* g, float scale) {
+  double v[1] = {0.0};
+  GSTRIDE(i, n) {
+    const float d = a[i] - b[i];
+    v[0] += (double)d * d;
+    if (g) g[i] = scale * 2.f * d;
+  }
+  v[0] /= (double)n;
+  double* dst[1] = {acc};
+  block_sum_atomic<1>(v, dst);
+}
+
+__constant__ float kVggMean[3] = {0.485f, 0.456f, 0.406f};
+__constant__ float kVggStd[3] = {0.229f, 0.224f, 0.225f};
+
+__global__ void vgg_norm_kernel(const float* __restrict__ x, float* __restrict__ y, int B, int HW) {
+  const long long n = (long long)B * HW;
+  GSTRIDE(i, n) {
+    const int b = (int)(i / HW), p = (int)(i - (long long)b * HW);
+    for (int c = 0; c < 3; ++c) y[i * 3 + c] = (x[((size_t)b * 3 + c) * HW + p] - kVggMean[c]) / kVggStd[c];
+  }
+}
+
+__global__ void vgg_norm_bwd_kernel(const float* __restrict__ gy, float* __restrict__ gx, int B, int HW) {
+  const long long n = (long long)B * HW;
+  GSTRIDE(i, n) {
+    const int b = (int)(i / HW), p = (int)(i - (long long)b * HW);
+    for (int c = 0; c < 3; ++c) gx[((size_t)b * 3 + c) * HW + p] += gy[i * 3 + c] / kVggStd[c];
+  }
+}
+
+__global__ __launch_bounds__(256) void freq_kernel(const float2* __restrict__ ze, const float2* __restrict__ zl, int BC,
+                                                   int H, int W, double* acc, float2* G, float scale) {
+  const long long n = (long long)BC * H * W;
+  const int ch = H / 2, cw = W / 2, rad = min(H, W) / 4;
+  double v[1] = {0.0};
+  GSTRIDE(i, n) {
+    const int q = (int)(i % ((long long)H * W));
+    const int y = q / W, x = q - y * W;
+    const float dist = sqrtf((float)((x - cw) * (x - cw)) + (float)((y - ch) * (y - ch)));
+    const float w = dist <= (float)rad ? 0.5f : 1.f;
+    const float2 a = ze[i], c = zl[i];
+    const float me = sqrtf(a.x * a.x + a.y * a.y), ml = sqrtf(c.x * c.x + c.y * c.y);
+    const float d = me - ml;
+    v[0] += (double)w * d * d;
+    if (G) {
+      const float k = me > 0.f ? scale * 2.f * w * d / me : 0.f;
+      G[i] = make_float2(k * a.x, k * a.y);
+    }
+  }
+  double* dst[1] = {acc};
+  block_sum_atomic<1>(v, dst);
+}
+
+__global__ void add_real_kernel(const float2* __restrict__ z, float* g, long long n, float scale) {
+  GSTRIDE(i, n) g[i] += scale * z[i].x;
+}
+
+__global__ void scale_acc_kernel(const double* __restrict__ acc, int n, float scale, float* out) {
+  const int i = threadIdx.x;
+  if (i < n) out[i] = (float)(acc[i] * scale);
+}
+
+// ---------------------------------------------------------------------------
+// optimiser
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sqsum_kernel(const float* __restrict__ g, long long n, double* acc) {
+  double v[1] = {0.0};
+  GSTRIDE(i, n) v[0] += (double)g[i] * g[i];
+  double* dst[1] = {acc};
+  block_sum_atomic<1>(v, dst);
+}
+
+__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, long long n, const double* __restrict__ sq, float max_norm,
+                            float lr, float b1, float b2, float eps, float wd, float bc1, float bc2s,
+                            float* norm_out) {
+  const float norm = (float)sqrt(*sq);
+  float coef = 1.f;
+  if (max_norm > 0.f) coef = fminf(max_norm / (norm + 1e-6f), 1.f);
+  if (norm_out && blockIdx.x == 0 && threadIdx.x == 0) *norm_out = norm;
+  const float step = lr / bc1;
+  GSTRIDE(i, n) {
+    const float pv = p[i];
+    const float gv = g[i] * coef + wd * pv;
+    const float mv = b1 * m[i] + (1.f - b1) * gv;
+    const float vv = b2 * v[i] + (1.f - b2) * gv * gv;
+    m[i] = mv;
+    v[i] = vv;
+    p[i] = pv - step * mv / (sqrtf(vv) / bc2s + eps);
+  }
+}
+
+}  // namespace upr
+
+using namespace upr;
+
+#define ST(s) ((hipStream_t)(s))
+
+extern "C" {
+
+int upr_t_zero(void* p, size_t bytes, void* stream) {
+  if (!p && bytes) return UPR_ERR_ARG;
+  if (!bytes) return UPR_OK;
+  return (int)hipMemsetAsync(p, 0, bytes, ST(stream));
+}
+
+int upr_t_conv_direct(const UprView* x, int B, int H, int W, int Cin, const float* w, const float* bias, int Cout,
+                      int kh, int kw, int stride, int pad, int dil, const UprView* y, int Ho, int Wo, int relu,
+                      int accumulate, void* stream) {
+  if (!x || !y || !x->data || !y->data || !w || B <= 0 || Cin <= 0 || Cout <= 0 || stride <= 0 || dil <= 0)
+    return UPR_ERR_ARG;
+  if (Ho != (H + 2 * pad - dil * (kh - 1) - 1) / stride + 1 || Wo != (W + 2 * pad - dil * (kw - 1) - 1) / stride + 1)
+    return UPR_ERR_SHAPE;
+  const long long n = (long long)B * Ho * Wo * Cout;
+  hipLaunchKernelGGL(conv_direct_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), mkv(x), B, H, W, Cin, w, bias,
+                     Cout, kh, kw, stride, pad, dil, mkv(y), Ho, Wo, relu, accumulate);
+  LAUNCH_CHECK();
+}
+
+int upr_t_conv_direct_dgrad(const UprView* dy, int Ho, int Wo, const float* w, int B, int H, int W, int Cin, int Cout,
+                            int kh, int kw, int stride, int pad, int dil, const UprView* dx, int accumulate,
+                            void* stream) {
+  if (!dy || !dx || !dy->data || !dx->data || !w || B <= 0 || stride <= 0 || dil <= 0) return UPR_ERR_ARG;
+  const long long n = (long long)B * H * W * Cin;
+  hipLaunchKernelGGL(conv_direct_dgrad_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), mkv(dy), Ho, Wo, w, B, H,
+                     W, Cin, Cout, kh, kw, stride, pad, dil, mkv(dx), accumulate);
+  LAUNCH_CHECK();
+}
+
+int upr_t_conv_direct_wgrad(const UprView* x, const UprView* dy, int B, int H, int W, int Cin, int Ho, int Wo,
+                            int Cout, int kh, int kw, int stride, int pad, int dil, float* dw, float* dbias,
+                            void* stream) {
+  if (!x || !dy || !dw || B <= 0) return UPR_ERR_ARG;
+  const int KC = kh * kw * Cin;
+  const int nE = Cout * KC + (dbias ? Cout : 0);
+  if (nE > 16 * 256) return UPR_ERR_UNSUPPORTED;
+  int CH = 12288 / (Cout + KC);
+  if (CH > 64) CH = 64;
+  if (CH < 1) return UPR_ERR_UNSUPPORTED;
+  const long long P = (long long)B * Ho * Wo;
+  const int grid = grid_for(P, CH, 1024);
+  const size_t lds = sizeof(float) * CH * (Cout + KC);
+  hipLaunchKernelGGL(conv_direct_wgrad_kernel, dim3(grid), dim3(256), lds, ST(stream), mkv(x), mkv(dy), B, H, W, Cin,
+                     Ho, Wo, Cout, kh, kw, stride, pad, dil, CH, dw, dbias);
+  LAUNCH_CHECK();
+}
+
+int upr_t_conv_mfma(const float* x, int B, int H, int W, int Cin, int x_cs, int x_coff, const float* wp,
+                    const float* bias, int N, int kh, int kw, int stride, int pad, int dil, const float* res,
+                    int res_cs, int relu, float* y, int y_cs, int y_coff, int store, void* stream) {
+  if (!x || !wp || !y || B <= 0 || Cin % 32 || N % 32 || Cin <= 0 || N <= 0) return UPR_ERR_ARG;
+  if (kh <= 0 || kw <= 0 || stride <= 0 || dil <= 0 || pad < 0) return UPR_ERR_ARG;
+  if (x_cs % 4 || x_coff % 4 || y_cs % 4 || y_coff % 4 || (res && res_cs % 4)) return UPR_ERR_ARG;
+  if (store == 1 && ((N / 4) % 32)) return UPR_ERR_SHAPE;
+  const int Ho = (H + 2 * pad - dil * (kh - 1) - 1) / stride + 1;
+  const int Wo = (W + 2 * pad - dil * (kw - 1) - 1) / stride + 1;
+  if (Ho <= 0 || Wo <= 0) return UPR_ERR_SHAPE;
+  ConvOp c;
+  memset(&c, 0, sizeof(c));
+  c.nseg = 1;
+  ConvSeg& s = c.seg[0];
+  s.src = x; s.C = Cin; s.cs = x_cs; s.coff = x_coff; s.Hin = H; s.Win = W;
+  s.kh = kh; s.kw = kw; s.stride = stride; s.pad = pad; s.dil = dil; s.pre = kPreNone; s.kbase = 0;
+  c.B = B; c.Ho = Ho; c.Wo = Wo; c.N = N; c.Kpad = kh * kw * Cin;
+  c.W = wp; c.bias = bias; c.res1 = res; c.res1_cs = res_cs; c.relu = relu;
+  c.out = y; c.out_cs = y_cs; c.out_coff = y_coff; c.store = store == 1 ? kStoreConvT2x2 : kStoreNHWC;
+  return launch_conv(c, kF32, ST(stream));
+}
+
+int upr_t_conv_wgrad(const float* x, int B, int H, int W, int Cin, int x_cs, int x_coff, const float* dy, int Ho,
+                     int Wo, int Cout, int dy_cs, int dy_coff, int kh, int kw, int stride, int pad, int dil,
+                     float* dwp, void* stream) {
+  if (!x || !dy || !dwp || B <= 0 || Cin % 32 || Cout % 32 || Cin <= 0 || Cout <= 0) return UPR_ERR_ARG;
+  const long long P = (long long)B * Ho * Wo;
+  const long long chunks = (P + WG_PPB - 1) / WG_PPB;
+  if (chunks > 0x7fffffff) return UPR_ERR_SHAPE;
+  dim3 grid((unsigned)chunks, Cout / 32, kh * kw * (Cin / 32));
+  hipLaunchKernelGGL(conv_wgrad_kernel, grid, dim3(256), 0, ST(stream), x, B, H, W, Cin, x_cs, x_coff, dy, Ho, Wo,
+                     Cout, dy_cs, dy_coff, kh, kw, stride, pad, dil, dwp);
+  LAUNCH_CHECK();
+}
+
+int upr_t_pack_weight(const float* w, float* out, int Co, int Ci, int kh, int kw, int mode, void* stream) {
+  if (!w || !out || Co <= 0 || Ci <= 0 || mode < 0 || mode > 3) return UPR_ERR_ARG;
+  if (mode >= 2 && (kh != 2 || kw != 2)) return UPR_ERR_SHAPE;
+  const long long n = (long long)Co * Ci * kh * kw;
+  hipLaunchKernelGGL(pack_weight_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), w, out, Co, Ci, kh, kw, mode);
+  LAUNCH_CHECK();
+}
+
+int upr_t_unpack_grad(const float* gp, float* g, int Co, int Ci, int kh, int kw, int mode, int accumulate,
+                      void* stream) {
+  if (!gp || !g || (mode != 0 && mode != 3)) return UPR_ERR_ARG;
+  const long long n = (long long)Co * Ci * kh * kw;
+  hipLaunchKernelGGL(unpack_grad_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), gp, g, Co, Ci, kh, kw, mode,
+                     accumulate);
+  LAUNCH_CHECK();
+}
+
+int upr_t_zero_upsample(const float* dy, int B, int Ho, int Wo, int C, int dy_cs, int dy_coff, float* z,
+                        void* stream) {
+  if (!dy || !z) return UPR_ERR_ARG;
+  const long long n = (long long)B * 4 * Ho * Wo * C;
+  hipLaunchKernelGGL(zero_upsample_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), dy, B, Ho, Wo, C, dy_cs,
+                     dy_coff, z);
+  LAUNCH_CHECK();
+}
+
+int upr_t_bn_stats(const float* x, int M, int C, int cs, int coff, double* acc, void* stream) {
+  if (!x || !acc || M <= 0 || C <= 0) return UPR_ERR_ARG;
+  hipLaunchKernelGGL(chan_reduce_kernel, dim3(reduce_grid(M)), dim3(256), 0, ST(stream), x, cs, coff, nullptr, 0, 0,
+                     nullptr, nullptr, M, C, 0, acc, nullptr);
+  LAUNCH_CHECK();
+}
+
+int upr_t_bn_finalize(const double* acc, int M, int C, float momentum, float eps, float* running_mean,
+                      float* running_var, int64_t* nbt, float* mean, float* invstd, void* stream) {
+  if (!acc || !mean || !invstd || M <= 0) return UPR_ERR_ARG;
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, ST(stream), acc, M, C, momentum, eps,
+                     running_mean, running_var, (long long*)nbt, mean, invstd);
+  LAUNCH_CHECK();
+}
+
+int upr_t_bn_apply(const float* x, int M, int C, int x_cs, int x_coff, const float* mean, const float* invstd,
+                   const float* gamma, const float* beta, const float* res, int res_cs, int res_coff, int res_post,
+                   int relu, float* y, int y_cs, int y_coff, void* stream) {
+  if (!x || !y || !mean || !invstd || !gamma || !beta) return UPR_ERR_ARG;
+  const long long n = (long long)M * C;
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), x, M, C, x_cs, x_coff, mean,
+                     invstd, gamma, beta, res, res_cs, res_coff, res_post, relu, y, y_cs, y_coff);
+  LAUNCH_CHECK();
+}
+
+int upr_t_bn_bwd_reduce(const float* g, int g_cs, int g_coff, const float* x, int x_cs, int x_coff, const float* mean,
+                        const float* invstd, int M, int C, double* acc, void* stream) {
+  if (!g || !x || !acc) return UPR_ERR_ARG;
+  hipLaunchKernelGGL(chan_reduce_kernel, dim3(reduce_grid(M)), dim3(256), 0, ST(stream), g, g_cs, g_coff, x, x_cs,
+                     x_coff, mean, invstd, M, C, 1, acc, nullptr);
+  LAUNCH_CHECK();
+}
+
+int upr_t_bn_bwd_apply(const float* g, int g_cs, int g_coff, const float* x, int x_cs, int x_coff, const float* mean,
+                       const float* invstd, const float* gamma, const double* acc, int M, int C, float* dgamma,
+                       float* dbeta, float* dx, int dx_cs, int dx_coff, int accumulate, void* stream) {
+  if (!g || !x || !acc || !dx || !gamma) return UPR_ERR_ARG;
+  const long long n = (long long)M * C;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), g, g_cs, g_coff, x, x_cs,
+                     x_coff, mean, invstd, gamma, acc, M, C, dgamma, dbeta, dx, dx_cs, dx_coff, accumulate);
+  LAUNCH_CHECK();
+}
+
+int upr_t_chan_sum(const float* g, int M, int C, int cs, int coff, float* out, int accumulate, void* stream) {
+  if (!g || !out) return UPR_ERR_ARG;
+  if (!accumulate) UPR_CHECK_HIP(hipMemsetAsync(out, 0, sizeof(float) * C, ST(stream)));
+  hipLaunchKernelGGL(chan_reduce_kernel, dim3(reduce_grid(M)), dim3(256), 0, ST(stream), g, cs, coff, nullptr, 0, 0,
+                     nullptr, nullptr, M, C, 2, nullptr, out);
+  LAUNCH_CHECK();
+}
+
+int upr_t_relu_mask(float* g, int g_cs, int g_coff, const float* y, int y_cs, int y_coff, int M, int C,
+                    void* stream) {
+  if (!g || !y) return UPR_ERR_ARG;
+  const long long n = (long long)M * C;
+  hipLaunchKernelGGL(relu_mask_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), g, g_cs, g_coff, y, y_cs, y_coff,
+                     M, C);
+  LAUNCH_CHECK();
+}
+
+int upr_t_copy(const UprView* src, const UprView* dst, int B, int H, int W, int C, int accumulate, void* stream) {
+  if (!src || !dst || !src->data || !dst->data) return UPR_ERR_ARG;
+  const long long n = (long long)B * H * W * C;
+  hipLaunchKernelGGL(copy_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), mkv(src), mkv(dst), B, H, W, C,
+                     accumulate);
+  LAUNCH_CHECK();
+}
+
+int upr_t_pointwise(const float* a, const float* b, float* out, size_t n, int op, const uint8_t* mask_in,
+                    uint8_t* mask_out, float p, uint64_t seed, void* stream) {
+  if (!a || !out || op < 0 || op > 5) return UPR_ERR_ARG;
+  if ((op == 1 || op == 4 || op == 5) && !b) return UPR_ERR_ARG;
+  if ((op == 2 && !mask_out) || (op == 3 && !mask_in)) return UPR_ERR_ARG;
+  if (n == 0) return UPR_OK;
+  hipLaunchKernelGGL(pointwise_kernel, dim3(grid_for((long long)n)), dim3(256), 0, ST(stream), a, b, out,
+                     (long long)n, op, mask_in, mask_out, p, (unsigned long long)seed);
+  LAUNCH_CHECK();
+}
+
+int upr_t_maxpool(const UprView* x, int B, int H, int W, int C, int k, int s, int p, const UprView* y, int Ho, int Wo,
+                  void* stream) {
+  if (!x || !y || k <= 0 || s <= 0) return UPR_ERR_ARG;
+  const long long n = (long long)B * Ho * Wo * C;
+  hipLaunchKernelGGL(maxpool_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), mkv(x), B, H, W, C, k, s, p, mkv(y),
+                     Ho, Wo);
+  LAUNCH_CHECK();
+}
+
+int upr_t_maxpool_bwd(const UprView* x, const UprView* dy, int B, int H, int W, int C, int k, int s, int p, int Ho,
+                      int Wo, const UprView* dx, void* stream) {
+  if (!x || !dy || !dx || k <= 0 || s <= 0) return UPR_ERR_ARG;
+  const long long n = (long long)B * Ho * Wo * C;
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), mkv(x), mkv(dy), B, H, W, C, k,
+                     s, p, Ho, Wo, mkv(dx));
+  LAUNCH_CHECK();
+}
+
+int upr_t_bilinear(const UprView* x, int B, int H, int W, int C, const UprView* y, int Ho, int Wo, int accumulate,
+                   void* stream) {
+  if (!x || !y || Ho <= 0 || Wo <= 0) return UPR_ERR_ARG;
+  const long long n = (long long)B * Ho * Wo * C;
+  hipLaunchKernelGGL(bilinear_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), mkv(x), B, H, W, C, mkv(y), Ho, Wo,
+                     (float)H / Ho, (float)W / Wo, accumulate);
+  LAUNCH_CHECK();
+}
+
+int upr_t_bilinear_bwd(const UprView* dy, int B, int H, int W, int C, int Ho, int Wo, const UprView* dx,
+                       void* stream) {
+  if (!dy || !dx) return UPR_ERR_ARG;
+  const long long n = (long long)B * Ho * Wo * C;
+  hipLaunchKernelGGL(bilinear_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), mkv(dy), B, H, W, C, Ho, Wo,
+                     (float)H / Ho, (float)W / Wo, mkv(dx));
+  LAUNCH_CHECK();
+}
+
+int upr_t_pixel_sum(const float* x, int B, int HW, int C, int cs, int coff, float scale, float* out, int accumulate,
+                    void* stream) {
+  if (!x || !out || B <= 0 || HW <= 0) return UPR_ERR_ARG;
+  if (!accumulate) UPR_CHECK_HIP(hipMemsetAsync(out, 0, sizeof(float) * B * C, ST(stream)));
+  int chunks = HW / 2048;
+  chunks = chunks < 1 ? 1 : (chunks > 256 ? 256 : chunks);
+  hipLaunchKernelGGL(pixel_sum_kernel, dim3(chunks, B), dim3(256), 0, ST(stream), x, HW, C, cs, coff, scale, out);
+  LAUNCH_CHECK();
+}
+
+int upr_t_broadcast(const float* v, int B, int HW, int C, float scale, float* y, int y_cs, int y_coff, int accumulate,
+                    void* stream) {
+  if (!v || !y) return UPR_ERR_ARG;
+  const long long n = (long long)B * HW * C;
+  hipLaunchKernelGGL(broadcast_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), v, B, HW, C, scale, y, y_cs,
+                     y_coff, accumulate);
+  LAUNCH_CHECK();
+}
+
+int upr_t_fam_ca_apply(const float* o, const float* ca, int B, int HW, int C, float* o2, float* m, void* stream) {
+  if (!o || !ca || !o2 || !m) return UPR_ERR_ARG;
+  hipLaunchKernelGGL(fam_ca_apply_kernel, dim3(grid_for((long long)B * HW)), dim3(256), 0, ST(stream), o, ca, B, HW,
+                     C, o2, m);
+  LAUNCH_CHECK();
+}
+
+int upr_t_fam_sa_apply(const float* o2, const float* s_pre, int B, int HW, int C, float* sa, float* out,
+                       void* stream) {
+  if (!o2 || !s_pre || !sa || !out) return UPR_ERR_ARG;
+  hipLaunchKernelGGL(fam_sa_apply_kernel, dim3(grid_for((long long)B * HW)), dim3(256), 0, ST(stream), o2, s_pre, B,
+                     HW, C, sa, out);
+  LAUNCH_CHECK();
+}
+
+int upr_t_fam_sa_bwd(const float* g, const float* o2, const float* sa, int B, int HW, int C, float* g_o2,
+                     float* g_spre, void* stream) {
+  if (!g || !o2 || !sa || !g_o2 || !g_spre) return UPR_ERR_ARG;
+  hipLaunchKernelGGL(fam_sa_bwd_kernel, dim3(grid_for((long long)B * HW)), dim3(256), 0, ST(stream), g, o2, sa, B,
+                     HW, C, g_o2, g_spre);
+  LAUNCH_CHECK();
+}
+
+int upr_t_fam_ca_bwd(const float* g_o2, const float* g_m, const float* o, const float* o2, const float* ca, int B,
+                     int HW, int C, float* g_o, float* g_ca, void* stream) {
+  if (!g_o2 || !g_m || !o || !o2 || !ca || !g_o || !g_ca || C > 32) return UPR_ERR_ARG;
+  UPR_CHECK_HIP(hipMemsetAsync(g_ca, 0, sizeof(float) * B * C, ST(stream)));
+  int chunks = HW / 4096;
+  chunks = chunks < 1 ? 1 : (chunks > 256 ? 256 : chunks);
+  hipLaunchKernelGGL(fam_ca_bwd_kernel, dim3(chunks, B), dim3(256), 0, ST(stream), g_o2, g_m, o, o2, ca, HW, C, g_o,
+                     g_ca);
+  LAUNCH_CHECK();
+}
+
+int upr_t_fam_pool_bwd(float* g_o, const float* g_pool, const float* o, int B, int HW, int C, void* stream) {
+  if (!g_o || !g_pool || !o) return UPR_ERR_ARG;
+  const long long n = (long long)B * HW * C;
+  hipLaunchKernelGGL(fam_pool_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), g_o, g_pool, o, B, HW, C);
+  LAUNCH_CHECK();
+}
+
+int upr_t_head_fwd(const float* x, const float* r, float* illu, int B, int H, int W, void* stream) {
+  if (!x || !r || !illu) return UPR_ERR_ARG;
+  hipLaunchKernelGGL(head_fwd_kernel, dim3(grid_for((long long)B * H * W)), dim3(256), 0, ST(stream), x, r, illu, B,
+                     H * W);
+  LAUNCH_CHECK();
+}
+
+int upr_t_retinex_fwd(const float* x, const float* illu, const float* o, float* e, float* refl, float* enh, int B,
+                      int H, int W, void* stream) {
+  if (!x || !illu || !o || !e || !refl || !enh) return UPR_ERR_ARG;
+  hipLaunchKernelGGL(retinex_fwd_kernel, dim3(grid_for((long long)B * H * W)), dim3(256), 0, ST(stream), x, illu, o,
+                     e, refl, enh, B, H * W);
+  LAUNCH_CHECK();
+}
+
+int upr_t_retinex_bwd(const float* x, const float* illu, const float* e, const float* refl, const float* g_enh,
+                      const float* g_refl, const float* g_illu, float* g_o, float* g_r, int B, int H, int W,
+                      void* stream) {
+  if (!x || !illu || !e || !refl || !g_enh || !g_o || !g_r) return UPR_ERR_ARG;
+  hipLaunchKernelGGL(retinex_bwd_kernel, dim3(grid_for((long long)B * H * W)), dim3(256), 0, ST(stream), x, illu, e,
+                     refl, g_enh, g_refl, g_illu, g_o, g_r, B, H * W);
+  LAUNCH_CHECK();
+}
+
+size_t upr_t_loss_workspace(int B, int H, int W) {
+  if (B <= 0 || H < 16 || W < 16) return 0;
+  return loss_ws_bytes(B, H, W);
+}
+
+int upr_t_loss_pixel(const float* low, const float* enh, const float* illu, const float* refl, int B, int H, int W,
+                     void* ws, float* terms, float* g_enh, float* g_illu, float* g_refl, int grads, float w_exp,
+                     float w_col, float w_spa, float w_dec, void* stream) {
+  if (!low || !enh || !illu || !refl || !ws || !terms || B <= 0) return UPR_ERR_ARG;
+  if (H % 16 || W % 16 || H < 16 || W < 16) return UPR_ERR_SHAPE;
+  if (grads && (!g_enh || !g_illu || !g_refl)) return UPR_ERR_ARG;
+  hipStream_t st = ST(stream);
+  const size_t zero_bytes = loss_ws_bytes(B, H, W) - align_up(sizeof(float) * (64 + 8 * B), 256);
+  UPR_CHECK_HIP(hipMemsetAsync(ws, 0, zero_bytes, st));
+  LossWS l = loss_ws(ws, B, H, W);
+  int chunks = (H * W) / 4096;
+  chunks = chunks < 1 ? 1 : (chunks > 128 ? 128 : chunks);
+  hipLaunchKernelGGL(loss_pass1_kernel, dim3(chunks, B), dim3(256), 0, st, low, enh, illu, refl, H, W, l);
+  UPR_CHECK_HIP(hipGetLastError());
+  hipLaunchKernelGGL(loss_pass2_kernel, dim3(chunks, B), dim3(256), 0, st, low, illu, H, W, l);
+  UPR_CHECK_HIP(hipGetLastError());
+  hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(256), 0, st, B, H, W, l, terms);
+  UPR_CHECK_HIP(hipGetLastError());
+  if (grads) {
+    hipLaunchKernelGGL(loss_grad_kernel, dim3(grid_for((long long)B * H * W)), dim3(256), 0, st, low, enh, illu, refl,
+                       B, H, W, l, g_enh, g_illu, g_refl, w_exp, w_col, w_spa, w_dec);
+  }
+  LAUNCH_CHECK();
+}
+
+int upr_t_loss_total(float* terms, float w_exp, float w_col, float w_spa, float w_dec, float w_per, float w_freq,
+                     void* stream) {
+  if (!terms) return UPR_ERR_ARG;
+  hipLaunchKernelGGL(loss_total_kernel, dim3(1), dim3(64), 0, ST(stream), terms, w_exp, w_col, w_spa, w_dec, w_per,
+                     w_freq);
+  LAUNCH_CHECK();
+}
+
+int upr_t_mse(const float* a, const float* b, size_t n, double* acc, float* g, float scale, void* stream) {
+  if (!a || !b || !acc) return UPR_ERR_ARG;
+  hipLaunchKernelGGL(mse_kernel, dim3(grid_for((long long)n, 256, 4096)), dim3(256), 0, ST(stream), a, b,
+                     (long long)n, acc, g, scale);
+  LAUNCH_CHECK();
+}
+
+int upr_t_vgg_norm(const float* x, float* y, int B, int H, int W, void* stream) {
+  if (!x || !y) return UPR_ERR_ARG;
+  hipLaunchKernelGGL(vgg_norm_kernel, dim3(grid_for((long long)B * H * W)), dim3(256), 0, ST(stream), x, y, B, H * W);
+  LAUNCH_CHECK();
+}
+
+int upr_t_vgg_norm_bwd(const float* g_y, float* g_x, int B, int H, int W, void* stream) {
+  if (!g_y || !g_x) return UPR_ERR_ARG;
+  hipLaunchKernelGGL(vgg_norm_bwd_kernel, dim3(grid_for((long long)B * H * W)), dim3(256), 0, ST(stream), g_y, g_x, B,
+                     H * W);
+  LAUNCH_CHECK();
+}
+
+int upr_t_freq(const float* Ze, const float* Zl, int BC, int H, int W, double* acc, float* G, float scale,
+               void* stream) {
+  if (!Ze || !Zl || !acc) return UPR_ERR_ARG;
+  hipLaunchKernelGGL(freq_kernel, dim3(grid_for((long long)BC * H * W, 256, 4096)), dim3(256), 0, ST(stream),
+                     (const float2*)Ze, (const float2*)Zl, BC, H, W, acc, (float2*)G, scale);
+  LAUNCH_CHECK();
+}
+
+int upr_t_add_real(const float* z, float* g, size_t n, float scale, void* stream) {
+  if (!z || !g) return UPR_ERR_ARG;
+  hipLaunchKernelGGL(add_real_kernel, dim3(grid_for((long long)n)), dim3(256), 0, ST(stream), (const float2*)z, g,
+                     (long long)n, scale);
+  LAUNCH_CHECK();
+}
+
+int upr_t_scale_acc(const double* acc, int n, float scale, float* out, void* stream) {
+  if (!acc || !out || n <= 0 || n > 256) return UPR_ERR_ARG;
+  hipLaunchKernelGGL(scale_acc_kernel, dim3(1), dim3(256), 0, ST(stream), acc, n, scale, out);
+  LAUNCH_CHECK();
+}
+
+int upr_t_sqsum(const float* g, size_t n, double* acc, void* stream) {
+  if (!g || !acc) return UPR_ERR_ARG;
+  hipLaunchKernelGGL(sqsum_kernel, dim3(grid_for((long long)n, 256, 2048)), dim3(256), 0, ST(stream), g,
+                     (long long)n, acc);
+  LAUNCH_CHECK();
+}
+
+int upr_t_adam(float* p, const float* g, float* m, float* v, size_t n, const double* sqsum, float max_norm, float lr,
+               float beta1, float beta2, float eps, float weight_decay, int step, float* norm_out, void* stream) {
+  if (!p || !g || !m || !v || !sqsum || step <= 0) return UPR_ERR_ARG;
+  const float bc1 = 1.f - powf(beta1, (float)step);
+  const float bc2s = sqrtf(1.f - powf(beta2, (float)step));
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for((long long)n)), dim3(256), 0, ST(stream), p, g, m, v, (long long)n,
+                     sqsum, max_norm, lr, beta1, beta2, eps, weight_decay, bc1, bc2s, norm_out);
+  LAUNCH_CHECK();
+}
+
+}  // extern "C"

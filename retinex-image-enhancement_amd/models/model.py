@@ -6,8 +6,10 @@ those of the reference (models/model.py:11-464), so
 values) and checkpoints load unchanged.  Execution is not PyTorch's: on a ROCm
 device `MultiScaleUP_Retinex.forward` / `ResidualIENet.forward` run the fused
 gfx950 kernel graph of libupr.so (BatchNorm folded, implicit-GEMM MFMA convs,
-fused FAM attention and Retinex tail).  There is no eager fallback: CPU tensors,
-training mode and the fused submodules' own forward() raise.
+fused FAM attention and Retinex tail).  In training mode the forward runs the
+HIP training engine (upr/train.py: batch-statistics BatchNorm, Dropout, an
+explicit backward reached through `loss.backward()`).  There is no eager
+fallback: CPU tensors and the fused submodules' own forward() raise.
 """
 import torch
 import torch.nn as nn
@@ -127,7 +129,8 @@ class _HipGraphMixin:
     _key_prefix = ""
 
     def _signature(self):
-        return tuple((t.data_ptr(), t._version) for t in self.state_dict().values())
+        from upr.autograd import weights_epoch
+        return (weights_epoch(),) + tuple((t.data_ptr(), t._version) for t in self.state_dict().values())
 
     def _run_hip(self, x):
         if not isinstance(x, torch.Tensor) or x.device.type != "cuda":
@@ -136,9 +139,12 @@ class _HipGraphMixin:
                 f"{type(self).__name__}.forward: input on '{dev}'. This framework executes UP-Retinex only on "
                 f"ROCm devices (gfx950 HIP kernels, no CPU path): use model.to('cuda') and a 'cuda' tensor.")
         if self.training:
-            raise NotImplementedError(
-                f"{type(self).__name__}: training-mode forward (batch-stat BatchNorm, Dropout, autograd) is not "
-                f"implemented on the HIP path yet; call .eval() for inference")
+            if self._ienet_only:
+                raise NotImplementedError(
+                    "ResidualIENet: standalone training-mode forward is not provided; train the full "
+                    "MultiScaleUP_Retinex (trainers/train.py) or call .eval()")
+            from upr.autograd import model_train_forward
+            return model_train_forward(self, x)
         key = (x.device, x.dtype)
         sig = self._signature()
         cache = self.__dict__.setdefault("_upr_cache", {})

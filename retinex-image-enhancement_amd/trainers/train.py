@@ -1,0 +1,54 @@
+"""UP-Retinex training step (drop-in for the reference trainers/train.py:27-131).
+
+`train_one_epoch` keeps the reference's signature and step order
+(zero_grad -> forward -> TotalLoss -> backward -> clip_grad_norm_(1.0) ->
+Adam.step()); the model, loss and optimiser it is handed run on the gfx950
+training kernels: `make_optimizer` builds upr.optim.Adam (flat-buffer fused
+clip + Adam), and `clip_grad_norm_` is upr.optim's.  `use_amp` is accepted
+and the step computes in fp32 (mixed-precision training kernels are the next
+scope row; the fp32 step is numerically the reference's no-AMP branch).
+"""
+import time
+
+import torch
+
+from upr import optim as uoptim
+
+clip_grad_norm_ = uoptim.clip_grad_norm_
+
+
+def make_optimizer(model, lr=1e-4, weight_decay=1e-5):
+    """optim.Adam(model.parameters(), lr, weight_decay) of train.py:241-245."""
+    return uoptim.Adam(model.parameters(), lr=lr, weight_decay=weight_decay)
+
+
+def train_step(model, img_low, criterion, optimizer, max_norm=1.0):
+    """One step body (train.py:63-103, no-AMP branch).  Returns (loss, loss_dict)."""
+    optimizer.zero_grad()
+    img_enhanced, reflectance, illu_map = model(img_low)
+    loss, loss_dict = criterion(img_low, img_enhanced, illu_map, reflectance)
+    loss.backward()
+    clip_grad_norm_(model.parameters(), max_norm=max_norm)
+    optimizer.step()
+    return loss, loss_dict
+
+
+def train_one_epoch(model, dataloader, criterion, optimizer, device, epoch, writer=None, scaler=None, use_amp=False):
+    model.train()
+    keys = ('total', 'exposure', 'smoothness', 'color', 'spatial', 'decouple', 'perceptual')
+    totals = {k: 0.0 for k in keys}
+    n = 0
+    t0 = time.time()
+    for batch_idx, img_low in enumerate(dataloader):
+        img_low = img_low.to(device, torch.float32)
+        _, loss_dict = train_step(model, img_low, criterion, optimizer)
+        for k in keys:
+            totals[k] += loss_dict[k]
+        n += 1
+        if writer is not None and batch_idx % 100 == 0:
+            for k, v in loss_dict.items():
+                writer.add_scalar(f'Loss/{k}', v, epoch * max(1, len(dataloader)) + batch_idx)
+    if n:
+        totals = {k: v / n for k, v in totals.items()}
+    totals["_epoch_seconds"] = time.time() - t0
+    return totals

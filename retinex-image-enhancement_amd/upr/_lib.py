@@ -73,6 +73,65 @@ SIGNATURES = {
     "upr_lab_tables": (None, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
 }
 
+
+class UprView(ctypes.Structure):
+    """include/upr_train.h UprView: element strides of (batch, row, col, channel)."""
+    _fields_ = [("data", ctypes.c_void_p), ("sb", ctypes.c_int64), ("sh", ctypes.c_int64),
+                ("sw", ctypes.c_int64), ("sc", ctypes.c_int64)]
+
+
+_vp = ctypes.POINTER(UprView)
+c_u64, c_i64p = ctypes.c_uint64, ctypes.c_void_p
+_i, _p, _f = c_int, c_void_p, c_float
+
+# mirrors include/upr_train.h exactly
+SIGNATURES.update({
+    "upr_t_zero": (_i, [_p, c_size_t, _p]),
+    "upr_t_conv_direct": (_i, [_vp, _i, _i, _i, _i, _p, _p, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _p]),
+    "upr_t_conv_direct_dgrad": (_i, [_vp, _i, _i, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _p]),
+    "upr_t_conv_direct_wgrad": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p]),
+    "upr_t_conv_mfma": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _p, _i, _i, _i, _i, _i, _i, _p, _i, _i, _p, _i, _i,
+                             _i, _p]),
+    "upr_t_conv_wgrad": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p]),
+    "upr_t_pack_weight": (_i, [_p, _p, _i, _i, _i, _i, _i, _p]),
+    "upr_t_unpack_grad": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p]),
+    "upr_t_zero_upsample": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _p]),
+    "upr_t_bn_stats": (_i, [_p, _i, _i, _i, _i, _p, _p]),
+    "upr_t_bn_finalize": (_i, [_p, _i, _i, _f, _f, _p, _p, _p, _p, _p, _p]),
+    "upr_t_bn_apply": (_i, [_p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _i, _i, _p]),
+    "upr_t_bn_bwd_reduce": (_i, [_p, _i, _i, _p, _i, _i, _p, _p, _i, _i, _p, _p]),
+    "upr_t_bn_bwd_apply": (_i, [_p, _i, _i, _p, _i, _i, _p, _p, _p, _p, _i, _i, _p, _p, _p, _i, _i, _i, _p]),
+    "upr_t_chan_sum": (_i, [_p, _i, _i, _i, _i, _p, _i, _p]),
+    "upr_t_relu_mask": (_i, [_p, _i, _i, _p, _i, _i, _i, _i, _p]),
+    "upr_t_copy": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _p]),
+    "upr_t_pointwise": (_i, [_p, _p, _p, c_size_t, _i, _p, _p, _f, c_u64, _p]),
+    "upr_t_maxpool": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _p]),
+    "upr_t_maxpool_bwd": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _p]),
+    "upr_t_bilinear": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _p]),
+    "upr_t_bilinear_bwd": (_i, [_vp, _i, _i, _i, _i, _i, _i, _vp, _p]),
+    "upr_t_pixel_sum": (_i, [_p, _i, _i, _i, _i, _i, _f, _p, _i, _p]),
+    "upr_t_broadcast": (_i, [_p, _i, _i, _i, _f, _p, _i, _i, _i, _p]),
+    "upr_t_fam_ca_apply": (_i, [_p, _p, _i, _i, _i, _p, _p, _p]),
+    "upr_t_fam_sa_apply": (_i, [_p, _p, _i, _i, _i, _p, _p, _p]),
+    "upr_t_fam_sa_bwd": (_i, [_p, _p, _p, _i, _i, _i, _p, _p, _p]),
+    "upr_t_fam_ca_bwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p]),
+    "upr_t_fam_pool_bwd": (_i, [_p, _p, _p, _i, _i, _i, _p]),
+    "upr_t_head_fwd": (_i, [_p, _p, _p, _i, _i, _i, _p]),
+    "upr_t_retinex_fwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _p]),
+    "upr_t_retinex_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p]),
+    "upr_t_loss_workspace": (c_size_t, [_i, _i, _i]),
+    "upr_t_loss_pixel": (_i, [_p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p, _i, _f, _f, _f, _f, _p]),
+    "upr_t_mse": (_i, [_p, _p, c_size_t, _p, _p, _f, _p]),
+    "upr_t_vgg_norm": (_i, [_p, _p, _i, _i, _i, _p]),
+    "upr_t_vgg_norm_bwd": (_i, [_p, _p, _i, _i, _i, _p]),
+    "upr_t_freq": (_i, [_p, _p, _i, _i, _i, _p, _p, _f, _p]),
+    "upr_t_add_real": (_i, [_p, _p, c_size_t, _f, _p]),
+    "upr_t_scale_acc": (_i, [_p, _i, _f, _p, _p]),
+    "upr_t_loss_total": (_i, [_p, _f, _f, _f, _f, _f, _f, _p]),
+    "upr_t_sqsum": (_i, [_p, c_size_t, _p, _p]),
+    "upr_t_adam": (_i, [_p, _p, _p, _p, c_size_t, _p, _f, _f, _f, _f, _f, _f, _i, _p, _p]),
+})
+
 _lib = None
 
 

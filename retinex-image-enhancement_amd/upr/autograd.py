@@ -1,0 +1,116 @@
+"""Autograd glue so the reference's training loop runs unchanged
+(trainers/train.py:91-103: `model(img_low)` -> `criterion(...)` ->
+`loss.backward()` -> clip -> `optimizer.step()`).
+
+Two autograd nodes, each a whole subgraph whose forward and backward are the
+HIP engines of upr/train.py and upr/loss_engine.py:
+  _ModelStep  MultiScaleUP_Retinex training forward; backward = the explicit
+              network backward, accumulating every parameter's gradient into
+              the flat gradient buffer (the .grad views);
+  _LossStep   TotalLoss forward; its gradients w.r.t. (enh, illu, refl) are
+              produced with the forward and scaled on the device by the
+              incoming gradient in backward (GradScaler / loss weights).
+"""
+import ctypes
+
+import torch
+
+from . import _lib as L
+from .train import FlatParams, UPRetinexTrainGraph, _chk, _p, _stream, zero
+
+_weights_epoch = [0]
+
+
+def weights_epoch():
+    """Bumped whenever the training kernels change parameters or BatchNorm
+    buffers in place (the inference handle cache keys on it)."""
+    return _weights_epoch[0]
+
+
+def bump_weights_epoch():
+    _weights_epoch[0] += 1
+
+
+class _ModelStep(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, graph):
+        enh, refl, illu = graph.forward(x)
+        bump_weights_epoch()  # BatchNorm running stats were updated
+        ctx.graph = graph
+        return enh, refl, illu
+
+    @staticmethod
+    def backward(ctx, g_enh, g_refl, g_illu):
+        graph = ctx.graph
+        flat = graph.flat
+        if flat.attach_grads():
+            zero(flat.grad)       # zero_grad(set_to_none=True) dropped the views
+        dev = graph.x.device
+        if g_enh is None:
+            g_enh = torch.empty_like(graph.enh)
+            zero(g_enh)
+        g_enh = g_enh.contiguous()
+        g_refl = g_refl.contiguous() if g_refl is not None else None
+        g_illu = g_illu.contiguous() if g_illu is not None else None
+        with torch.cuda.device(dev):
+            graph.backward(g_enh, g_refl, g_illu)
+        return None, None, None
+
+
+def model_train_forward(model, x):
+    """Training-mode forward of MultiScaleUP_Retinex on the HIP engine."""
+    st = model.__dict__.get("_upr_train")
+    if st is None or st["device"] != x.device:
+        ps = list(model.parameters())
+        flat = getattr(ps[0], "_upr_flat", None)
+        if flat is None or any(getattr(p, "_upr_flat", None) is not flat for p in ps) or \
+                flat.flat.device != x.device:
+            flat = FlatParams(model)
+        graph = UPRetinexTrainGraph(model)
+        graph.flat = flat
+        anchor = torch.empty(0, device=x.device, requires_grad=True)
+        st = {"device": x.device, "flat": flat, "graph": graph, "anchor": anchor}
+        model.__dict__["_upr_train"] = st
+    if x.dtype != torch.float32:
+        raise TypeError("UP-Retinex HIP training computes in float32; pass a float32 batch")
+    return _ModelStep.apply(x.contiguous(), st["anchor"], st["graph"])
+
+
+class _LossStep(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, low, enh, illu, refl, engine):
+        terms, grads = engine(low, enh, illu, refl, grads=True)
+        ctx.grads = grads
+        total = _scalar_of(terms, 7)
+        ctx.mark_non_differentiable(terms)
+        return total, terms
+
+    @staticmethod
+    def backward(ctx, g, _g_terms):
+        lib = L.lib()
+        g = g.contiguous().to(torch.float32)
+        outs = []
+        for t in ctx.grads:
+            _chk(lib.upr_t_pointwise(_p(t), _p(g), _p(t), t.numel(), 5, None, None, ctypes.c_float(0),
+                                     ctypes.c_uint64(0), _stream()), "scale_grad")
+            outs.append(t)
+        g_enh, g_illu, g_refl = outs
+        return None, g_enh, g_illu, g_refl, None
+
+
+def _scalar_of(terms, i):
+    """0-dim device tensor holding terms[i] (a one-element device copy)."""
+    out = torch.empty((), dtype=torch.float32, device=terms.device)
+    src = L.UprView(terms.data_ptr() + 4 * i, 0, 0, 0, 1)
+    dst = L.UprView(out.data_ptr(), 0, 0, 0, 1)
+    _chk(L.lib().upr_t_copy(ctypes.byref(src), ctypes.byref(dst), 1, 1, 1, 1, 0, _stream()), "scalar")
+    return out
+
+
+def loss_forward(engine, low, enh, illu, refl):
+    """TotalLoss.forward on the HIP engine -> (total 0-dim tensor, device terms[9]).
+    With autograd recording (training), total carries the loss backward."""
+    if torch.is_grad_enabled() and (enh.requires_grad or illu.requires_grad or refl.requires_grad):
+        return _LossStep.apply(low, enh, illu, refl, engine)
+    terms, _ = engine(low, enh, illu, refl, grads=False)
+    return _scalar_of(terms, 7), terms

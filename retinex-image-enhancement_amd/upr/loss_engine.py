@@ -1,0 +1,190 @@
+"""TotalLoss (losses/loss.py:586-753) forward + gradient on gfx950 kernels.
+
+One call computes every loss term AND its gradient w.r.t. the network outputs
+(enhanced, illumination, reflectance) — the backward of a loss is cheap next
+to the network's, so it is produced eagerly and handed to the network's
+backward:
+
+  * exposure / smoothness / colour / spatial / decoupling / texture weight:
+    upr_t_loss_pixel (two reduction passes, a one-block finaliser and one
+    gradient pass over the pixels);
+  * perceptual (loss.py:179-255): VGG-19 features[0..18] on the MFMA conv
+    kernels for both images, three MSE levels, backward through the enhanced
+    branch (input gradients only: the VGG is frozen);
+  * frequency (loss.py:430-520): 2-D FFTs through torch.fft (rocFFT, the
+    library FFT — SURVEY.md §7), magnitude / mask / MSE and the gradient
+    spectrum in upr_t_freq, inverse FFT, real part added by upr_t_add_real.
+"""
+import ctypes
+
+import torch
+import torch.nn as nn
+
+from . import _lib as L
+from .train import Act, Conv, _chk, _fp, _p, _stream, empty, relu_mask, zero
+
+WEIGHTS = dict(exposure=10.0, smoothness=1.0, color=0.5, spatial=1.0, decouple=0.1, perceptual=1.0,
+               frequency=0.5)
+TERM_ORDER = ("exposure", "smoothness", "color", "spatial", "decouple", "perceptual", "frequency", "total")
+
+VGG19_E = (64, 64, "M", 128, 128, "M", 256, 256, 256, 256, "M", 512, 512, 512, 512, "M", 512, 512, 512, 512, "M")
+
+
+def vgg19_features(seed=None):
+    """torchvision.models.vgg19().features layout (config "E"); with a seed,
+    PyTorch's default Conv2d init drawn under torch.manual_seed(seed) — the
+    offline stand-in for the pretrained weights (loss.py:195 downloads them)."""
+    if seed is not None:
+        torch.manual_seed(seed)
+    layers, c = [], 3
+    for v in VGG19_E:
+        if v == "M":
+            layers.append(nn.MaxPool2d(kernel_size=2, stride=2))
+        else:
+            layers += [nn.Conv2d(c, v, kernel_size=3, padding=1), nn.ReLU(inplace=True)]
+            c = v
+    return nn.Sequential(*layers)
+
+
+class VGGPerceptual:
+    """PerceptualLoss slices (loss.py:198-211): slice1 = features[0..4],
+    slice2 = [5..9], slice3 = [10..18]; each ends with a 2x2 max-pool."""
+
+    SLICES = ((0, 2), (5, 7), (10, 12, 14, 16))
+
+    def __init__(self, features):
+        self.convs = {i: Conv(features[i], frozen=True) for s in self.SLICES for i in s}
+
+    def pack(self):
+        for c in self.convs.values():
+            c.pack()
+
+    def run(self, x_nhwc, keep):
+        """x_nhwc: Act [B,H,W,3] (normalised).  Returns the three slice outputs;
+        with keep, the intermediate activations for the backward."""
+        lib, st = L.lib(), _stream()
+        h = x_nhwc
+        feats, trace = [], []
+        for sl in self.SLICES:
+            for i in sl:
+                inp = h
+                h = self.convs[i].fwd(h, relu=True) if self.convs[i].mfma else \
+                    self.convs[i].fwd(None, relu=True, x_view=(h.view(), h.B, h.H, h.W),
+                                      out=Act.new(h.B, h.H, h.W, self.convs[i].Cout, h.t.device, fresh=False))
+                if keep:
+                    trace.append(("conv", i, inp, h))
+            p = Act.new(h.B, h.H // 2, h.W // 2, h.C, h.t.device, fresh=False)
+            _chk(lib.upr_t_maxpool(ctypes.byref(h.view()), h.B, h.H, h.W, h.C, 2, 2, 0, ctypes.byref(p.view()), p.H,
+                                   p.W, st), "vgg_pool")
+            if keep:
+                trace.append(("pool", None, h, p))
+            h = p
+            feats.append(p)
+        return feats, trace
+
+    def backward(self, trace, g_feats):
+        """g_feats: gradient Acts of the three slice outputs -> gradient Act of the input."""
+        lib, st = L.lib(), _stream()
+        g = None
+        level = 2
+        for kind, i, inp, out in reversed(trace):
+            if kind == "pool":
+                if g is None:
+                    g = g_feats[level]
+                else:
+                    _chk(lib.upr_t_pointwise(_fp(g.t), _fp(g_feats[level].t), _fp(g.t), g.t.numel(), 4, None, None,
+                                             ctypes.c_float(0), ctypes.c_uint64(0), st), "add")
+                level -= 1
+                gi = Act.new(inp.B, inp.H, inp.W, inp.C, inp.t.device, fresh=False)
+                zero(gi.t)
+                _chk(lib.upr_t_maxpool_bwd(ctypes.byref(inp.view()), ctypes.byref(g.view()), inp.B, inp.H, inp.W,
+                                           inp.C, 2, 2, 0, out.H, out.W, ctypes.byref(gi.view()), st), "pool_bwd")
+                g = gi
+            else:
+                relu_mask(g, out)
+                gi = Act.new(inp.B, inp.H, inp.W, inp.C, inp.t.device)
+                c = self.convs[i]
+                if c.mfma:
+                    c.bwd(inp, g, gi)
+                else:
+                    c.bwd(None, g, gi, x_view=(inp.view(), inp.B, inp.H, inp.W))
+                g = gi
+        return g
+
+
+class TotalLossEngine:
+    """losses/loss.py TotalLoss with adaptive_weights=False,
+    use_dynamic_smooth_weight=True, texture_method='tv' (train.py:224-234)."""
+
+    def __init__(self, vgg_features, weights=None, use_freq_loss=True):
+        self.w = dict(WEIGHTS)
+        if weights:
+            self.w.update(weights)
+        self.use_freq = use_freq_loss
+        self.vgg = VGGPerceptual(vgg_features)
+        self.features = vgg_features
+
+    def __call__(self, low, enh, illu, refl, grads=True):
+        """All NCHW fp32 device tensors.  Returns (terms [9] device tensor in
+        upr_t_loss_total order, (g_enh, g_illu, g_refl) or None)."""
+        lib, st = L.lib(), _stream()
+        B, C, H, W = enh.shape
+        dev = enh.device
+        w = self.w
+        terms = torch.empty(9, dtype=torch.float32, device=dev)
+        zero(terms)
+        ws = torch.empty(lib.upr_t_loss_workspace(B, H, W), dtype=torch.uint8, device=dev)
+        g_enh = g_illu = g_refl = None
+        if grads:
+            g_enh, g_illu, g_refl = empty(enh.shape, dev), empty(illu.shape, dev), empty(refl.shape, dev)
+        _chk(lib.upr_t_loss_pixel(_p(low), _p(enh), _p(illu), _p(refl), B, H, W, _p(ws), _p(terms), _p(g_enh),
+                                  _p(g_illu), _p(g_refl), int(grads), ctypes.c_float(w["exposure"]),
+                                  ctypes.c_float(w["color"]), ctypes.c_float(w["spatial"]),
+                                  ctypes.c_float(w["decouple"]), st), "loss_pixel")
+        acc = torch.empty(4, dtype=torch.float64, device=dev)
+        zero(acc)
+        # ---- perceptual ----
+        self.vgg.pack()
+        ne = Act.new(B, H, W, 3, dev, fresh=False)
+        nl = Act.new(B, H, W, 3, dev, fresh=False)
+        _chk(lib.upr_t_vgg_norm(_p(enh), _fp(ne.t), B, H, W, st), "vgg_norm")
+        _chk(lib.upr_t_vgg_norm(_p(low), _fp(nl.t), B, H, W, st), "vgg_norm")
+        fe, trace = self.vgg.run(ne, keep=grads)
+        fl, _ = self.vgg.run(nl, keep=False)
+        gfe = []
+        for a, b in zip(fe, fl):
+            n = a.t.numel()
+            g = Act.new(a.B, a.H, a.W, a.C, dev, fresh=False) if grads else None
+            _chk(lib.upr_t_mse(_fp(a.t), _fp(b.t), n, _p(acc[1:2]), _fp(g.t) if g else None,
+                               ctypes.c_float(w["perceptual"] / n), st), "mse")
+            gfe.append(g)
+        _chk(lib.upr_t_scale_acc(_p(acc[1:2]), 1, ctypes.c_float(1.0), _fp(terms, 5), st), "scale")
+        if grads:
+            g_in = self.vgg.backward(trace, gfe)
+            _chk(lib.upr_t_vgg_norm_bwd(_fp(g_in.t), _p(g_enh), B, H, W, st), "vgg_norm_bwd")
+        # ---- frequency ----
+        if self.use_freq:
+            ze = torch.fft.fft2(enh, dim=(-2, -1))
+            zl = torch.fft.fft2(low, dim=(-2, -1))
+            n = enh.numel()
+            G = torch.empty_like(ze) if grads else None
+            _chk(lib.upr_t_freq(_p(ze), _p(zl), B * C, H, W, _p(acc[2:3]), _p(G),
+                                ctypes.c_float(w["frequency"] / n), st), "freq")
+            _chk(lib.upr_t_scale_acc(_p(acc[2:3]), 1, ctypes.c_float(1.0 / n), _fp(terms, 6), st), "scale")
+            if grads:
+                gx = torch.fft.ifft2(G, dim=(-2, -1))
+                _chk(lib.upr_t_add_real(_p(gx), _p(g_enh), n, ctypes.c_float(float(H * W)), st), "add_real")
+        _chk(lib.upr_t_loss_total(_p(terms), ctypes.c_float(w["exposure"]), ctypes.c_float(w["color"]),
+                                  ctypes.c_float(w["spatial"]), ctypes.c_float(w["decouple"]),
+                                  ctypes.c_float(w["perceptual"]), ctypes.c_float(w["frequency"] if self.use_freq
+                                                                                  else 0.0), st), "total")
+        return terms, ((g_enh, g_illu, g_refl) if grads else None)
+
+
+def terms_dict(terms):
+    """One device->host copy of the 9 loss scalars -> the reference's loss_dict
+    (loss.py:741-751) + the dynamic smooth weight."""
+    v = terms.cpu().tolist()
+    d = {k: v[i] for i, k in enumerate(TERM_ORDER)}
+    d["smooth_weight"] = v[8]
+    return d

@@ -1,0 +1,807 @@
+"""Training engine: explicit forward + backward of MultiScaleUP_Retinex on the
+gfx950 kernels of include/upr_train.h (+ the inference conv kernels).
+
+Reference: trainers/train.py:63-103 runs `model(img_low)` in train mode,
+`criterion(...)` (losses/loss.py TotalLoss), `loss.backward()`,
+`clip_grad_norm_(1.0)` and `Adam.step()` on PyTorch autograd.  Here the same
+step is a fixed graph written out by hand: every layer object below owns the
+forward kernels of one reference module and the matching backward kernels;
+activations the backward needs are kept from the forward.  PyTorch only
+allocates device memory (torch.empty) and supplies the stream; there is no
+autograd tape and no torch compute.
+
+Layouts: network input / outputs NCHW (the reference's tensors), every
+activation NHWC fp32 (`Act`, possibly a channel slice of a concat buffer).
+Parameters and their gradients live in ONE flat fp32 buffer each
+(`FlatParams`), so clip_grad_norm_ and Adam are single launches.
+"""
+import ctypes
+
+import torch
+
+from . import _lib as L
+
+F32 = torch.float32
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _chk(rc, what):
+    L.check(rc, what)
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _fp(t, off=0):
+    """Pointer to element `off` of a fp32 tensor."""
+    return ctypes.c_void_p(t.data_ptr() + 4 * off) if t is not None else None
+
+
+def empty(shape, dev):
+    return torch.empty(shape, dtype=F32, device=dev)
+
+
+class Act:
+    """NHWC activation: channels [coff, coff+C) of a [B,H,W,cs] fp32 tensor.
+
+    `fresh` marks a gradient buffer nothing has written yet: the first
+    producer overwrites (or zeroes it when it scatters with atomics), later
+    producers accumulate."""
+
+    def __init__(self, t, C=None, coff=0):
+        assert t.dim() == 4 and t.dtype == F32 and t.is_contiguous()
+        self.t = t
+        self.B, self.H, self.W, self.cs = t.shape
+        self.C = self.cs if C is None else C
+        self.coff = coff
+        self.fresh = False
+
+    @staticmethod
+    def new(B, H, W, C, dev, fresh=True):
+        a = Act(empty((B, H, W, C), dev))
+        a.fresh = fresh
+        return a
+
+    def slice(self, coff, C):
+        s = Act(self.t, C, self.coff + coff)
+        s.fresh = self.fresh
+        return s
+
+    @property
+    def M(self):
+        return self.B * self.H * self.W
+
+    def ptr(self):
+        return _fp(self.t, self.coff)
+
+    def view(self):
+        return L.UprView(self.t.data_ptr() + 4 * self.coff, self.H * self.W * self.cs, self.W * self.cs, self.cs, 1)
+
+    def zero_if_fresh(self):
+        if self.fresh:
+            _chk(L.lib().upr_t_zero(_p(self.t), self.t.numel() * 4, _stream()), "zero")
+            self.fresh = False
+
+    def consume_fresh(self):
+        """Returns 1 (accumulate) or 0 (overwrite) for the next producer."""
+        acc = 0 if self.fresh else 1
+        self.fresh = False
+        return acc
+
+
+def nchw_view(t, coff=0):
+    B, C, H, W = t.shape
+    return L.UprView(t.data_ptr() + 4 * coff * H * W, C * H * W, W, 1, H * W)
+
+
+def zero(t):
+    _chk(L.lib().upr_t_zero(_p(t), t.numel() * t.element_size(), _stream()), "zero")
+
+
+class FlatParams:
+    """All trainable parameters of a module in one flat device buffer (and the
+    gradients in another); each nn.Parameter's .data / .grad become views.
+    Order = module.named_parameters() (the reference optimiser's order)."""
+
+    def __init__(self, module):
+        params = list(module.named_parameters()) if hasattr(module, "named_parameters") else \
+            [(str(i), p) for i, p in enumerate(module)]
+        dev = params[0][1].device
+        if dev.type != "cuda":
+            raise RuntimeError("HIP training needs the parameters on a ROCm device (model.to('cuda'))")
+        align = 16  # 64-byte aligned tensors (the conv kernels' vector loads of bias / weights)
+        n = sum((p.numel() + align - 1) // align * align for _, p in params)
+        self.numel = n
+        self.flat = torch.zeros((n,), dtype=F32, device=dev)
+        self.grad = torch.zeros((n,), dtype=F32, device=dev)
+        self.offsets = {}
+        off = 0
+        for name, p in params:
+            k = p.numel()
+            self.flat[off:off + k].view(p.shape).copy_(p.data)   # one-time device copy (plumbing)
+            p.data = self.flat[off:off + k].view(p.shape)
+            p._upr_flat = self
+            self.offsets[name] = (off, k)
+            off += (k + align - 1) // align * align
+        self.params = dict(params)
+        self.attach_grads()
+
+    def attach_grads(self):
+        """(Re)point every .grad at its slice of the flat gradient buffer;
+        returns True if any had been detached (zero_grad(set_to_none=True))."""
+        detached = False
+        for name, p in self.params.items():
+            off, k = self.offsets[name]
+            g = p.grad
+            if g is None or g.data_ptr() != self.grad.data_ptr() + 4 * off:
+                detached = True
+                p.grad = self.grad[off:off + k].view(p.shape)
+        return detached
+
+    def g(self, p):
+        """Gradient view of parameter p."""
+        return p.grad
+
+
+# ---------------------------------------------------------------------------
+# layers
+# ---------------------------------------------------------------------------
+class Conv:
+    """nn.Conv2d (model.py / VGG) forward, input-gradient and weight-gradient.
+
+    Cin, Cout multiples of 32 run on the MFMA implicit-GEMM kernels (weights
+    re-packed every step: [Cout][(ky,kx,ci)] forward, flipped [Cin][(ky,kx,co)]
+    for the input gradient); other shapes on the direct kernels."""
+
+    def __init__(self, m, frozen=False):
+        self.m = m
+        self.Cout, self.Cin, self.kh, self.kw = m.weight.shape
+        self.s = m.stride[0]
+        self.p = m.padding[0]
+        self.d = m.dilation[0]
+        self.bias = m.bias
+        self.mfma = self.Cin % 32 == 0 and self.Cout % 32 == 0
+        self.frozen = frozen
+        self.wp = self.wt = None
+
+    def out_hw(self, H, W):
+        return ((H + 2 * self.p - self.d * (self.kh - 1) - 1) // self.s + 1,
+                (W + 2 * self.p - self.d * (self.kw - 1) - 1) // self.s + 1)
+
+    def pack(self):
+        if not self.mfma:
+            return
+        lib, st = L.lib(), _stream()
+        w = self.m.weight
+        if self.wp is None:
+            self.wp = torch.empty_like(w).view(-1)
+            self.wt = torch.empty_like(w).view(-1)
+            self.gp = torch.empty_like(w).view(-1)
+        _chk(lib.upr_t_pack_weight(_p(w), _p(self.wp), self.Cout, self.Cin, self.kh, self.kw, 0, st), "pack")
+        _chk(lib.upr_t_pack_weight(_p(w), _p(self.wt), self.Cout, self.Cin, self.kh, self.kw, 1, st), "pack")
+
+    def fwd(self, x, relu=False, out=None, res=None, x_view=None):
+        """x: Act (or x_view: (UprView, B, H, W) for an NCHW network input)."""
+        lib, st = L.lib(), _stream()
+        if x_view is not None:
+            xv, B, H, W = x_view
+        else:
+            B, H, W = x.B, x.H, x.W
+        Ho, Wo = self.out_hw(H, W)
+        if out is None:
+            out = Act.new(B, Ho, Wo, self.Cout, x.t.device, fresh=False)
+        out.fresh = False
+        if self.mfma and x_view is None:
+            _chk(lib.upr_t_conv_mfma(_fp(x.t), B, H, W, self.Cin, x.cs, x.coff, _p(self.wp),
+                                     _p(self.bias), self.Cout, self.kh, self.kw, self.s, self.p, self.d,
+                                     res.ptr() if res is not None else None, res.cs if res is not None else 0,
+                                     int(relu), _fp(out.t), out.cs, out.coff, 0, st), "conv_mfma")
+        else:
+            assert res is None
+            v = x.view() if x_view is None else xv
+            _chk(lib.upr_t_conv_direct(ctypes.byref(v), B, H, W, self.Cin, _p(self.m.weight), _p(self.bias),
+                                       self.Cout, self.kh, self.kw, self.s, self.p, self.d,
+                                       ctypes.byref(out.view()), Ho, Wo, int(relu), 0, st), "conv_direct")
+        return out
+
+    def bwd(self, x, gy, gx=None, x_view=None):
+        """gy: Act gradient of this conv's output (pre-activation).
+        Accumulates the weight / bias gradients; gx (Act, nullable) receives
+        the input gradient (overwrite when fresh, else accumulate)."""
+        lib, st = L.lib(), _stream()
+        if x_view is not None:
+            xv, B, H, W = x_view
+        else:
+            B, H, W = x.B, x.H, x.W
+        Ho, Wo = gy.H, gy.W
+        if not self.frozen:
+            gw = self.m.weight.grad
+            if self.mfma and x_view is None:
+                zero(self.gp)
+                _chk(lib.upr_t_conv_wgrad(_fp(x.t), B, H, W, self.Cin, x.cs, x.coff, _fp(gy.t), Ho, Wo, self.Cout,
+                                          gy.cs, gy.coff, self.kh, self.kw, self.s, self.p, self.d, _p(self.gp), st),
+                     "conv_wgrad")
+                _chk(lib.upr_t_unpack_grad(_p(self.gp), _p(gw), self.Cout, self.Cin, self.kh, self.kw, 0, 1, st),
+                     "unpack")
+                if self.bias is not None:
+                    _chk(lib.upr_t_chan_sum(gy.ptr(), gy.M, self.Cout, gy.cs, 0, _p(self.bias.grad), 1, st), "dbias")
+            else:
+                v = x.view() if x_view is None else xv
+                _chk(lib.upr_t_conv_direct_wgrad(ctypes.byref(v), ctypes.byref(gy.view()), B, H, W, self.Cin, Ho, Wo,
+                                                 self.Cout, self.kh, self.kw, self.s, self.p, self.d, _p(gw),
+                                                 _p(self.bias.grad) if self.bias is not None else None, st),
+                     "conv_direct_wgrad")
+        if gx is None:
+            return
+        if self.mfma:
+            acc = gx.consume_fresh()
+            src, sH, sW, scs, scoff = gy.t, Ho, Wo, gy.cs, gy.coff
+            if self.s != 1:
+                assert self.s == 2 and H == 2 * Ho and W == 2 * Wo, "stride-2 dgrad needs even sizes"
+                z = empty((B, H, W, self.Cout), gy.t.device)
+                _chk(lib.upr_t_zero_upsample(_fp(gy.t), B, Ho, Wo, self.Cout, gy.cs, gy.coff,
+                                             _p(z), st), "zero_upsample")
+                src, sH, sW, scs, scoff = z, H, W, self.Cout, 0
+            pad_t = self.d * (self.kh - 1) - self.p
+            _chk(lib.upr_t_conv_mfma(_fp(src), B, sH, sW, self.Cout, scs, scoff, _p(self.wt), None, self.Cin,
+                                     self.kh, self.kw, 1, pad_t, self.d, gx.ptr() if acc else None,
+                                     gx.cs if acc else 0, 0, _fp(gx.t), gx.cs, gx.coff, 0, st), "conv_dgrad")
+        else:
+            acc = gx.consume_fresh()
+            _chk(lib.upr_t_conv_direct_dgrad(ctypes.byref(gy.view()), Ho, Wo, _p(self.m.weight), B, H, W, self.Cin,
+                                             self.Cout, self.kh, self.kw, self.s, self.p, self.d,
+                                             ctypes.byref(gx.view()), acc, st), "conv_direct_dgrad")
+
+
+class ConvT:
+    """nn.ConvTranspose2d(k=2, s=2) (UpBlock.up, model.py:261): a GEMM with
+    N = 4*Cout and a pixel-shuffle store; dgrad = k2 s2 conv over dy; wgrad =
+    the same GEMM over pixels with dy as the 'input'."""
+
+    def __init__(self, m):
+        self.m = m
+        self.Cin, self.Cout = m.weight.shape[0], m.weight.shape[1]
+        self.wp = None
+
+    def pack(self):
+        lib, st = L.lib(), _stream()
+        w = self.m.weight
+        if self.wp is None:
+            self.wp = torch.empty_like(w).view(-1)
+            self.wd = torch.empty_like(w).view(-1)
+            self.gp = torch.empty_like(w).view(-1)
+            self.b4 = empty((4 * self.Cout,), w.device)
+        _chk(lib.upr_t_pack_weight(_p(w), _p(self.wp), self.Cout, self.Cin, 2, 2, 2, st), "pack")
+        _chk(lib.upr_t_pack_weight(_p(w), _p(self.wd), self.Cout, self.Cin, 2, 2, 3, st), "pack")
+        src = L.UprView(self.m.bias.data_ptr(), 0, 0, 0, 1)
+        dst = L.UprView(self.b4.data_ptr(), 0, 0, self.Cout, 1)
+        _chk(lib.upr_t_copy(ctypes.byref(src), ctypes.byref(dst), 1, 1, 4, self.Cout, 0, st), "bias4")
+
+    def fwd(self, x):
+        out = Act.new(x.B, 2 * x.H, 2 * x.W, self.Cout, x.t.device, fresh=False)
+        _chk(L.lib().upr_t_conv_mfma(x.ptr(), x.B, x.H, x.W, self.Cin, x.cs, 0, _p(self.wp), _p(self.b4),
+                                     4 * self.Cout, 1, 1, 1, 0, 1, None, 0, 0, _fp(out.t), out.cs, 0, 1, _stream()),
+             "convT")
+        return out
+
+    def bwd(self, x, gy, gx):
+        lib, st = L.lib(), _stream()
+        zero(self.gp)
+        # dwp[ci][(a,b,co)] = sum_p x[p][ci] * gy[2y+a][2x+b][co]: a k2 s2 "conv" of gy producing x
+        _chk(lib.upr_t_conv_wgrad(gy.ptr(), gy.B, gy.H, gy.W, self.Cout, gy.cs, 0, x.ptr(), x.H, x.W, self.Cin,
+                                  x.cs, 0, 2, 2, 2, 0, 1, _p(self.gp), st), "convT_wgrad")
+        _chk(lib.upr_t_unpack_grad(_p(self.gp), _p(self.m.weight.grad), self.Cout, self.Cin, 2, 2, 3, 1, st),
+             "unpack")
+        _chk(lib.upr_t_chan_sum(gy.ptr(), gy.M, self.Cout, gy.cs, 0, _p(self.m.bias.grad), 1, st), "dbias")
+        acc = gx.consume_fresh()
+        _chk(lib.upr_t_conv_mfma(gy.ptr(), gy.B, gy.H, gy.W, self.Cout, gy.cs, 0, _p(self.wd), None, self.Cin, 2, 2,
+                                 2, 0, 1, gx.ptr() if acc else None, gx.cs if acc else 0, 0, _fp(gx.t), gx.cs,
+                                 gx.coff, 0, st), "convT_dgrad")
+
+
+class BN:
+    """nn.BatchNorm2d in training mode (batch statistics, running-stat update)."""
+
+    def __init__(self, m):
+        self.m = m
+        self.C = m.num_features
+        dev = m.weight.device
+        self.mean = empty((self.C,), dev)
+        self.invstd = empty((self.C,), dev)
+        self.acc = torch.empty((2 * self.C,), dtype=torch.float64, device=dev)
+
+    def fwd(self, x, relu=False, out=None, res=None, res_post=False):
+        lib, st = L.lib(), _stream()
+        m = self.m
+        zero(self.acc)
+        _chk(lib.upr_t_bn_stats(x.ptr(), x.M, self.C, x.cs, 0, _p(self.acc), st), "bn_stats")
+        _chk(lib.upr_t_bn_finalize(_p(self.acc), x.M, self.C, ctypes.c_float(m.momentum), ctypes.c_float(m.eps),
+                                   _p(m.running_mean), _p(m.running_var), _p(m.num_batches_tracked), _p(self.mean),
+                                   _p(self.invstd), st), "bn_finalize")
+        if out is None:
+            out = Act.new(x.B, x.H, x.W, self.C, x.t.device, fresh=False)
+        _chk(lib.upr_t_bn_apply(x.ptr(), x.M, self.C, x.cs, 0, _p(self.mean), _p(self.invstd), _p(m.weight),
+                                _p(m.bias), res.ptr() if res is not None else None, res.cs if res is not None else 0,
+                                0, int(res_post), int(relu), _fp(out.t), out.cs, out.coff, st), "bn_apply")
+        self.x = x
+        return out
+
+    def bwd(self, g, gx):
+        """g: Act gradient of the BN output (ReLU already masked)."""
+        lib, st = L.lib(), _stream()
+        m, x = self.m, self.x
+        zero(self.acc)
+        _chk(lib.upr_t_bn_bwd_reduce(_fp(g.t), g.cs, g.coff, x.ptr(), x.cs, 0, _p(self.mean), _p(self.invstd), x.M,
+                                     self.C, _p(self.acc), st), "bn_bwd_reduce")
+        acc = gx.consume_fresh()
+        _chk(lib.upr_t_bn_bwd_apply(_fp(g.t), g.cs, g.coff, x.ptr(), x.cs, 0, _p(self.mean), _p(self.invstd),
+                                    _p(m.weight), _p(self.acc), x.M, self.C, _p(m.weight.grad), _p(m.bias.grad),
+                                    _fp(gx.t), gx.cs, gx.coff, acc, st), "bn_bwd_apply")
+
+
+def relu_mask(g, y):
+    _chk(L.lib().upr_t_relu_mask(_fp(g.t), g.cs, g.coff, _fp(y.t), y.cs, y.coff, g.M, g.C, _stream()), "relu_mask")
+
+
+def add_into(dst, src):
+    """dst (+)= src (Acts of equal shape)."""
+    acc = dst.consume_fresh()
+    _chk(L.lib().upr_t_copy(ctypes.byref(src.view()), ctypes.byref(dst.view()), src.B, src.H, src.W, src.C, acc,
+                            _stream()), "copy")
+
+
+def pointwise(a, b, out, n, op, mask_in=None, mask_out=None, p=0.0, seed=0):
+    _chk(L.lib().upr_t_pointwise(_p(a), _p(b), _p(out), n, op, _p(mask_in), _p(mask_out), ctypes.c_float(p),
+                                 ctypes.c_uint64(seed), _stream()), "pointwise")
+
+
+# ---------------------------------------------------------------------------
+# reference modules
+# ---------------------------------------------------------------------------
+class ResBlockT:
+    """ResBlock (model.py:100-135)."""
+
+    def __init__(self, m):
+        self.conv1, self.bn1 = Conv(m.conv1), BN(m.bn1)
+        self.conv2, self.bn2 = Conv(m.conv2), BN(m.bn2)
+        self.proj = len(m.shortcut) > 0
+        if self.proj:
+            self.sconv, self.sbn = Conv(m.shortcut[0]), BN(m.shortcut[1])
+
+    def convs(self):
+        return [self.conv1, self.conv2] + ([self.sconv] if self.proj else [])
+
+    def fwd(self, x):
+        self.x = x
+        self.a1 = self.bn1.fwd(self.conv1.fwd(x), relu=True)
+        c2 = self.conv2.fwd(self.a1)
+        sc = self.sbn.fwd(self.sconv.fwd(x)) if self.proj else x
+        self.out = self.bn2.fwd(c2, relu=True, res=sc)
+        return self.out
+
+    def bwd(self, g, gx):
+        relu_mask(g, self.out)
+        g_c2 = Act.new(g.B, g.H, g.W, self.conv2.Cout, g.t.device)
+        self.bn2.bwd(g, g_c2)
+        if self.proj:
+            g_cs = Act.new(g.B, g.H, g.W, self.sconv.Cout, g.t.device)
+            self.sbn.bwd(g, g_cs)
+            self.sconv.bwd(self.x, g_cs, gx)
+        else:
+            add_into(gx, g)
+        g_a1 = Act.new(self.a1.B, self.a1.H, self.a1.W, self.a1.C, g.t.device)
+        self.conv2.bwd(self.a1, g_c2, g_a1)
+        relu_mask(g_a1, self.a1)
+        g_c1 = Act.new(g_a1.B, g_a1.H, g_a1.W, g_a1.C, g.t.device)
+        self.bn1.bwd(g_a1, g_c1)
+        self.conv1.bwd(self.x, g_c1, gx)
+
+
+class PreActResBlockT:
+    """PreActResBlock (model.py:138-178)."""
+
+    def __init__(self, m):
+        self.bn1, self.conv1 = BN(m.bn1), Conv(m.conv1)
+        self.bn2, self.conv2 = BN(m.bn2), Conv(m.conv2)
+        self.proj = len(m.shortcut) > 0
+        if self.proj:
+            self.sconv, self.sbn = Conv(m.shortcut[0]), BN(m.shortcut[1])
+
+    def convs(self):
+        return [self.conv1, self.conv2] + ([self.sconv] if self.proj else [])
+
+    def fwd(self, x):
+        self.x = x
+        self.o = self.bn1.fwd(x, relu=True)
+        sc = self.sbn.fwd(self.sconv.fwd(self.o)) if self.proj else x
+        self.a2 = self.bn2.fwd(self.conv1.fwd(self.o), relu=True)
+        return self.conv2.fwd(self.a2, res=sc)
+
+    def bwd(self, g, gx):
+        dev = g.t.device
+        g_a2 = Act.new(self.a2.B, self.a2.H, self.a2.W, self.a2.C, dev)
+        self.conv2.bwd(self.a2, g, g_a2)
+        relu_mask(g_a2, self.a2)
+        g_c1 = Act.new(g_a2.B, g_a2.H, g_a2.W, g_a2.C, dev)
+        self.bn2.bwd(g_a2, g_c1)
+        g_o = Act.new(self.o.B, self.o.H, self.o.W, self.o.C, dev)
+        self.conv1.bwd(self.o, g_c1, g_o)
+        if self.proj:
+            g_cs = Act.new(g.B, g.H, g.W, self.sconv.Cout, dev)
+            self.sbn.bwd(g, g_cs)
+            self.sconv.bwd(self.o, g_cs, g_o)
+        else:
+            add_into(gx, g)
+        relu_mask(g_o, self.o)
+        self.bn1.bwd(g_o, gx)
+
+
+class ASPPT:
+    """ASPPModule (model.py:181-251); Dropout(0.1) mask from a counter hash."""
+
+    def __init__(self, m, dropout_mask_fn=None):
+        self.c1, self.b1 = Conv(m.conv1x1[0]), BN(m.conv1x1[1])
+        self.br = [(Conv(s[0]), BN(s[1])) for s in m.aspp_branches]
+        self.gc, self.gb = Conv(m.global_pool[1]), BN(m.global_pool[2])
+        self.fc, self.fb = Conv(m.fusion[0]), BN(m.fusion[1])
+        self.p = m.fusion[3].p
+        self.C = self.c1.Cout
+        self.seed = 0
+
+    def convs(self):
+        return [self.c1, self.gc, self.fc] + [c for c, _ in self.br]
+
+    def fwd(self, x):
+        dev = x.t.device
+        C, nb = self.C, len(self.br) + 2
+        self.x = x
+        cat = Act.new(x.B, x.H, x.W, C * nb, dev, fresh=False)
+        self.cat = cat
+        self.b1.fwd(self.c1.fwd(x), relu=True, out=cat.slice(0, C))
+        for i, (cv, bn) in enumerate(self.br):
+            bn.fwd(cv.fwd(x), relu=True, out=cat.slice(C * (i + 1), C))
+        # global branch: mean -> 1x1 -> BN (over the batch) -> ReLU -> broadcast
+        self.gm = Act.new(x.B, 1, 1, x.C, dev, fresh=False)
+        _chk(L.lib().upr_t_pixel_sum(x.ptr(), x.B, x.H * x.W, x.C, x.cs, 0, ctypes.c_float(1.0 / (x.H * x.W)),
+                                     _fp(self.gm.t), 0, _stream()), "gap")
+        self.gp = self.gb.fwd(self.gc.fwd(self.gm), relu=True)
+        _chk(L.lib().upr_t_broadcast(_fp(self.gp.t), x.B, x.H * x.W, C, ctypes.c_float(1.0), _fp(cat.t), cat.cs,
+                                     C * (nb - 1), 0, _stream()), "broadcast")
+        self.a = self.fb.fwd(self.fc.fwd(cat), relu=True)
+        out = Act.new(x.B, x.H, x.W, C, dev, fresh=False)
+        self.mask = torch.empty((out.t.numel(),), dtype=torch.uint8, device=dev)
+        self.seed += 1
+        pointwise(self.a.t, None, out.t, out.t.numel(), 2, mask_out=self.mask, p=self.p,
+                  seed=(id(self) & 0xffffffff) * 1000003 + self.seed)
+        return out
+
+    def bwd(self, g, gx):
+        dev = g.t.device
+        C, nb, x = self.C, len(self.br) + 2, self.x
+        g_a = Act.new(g.B, g.H, g.W, C, dev, fresh=False)
+        pointwise(g.t, None, g_a.t, g.t.numel(), 3, mask_in=self.mask, p=self.p)
+        relu_mask(g_a, self.a)
+        g_cf = Act.new(g.B, g.H, g.W, C, dev)
+        self.fb.bwd(g_a, g_cf)
+        g_cat = Act.new(g.B, g.H, g.W, C * nb, dev)
+        self.fc.bwd(self.cat, g_cf, g_cat)
+        # global branch
+        g_gp = Act.new(x.B, 1, 1, C, dev, fresh=False)
+        _chk(L.lib().upr_t_pixel_sum(_fp(g_cat.t), x.B, x.H * x.W, C, g_cat.cs, C * (nb - 1), ctypes.c_float(1.0),
+                                     _fp(g_gp.t), 0, _stream()), "gsum")
+        relu_mask(g_gp, self.gp)
+        g_gc = Act.new(x.B, 1, 1, C, dev)
+        self.gb.bwd(g_gp, g_gc)
+        g_gm = Act.new(x.B, 1, 1, x.C, dev)
+        self.gc.bwd(self.gm, g_gc, g_gm)
+        # conv branches (the first one initialises gx)
+        for i, (cv, bn) in enumerate([(self.c1, self.b1)] + self.br):
+            gs = g_cat.slice(C * i, C)
+            relu_mask(gs, self.cat.slice(C * i, C))
+            g_c = Act.new(g.B, g.H, g.W, C, dev)
+            bn.bwd(gs, g_c)
+            cv.bwd(x, g_c, gx)
+        acc = gx.consume_fresh()
+        _chk(L.lib().upr_t_broadcast(_fp(g_gm.t), x.B, x.H * x.W, x.C, ctypes.c_float(1.0 / (x.H * x.W)), gx.ptr(),
+                                     gx.cs, 0, acc, _stream()), "broadcast_bwd")
+
+
+class UpBlockT:
+    """UpBlock (model.py:254-274) + the caller's skip add (model.py:346-348)."""
+
+    def __init__(self, m):
+        self.up = ConvT(m.up)
+        self.c1, self.b1 = Conv(m.conv[0]), BN(m.conv[1])
+        self.c2, self.b2 = Conv(m.conv[3]), BN(m.conv[4])
+
+    def convs(self):
+        return [self.up, self.c1, self.c2]
+
+    def fwd(self, x, skip):
+        self.x = x
+        self.u = self.up.fwd(x)
+        self.a1 = self.b1.fwd(self.c1.fwd(self.u), relu=True)
+        self.a2 = self.b2.fwd(self.c2.fwd(self.a1), relu=True)
+        out = Act.new(self.a2.B, self.a2.H, self.a2.W, self.a2.C, x.t.device, fresh=False)
+        pointwise(self.a2.t, skip.t, out.t, out.t.numel(), 4)
+        return out
+
+    def bwd(self, g, gx, g_skip):
+        dev = g.t.device
+        add_into(g_skip, g)
+        relu_mask(g, self.a2)
+        g_c2 = Act.new(g.B, g.H, g.W, g.C, dev)
+        self.b2.bwd(g, g_c2)
+        g_a1 = Act.new(g.B, g.H, g.W, g.C, dev)
+        self.c2.bwd(self.a1, g_c2, g_a1)
+        relu_mask(g_a1, self.a1)
+        g_c1 = Act.new(g.B, g.H, g.W, g.C, dev)
+        self.b1.bwd(g_a1, g_c1)
+        g_u = Act.new(g.B, g.H, g.W, g.C, dev)
+        self.c1.bwd(self.u, g_c1, g_u)
+        self.up.bwd(self.x, g_u, gx)
+
+
+class FAMT:
+    """EnhancedFAM (model.py:11-97)."""
+
+    def __init__(self, m):
+        self.b1 = Conv(m.branch1)
+        self.b2 = Conv(m.branch2_conv)
+        self.b3a, self.b3b = Conv(m.branch3_conv1), Conv(m.branch3_conv2)
+        self.b4a, self.b4b = Conv(m.branch4_conv1), Conv(m.branch4_conv2)
+        self.fu = Conv(m.fusion)
+        self.ca1, self.ca2 = Conv(m.channel_attention[1]), Conv(m.channel_attention[3])
+        self.sa = Conv(m.spatial_attention[0])
+
+    def convs(self):
+        return [self.b1, self.b2, self.b3a, self.b3b, self.b4a, self.b4b, self.fu, self.ca1, self.ca2, self.sa]
+
+    def fwd(self, x):
+        dev = x.t.device
+        lib, st = L.lib(), _stream()
+        C = self.fu.Cout
+        B, H, W = x.B, x.H, x.W
+        HW = H * W
+        self.x = x
+        cat = Act.new(B, H, W, 4 * C, dev, fresh=False)
+        self.cat = cat
+        self.b1.fwd(x, out=cat.slice(0, C))
+        self.mp = Act.new(B, H, W, x.C, dev, fresh=False)
+        _chk(lib.upr_t_maxpool(ctypes.byref(x.view()), B, H, W, x.C, 3, 1, 1, ctypes.byref(self.mp.view()), H, W, st),
+             "maxpool")
+        self.b2.fwd(self.mp, out=cat.slice(C, C))
+        self.t3 = self.b3a.fwd(x, relu=True)
+        self.b3b.fwd(self.t3, out=cat.slice(2 * C, C))
+        self.t4 = self.b4a.fwd(x, relu=True)
+        self.b4b.fwd(self.t4, out=cat.slice(3 * C, C))
+        self.o = self.fu.fwd(cat, relu=True)
+        self.pool = Act.new(B, 1, 1, C, dev, fresh=False)
+        _chk(lib.upr_t_pixel_sum(_fp(self.o.t), B, HW, C, C, 0, ctypes.c_float(1.0 / HW), _fp(self.pool.t), 0, st),
+             "gap")
+        self.h1 = self.ca1.fwd(self.pool, relu=True)
+        z = self.ca2.fwd(self.h1)
+        self.ca = empty((B, C), dev)
+        pointwise(z.t, None, self.ca, B * C, 0)
+        self.o2 = empty((B, H, W, C), dev)
+        self.m = Act.new(B, H, W, 2, dev, fresh=False)
+        _chk(lib.upr_t_fam_ca_apply(_p(self.o.t), _p(self.ca), B, HW, C, _p(self.o2), _fp(self.m.t), st), "ca_apply")
+        s_pre = self.sa.fwd(self.m)
+        self.sav = empty((B, H, W), dev)
+        out = Act.new(B, H, W, C, dev, fresh=False)
+        _chk(lib.upr_t_fam_sa_apply(_p(self.o2), _fp(s_pre.t), B, HW, C, _p(self.sav), _fp(out.t), st), "sa_apply")
+        return out
+
+    def bwd(self, g, gx):
+        """g: contiguous Act [B,H,W,32]; gx receives the input gradient."""
+        dev = g.t.device
+        lib, st = L.lib(), _stream()
+        B, H, W, C = g.B, g.H, g.W, self.fu.Cout
+        HW = H * W
+        g_o2 = empty((B, H, W, C), dev)
+        g_s = Act.new(B, H, W, 1, dev, fresh=False)
+        _chk(lib.upr_t_fam_sa_bwd(_fp(g.t), _p(self.o2), _p(self.sav), B, HW, C, _p(g_o2), _fp(g_s.t), st), "sa_bwd")
+        g_m = Act.new(B, H, W, 2, dev)
+        self.sa.bwd(self.m, g_s, g_m)
+        g_o = Act.new(B, H, W, C, dev, fresh=False)
+        g_ca = empty((B, C), dev)
+        _chk(lib.upr_t_fam_ca_bwd(_p(g_o2), _fp(g_m.t), _fp(self.o.t), _p(self.o2), _p(self.ca), B, HW, C, _fp(g_o.t),
+                                  _p(g_ca), st), "ca_bwd")
+        g_z = Act.new(B, 1, 1, C, dev, fresh=False)
+        pointwise(g_ca, self.ca, g_z.t, B * C, 1)
+        g_h1 = Act.new(B, 1, 1, self.h1.C, dev)
+        self.ca2.bwd(self.h1, g_z, g_h1)
+        relu_mask(g_h1, self.h1)
+        g_pool = Act.new(B, 1, 1, C, dev)
+        self.ca1.bwd(self.pool, g_h1, g_pool)
+        _chk(lib.upr_t_fam_pool_bwd(_fp(g_o.t), _fp(g_pool.t), _fp(self.o.t), B, HW, C, st), "pool_bwd")
+        g_cat = Act.new(B, H, W, 4 * C, dev)
+        self.fu.bwd(self.cat, g_o, g_cat)
+        self.b1.bwd(self.x, g_cat.slice(0, C), gx)
+        g_mp = Act.new(B, H, W, self.x.C, dev)
+        self.b2.bwd(self.mp, g_cat.slice(C, C), g_mp)
+        gx.zero_if_fresh()
+        _chk(lib.upr_t_maxpool_bwd(ctypes.byref(self.x.view()), ctypes.byref(g_mp.view()), B, H, W, self.x.C, 3, 1, 1,
+                                   H, W, ctypes.byref(gx.view()), st), "maxpool_bwd")
+        for (ca_, cb_, t) in ((self.b3a, self.b3b, self.t3), (self.b4a, self.b4b, self.t4)):
+            k = 2 if cb_ is self.b3b else 3
+            g_t = Act.new(B, H, W, t.C, dev)
+            cb_.bwd(t, g_cat.slice(k * C, C), g_t)
+            relu_mask(g_t, t)
+            ca_.bwd(self.x, g_t, gx)
+
+
+class IENetT:
+    """ResidualIENet (model.py:277-360)."""
+
+    def __init__(self, m):
+        Blk = PreActResBlockT if m._use_preact else ResBlockT
+        self.inp = Conv(m.input_layer)
+        self.enc = [Blk(m.enc1), Blk(m.enc2), Blk(m.enc3)]
+        self.mid = []
+        for sub in m.bottleneck:
+            self.mid.append(ASPPT(sub) if type(sub).__name__ == "ASPPModule" else Blk(sub))
+        self.dec = [UpBlockT(m.dec3), UpBlockT(m.dec2), UpBlockT(m.dec1)]
+        self.h0, self.h2 = Conv(m.residual_head[0]), Conv(m.residual_head[2])
+
+    def convs(self):
+        out = [self.inp, self.h0, self.h2]
+        for b in self.enc + self.mid + self.dec:
+            out += b.convs()
+        return out
+
+    def fwd(self, x):
+        B, _, H, W = x.shape
+        self.xin = (nchw_view(x), B, H, W)
+        self.x1 = self.inp.fwd(None, relu=True, x_view=self.xin, out=Act.new(B, H, W, 32, x.device, fresh=False))
+        self.x2 = self.enc[0].fwd(self.x1)
+        self.x3 = self.enc[1].fwd(self.x2)
+        self.x4 = self.enc[2].fwd(self.x3)
+        t = self.x4
+        self.mids = []
+        for b in self.mid:
+            self.mids.append(t)
+            t = b.fwd(t)
+        self.x5 = t
+        d3 = self.dec[0].fwd(self.x5, self.x3)
+        d2 = self.dec[1].fwd(d3, self.x2)
+        self.d1 = self.dec[2].fwd(d2, self.x1)
+        self.d3, self.d2 = d3, d2
+        self.h = self.h0.fwd(self.d1, relu=True)
+        r = self.h2.fwd(self.h)
+        illu = empty((B, 1, H, W), x.device)
+        _chk(L.lib().upr_t_head_fwd(_p(x), _fp(r.t), _p(illu), B, H, W, _stream()), "head")
+        return illu
+
+    def bwd(self, g_r):
+        """g_r: Act [B,H,W,1], gradient of the residual-head output."""
+        dev = g_r.t.device
+        B, H, W = g_r.B, g_r.H, g_r.W
+
+        def like(a):
+            return Act.new(a.B, a.H, a.W, a.C, dev)
+        g_h = like(self.h)
+        self.h2.bwd(self.h, g_r, g_h)
+        relu_mask(g_h, self.h)
+        g_d1 = like(self.d1)
+        self.h0.bwd(self.d1, g_h, g_d1)
+        g_x1, g_x2, g_x3 = like(self.x1), like(self.x2), like(self.x3)
+        g_d2, g_d3 = like(self.d2), like(self.d3)
+        self.dec[2].bwd(g_d1, g_d2, g_x1)
+        self.dec[1].bwd(g_d2, g_d3, g_x2)
+        g_t = like(self.x5)
+        self.dec[0].bwd(g_d3, g_t, g_x3)
+        for b, xin in zip(reversed(self.mid), reversed(self.mids)):
+            g_in = like(xin)
+            b.bwd(g_t, g_in)
+            g_t = g_in
+        self.enc[2].bwd(g_t, g_x3)
+        self.enc[1].bwd(g_x3, g_x2)
+        self.enc[0].bwd(g_x2, g_x1)
+        relu_mask(g_x1, self.x1)
+        self.inp.bwd(None, g_x1, None, x_view=self.xin)
+
+
+class UPRetinexTrainGraph:
+    """MultiScaleUP_Retinex.forward (model.py:415-455) in training mode and its
+    backward.  Built once per model; buffers are reallocated per step by the
+    caching allocator (torch.empty), weights re-packed per step."""
+
+    def __init__(self, model):
+        self.model = model
+        self.ie = IENetT(model.ie_net)
+        self.s1c, self.s1f = Conv(model.scale1[0]), FAMT(model.scale1[2])
+        self.s2c, self.s2f = Conv(model.scale2[1]), FAMT(model.scale2[3])
+        self.s3c, self.s3f = Conv(model.scale3[1]), FAMT(model.scale3[3])
+        self.fusion, self.outc = Conv(model.fusion), Conv(model.output_layer)
+        self._convs = self.ie.convs() + [self.s1c, self.s2c, self.s3c, self.fusion, self.outc] + \
+            self.s1f.convs() + self.s2f.convs() + self.s3f.convs()
+
+    def pack(self):
+        for c in self._convs:
+            c.pack()
+
+    def forward(self, x):
+        """x [B,3,H,W] fp32 NCHW (H, W multiples of 16) -> (enh, refl, illu)."""
+        lib, st = L.lib(), _stream()
+        B, _, H, W = x.shape
+        dev = x.device
+        self.x = x
+        self.pack()
+        illu = self.ie.fwd(x)
+        self.illu = illu
+        # pyramid (model.py:415-432): bilinear 0.5 / 0.25, max-pool 2 / 4
+        xv = nchw_view(x)
+        pyr = []
+        for f, k in ((2, 2), (4, 4)):
+            xs = Act.new(B, H // f, W // f, 3, dev, fresh=False)
+            _chk(lib.upr_t_bilinear(ctypes.byref(xv), B, H, W, 3, ctypes.byref(xs.view()), H // f, W // f, 0, st),
+                 "bilinear")
+            xp = Act.new(B, H // f // k, W // f // k, 3, dev, fresh=False)
+            _chk(lib.upr_t_maxpool(ctypes.byref(xs.view()), B, H // f, W // f, 3, k, k, 0, ctypes.byref(xp.view()),
+                                   H // f // k, W // f // k, st), "maxpool")
+            pyr.append(xp)
+        self.pyr = pyr
+        self.s1 = self.s1c.fwd(None, relu=True, x_view=(xv, B, H, W),
+                               out=Act.new(B, H, W, 32, dev, fresh=False))
+        f1 = self.s1f.fwd(self.s1)
+        self.s2 = self.s2c.fwd(pyr[0], relu=True)
+        f2 = self.s2f.fwd(self.s2)
+        self.s3 = self.s3c.fwd(pyr[1], relu=True)
+        f3 = self.s3f.fwd(self.s3)
+        fused = Act.new(B, H, W, 96, dev, fresh=False)
+        _chk(lib.upr_t_copy(ctypes.byref(f1.view()), ctypes.byref(fused.slice(0, 32).view()), B, H, W, 32, 0, st),
+             "cat")
+        for i, f in enumerate((f2, f3)):
+            _chk(lib.upr_t_bilinear(ctypes.byref(f.view()), B, f.H, f.W, 32,
+                                    ctypes.byref(fused.slice(32 * (i + 1), 32).view()), H, W, 0, st), "upsample")
+        self.fused = fused
+        self.fz = self.fusion.fwd(fused)
+        o = self.outc.fwd(self.fz)
+        self.e = empty((B, H, W, 3), dev)
+        refl = empty((B, 3, H, W), dev)
+        enh = empty((B, 3, H, W), dev)
+        _chk(lib.upr_t_retinex_fwd(_p(x), _p(illu), _fp(o.t), _p(self.e), _p(refl), _p(enh), B, H, W, st),
+             "retinex")
+        self.refl, self.enh = refl, enh
+        self.f_hw = [(f2.H, f2.W), (f3.H, f3.W)]
+        return enh, refl, illu
+
+    def backward(self, g_enh, g_refl=None, g_illu=None):
+        """Accumulates every parameter gradient into the model's .grad views
+        (zeroed first by the caller)."""
+        lib, st = L.lib(), _stream()
+        x = self.x
+        B, _, H, W = x.shape
+        dev = x.device
+        g_o = Act.new(B, H, W, 3, dev, fresh=False)
+        g_r = Act.new(B, H, W, 1, dev, fresh=False)
+        _chk(lib.upr_t_retinex_bwd(_p(x), _p(self.illu), _p(self.e), _p(self.refl), _p(g_enh), _p(g_refl),
+                                   _p(g_illu), _fp(g_o.t), _fp(g_r.t), B, H, W, st), "retinex_bwd")
+        g_fz = Act.new(B, H, W, 32, dev)
+        self.outc.bwd(self.fz, g_o, g_fz)
+        g_fused = Act.new(B, H, W, 96, dev)
+        self.fusion.bwd(self.fused, g_fz, g_fused)
+        for (sc, sf, s_act, xin), i in zip(((self.s1c, self.s1f, self.s1, None),
+                                            (self.s2c, self.s2f, self.s2, self.pyr[0]),
+                                            (self.s3c, self.s3f, self.s3, self.pyr[1])), range(3)):
+            g_f = Act.new(s_act.B, s_act.H, s_act.W, 32, dev, fresh=False)
+            if i == 0:
+                _chk(lib.upr_t_copy(ctypes.byref(g_fused.slice(0, 32).view()), ctypes.byref(g_f.view()), B, H, W, 32, 0,
+                                    st), "split")
+            else:
+                zero(g_f.t)
+                _chk(lib.upr_t_bilinear_bwd(ctypes.byref(g_fused.slice(32 * i, 32).view()), B, g_f.H, g_f.W, 32, H, W,
+                                            ctypes.byref(g_f.view()), st), "upsample_bwd")
+            g_s = Act.new(s_act.B, s_act.H, s_act.W, 32, dev)
+            sf.bwd(g_f, g_s)
+            relu_mask(g_s, s_act)
+            if i == 0:
+                sc.bwd(None, g_s, None, x_view=(nchw_view(x), B, H, W))
+            else:
+                sc.bwd(xin, g_s, None)
+        self.ie.bwd(g_r)

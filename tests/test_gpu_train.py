@@ -1,0 +1,234 @@
+"""GPU parity of the HIP training path (include/upr_train.h, upr/train.py,
+upr/loss_engine.py, upr/optim.py) against the CPU oracle (oracle/train.py,
+oracle/net.py in train mode) and the reference goldens G6/G7.
+
+Tolerances (fp32 everywhere; differences are summation order only):
+  * op level (conv fwd / dgrad / wgrad, BatchNorm train fwd / bwd): max |d|
+    <= 1e-4 * max|ref| + 1e-6;
+  * loss terms rel 1e-4, loss gradients max |d| <= 1e-4 * max|ref|;
+  * full step: loss dict rel 1e-4, per-parameter gradient L2 norms rel 1e-3
+    and max |d| <= 2e-3 * max|ref| (BatchNorm over B=2 at 64x64 amplifies
+    reduction-order noise), parameter deltas after Adam rel 1e-3, BatchNorm
+    running stats <= 1e-4.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import has_gpu
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not has_gpu(), reason="needs a ROCm device")]
+
+DEV = "cuda"
+VGG_SEED = 1234
+
+
+def _close(a, b, rel, what):
+    a = a.detach().float().cpu()
+    b = b.detach().float().cpu()
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    err = (a - b).abs().max().item()
+    tol = rel * max(b.abs().max().item(), 1e-12) + 1e-6
+    assert err <= tol, f"{what}: max|d| {err:.3e} > {tol:.3e}"
+
+
+def _act(t_nhwc):
+    from upr.train import Act
+    return Act(t_nhwc.contiguous())
+
+
+@pytest.mark.parametrize("cin,cout,k,s,p,d,bias", [
+    (32, 64, 3, 2, 1, 1, False),    # encoder conv1 (stride 2)
+    (64, 64, 3, 1, 1, 1, False),    # encoder conv2
+    (32, 64, 1, 2, 0, 1, False),    # projecting shortcut
+    (32, 32, 3, 1, 2, 2, True),     # FAM branch4_conv2 (dilation 2)
+    (256, 256, 3, 1, 6, 6, False),  # ASPP d6
+    (3, 32, 3, 1, 1, 1, True),      # input layer (direct)
+    (32, 3, 1, 1, 0, 1, True),      # output layer (direct)
+    (2, 1, 7, 1, 3, 1, True),       # spatial attention (direct)
+])
+def test_conv_layer(cin, cout, k, s, p, d, bias):
+    from upr.train import Act, Conv
+    torch.manual_seed(0)
+    m = torch.nn.Conv2d(cin, cout, k, stride=s, padding=p, dilation=d, bias=bias)
+    H = W = 16 if cin >= 256 else 24
+    x = torch.randn(2, cin, H, W)
+    gy_shape = m(x).shape
+    gy = torch.randn(gy_shape)
+    xr = x.clone().requires_grad_(True)
+    y = m(xr)
+    y.backward(gy)
+    md = torch.nn.Conv2d(cin, cout, k, stride=s, padding=p, dilation=d, bias=bias).to(DEV)
+    md.load_state_dict(m.state_dict())
+    md.weight.grad = torch.zeros_like(md.weight)
+    if bias:
+        md.bias.grad = torch.zeros_like(md.bias)
+    c = Conv(md)
+    c.pack()
+    xa = Act(x.permute(0, 2, 3, 1).contiguous().to(DEV))
+    ya = c.fwd(xa)
+    _close(ya.t.permute(0, 3, 1, 2), y, 1e-4, "fwd")
+    gya = Act(gy.permute(0, 2, 3, 1).contiguous().to(DEV))
+    gxa = Act.new(2, H, W, cin, DEV)
+    c.bwd(xa, gya, gxa)
+    torch.cuda.synchronize()
+    _close(gxa.t.permute(0, 3, 1, 2), xr.grad, 1e-4, "dgrad")
+    _close(md.weight.grad, m.weight.grad, 1e-4, "wgrad")
+    if bias:
+        _close(md.bias.grad, m.bias.grad, 1e-4, "dbias")
+
+
+def test_convT_layer():
+    from upr.train import Act, ConvT
+    torch.manual_seed(1)
+    m = torch.nn.ConvTranspose2d(64, 32, 2, 2)
+    x = torch.randn(2, 64, 12, 12)
+    xr = x.clone().requires_grad_(True)
+    y = m(xr)
+    gy = torch.randn(y.shape)
+    y.backward(gy)
+    md = torch.nn.ConvTranspose2d(64, 32, 2, 2).to(DEV)
+    md.load_state_dict(m.state_dict())
+    md.weight.grad = torch.zeros_like(md.weight)
+    md.bias.grad = torch.zeros_like(md.bias)
+    c = ConvT(md)
+    c.pack()
+    xa = Act(x.permute(0, 2, 3, 1).contiguous().to(DEV))
+    ya = c.fwd(xa)
+    _close(ya.t.permute(0, 3, 1, 2), y, 1e-4, "fwd")
+    gxa = Act.new(2, 12, 12, 64, DEV)
+    c.bwd(xa, Act(gy.permute(0, 2, 3, 1).contiguous().to(DEV)), gxa)
+    torch.cuda.synchronize()
+    _close(gxa.t.permute(0, 3, 1, 2), xr.grad, 1e-4, "dgrad")
+    _close(md.weight.grad, m.weight.grad, 1e-4, "wgrad")
+    _close(md.bias.grad, m.bias.grad, 1e-4, "dbias")
+
+
+def test_batchnorm_train():
+    from upr.train import Act, BN, relu_mask
+    torch.manual_seed(2)
+    m = torch.nn.BatchNorm2d(64)
+    with torch.no_grad():
+        m.weight.uniform_(0.5, 1.5)
+        m.bias.uniform_(-0.2, 0.2)
+    md = torch.nn.BatchNorm2d(64).to(DEV)
+    md.load_state_dict(m.state_dict())
+    md.weight.grad = torch.zeros_like(md.weight)
+    md.bias.grad = torch.zeros_like(md.bias)
+    x = torch.randn(2, 64, 20, 20) * 2 + 0.5
+    xr = x.clone().requires_grad_(True)
+    y = torch.relu(m.train()(xr))
+    gy = torch.randn(y.shape)
+    y.backward(gy)
+    bn = BN(md)
+    xa = Act(x.permute(0, 2, 3, 1).contiguous().to(DEV))
+    ya = bn.fwd(xa, relu=True)
+    _close(ya.t.permute(0, 3, 1, 2), y, 1e-4, "bn fwd")
+    g = Act(gy.permute(0, 2, 3, 1).contiguous().to(DEV))
+    relu_mask(g, ya)
+    gx = Act.new(2, 20, 20, 64, DEV)
+    bn.bwd(g, gx)
+    torch.cuda.synchronize()
+    _close(gx.t.permute(0, 3, 1, 2), xr.grad, 1e-4, "bn dgrad")
+    _close(md.weight.grad, m.weight.grad, 1e-4, "dgamma")
+    _close(md.bias.grad, m.bias.grad, 1e-4, "dbeta")
+    _close(md.running_mean, m.running_mean, 1e-5, "running_mean")
+    _close(md.running_var, m.running_var, 1e-5, "running_var")
+    assert int(md.num_batches_tracked) == 1
+
+
+def test_loss_terms_and_grads(golden):
+    """G6 inputs on the device vs the reference's loss values and gradients."""
+    from losses.loss import TotalLoss
+    g = golden("g6_losses.npz")
+    low, enh, illu, refl = (torch.from_numpy(g[k]).to(DEV) for k in ("low", "enh", "illu", "refl"))
+    crit = TotalLoss(use_freq_loss=True).to(DEV)
+    e = enh.clone().requires_grad_(True)
+    i = illu.clone().requires_grad_(True)
+    r = refl.clone().requires_grad_(True)
+    total, d = crit(low, e, i, r)
+    for k in ("exposure", "smoothness", "color", "spatial", "decouple", "perceptual", "frequency", "total"):
+        np.testing.assert_allclose(d[k], float(g["dict_" + k]), rtol=1e-4, atol=1e-8, err_msg=k)
+    total.backward()
+    torch.cuda.synchronize()
+    for name, t in (("grad_enh", e), ("grad_illu", i), ("grad_refl", r)):
+        _close(t.grad, torch.from_numpy(g[name]), 1e-4, name)
+
+
+def _model(pre, aspp, seed=0):
+    from models.model import UP_Retinex
+    torch.manual_seed(seed)
+    return UP_Retinex(use_preact=pre, use_aspp=aspp)
+
+
+def test_train_step_matches_reference_g7(golden):
+    """One trainers/train.py step body (plain model, seed 0, B=2 64x64) vs the
+    reference's own step recorded in G7."""
+    from losses.loss import TotalLoss
+    from trainers.train import make_optimizer, train_step
+    g = golden("g7_train_step.npz")
+    model = _model(False, False).to(DEV)
+    sd0 = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    model.train()
+    crit = TotalLoss(use_freq_loss=True).to(DEV)
+    opt = make_optimizer(model, lr=1e-4, weight_decay=1e-5)
+    x = torch.from_numpy(g["x"]).to(DEV)
+    loss, d = train_step(model, x, crit, opt)
+    torch.cuda.synchronize()
+    for k in ("total", "exposure", "smoothness", "color", "spatial", "decouple", "perceptual", "frequency"):
+        np.testing.assert_allclose(d[k], float(g["dict_" + k]), rtol=1e-4, atol=1e-9, err_msg=k)
+    names = [str(n) for n in g["param_names"]]
+    params = dict(model.named_parameters())
+    norm = float(g["clip_norm"])
+    coef = min(1.0, 1.0 / (norm + 1e-6))
+    gn = np.array([float(params[n].grad.norm()) * coef for n in names])
+    np.testing.assert_allclose(gn, g["grad_norm"], rtol=1e-3, atol=1e-10)
+    for n in names:
+        key = "grad/" + n
+        if key in g.files:
+            _close(params[n].grad * coef, torch.from_numpy(g[key]), 2e-3, key)
+    sd = model.state_dict()
+    dn = np.array([float((sd[n].cpu() - sd0[n].cpu()).norm()) for n in names])
+    np.testing.assert_allclose(dn, g["delta_norm"], rtol=1e-3, atol=1e-11)
+    for k in g["buf_names"]:
+        _close(sd[str(k)], torch.from_numpy(g["buf/" + str(k)]), 1e-4, str(k))
+
+
+@pytest.mark.parametrize("pre,aspp", [(True, False), (False, True), (True, True)])
+def test_train_grads_variants_vs_oracle(pre, aspp):
+    """Training-mode forward + backward of the other variants vs the oracle
+    (oracle/net.py train mode + oracle/train.py losses), the ASPP Dropout mask
+    replayed from the device."""
+    from oracle import train as otrain
+    from losses.loss import TotalLoss
+    model = _model(pre, aspp, seed=3)
+    sd_cpu = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    model = model.to(DEV).train()
+    crit = TotalLoss(use_freq_loss=True).to(DEV)
+    x = torch.rand(2, 3, 64, 64, generator=torch.Generator().manual_seed(5)) * 0.6
+    enh, refl, illu = model(x.to(DEV))
+    total, d = crit(x.to(DEV), enh, illu, refl)
+    st = model.__dict__["_upr_train"]
+    total.backward()
+    torch.cuda.synchronize()
+    masks = []
+    if aspp:
+        asp = [b for b in st["graph"].ie.mid if type(b).__name__ == "ASPPT"][0]
+        masks.append(asp.mask.cpu().view(2, 64 // 8, 64 // 8, 256).permute(0, 3, 1, 2).float())
+    it = iter(masks)
+    names = otrain.param_names(sd_cpu)
+    params = {k: sd_cpu[k].clone().requires_grad_(True) for k in names}
+    work = dict(sd_cpu)
+    work.update(params)
+    from oracle import net as onet
+    with otrain.train_mode(dropout_mask=lambda shape: next(it)):
+        e_r, r_r, i_r = onet.forward(work, x, pre, aspp)
+    vgg = otrain.vgg19_state(VGG_SEED)
+    t_r, d_r = otrain.total_loss(vgg, x, e_r, i_r, r_r)
+    t_r.backward()
+    _close(enh, e_r, 1e-4, "enh")
+    _close(illu, i_r, 1e-4, "illu")
+    np.testing.assert_allclose(d["total"], d_r["total"], rtol=1e-4)
+    dev_params = dict(model.named_parameters())
+    for n in names:
+        _close(dev_params[n].grad, params[n].grad, 3e-3, "grad " + n)
