@@ -12,10 +12,13 @@ from upr import _lib as L
 from upr import runtime
 
 
-def header_functions():
-    src = open(os.path.join(REPO, "include", "upr.h")).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(upr_[a-z0-9_]+)\s*\(", src)))
+def header_functions(headers=("upr.h", "upr_train.h")):
+    names = set()
+    for h in headers:
+        src = open(os.path.join(REPO, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names |= set(re.findall(r"\b(upr_[a-z0-9_]+)\s*\(", src))
+    return sorted(names)
 
 
 def test_library_builds_and_loads():
@@ -25,7 +28,7 @@ def test_library_builds_and_loads():
 
 def test_exports_every_header_symbol():
     names = header_functions()
-    assert len(names) >= 15
+    assert len(names) >= 60
     cdll = ctypes.CDLL(L.LIB_PATH)
     for n in names:
         assert hasattr(cdll, n), f"{n} declared in include/upr.h but not exported"
@@ -56,3 +59,13 @@ def test_null_args_rejected_without_device():
         == L.UPR_ERR_ARG
     out = ctypes.c_void_p()
     assert lib.upr_model_create(None, 0, 0, 0, 7, 0, ctypes.byref(out)) == L.UPR_ERR_ARG
+    # training entries (include/upr_train.h) validate before touching the device
+    assert lib.upr_t_conv_mfma(None, 1, 8, 8, 32, 32, 0, None, None, 32, 3, 3, 1, 1, 1, None, 0, 0, None, 32, 0, 0,
+                               None) == L.UPR_ERR_ARG
+    assert lib.upr_t_conv_wgrad(None, 1, 8, 8, 31, 31, 0, None, 8, 8, 32, 32, 0, 3, 3, 1, 1, 1, None,
+                                None) == L.UPR_ERR_ARG
+    assert lib.upr_t_adam(None, None, None, None, 10, None, 1.0, 1e-4, 0.9, 0.999, 1e-8, 0.0, 1, None,
+                          None) == L.UPR_ERR_ARG
+    assert lib.upr_t_loss_workspace(2, 64, 64) > 0
+    assert lib.upr_t_loss_workspace(2, 8, 8) == 0
+    assert lib.upr_t_pointwise(None, None, None, 4, 0, None, None, 0.0, 0, None) == L.UPR_ERR_ARG
