@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events")
     ap.add_argument("--breakdown", action="store_true", help="print per-layer stats to stderr")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC traffic passes")
+    ap.add_argument("--train", action="store_true",
+                    help="configs[4]: one training step (fwd + TotalLoss + bwd + clip + Adam) per step, "
+                         "bs=8 512x512 plain model (batch/size overridable)")
     return ap.parse_args()
 
 
@@ -128,8 +131,97 @@ def pmc_traffic(args):
             "launches_per_forward": n_launch / 2.0}
 
 
+TRAIN_GFLOP_PER_IMG = 668.0  # model fwd+bwd + VGG19 fwd x2 + dgrad, 512x512
+
+
+def cpu_train_baseline(sd, size, budget_s):
+    """Oracle training step (oracle/train.py, torch-CPU fp32) on 1 image until the budget is spent."""
+    from oracle import train as otrain
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    vgg = otrain.vgg19_state(1234)
+    x = torch.rand(1, 3, size, size, generator=torch.Generator().manual_seed(98))
+    n, t0 = 0, time.perf_counter()
+    while True:
+        sdc = {k: v.clone() for k, v in sd.items()}
+        otrain.train_step(sdc, vgg, x, False, False)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or n >= 16:
+            break
+    return {"value": n / el, "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{n} x 1x3x{size}x{size} training steps of oracle/train.py (torch-CPU autograd), {el:.1f}s"}
+
+
+def train_main(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    from models.model import UP_Retinex
+    from losses.loss import TotalLoss
+    from trainers.train import make_optimizer, train_step
+    B = args.batch if args.batch != 32 else 8
+    S = args.size
+    torch.manual_seed(0)
+    model = UP_Retinex(use_preact=args.variant == "preact_aspp", use_aspp=args.variant == "preact_aspp")
+    sd_cpu = {k: v.clone() for k, v in model.state_dict().items()}
+    model = model.to(dev).train()
+    crit = TotalLoss(use_freq_loss=True).to(dev)
+    opt = make_optimizer(model, lr=1e-4, weight_decay=1e-5)
+    x = torch.rand(B, 3, S, S, generator=torch.Generator().manual_seed(2 + rank)).to(dev)
+    for _ in range(args.warmup):
+        train_step(model, x, crit, opt)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    d = None
+    for _ in range(args.steps):
+        _, d = train_step(model, x, crit, opt)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = t.item()
+    imgs = world * B * args.steps
+    gf = TRAIN_GFLOP_PER_IMG * (S / 512.0) ** 2
+    achieved = gf * B * args.steps / elapsed / 1e3
+    out = {
+        "metric": f"train images/sec at {S}x{S} bs={B} (UP-Retinex fwd + TotalLoss + bwd + clip + Adam)",
+        "value": imgs / elapsed, "unit": "images/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic torch.rand inputs, random-init weights (seed 0), seeded random-init VGG19 (seed 1234)",
+        "config": {"workload": f"configs[4]: bs={B}/GPU {S}x{S} {args.variant} train step (fp32; AMP flag "
+                               f"computes in fp32 here)", "global_batch": world * B, "image_size": S,
+                   "variant": args.variant, "parallelism": f"data-parallel x{world} (per-rank shard)"},
+        "last_loss": d,
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_TFLOPS["fp32"], "unit": "TFLOP/s",
+                     "frac": achieved / PEAK_TFLOPS["fp32"], "traffic": None,
+                     "kernel": "whole training step (algorithmic 668 GF/img at 512^2 over step time)"},
+    }
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        out["cpu_baseline"] = cpu_train_baseline(sd_cpu, S, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out))
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.train:
+        return train_main(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

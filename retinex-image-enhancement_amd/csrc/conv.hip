@@ -49,9 +49,9 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return base + idx;
 }
 
-template <typename T, int WAVES_M, int WAVES_N, int WM, int WN>
+template <typename T, int WAVES_M, int WAVES_N, int WM, int WN, int BK>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvOp op) {
-  constexpr int BK = 32;
+  static_assert(BK == 32 || (BK == 64 && sizeof(T) == 2), "BK 64 is the fp16 variant");
   constexpr int EPC = Frag<T>::EPC;
   constexpr int CH = BK / EPC;              // 16-byte chunks per row of a K step
   constexpr int ROWS_PASS = 256 / CH;
@@ -60,9 +60,10 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvOp op) {
   constexpr int A_IT = BM / ROWS_PASS;
   constexpr int B_IT = (BN * CH + 255) / 256;
   // LDS row stride: fp32 10 x 16 B with the k-permutation {g, g+4} below, fp16
-  // 6 x 16 B: the fragment reads (16 rows x 4 chunks per ds_read_b128) are then
-  // bank-conflict free (same analysis as conv_halo.hip)
-  constexpr int LDS_ROW = sizeof(T) == 4 ? 40 : 48;
+  // 6 x 16 B (BK 32) / 9 x 16 B (BK 64): the fragment reads (16 rows x 4
+  // chunks per ds_read_b128) are then bank-conflict free (row r starts at bank
+  // 36r mod 64 for the 144-byte rows: 16 distinct multiples of 4)
+  constexpr int LDS_ROW = sizeof(T) == 4 ? 40 : (BK == 64 ? 72 : 48);
   static_assert(A_IT >= 1, "tile too small");
 
   __shared__ __attribute__((aligned(16))) T As[BM * LDS_ROW];
@@ -229,18 +230,21 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvOp op) {
             acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[a][j >> 2][j & 3], bf[b][j >> 2][j & 3],
                                                             acc[a][b], 0, 0, 0);
     } else {
-      f16x8 af[WM], bf[WN];
 #pragma unroll
-      for (int a = 0; a < WM; ++a)
-        af[a] = *(const f16x8*)((const half_t*)As + (wm * WM * 16 + a * 16 + fr) * LDS_ROW + fk);
+      for (int kk = 0; kk < BK / 32; ++kk) {
+        f16x8 af[WM], bf[WN];
 #pragma unroll
-      for (int b = 0; b < WN; ++b)
-        bf[b] = *(const f16x8*)((const half_t*)Bs + (wn * WN * 16 + b * 16 + fr) * LDS_ROW + fk);
-#pragma unroll
-      for (int a = 0; a < WM; ++a)
+        for (int a = 0; a < WM; ++a)
+          af[a] = *(const f16x8*)((const half_t*)As + (wm * WM * 16 + a * 16 + fr) * LDS_ROW + kk * 32 + fk);
 #pragma unroll
         for (int b = 0; b < WN; ++b)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a], bf[b], acc[a][b], 0, 0, 0);
+          bf[b] = *(const f16x8*)((const half_t*)Bs + (wn * WN * 16 + b * 16 + fr) * LDS_ROW + kk * 32 + fk);
+#pragma unroll
+        for (int a = 0; a < WM; ++a)
+#pragma unroll
+          for (int b = 0; b < WN; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a], bf[b], acc[a][b], 0, 0, 0);
+      }
     }
   }
 
@@ -342,15 +346,30 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvOp op) {
   }
 }
 
-template <typename T, int WAVES_M, int WAVES_N, int WM, int WN>
+template <typename T, int WAVES_M, int WAVES_N, int WM, int WN, int BK = 32>
 static int launch_cfg(const ConvOp& op, hipStream_t stream) {
   constexpr int BM = WAVES_M * WM * 16;
   constexpr int BN = WAVES_N * WN * 16;
   const int M = op.B * op.Ho * op.Wo;
   if (op.N % BN) return kErrShape;
   const int grid = ((M + BM - 1) / BM) * (op.N / BN);
-  hipLaunchKernelGGL((conv_igemm_kernel<T, WAVES_M, WAVES_N, WM, WN>), dim3(grid), dim3(256), 0, stream, op);
+  hipLaunchKernelGGL((conv_igemm_kernel<T, WAVES_M, WAVES_N, WM, WN, BK>), dim3(grid), dim3(256), 0, stream, op);
   return (int)hipGetLastError();
+}
+
+// fp16 with every segment a multiple of 64 channels: 64-deep K steps (half the
+// barriers and LDS round trips per MFMA; UPR_IGEMM_BK=32 forces the 32-deep
+// variant for A/B timing)
+static bool k64_ok(const ConvOp& op) {
+  static int force32 = -1;
+  if (force32 < 0) {
+    const char* e = getenv("UPR_IGEMM_BK");
+    force32 = (e && strcmp(e, "32") == 0) ? 1 : 0;
+  }
+  if (force32) return false;
+  for (int s = 0; s < op.nseg; ++s)
+    if (op.seg[s].C % 64) return false;
+  return true;
 }
 
 template <typename T>
@@ -358,6 +377,13 @@ static int launch_t(const ConvOp& op, hipStream_t stream) {
   if (op.store == kStoreHeadIllu) {
     if (op.N != 32) return kErrShape;
     return launch_cfg<T, 4, 1, 4, 2>(op, stream);
+  }
+  if constexpr (sizeof(T) == 2) {
+    if (k64_ok(op)) {
+      if (op.N % 128 == 0 && op.N >= 256) return launch_cfg<T, 2, 2, 4, 4, 64>(op, stream);
+      if (op.N % 64 == 0) return launch_cfg<T, 2, 2, 4, 2, 64>(op, stream);
+      if (op.N % 32 == 0) return launch_cfg<T, 4, 1, 4, 2, 64>(op, stream);
+    }
   }
   if (op.N % 128 == 0 && op.N >= 256) return launch_cfg<T, 2, 2, 4, 4>(op, stream);
   if (op.N % 64 == 0) return launch_cfg<T, 2, 2, 4, 2>(op, stream);
