@@ -149,7 +149,7 @@ def forward(sd, x, use_preact=None, use_aspp=None):
     """
     if use_preact is None or use_aspp is None:
         use_preact, use_aspp = variant_of(sd)
-    x = x.float()
+    x = x if x.dtype == torch.float64 else x.float()
     illu = ienet(sd, x, use_preact, use_aspp)
     refl = x / (illu + 1e-6)                                           # model.py:411-412
     x2 = F.interpolate(x, scale_factor=0.5, mode="bilinear", align_corners=False)

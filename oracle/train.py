@@ -78,8 +78,8 @@ def edge_map(img):
     """EdgeAwareSmoothnessLoss.compute_edge_map — loss.py:110-136."""
     gray = img.mean(1, keepdim=True) if img.shape[1] > 1 else img
     p = F.pad(gray, (1, 1, 1, 1), mode="reflect")
-    kx = torch.tensor(SOBEL_X).view(1, 1, 3, 3)
-    ky = torch.tensor(SOBEL_Y).view(1, 1, 3, 3)
+    kx = torch.tensor(SOBEL_X, dtype=img.dtype).view(1, 1, 3, 3)
+    ky = torch.tensor(SOBEL_Y, dtype=img.dtype).view(1, 1, 3, 3)
     gx = F.conv2d(p, kx)
     gy = F.conv2d(p, ky)
     return torch.sqrt(gx ** 2 + gy ** 2)
@@ -146,8 +146,8 @@ def vgg_features(vgg_sd, x):
 
 def perceptual_loss(vgg_sd, enh, low):
     """PerceptualLoss.forward — loss.py:221-255."""
-    mean = torch.tensor(VGG_MEAN).view(1, 3, 1, 1)
-    std = torch.tensor(VGG_STD).view(1, 3, 1, 1)
+    mean = torch.tensor(VGG_MEAN, dtype=enh.dtype).view(1, 3, 1, 1)
+    std = torch.tensor(VGG_STD, dtype=enh.dtype).view(1, 3, 1, 1)
     fe = vgg_features(vgg_sd, (enh - mean) / std)
     fl = vgg_features(vgg_sd, (low - mean) / std)
     return sum(F.mse_loss(a, b) for a, b in zip(fe, fl))
@@ -166,7 +166,7 @@ def frequency_loss(enh, low, w_high=1.0, w_low=0.5):
     """FrequencyLoss.forward — loss.py:447-487."""
     me = torch.abs(torch.fft.fft2(enh, dim=(-2, -1)))
     ml = torch.abs(torch.fft.fft2(low, dim=(-2, -1)))
-    hm, lm = freq_masks(enh.shape[2], enh.shape[3])
+    hm, lm = (m.to(enh.dtype) for m in freq_masks(enh.shape[2], enh.shape[3]))
     return w_high * F.mse_loss(me * hm, ml * hm) + w_low * F.mse_loss(me * lm, ml * lm)
 
 

@@ -182,14 +182,21 @@ def test_train_step_matches_reference_g7(golden):
     norm = float(g["clip_norm"])
     coef = min(1.0, 1.0 / (norm + 1e-6))
     gn = np.array([float(params[n].grad.norm()) * coef for n in names])
-    np.testing.assert_allclose(gn, g["grad_norm"], rtol=1e-3, atol=1e-10)
+    # conv biases feeding a BatchNorm have an exactly-zero true gradient: their
+    # norms are rounding noise in both implementations, hence the absolute floor
+    np.testing.assert_allclose(gn, g["grad_norm"], rtol=1e-3, atol=1e-6 * float(g["grad_norm"].max()))
     for n in names:
         key = "grad/" + n
         if key in g.files:
             _close(params[n].grad * coef, torch.from_numpy(g[key]), 2e-3, key)
     sd = model.state_dict()
     dn = np.array([float((sd[n].cpu() - sd0[n].cpu()).norm()) for n in names])
-    np.testing.assert_allclose(dn, g["delta_norm"], rtol=1e-3, atol=1e-11)
+    # Adam normalises each element by sqrt(v): a noise-level gradient (the
+    # BN-fed conv biases above) still moves its parameter by ~lr, so those are
+    # compared against the step size rather than relatively
+    noise = gn < 1e-6 * gn.max()
+    np.testing.assert_allclose(dn[~noise], g["delta_norm"][~noise], rtol=1e-3, atol=1e-11)
+    assert np.all(dn[noise] <= 1e-4 * np.sqrt([params[n].numel() for n in np.array(names)[noise]]) * 1.01)
     for k in g["buf_names"]:
         _close(sd[str(k)], torch.from_numpy(g["buf/" + str(k)]), 1e-4, str(k))
 
@@ -198,37 +205,59 @@ def test_train_step_matches_reference_g7(golden):
 def test_train_grads_variants_vs_oracle(pre, aspp):
     """Training-mode forward + backward of the other variants vs the oracle
     (oracle/net.py train mode + oracle/train.py losses), the ASPP Dropout mask
-    replayed from the device."""
+    replayed from the device.
+
+    Tolerance: the oracle is run in fp64 (the exact answer) and in fp32 (the
+    reference's own arithmetic).  Small-batch BatchNorm makes fp32 training
+    gradients noisy — the fp32 CPU oracle itself deviates from fp64 by up to
+    ~2e-2 of a tensor's max on the ASPP variants — so the device gradient must
+    be within max(4 x that fp32 deviation, 2e-3 x max|g64|) of fp64.  B = 4:
+    the ASPP global-pool BatchNorm normalises over the batch only (over B = 2
+    its input gradient is exactly zero, pure rounding noise)."""
+    from oracle import net as onet
     from oracle import train as otrain
     from losses.loss import TotalLoss
+    B = 4
     model = _model(pre, aspp, seed=3)
     sd_cpu = {k: v.detach().clone() for k, v in model.state_dict().items()}
     model = model.to(DEV).train()
     crit = TotalLoss(use_freq_loss=True).to(DEV)
-    x = torch.rand(2, 3, 64, 64, generator=torch.Generator().manual_seed(5)) * 0.6
+    x = torch.rand(B, 3, 64, 64, generator=torch.Generator().manual_seed(5)) * 0.6
     enh, refl, illu = model(x.to(DEV))
     total, d = crit(x.to(DEV), enh, illu, refl)
     st = model.__dict__["_upr_train"]
     total.backward()
     torch.cuda.synchronize()
-    masks = []
+    mask = None
     if aspp:
         asp = [b for b in st["graph"].ie.mid if type(b).__name__ == "ASPPT"][0]
-        masks.append(asp.mask.cpu().view(2, 64 // 8, 64 // 8, 256).permute(0, 3, 1, 2).float())
-    it = iter(masks)
+        mask = asp.mask.cpu().view(B, 8, 8, 256).permute(0, 3, 1, 2).float()
     names = otrain.param_names(sd_cpu)
-    params = {k: sd_cpu[k].clone().requires_grad_(True) for k in names}
-    work = dict(sd_cpu)
-    work.update(params)
-    from oracle import net as onet
-    with otrain.train_mode(dropout_mask=lambda shape: next(it)):
-        e_r, r_r, i_r = onet.forward(work, x, pre, aspp)
     vgg = otrain.vgg19_state(VGG_SEED)
-    t_r, d_r = otrain.total_loss(vgg, x, e_r, i_r, r_r)
-    t_r.backward()
-    _close(enh, e_r, 1e-4, "enh")
-    _close(illu, i_r, 1e-4, "illu")
-    np.testing.assert_allclose(d["total"], d_r["total"], rtol=1e-4)
+
+    def oracle(dt):
+        s2 = {k: (v.to(dt) if v.is_floating_point() else v.clone()) for k, v in sd_cpu.items()}
+        params = {k: s2[k].clone().requires_grad_(True) for k in names}
+        work = dict(s2)
+        work.update(params)
+        with otrain.train_mode(dropout_mask=lambda shape: mask.to(dt)):
+            e_r, r_r, i_r = onet.forward(work, x.to(dt), pre, aspp)
+        t_r, d_r = otrain.total_loss({k: v.to(dt) for k, v in vgg.items()}, x.to(dt), e_r, i_r, r_r)
+        t_r.backward()
+        return e_r, i_r, d_r, {k: params[k].grad.double() for k in names}
+
+    e64, i64, d64, g64 = oracle(torch.float64)
+    _, _, _, g32 = oracle(torch.float32)
+    _close(enh, e64, 1e-4, "enh")
+    _close(illu, i64, 1e-4, "illu")
+    np.testing.assert_allclose(d["total"], d64["total"], rtol=1e-4)
     dev_params = dict(model.named_parameters())
+    gmax = max(v.abs().max().item() for v in g64.values())
     for n in names:
-        _close(dev_params[n].grad, params[n].grad, 3e-3, "grad " + n)
+        ref = g64[n]
+        if ref.abs().max().item() < 1e-9 * gmax:
+            continue  # BN-fed conv bias: zero true gradient (rounding noise)
+        dev_err = (dev_params[n].grad.double().cpu() - ref).abs().max().item()
+        cpu_err = (g32[n] - ref).abs().max().item()
+        tol = max(4.0 * cpu_err, 2e-3 * ref.abs().max().item()) + 1e-9
+        assert dev_err <= tol, f"grad {n}: device |d| {dev_err:.3e} vs fp64 > {tol:.3e} (fp32 CPU |d| {cpu_err:.3e})"
