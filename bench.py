@@ -218,6 +218,13 @@ def train_main(args):
         torch.distributed.destroy_process_group()
 
 
+def _cfg_index(args):
+    """BASELINE.json configs[] entry a forward run corresponds to."""
+    if args.size == 1024 and args.variant == "preact_aspp":
+        return 3  # bs=256 1024^2 over 8 GPUs = 32 per GPU
+    return 1 if args.precision == "fp32" and args.variant == "plain" else 2
+
+
 def main():
     args = parse()
     if args.train:
@@ -280,7 +287,7 @@ def main():
 
     total_imgs = world * B * args.steps
     out = {
-        "metric": "images/sec at 512x512 bs=32 (UP-Retinex forward)",
+        "metric": f"images/sec at {S}x{S} bs={B} per GPU (UP-Retinex forward)",
         "value": total_imgs / elapsed,
         "unit": "images/s",
         "n_gpus": world,
@@ -292,7 +299,7 @@ def main():
         "vs_baseline": None,
         "dtype": "f32" if args.precision == "fp32" else "f16 (fp32 accumulate)",
         "data": "synthetic torch.rand inputs, random-init weights (torch.manual_seed(0))",
-        "config": {"workload": f"configs[{1 if args.precision == 'fp32' else 2}]: bs={B}/GPU {S}x{S} "
+        "config": {"workload": f"configs[{_cfg_index(args)}]: bs={B}/GPU {S}x{S} "
                                f"{args.variant} forward, {args.precision}",
                    "global_batch": world * B, "image_size": S, "variant": args.variant,
                    "parallelism": f"batch-shard x{world} (no data-path collective)"},
@@ -318,7 +325,7 @@ def main():
             "gemm_gflop_per_img": g_flops / (args.steps * B) / 1e9,
             "gemm_alg_GB_per_img": g_bytes / (args.steps * B) / 1e9,
             "gemm_share_of_device_time": g_ms / all_ms if all_ms else None,
-            "ref_equiv_tflops": REF_GFLOP_PER_IMG[args.variant] * total_imgs / world / elapsed / 1e3,
+            "ref_equiv_tflops": REF_GFLOP_PER_IMG[args.variant] * (S / 512) ** 2 * total_imgs / world / elapsed / 1e3,
         }
         if args.breakdown and rank == 0:
             for s in stats:

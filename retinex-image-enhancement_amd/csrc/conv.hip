@@ -392,6 +392,7 @@ static int launch_t(const ConvOp& op, hipStream_t stream) {
 }
 
 int launch_conv_halo(const ConvOp& op, int dtype, hipStream_t st);
+int launch_conv_wide(const ConvOp& op, hipStream_t st);
 
 // UPR_CONV_IMPL=generic forces the implicit-GEMM kernel everywhere (A/B tests);
 // default: halo-tiled kernel where the shape allows, implicit GEMM otherwise.
@@ -409,6 +410,10 @@ int launch_conv(const ConvOp& op, int dtype, hipStream_t stream) {
   for (int s = 0; s < op.nseg; ++s)
     if (op.seg[s].C % 32 || op.seg[s].src == nullptr) return kErrShape;
   if (conv_impl_mode() == 0) {
+    if (dtype == kF16) {
+      const int rc = launch_conv_wide(op, stream);
+      if (rc != kErrUnsupported) return rc;
+    }
     const int rc = launch_conv_halo(op, dtype, stream);
     if (rc != kErrUnsupported) return rc;
   }

@@ -1,0 +1,338 @@
+// Wide-tile implicit-GEMM convolution, fp16 operands / fp32 accumulate, for the
+// MFMA-bound layers of the UP-Retinex graph (>= 64 input channels, >= 128
+// output channels: encoder blocks 2-3, bottleneck ResBlocks, ASPP branches and
+// fusion, decoder 3 and the ConvTranspose GEMMs; models/model.py:100-274).
+//
+// Why a second GEMM kernel: the 128x128 register-staged tiles of conv.hip and
+// the 128-pixel halo tiles of conv_halo.hip move ~64 B/clk/CU of operands at
+// full MFMA rate, which the L2 cannot feed.  Here:
+//
+// * Tile 256 pixels x BN (256 or 128) channels, 8 waves (512 threads); each wave
+//   owns a 128x64 (BN 256) or 64x64 (BN 128) accumulator block of
+//   v_mfma_f32_16x16x32_f16 tiles -> half the operand bytes per flop.
+// * K step = 64 channels of one tap of one segment.  Both operands go global ->
+//   LDS by LDS-DMA (global_load_lds_dwordx4): no staging registers, no
+//   ds_write pass.  A is a per-lane gather (each lane's source is its output
+//   pixel shifted by the tap; out-of-image taps and rows past M read a
+//   128-byte zero line), B rows are the packed [N][Kpad] weights.
+// * Two LDS stages, one barrier per K step: the DMA of step s+1 is issued right
+//   after the barrier and flies while the MFMAs of step s run.
+// * LDS image: 128-byte rows (64 fp16), lane-linear as LDS-DMA requires; the
+//   16-byte chunk index is XOR-swizzled by (row >> 1) & 7 on the SOURCE
+//   address, and the fragment reads apply the same XOR -> the ds_read_b128
+//   lane groups hit 16 distinct bank slots (conflict free).
+//
+// Segments must be plain (no pre-activation / max-pool prologue: those need
+// register staging and stay on conv.hip / conv_halo.hip), C % 64 == 0.
+#include <cstdlib>
+#include <cstring>
+
+#include "upr_common.h"
+
+namespace upr {
+
+typedef float f32x4_w __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8_w __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+
+// 128 zero bytes: the source of every padded / out-of-range A chunk
+__device__ __attribute__((aligned(128))) uint4 g_wide_zero[8];
+
+constexpr int WBM = 256;  // output pixels per tile
+constexpr int WBK = 64;   // channels per K step
+
+template <int BN>
+struct WideCfg {
+  static constexpr int WAVES_M = BN == 256 ? 2 : 4;
+  static constexpr int WAVES_N = 8 / WAVES_M;
+  static constexpr int WM = WBM / WAVES_M / 16;  // 16x16 tiles per wave along M
+  static constexpr int WN = BN / WAVES_N / 16;   // along N
+  static constexpr int A_BYTES = WBM * WBK * 2;
+  static constexpr int B_BYTES = BN * WBK * 2;
+  static constexpr int STAGE = A_BYTES + B_BYTES;
+  static constexpr int LDS = 2 * STAGE;
+  static constexpr int BJ = BN / 64;  // B DMA instructions per wave per step (8 rows each)
+};
+
+__device__ __forceinline__ int wide_xcd_remap(int bid, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7;
+  const int xcd = bid & 7, idx = bid >> 3;
+  return ((xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+__device__ __forceinline__ void glds16(const void* g, unsigned char* lds) {
+  __builtin_amdgcn_global_load_lds(g, (lds_void_ptr)lds, 16, 0, 0);
+}
+
+template <int BN>
+__global__ __launch_bounds__(512) void conv_wide_kernel(ConvOp op) {
+  using C = WideCfg<BN>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave % C::WAVES_M;
+  const int wn = wave / C::WAVES_M;
+
+  const int M = op.B * op.Ho * op.Wo;
+  const int HW = op.Ho * op.Wo;
+  const int mtiles = (M + WBM - 1) / WBM;
+  const int ntiles = op.N / BN;
+  const int L = wide_xcd_remap(blockIdx.x, mtiles * ntiles);
+  const int ntile = L % ntiles;  // the n-tiles of one pixel tile run back to back (A reuse in L2)
+  const int mtile = L / ntiles;
+  const int m0 = mtile * WBM;
+  const int n0 = ntile * BN;
+
+  // ---- this lane's 4 A rows (output pixels) and DMA chunk swizzles ---------
+  const int q8 = lane >> 3;       // row within an 8-row DMA group
+  const int qc = lane & 7;        // LDS chunk this lane fills
+  int rb[4], ry[4], rx[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + wave * 32 + i * 8 + q8;
+    if (m < M) {
+      const int b = m / HW, r = m - b * HW;
+      rb[i] = b;
+      ry[i] = r / op.Wo;
+      rx[i] = r - ry[i] * op.Wo;
+    } else {
+      rb[i] = -1; ry[i] = 0; rx[i] = 0;
+    }
+  }
+  // logical chunk stored at LDS chunk qc of row R is qc ^ ((R >> 1) & 7); for
+  // R = wave*32 + i*8 + q8 (A) or wave*BN/8 + j*8 + q8 (B) that is (4i + lane>>4) & 7
+  const int sw_lane = lane >> 4;
+
+  int total_steps = 0;
+  for (int s = 0; s < op.nseg; ++s) total_steps += op.seg[s].kh * op.seg[s].kw * (op.seg[s].C / WBK);
+
+  int cur_seg = 0, cur_tap = 0, cur_c0 = 0;
+  const half_t* Wt = (const half_t*)op.W;
+  const half_t* zero = (const half_t*)g_wide_zero;
+
+  auto issue = [&](int stage) {
+    const ConvSeg& sg = op.seg[cur_seg];
+    const int r = cur_tap / sg.kw, s = cur_tap - r * sg.kw;
+    const int dy = r * sg.dil - sg.pad, dx = s * sg.dil - sg.pad;
+    const half_t* src = (const half_t*)sg.src + sg.coff + cur_c0;
+    unsigned char* As = smem + stage * C::STAGE;
+    unsigned char* Bs = As + C::A_BYTES;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int iy = ry[i] * sg.stride + dy;
+      const int ix = rx[i] * sg.stride + dx;
+      const int ch = qc ^ ((4 * i + sw_lane) & 7);
+      const half_t* p = zero;
+      if (rb[i] >= 0 && (unsigned)iy < (unsigned)sg.Hin && (unsigned)ix < (unsigned)sg.Win)
+        p = src + (size_t)((rb[i] * sg.Hin + iy) * sg.Win + ix) * sg.cs + ch * 8;
+      glds16(p, As + (wave * 32 + i * 8) * 128);
+    }
+    const int kb = sg.kbase + cur_tap * sg.C + cur_c0;
+#pragma unroll
+    for (int j = 0; j < C::BJ; ++j) {
+      const int n = wave * (BN / 8) + j * 8 + q8;
+      const int ch = qc ^ ((4 * j + sw_lane) & 7);
+      glds16(Wt + (size_t)(n0 + n) * op.Kpad + kb + ch * 8, Bs + (wave * (BN / 8) + j * 8) * 128);
+    }
+    // advance the (segment, tap, channel) cursor
+    cur_c0 += WBK;
+    if (cur_c0 >= sg.C) {
+      cur_c0 = 0;
+      if (++cur_tap >= sg.kh * sg.kw) { cur_tap = 0; ++cur_seg; }
+    }
+  };
+
+  f32x4_w acc[C::WM][C::WN];
+#pragma unroll
+  for (int a = 0; a < C::WM; ++a)
+#pragma unroll
+    for (int b = 0; b < C::WN; ++b) acc[a][b] = f32x4_w{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15;
+  const int fg = lane >> 4;
+  const int rsw = (fr >> 1) & 7;  // swizzle of every fragment row this lane reads
+
+  if (total_steps > 0) issue(0);
+  for (int step = 0; step < total_steps; ++step) {
+    // stage step&1 has landed (own DMA retired, then everyone's via the
+    // barrier) and every wave is done reading the other stage (step-1)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (step + 1 < total_steps) issue((step + 1) & 1);
+    const half_t* As = (const half_t*)(smem + (step & 1) * C::STAGE);
+    const half_t* Bs = As + C::A_BYTES / 2;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int pc = ((kk * 4 + fg) ^ rsw) * 8;
+      f16x8_w bf[C::WN];
+#pragma unroll
+      for (int b = 0; b < C::WN; ++b) bf[b] = *(const f16x8_w*)(Bs + (wn * C::WN * 16 + b * 16 + fr) * 64 + pc);
+#pragma unroll
+      for (int a = 0; a < C::WM; ++a) {
+        const f16x8_w af = *(const f16x8_w*)(As + (wm * C::WM * 16 + a * 16 + fr) * 64 + pc);
+#pragma unroll
+        for (int b = 0; b < C::WN; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf[b], acc[a][b], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- epilogue through LDS ---------------------------------------------------
+  // Four passes of 64 tile rows: the waves owning those rows park their raw
+  // fp32 accumulators in LDS ([64][BN + 4] floats: conflict-free 4-byte
+  // writes), then every thread finishes 8 consecutive channels of one pixel
+  // per iteration (scale / bias / per-image bias / residuals / ReLU, 16-byte
+  // loads and stores).  With 512 threads and BN/8 chunks per row, a thread's
+  // channel chunk is the same in every iteration, so the per-image pooled sums
+  // (ASPP global branch) stay in registers until the end.
+  constexpr int EST = BN + 4;
+  constexpr int CPR = BN / 8;             // 8-channel chunks per row
+  constexpr int RPI = 512 / CPR;          // rows per iteration
+  constexpr int APP = 4;                  // 16-row accumulator tiles per pass
+  constexpr int PPW = C::WM / APP;        // passes per wave-row group
+  float* Es = (float*)smem;
+  const int col8 = tid % CPR;
+  const int nch = n0 + col8 * 8;
+  float sc[8], bi[8], psum[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sc[e] = op.scale ? op.scale[nch + e] : 1.f;
+    bi[e] = op.bias ? op.bias[nch + e] : 0.f;
+    psum[e] = 0.f;
+  }
+  const bool one_image = (m0 / HW) == (min(m0 + WBM, M) - 1) / HW;
+  const bool convt = op.store == kStoreConvT2x2;
+  __syncthreads();  // every wave is done with the last stage
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    if (wm == p / PPW) {
+#pragma unroll
+      for (int a = 0; a < APP; ++a)
+#pragma unroll
+        for (int b = 0; b < C::WN; ++b)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            Es[(a * 16 + fg * 4 + i) * EST + wn * C::WN * 16 + b * 16 + fr] = acc[(p % PPW) * APP + a][b][i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < 64 / RPI; ++it) {
+      const int row = tid / CPR + it * RPI;
+      const int m = m0 + p * 64 + row;
+      if (m < M) {
+        const f32x4_w lo = *(const f32x4_w*)(Es + row * EST + col8 * 8);
+        const f32x4_w hi = *(const f32x4_w*)(Es + row * EST + col8 * 8 + 4);
+        float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const int img = m / HW;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = v[e] * sc[e] + bi[e];
+        if (op.img_bias) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += op.img_bias[img * op.N + nch + e];
+        }
+        if (op.res1) {
+          const f16x8_w r = *(const f16x8_w*)((const half_t*)op.res1 + (size_t)m * op.res1_cs + nch);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += (float)r[e];
+        }
+        if (op.relu) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
+        if (op.res2) {
+          const f16x8_w r = *(const f16x8_w*)((const half_t*)op.res2 + (size_t)m * op.res2_cs + nch);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += (float)r[e];
+        }
+        f16x8_w o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (half_t)v[e];
+        size_t off;
+        if (convt) {
+          const int cout = op.N >> 2;
+          const int q = nch / cout, co = nch - q * cout;
+          const int pix = m - img * HW;
+          const int oy = pix / op.Wo, ox = pix - oy * op.Wo;
+          const size_t opix = ((size_t)img * 2 * op.Ho + 2 * oy + (q >> 1)) * (2 * op.Wo) + 2 * ox + (q & 1);
+          off = opix * op.out_cs + op.out_coff + co;
+        } else {
+          off = (size_t)m * op.out_cs + op.out_coff + nch;
+        }
+        *(f16x8_w*)((half_t*)op.out + off) = o;
+        if (op.pool) {
+          if (one_image) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) psum[e] += (float)o[e];
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) atomicAdd(op.pool + img * op.N + nch + e, (float)o[e]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (op.pool && one_image && !convt) {
+    // block-level reduction of the RPI partial sums per channel through LDS
+    // (the last pass ended with a barrier), then ONE atomic per channel: the
+    // pooled vector of an image is hit by HW/256 tiles, not by 16x that many
+    // per-wave atomics (contended same-address atomics serialise)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) Es[(tid / CPR) * BN + col8 * 8 + e] = psum[e];
+    __syncthreads();
+    if (tid < BN) {
+      float t = 0.f;
+      for (int g = 0; g < RPI; ++g) t += Es[g * BN + tid];
+      atomicAdd(op.pool + (m0 / HW) * op.N + n0 + tid, t);
+    }
+  }
+}
+
+template <int BN>
+static int launch_wide_bn(const ConvOp& op, hipStream_t st) {
+  using C = WideCfg<BN>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    const hipError_t e = hipFuncSetAttribute((const void*)conv_wide_kernel<BN>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    if (e != hipSuccess) return (int)e;
+    attr_set = true;
+  }
+  const int M = op.B * op.Ho * op.Wo;
+  const int grid = ((M + WBM - 1) / WBM) * (op.N / BN);
+  hipLaunchKernelGGL((conv_wide_kernel<BN>), dim3(grid), dim3(512), C::LDS, st, op);
+  return (int)hipGetLastError();
+}
+
+// UPR_CONV_WIDE=0 disables this path (A/B timing against conv_halo / conv_igemm)
+static bool wide_enabled() {
+  static int en = -1;
+  if (en < 0) {
+    const char* e = getenv("UPR_CONV_WIDE");
+    en = (e && strcmp(e, "0") == 0) ? 0 : 1;
+  }
+  return en == 1;
+}
+
+// fp16 only; returns kErrUnsupported for shapes this kernel does not take
+int launch_conv_wide(const ConvOp& op, hipStream_t st) {
+  if (!wide_enabled()) return kErrUnsupported;
+  if (op.store == kStoreHeadIllu || op.N % 128) return kErrUnsupported;
+  if (op.Kpad % 8 || ((uintptr_t)op.W % 16)) return kErrUnsupported;
+  for (int s = 0; s < op.nseg; ++s) {
+    const ConvSeg& sg = op.seg[s];
+    if (sg.pre != kPreNone || sg.C % WBK || sg.cs % 8 || sg.coff % 8 || sg.kbase % 8) return kErrUnsupported;
+    if ((uintptr_t)sg.src % 16) return kErrUnsupported;
+  }
+  if (op.N % 256 == 0) return launch_wide_bn<256>(op, st);
+  // 128-channel tiles of pure stride-1 3x3 convs stay on the halo kernel (it
+  // stages each input pixel once for all 9 taps and measured faster there)
+  bool all_s1_3x3 = true;
+  for (int s = 0; s < op.nseg; ++s)
+    if (!(op.seg[s].kh == 3 && op.seg[s].stride == 1)) all_s1_3x3 = false;
+  if (all_s1_3x3 && op.Wo >= 24 && op.Ho >= 8) return kErrUnsupported;
+  return launch_wide_bn<128>(op, st);
+}
+
+}  // namespace upr

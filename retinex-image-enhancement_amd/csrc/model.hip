@@ -30,6 +30,7 @@
 namespace upr {
 
 int launch_prep(const void* x, void* x2p, void* x3p, int B, int H, int W, int dtype, hipStream_t st);
+int launch_preact_f16(const void* x, const float* sc, const float* sh, void* o, size_t npix, int C, hipStream_t st);
 int launch_conv3(const void* x, const float* w, const float* bias, void* out0, void* out1, int B, int h, int wd,
                  int dtype, hipStream_t st);
 int launch_fam_ca(const float* pool, const float* w1, const float* b1, const float* w2, const float* b2, float* ca,
@@ -245,6 +246,7 @@ enum BufId : int {
   B_CA,     // float ca [3][B][32]
   B_IB,     // float ASPP per-image bias [B][256]
   B_ILLU32, // float illu when the model dtype is fp16 (head writes fp32 then tail reads)
+  B_PA2, B_PA3, B_PA4,  // fp16 PreAct: materialised relu(bn1(x)) of the blocks at levels 1, 2, 3
   B_COUNT
 };
 
@@ -258,7 +260,7 @@ static std::vector<double> conv3_kmajor(const std::vector<double>& w) {
   return t;
 }
 
-enum OpKind { OP_GEMM, OP_CONV3, OP_PREP, OP_FAM_CA, OP_FAM_MIX, OP_FAM_SA, OP_ASPP_G, OP_TAIL };
+enum OpKind { OP_GEMM, OP_CONV3, OP_PREP, OP_FAM_CA, OP_FAM_MIX, OP_FAM_SA, OP_ASPP_G, OP_TAIL, OP_PREACT };
 
 struct Op {
   OpKind kind;
@@ -337,6 +339,9 @@ static BufGeom buf_geom(int id, int use_aspp) {
     case B_MM3: return {2, 4, 1, 2};
     case B_P3: case B_Q3: return {3, 4, 1, 2};
     case B_ILLU32: return {1, 0, 1, 0};
+    case B_PA2: return {64, 1, 0, 0};
+    case B_PA3: return {128, 2, 0, 0};
+    case B_PA4: return {256, 3, 0, 0};
     default: return {0, 0, 1, 0};
   }
 }
@@ -347,6 +352,12 @@ static void buf_dims(const BufGeom& g, int H, int W, int& h, int& w) {
   if (g.pyramid == 2) { h = (H / 4) / 4; w = (W / 4) / 4; return; }
   h = H >> g.shift; w = W >> g.shift;
 }
+
+// fp16 PreAct blocks with >= 64 input channels materialise o = relu(bn1(x))
+// once (OP_PREACT) so that conv1 and the projecting shortcut read plain
+// segments and run on the wide-tile LDS-DMA kernel (conv_wide.hip); fp32 and
+// 32-channel inputs keep the per-tap prologue.
+static bool preact_materialised(const UprModel* m) { return m->use_preact && m->dtype == kF16; }
 
 static size_t ws_layout(const UprModel* m, int B, int H, int W, size_t* offs) {
   size_t off = 0;
@@ -362,6 +373,7 @@ static size_t ws_layout(const UprModel* m, int B, int H, int W, size_t* offs) {
       buf_dims(g, H, W, h, w);
       bytes = (size_t)B * h * w * g.C * (g.is_f32 ? 4 : elt);
     }
+    if (id >= B_PA2 && id <= B_PA4 && !preact_materialised(m)) bytes = 0;
     if (m->flags & UPR_MODEL_IENET_ONLY) {
       const bool scale_buf = id == B_X2P || id == B_X3P || id == B_S1IN || id == B_S2IN || id == B_S3IN ||
                              (id >= B_H1 && id <= B_Q3);
@@ -442,8 +454,16 @@ struct Builder {
       BNFold bn1, bn2, bns;
       if (!bn_fold(P, p + ".bn1", cin, bn1) || !bn_fold(P, p + ".bn2", cout, bn2)) { ok = false; return; }
       const size_t pre_s = blob.add_f32(bn1.s), pre_h = blob.add_f32(bn1.sh);
+      int osrc = in, opre = kPreAffineRelu;
+      if (preact_materialised(m) && cin % 64 == 0) {
+        Op po;
+        po.kind = OP_PREACT; po.name = p + ".bn1_relu"; po.in = in; po.level = in_level; po.w = pre_s; po.b = pre_h;
+        po.out = in_level == 1 ? B_PA2 : (in_level == 2 ? B_PA3 : B_PA4);
+        m->ops.push_back(po);
+        osrc = po.out; opre = kPreNone;
+      }
       std::vector<SegWeights> s1(1);
-      s1[0].spec = seg(in, cin, cin, 0, 3, stride, 1, 1, kPreAffineRelu);
+      s1[0].spec = seg(osrc, cin, cin, 0, 3, stride, 1, 1, opre);
       s1[0].spec.pre_scale = pre_s; s1[0].spec.pre_shift = pre_h;
       s1[0].w = conv_w(*w1, &bn2.s);
       int l1 = add_layer(cout, s1, bn2.sh);
@@ -456,7 +476,7 @@ struct Builder {
         const HostTensor* ws = T(p + ".shortcut.0.weight");
         if (!ws || !bn_fold(P, p + ".shortcut.1", cout, bns)) { ok = false; return; }
         SegWeights sc;
-        sc.spec = seg(in, cin, cin, 0, 1, stride, 0, 1, kPreAffineRelu);
+        sc.spec = seg(osrc, cin, cin, 0, 1, stride, 0, 1, opre);
         sc.spec.pre_scale = pre_s; sc.spec.pre_shift = pre_h;
         sc.w = conv_w(*ws, &bns.s);
         s2.push_back(sc);
@@ -823,6 +843,14 @@ static int run_forward(UprModel* m, const void* x, int B, int H, int W, void* en
           m->cur_flops[oi] = 2.0 * Mpx * L.N * K;
           m->cur_bytes[oi] = bytes;
         }
+        break;
+      }
+      case OP_PREACT: {
+        int h, w;
+        lvl_dims(o.level, h, w);
+        const int C = buf_geom(o.out, m->use_aspp).C;
+        rc = launch_preact_f16(buf(o.in), fptr(o.w), fptr(o.b), buf(o.out), (size_t)B * h * w, C, st);
+        if (m->prof) m->cur_bytes[oi] = 2.0 * B * h * w * C * elt;
         break;
       }
       case OP_ASPP_G: {

@@ -8,6 +8,8 @@
 //  fam_mix        y*ca -> [mean_c, max_c] map + 3-channel head projection (:89-93)
 //  fam_sa         7x7 spatial attention conv + sigmoid, scales the projection (:56-59, :94-95)
 //  retinex_tail   sigmoid(head) , R = x/(I+1e-6), R*E + (1-R)*E^2 (:411-412, :430-442)
+#include <algorithm>
+
 #include "upr_common.h"
 
 namespace upr {
@@ -359,6 +361,32 @@ int launch_tail(const void* x, const float* illu_f32, const void* illu_t, const 
   else
     hipLaunchKernelGGL((retinex_tail_kernel<float>), dim3(grid1d(n)), dim3(256), 0, st, (const float*)x, illu_f32,
                        (const float*)illu_t, q1, q2, q3, cst, (float*)enh, (float*)refl, B, H, W, h2, w2, h3, w3);
+  return (int)hipGetLastError();
+}
+
+// PreActResBlock prologue materialised (models/model.py:164-166):
+// o = relu(bn1(x)) with the eval BatchNorm folded to (scale, shift), fp16 NHWC,
+// 8 channels per thread (16-byte loads / stores).  Rounds exactly like the
+// per-tap prologue of conv.hip / conv_halo.hip (fp32 math, one fp16 rounding).
+__global__ __launch_bounds__(256) void preact_kernel(const half_t* __restrict__ x, const float* __restrict__ sc,
+                                                     const float* __restrict__ sh, half_t* __restrict__ o, size_t n8,
+                                                     int C8) {
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C8) * 8;
+    const h8 v = ((const h8*)x)[i];
+    h8 r;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) r[e] = (half_t)fmaxf((float)v[e] * sc[c + e] + sh[c + e], 0.f);
+    ((h8*)o)[i] = r;
+  }
+}
+
+int launch_preact_f16(const void* x, const float* sc, const float* sh, void* o, size_t npix, int C, hipStream_t st) {
+  if (C % 8) return kErrShape;
+  const size_t n8 = npix * (C / 8);
+  const int grid = (int)std::min<size_t>((n8 + 255) / 256, 256 * 16);
+  hipLaunchKernelGGL(preact_kernel, dim3(grid), dim3(256), 0, st, (const half_t*)x, sc, sh, (half_t*)o, n8, C / 8);
   return (int)hipGetLastError();
 }
 

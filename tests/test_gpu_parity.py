@@ -55,6 +55,10 @@ CONV_CASES = [
     (1, 9, 48, 32, 128, 1, 1, 0, 1, False, False),
     (1, 16, 64, 128, 64, 3, 1, 1, 1, True, True),
     (1, 8, 32, 256, 256, 3, 1, 1, 1, False, False),
+    # shapes routed to the wide-tile LDS-DMA kernel in fp16 (Cin % 64, Cout % 128), partial tiles
+    (3, 20, 28, 64, 128, 3, 2, 1, 1, True, True),
+    (2, 30, 34, 256, 256, 3, 1, 12, 12, False, True),
+    (1, 17, 23, 128, 512, 1, 1, 0, 1, True, False),
 ]
 
 
@@ -258,3 +262,44 @@ def test_multiscale_kernel(golden):
         assert abs(factor[b].item() - fac[b]) < 1e-6
         ref = torch.clamp(enh[b] * fac[b], 0, 1)
         assert maxdiff(out[b], ref) <= 1e-6
+
+
+# ---------------------------------------------------------------------------
+# full-size configs (BASELINE.json configs[1..3]): the whole batch runs on the
+# GPU, the oracle checks the first and the last image of the batch (direct
+# per-pixel parity at full size; the last image exercises the largest offsets)
+# ---------------------------------------------------------------------------
+FULL_CASES = [
+    # B, size, pre, aspp, dtype
+    (32, 512, False, False, torch.float32),   # configs[1]
+    (32, 512, True, True, torch.float16),     # configs[2]
+    (32, 1024, True, True, torch.float32),    # configs[3] per-GPU shard
+    (32, 1024, True, True, torch.float16),
+]
+
+
+@pytest.mark.parametrize("case", FULL_CASES, ids=lambda c: f"B{c[0]}_{c[1]}_pre{int(c[2])}aspp{int(c[3])}_{str(c[4])[6:]}")
+def test_full_size_config(case):
+    B, S, pre, aspp, dt = case
+    m = make_model(pre, aspp)
+    sd = m.state_dict()
+    g = torch.Generator(device=DEV).manual_seed(1)
+    x = torch.rand(B, 3, S, S, generator=g, device=DEV)
+    m = m.to(DEV)
+    with torch.no_grad():
+        out = m(x.to(dt))
+    torch.cuda.synchronize()
+    for k, o in enumerate(out):
+        assert torch.isfinite(o).all(), f"non-finite output {k}"
+    tol = FP32_TOL if dt == torch.float32 else FP16_TOL
+    for b in (0, B - 1):
+        with torch.no_grad():
+            ref = onet.forward(sd, x[b:b + 1].cpu(), pre, aspp)
+        for name, a, r in zip(("enh", "refl", "illu"), out, ref):
+            err = maxdiff(a[b:b + 1], r)
+            if name == "refl" and dt == torch.float16:
+                err /= max(1.0, r.abs().max().item())
+            print(f"B{B} {S}^2 {dt} image {b} {name} max|d| = {err:.3e}")
+            assert err <= tol, f"image {b} {name}: {err}"
+    del out, x
+    torch.cuda.empty_cache()
