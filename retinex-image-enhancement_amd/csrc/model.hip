@@ -246,7 +246,7 @@ enum BufId : int {
   B_CA,     // float ca [3][B][32]
   B_IB,     // float ASPP per-image bias [B][256]
   B_ILLU32, // float illu when the model dtype is fp16 (head writes fp32 then tail reads)
-  B_PA2, B_PA3, B_PA4,  // fp16 PreAct: materialised relu(bn1(x)) of the blocks at levels 1, 2, 3
+  B_PA1, B_PA2, B_PA3, B_PA4,  // fp16 PreAct: materialised relu(bn1(x)) of the blocks at levels 0..3
   B_COUNT
 };
 
@@ -339,6 +339,7 @@ static BufGeom buf_geom(int id, int use_aspp) {
     case B_MM3: return {2, 4, 1, 2};
     case B_P3: case B_Q3: return {3, 4, 1, 2};
     case B_ILLU32: return {1, 0, 1, 0};
+    case B_PA1: return {32, 0, 0, 0};
     case B_PA2: return {64, 1, 0, 0};
     case B_PA3: return {128, 2, 0, 0};
     case B_PA4: return {256, 3, 0, 0};
@@ -353,10 +354,12 @@ static void buf_dims(const BufGeom& g, int H, int W, int& h, int& w) {
   h = H >> g.shift; w = W >> g.shift;
 }
 
-// fp16 PreAct blocks with >= 64 input channels materialise o = relu(bn1(x))
-// once (OP_PREACT) so that conv1 and the projecting shortcut read plain
-// segments and run on the wide-tile LDS-DMA kernel (conv_wide.hip); fp32 and
-// 32-channel inputs keep the per-tap prologue.
+// fp16 PreAct blocks materialise o = relu(bn1(x)) once (OP_PREACT) so that
+// conv1 and the projecting shortcut read plain segments: >= 64 channels run on
+// the wide-tile LDS-DMA kernel (conv_wide.hip), 32 channels on the halo kernel
+// without its per-tap prologue (measured: enc1 0.84 + 0.49 ms -> 0.40 + 0.38
+// ms against ~0.15 ms for the extra pass).  fp32 keeps the per-tap prologue
+// (MFMA-bound there: the prologue is hidden).
 static bool preact_materialised(const UprModel* m) { return m->use_preact && m->dtype == kF16; }
 
 static size_t ws_layout(const UprModel* m, int B, int H, int W, size_t* offs) {
@@ -373,7 +376,7 @@ static size_t ws_layout(const UprModel* m, int B, int H, int W, size_t* offs) {
       buf_dims(g, H, W, h, w);
       bytes = (size_t)B * h * w * g.C * (g.is_f32 ? 4 : elt);
     }
-    if (id >= B_PA2 && id <= B_PA4 && !preact_materialised(m)) bytes = 0;
+    if (id >= B_PA1 && id <= B_PA4 && !preact_materialised(m)) bytes = 0;
     if (m->flags & UPR_MODEL_IENET_ONLY) {
       const bool scale_buf = id == B_X2P || id == B_X3P || id == B_S1IN || id == B_S2IN || id == B_S3IN ||
                              (id >= B_H1 && id <= B_Q3);
@@ -455,10 +458,10 @@ struct Builder {
       if (!bn_fold(P, p + ".bn1", cin, bn1) || !bn_fold(P, p + ".bn2", cout, bn2)) { ok = false; return; }
       const size_t pre_s = blob.add_f32(bn1.s), pre_h = blob.add_f32(bn1.sh);
       int osrc = in, opre = kPreAffineRelu;
-      if (preact_materialised(m) && cin % 64 == 0) {
+      if (preact_materialised(m)) {
         Op po;
         po.kind = OP_PREACT; po.name = p + ".bn1_relu"; po.in = in; po.level = in_level; po.w = pre_s; po.b = pre_h;
-        po.out = in_level == 1 ? B_PA2 : (in_level == 2 ? B_PA3 : B_PA4);
+        po.out = in_level == 0 ? B_PA1 : (in_level == 1 ? B_PA2 : (in_level == 2 ? B_PA3 : B_PA4));
         m->ops.push_back(po);
         osrc = po.out; opre = kPreNone;
       }
