@@ -393,6 +393,7 @@ static int launch_t(const ConvOp& op, hipStream_t stream) {
 
 int launch_conv_halo(const ConvOp& op, int dtype, hipStream_t st);
 int launch_conv_wide(const ConvOp& op, hipStream_t st);
+int launch_conv_stream(const ConvOp& op, hipStream_t st);
 
 // UPR_CONV_IMPL=generic forces the implicit-GEMM kernel everywhere (A/B tests);
 // default: halo-tiled kernel where the shape allows, implicit GEMM otherwise.
@@ -411,7 +412,9 @@ int launch_conv(const ConvOp& op, int dtype, hipStream_t stream) {
     if (op.seg[s].C % 32 || op.seg[s].src == nullptr) return kErrShape;
   if (conv_impl_mode() == 0) {
     if (dtype == kF16) {
-      const int rc = launch_conv_wide(op, stream);
+      int rc = launch_conv_wide(op, stream);
+      if (rc != kErrUnsupported) return rc;
+      rc = launch_conv_stream(op, stream);
       if (rc != kErrUnsupported) return rc;
     }
     const int rc = launch_conv_halo(op, dtype, stream);

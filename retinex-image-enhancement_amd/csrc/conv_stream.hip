@@ -1,0 +1,401 @@
+// Streaming halo convolution for the HBM-bound fp16 layers: stride-1 3x3 over
+// 32 or 64 channels at the 512^2 / 256^2 levels (UpBlock convs of dec1/dec2,
+// models/model.py:261-269; the residual head + illumination, :324-328 and
+// :351-358; EnhancedFAM's fused branch3/branch4 first convs, :35-44).
+//
+// These layers move ~130 B per output pixel for ~18 KFLOP: at 8 TB/s the HBM
+// time is ~2x the fp16 MFMA time, so what matters is keeping enough bytes in
+// flight per CU.  Structure:
+//
+// * Persistent blocks (256 threads, 4 waves) walk TH x 32 output tiles; the
+//   tiles of each XCD are one contiguous band, so the halo rows shared by
+//   neighbouring tiles meet in that XCD's L2.
+// * The input REGION of a tile ((TH+2) x 34 pixels, all C channels) is
+//   staged global -> LDS by LDS-DMA (global_load_lds_dwordx4) into one of two
+//   slots; the DMA of tile t+1 is issued before the MFMAs of tile t and stays
+//   in flight through tile t's epilogue (raw s_barrier + counted vmcnt: the
+//   epilogue's residual / input loads are inline asm so that hipcc does not
+//   drain the DMA with a vmcnt(0) at their use).
+// * The whole filter sits in LDS for the block's lifetime.
+// * Roles swapped in the MFMA (A = weights, B = pixels): every lane ends with
+//   4 consecutive output channels of one pixel, so the epilogue stores 8-byte
+//   channel runs straight from the accumulators (no LDS transpose) and the
+//   residual head reduces over channels with two lane shuffles.
+// * LDS images are lane-linear (LDS-DMA), 16-byte chunks XOR-swizzled on the
+//   source address: pixel q of a 64-byte row image stores logical chunk c at
+//   c ^ (((q >> 2) & 1) << 1), of a 128-byte image at c ^ (q & 7): the
+//   fragment reads (16 consecutive pixels from ANY start) are then conflict
+//   free in every ds_read_b128 lane group (checked exhaustively on the host
+//   for all 16 start offsets).
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
+#include "upr_common.h"
+
+namespace upr {
+
+typedef float f32x4_s __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8_s __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4_s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void* lds_void_ptr_s;
+
+// zero source for out-of-image taps; write sink for out-of-image outputs (every
+// lane issues the same number of memory instructions in every tile, which is
+// what makes the counted vmcnt waits exact)
+__device__ __attribute__((aligned(256))) uint4 g_stream_zero[16];
+__device__ __attribute__((aligned(256))) uint2 g_stream_sink[64 * 64];
+
+constexpr int ST_TW = 32;  // tile width (output pixels)
+
+template <int C, int NB, int TH, bool HEAD>
+struct StreamCfg {
+  static constexpr int RB = C * 2;                  // bytes per region pixel
+  static constexpr int CPP = RB / 16;               // chunks per pixel
+  static constexpr int RW = ST_TW + 2, RH = TH + 2;
+  static constexpr int RPX = RW * RH;               // region pixels
+  static constexpr int NI = (RPX * RB + 4096 - 1) / 4096;  // DMA instructions per wave (4 waves x 1 KiB)
+  static constexpr int SLOT = NI * 4096;            // bytes per region slot
+  static constexpr int WBYTES = 9 * C * NB * 2;     // resident filter
+  static constexpr int LDS = WBYTES + 2 * SLOT;
+  static constexpr int GPW = TH / 2;                // 16-pixel groups per wave (tile has 2*TH groups)
+  static constexpr int NT = NB / 16;                // 16-channel tiles
+  static constexpr int KS = C / 32;                 // 32-deep k slices per tap
+  // memory instructions per wave per tile (constant by construction)
+  static constexpr int G = NI;                      // region DMA
+  static constexpr int R = HEAD ? 3 * GPW : 0;      // asm loads (x for the head; residual handled separately)
+  static constexpr int S = HEAD ? GPW : GPW * NT;   // stores
+};
+
+__device__ __forceinline__ int region_swz(int q, int cpp) {
+  return cpp == 4 ? (((q >> 2) & 1) << 1) : (q & 7);
+}
+
+// inline-asm loads: invisible to hipcc's vmcnt bookkeeping (waited for by hand)
+__device__ __forceinline__ uint2 asm_load_b64(const void* p) {
+  uint2 v;
+  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ unsigned asm_load_u16(const void* p) {
+  unsigned v;
+  asm volatile("global_load_ushort %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ unsigned asm_load_b32(const void* p) {
+  unsigned v;
+  asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+
+struct StreamArgs {
+  ConvOp op;
+  int tiles_x, tiles_y, ntiles;
+  int res_count;  // residual loads per wave per tile (0 or GPW*NT)
+};
+
+template <int C, int NB, int TH, bool HEAD>
+__global__ __launch_bounds__(256) void conv_stream_kernel(StreamArgs args) {
+  using K = StreamCfg<C, NB, TH, HEAD>;
+  const ConvOp& op = args.op;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* Wl = smem;                  // filter [tap][kslice][n][64 B]
+  unsigned char* slots = smem + K::WBYTES;   // 2 region slots
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const ConvSeg& sg = op.seg[0];
+  const int H = op.Ho, W = op.Wo;
+
+  // ---- tiles of this block: XCD-contiguous bands --------------------------
+  const int nblk = gridDim.x;
+  const int xcd = blockIdx.x & 7, idx = blockIdx.x >> 3;
+  const int per_xcd = nblk >> 3;             // grid is a multiple of 8
+  const int band0 = (int)((long long)args.ntiles * xcd / 8), band1 = (int)((long long)args.ntiles * (xcd + 1) / 8);
+  // tile sequence: band0 + idx, band0 + idx + per_xcd, ...
+  auto tile_coords = [&](int t, int& b, int& oy0, int& ox0) {
+    const int tx = t % args.tiles_x;
+    const int r = t / args.tiles_x;
+    const int ty = r % args.tiles_y;
+    b = r / args.tiles_y;
+    oy0 = ty * TH;
+    ox0 = tx * ST_TW;
+  };
+
+  // ---- resident filter: global [N][Kpad] (k = tap*C + c) -> LDS ------------
+  {
+    const half_t* Wg = (const half_t*)op.W;
+    constexpr int CH = 9 * C * NB / 8;  // 16-byte chunks
+    for (int i = tid; i < CH; i += 256) {
+      // LDS chunk i: row-block (tap, ks), row n, chunk pc (4 per 64-B row)
+      const int pc = i & 3;
+      const int n = (i >> 2) % NB;
+      const int tk = (i >> 2) / NB;  // tap * KS + ks
+      const int tap = tk / K::KS, ks = tk % K::KS;
+      const int c = pc ^ (((n >> 2) & 1) << 1);
+      const uint4 v = *(const uint4*)(Wg + (size_t)n * op.Kpad + tap * C + ks * 32 + c * 8);
+      *(uint4*)(Wl + (size_t)i * 16) = v;
+    }
+  }
+
+  // ---- per-lane DMA geometry (tile invariant) ------------------------------
+  // instruction j of this wave covers region bytes [(wave*NI + j)*1024, +1024)
+  int dq[K::NI];  // packed hy<<16 | hx<<8 | logical chunk, or -1 past the region
+#pragma unroll
+  for (int j = 0; j < K::NI; ++j) {
+    const int u = (wave * K::NI + j) * 64 + lane;  // 16-byte unit
+    const int q = u / K::CPP, pc = u % K::CPP;
+    if (q < K::RPX) {
+      const int c = pc ^ region_swz(q, K::CPP);
+      dq[j] = ((q / K::RW) << 16) | ((q % K::RW) << 8) | c;
+    } else {
+      dq[j] = -1;
+    }
+  }
+  const half_t* src = (const half_t*)sg.src + sg.coff;
+  const half_t* zero = (const half_t*)g_stream_zero;
+
+  auto issue_region = [&](int t, int slot) {
+    int b, oy0, ox0;
+    tile_coords(t, b, oy0, ox0);
+    unsigned char* dst = slots + slot * K::SLOT + wave * K::NI * 1024;
+#pragma unroll
+    for (int j = 0; j < K::NI; ++j) {
+      const half_t* p = zero;
+      if (dq[j] >= 0) {
+        const int iy = oy0 - 1 + (dq[j] >> 16);
+        const int ix = ox0 - 1 + ((dq[j] >> 8) & 255);
+        if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+          p = src + (size_t)((b * H + iy) * W + ix) * sg.cs + (dq[j] & 255) * 8;
+      }
+      __builtin_amdgcn_global_load_lds(p, (lds_void_ptr_s)(dst + j * 1024), 16, 0, 0);
+    }
+  };
+
+  const int first = band0 + idx;
+  const int step = per_xcd;
+  __syncthreads();  // filter in LDS (ordinary loads: hipcc waited for them)
+  if (first < band1) issue_region(first, 0);
+
+  // epilogue constants
+  const float* bias = op.bias;
+  float bv[K::NT][4];
+#pragma unroll
+  for (int nt = 0; nt < K::NT; ++nt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bv[nt][i] = bias ? bias[nt * 16 + fg * 4 + i] : 0.f;
+  float hw2[K::NT][4];
+  if constexpr (HEAD) {
+#pragma unroll
+    for (int nt = 0; nt < K::NT; ++nt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) hw2[nt][i] = op.head_w[nt * 16 + fg * 4 + i];
+  }
+  const int wswz = ((fr >> 2) & 1) << 1;  // filter row swizzle (rows fr + 16k)
+
+  int it = 0;
+  for (int t = first; t < band1; t += step, ++it) {
+    const int slot = it & 1;
+    // (A) the region of tile t has landed: younger than its DMA are only the
+    // previous tile's S stores
+    if (it == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K::S) : "memory");
+    __builtin_amdgcn_s_barrier();
+    int b, oy0, ox0;
+    tile_coords(t, b, oy0, ox0);
+    // residual / head inputs of tile t (asm loads, before the next DMA)
+    uint2 res[K::GPW][K::NT];
+    unsigned xin[K::GPW][3];
+    size_t opix[K::GPW];
+    bool ovalid[K::GPW];
+#pragma unroll
+    for (int g = 0; g < K::GPW; ++g) {
+      const int gy = (wave * K::GPW + g) >> 1, gx = ((wave * K::GPW + g) & 1) * 16 + fr;
+      const int y = oy0 + gy, x = ox0 + gx;
+      ovalid[g] = y < H && x < W;
+      opix[g] = ovalid[g] ? (size_t)(b * H + y) * W + x : 0;
+      if (args.res_count) {
+#pragma unroll
+        for (int nt = 0; nt < K::NT; ++nt)
+          res[g][nt] = asm_load_b64(ovalid[g] ? (const void*)((const half_t*)op.res2 + opix[g] * op.res2_cs + nt * 16 + fg * 4)
+                                              : (const void*)zero);
+      }
+      if constexpr (HEAD) {
+        const size_t HW = (size_t)H * W;
+        const size_t pb = (size_t)b * 3 * HW + (opix[g] - (size_t)b * HW);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          if (op.x_f16) xin[g][c] = asm_load_u16(ovalid[g] ? (const void*)((const half_t*)op.x_nchw + pb + c * HW) : (const void*)zero);
+          else xin[g][c] = asm_load_b32(ovalid[g] ? (const void*)(op.x_nchw + pb + c * HW) : (const void*)zero);
+        }
+      }
+    }
+    const bool has_next = t + step < band1;
+    if (has_next) issue_region(t + step, slot ^ 1);
+
+    // ---- MFMAs: D[n][px] = sum_k W[n][k] * X[px][k] -------------------------
+    f32x4_s acc[K::NT][K::GPW];
+#pragma unroll
+    for (int nt = 0; nt < K::NT; ++nt)
+#pragma unroll
+      for (int g = 0; g < K::GPW; ++g) acc[nt][g] = f32x4_s{0.f, 0.f, 0.f, 0.f};
+    const unsigned char* reg = slots + slot * K::SLOT;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int r = tap / 3, s = tap % 3;
+#pragma unroll
+      for (int ks = 0; ks < K::KS; ++ks) {
+        f16x8_s wf[K::NT];
+#pragma unroll
+        for (int nt = 0; nt < K::NT; ++nt)
+          wf[nt] = *(const f16x8_s*)(Wl + ((size_t)((tap * K::KS + ks) * NB + nt * 16 + fr) * 64) + ((fg ^ wswz) * 16));
+#pragma unroll
+        for (int g = 0; g < K::GPW; ++g) {
+          const int gy = (wave * K::GPW + g) >> 1, gx = ((wave * K::GPW + g) & 1) * 16;
+          const int q = (gy + r) * K::RW + gx + fr + s;
+          const int c = (ks * 4 + fg) ^ region_swz(q, K::CPP);
+          const f16x8_s xf = *(const f16x8_s*)(reg + q * K::RB + c * 16);
+#pragma unroll
+          for (int nt = 0; nt < K::NT; ++nt)
+            acc[nt][g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[nt], xf, acc[nt][g], 0, 0, 0);
+        }
+      }
+    }
+
+    // (B) this tile's asm loads are done; the next region's DMA may fly on
+    if (has_next) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K::G) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // pin every use of the asm-loaded registers below the wait (volatile asm
+    // statements keep their order; plain arithmetic could float above it)
+#pragma unroll
+    for (int g = 0; g < K::GPW; ++g) {
+      if (args.res_count) {
+#pragma unroll
+        for (int nt = 0; nt < K::NT; ++nt) asm volatile("" : "+v"(res[g][nt].x), "+v"(res[g][nt].y));
+      }
+      if constexpr (HEAD) asm volatile("" : "+v"(xin[g][0]), "+v"(xin[g][1]), "+v"(xin[g][2]));
+    }
+
+    // ---- epilogue -------------------------------------------------------------
+    if constexpr (HEAD) {
+      // r = sum_n relu(v_n) * w2_n ; illu = sigmoid(mean_c(x) + r + b2)
+#pragma unroll
+      for (int g = 0; g < K::GPW; ++g) {
+        float part = 0.f;
+#pragma unroll
+        for (int nt = 0; nt < K::NT; ++nt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) part += fmaxf(acc[nt][g][i] + bv[nt][i], 0.f) * hw2[nt][i];
+        part += __shfl_xor(part, 16);
+        part += __shfl_xor(part, 32);
+        float x0, x1, x2;
+        if (op.x_f16) {
+          x0 = (float)__builtin_bit_cast(half_t, (unsigned short)(xin[g][0] & 0xffff));
+          x1 = (float)__builtin_bit_cast(half_t, (unsigned short)(xin[g][1] & 0xffff));
+          x2 = (float)__builtin_bit_cast(half_t, (unsigned short)(xin[g][2] & 0xffff));
+        } else {
+          x0 = __builtin_bit_cast(float, xin[g][0]);
+          x1 = __builtin_bit_cast(float, xin[g][1]);
+          x2 = __builtin_bit_cast(float, xin[g][2]);
+        }
+        const float z = (x0 + x1 + x2) / 3.f + (part + op.head_b);
+        const float il = 1.f / (1.f + expf(-z));
+        float* dst = (ovalid[g] && fg == 0) ? op.illu + opix[g] : (float*)(g_stream_sink + tid);
+        *dst = il;
+      }
+    } else {
+#pragma unroll
+      for (int g = 0; g < K::GPW; ++g) {
+#pragma unroll
+        for (int nt = 0; nt < K::NT; ++nt) {
+          float v[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            v[i] = acc[nt][g][i] + bv[nt][i];
+            if (op.relu) v[i] = fmaxf(v[i], 0.f);
+          }
+          if (args.res_count) {
+            const f16x4_s rr = __builtin_bit_cast(f16x4_s, res[g][nt]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] += (float)rr[i];
+          }
+          f16x4_s o;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) o[i] = (half_t)v[i];
+          uint2* dst = ovalid[g] ? (uint2*)((half_t*)op.out + opix[g] * op.out_cs + op.out_coff + nt * 16 + fg * 4)
+                                 : g_stream_sink + tid;
+          *dst = __builtin_bit_cast(uint2, o);
+        }
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int C, int NB, int TH, bool HEAD>
+static int launch_stream_cfg(const ConvOp& op, hipStream_t st) {
+  using K = StreamCfg<C, NB, TH, HEAD>;
+  static int occ = 0;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)conv_stream_kernel<C, NB, TH, HEAD>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, K::LDS);
+    if (e != hipSuccess) return (int)e;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)conv_stream_kernel<C, NB, TH, HEAD>, 256,
+                                                     K::LDS);
+    if (e != hipSuccess) return (int)e;
+    if (occ < 1) occ = 1;
+    attr = true;
+  }
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  StreamArgs a;
+  a.op = op;
+  a.tiles_x = cdiv(op.Wo, ST_TW);
+  a.tiles_y = cdiv(op.Ho, TH);
+  a.ntiles = op.B * a.tiles_x * a.tiles_y;
+  a.res_count = op.res2 ? 1 : 0;
+  int grid = cus * occ;
+  grid = std::min(grid, cdiv(a.ntiles, 8) * 8);
+  grid = std::max(8, grid / 8 * 8);
+  hipLaunchKernelGGL((conv_stream_kernel<C, NB, TH, HEAD>), dim3(grid), dim3(256), K::LDS, st, a);
+  return (int)hipGetLastError();
+}
+
+// UPR_CONV_STREAM=0 disables this path (A/B timing)
+static bool stream_enabled() {
+  static int en = -1;
+  if (en < 0) {
+    const char* e = getenv("UPR_CONV_STREAM");
+    en = (e && strcmp(e, "0") == 0) ? 0 : 1;
+  }
+  return en == 1;
+}
+
+// fp16 only; kErrUnsupported for every op this kernel does not take
+int launch_conv_stream(const ConvOp& op, hipStream_t st) {
+  if (!stream_enabled() || op.nseg != 1) return kErrUnsupported;
+  const ConvSeg& s = op.seg[0];
+  if (s.kh != 3 || s.kw != 3 || s.stride != 1 || s.dil != 1 || s.pad != 1 || s.pre != kPreNone) return kErrUnsupported;
+  if (s.Hin != op.Ho || s.Win != op.Wo) return kErrUnsupported;
+  if ((s.C != 32 && s.C != 64) || s.cs % 8 || s.coff % 8 || (uintptr_t)s.src % 16) return kErrUnsupported;
+  if (op.res1 || op.img_bias || op.pool || op.scale || op.Kpad % 8 || s.kbase != 0) return kErrUnsupported;
+  if (op.Wo < 24 || op.Ho < 8) return kErrUnsupported;
+  if (op.store == kStoreHeadIllu) {
+    if (op.N != 32 || s.C != 32 || op.res2) return kErrUnsupported;
+    return launch_stream_cfg<32, 32, 8, true>(op, st);
+  }
+  if (op.store != kStoreNHWC || op.out_cs % 4 || op.out_coff % 4) return kErrUnsupported;
+  if (op.res2 && op.res2_cs % 4) return kErrUnsupported;
+  if (s.C == 32 && op.N == 32) return launch_stream_cfg<32, 32, 8, false>(op, st);
+  if (s.C == 32 && op.N == 64) return launch_stream_cfg<32, 64, 8, false>(op, st);
+  if (s.C == 64 && op.N == 64) return launch_stream_cfg<64, 64, 4, false>(op, st);
+  return kErrUnsupported;
+}
+
+}  // namespace upr

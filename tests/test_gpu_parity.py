@@ -59,6 +59,10 @@ CONV_CASES = [
     (3, 20, 28, 64, 128, 3, 2, 1, 1, True, True),
     (2, 30, 34, 256, 256, 3, 1, 12, 12, False, True),
     (1, 17, 23, 128, 512, 1, 1, 0, 1, True, False),
+    # shapes routed to the streaming LDS-DMA halo kernel in fp16 (3x3 s1, C 32/64, no pre-ReLU residual)
+    (2, 20, 45, 32, 32, 3, 1, 1, 1, True, False),
+    (1, 9, 70, 32, 64, 3, 1, 1, 1, False, False),
+    (3, 13, 29, 64, 64, 3, 1, 1, 1, True, False),
 ]
 
 
