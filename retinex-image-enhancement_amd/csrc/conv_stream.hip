@@ -332,6 +332,269 @@ __global__ __launch_bounds__(256) void conv_stream_kernel(StreamArgs args) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// ---------------------------------------------------------------------------
+// EnhancedFAM fusion GEMM (models/model.py:29-44, :66-78) on the same streaming
+// structure: y = relu(Wf3.conv3x3(h3) + Wf4.conv3x3_d2(h4) + Wf1.x + Wf2.maxpool3(x) + b)
+// with the fusion 1x1 composed into every branch (model.hip), K = 640, N = 32,
+// plus the per-image channel sums of y for the channel attention.
+//   * two regions per 4 x 32 tile: h (64 channels = [h3 | h4], 2-pixel halo,
+//     8 x 36 px x 128 B) and x (32 channels, 1-pixel halo, 6 x 34 px x 64 B,
+//     -inf outside the image: the max-pool ignores padding);
+//   * the max-pool branch's operand is the 3x3 max of the x region, taken from
+//     LDS while building the MFMA fragment.
+// ---------------------------------------------------------------------------
+__device__ __attribute__((aligned(256))) unsigned g_stream_ninf[64] = {
+#define NINF4 0xFC00FC00u, 0xFC00FC00u, 0xFC00FC00u, 0xFC00FC00u
+    NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4
+#undef NINF4
+};
+
+struct FamCfg {
+  static constexpr int TH = 4, GPW = 2, NT = 2, NB = 32;
+  static constexpr int HRW = ST_TW + 4, HRH = TH + 4, HPX = HRW * HRH;  // 36 x 8
+  static constexpr int XRW = ST_TW + 2, XRH = TH + 2, XPX = XRW * XRH;  // 34 x 6
+  static constexpr int HNI = (HPX * 128 + 4095) / 4096;                 // 9
+  static constexpr int XNI = (XPX * 64 + 4095) / 4096;                  // 4
+  static constexpr int G = HNI + XNI;
+  static constexpr int HSLOT = HNI * 4096, XSLOT = XNI * 4096;
+  static constexpr int SLOT = HSLOT + XSLOT;
+  static constexpr int NSL = 20;                                        // 32-deep k slices
+  static constexpr int WBYTES = NSL * NB * 64;
+  static constexpr int LDS = WBYTES + 2 * SLOT;
+  static constexpr int S = GPW * NT;                                    // stores per wave per tile
+};
+
+__global__ __launch_bounds__(256) void conv_stream_fam_kernel(StreamArgs args) {
+  using K = FamCfg;
+  const ConvOp& op = args.op;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* Wl = smem;
+  unsigned char* slots = smem + K::WBYTES;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int H = op.Ho, W = op.Wo;
+  const int nblk = gridDim.x;
+  const int xcd = blockIdx.x & 7, idx = blockIdx.x >> 3;
+  const int per_xcd = nblk >> 3;
+  const int band0 = (int)((long long)args.ntiles * xcd / 8), band1 = (int)((long long)args.ntiles * (xcd + 1) / 8);
+  auto tile_coords = [&](int t, int& b, int& oy0, int& ox0) {
+    const int tx = t % args.tiles_x;
+    const int r = t / args.tiles_x;
+    b = r / args.tiles_y;
+    oy0 = (r % args.tiles_y) * K::TH;
+    ox0 = tx * ST_TW;
+  };
+  // resident filter: slice sl = global k [32 sl, 32 sl + 32)
+  {
+    const half_t* Wg = (const half_t*)op.W;
+    for (int i = tid; i < K::NSL * K::NB * 4; i += 256) {
+      const int pc = i & 3, n = (i >> 2) % K::NB, sl = (i >> 2) / K::NB;
+      const int c = pc ^ (((n >> 2) & 1) << 1);
+      *(uint4*)(Wl + (size_t)i * 16) = *(const uint4*)(Wg + (size_t)n * op.Kpad + sl * 32 + c * 8);
+    }
+  }
+  int hq[K::HNI], xq[K::XNI];
+#pragma unroll
+  for (int j = 0; j < K::HNI; ++j) {
+    const int u = (wave * K::HNI + j) * 64 + lane, q = u >> 3, pc = u & 7;
+    hq[j] = q < K::HPX ? ((q / K::HRW) << 16) | ((q % K::HRW) << 8) | (pc ^ (q & 7)) : -1;
+  }
+#pragma unroll
+  for (int j = 0; j < K::XNI; ++j) {
+    const int u = (wave * K::XNI + j) * 64 + lane, q = u >> 2, pc = u & 3;
+    xq[j] = q < K::XPX ? ((q / K::XRW) << 16) | ((q % K::XRW) << 8) | (pc ^ region_swz(q, 4)) : -1;
+  }
+  const ConvSeg& sh = op.seg[0];
+  const ConvSeg& sx = op.seg[2];
+  const half_t* hsrc = (const half_t*)sh.src;  // [h3 | h4], pixel stride sh.cs
+  const half_t* xsrc = (const half_t*)sx.src + sx.coff;
+  const half_t* zero = (const half_t*)g_stream_zero;
+  const half_t* ninf = (const half_t*)g_stream_ninf;
+  auto issue_region = [&](int t, int slot) {
+    int b, oy0, ox0;
+    tile_coords(t, b, oy0, ox0);
+    unsigned char* hd = slots + slot * K::SLOT + wave * K::HNI * 1024;
+    unsigned char* xd = slots + slot * K::SLOT + K::HSLOT + wave * K::XNI * 1024;
+#pragma unroll
+    for (int j = 0; j < K::HNI; ++j) {
+      const half_t* p = zero;
+      if (hq[j] >= 0) {
+        const int iy = oy0 - 2 + (hq[j] >> 16), ix = ox0 - 2 + ((hq[j] >> 8) & 255);
+        if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+          p = hsrc + (size_t)((b * H + iy) * W + ix) * sh.cs + (hq[j] & 255) * 8;
+      }
+      __builtin_amdgcn_global_load_lds(p, (lds_void_ptr_s)(hd + j * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < K::XNI; ++j) {
+      const half_t* p = ninf;
+      if (xq[j] >= 0) {
+        const int iy = oy0 - 1 + (xq[j] >> 16), ix = ox0 - 1 + ((xq[j] >> 8) & 255);
+        if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+          p = xsrc + (size_t)((b * H + iy) * W + ix) * sx.cs + (xq[j] & 255) * 8;
+      }
+      __builtin_amdgcn_global_load_lds(p, (lds_void_ptr_s)(xd + j * 1024), 16, 0, 0);
+    }
+  };
+  const int first = band0 + idx, step = per_xcd;
+  __syncthreads();
+  if (first < band1) issue_region(first, 0);
+  float bv[K::NT][4];
+#pragma unroll
+  for (int nt = 0; nt < K::NT; ++nt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bv[nt][i] = op.bias ? op.bias[nt * 16 + fg * 4 + i] : 0.f;
+  const int wswz = ((fr >> 2) & 1) << 1;
+  float pool[K::NT][4];
+#pragma unroll
+  for (int nt = 0; nt < K::NT; ++nt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pool[nt][i] = 0.f;
+  int pool_img = -1;
+  bool flushed = false;
+  // flush this lane's pooled sums of image pool_img (reduced over the 16 pixel lanes)
+  auto flush = [&]() {
+#pragma unroll
+    for (int nt = 0; nt < K::NT; ++nt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float v = pool[nt][i];
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        v += __shfl_xor(v, 4);
+        v += __shfl_xor(v, 8);
+        if (fr == 0) atomicAdd(op.pool + (size_t)pool_img * op.N + nt * 16 + fg * 4 + i, v);
+        pool[nt][i] = 0.f;
+      }
+  };
+
+  int it = 0;
+  for (int t = first; t < band1; t += step, ++it) {
+    const int slot = it & 1;
+    if (it == 0 || flushed) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K::S) : "memory");
+    __builtin_amdgcn_s_barrier();
+    flushed = false;
+    int b, oy0, ox0;
+    tile_coords(t, b, oy0, ox0);
+    const bool has_next = t + step < band1;
+    if (has_next) issue_region(t + step, slot ^ 1);
+
+    f32x4_s acc[K::NT][K::GPW];
+#pragma unroll
+    for (int nt = 0; nt < K::NT; ++nt)
+#pragma unroll
+      for (int g = 0; g < K::GPW; ++g) acc[nt][g] = f32x4_s{0.f, 0.f, 0.f, 0.f};
+    const unsigned char* hreg = slots + slot * K::SLOT;
+    const unsigned char* xreg = hreg + K::HSLOT;
+    auto wfrag = [&](int sl, f16x8_s (&wf)[K::NT]) {
+#pragma unroll
+      for (int nt = 0; nt < K::NT; ++nt)
+        wf[nt] = *(const f16x8_s*)(Wl + ((size_t)(sl * K::NB + nt * 16 + fr) * 64) + ((fg ^ wswz) * 16));
+    };
+    // h3 (3x3, d1) and h4 (3x3, d2): slices 0..8 and 9..17
+#pragma unroll
+    for (int seg = 0; seg < 2; ++seg) {
+      const int d = seg + 1;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int r = tap / 3, s = tap % 3;
+        f16x8_s wf[K::NT];
+        wfrag(seg * 9 + tap, wf);
+#pragma unroll
+        for (int g = 0; g < K::GPW; ++g) {
+          const int gx = g * 16;
+          const int q = (wave + 2 + (r - 1) * d) * K::HRW + gx + 2 + (s - 1) * d + fr;
+          const int c = (seg * 4 + fg) ^ (q & 7);
+          const f16x8_s xf = *(const f16x8_s*)(hreg + q * 128 + c * 16);
+#pragma unroll
+          for (int nt = 0; nt < K::NT; ++nt)
+            acc[nt][g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[nt], xf, acc[nt][g], 0, 0, 0);
+        }
+      }
+    }
+    // x (1x1) and maxpool3(x) (1x1): slices 18, 19
+    {
+      f16x8_s w1[K::NT], w2[K::NT];
+      wfrag(18, w1);
+      wfrag(19, w2);
+#pragma unroll
+      for (int g = 0; g < K::GPW; ++g) {
+        const int gx = g * 16;
+        f16x8_s ctr = {}, mx = {};
+#pragma unroll
+        for (int dr = 0; dr < 3; ++dr)
+#pragma unroll
+          for (int ds = 0; ds < 3; ++ds) {
+            const int q = (wave + dr) * K::XRW + gx + ds + fr;
+            const f16x8_s v = *(const f16x8_s*)(xreg + q * 64 + ((fg ^ region_swz(q, 4)) * 16));
+            if (dr == 0 && ds == 0) mx = v;
+            else mx = __builtin_elementwise_max(mx, v);
+            if (dr == 1 && ds == 1) ctr = v;
+          }
+#pragma unroll
+        for (int nt = 0; nt < K::NT; ++nt) {
+          acc[nt][g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[nt], ctr, acc[nt][g], 0, 0, 0);
+          acc[nt][g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w2[nt], mx, acc[nt][g], 0, 0, 0);
+        }
+      }
+    }
+    if (has_next) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K::G) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // epilogue: y = relu(acc + b) in fp16, pooled sums of the stored values
+    if (op.pool && pool_img != b) {
+      if (pool_img >= 0) { flush(); flushed = true; }
+      pool_img = b;
+    }
+#pragma unroll
+    for (int g = 0; g < K::GPW; ++g) {
+      const int y = oy0 + wave, x = ox0 + g * 16 + fr;
+      const bool ok = y < H && x < W;
+      const size_t opix = ok ? (size_t)(b * H + y) * W + x : 0;
+#pragma unroll
+      for (int nt = 0; nt < K::NT; ++nt) {
+        f16x4_s o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          o[i] = (half_t)fmaxf(acc[nt][g][i] + bv[nt][i], 0.f);
+          if (ok) pool[nt][i] += (float)o[i];
+        }
+        uint2* dst = ok ? (uint2*)((half_t*)op.out + opix * op.out_cs + op.out_coff + nt * 16 + fg * 4)
+                        : g_stream_sink + tid;
+        *dst = __builtin_bit_cast(uint2, o);
+      }
+    }
+  }
+  if (op.pool && pool_img >= 0) flush();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+static int launch_stream_fam(const ConvOp& op, hipStream_t st) {
+  static int occ = 0;
+  if (!occ) {
+    hipError_t e = hipFuncSetAttribute((const void*)conv_stream_fam_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       FamCfg::LDS);
+    if (e != hipSuccess) return (int)e;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)conv_stream_fam_kernel, 256, FamCfg::LDS);
+    if (e != hipSuccess) return (int)e;
+    if (occ < 1) occ = 1;
+  }
+  int cus = 0, dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
+  StreamArgs a;
+  a.op = op;
+  a.tiles_x = cdiv(op.Wo, ST_TW);
+  a.tiles_y = cdiv(op.Ho, FamCfg::TH);
+  a.ntiles = op.B * a.tiles_x * a.tiles_y;
+  a.res_count = 0;
+  int grid = std::min(cus * occ, cdiv(a.ntiles, 8) * 8);
+  grid = std::max(8, grid / 8 * 8);
+  hipLaunchKernelGGL(conv_stream_fam_kernel, dim3(grid), dim3(256), FamCfg::LDS, st, a);
+  return (int)hipGetLastError();
+}
+
 template <int C, int NB, int TH, bool HEAD>
 static int launch_stream_cfg(const ConvOp& op, hipStream_t st) {
   using K = StreamCfg<C, NB, TH, HEAD>;
@@ -378,8 +641,25 @@ static bool stream_enabled() {
 }
 
 // fp16 only; kErrUnsupported for every op this kernel does not take
+static bool fam_program(const ConvOp& op) {
+  if (op.nseg != 4 || op.N != 32 || op.store != kStoreNHWC || op.res1 || op.res2 || op.img_bias || op.scale) return false;
+  if (op.Kpad != 640 || op.Wo < 24 || op.Ho < 8 || op.out_cs % 4 || op.out_coff % 4) return false;
+  const ConvSeg* s = op.seg;
+  auto same_res = [&](const ConvSeg& q) { return q.Hin == op.Ho && q.Win == op.Wo && q.stride == 1 && q.C == 32; };
+  for (int i = 0; i < 4; ++i)
+    if (!same_res(s[i]) || s[i].kbase != (i < 2 ? 288 * i : 576 + 32 * (i - 2))) return false;
+  if (s[0].kh != 3 || s[0].dil != 1 || s[0].pad != 1 || s[0].pre != kPreNone || s[0].coff != 0) return false;
+  if (s[1].kh != 3 || s[1].dil != 2 || s[1].pad != 2 || s[1].pre != kPreNone || s[1].coff != 32) return false;
+  if (s[0].src != s[1].src || s[0].cs != 64 || s[1].cs != 64 || (uintptr_t)s[0].src % 16) return false;
+  if (s[2].kh != 1 || s[2].pre != kPreNone || s[3].kh != 1 || s[3].pre != kPreMaxPool3) return false;
+  if (s[2].src != s[3].src || s[2].cs != s[3].cs || s[2].coff != s[3].coff || s[2].cs % 8 || s[2].coff % 8) return false;
+  return (uintptr_t)s[2].src % 16 == 0;
+}
+
 int launch_conv_stream(const ConvOp& op, hipStream_t st) {
-  if (!stream_enabled() || op.nseg != 1) return kErrUnsupported;
+  if (!stream_enabled()) return kErrUnsupported;
+  if (fam_program(op)) return launch_stream_fam(op, st);
+  if (op.nseg != 1) return kErrUnsupported;
   const ConvSeg& s = op.seg[0];
   if (s.kh != 3 || s.kw != 3 || s.stride != 1 || s.dil != 1 || s.pad != 1 || s.pre != kPreNone) return kErrUnsupported;
   if (s.Hin != op.Ho || s.Win != op.Wo) return kErrUnsupported;
