@@ -32,7 +32,8 @@ namespace upr {
 int launch_prep(const void* x, void* x2p, void* x3p, int B, int H, int W, int dtype, hipStream_t st);
 int launch_preact_f16(const void* x, const float* sc, const float* sh, void* o, size_t npix, int C, hipStream_t st);
 int launch_conv3(const void* x, const float* w, const float* bias, void* out0, void* out1, int B, int h, int wd,
-                 int dtype, hipStream_t st);
+                 int dtype, hipStream_t st, void* out2 = nullptr, const float* ps = nullptr,
+                 const float* ph = nullptr);
 int launch_fam_ca(const float* pool, const float* w1, const float* b1, const float* w2, const float* b2, float* ca,
                   int B, int HW, hipStream_t st);
 int launch_fam_mix(const void* y, const float* ca, const float* P, float* mm, float* p, int B, int HW, int dtype,
@@ -275,7 +276,8 @@ struct Op {
   int img_bias = 0;
   size_t head_w = 0; float head_b = 0.f;
   // conv3 / fam
-  int in = -1, out1 = -1;
+  int in = -1, out1 = -1, out2 = -1;  // conv3: out2 = fused enc1 PreAct output (scale b2/sh2)
+  size_t ps = 0, ph = 0;
   size_t w = 0, b = 0;
   int fam = 0;       // which scale (0..2)
   size_t ca_w1 = 0, ca_b1 = 0, ca_w2 = 0, ca_b2 = 0, P = 0, sa_w = 0;
@@ -458,7 +460,14 @@ struct Builder {
       if (!bn_fold(P, p + ".bn1", cin, bn1) || !bn_fold(P, p + ".bn2", cout, bn2)) { ok = false; return; }
       const size_t pre_s = blob.add_f32(bn1.s), pre_h = blob.add_f32(bn1.sh);
       int osrc = in, opre = kPreAffineRelu;
-      if (preact_materialised(m)) {
+      Op* conv3_producer = nullptr;
+      for (auto& o : m->ops)
+        if (o.kind == OP_CONV3 && o.out == in) conv3_producer = &o;
+      if (preact_materialised(m) && conv3_producer) {
+        // enc1: the 3->32 input conv writes relu(bn1(x1)) beside x1 (one pass)
+        conv3_producer->out2 = B_PA1; conv3_producer->ps = pre_s; conv3_producer->ph = pre_h;
+        osrc = B_PA1; opre = kPreNone;
+      } else if (preact_materialised(m)) {
         Op po;
         po.kind = OP_PREACT; po.name = p + ".bn1_relu"; po.in = in; po.level = in_level; po.w = pre_s; po.b = pre_h;
         po.out = in_level == 0 ? B_PA1 : (in_level == 1 ? B_PA2 : (in_level == 2 ? B_PA3 : B_PA4));
@@ -787,7 +796,8 @@ static int run_forward(UprModel* m, const void* x, int B, int H, int W, void* en
         int h, w;
         lvl_dims(o.lvl_shift, h, w);
         rc = launch_conv3(buf(o.in), fptr(o.w), fptr(o.b), buf(o.out), o.out1 >= 0 ? buf(o.out1) : nullptr, B, h, w,
-                          dt, st);
+                          dt, st, o.out2 >= 0 ? buf(o.out2) : nullptr, o.out2 >= 0 ? fptr(o.ps) : nullptr,
+                          o.out2 >= 0 ? fptr(o.ph) : nullptr);
         break;
       }
       case OP_GEMM: {

@@ -9,6 +9,7 @@
 //  fam_sa         7x7 spatial attention conv + sigmoid, scales the projection (:56-59, :94-95)
 //  retinex_tail   sigmoid(head) , R = x/(I+1e-6), R*E + (1-R)*E^2 (:411-412, :430-442)
 #include <algorithm>
+#include <cstdlib>
 
 #include "upr_common.h"
 
@@ -303,10 +304,112 @@ int launch_prep(const void* x, void* x2p, void* x3p, int B, int H, int W, int dt
   return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// fp16 3 -> 32/64 first convs on MFMA (input_layer + scale1.0 in one launch,
+// scale2.1 / scale3.1; models/model.py:296, :380-390).  A block owns an 8 x 32
+// output tile; the 3 x 10 x 34 input region (planar, zero padded) sits in
+// LDS; K = 27 taps x channels padded to 32 = one v_mfma_f32_16x16x32_f16 per
+// (16 pixels, 16 outputs), weights as the A operand (in registers), pixels as
+// B, so each lane ends with 4 consecutive output channels of one pixel and
+// stores 8-byte runs.  Optionally also writes o = relu(bn1(out0)) (the enc1
+// PreAct prologue, rounded exactly like OP_PREACT: from the stored fp16 value).
+// ---------------------------------------------------------------------------
+template <int NO>
+__global__ __launch_bounds__(256) void conv3_mfma_kernel(const half_t* __restrict__ x, const float* __restrict__ w,
+                                                         const float* __restrict__ bias, half_t* __restrict__ out0,
+                                                         half_t* __restrict__ out1, half_t* __restrict__ out2,
+                                                         const float* __restrict__ ps, const float* __restrict__ ph,
+                                                         int h, int wd, int tiles_x, int tiles_y) {
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  constexpr int NT = NO * 2, RW = 34, RH = 10, RP = RW * RH;
+  __shared__ half_t reg[3 * RP];
+  __shared__ __attribute__((aligned(16))) half_t tr[4][3][16 * 32];  // per-wave 16-pixel transpose, <= 3 outputs
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fg = lane >> 4;
+  const int tx = blockIdx.x % tiles_x, ty = (blockIdx.x / tiles_x) % tiles_y, b = blockIdx.x / (tiles_x * tiles_y);
+  const int oy0 = ty * 8, ox0 = tx * 32;
+  const size_t HW = (size_t)h * wd;
+  for (int e = tid; e < 3 * RP; e += 256) {
+    const int c = e / RP, r = e - c * RP, hy = r / RW, hx = r - hy * RW;
+    const int iy = oy0 - 1 + hy, ix = ox0 - 1 + hx;
+    reg[e] = ((unsigned)iy < (unsigned)h && (unsigned)ix < (unsigned)wd) ? x[((size_t)b * 3 + c) * HW + (size_t)iy * wd + ix]
+                                                                         : (half_t)0.f;
+  }
+  h8 wf[NT];
+  float bv[NT][4];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = fg * 8 + e;
+      wf[nt][e] = k < 27 ? (half_t)w[k * (NO * 32) + nt * 16 + fr] : (half_t)0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bv[nt][i] = bias[nt * 16 + fg * 4 + i];
+  }
+  int koff[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = fg * 8 + e, c = k / 9, ky = (k % 9) / 3, kx = k % 3;
+    koff[e] = k < 27 ? c * RP + ky * RW + kx : -1;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int gy = wave * 2 + (g >> 1), gx = (g & 1) * 16 + fr;
+    h8 xf;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) xf[e] = koff[e] >= 0 ? reg[koff[e] + gy * RW + gx] : (half_t)0.f;
+    f4 acc[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[nt], xf, f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    // transpose through this wave's LDS scratch: lane (pixel fr, channels
+    // 4fg..4fg+3 of tile nt) -> lane l stores 16 bytes (pixel l/4, channels
+    // 8(l%4)..): every store instruction writes the group's 1 KiB run of one
+    // output contiguously
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      h4 o;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] = (half_t)fmaxf(acc[nt][i] + bv[nt][i], 0.f);
+      *(h4*)(&tr[wave][nt >> 1][fr * 32 + (nt & 1) * 16 + fg * 4]) = o;
+      if (out2 && nt < 2) {
+        h4 q;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int c = nt * 16 + fg * 4 + i;
+          q[i] = (half_t)fmaxf((float)o[i] * ps[c] + ph[c], 0.f);
+        }
+        *(h4*)(&tr[wave][2][fr * 32 + nt * 16 + fg * 4]) = q;
+      }
+    }
+    const int y = oy0 + gy, xs = ox0 + (g & 1) * 16 + (lane >> 2);
+    if (y < h && xs < wd) {
+      const size_t off = ((size_t)b * HW + (size_t)y * wd + xs) * 32 + (lane & 3) * 8;
+      *(h8*)(out0 + off) = *(const h8*)(&tr[wave][0][lane * 8]);
+      if (NO == 2) *(h8*)(out1 + off) = *(const h8*)(&tr[wave][1][lane * 8]);
+      if (out2) *(h8*)(out2 + off) = *(const h8*)(&tr[wave][2][lane * 8]);
+    }
+  }
+}
+
 int launch_conv3(const void* x, const float* w, const float* bias, void* out0, void* out1, int B, int h, int wd,
-                 int dtype, hipStream_t st) {
+                 int dtype, hipStream_t st, void* out2, const float* ps, const float* ph) {
   const int n = B * h * wd;
   if (n <= 0) return kErrShape;
+  if (dtype == kF16 && getenv("UPR_CONV3_DIRECT") == nullptr) {
+    const int tx = cdiv(wd, 32), ty = cdiv(h, 8);
+    if (out1)
+      hipLaunchKernelGGL((conv3_mfma_kernel<2>), dim3(B * tx * ty), dim3(256), 0, st, (const half_t*)x, w, bias,
+                         (half_t*)out0, (half_t*)out1, (half_t*)out2, ps, ph, h, wd, tx, ty);
+    else
+      hipLaunchKernelGGL((conv3_mfma_kernel<1>), dim3(B * tx * ty), dim3(256), 0, st, (const half_t*)x, w, bias,
+                         (half_t*)out0, (half_t*)nullptr, (half_t*)out2, ps, ph, h, wd, tx, ty);
+    return (int)hipGetLastError();
+  }
+  if (out2) return kErrUnsupported;  // the fused PreAct output exists on the MFMA path only
   if (dtype == kF16) {
     if (out1)
       hipLaunchKernelGGL((conv3_direct_kernel<half_t, half_t, 2>), dim3(grid1d(n)), dim3(256), 0, st,
