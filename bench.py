@@ -74,7 +74,8 @@ def cpu_baseline(sd, pre, aspp, size, budget_s):
             "sample": f"{n} x 1x3x{size}x{size} fp32 forwards of oracle/net.py (torch-CPU), {el:.1f}s"}
 
 
-CONV_KERNELS = ("conv_halo_kernel", "conv_igemm_kernel")
+CONV_KERNELS = ("conv_halo_kernel", "conv_igemm_kernel", "conv_wide_kernel", "conv_stream_kernel",
+                "conv_stream_fam_kernel")
 
 
 def pmc_traffic(args):
@@ -113,7 +114,7 @@ def pmc_traffic(args):
             tot, n = 0.0, 0
             with open(path) as f:
                 for r in csv.DictReader(f):
-                    if r["Counter_Name"] == ctr and r["Kernel_Name"].startswith(CONV_KERNELS):
+                    if r["Counter_Name"] == ctr and any(k in r["Kernel_Name"] for k in CONV_KERNELS):
                         tot += float(r["Counter_Value"])
                         n += 1
             out[ctr] = (tot, n)
@@ -313,18 +314,26 @@ def main():
         all_ms = sum(s["ms"] for s in stats)
         achieved = g_flops / (g_ms * 1e-3) / 1e12 if g_ms > 0 else 0.0
         peak = PEAK_TFLOPS[args.precision]
+        # per-layer roofline: each conv launch is bounded by max(flops / MFMA
+        # peak, algorithmic bytes / HBM peak); layer_frac = sum of those bounds
+        # over the measured conv time (1.0 = every conv at its own roofline)
+        t_roof = sum(max(s["flops"] / (peak * 1e12), s["bytes"] / (PEAK_HBM_GBS * 1e9)) for s in gemm)
+        n_hbm = sum(1 for s in gemm if s["bytes"] / (PEAK_HBM_GBS * 1e9) > s["flops"] / (peak * 1e12))
         out["roofline"] = {
             "bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
             "traffic": traffic["bytes_per_launch"] if traffic else None,
             "traffic_unit": "bytes per conv launch (rocprofv3 FETCH_SIZE*2 + WRITE_SIZE)",
             "traffic_per_img_GB": traffic["bytes_per_forward"] / B / 1e9 if traffic else None,
             "alg_bytes_per_launch": g_bytes / max(g_calls, 1),
-            "kernel": "conv_halo_kernel<*> + conv_igemm_kernel<*> (all conv launches of the step)",
+            "kernel": "conv family: conv_wide/conv_stream/conv_stream_fam/conv_halo/conv_igemm (all conv launches of the step)",
             "launches_per_step": g_calls / args.steps,
             "avg_launch_us": 1000.0 * g_ms / max(g_calls, 1),
             "gemm_gflop_per_img": g_flops / (args.steps * B) / 1e9,
             "gemm_alg_GB_per_img": g_bytes / (args.steps * B) / 1e9,
             "gemm_share_of_device_time": g_ms / all_ms if all_ms else None,
+            "layer_roofline_frac": (t_roof * 1e3) / g_ms if g_ms > 0 else None,
+            "layer_roofline_note": f"sum over conv launches of max(flops/MFMA peak, alg bytes/HBM peak) / measured; "
+                                   f"{n_hbm} of {len(gemm)} conv ops are HBM-bound at {args.precision}",
             "ref_equiv_tflops": REF_GFLOP_PER_IMG[args.variant] * (S / 512) ** 2 * total_imgs / world / elapsed / 1e3,
         }
         if args.breakdown and rank == 0:
