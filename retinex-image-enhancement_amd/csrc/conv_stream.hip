@@ -47,6 +47,9 @@ __device__ __attribute__((aligned(256))) uint4 g_stream_zero[16];
 __device__ __attribute__((aligned(256))) uint2 g_stream_sink[64 * 64];
 
 constexpr int ST_TW = 32;  // tile width (output pixels)
+// L2 prefetch of tile t+2 (prefetch_region): measured 5-8% SLOWER on the FAM
+// fusion and the 3x3 stream kernels (1.05 -> 1.14 ms, 0.50 -> 0.54 ms), so off
+constexpr bool kStreamPrefetch = false;
 
 template <int C, int NB, int TH, bool HEAD>
 struct StreamCfg {
@@ -57,7 +60,7 @@ struct StreamCfg {
   static constexpr int NI = (RPX * RB + 4096 - 1) / 4096;  // DMA instructions per wave (4 waves x 1 KiB)
   static constexpr int SLOT = NI * 4096;            // bytes per region slot
   static constexpr int WBYTES = 9 * C * NB * 2;     // resident filter
-  static constexpr int LDS = WBYTES + 2 * SLOT;
+  static constexpr int LDS = WBYTES + 2 * SLOT + 1024;  // + per-wave prefetch dummy rows
   static constexpr int GPW = TH / 2;                // 16-pixel groups per wave (tile has 2*TH groups)
   static constexpr int NT = NB / 16;                // 16-channel tiles
   static constexpr int KS = C / 32;                 // 32-deep k slices per tap
@@ -65,6 +68,7 @@ struct StreamCfg {
   static constexpr int G = NI;                      // region DMA
   static constexpr int R = HEAD ? 3 * GPW : 0;      // asm loads (x for the head; residual handled separately)
   static constexpr int S = HEAD ? GPW : GPW * NT;   // stores
+  static constexpr int NPF = kStreamPrefetch ? (RH * ((RW * RB + 127) / 128 + 1) + 255) / 256 : 0;
 };
 
 __device__ __forceinline__ int region_swz(int q, int cpp) {
@@ -86,6 +90,30 @@ __device__ __forceinline__ unsigned asm_load_b32(const void* p) {
   unsigned v;
   asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p) : "memory");
   return v;
+}
+
+// L2 prefetch of a future tile's region: one 4-byte LDS-DMA per 128-byte line
+// into a per-wave dummy LDS row (never read), so that the region DMA issued
+// one tile later hits L2.  LDS-DMA has no VGPR destination, so nothing has to
+// stay allocated while it flies.  Each thread issues exactly NPF of them
+// (out-of-image lines read the zero line): the per-wave memory-instruction
+// count stays constant for the counted vmcnt waits.
+template <int NPF>
+__device__ __forceinline__ void prefetch_region(const half_t* src, int cs, int b, int H, int W, int iy0, int ix0,
+                                                int rh, int rw, int tid, const void* zero, unsigned char* dummy) {
+  const int ix_lo = max(ix0, 0), ix_hi = min(ix0 + rw, W);
+  const int row_bytes = (ix_hi - ix_lo) * cs * 2;
+  const int lpr = (rw * cs * 2 + 127) / 128 + 1;
+#pragma unroll
+  for (int k = 0; k < NPF; ++k) {
+    const int li = tid + 256 * k;
+    const int row = li / lpr, l = li - row * lpr;
+    const int iy = iy0 + row;
+    const void* p = zero;
+    if (row < rh && (unsigned)iy < (unsigned)H && l * 128 < row_bytes)
+      p = (const unsigned char*)(src + ((size_t)(b * H + iy) * W + ix_lo) * cs) + l * 128;
+    __builtin_amdgcn_global_load_lds(p, (lds_void_ptr_s)dummy, 4, 0, 0);
+  }
 }
 
 struct StreamArgs {
@@ -193,13 +221,14 @@ __global__ __launch_bounds__(256) void conv_stream_kernel(StreamArgs args) {
   }
   const int wswz = ((fr >> 2) & 1) << 1;  // filter row swizzle (rows fr + 16k)
 
+  unsigned char* pf_dummy = slots + 2 * K::SLOT + wave * 256;
   int it = 0;
   for (int t = first; t < band1; t += step, ++it) {
     const int slot = it & 1;
     // (A) the region of tile t has landed: younger than its DMA are only the
     // previous tile's S stores
     if (it == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K::S) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K::S + K::NPF) : "memory");
     __builtin_amdgcn_s_barrier();
     int b, oy0, ox0;
     tile_coords(t, b, oy0, ox0);
@@ -232,6 +261,12 @@ __global__ __launch_bounds__(256) void conv_stream_kernel(StreamArgs args) {
     }
     const bool has_next = t + step < band1;
     if (has_next) issue_region(t + step, slot ^ 1);
+    {
+      int pb = 0, py = 0, px = 0;
+      const bool pf = t + 2 * step < band1;
+      if (pf) tile_coords(t + 2 * step, pb, py, px);
+      prefetch_region<K::NPF>(src, sg.cs, pb, H, W, pf ? py - 1 : -1000, px - 1, K::RH, K::RW, tid, zero, pf_dummy);
+    }
 
     // ---- MFMAs: D[n][px] = sum_k W[n][k] * X[px][k] -------------------------
     f32x4_s acc[K::NT][K::GPW];
@@ -262,8 +297,9 @@ __global__ __launch_bounds__(256) void conv_stream_kernel(StreamArgs args) {
       }
     }
 
-    // (B) this tile's asm loads are done; the next region's DMA may fly on
-    if (has_next) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K::G) : "memory");
+    // (B) this tile's asm loads are done; the next region's DMA (and the L2
+    // prefetch behind it) may fly on
+    if (has_next) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K::G + K::NPF) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // pin every use of the asm-loaded registers below the wait (volatile asm
     // statements keep their order; plain arithmetic could float above it)
@@ -360,8 +396,11 @@ struct FamCfg {
   static constexpr int SLOT = HSLOT + XSLOT;
   static constexpr int NSL = 20;                                        // 32-deep k slices
   static constexpr int WBYTES = NSL * NB * 64;
-  static constexpr int LDS = WBYTES + 2 * SLOT;
+  static constexpr int LDS = WBYTES + 2 * SLOT + 1024;                  // + prefetch dummy rows
   static constexpr int S = GPW * NT;                                    // stores per wave per tile
+  static constexpr int HPF = kStreamPrefetch ? (HRH * ((HRW * 128 + 127) / 128 + 1) + 255) / 256 : 0;
+  static constexpr int XPF = kStreamPrefetch ? (XRH * ((XRW * 64 + 127) / 128 + 1) + 255) / 256 : 0;
+  static constexpr int NPF = HPF + XPF;
 };
 
 __global__ __launch_bounds__(256) void conv_stream_fam_kernel(StreamArgs args) {
@@ -452,6 +491,7 @@ __global__ __launch_bounds__(256) void conv_stream_fam_kernel(StreamArgs args) {
     for (int i = 0; i < 4; ++i) pool[nt][i] = 0.f;
   int pool_img = -1;
   bool flushed = false;
+  unsigned char* pf_dummy = slots + 2 * K::SLOT + wave * 256;
   // flush this lane's pooled sums of image pool_img (reduced over the 16 pixel lanes)
   auto flush = [&]() {
 #pragma unroll
@@ -472,13 +512,20 @@ __global__ __launch_bounds__(256) void conv_stream_fam_kernel(StreamArgs args) {
   for (int t = first; t < band1; t += step, ++it) {
     const int slot = it & 1;
     if (it == 0 || flushed) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K::S) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K::S + K::NPF) : "memory");
     __builtin_amdgcn_s_barrier();
     flushed = false;
     int b, oy0, ox0;
     tile_coords(t, b, oy0, ox0);
     const bool has_next = t + step < band1;
     if (has_next) issue_region(t + step, slot ^ 1);
+    {
+      int pb = 0, py = 0, px = 0;
+      const bool pf = t + 2 * step < band1;
+      if (pf) tile_coords(t + 2 * step, pb, py, px);
+      prefetch_region<K::HPF>(hsrc, sh.cs, pb, H, W, pf ? py - 2 : -1000, px - 2, K::HRH, K::HRW, tid, zero, pf_dummy);
+      prefetch_region<K::XPF>(xsrc, sx.cs, pb, H, W, pf ? py - 1 : -1000, px - 1, K::XRH, K::XRW, tid, zero, pf_dummy);
+    }
 
     f32x4_s acc[K::NT][K::GPW];
 #pragma unroll
@@ -539,7 +586,7 @@ __global__ __launch_bounds__(256) void conv_stream_fam_kernel(StreamArgs args) {
         }
       }
     }
-    if (has_next) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K::G) : "memory");
+    if (has_next) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K::G + K::NPF) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // epilogue: y = relu(acc + b) in fp16, pooled sums of the stored values
     if (op.pool && pool_img != b) {
@@ -565,8 +612,8 @@ __global__ __launch_bounds__(256) void conv_stream_fam_kernel(StreamArgs args) {
       }
     }
   }
-  if (op.pool && pool_img >= 0) flush();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (op.pool && pool_img >= 0) flush();
 }
 
 static int launch_stream_fam(const ConvOp& op, hipStream_t st) {
@@ -592,6 +639,308 @@ static int launch_stream_fam(const ConvOp& op, hipStream_t st) {
   int grid = std::min(cus * occ, cdiv(a.ntiles, 8) * 8);
   grid = std::max(8, grid / 8 * 8);
   hipLaunchKernelGGL(conv_stream_fam_kernel, dim3(grid), dim3(256), FamCfg::LDS, st, a);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Whole EnhancedFAM conv stack in one pass (fp16): h = relu([branch3_conv1;
+// branch4_conv1](x) + b) is computed for the tile's 2-pixel-halo region
+// straight into LDS (zero outside the image = the fusion convs' padding) and
+// consumed there by the fusion GEMM of conv_stream_fam_kernel — h never
+// touches HBM (models/model.py:35-44, :66-78).  Per 4 x 32 tile: x region
+// 10 x 38 px (3-pixel halo, zero fill; the max-pool masks out-of-image
+// neighbours itself), h region 8 x 36 px x 64 ch, filters of both convs
+// resident: 76 + 36 + 2 x 24 KiB = 160 KiB of LDS, one block per CU.
+// ---------------------------------------------------------------------------
+struct FamFusedCfg {
+  static constexpr int TH = 4, GPW = 2, NT = 2, NB = 32;
+  static constexpr int XRW = ST_TW + 6, XRH = TH + 6, XPX = XRW * XRH;  // 38 x 10
+  static constexpr int HRW = ST_TW + 4, HRH = TH + 4, HPX = HRW * HRH;  // 36 x 8
+  static constexpr int XNI = (XPX * 64 + 4095) / 4096;                  // 6
+  static constexpr int XSLOT = XNI * 4096;
+  static constexpr int HBYTES = HPX * 128;
+  static constexpr int W34 = 9 * 64 * 64;                              // [tap][n 64][64 B]
+  static constexpr int WF = 20 * NB * 64;                              // [slice][n 32][64 B]
+  static constexpr int LDS = W34 + WF + HBYTES + 2 * XSLOT;
+  static constexpr int HG = HPX / 16;                                  // 18 groups of 16 h pixels
+  static constexpr int HGW = (HG + 3) / 4;                             // per wave (5, last ones partial)
+  static constexpr int G = XNI;
+  static constexpr int S = GPW * NT;
+};
+
+struct FamFusedArgs {
+  const half_t* x; int x_cs;
+  const half_t* w34; int w34_kpad; const float* b34;   // [64][Kpad] (k = tap*32 + c), bias [64]
+  const half_t* wf; int wf_kpad; const float* bf;      // [32][640]
+  half_t* out; int out_cs;
+  float* pool;
+  int B, H, W;
+  int tiles_x, tiles_y, ntiles;
+};
+
+__global__ __launch_bounds__(256) void conv_fam_fused_kernel(FamFusedArgs a) {
+  using K = FamFusedCfg;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* W34l = smem;
+  unsigned char* WFl = smem + K::W34;
+  unsigned char* hreg = WFl + K::WF;
+  unsigned char* xslots = hreg + K::HBYTES;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int H = a.H, W = a.W;
+  const int xcd = blockIdx.x & 7, idx = blockIdx.x >> 3, per_xcd = gridDim.x >> 3;
+  const int band0 = (int)((long long)a.ntiles * xcd / 8), band1 = (int)((long long)a.ntiles * (xcd + 1) / 8);
+  auto tile_coords = [&](int t, int& b, int& oy0, int& ox0) {
+    const int tx = t % a.tiles_x, r = t / a.tiles_x;
+    b = r / a.tiles_y;
+    oy0 = (r % a.tiles_y) * K::TH;
+    ox0 = tx * ST_TW;
+  };
+  // resident filters (64-B rows, chunk ^ ((n >> 2) & 1) * 2)
+  for (int i = tid; i < 9 * 64 * 4; i += 256) {
+    const int pc = i & 3, n = (i >> 2) & 63, tap = i >> 8;
+    const int c = pc ^ (((n >> 2) & 1) << 1);
+    *(uint4*)(W34l + (size_t)i * 16) = *(const uint4*)(a.w34 + (size_t)n * a.w34_kpad + tap * 32 + c * 8);
+  }
+  for (int i = tid; i < 20 * K::NB * 4; i += 256) {
+    const int pc = i & 3, n = (i >> 2) % K::NB, sl = (i >> 2) / K::NB;
+    const int c = pc ^ (((n >> 2) & 1) << 1);
+    *(uint4*)(WFl + (size_t)i * 16) = *(const uint4*)(a.wf + (size_t)n * a.wf_kpad + sl * 32 + c * 8);
+  }
+  int xq[K::XNI];
+#pragma unroll
+  for (int j = 0; j < K::XNI; ++j) {
+    const int u = (wave * K::XNI + j) * 64 + lane, q = u >> 2, pc = u & 3;
+    xq[j] = q < K::XPX ? ((q / K::XRW) << 16) | ((q % K::XRW) << 8) | (pc ^ region_swz(q, 4)) : -1;
+  }
+  const half_t* zero = (const half_t*)g_stream_zero;
+  auto issue_region = [&](int t, int slot) {
+    int b, oy0, ox0;
+    tile_coords(t, b, oy0, ox0);
+    unsigned char* xd = xslots + slot * K::XSLOT + wave * K::XNI * 1024;
+#pragma unroll
+    for (int j = 0; j < K::XNI; ++j) {
+      const half_t* p = zero;
+      if (xq[j] >= 0) {
+        const int iy = oy0 - 3 + (xq[j] >> 16), ix = ox0 - 3 + ((xq[j] >> 8) & 255);
+        if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+          p = a.x + (size_t)((b * H + iy) * W + ix) * a.x_cs + (xq[j] & 255) * 8;
+      }
+      __builtin_amdgcn_global_load_lds(p, (lds_void_ptr_s)(xd + j * 1024), 16, 0, 0);
+    }
+  };
+  const int first = band0 + idx, step = per_xcd;
+  __syncthreads();
+  if (first < band1) issue_region(first, 0);
+
+  const int wswz = ((fr >> 2) & 1) << 1;
+  float b34v[4][4], bfv[K::NT][4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b34v[nt][i] = a.b34[nt * 16 + fg * 4 + i];
+#pragma unroll
+  for (int nt = 0; nt < K::NT; ++nt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bfv[nt][i] = a.bf[nt * 16 + fg * 4 + i];
+  float pool[K::NT][4];
+#pragma unroll
+  for (int nt = 0; nt < K::NT; ++nt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pool[nt][i] = 0.f;
+  int pool_img = -1;
+  bool flushed = false;
+  auto flush = [&]() {
+#pragma unroll
+    for (int nt = 0; nt < K::NT; ++nt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float v = pool[nt][i];
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        v += __shfl_xor(v, 4);
+        v += __shfl_xor(v, 8);
+        if (fr == 0) atomicAdd(a.pool + (size_t)pool_img * K::NB + nt * 16 + fg * 4 + i, v);
+        pool[nt][i] = 0.f;
+      }
+  };
+
+  int it = 0;
+  for (int t = first; t < band1; t += step, ++it) {
+    const int slot = it & 1;
+    if (it == 0 || flushed) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K::S) : "memory");
+    __builtin_amdgcn_s_barrier();
+    flushed = false;
+    int b, oy0, ox0;
+    tile_coords(t, b, oy0, ox0);
+    const bool has_next = t + step < band1;
+    if (has_next) issue_region(t + step, slot ^ 1);
+    const unsigned char* xreg = xslots + slot * K::XSLOT;
+
+    // ---- phase 1: h over the 8 x 36 region, into LDS -------------------------
+    {
+      f32x4_s hacc[4][K::HGW];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int g = 0; g < K::HGW; ++g) hacc[nt][g] = f32x4_s{0.f, 0.f, 0.f, 0.f};
+      int hb[K::HGW];  // x-region pixel of this lane's h pixel (tap 0,0)
+      // 18 groups over 4 waves: group min(wave + 4g, 17) -> waves 2, 3 redo
+      // group 17 as their 5th (same values written twice; no branch inside
+      // the MFMA loop)
+#pragma unroll
+      for (int g = 0; g < K::HGW; ++g) {
+        const int q = min(wave + 4 * g, K::HG - 1) * 16 + fr;
+        hb[g] = (q / K::HRW) * K::XRW + (q % K::HRW);
+      }
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int r = tap / 3, s = tap % 3;
+        f16x8_s wf[4];
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+          wf[nt] = *(const f16x8_s*)(W34l + ((size_t)(tap * 64 + nt * 16 + fr) * 64) + ((fg ^ wswz) * 16));
+#pragma unroll
+        for (int g = 0; g < K::HGW; ++g) {
+          const int q = hb[g] + r * K::XRW + s;
+          const f16x8_s xf = *(const f16x8_s*)(xreg + q * 64 + ((fg ^ region_swz(q, 4)) * 16));
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt)
+            hacc[nt][g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[nt], xf, hacc[nt][g], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < K::HGW; ++g) {
+        const int q = min(wave + 4 * g, K::HG - 1) * 16 + fr;
+        const int iy = oy0 - 2 + q / K::HRW, ix = ox0 - 2 + q % K::HRW;
+        const bool in = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          f16x4_s o;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) o[i] = in ? (half_t)fmaxf(hacc[nt][g][i] + b34v[nt][i], 0.f) : (half_t)0.f;
+          const int c = nt * 2 + (fg >> 1);  // 16-byte chunk of channels nt*16 + 4fg
+          *(f16x4_s*)(hreg + q * 128 + ((c ^ (q & 7)) * 16) + (fg & 1) * 8) = o;
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+
+    // ---- phase 2: fusion GEMM (as conv_stream_fam_kernel) --------------------
+    f32x4_s acc[K::NT][K::GPW];
+#pragma unroll
+    for (int nt = 0; nt < K::NT; ++nt)
+#pragma unroll
+      for (int g = 0; g < K::GPW; ++g) acc[nt][g] = f32x4_s{0.f, 0.f, 0.f, 0.f};
+    auto wfrag = [&](int sl, f16x8_s (&wf)[K::NT]) {
+#pragma unroll
+      for (int nt = 0; nt < K::NT; ++nt)
+        wf[nt] = *(const f16x8_s*)(WFl + ((size_t)(sl * K::NB + nt * 16 + fr) * 64) + ((fg ^ wswz) * 16));
+    };
+#pragma unroll
+    for (int seg = 0; seg < 2; ++seg) {
+      const int d = seg + 1;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int r = tap / 3, s = tap % 3;
+        f16x8_s wf[K::NT];
+        wfrag(seg * 9 + tap, wf);
+#pragma unroll
+        for (int g = 0; g < K::GPW; ++g) {
+          const int q = (wave + 2 + (r - 1) * d) * K::HRW + g * 16 + 2 + (s - 1) * d + fr;
+          const int c = (seg * 4 + fg) ^ (q & 7);
+          const f16x8_s xf = *(const f16x8_s*)(hreg + q * 128 + c * 16);
+#pragma unroll
+          for (int nt = 0; nt < K::NT; ++nt)
+            acc[nt][g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[nt], xf, acc[nt][g], 0, 0, 0);
+        }
+      }
+    }
+    {
+      f16x8_s w1[K::NT], w2[K::NT];
+      wfrag(18, w1);
+      wfrag(19, w2);
+      const half_t ninf = (half_t)(-INFINITY);
+#pragma unroll
+      for (int g = 0; g < K::GPW; ++g) {
+        const int oy = oy0 + wave, ox = ox0 + g * 16 + fr;
+        f16x8_s ctr = {}, mx;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) mx[e] = ninf;
+#pragma unroll
+        for (int dr = 0; dr < 3; ++dr)
+#pragma unroll
+          for (int ds = 0; ds < 3; ++ds) {
+            const int q = (wave + 2 + dr) * K::XRW + g * 16 + 2 + ds + fr;
+            const f16x8_s v = *(const f16x8_s*)(xreg + q * 64 + ((fg ^ region_swz(q, 4)) * 16));
+            const bool in = (unsigned)(oy + dr - 1) < (unsigned)H && (unsigned)(ox + ds - 1) < (unsigned)W;
+            if (in) mx = __builtin_elementwise_max(mx, v);
+            if (dr == 1 && ds == 1) ctr = v;
+          }
+#pragma unroll
+        for (int nt = 0; nt < K::NT; ++nt) {
+          acc[nt][g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[nt], ctr, acc[nt][g], 0, 0, 0);
+          acc[nt][g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w2[nt], mx, acc[nt][g], 0, 0, 0);
+        }
+      }
+    }
+    if (has_next) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K::G) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (a.pool && pool_img != b) {
+      if (pool_img >= 0) { flush(); flushed = true; }
+      pool_img = b;
+    }
+#pragma unroll
+    for (int g = 0; g < K::GPW; ++g) {
+      const int y = oy0 + wave, x = ox0 + g * 16 + fr;
+      const bool ok = y < H && x < W;
+      const size_t opix = ok ? (size_t)(b * H + y) * W + x : 0;
+#pragma unroll
+      for (int nt = 0; nt < K::NT; ++nt) {
+        f16x4_s o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          o[i] = (half_t)fmaxf(acc[nt][g][i] + bfv[nt][i], 0.f);
+          if (ok) pool[nt][i] += (float)o[i];
+        }
+        uint2* dst = ok ? (uint2*)(a.out + opix * a.out_cs + nt * 16 + fg * 4) : g_stream_sink + tid;
+        *dst = __builtin_bit_cast(uint2, o);
+      }
+    }
+  }
+  if (a.pool && pool_img >= 0) flush();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+int launch_fam_fused(const void* x, int x_cs, const void* w34, int w34_kpad, const float* b34, const void* wf,
+                     int wf_kpad, const float* bf, void* out, int out_cs, float* pool, int B, int H, int W,
+                     hipStream_t st) {
+  if (x_cs % 8 || out_cs % 4 || wf_kpad < 640 || w34_kpad < 288 || (uintptr_t)x % 16) return kErrShape;
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)conv_fam_fused_kernel,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, FamFusedCfg::LDS);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  int cus = 0, dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
+  FamFusedArgs a;
+  a.x = (const half_t*)x; a.x_cs = x_cs;
+  a.w34 = (const half_t*)w34; a.w34_kpad = w34_kpad; a.b34 = b34;
+  a.wf = (const half_t*)wf; a.wf_kpad = wf_kpad; a.bf = bf;
+  a.out = (half_t*)out; a.out_cs = out_cs; a.pool = pool;
+  a.B = B; a.H = H; a.W = W;
+  a.tiles_x = cdiv(W, ST_TW);
+  a.tiles_y = cdiv(H, FamFusedCfg::TH);
+  a.ntiles = B * a.tiles_x * a.tiles_y;
+  int grid = std::min(cus, cdiv(a.ntiles, 8) * 8);
+  grid = std::max(8, grid / 8 * 8);
+  hipLaunchKernelGGL(conv_fam_fused_kernel, dim3(grid), dim3(256), FamFusedCfg::LDS, st, a);
   return (int)hipGetLastError();
 }
 
