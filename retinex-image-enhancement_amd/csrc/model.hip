@@ -31,9 +31,6 @@
 namespace upr {
 
 int launch_prep(const void* x, void* x2p, void* x3p, int B, int H, int W, int dtype, hipStream_t st);
-int launch_fam_fused(const void* x, int x_cs, const void* w34, int w34_kpad, const float* b34, const void* wf,
-                     int wf_kpad, const float* bf, void* out, int out_cs, float* pool, int B, int H, int W,
-                     hipStream_t st);
 int launch_preact_f16(const void* x, const float* sc, const float* sh, void* o, size_t npix, int C, hipStream_t st);
 int launch_conv3(const void* x, const float* w, const float* bias, void* out0, void* out1, int B, int h, int wd,
                  int dtype, hipStream_t st, void* out2 = nullptr, const float* ps = nullptr,
@@ -265,13 +262,13 @@ static std::vector<double> conv3_kmajor(const std::vector<double>& w) {
   return t;
 }
 
-enum OpKind { OP_GEMM, OP_CONV3, OP_PREP, OP_FAM_CA, OP_FAM_MIX, OP_FAM_SA, OP_ASPP_G, OP_TAIL, OP_PREACT, OP_FAM_FUSED };
+enum OpKind { OP_GEMM, OP_CONV3, OP_PREP, OP_FAM_CA, OP_FAM_MIX, OP_FAM_SA, OP_ASPP_G, OP_TAIL, OP_PREACT };
 
 struct Op {
   OpKind kind;
   std::string name;
   // GEMM
-  int layer = -1, layer2 = -1;  // OP_FAM_FUSED: branch34 layer + fusion layer
+  int layer = -1;
   int level = 0;  // resolution level of the output pixels: H >> level (ConvT: input level)
   int out = -1, out_cs = 0, out_coff = 0;
   int res1 = -1, res1_cs = 0, res2 = -1, res2_cs = 0;
@@ -614,12 +611,7 @@ struct Builder {
     sh[0].w.insert(sh[0].w.end(), w4a->v.begin(), w4a->v.end());
     std::vector<double> hb = b3a->v;
     hb.insert(hb.end(), b4a->v.begin(), b4a->v.end());
-    const int l34 = add_layer(2 * C, sh, hb);
-    // UPR_FAM_FUSED=1 (fp16): h computed per tile into LDS and consumed there
-    // (conv_fam_fused_kernel).  Off by default: at one wave per SIMD its 2.25x
-    // recomputed h MFMAs cost more than h's HBM round trip (1.83 vs 1.55 ms).
-    const bool fused = dt == kF16 && getenv("UPR_FAM_FUSED") && strcmp(getenv("UPR_FAM_FUSED"), "1") == 0;
-    if (!fused) gemm(p + ".branch34_conv1", l34, lshift, hbuf, 2 * C, 1);
+    gemm(p + ".branch34_conv1", add_layer(2 * C, sh, hb), lshift, hbuf, 2 * C, 1);
     // (2) y = relu(fusion(cat[b1,b2,b3,b4])) as one GEMM over the virtual concat
     const std::vector<double>& F = wf->v;
     std::vector<double> F1 = cols(F, C, 4 * C, 0, C), F2 = cols(F, C, 4 * C, C, C);
@@ -638,16 +630,7 @@ struct Builder {
       for (int mm_ = 0; mm_ < C; ++mm_)
         fb[o] += F1[o * C + mm_] * bb1->v[mm_] + F2[o * C + mm_] * bb2->v[mm_] + F3[o * C + mm_] * b3b->v[mm_] +
                  F4[o * C + mm_] * b4b->v[mm_];
-    const int lf = add_layer(C, sf, fb);
-    if (!fused) {
-      gemm(p + ".fusion", lf, lshift, ybuf, C, 1, -1, 0, -1, 0, kStoreNHWC, 0, k);
-    } else {
-      // fp16: both convs in one streaming kernel, h stays in LDS (conv_stream.hip)
-      Op o;
-      o.kind = OP_FAM_FUSED; o.name = p + ".convs_fused"; o.layer = l34; o.layer2 = lf; o.in = in; o.out = ybuf;
-      o.level = lshift; o.pool_slot = k;
-      m->ops.push_back(o);
-    }
+    gemm(p + ".fusion", add_layer(C, sf, fb), lshift, ybuf, C, 1, -1, 0, -1, 0, kStoreNHWC, 0, k);
     // (3) channel attention, (4) mix + projection, (5) spatial attention
     Op oc;
     oc.kind = OP_FAM_CA; oc.name = p + ".channel_attention"; oc.fam = k; oc.lvl_shift = lshift;
@@ -876,20 +859,6 @@ static int run_forward(UprModel* m, const void* x, int B, int H, int W, void* en
         }
         break;
       }
-      case OP_FAM_FUSED: {
-        int h, w;
-        lvl_dims(o.level, h, w);
-        const GemmLayer& Lh = m->layers[o.layer];
-        const GemmLayer& Lf = m->layers[o.layer2];
-        rc = launch_fam_fused(buf(o.in), 32, blob + Lh.w, Lh.Kpad, fptr(Lh.bias), blob + Lf.w, Lf.Kpad,
-                              fptr(Lf.bias), buf(o.out), 32, pool + (size_t)o.pool_slot * B * 256, B, h, w, st);
-        if (m->prof) {
-          const double px = (double)B * h * w;
-          m->cur_flops[oi] = 2.0 * px * (64.0 * 288.0 + 32.0 * 640.0);
-          m->cur_bytes[oi] = px * (32.0 + 32.0) * elt + (64.0 * Lh.Kpad + 32.0 * Lf.Kpad) * elt;
-        }
-        break;
-      }
       case OP_PREACT: {
         int h, w;
         lvl_dims(o.level, h, w);
@@ -1042,7 +1011,7 @@ int upr_model_profile_read(UprModel* model, UprOpStat* out, int max_ops, int* n_
       UprOpStat& s = out[i];
       memset(&s, 0, sizeof(s));
       strncpy(s.name, model->ops[i].name.c_str(), sizeof(s.name) - 1);
-      s.kind = (model->ops[i].kind == OP_GEMM || model->ops[i].kind == OP_FAM_FUSED) ? UPR_OP_CONV_IGEMM : UPR_OP_OTHER;
+      s.kind = model->ops[i].kind == OP_GEMM ? UPR_OP_CONV_IGEMM : UPR_OP_OTHER;
       if (i < model->st_ms.size()) {
         s.calls = model->st_calls[i];
         s.ms = model->st_ms[i];
