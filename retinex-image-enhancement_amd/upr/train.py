@@ -441,7 +441,9 @@ class PreActResBlockT:
 
 
 class ASPPT:
-    """ASPPModule (model.py:181-251); Dropout(0.1) mask from a counter hash."""
+    """ASPPModule (model.py:181-251); Dropout(0.1) mask from a counter hash
+    whose seed is drawn from torch's default generator (so, as with the
+    reference's nn.Dropout, torch.manual_seed makes the masks reproducible)."""
 
     def __init__(self, m, dropout_mask_fn=None):
         self.c1, self.b1 = Conv(m.conv1x1[0]), BN(m.conv1x1[1])
@@ -474,9 +476,8 @@ class ASPPT:
         self.a = self.fb.fwd(self.fc.fwd(cat), relu=True)
         out = Act.new(x.B, x.H, x.W, C, dev, fresh=False)
         self.mask = torch.empty((out.t.numel(),), dtype=torch.uint8, device=dev)
-        self.seed += 1
-        pointwise(self.a.t, None, out.t, out.t.numel(), 2, mask_out=self.mask, p=self.p,
-                  seed=(id(self) & 0xffffffff) * 1000003 + self.seed)
+        self.seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        pointwise(self.a.t, None, out.t, out.t.numel(), 2, mask_out=self.mask, p=self.p, seed=self.seed)
         return out
 
     def bwd(self, g, gx):

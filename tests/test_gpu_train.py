@@ -212,8 +212,9 @@ def test_train_grads_variants_vs_oracle(pre, aspp):
     gradients noisy — the fp32 CPU oracle itself deviates from fp64 by up to
     ~2e-2 of a tensor's max on the ASPP variants (the global-pool BN normalises
     over B values) — so per tensor the device gradient's relative L2 error vs
-    fp64 must be within max(4 x the fp32 oracle's, 1e-3), and its max|d|
-    within max(8 x the fp32 oracle's, 5e-3 x max|g64|), the fp32 oracle's
+    fp64 must be within max(4 x the fp32 oracle's, 2 x the median over all
+    tensors of the fp32 oracle's, 1e-3), and its max|d| within
+    max(8 x the fp32 oracle's, that median floor x max|g64|, 5e-3 x max|g64|), the fp32 oracle's
     deviation being the larger of two runs with different CPU kernels (NCHW
     and channels-last inputs: two summation orders): a different summation
     order lands anywhere in that noise band, a wrong kernel lands far outside.  B = 4:
@@ -262,6 +263,7 @@ def test_train_grads_variants_vs_oracle(pre, aspp):
     np.testing.assert_allclose(d["total"], d64["total"], rtol=1e-4)
     dev_params = dict(model.named_parameters())
     gmax = max(v.abs().max().item() for v in g64.values())
+    rows = []
     for n in names:
         ref = g64[n]
         if ref.abs().max().item() < 1e-9 * gmax:
@@ -272,8 +274,14 @@ def test_train_grads_variants_vs_oracle(pre, aspp):
         rn = ref.norm().item()
         dev_l2 = (dev - ref).norm().item() / rn
         cpu_l2 = max((g32[n] - ref).norm().item(), (g32b[n] - ref).norm().item()) / rn
+        rows.append((n, ref, dev_err, cpu_err, dev_l2, cpu_l2))
+    # the batch-statistics amplification perturbs the whole gradient by a
+    # similar relative amount, so a tensor whose own fp32 CPU deviation landed
+    # low is also judged against the network-wide fp32 noise level (median)
+    floor_l2 = 2.0 * float(np.median([r[5] for r in rows]))
+    for n, ref, dev_err, cpu_err, dev_l2, cpu_l2 in rows:
         print(f"{n}: max|d| dev {dev_err:.3e} cpu32 {cpu_err:.3e}; rel-L2 dev {dev_l2:.3e} cpu32 {cpu_l2:.3e}")
-        tol_l2 = max(4.0 * cpu_l2, 1e-3)
+        tol_l2 = max(4.0 * cpu_l2, floor_l2, 1e-3)
         assert dev_l2 <= tol_l2, f"grad {n}: device rel-L2 {dev_l2:.3e} vs fp64 > {tol_l2:.3e} (fp32 CPU {cpu_l2:.3e})"
-        tol = max(8.0 * cpu_err, 5e-3 * ref.abs().max().item()) + 1e-9
+        tol = max(8.0 * cpu_err, floor_l2 * ref.abs().max().item(), 5e-3 * ref.abs().max().item()) + 1e-9
         assert dev_err <= tol, f"grad {n}: device |d| {dev_err:.3e} vs fp64 > {tol:.3e} (fp32 CPU |d| {cpu_err:.3e})"
