@@ -74,6 +74,20 @@ def cpu_baseline(sd, pre, aspp, size, budget_s):
             "sample": f"{n} x 1x3x{size}x{size} fp32 forwards of oracle/net.py (torch-CPU), {el:.1f}s"}
 
 
+def parity_vs_cpu(sd, pre, aspp, x, outs, precision):
+    """Per-pixel max |d| of image 0 of the last timed step's outputs against the
+    CPU oracle (oracle/net.py, fp32) on the same input (the fp16 run's input is
+    the fp16-rounded image, widened to fp32 for the oracle)."""
+    from oracle import net as onet  # checker only
+    with torch.no_grad():
+        ref = onet.forward(sd, x[:1].float().cpu(), pre, aspp)
+    names = ("enhanced", "reflectance", "illumination")
+    d = {n: (o[:1].float().cpu() - r).abs().max().item() for n, o, r in zip(names, outs, ref)}
+    tol = 1e-3 if precision == "fp32" else 3e-2
+    return {"max_abs_diff": d, "tol": tol, "pass": all(v <= tol for v in d.values()),
+            "sample": "image 0 of the last timed batch vs oracle/net.py fp32 on host cores"}
+
+
 CONV_KERNELS = ("conv_halo_kernel", "conv_igemm_kernel", "conv_wide_kernel", "conv_stream_kernel",
                 "conv_stream_fam_kernel")
 
@@ -260,6 +274,8 @@ def main():
         with torch.no_grad():
             return model(x)
 
+    last = [None]
+
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -275,7 +291,7 @@ def main():
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        last[0] = step()
     barrier()
     elapsed = time.perf_counter() - t0
     stats = handle.profile_read() if not args.no_profile else []
@@ -344,6 +360,7 @@ def main():
                       f"{tf:8.1f} TF/s {gbs:8.1f} GB/s", file=sys.stderr)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(sd_cpu, pre, aspp, S, args.cpu_seconds)
+        out["parity"] = parity_vs_cpu(sd_cpu, pre, aspp, x, last[0], args.precision)
     if rank == 0:
         print(json.dumps(out))
     if world > 1:

@@ -16,7 +16,19 @@
 //   pixel shifted by the tap; out-of-image taps and rows past M read a
 //   128-byte zero line), B rows are the packed [N][Kpad] weights.
 // * Two LDS stages, one barrier per K step: the DMA of step s+1 is issued right
-//   after the barrier and flies while the MFMAs of step s run.
+//   after the barrier and flies while the MFMAs of step s run.  The fragments
+//   of the second 32-deep half of step s are read before the barrier and its
+//   MFMAs run after it (half-step software pipeline), so the MFMA pipe stays
+//   busy across the barrier and the next step's first fragment reads; the
+//   fragment reads of one half are interleaved with the MFMAs of the other
+//   (sched_group_barrier), which also keeps the wave at 254 VGPRs, no spills.
+// * The (segment, tap, channel) cursor keeps the current segment's geometry in
+//   registers (no kernarg loads in the K loop).
+// * Measured on bneck (bs 32, 64x64x256 -> 256, 3x3): 0.189 ms = 820 TF/s; with
+//   both DMAs removed (timing ablation) 0.119 ms = 1300 TF/s, i.e. ~1/3 of the
+//   time is operand traffic; a 4-stage 32-deep ring (three steps of DMA in
+//   flight across each barrier) measured 3-8% SLOWER (twice the per-step
+//   overhead for no latency it could still hide).
 // * LDS image: 128-byte rows (64 fp16), lane-linear as LDS-DMA requires; the
 //   16-byte chunk index is XOR-swizzled by (row >> 1) & 7 on the SOURCE
 //   address, and the fragment reads apply the same XOR -> the ds_read_b128
@@ -64,120 +76,68 @@ __device__ __forceinline__ void glds16(const void* g, unsigned char* lds) {
   __builtin_amdgcn_global_load_lds(g, (lds_void_ptr)lds, 16, 0, 0);
 }
 
-template <int BN>
-__global__ __launch_bounds__(512) void conv_wide_kernel(ConvOp op) {
-  using C = WideCfg<BN>;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wm = wave % C::WAVES_M;
-  const int wn = wave / C::WAVES_M;
 
-  const int M = op.B * op.Ho * op.Wo;
-  const int HW = op.Ho * op.Wo;
-  const int mtiles = (M + WBM - 1) / WBM;
-  const int ntiles = op.N / BN;
-  const int L = wide_xcd_remap(blockIdx.x, mtiles * ntiles);
-  const int ntile = L % ntiles;  // the n-tiles of one pixel tile run back to back (A reuse in L2)
-  const int mtile = L / ntiles;
-  const int m0 = mtile * WBM;
-  const int n0 = ntile * BN;
+// (segment, tap, channel) cursor of the K loop with the current segment's
+// geometry held in registers: the per-step DMA issue needs no kernarg loads
+// (a dynamically indexed op.seg[] read is a scalar load + lgkmcnt wait in
+// every step), only a reload when the cursor crosses into the next segment.
+template <int NR, int BK>
+struct SegCursor {
+  const ConvOp& op;
+  const int (&rb)[NR];  // per lane row: image (-1 = past M), output row, output column
+  const int (&ry)[NR];
+  const int (&rx)[NR];
+  const int chunk;
+  int seg, ty, tx, c0;
+  const half_t* src;
+  int Hin, Win, cs, stride, kh, kw, dil, pad, C, kbase;
 
-  // ---- this lane's 4 A rows (output pixels) and DMA chunk swizzles ---------
-  const int q8 = lane >> 3;       // row within an 8-row DMA group
-  const int qc = lane & 7;        // LDS chunk this lane fills
-  int rb[4], ry[4], rx[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = m0 + wave * 32 + i * 8 + q8;
-    if (m < M) {
-      const int b = m / HW, r = m - b * HW;
-      rb[i] = b;
-      ry[i] = r / op.Wo;
-      rx[i] = r - ry[i] * op.Wo;
-    } else {
-      rb[i] = -1; ry[i] = 0; rx[i] = 0;
-    }
+  __device__ SegCursor(const ConvOp& o, const int (&b)[NR], const int (&y)[NR], const int (&x)[NR], int ch)
+      : op(o), rb(b), ry(y), rx(x), chunk(ch), seg(0), ty(0), tx(0), c0(0) {
+    load();
   }
-  // logical chunk stored at LDS chunk qc of row R is qc ^ ((R >> 1) & 7); for
-  // R = wave*32 + i*8 + q8 (A) or wave*BN/8 + j*8 + q8 (B) that is (4i + lane>>4) & 7
-  const int sw_lane = lane >> 4;
-
-  int total_steps = 0;
-  for (int s = 0; s < op.nseg; ++s) total_steps += op.seg[s].kh * op.seg[s].kw * (op.seg[s].C / WBK);
-
-  int cur_seg = 0, cur_tap = 0, cur_c0 = 0;
-  const half_t* Wt = (const half_t*)op.W;
-  const half_t* zero = (const half_t*)g_wide_zero;
-
-  auto issue = [&](int stage) {
-    const ConvSeg& sg = op.seg[cur_seg];
-    const int r = cur_tap / sg.kw, s = cur_tap - r * sg.kw;
-    const int dy = r * sg.dil - sg.pad, dx = s * sg.dil - sg.pad;
-    const half_t* src = (const half_t*)sg.src + sg.coff + cur_c0;
-    unsigned char* As = smem + stage * C::STAGE;
-    unsigned char* Bs = As + C::A_BYTES;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int iy = ry[i] * sg.stride + dy;
-      const int ix = rx[i] * sg.stride + dx;
-      const int ch = qc ^ ((4 * i + sw_lane) & 7);
-      const half_t* p = zero;
-      if (rb[i] >= 0 && (unsigned)iy < (unsigned)sg.Hin && (unsigned)ix < (unsigned)sg.Win)
-        p = src + (size_t)((rb[i] * sg.Hin + iy) * sg.Win + ix) * sg.cs + ch * 8;
-      glds16(p, As + (wave * 32 + i * 8) * 128);
-    }
-    const int kb = sg.kbase + cur_tap * sg.C + cur_c0;
-#pragma unroll
-    for (int j = 0; j < C::BJ; ++j) {
-      const int n = wave * (BN / 8) + j * 8 + q8;
-      const int ch = qc ^ ((4 * j + sw_lane) & 7);
-      glds16(Wt + (size_t)(n0 + n) * op.Kpad + kb + ch * 8, Bs + (wave * (BN / 8) + j * 8) * 128);
-    }
-    // advance the (segment, tap, channel) cursor
-    cur_c0 += WBK;
-    if (cur_c0 >= sg.C) {
-      cur_c0 = 0;
-      if (++cur_tap >= sg.kh * sg.kw) { cur_tap = 0; ++cur_seg; }
-    }
-  };
-
-  f32x4_w acc[C::WM][C::WN];
-#pragma unroll
-  for (int a = 0; a < C::WM; ++a)
-#pragma unroll
-    for (int b = 0; b < C::WN; ++b) acc[a][b] = f32x4_w{0.f, 0.f, 0.f, 0.f};
-
-  const int fr = lane & 15;
-  const int fg = lane >> 4;
-  const int rsw = (fr >> 1) & 7;  // swizzle of every fragment row this lane reads
-
-  if (total_steps > 0) issue(0);
-  for (int step = 0; step < total_steps; ++step) {
-    // stage step&1 has landed (own DMA retired, then everyone's via the
-    // barrier) and every wave is done reading the other stage (step-1)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (step + 1 < total_steps) issue((step + 1) & 1);
-    const half_t* As = (const half_t*)(smem + (step & 1) * C::STAGE);
-    const half_t* Bs = As + C::A_BYTES / 2;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int pc = ((kk * 4 + fg) ^ rsw) * 8;
-      f16x8_w bf[C::WN];
-#pragma unroll
-      for (int b = 0; b < C::WN; ++b) bf[b] = *(const f16x8_w*)(Bs + (wn * C::WN * 16 + b * 16 + fr) * 64 + pc);
-#pragma unroll
-      for (int a = 0; a < C::WM; ++a) {
-        const f16x8_w af = *(const f16x8_w*)(As + (wm * C::WM * 16 + a * 16 + fr) * 64 + pc);
-#pragma unroll
-        for (int b = 0; b < C::WN; ++b)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf[b], acc[a][b], 0, 0, 0);
+  __device__ __forceinline__ void load() {
+    const ConvSeg& sg = op.seg[seg];
+    src = (const half_t*)sg.src + sg.coff + chunk * 8;
+    Hin = sg.Hin; Win = sg.Win; cs = sg.cs; stride = sg.stride; kh = sg.kh; kw = sg.kw;
+    dil = sg.dil; pad = sg.pad; C = sg.C; kbase = sg.kbase;
+  }
+  // source of row i at the current (tap, c0); `zero` when padded / past M
+  __device__ __forceinline__ const half_t* a_src(int i, const half_t* zero) const {
+    const int iy = ry[i] * stride + ty * dil - pad;
+    const int ix = rx[i] * stride + tx * dil - pad;
+    if (rb[i] >= 0 && (unsigned)iy < (unsigned)Hin && (unsigned)ix < (unsigned)Win)
+      return src + c0 + (size_t)((rb[i] * Hin + iy) * Win + ix) * cs;
+    return zero;
+  }
+  __device__ __forceinline__ int kb() const { return kbase + (ty * kw + tx) * C + c0; }
+  __device__ __forceinline__ void advance() {
+    c0 += BK;
+    if (c0 >= C) {
+      c0 = 0;
+      if (++tx >= kw) {
+        tx = 0;
+        if (++ty >= kh) {
+          ty = 0;
+          if (++seg < op.nseg) load();
+        }
       }
     }
   }
+};
 
+// Epilogue shared by the wide kernels: 256 x BN accumulator tile -> LDS ->
+// scale / bias / per-image bias / residuals / ReLU -> 16-byte fp16 stores.
+template <int BN, int WM, int WN, int WAVES_M>
+__device__ __forceinline__ void wide_epilogue(const ConvOp& op, f32x4_w (&acc)[WM][WN], unsigned char* smem, int m0,
+                                              int n0, int M, int HW) {
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave % WAVES_M;
+  const int wn = wave / WAVES_M;
+  const int fr = lane & 15;
+  const int fg = lane >> 4;
   // ---- epilogue through LDS ---------------------------------------------------
   // Four passes of 64 tile rows: the waves owning those rows park their raw
   // fp32 accumulators in LDS ([64][BN + 4] floats: conflict-free 4-byte
@@ -190,7 +150,7 @@ __global__ __launch_bounds__(512) void conv_wide_kernel(ConvOp op) {
   constexpr int CPR = BN / 8;             // 8-channel chunks per row
   constexpr int RPI = 512 / CPR;          // rows per iteration
   constexpr int APP = 4;                  // 16-row accumulator tiles per pass
-  constexpr int PPW = C::WM / APP;        // passes per wave-row group
+  constexpr int PPW = WM / APP;        // passes per wave-row group
   float* Es = (float*)smem;
   const int col8 = tid % CPR;
   const int nch = n0 + col8 * 8;
@@ -210,10 +170,10 @@ __global__ __launch_bounds__(512) void conv_wide_kernel(ConvOp op) {
 #pragma unroll
       for (int a = 0; a < APP; ++a)
 #pragma unroll
-        for (int b = 0; b < C::WN; ++b)
+        for (int b = 0; b < WN; ++b)
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            Es[(a * 16 + fg * 4 + i) * EST + wn * C::WN * 16 + b * 16 + fr] = acc[(p % PPW) * APP + a][b][i];
+            Es[(a * 16 + fg * 4 + i) * EST + wn * WN * 16 + b * 16 + fr] = acc[(p % PPW) * APP + a][b][i];
     }
     __syncthreads();
 #pragma unroll
@@ -289,20 +249,209 @@ __global__ __launch_bounds__(512) void conv_wide_kernel(ConvOp op) {
   }
 }
 
-template <int BN>
+template <int BN, bool PIPE>
+__global__ __launch_bounds__(512) void conv_wide_kernel(ConvOp op) {
+  using C = WideCfg<BN>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave % C::WAVES_M;
+  const int wn = wave / C::WAVES_M;
+
+  const int M = op.B * op.Ho * op.Wo;
+  const int HW = op.Ho * op.Wo;
+  const int mtiles = (M + WBM - 1) / WBM;
+  const int ntiles = op.N / BN;
+  const int L = wide_xcd_remap(blockIdx.x, mtiles * ntiles);
+  const int ntile = L % ntiles;  // the n-tiles of one pixel tile run back to back (A reuse in L2)
+  const int mtile = L / ntiles;
+  const int m0 = mtile * WBM;
+  const int n0 = ntile * BN;
+
+  // ---- this lane's 4 A rows (output pixels) and DMA chunk swizzles ---------
+  const int q8 = lane >> 3;       // row within an 8-row DMA group
+  const int qc = lane & 7;        // LDS chunk this lane fills
+  int rb[4], ry[4], rx[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + wave * 32 + i * 8 + q8;
+    if (m < M) {
+      const int b = m / HW, r = m - b * HW;
+      rb[i] = b;
+      ry[i] = r / op.Wo;
+      rx[i] = r - ry[i] * op.Wo;
+    } else {
+      rb[i] = -1; ry[i] = 0; rx[i] = 0;
+    }
+  }
+  // logical chunk stored at LDS chunk qc of row R is qc ^ ((R >> 1) & 7); for
+  // R = wave*32 + i*8 + q8 (A) or wave*BN/8 + j*8 + q8 (B) that is (4i + lane>>4) & 7
+  const int sw_lane = lane >> 4;
+
+  int total_steps = 0;
+  for (int s = 0; s < op.nseg; ++s) total_steps += op.seg[s].kh * op.seg[s].kw * (op.seg[s].C / WBK);
+
+  const half_t* Wt = (const half_t*)op.W;
+  const half_t* zero = (const half_t*)g_wide_zero;
+  // the 4 rows share the chunk swizzle pattern per i: chunk = qc ^ ((4i + lane>>4) & 7)
+  SegCursor<4, WBK> cur(op, rb, ry, rx, 0);
+
+  auto issue = [&](int stage) {
+    unsigned char* As = smem + stage * C::STAGE;
+    unsigned char* Bs = As + C::A_BYTES;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ch = qc ^ ((4 * i + sw_lane) & 7);
+      glds16(cur.a_src(i, zero) + ch * 8, As + (wave * 32 + i * 8) * 128);
+    }
+    const int kb = cur.kb();
+#pragma unroll
+    for (int j = 0; j < C::BJ; ++j) {
+      const int n = wave * (BN / 8) + j * 8 + q8;
+      const int ch = qc ^ ((4 * j + sw_lane) & 7);
+      glds16(Wt + (size_t)(n0 + n) * op.Kpad + kb + ch * 8, Bs + (wave * (BN / 8) + j * 8) * 128);
+    }
+    cur.advance();
+  };
+
+  f32x4_w acc[C::WM][C::WN];
+#pragma unroll
+  for (int a = 0; a < C::WM; ++a)
+#pragma unroll
+    for (int b = 0; b < C::WN; ++b) acc[a][b] = f32x4_w{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15;
+  const int fg = lane >> 4;
+  const int rsw = (fr >> 1) & 7;  // swizzle of every fragment row this lane reads
+
+  if constexpr (!PIPE) {
+    if (total_steps > 0) issue(0);
+    for (int step = 0; step < total_steps; ++step) {
+      // stage step&1 has landed (own DMA retired, then everyone's via the
+      // barrier) and every wave is done reading the other stage (step-1)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (step + 1 < total_steps) issue((step + 1) & 1);
+      const half_t* As = (const half_t*)(smem + (step & 1) * C::STAGE);
+      const half_t* Bs = As + C::A_BYTES / 2;
+  #pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int pc = ((kk * 4 + fg) ^ rsw) * 8;
+        f16x8_w bf[C::WN];
+  #pragma unroll
+        for (int b = 0; b < C::WN; ++b) bf[b] = *(const f16x8_w*)(Bs + (wn * C::WN * 16 + b * 16 + fr) * 64 + pc);
+  #pragma unroll
+        for (int a = 0; a < C::WM; ++a) {
+          const f16x8_w af = *(const f16x8_w*)(As + (wm * C::WM * 16 + a * 16 + fr) * 64 + pc);
+  #pragma unroll
+          for (int b = 0; b < C::WN; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf[b], acc[a][b], 0, 0, 0);
+        }
+      }
+    }
+  } else {
+    // Half-step software pipeline: the fragments of the second 32-deep half
+    // of step s are read BEFORE the barrier that releases step s+1, and the
+    // MFMAs of that half run AFTER it, so the MFMA pipe stays busy across the
+    // barrier, the DMA issue and the first fragment reads of step s+1.
+    // WAR: each wave retires its reads of buffer s&1 (lgkmcnt(0)) before the
+    // barrier after which buffer s&1 is refilled.  RAW: own DMA of step s+1
+    // retired (vmcnt(0)) before that same barrier.
+    f16x8_w a0[C::WM], b0[C::WN], a1[C::WM], b1[C::WN];
+    auto rd = [&](int buf, int kk, f16x8_w (&af)[C::WM], f16x8_w (&bf)[C::WN]) {
+      const half_t* As = (const half_t*)(smem + buf * C::STAGE);
+      const half_t* Bs = As + C::A_BYTES / 2;
+      const int pc = ((kk * 4 + fg) ^ rsw) * 8;
+#pragma unroll
+      for (int b = 0; b < C::WN; ++b) bf[b] = *(const f16x8_w*)(Bs + (wn * C::WN * 16 + b * 16 + fr) * 64 + pc);
+#pragma unroll
+      for (int a = 0; a < C::WM; ++a) af[a] = *(const f16x8_w*)(As + (wm * C::WM * 16 + a * 16 + fr) * 64 + pc);
+    };
+    auto mm = [&](const f16x8_w (&af)[C::WM], const f16x8_w (&bf)[C::WN]) {
+#pragma unroll
+      for (int a = 0; a < C::WM; ++a)
+#pragma unroll
+        for (int b = 0; b < C::WN; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a], bf[b], acc[a][b], 0, 0, 0);
+    };
+    // (the host routes total_steps < 2 to the plain loop)
+    // ds_read / MFMA interleave of one half-step: one A fragment (and, for the
+    // first four, one B fragment) of the next half between each group of WN
+    // MFMAs, so the fragments of the half being consumed free registers as the
+    // next half's arrive
+    auto interleave = [&]() {
+#pragma unroll
+      for (int a = 0; a < C::WN; ++a) {
+        __builtin_amdgcn_sched_group_barrier(0x008, C::WN, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      }
+#pragma unroll
+      for (int a = C::WN; a < C::WM; ++a) {
+        __builtin_amdgcn_sched_group_barrier(0x008, C::WN, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+    };
+    issue(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    issue(1);
+    rd(0, 0, a0, b0);
+    for (int step = 0; step < total_steps - 1; ++step) {
+      rd(step & 1, 1, a1, b1);
+      mm(a0, b0);
+      interleave();
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      issue(step & 1);  // step + 2 (past the end: a harmless re-read into a buffer nobody reads again)
+      rd((step + 1) & 1, 0, a0, b0);
+      mm(a1, b1);
+      interleave();
+    }
+    rd((total_steps - 1) & 1, 1, a1, b1);
+    mm(a0, b0);
+    mm(a1, b1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave is done with both stages before the epilogue reuses LDS
+  }
+
+  wide_epilogue<BN, C::WM, C::WN, C::WAVES_M>(op, acc, smem, m0, n0, M, HW);
+}
+
+
+template <int BN, bool PIPE>
 static int launch_wide_bn(const ConvOp& op, hipStream_t st) {
   using C = WideCfg<BN>;
   static bool attr_set = false;
   if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute((const void*)conv_wide_kernel<BN>,
+    const hipError_t e = hipFuncSetAttribute((const void*)conv_wide_kernel<BN, PIPE>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
   const int M = op.B * op.Ho * op.Wo;
   const int grid = ((M + WBM - 1) / WBM) * (op.N / BN);
-  hipLaunchKernelGGL((conv_wide_kernel<BN>), dim3(grid), dim3(512), C::LDS, st, op);
+  hipLaunchKernelGGL((conv_wide_kernel<BN, PIPE>), dim3(grid), dim3(512), C::LDS, st, op);
   return (int)hipGetLastError();
+}
+
+// UPR_WIDE_KIND=0 selects the plain main loop (A/B timing); default: the
+// half-step pipeline across the barrier
+static int wide_kind() {
+  static int k = -1;
+  if (k < 0) {
+    const char* e = getenv("UPR_WIDE_KIND");
+    k = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  return k;
+}
+
+template <int BN>
+static int launch_wide_any(const ConvOp& op, hipStream_t st) {
+  int steps = 0;
+  for (int s = 0; s < op.nseg; ++s) steps += op.seg[s].kh * op.seg[s].kw * (op.seg[s].C / WBK);
+  if (steps < 2) return launch_wide_bn<BN, false>(op, st);
+  return wide_kind() == 0 ? launch_wide_bn<BN, false>(op, st) : launch_wide_bn<BN, true>(op, st);
 }
 
 // UPR_CONV_WIDE=0 disables this path (A/B timing against conv_halo / conv_igemm)
@@ -325,14 +474,14 @@ int launch_conv_wide(const ConvOp& op, hipStream_t st) {
     if (sg.pre != kPreNone || sg.C % WBK || sg.cs % 8 || sg.coff % 8 || sg.kbase % 8) return kErrUnsupported;
     if ((uintptr_t)sg.src % 16) return kErrUnsupported;
   }
-  if (op.N % 256 == 0) return launch_wide_bn<256>(op, st);
+  if (op.N % 256 == 0) return launch_wide_any<256>(op, st);
   // 128-channel tiles of pure stride-1 3x3 convs stay on the halo kernel (it
   // stages each input pixel once for all 9 taps and measured faster there)
   bool all_s1_3x3 = true;
   for (int s = 0; s < op.nseg; ++s)
     if (!(op.seg[s].kh == 3 && op.seg[s].stride == 1)) all_s1_3x3 = false;
   if (all_s1_3x3 && op.Wo >= 24 && op.Ho >= 8) return kErrUnsupported;
-  return launch_wide_bn<128>(op, st);
+  return launch_wide_any<128>(op, st);
 }
 
 }  // namespace upr
