@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--train", action="store_true",
                     help="configs[4]: one training step (fwd + TotalLoss + bwd + clip + Adam) per step, "
                          "bs=8 512x512 plain model (batch/size overridable)")
+    ap.add_argument("--amp", action="store_true",
+                    help="with --train: the reference's AMP branch (GradScaler: scaled backward, unscale_, "
+                         "skip on inf/nan, scale update); arithmetic stays fp32")
     return ap.parse_args()
 
 
@@ -190,8 +193,20 @@ def train_main(args):
     crit = TotalLoss(use_freq_loss=True).to(dev)
     opt = make_optimizer(model, lr=1e-4, weight_decay=1e-5)
     x = torch.rand(B, 3, S, S, generator=torch.Generator().manual_seed(2 + rank)).to(dev)
+    from upr.dist import allreduce_grads
+    scaler = None
+    if args.amp:
+        from trainers.train import GradScaler
+        scaler = GradScaler()
+
+    def tstep():
+        if world == 1:
+            return train_step(model, x, crit, opt, scaler=scaler, use_amp=args.amp)
+        return train_step(model, x, crit, opt, scaler=scaler, use_amp=args.amp,
+                          grad_hook=lambda: allreduce_grads(opt))
+
     for _ in range(args.warmup):
-        train_step(model, x, crit, opt)
+        tstep()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -199,7 +214,7 @@ def train_main(args):
     t0 = time.perf_counter()
     d = None
     for _ in range(args.steps):
-        _, d = train_step(model, x, crit, opt)
+        _, d = tstep()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -217,9 +232,11 @@ def train_main(args):
         "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic torch.rand inputs, random-init weights (seed 0), seeded random-init VGG19 (seed 1234)",
-        "config": {"workload": f"configs[4]: bs={B}/GPU {S}x{S} {args.variant} train step (fp32; AMP flag "
-                               f"computes in fp32 here)", "global_batch": world * B, "image_size": S,
-                   "variant": args.variant, "parallelism": f"data-parallel x{world} (per-rank shard)"},
+        "config": {"workload": f"configs[4]: bs={B}/GPU {S}x{S} {args.variant} train step"
+                               + (" with GradScaler (AMP control flow, fp32 arithmetic)" if args.amp else " (fp32)"),
+                   "global_batch": world * B, "image_size": S, "variant": args.variant,
+                   "parallelism": f"data-parallel x{world} (per-rank shard"
+                                  + (", RCCL all-reduce of the flat gradient buffer)" if world > 1 else ")")},
         "last_loss": d,
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_TFLOPS["fp32"], "unit": "TFLOP/s",
                      "frac": achieved / PEAK_TFLOPS["fp32"], "traffic": None,

@@ -171,14 +171,15 @@ int upr_t_retinex_bwd(const float* x, const float* illu, const float* e, const f
 size_t upr_t_loss_workspace(int B, int H, int W);
 /* Every non-perceptual, non-frequency term: exposure (:29-58), edge-aware
  * smoothness (:138-176), colour (:351-371), spatial (:408-427), decoupling
- * (:275-334), texture complexity 'tv' (:523-548) and the dynamic smooth weight
- * (:704-720).  terms (device fp32, layout of upr_t_loss_total) receives
- * [0..4] and [8];
+ * (:275-334), texture complexity of img_low (:523-583; texture 0 = 'tv',
+ * 1 = 'edge_density') and the dynamic smooth weight
+ * clamp(w_smooth * (1 - 0.8 * batch-mean complexity), 0.1, 5) (:704-720).
+ * terms (device fp32, layout of upr_t_loss_total) receives [0..4] and [8];
  * with grads != 0, g_enh / g_illu / g_refl (NCHW) are OVERWRITTEN with the
  * weighted gradient of those terms. */
 int upr_t_loss_pixel(const float* low, const float* enh, const float* illu, const float* refl, int B, int H, int W,
                      void* ws, float* terms, float* g_enh, float* g_illu, float* g_refl, int grads, float w_exp,
-                     float w_col, float w_spa, float w_dec, void* stream);
+                     float w_col, float w_spa, float w_dec, float w_smooth, int texture, void* stream);
 /* Perceptual MSE level (F.mse_loss): acc (fp64) += sum (a-b)^2 / n; with
  * g != NULL, g = scale*2*(a-b) (scale = weight/n). */
 int upr_t_mse(const float* a, const float* b, size_t n, double* acc, float* g, float scale, void* stream);
@@ -202,6 +203,10 @@ int upr_t_loss_total(float* terms, float w_exp, float w_col, float w_spa, float 
                      void* stream);
 
 /* ---- optimiser (torch.nn.utils.clip_grad_norm_ + torch.optim.Adam) ------ */
+/* GradScaler.unscale_ (trainers/train.py:84-86 with use_amp; torch.amp.GradScaler):
+ * g[i] *= 1 / *scale over n elements; *found_inf (caller-zeroed) = 1 when any
+ * unscaled value is inf or nan.  scale and found_inf are device fp32 scalars. */
+int upr_t_unscale(float* g, size_t n, const float* scale, float* found_inf, void* stream);
 /* acc (fp64, zeroed) += sum g^2 over n elements. */
 int upr_t_sqsum(const float* g, size_t n, double* acc, void* stream);
 /* One Adam step over a flat parameter buffer with the clip_grad_norm_(max_norm)

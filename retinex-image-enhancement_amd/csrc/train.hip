@@ -802,6 +802,7 @@ struct LossWS {
   double* patch;   // B * (H/16) * (W/16) sums of gray(enh)
   double* rowsum;  // B*H   sum_{x<W-1} edge
   double* colsum;  // B*W   sum_{y<H-1} edge
+  double* ed;      // 2B    texture 'edge_density': per image sum of |Sobel|, count above threshold
   float* scal;     // finalised scalars for the gradient pass
 };
 
@@ -812,13 +813,14 @@ static LossWS loss_ws(void* ws, int B, int H, int W) {
   l.patch = (double*)p; p += align_up(sizeof(double) * B * (H / 16) * (W / 16), 256);
   l.rowsum = (double*)p; p += align_up(sizeof(double) * B * H, 256);
   l.colsum = (double*)p; p += align_up(sizeof(double) * B * W, 256);
+  l.ed = (double*)p; p += align_up(sizeof(double) * 2 * B, 256);
   l.scal = (float*)p;
   return l;
 }
 static size_t loss_ws_bytes(int B, int H, int W) {
   return align_up(sizeof(double) * (LA_FIXED + 7 * B), 256) + align_up(sizeof(double) * B * (H / 16) * (W / 16), 256) +
          align_up(sizeof(double) * B * H, 256) + align_up(sizeof(double) * B * W, 256) +
-         align_up(sizeof(float) * (64 + 8 * B), 256);
+         align_up(sizeof(double) * 2 * B, 256) + align_up(sizeof(float) * (64 + 8 * B), 256);
 }
 
 // scalar slots
@@ -952,8 +954,30 @@ __global__ __launch_bounds__(256) void loss_pass2_kernel(const float* __restrict
   block_sum_atomic<2>(v, dst);
 }
 
+// texture complexity 'edge_density' (loss.py:549-577): per image, the share of
+// pixels whose Sobel magnitude of gray(low) exceeds 1.5x the image mean.
+// mode 0: per-image sum of magnitudes; mode 1: per-image count above threshold
+__global__ __launch_bounds__(256) void edge_density_kernel(const float* __restrict__ low, int H, int W, LossWS ws,
+                                                           int mode) {
+  const int b = blockIdx.y;
+  const int HW = H * W;
+  const size_t base = (size_t)b * 3 * HW;
+  const int per = (HW + gridDim.x - 1) / gridDim.x;
+  const int p0 = blockIdx.x * per, p1 = min(HW, p0 + per);
+  const float thr = mode ? (float)(ws.ed[b] / HW) * 1.5f : 0.f;
+  double v[1] = {0.0};
+  for (int q = p0 + threadIdx.x; q < p1; q += 256) {
+    const int y = q / W, x = q - y * W;
+    const float e = edge_at(low, base, H, W, y, x);
+    v[0] += mode ? (e > thr ? 1.0 : 0.0) : (double)e;
+  }
+  double* dst[1] = {ws.ed + mode * gridDim.y + b};
+  block_sum_atomic<1>(v, dst);
+}
+
 // finalise: one block
-__global__ void loss_final_kernel(int B, int H, int W, LossWS ws, float* __restrict__ terms) {
+__global__ void loss_final_kernel(int B, int H, int W, LossWS ws, float* __restrict__ terms, int texture,
+                                  float w_smooth) {
   __shared__ double ex[256];
   const int HW = H * W;
   const double N = (double)B * HW;
@@ -974,8 +998,13 @@ __global__ void loss_final_kernel(int B, int H, int W, LossWS ws, float* __restr
   const double col = (mu0 - mu1) * (mu0 - mu1) + (mu0 - mu2) * (mu0 - mu2) + (mu1 - mu2) * (mu1 - mu2);
   const double spa = ws.acc[LA_SPA_H] / nh + ws.acc[LA_SPA_V] / nv;
   const double smo = ws.acc[LA_SM_H] / nh1 + ws.acc[LA_SM_V] / nv1;
-  const double tc = ws.acc[LA_TV_H] / nh + ws.acc[LA_TV_V] / nv;
-  double wsm = 1.0 * (1.0 - tc * 0.8);
+  double tc = ws.acc[LA_TV_H] / nh + ws.acc[LA_TV_V] / nv;
+  if (texture == 1) {
+    tc = 0.0;
+    for (int b = 0; b < B; ++b) tc += ws.ed[B + b] / HW;
+    tc /= B;
+  }
+  double wsm = (double)w_smooth * (1.0 - tc * 0.8);
   wsm = wsm < 0.1 ? 0.1 : (wsm > 5.0 ? 5.0 : wsm);
   double frob = 0.0, md = 0.0;
   for (int b = 0; b < B; ++b) {
@@ -1157,6 +1186,20 @@ __global__ __launch_bounds__(256) void sqsum_kernel(const float* __restrict__ g,
   GSTRIDE(i, n) v[0] += (double)g[i] * g[i];
   double* dst[1] = {acc};
   block_sum_atomic<1>(v, dst);
+}
+
+// GradScaler.unscale_ (torch.amp.GradScaler, train.py:84-86): g *= 1/scale and
+// found_inf = 1 if any unscaled value is inf/nan (a benign same-value race)
+__global__ __launch_bounds__(256) void unscale_kernel(float* __restrict__ g, long long n,
+                                                      const float* __restrict__ scale, float* __restrict__ found_inf) {
+  const float inv = 1.f / *scale;
+  bool bad = false;
+  GSTRIDE(i, n) {
+    const float v = g[i] * inv;
+    g[i] = v;
+    bad |= !isfinite(v);
+  }
+  if (bad) *found_inf = 1.f;
 }
 
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
@@ -1501,8 +1544,9 @@ size_t upr_t_loss_workspace(int B, int H, int W) {
 
 int upr_t_loss_pixel(const float* low, const float* enh, const float* illu, const float* refl, int B, int H, int W,
                      void* ws, float* terms, float* g_enh, float* g_illu, float* g_refl, int grads, float w_exp,
-                     float w_col, float w_spa, float w_dec, void* stream) {
+                     float w_col, float w_spa, float w_dec, float w_smooth, int texture, void* stream) {
   if (!low || !enh || !illu || !refl || !ws || !terms || B <= 0) return UPR_ERR_ARG;
+  if (texture != 0 && texture != 1) return UPR_ERR_ARG;
   if (H % 16 || W % 16 || H < 16 || W < 16) return UPR_ERR_SHAPE;
   if (grads && (!g_enh || !g_illu || !g_refl)) return UPR_ERR_ARG;
   hipStream_t st = ST(stream);
@@ -1515,7 +1559,13 @@ int upr_t_loss_pixel(const float* low, const float* enh, const float* illu, cons
   UPR_CHECK_HIP(hipGetLastError());
   hipLaunchKernelGGL(loss_pass2_kernel, dim3(chunks, B), dim3(256), 0, st, low, illu, H, W, l);
   UPR_CHECK_HIP(hipGetLastError());
-  hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(256), 0, st, B, H, W, l, terms);
+  if (texture == 1) {
+    for (int mode = 0; mode < 2; ++mode) {
+      hipLaunchKernelGGL(edge_density_kernel, dim3(chunks, B), dim3(256), 0, st, low, H, W, l, mode);
+      UPR_CHECK_HIP(hipGetLastError());
+    }
+  }
+  hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(256), 0, st, B, H, W, l, terms, texture, w_smooth);
   UPR_CHECK_HIP(hipGetLastError());
   if (grads) {
     hipLaunchKernelGGL(loss_grad_kernel, dim3(grid_for((long long)B * H * W)), dim3(256), 0, st, low, enh, illu, refl,
@@ -1577,6 +1627,13 @@ int upr_t_sqsum(const float* g, size_t n, double* acc, void* stream) {
   if (!g || !acc) return UPR_ERR_ARG;
   hipLaunchKernelGGL(sqsum_kernel, dim3(grid_for((long long)n, 256, 2048)), dim3(256), 0, ST(stream), g,
                      (long long)n, acc);
+  LAUNCH_CHECK();
+}
+
+int upr_t_unscale(float* g, size_t n, const float* scale, float* found_inf, void* stream) {
+  if (!g || !scale || !found_inf) return UPR_ERR_ARG;
+  hipLaunchKernelGGL(unscale_kernel, dim3(grid_for((long long)n, 256, 2048)), dim3(256), 0, ST(stream), g,
+                     (long long)n, scale, found_inf);
   LAUNCH_CHECK();
 }
 

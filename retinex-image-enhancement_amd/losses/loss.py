@@ -13,8 +13,9 @@ Differences, all forced by the environment and recorded in DESIGN.md:
     (e.g. a local copy of torchvision's vgg19 weights); without one the VGG is
     PyTorch-default-initialised under `vgg_seed` (1234, the seed the parity
     fixtures use).
-  * adaptive_weights=True (DWA, :755-798) and texture_method='edge_density'
-    inside TotalLoss are not implemented on the device and raise.
+  * use_dynamic_smooth_weight=False is not implemented on the device and
+    raises.  adaptive_weights=True (DWA, :755-798) keeps the reference's host
+    loss history; texture_method 'tv' and 'edge_density' both run on the device.
 """
 import torch
 import torch.nn as nn
@@ -48,7 +49,8 @@ class _EngineHolder(nn.Module):
         if eng is None or eng[0] != dev:
             feats = self.features.to(dev) if hasattr(self, "features") else E.vgg19_features(_VGG_SEED).to(dev)
             eng = (dev, E.TotalLossEngine(feats, weights=getattr(self, "_weights", None),
-                                          use_freq_loss=getattr(self, "use_freq_loss", True)))
+                                          use_freq_loss=getattr(self, "use_freq_loss", True),
+                                          texture_method=getattr(self, "texture_method", "tv")))
             self.__dict__["_eng"] = eng
         return eng[1]
 
@@ -154,11 +156,11 @@ class TotalLoss(_EngineHolder):
                  weight_perceptual=1.0, weight_freq=0.5, use_freq_loss=True, adaptive_weights=False,
                  use_dynamic_smooth_weight=True, texture_method='tv', vgg_weights=None, vgg_seed=_VGG_SEED):
         super().__init__()
-        if adaptive_weights:
-            raise NotImplementedError("adaptive_weights (DWA, loss.py:755-798) is not implemented on the device")
-        if not use_dynamic_smooth_weight or texture_method != 'tv' or weight_smooth != 1.0:
-            raise NotImplementedError("the device loss implements the dynamic smooth weight with texture_method='tv'"
-                                      " and weight_smooth=1.0 (the reference training defaults)")
+        if not use_dynamic_smooth_weight:
+            raise NotImplementedError("the device loss implements the dynamic smooth weight "
+                                      "(use_dynamic_smooth_weight=True, the reference training default)")
+        if texture_method not in E.TEXTURE:
+            raise ValueError(f"不支持的纹理复杂度计算方法: {texture_method}")
         self.features = _features(vgg_weights, vgg_seed)
         self.use_freq_loss = use_freq_loss
         self.adaptive_weights = adaptive_weights
@@ -166,6 +168,8 @@ class TotalLoss(_EngineHolder):
         self.texture_method = texture_method
         self._weights = dict(exposure=weight_exp, smoothness=weight_smooth, color=weight_col, spatial=weight_spa,
                              decouple=weight_decouple, perceptual=weight_perceptual, frequency=weight_freq)
+        if adaptive_weights:
+            self.loss_history = {k: [] for k in _DWA_KEYS}
 
     def forward(self, img_low, img_enhanced, illu_map, reflectance=None, epoch=0):
         if reflectance is None:
@@ -173,9 +177,43 @@ class TotalLoss(_EngineHolder):
         for t, n in ((img_low, "img_low"), (img_enhanced, "img_enhanced"), (illu_map, "illu_map"),
                      (reflectance, "reflectance")):
             _require(t, n)
-        total, terms = loss_forward(self._engine(img_enhanced.device), img_low.contiguous(), img_enhanced,
-                                    illu_map, reflectance)
-        return total, E.terms_dict(terms)
+        eng = self._engine(img_enhanced.device)
+        # weights of this step (loss.py:690-702): DWA from the history after epoch 1
+        eng.w = self._compute_adaptive_weights() if self.adaptive_weights and epoch > 1 else dict(self._weights)
+        total, terms = loss_forward(eng, img_low.contiguous(), img_enhanced, illu_map, reflectance)
+        d = E.terms_dict(terms)
+        if self.adaptive_weights:
+            for k in _DWA_KEYS:
+                self.loss_history[k].append(d[k])
+        return total, d
+
+    def _compute_adaptive_weights(self):
+        """Dynamic Weight Average (loss.py:755-798): w_k = (L_k[-1] / L_k[-2]) / T
+        (T = 2, ratio 1 when L_k[-2] <= 1e-8; the constructor weight while a
+        term has < 2 entries), renormalised to sum to the number of terms.  The
+        smoothness weight is then replaced by the dynamic smooth weight."""
+        return dwa_weights(self.loss_history, self._weights)
+
+
+_DWA_KEYS = ("exposure", "smoothness", "color", "spatial", "decouple", "perceptual", "frequency")
+
+
+def dwa_weights(history, defaults, temperature=2.0):
+    """The weight rule of TotalLoss._compute_adaptive_weights (loss.py:755-798)
+    over host loss histories (python floats, as the reference's .item()s)."""
+    w = {}
+    for k in history:
+        h = history[k]
+        if len(h) >= 2:
+            ratio = h[-1] / h[-2] if h[-2] > 1e-8 else 1.0
+            w[k] = ratio / temperature
+        else:
+            w[k] = defaults.get(k, 1.0)
+    tot = sum(w.values())
+    if w and tot > 0:
+        n = len(w)
+        w = {k: n * v / tot for k, v in w.items()}
+    return w
 
 
 def calculate_texture_complexity(img, method='tv'):  # pragma: no cover - not on the training hot path

@@ -4,17 +4,32 @@
 (zero_grad -> forward -> TotalLoss -> backward -> clip_grad_norm_(1.0) ->
 Adam.step()); the model, loss and optimiser it is handed run on the gfx950
 training kernels: `make_optimizer` builds upr.optim.Adam (flat-buffer fused
-clip + Adam), and `clip_grad_norm_` is upr.optim's.  `use_amp` is accepted
-and the step computes in fp32 (mixed-precision training kernels are the next
-scope row; the fp32 step is numerically the reference's no-AMP branch).
+clip + Adam), and `clip_grad_norm_` is upr.optim's.  With `use_amp` and a
+scaler the step follows the reference's AMP branch (train.py:71-89): scaled
+backward, unscale_ (one launch over the flat gradient buffer), clip, a step
+skipped on inf/nan, scale update — upr.amp.GradScaler (a torch.amp.GradScaler
+handed in is mirrored by one with its settings).  The arithmetic stays fp32
+(precision >= autocast's).
 """
 import time
 
 import torch
 
+from upr import amp as uamp
 from upr import optim as uoptim
 
 clip_grad_norm_ = uoptim.clip_grad_norm_
+GradScaler = uamp.GradScaler
+_mirrors = {}
+
+
+def _as_upr_scaler(scaler):
+    if scaler is None or isinstance(scaler, uamp.GradScaler):
+        return scaler
+    m = _mirrors.get(id(scaler))
+    if m is None or m[0] is not scaler:
+        m = _mirrors[id(scaler)] = (scaler, uamp.GradScaler.from_torch(scaler))
+    return m[1]
 
 
 def make_optimizer(model, lr=1e-4, weight_decay=1e-5):
@@ -22,14 +37,28 @@ def make_optimizer(model, lr=1e-4, weight_decay=1e-5):
     return uoptim.Adam(model.parameters(), lr=lr, weight_decay=weight_decay)
 
 
-def train_step(model, img_low, criterion, optimizer, max_norm=1.0):
-    """One step body (train.py:63-103, no-AMP branch).  Returns (loss, loss_dict)."""
+def train_step(model, img_low, criterion, optimizer, max_norm=1.0, scaler=None, use_amp=False, grad_hook=None):
+    """One step body (train.py:63-103).  Returns (loss, loss_dict).  grad_hook
+    (e.g. upr.dist.allreduce_grads for data parallelism) runs between the
+    backward and the unscale / clip."""
     optimizer.zero_grad()
     img_enhanced, reflectance, illu_map = model(img_low)
     loss, loss_dict = criterion(img_low, img_enhanced, illu_map, reflectance)
-    loss.backward()
-    clip_grad_norm_(model.parameters(), max_norm=max_norm)
-    optimizer.step()
+    scaler = _as_upr_scaler(scaler) if use_amp else None
+    if scaler is not None:
+        scaler.scale(loss).backward()
+        if grad_hook is not None:
+            grad_hook()
+        scaler.unscale_(optimizer)
+        clip_grad_norm_(model.parameters(), max_norm=max_norm)
+        scaler.step(optimizer)
+        scaler.update()
+    else:
+        loss.backward()
+        if grad_hook is not None:
+            grad_hook()
+        clip_grad_norm_(model.parameters(), max_norm=max_norm)
+        optimizer.step()
     return loss, loss_dict
 
 
@@ -41,7 +70,7 @@ def train_one_epoch(model, dataloader, criterion, optimizer, device, epoch, writ
     t0 = time.time()
     for batch_idx, img_low in enumerate(dataloader):
         img_low = img_low.to(device, torch.float32)
-        _, loss_dict = train_step(model, img_low, criterion, optimizer)
+        _, loss_dict = train_step(model, img_low, criterion, optimizer, scaler=scaler, use_amp=use_amp)
         for k in keys:
             totals[k] += loss_dict[k]
         n += 1

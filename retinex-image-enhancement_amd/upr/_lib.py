@@ -120,7 +120,7 @@ SIGNATURES.update({
     "upr_t_retinex_fwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _p]),
     "upr_t_retinex_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p]),
     "upr_t_loss_workspace": (c_size_t, [_i, _i, _i]),
-    "upr_t_loss_pixel": (_i, [_p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p, _i, _f, _f, _f, _f, _p]),
+    "upr_t_loss_pixel": (_i, [_p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p, _i, _f, _f, _f, _f, _f, _i, _p]),
     "upr_t_mse": (_i, [_p, _p, c_size_t, _p, _p, _f, _p]),
     "upr_t_vgg_norm": (_i, [_p, _p, _i, _i, _i, _p]),
     "upr_t_vgg_norm_bwd": (_i, [_p, _p, _i, _i, _i, _p]),
@@ -129,6 +129,7 @@ SIGNATURES.update({
     "upr_t_scale_acc": (_i, [_p, _i, _f, _p, _p]),
     "upr_t_loss_total": (_i, [_p, _f, _f, _f, _f, _f, _f, _p]),
     "upr_t_sqsum": (_i, [_p, c_size_t, _p, _p]),
+    "upr_t_unscale": (_i, [_p, c_size_t, _p, _p, _p]),
     "upr_t_adam": (_i, [_p, _p, _p, _p, c_size_t, _p, _f, _f, _f, _f, _f, _f, _i, _p, _p]),
 })
 

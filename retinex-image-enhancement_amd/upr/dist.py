@@ -58,3 +58,17 @@ def sharded_forward(model, x_local, total, collect=False, collect_dtype=None):
         return enh, refl, illu
     src = enh if collect_dtype is None else enh.to(collect_dtype)
     return gather_shards(src, total), refl, illu
+
+
+def allreduce_grads(optimizer, group=None):
+    """Data-parallel training: average the gradients over the
+    ranks with ONE all-reduce of the optimiser's flat gradient buffer (RCCL
+    over xGMI on ROCm devices; gloo on CPU).  BatchNorm statistics stay per
+    rank, as the reference has no SyncBN.  Call between the backward and the
+    unscale / clip (trainers.train.train_step's grad_hook)."""
+    world = dist.get_world_size(group)
+    if world == 1:
+        return
+    g = optimizer.flat.grad
+    dist.all_reduce(g, op=dist.ReduceOp.SUM, group=group)
+    g.div_(world)

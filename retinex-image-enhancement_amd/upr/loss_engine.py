@@ -25,6 +25,7 @@ from .train import Act, Conv, _chk, _fp, _p, _stream, empty, relu_mask, zero
 
 WEIGHTS = dict(exposure=10.0, smoothness=1.0, color=0.5, spatial=1.0, decouple=0.1, perceptual=1.0,
                frequency=0.5)
+TEXTURE = {"tv": 0, "edge_density": 1}  # calculate_texture_complexity methods (loss.py:523-583)
 TERM_ORDER = ("exposure", "smoothness", "color", "spatial", "decouple", "perceptual", "frequency", "total")
 
 VGG19_E = (64, 64, "M", 128, 128, "M", 256, 256, 256, 256, "M", 512, 512, 512, 512, "M", 512, 512, 512, 512, "M")
@@ -113,13 +114,19 @@ class VGGPerceptual:
 
 
 class TotalLossEngine:
-    """losses/loss.py TotalLoss with adaptive_weights=False,
-    use_dynamic_smooth_weight=True, texture_method='tv' (train.py:224-234)."""
+    """losses/loss.py TotalLoss with use_dynamic_smooth_weight=True
+    (train.py:224-234).  `w` holds the weights of the current step (the DWA
+    weights when TotalLoss adapts them); `w_smooth` is the constructor's
+    weight_smooth, which the dynamic smooth weight scales (loss.py:713)."""
 
-    def __init__(self, vgg_features, weights=None, use_freq_loss=True):
+    def __init__(self, vgg_features, weights=None, use_freq_loss=True, texture_method="tv"):
+        if texture_method not in TEXTURE:
+            raise ValueError(f"不支持的纹理复杂度计算方法: {texture_method}")
         self.w = dict(WEIGHTS)
         if weights:
             self.w.update(weights)
+        self.w_smooth = self.w["smoothness"]
+        self.texture_method = texture_method
         self.use_freq = use_freq_loss
         self.vgg = VGGPerceptual(vgg_features)
         self.features = vgg_features
@@ -140,7 +147,8 @@ class TotalLossEngine:
         _chk(lib.upr_t_loss_pixel(_p(low), _p(enh), _p(illu), _p(refl), B, H, W, _p(ws), _p(terms), _p(g_enh),
                                   _p(g_illu), _p(g_refl), int(grads), ctypes.c_float(w["exposure"]),
                                   ctypes.c_float(w["color"]), ctypes.c_float(w["spatial"]),
-                                  ctypes.c_float(w["decouple"]), st), "loss_pixel")
+                                  ctypes.c_float(w["decouple"]), ctypes.c_float(self.w_smooth),
+                                  TEXTURE[self.texture_method], st), "loss_pixel")
         acc = torch.empty(4, dtype=torch.float64, device=dev)
         zero(acc)
         # ---- perceptual ----

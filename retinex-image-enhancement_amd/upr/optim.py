@@ -52,6 +52,14 @@ def clip_grad_norm_(parameters, max_norm, norm_type=2.0):
     return cs.norm
 
 
+def discard_clip(optimizer):
+    """Drop the clip recorded by clip_grad_norm_ for a step that is skipped
+    (GradScaler.step on a non-finite step)."""
+    cs = _clip.get(id(optimizer.flat))
+    if cs is not None:
+        cs.max_norm = 0.0
+
+
 class Adam:
     """torch.optim.Adam(params, lr, betas, eps, weight_decay) (L2 decay added to
     the gradient, bias-corrected moments) over the flat buffer."""

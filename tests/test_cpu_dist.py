@@ -50,3 +50,31 @@ def test_gloo_gather_world2():
         for p in procs:
             p.join(timeout=60)
         assert sorted(res) == [(0, True), (1, True)]
+
+
+def _grad_worker(rank, world, port, q):
+    from types import SimpleNamespace
+    from upr.dist import allreduce_grads
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = torch.arange(10, dtype=torch.float32) * (rank + 1)
+    opt = SimpleNamespace(flat=SimpleNamespace(grad=g))
+    allreduce_grads(opt)
+    # mean over ranks of k * (r + 1) = k * (world + 1) / 2
+    want = torch.arange(10, dtype=torch.float32) * (world + 1) / 2
+    q.put((rank, bool(torch.allclose(opt.flat.grad, want))))
+    dist.destroy_process_group()
+
+
+def test_gloo_allreduce_grads_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_grad_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert sorted(res) == [(0, True), (1, True)]

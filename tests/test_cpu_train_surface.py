@@ -41,9 +41,9 @@ def test_losses_refuse_cpu_tensors():
 
 def test_unsupported_options_raise():
     with pytest.raises(NotImplementedError):
-        L.TotalLoss(adaptive_weights=True)
-    with pytest.raises(NotImplementedError):
-        L.TotalLoss(texture_method="edge_density")
+        L.TotalLoss(use_dynamic_smooth_weight=False)
+    with pytest.raises(ValueError):
+        L.TotalLoss(texture_method="laplacian")
 
 
 def test_model_train_forward_refuses_cpu():

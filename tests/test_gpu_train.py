@@ -155,6 +155,59 @@ def test_loss_terms_and_grads(golden):
         _close(t.grad, torch.from_numpy(g[name]), 1e-4, name)
 
 
+@pytest.mark.parametrize("texture,w_smooth", [("edge_density", 1.0), ("edge_density", 2.0), ("tv", 0.5)])
+def test_loss_texture_methods_vs_oracle(golden, texture, w_smooth):
+    """TotalLoss(texture_method, weight_smooth) on the G6 inputs: the dynamic
+    smooth weight from the edge-density complexity (oracle pinned to G6's
+    tex_edge) and the total + gradients against the oracle's autograd."""
+    from losses.loss import TotalLoss
+    from oracle import train as otrain
+    g = golden("g6_losses.npz")
+    low, enh, illu, refl = (torch.from_numpy(g[k]) for k in ("low", "enh", "illu", "refl"))
+    crit = TotalLoss(use_freq_loss=True, texture_method=texture, weight_smooth=w_smooth).to(DEV)
+    e, i, r = (t.to(DEV).clone().requires_grad_(True) for t in (enh, illu, refl))
+    total, d = crit(low.to(DEV), e, i, r)
+    total.backward()
+    torch.cuda.synchronize()
+    tex = g["tex_edge"] if texture == "edge_density" else g["tex_tv"]
+    want_w = float(np.clip(w_smooth * (1.0 - 0.8 * np.mean(tex, dtype=np.float64)), 0.1, 5.0))
+    # a Sobel magnitude within rounding of the 1.5x-mean threshold may flip one
+    # pixel's edge bit (device FMA order vs the CPU conv): allow two flips
+    B, _, H, W = low.shape
+    np.testing.assert_allclose(d["smooth_weight"], want_w, rtol=1e-6,
+                               atol=(0.8 * w_smooth * 2.0 / (B * H * W) if texture == "edge_density" else 0.0))
+    ce, ci, cr = (t.clone().requires_grad_(True) for t in (enh, illu, refl))
+    t_ref, d_ref = otrain.total_loss(otrain.vgg19_state(VGG_SEED), low, ce, ci, cr, texture_method=texture,
+                                     weight_smooth=w_smooth)
+    t_ref.backward()
+    np.testing.assert_allclose(d["total"], d_ref["total"], rtol=1e-4)
+    for name, a, b in (("grad_enh", e, ce), ("grad_illu", i, ci), ("grad_refl", r, cr)):
+        _close(a.grad, b.grad, 1e-4, name)
+
+
+def test_loss_adaptive_weights_dwa():
+    """adaptive_weights=True (DWA, loss.py:755-798): after epoch 1 the step's
+    weights come from the last two values of every term; the total equals the
+    DWA-weighted sum with the dynamic smooth weight."""
+    from losses.loss import TotalLoss, dwa_weights
+    torch.manual_seed(4)
+    low = torch.rand(2, 3, 64, 64).to(DEV) * 0.5
+    crit = TotalLoss(use_freq_loss=True, adaptive_weights=True).to(DEV)
+    outs = []
+    for k in range(3):
+        enh = torch.rand(2, 3, 64, 64, generator=torch.Generator().manual_seed(20 + k)).to(DEV)
+        illu = torch.rand(2, 1, 64, 64, generator=torch.Generator().manual_seed(30 + k)).to(DEV) * 0.8 + 0.1
+        refl = enh / (illu + 1e-6)
+        with torch.no_grad():
+            outs.append(crit(low, enh, illu, refl, epoch=2 if k == 2 else 1)[1])
+    hist = {key: [o[key] for o in outs[:2]] for key in crit.loss_history}
+    w = dwa_weights(hist, crit._weights)
+    w["smoothness"] = outs[2]["smooth_weight"]
+    want = sum(w[key] * outs[2][key] for key in w)
+    np.testing.assert_allclose(outs[2]["total"], want, rtol=1e-5)
+    assert len(crit.loss_history["exposure"]) == 3
+
+
 def _model(pre, aspp, seed=0):
     from models.model import UP_Retinex
     torch.manual_seed(seed)
@@ -285,3 +338,60 @@ def test_train_grads_variants_vs_oracle(pre, aspp):
         assert dev_l2 <= tol_l2, f"grad {n}: device rel-L2 {dev_l2:.3e} vs fp64 > {tol_l2:.3e} (fp32 CPU {cpu_l2:.3e})"
         tol = max(8.0 * cpu_err, floor_l2 * ref.abs().max().item(), 5e-3 * ref.abs().max().item()) + 1e-9
         assert dev_err <= tol, f"grad {n}: device |d| {dev_err:.3e} vs fp64 > {tol:.3e} (fp32 CPU |d| {cpu_err:.3e})"
+
+
+def _amp_setup(seed=0):
+    from losses.loss import TotalLoss
+    from trainers.train import make_optimizer
+    model = _model(False, False, seed=seed).to(DEV).train()
+    crit = TotalLoss(use_freq_loss=True).to(DEV)
+    opt = make_optimizer(model, lr=1e-4, weight_decay=1e-5)
+    return model, crit, opt
+
+
+def test_amp_gradscaler_step_equals_fp32_step():
+    """The AMP branch (train.py:71-89) with a power-of-two loss scale: scaling
+    commutes exactly with every rounding, so after unscale_ the gradients, the
+    clipped Adam update and the parameters equal the no-AMP step's."""
+    from trainers.train import GradScaler, train_step
+    x = (torch.rand(2, 3, 64, 64, generator=torch.Generator().manual_seed(11)) * 0.5).to(DEV)
+    m1, c1, o1 = _amp_setup()
+    train_step(m1, x, c1, o1)
+    m2, c2, o2 = _amp_setup()
+    scaler = GradScaler(init_scale=2.0 ** 16)
+    l2, d2 = train_step(m2, x, c2, o2, scaler=scaler, use_amp=True)
+    torch.cuda.synchronize()
+    assert scaler.get_scale() == 2.0 ** 16  # finite step, growth interval not reached
+    p1 = dict(m1.named_parameters())
+    for n, p in m2.named_parameters():
+        _close(p, p1[n], 1e-6, n)
+
+
+def test_amp_gradscaler_skips_nonfinite_step():
+    """An inf gradient: the step is skipped (parameters and Adam state
+    untouched), the scale backs off by 0.5, and the next finite step runs."""
+    from trainers.train import GradScaler, clip_grad_norm_
+    x = (torch.rand(2, 3, 64, 64, generator=torch.Generator().manual_seed(12)) * 0.5).to(DEV)
+    model, crit, opt = _amp_setup(seed=1)
+    scaler = GradScaler(init_scale=1024.0)
+    before = {n: p.detach().clone() for n, p in model.named_parameters()}
+    opt.zero_grad()
+    enh, refl, illu = model(x)
+    loss, _ = crit(x, enh, illu, refl)
+    scaler.scale(loss).backward()
+    next(iter(model.parameters())).grad.view(-1)[0] = float("inf")
+    scaler.unscale_(opt)
+    clip_grad_norm_(model.parameters(), 1.0)
+    scaler.step(opt)
+    scaler.update()
+    torch.cuda.synchronize()
+    assert scaler.get_scale() == 512.0
+    assert opt.step_count == 0
+    for n, p in model.named_parameters():
+        assert torch.equal(p.detach(), before[n]), n
+    from trainers.train import train_step
+    train_step(model, x, crit, opt, scaler=scaler, use_amp=True)
+    torch.cuda.synchronize()
+    assert opt.step_count == 1 and scaler.get_scale() == 512.0
+    moved = sum(int(not torch.equal(p.detach(), before[n])) for n, p in model.named_parameters())
+    assert moved > 0
