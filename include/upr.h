@@ -109,6 +109,18 @@ int upr_conv2d_nhwc(const void* x, int B, int H, int W, int Cin, const void* w, 
  * 256, NaN / |x*255| >= 2^31 -> 0.  n elements, any layout. */
 int upr_quantize_u8(const void* x, uint8_t* out, size_t n, int dtype, void* stream);
 
+/* letterbox / letterbox_tensor (utils/letterbox.py:9-102) of ONE image in one
+ * launch: src is u8 HWC RGB (src_kind 0) or float32 CHW in [0,1] (src_kind 1,
+ * quantised as (x*255).astype(uint8), letterbox.py:93); the H x W source is
+ * resized to nh x nw with cv2.resize INTER_LINEAR 8-bit fixed-point semantics
+ * (xtab [4][nw], ytab [4][nh] int32: source index 0 / 1, 11-bit weights 0 / 1,
+ * built on the host like OpenCV's tables; both NULL when nh == H, nw == W),
+ * placed at (top, left) of an Ho x Wo canvas filled with `color`
+ * (0xBBGGRR bytes: channel c = (color >> 8c) & 255); out is float32 CHW / 255
+ * (out_kind 0, what letterbox_tensor returns) or u8 HWC (out_kind 1). */
+int upr_letterbox(const void* src, int src_kind, int H, int W, int top, int left, int nh, int nw, int Ho, int Wo,
+                  const int32_t* xtab, const int32_t* ytab, int color, void* out, int out_kind, void* stream);
+
 /* cv2.cvtColor(..., COLOR_RGB2LAB) / (..., COLOR_LAB2RGB) on 8-bit interleaved
  * pixels (adaptive_params.py:142-145, :158-161 — the reference goes through
  * BGR, which is the same arithmetic). */

@@ -14,6 +14,8 @@ int launch_clahe_u8(const uint8_t* src, uint8_t* dst, uint8_t* lut, int B, int H
 int launch_rgb2lab(const uint8_t* rgb, uint8_t* lab, size_t npix, hipStream_t st);
 int launch_lab2rgb(const uint8_t* lab, uint8_t* rgb, size_t npix, hipStream_t st);
 int launch_quantize(const void* x, uint8_t* out, size_t n, int dtype, hipStream_t st);
+int launch_letterbox(const void* src, int src_kind, int H, int W, int top, int left, int nh, int nw, int Ho, int Wo,
+                     const int* xtab, const int* ytab, int color, void* out, int out_kind, hipStream_t st);
 int launch_gray_hist(const void* img, int* hist, int B, int H, int W, int dtype, hipStream_t st);
 int launch_multiscale(const void* x, const void* enh, void* out, double* sums, double* factor, int B, int H, int W,
                       int dtype, hipStream_t st);
@@ -33,6 +35,17 @@ int upr_quantize_u8(const void* x, uint8_t* out, size_t n, int dtype, void* stre
   if (!x || !out || !dtype_ok(dtype)) return UPR_ERR_ARG;
   if (n == 0) return UPR_OK;
   return launch_quantize(x, out, n, dtype, (hipStream_t)stream);
+}
+
+int upr_letterbox(const void* src, int src_kind, int H, int W, int top, int left, int nh, int nw, int Ho, int Wo,
+                  const int32_t* xtab, const int32_t* ytab, int color, void* out, int out_kind, void* stream) {
+  if (!src || !out || (src_kind != 0 && src_kind != 1) || (out_kind != 0 && out_kind != 1)) return UPR_ERR_ARG;
+  if (H <= 0 || W <= 0 || nh <= 0 || nw <= 0 || top < 0 || left < 0 || top + nh > Ho || left + nw > Wo)
+    return UPR_ERR_SHAPE;
+  if ((xtab == nullptr) != (ytab == nullptr)) return UPR_ERR_ARG;
+  if (!xtab && (nh != H || nw != W)) return UPR_ERR_SHAPE;
+  return launch_letterbox(src, src_kind, H, W, top, left, nh, nw, Ho, Wo, xtab, ytab, color, out, out_kind,
+                          (hipStream_t)stream);
 }
 
 int upr_rgb2lab_u8(const uint8_t* rgb, uint8_t* lab, size_t npix, void* stream) {

@@ -569,3 +569,64 @@ int launch_ms_features(const void* x, void* out, int B, int H, int W, int scale_
 }
 
 }  // namespace upr
+
+// ---------------------------------------------------------------------------
+// letterbox (utils/letterbox.py:9-102): quantise (float CHW source: the
+// reference's (x*255).astype(uint8)), cv2.resize INTER_LINEAR in OpenCV's
+// 8-bit fixed point (11-bit coefficients; horizontal pass in int, vertical as
+// VResizeLinearVec_32s8u: >>4, two >>16 products, (v+2)>>2), grey border, and
+// the output store (float CHW /255 or u8 HWC) -- one thread per output pixel.
+// xtab / ytab: [4][n] = source index 0, source index 1, weight 0, weight 1
+// (host-built, as OpenCV builds them); NULL when the unpadded size equals the
+// source size (no resize).
+// ---------------------------------------------------------------------------
+namespace upr {
+
+__device__ __forceinline__ int lb_src(const void* src, int kind, int H, int W, int y, int x, int c) {
+  if (kind == 0) return ((const uint8_t*)src)[((size_t)y * W + x) * 3 + c];
+  return quant_u8(((const float*)src)[((size_t)c * H + y) * W + x]);
+}
+
+__global__ __launch_bounds__(256) void letterbox_kernel(const void* __restrict__ src, int src_kind, int H, int W,
+                                                        int top, int left, int nh, int nw, int Ho, int Wo,
+                                                        const int* __restrict__ xtab, const int* __restrict__ ytab,
+                                                        int color, void* __restrict__ out, int out_kind) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= Ho * Wo) return;
+  const int y = p / Wo, x = p - y * Wo;
+  const int yy = y - top, xx = x - left;
+  const bool inside = yy >= 0 && yy < nh && xx >= 0 && xx < nw;
+  int v[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    if (!inside) {
+      v[c] = (color >> (8 * c)) & 255;
+    } else if (!xtab) {
+      v[c] = lb_src(src, src_kind, H, W, yy, xx, c);
+    } else {
+      const int x0 = xtab[xx], x1 = xtab[nw + xx], a0 = xtab[2 * nw + xx], a1 = xtab[3 * nw + xx];
+      const int y0 = ytab[yy], y1 = ytab[nh + yy], b0 = ytab[2 * nh + yy], b1 = ytab[3 * nh + yy];
+      const int r0 = (lb_src(src, src_kind, H, W, y0, x0, c) * a0 + lb_src(src, src_kind, H, W, y0, x1, c) * a1) >> 4;
+      const int r1 = (lb_src(src, src_kind, H, W, y1, x0, c) * a0 + lb_src(src, src_kind, H, W, y1, x1, c) * a1) >> 4;
+      const int s = ((r0 * b0) >> 16) + ((r1 * b1) >> 16);
+      v[c] = sat_u8((s + 2) >> 2);
+    }
+  }
+  if (out_kind == 0) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) ((float*)out)[(size_t)c * Ho * Wo + p] = (float)v[c] / 255.f;
+  } else {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) ((uint8_t*)out)[(size_t)p * 3 + c] = (uint8_t)v[c];
+  }
+}
+
+int launch_letterbox(const void* src, int src_kind, int H, int W, int top, int left, int nh, int nw, int Ho, int Wo,
+                     const int* xtab, const int* ytab, int color, void* out, int out_kind, hipStream_t st) {
+  const int n = Ho * Wo;
+  hipLaunchKernelGGL(letterbox_kernel, dim3((n + 255) / 256), dim3(256), 0, st, src, src_kind, H, W, top, left, nh,
+                     nw, Ho, Wo, xtab, ytab, color, out, out_kind);
+  return (int)hipGetLastError();
+}
+
+}  // namespace upr

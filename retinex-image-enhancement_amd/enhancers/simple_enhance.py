@@ -19,24 +19,23 @@ from models.model import UP_Retinex
 from enhancers.adaptive_params import AdaptiveParameterAdjuster
 from enhancers.multi_scale import MultiScaleEnhancer
 from enhancers.content_aware import ContentAwareEnhancer
-from utils.letterbox import letterbox_tensor
+from utils.letterbox import letterbox_u8_image
 
 VALID_EXTENSIONS = {'.jpg', '.jpeg', '.png', '.bmp', '.tif', '.tiff'}
 
 
-def _to_tensor(img):
-    """torchvision ToTensor for an RGB PIL image: uint8 HWC -> float32 CHW / 255."""
-    a = np.asarray(img, dtype=np.uint8)
-    return torch.from_numpy(np.ascontiguousarray(a.transpose(2, 0, 1))).float().div(255)
+def load_image(image_path, max_size=None, device=None):
+    """Decode + letterbox (reference :23-62) -> ([1,3,H,W] float32, (W, H)).
 
-
-def load_image(image_path, max_size=None):
-    """Decode, letterbox (reference :23-62) -> ([1,3,H,W] float32, (W, H))."""
+    The decoded uint8 pixels go to the ROCm device as bytes and ToTensor +
+    letterbox_tensor run there as one launch (utils/letterbox.py); the tensor is
+    returned on that device (the reference returns it on the CPU and the caller
+    moves it -- the callers' .to(device) is then a no-op)."""
     img = Image.open(image_path).convert('RGB')
     original_size = img.size
-    t = _to_tensor(img)
-    new_shape = max_size if max_size is not None else tuple(t.shape[1:])
-    t, _, _ = letterbox_tensor(t, new_shape=new_shape, auto=True, scaleup=False)
+    a = np.asarray(img, dtype=np.uint8)
+    new_shape = max_size if max_size is not None else a.shape[:2]
+    t, _, _ = letterbox_u8_image(a, new_shape=new_shape, auto=True, scaleup=False, device=device)
     return t.unsqueeze(0), original_size
 
 

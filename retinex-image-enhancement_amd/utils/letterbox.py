@@ -1,34 +1,34 @@
-"""YOLO-style letterbox (drop-in for reference utils/letterbox.py).
+"""YOLO-style letterbox (drop-in for reference utils/letterbox.py:9-102).
 
-Host-side preprocessing of the enhance harness.  With the reference's default
-call (new_shape = the image's own size, scaleup=False) it is the uint8 round
-trip x -> (x*255).astype(uint8) -> /255, exact for 8-bit inputs.  With
---max_size it resizes with OpenCV INTER_LINEAR semantics (8-bit fixed point:
-11-bit coefficients; vertical pass as OpenCV's SSE2 path computes it) and pads
-with grey 114 to a multiple of 32.  cv2 is not available in this environment:
-the resize restatement is "parity unpinned" (see DESIGN.md).
+The geometry (scale ratio, unpadded size, border split) is host scalar math as
+in the reference; the pixels -- the (x*255).astype(uint8) quantisation of
+letterbox_tensor, cv2.resize INTER_LINEAR in OpenCV's 8-bit fixed point
+(11-bit coefficients, tables built here on the host as OpenCV builds them),
+the grey-114 border and the /255 -- are ONE device launch (upr_letterbox).
+With the harness's default call (new_shape = the image's own size,
+scaleup=False) it is the uint8 round trip, exact for 8-bit inputs.
+
+Device only, like every other op of this package: a CPU tensor is moved to the
+current ROCm device and the result is returned on the input's device (the
+reference returns CPU tensors; the harness moves them to the device next).
+cv2 is absent here, so the resize arithmetic is "parity unpinned" (DESIGN.md);
+its CPU restatement is oracle/letterbox.py (test infrastructure).
 """
 import math
 
 import numpy as np
 import torch
 
-_COEF_BITS = 11
-_COEF_SCALE = 1 << _COEF_BITS
+from upr import _lib as L
+
+_COEF_SCALE = 1 << 11
 
 
-def _round(v):
-    # cvRound on float: round half to even
-    return int(np.rint(v))
-
-
-def _linear_taps(dst, src):
-    """OpenCV resize INTER_LINEAR source index / fixed-point weights along one axis."""
+def linear_taps(dst, src):
+    """OpenCV resize INTER_LINEAR source indices / 11-bit weights along one axis
+    -> int32 [4][dst] (index 0, index 1, weight 0, weight 1)."""
     scale = src / dst
-    idx0 = np.zeros(dst, np.int64)
-    idx1 = np.zeros(dst, np.int64)
-    w0 = np.zeros(dst, np.int64)
-    w1 = np.zeros(dst, np.int64)
+    t = np.zeros((4, dst), np.int32)
     for d in range(dst):
         f = np.float32((d + 0.5) * scale - 0.5)
         s = int(math.floor(f))
@@ -37,30 +37,15 @@ def _linear_taps(dst, src):
             f, s = np.float32(0), 0
         if s >= src - 1:
             f, s = np.float32(0), src - 1
-        idx0[d] = s
-        idx1[d] = min(s + 1, src - 1)
-        w0[d] = _round(np.float32(np.float32(1) - f) * np.float32(_COEF_SCALE))
-        w1[d] = _round(f * np.float32(_COEF_SCALE))
-    return idx0, idx1, w0, w1
+        t[0, d] = s
+        t[1, d] = min(s + 1, src - 1)
+        t[2, d] = int(np.rint(np.float32(np.float32(1) - f) * np.float32(_COEF_SCALE)))
+        t[3, d] = int(np.rint(f * np.float32(_COEF_SCALE)))
+    return t
 
 
-def resize_linear_u8(img, new_wh):
-    """cv2.resize(img, (W', H'), interpolation=INTER_LINEAR) for uint8 HWC."""
-    img = np.asarray(img, np.uint8)
-    H, W = img.shape[:2]
-    nw, nh = new_wh
-    x0, x1, a0, a1 = _linear_taps(nw, W)
-    y0, y1, b0, b1 = _linear_taps(nh, H)
-    s = img.astype(np.int64)
-    rows = s[:, x0] * a0[None, :, None] + s[:, x1] * a1[None, :, None]      # horizontal pass (int)
-    r0, r1 = rows[y0] >> 4, rows[y1] >> 4                                    # VResizeLinearVec_32s8u
-    v = ((r0 * b0[:, None, None]) >> 16) + ((r1 * b1[:, None, None]) >> 16)
-    return np.clip((v + 2) >> 2, 0, 255).astype(np.uint8)
-
-
-def letterbox(img, new_shape=640, color=(114, 114, 114), auto=True, scale_fill=False, scaleup=True):
-    """Reference utils/letterbox.py:9-62 on a uint8 HWC array."""
-    shape = img.shape[:2]
+def letterbox_geometry(shape, new_shape=640, auto=True, scale_fill=False, scaleup=True):
+    """Reference letterbox.py:21-52 -> (new_unpad (w, h), ratio, (dw, dh), (top, bottom, left, right))."""
     if isinstance(new_shape, int):
         new_shape = (new_shape, new_shape)
     r = min(new_shape[0] / shape[0], new_shape[1] / shape[1])
@@ -77,23 +62,68 @@ def letterbox(img, new_shape=640, color=(114, 114, 114), auto=True, scale_fill=F
         ratio = new_shape[1] / shape[1], new_shape[0] / shape[0]
     dw /= 2
     dh /= 2
-    if shape[::-1] != new_unpad:
-        img = resize_linear_u8(img, new_unpad)
-    top, bottom = int(round(dh - 0.1)), int(round(dh + 0.1))
-    left, right = int(round(dw - 0.1)), int(round(dw + 0.1))
-    if top or bottom or left or right:
-        out = np.empty((img.shape[0] + top + bottom, img.shape[1] + left + right) + img.shape[2:], np.uint8)
-        out[...] = np.asarray(color, np.uint8)[: img.shape[2]] if img.ndim == 3 else color[0]
-        out[top:top + img.shape[0], left:left + img.shape[1]] = img
-        img = out
-    return img, ratio, (dw, dh)
+    border = (int(round(dh - 0.1)), int(round(dh + 0.1)), int(round(dw - 0.1)), int(round(dw + 0.1)))
+    return new_unpad, ratio, (dw, dh), border
+
+
+def _device(t):
+    if not torch.cuda.is_available():
+        raise RuntimeError("letterbox runs on ROCm devices only (no CPU fallback)")
+    return t.device if t.device.type == "cuda" else torch.device("cuda", torch.cuda.current_device())
+
+
+def _run(src, src_kind, H, W, new_shape, color, auto, scale_fill, scaleup, out_kind):
+    (nw, nh), ratio, pad, (top, bottom, left, right) = letterbox_geometry((H, W), new_shape, auto, scale_fill,
+                                                                          scaleup)
+    Ho, Wo = nh + top + bottom, nw + left + right
+    dev = src.device
+    xt = yt = None
+    if (nw, nh) != (W, H):
+        xt = torch.from_numpy(linear_taps(nw, W)).to(dev)
+        yt = torch.from_numpy(linear_taps(nh, H)).to(dev)
+    if out_kind == 0:
+        out = torch.empty((3, Ho, Wo), dtype=torch.float32, device=dev)
+    else:
+        out = torch.empty((Ho, Wo, 3), dtype=torch.uint8, device=dev)
+    col = int(color[0]) | (int(color[1]) << 8) | (int(color[2]) << 16)
+    with torch.cuda.device(dev):
+        rc = L.lib().upr_letterbox(src.data_ptr(), src_kind, H, W, top, left, nh, nw, Ho, Wo,
+                                   xt.data_ptr() if xt is not None else None,
+                                   yt.data_ptr() if yt is not None else None, col, out.data_ptr(), out_kind,
+                                   torch.cuda.current_stream(dev).cuda_stream)
+    L.check(rc, "upr_letterbox")
+    return out, ratio, pad
+
+
+def letterbox(img, new_shape=640, color=(114, 114, 114), auto=True, scale_fill=False, scaleup=True):
+    """Reference letterbox.py:9-62: uint8 HWC RGB array (numpy, or a uint8
+    tensor) -> (letterboxed uint8 HWC, ratio, (dw, dh)); numpy in, numpy out."""
+    as_numpy = isinstance(img, np.ndarray)
+    t = torch.from_numpy(np.ascontiguousarray(img)) if as_numpy else img
+    if t.dtype != torch.uint8 or t.dim() != 3 or t.shape[2] != 3:
+        raise ValueError("letterbox expects a uint8 H x W x 3 image")
+    t = t.to(_device(t)).contiguous()
+    out, ratio, pad = _run(t, 0, t.shape[0], t.shape[1], new_shape, color, auto, scale_fill, scaleup, 1)
+    return (out.cpu().numpy() if as_numpy else out), ratio, pad
 
 
 def letterbox_tensor(img_tensor, new_shape=640, color=(114, 114, 114), auto=True, scale_fill=False, scaleup=True):
-    """Reference utils/letterbox.py:65-102: [C,H,W] float in [0,1] -> letterboxed [C,H',W'] float."""
-    img_np = img_tensor.detach().cpu().numpy()
-    img_np = np.transpose(img_np, (1, 2, 0))
-    img_np = (img_np * 255).astype(np.uint8)
-    img_lb, ratio, pad = letterbox(img_np, new_shape, color, auto, scale_fill, scaleup)
-    img_lb = img_lb.astype(np.float32) / 255.0
-    return torch.from_numpy(np.ascontiguousarray(np.transpose(img_lb, (2, 0, 1)))), ratio, pad
+    """Reference letterbox.py:65-102: [3,H,W] float in [0,1] -> letterboxed
+    [3,H',W'] float (the (x*255).astype(uint8) quantisation included)."""
+    if img_tensor.dim() != 3 or img_tensor.shape[0] != 3:
+        raise ValueError("letterbox_tensor expects a [3, H, W] tensor")
+    dev = _device(img_tensor)
+    t = img_tensor.detach().to(dev, torch.float32).contiguous()
+    return _run(t, 1, t.shape[1], t.shape[2], new_shape, color, auto, scale_fill, scaleup, 0)
+
+
+def letterbox_u8_image(img_u8_hwc, new_shape, color=(114, 114, 114), auto=True, scale_fill=False, scaleup=False,
+                       device=None):
+    """Harness fast path: a decoded uint8 HWC image goes to the device as bytes
+    (3 B/pixel over PCIe, not 12) and comes back as the letterboxed [3,H',W']
+    float tensor -- ToTensor + letterbox_tensor in one launch (bit-identical:
+    (k/255)*255 quantises back to k)."""
+    t = torch.from_numpy(np.ascontiguousarray(img_u8_hwc))
+    dev = device if device is not None else _device(t)
+    t = t.to(dev)
+    return _run(t, 0, t.shape[0], t.shape[1], new_shape, color, auto, scale_fill, scaleup, 0)

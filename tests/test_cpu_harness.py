@@ -1,20 +1,26 @@
-"""Host-side harness pieces that run without a device: letterbox geometry and
-uint8 round trip (reference utils/letterbox.py:9-102), image IO helpers, CLI
-argument surface."""
+"""Host-side harness pieces that run without a device: the letterbox geometry
+(reference utils/letterbox.py:9-62) and its CPU restatement oracle/letterbox.py
+(the checker of the device kernel, tests/test_gpu_enhancers.py), image IO
+helpers, CLI argument surface."""
 import numpy as np
 import torch
 from PIL import Image
 
-from utils.letterbox import letterbox, letterbox_tensor, resize_linear_u8
+from oracle.letterbox import letterbox, linear_taps as oracle_taps, resize_linear_u8
+from utils.letterbox import letterbox_geometry, linear_taps
 
 
-def test_letterbox_identity_roundtrip_is_exact():
-    rng = np.random.default_rng(0)
-    a = rng.integers(0, 256, (48, 80, 3)).astype(np.uint8)
-    t = torch.from_numpy(a.transpose(2, 0, 1).copy()).float().div(255)
-    out, ratio, pad = letterbox_tensor(t, new_shape=tuple(t.shape[1:]), auto=True, scaleup=False)
-    assert ratio == (1.0, 1.0) and pad == (0.0, 0.0)
-    assert torch.equal(out, t)
+def test_letterbox_geometry_identity():
+    unpad, ratio, pad, border = letterbox_geometry((48, 80), (48, 80), auto=True, scaleup=False)
+    assert unpad == (80, 48) and ratio == (1.0, 1.0) and pad == (0.0, 0.0) and border == (0, 0, 0, 0)
+
+
+def test_product_taps_match_oracle_taps():
+    for dst, src in ((85, 200), (128, 300), (60, 30), (13, 30), (30, 30)):
+        t = linear_taps(dst, src)
+        o = oracle_taps(dst, src)
+        for i in range(4):
+            np.testing.assert_array_equal(t[i], o[i])
 
 
 def test_letterbox_pad_geometry():
@@ -45,17 +51,22 @@ def test_resize_linear_properties():
 
 
 def test_save_and_compare(tmp_path):
-    from enhancers.simple_enhance import save_image, create_comparison, load_image
+    from enhancers.simple_enhance import save_image, create_comparison
     x = torch.rand(1, 3, 16, 24)
     save_image(x, str(tmp_path / "a.png"))
     save_image(x[:, :1], str(tmp_path / "b.png"))
     create_comparison(x, x, str(tmp_path / "c.png"))
     assert np.asarray(Image.open(tmp_path / "b.png")).shape == (16, 24, 3)
     assert np.asarray(Image.open(tmp_path / "c.png")).shape == (16, 48, 3)
-    img, size = load_image(str(tmp_path / "a.png"))
-    assert img.shape == (1, 3, 16, 24) and size == (24, 16)
-    expect = torch.from_numpy(np.asarray(Image.open(tmp_path / "a.png")).transpose(2, 0, 1).copy()).float() / 255
-    assert torch.equal(img[0], expect)
+
+
+def test_letterbox_refuses_without_device():
+    import pytest
+    from utils.letterbox import letterbox_tensor
+    if torch.cuda.is_available():
+        pytest.skip("a ROCm device is present")
+    with pytest.raises(RuntimeError, match="ROCm"):
+        letterbox_tensor(torch.rand(3, 8, 8), new_shape=(8, 8))
 
 
 def test_cli_surface():

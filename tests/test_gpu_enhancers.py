@@ -121,3 +121,51 @@ def test_main_cli_single_file(tmp_path, golden):
     cli.main(["--mode", "enhance", "--input_path", str(p), "--output_dir", str(tmp_path / "o2"), "--seed", "0",
               "--device", DEV, "--multi_scale", "--precision", "fp16"])
     assert (tmp_path / "o2" / "img_enhanced.png").exists()
+
+
+@pytest.mark.parametrize("shape,new_shape,scaleup", [
+    ((48, 80), (48, 80), False),     # harness default: identity (u8 round trip)
+    ((37, 53), 64, False),           # pad only (grey 114 border, odd split)
+    ((300, 200), 128, False),        # downscale + pad
+    ((40, 30), 96, True),            # upscale
+    ((257, 131), 160, False),        # odd sizes
+])
+def test_letterbox_device_matches_oracle(shape, new_shape, scaleup):
+    """upr_letterbox vs oracle/letterbox.py (OpenCV INTER_LINEAR 8-bit fixed
+    point restated; cv2 absent, parity unpinned): bit-exact uint8, and the
+    float path equal to the oracle's uint8 / 255."""
+    from oracle import letterbox as olb
+    from utils.letterbox import letterbox, letterbox_tensor, letterbox_u8_image
+    rng = np.random.default_rng(sum(shape))
+    a = rng.integers(0, 256, shape + (3,)).astype(np.uint8)
+    want, r_o, p_o = olb.letterbox(a, new_shape, auto=True, scaleup=scaleup)
+    got, r, p = letterbox(a, new_shape, auto=True, scaleup=scaleup)
+    assert (r, p) == (r_o, p_o)
+    np.testing.assert_array_equal(got, want)
+    # float [3,H,W] input: the reference's (x*255).astype(uint8) first
+    t = torch.from_numpy(a.transpose(2, 0, 1).copy()).float().div(255)
+    out, _, _ = letterbox_tensor(t.to(DEV), new_shape, auto=True, scaleup=scaleup)
+    ref = torch.from_numpy(want.astype(np.float32) / 255.0).permute(2, 0, 1)
+    assert torch.equal(out.cpu(), ref)
+    out8, _, _ = letterbox_u8_image(a, new_shape, auto=True, scaleup=scaleup)
+    assert torch.equal(out8.cpu(), ref)
+
+
+def test_letterbox_quantisation_wraps_like_numpy():
+    """letterbox_tensor quantises as numpy's astype(uint8) on x*255: truncation
+    and wrap mod 256 (1.2 -> 50, -0.1 -> 231)."""
+    from utils.letterbox import letterbox_tensor
+    x = torch.tensor([0.0, 1.0, 1.2, -0.1, 0.5, 0.999]).repeat(3, 4, 1)  # [3, 4, 6]
+    out, _, _ = letterbox_tensor(x.to(DEV), new_shape=(4, 6), auto=True, scaleup=False)
+    q = ((x.numpy() * np.float32(255)).astype(np.int64) % 256).astype(np.float32) / 255.0
+    assert torch.equal(out.cpu(), torch.from_numpy(q))
+
+
+def test_load_image_on_device(tmp_path):
+    from enhancers.simple_enhance import load_image, save_image
+    x = torch.rand(1, 3, 16, 24)
+    save_image(x, str(tmp_path / "a.png"))
+    img, size = load_image(str(tmp_path / "a.png"))
+    assert img.is_cuda and img.shape == (1, 3, 16, 24) and size == (24, 16)
+    expect = torch.from_numpy(np.asarray(Image.open(tmp_path / "a.png")).transpose(2, 0, 1).copy()).float() / 255
+    assert torch.equal(img[0].cpu(), expect)
