@@ -249,8 +249,13 @@ __device__ __forceinline__ void wide_epilogue(const ConvOp& op, f32x4_w (&acc)[W
   }
 }
 
-template <int BN, bool PIPE>
-__global__ __launch_bounds__(512) void conv_wide_kernel(ConvOp op) {
+// MINW: minimum waves per SIMD (HIP's second launch-bounds argument); 4 = two
+// 512-thread blocks per CU
+// (MINW 4 also selects ONE LDS stage: load -> compute per step, the other
+// block on the CU overlapping)
+template <int BN, bool PIPE, int MINW = 2>
+__global__ __launch_bounds__(512, MINW) void conv_wide_kernel(ConvOp op) {
+  constexpr bool ONE = MINW >= 4;
   using C = WideCfg<BN>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
@@ -332,8 +337,8 @@ __global__ __launch_bounds__(512) void conv_wide_kernel(ConvOp op) {
       // barrier) and every wave is done reading the other stage (step-1)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (step + 1 < total_steps) issue((step + 1) & 1);
-      const half_t* As = (const half_t*)(smem + (step & 1) * C::STAGE);
+      if (!ONE && step + 1 < total_steps) issue((step + 1) & 1);
+      const half_t* As = (const half_t*)(smem + (ONE ? 0 : (step & 1)) * C::STAGE);
       const half_t* Bs = As + C::A_BYTES / 2;
   #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
@@ -348,6 +353,10 @@ __global__ __launch_bounds__(512) void conv_wide_kernel(ConvOp op) {
           for (int b = 0; b < C::WN; ++b)
             acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf[b], acc[a][b], 0, 0, 0);
         }
+      }
+      if (ONE && step + 1 < total_steps) {
+        __syncthreads();  // every wave is done reading the single stage
+        issue(0);
       }
     }
   } else {
@@ -446,12 +455,50 @@ static int wide_kind() {
   return k;
 }
 
+static int launch_wide_onestep128(const ConvOp& op, hipStream_t st);
+
+// Routing of the 128-wide single-stage two-blocks-per-CU variant (measured,
+// fp16 preact+ASPP bs 32: it beats the one-block double-buffered kernel on
+// every 128-wide GEMM of the graph -- enc2.conv1 0.184 -> 0.160 ms, enc2.conv2
+// 0.255 -> 0.204, dec1.up 0.369 -> 0.258 -- and, as 128-wide halves, on the
+// 2-step 256-wide dec2.up 0.178 -> 0.157; 4-step 256-wide GEMMs break even).
+// UPR_WIDE_ONESTEP = max K steps for 128-wide GEMMs (0 = never; A/B timing),
+// UPR_WIDE_SPLIT256 = max K steps for splitting 256-wide GEMMs.
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+static int onestep_max() {
+  static const int v = env_int("UPR_WIDE_ONESTEP", 1 << 30);
+  return v;
+}
+static int split256_max() {
+  static const int v = env_int("UPR_WIDE_SPLIT256", 2);
+  return v;
+}
+
 template <int BN>
 static int launch_wide_any(const ConvOp& op, hipStream_t st) {
   int steps = 0;
   for (int s = 0; s < op.nseg; ++s) steps += op.seg[s].kh * op.seg[s].kw * (op.seg[s].C / WBK);
+  if (steps <= (BN == 128 ? onestep_max() : split256_max())) return launch_wide_onestep128(op, st);
   if (steps < 2) return launch_wide_bn<BN, false>(op, st);
   return wide_kind() == 0 ? launch_wide_bn<BN, false>(op, st) : launch_wide_bn<BN, true>(op, st);
+}
+
+// One-step GEMMs (K = 64: the dec1 ConvTranspose) are latency-bound at one
+// block per CU (load -> MFMA -> epilogue, nothing to overlap): with one LDS
+// stage and <= 128 VGPRs two blocks share a CU and one's epilogue hides the
+// other's operand fetch (dec1.up 0.369 -> 0.258 ms).  128-wide tiles only (a
+// 256-wide tile needs 128 accumulator registers per lane on its own).
+static int launch_wide_onestep128(const ConvOp& op, hipStream_t st) {
+  using C = WideCfg<128>;
+  constexpr int EPI = 64 * (128 + 4) * 4;
+  constexpr int LDS1 = C::STAGE > EPI ? C::STAGE : EPI;
+  const int M = op.B * op.Ho * op.Wo;
+  const int grid = ((M + WBM - 1) / WBM) * (op.N / 128);
+  hipLaunchKernelGGL((conv_wide_kernel<128, false, 4>), dim3(grid), dim3(512), LDS1, st, op);
+  return (int)hipGetLastError();
 }
 
 // UPR_CONV_WIDE=0 disables this path (A/B timing against conv_halo / conv_igemm)
