@@ -121,6 +121,11 @@ int upr_quantize_u8(const void* x, uint8_t* out, size_t n, int dtype, void* stre
 int upr_letterbox(const void* src, int src_kind, int H, int W, int top, int left, int nh, int nw, int Ho, int Wo,
                   const int32_t* xtab, const int32_t* ytab, int color, void* out, int out_kind, void* stream);
 
+/* save_image's pixels (enhancers/simple_enhance.py:65-99): one image x [C,H,W]
+ * (C = 3, or 1 = replicated to RGB) -> u8 HWC RGB as
+ * (np.clip(x, 0, 1) * 255).astype(np.uint8). */
+int upr_to_u8_hwc(const void* x, int C, int H, int W, int dtype, uint8_t* out, void* stream);
+
 /* cv2.cvtColor(..., COLOR_RGB2LAB) / (..., COLOR_LAB2RGB) on 8-bit interleaved
  * pixels (adaptive_params.py:142-145, :158-161 — the reference goes through
  * BGR, which is the same arithmetic). */

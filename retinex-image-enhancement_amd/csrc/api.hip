@@ -14,6 +14,7 @@ int launch_clahe_u8(const uint8_t* src, uint8_t* dst, uint8_t* lut, int B, int H
 int launch_rgb2lab(const uint8_t* rgb, uint8_t* lab, size_t npix, hipStream_t st);
 int launch_lab2rgb(const uint8_t* lab, uint8_t* rgb, size_t npix, hipStream_t st);
 int launch_quantize(const void* x, uint8_t* out, size_t n, int dtype, hipStream_t st);
+int launch_to_u8_hwc(const void* x, int C, int H, int W, int dtype, uint8_t* out, hipStream_t st);
 int launch_letterbox(const void* src, int src_kind, int H, int W, int top, int left, int nh, int nw, int Ho, int Wo,
                      const int* xtab, const int* ytab, int color, void* out, int out_kind, hipStream_t st);
 int launch_gray_hist(const void* img, int* hist, int B, int H, int W, int dtype, hipStream_t st);
@@ -46,6 +47,12 @@ int upr_letterbox(const void* src, int src_kind, int H, int W, int top, int left
   if (!xtab && (nh != H || nw != W)) return UPR_ERR_SHAPE;
   return launch_letterbox(src, src_kind, H, W, top, left, nh, nw, Ho, Wo, xtab, ytab, color, out, out_kind,
                           (hipStream_t)stream);
+}
+
+int upr_to_u8_hwc(const void* x, int C, int H, int W, int dtype, uint8_t* out, void* stream) {
+  if (!x || !out || !dtype_ok(dtype) || (C != 1 && C != 3)) return UPR_ERR_ARG;
+  if (H <= 0 || W <= 0) return UPR_ERR_SHAPE;
+  return launch_to_u8_hwc(x, C, H, W, dtype, out, (hipStream_t)stream);
 }
 
 int upr_rgb2lab_u8(const uint8_t* rgb, uint8_t* lab, size_t npix, void* stream) {

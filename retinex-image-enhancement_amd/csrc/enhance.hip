@@ -630,3 +630,35 @@ int launch_letterbox(const void* src, int src_kind, int H, int W, int top, int l
 }
 
 }  // namespace upr
+
+// ---------------------------------------------------------------------------
+// save_image / create_comparison pixels (enhancers/simple_enhance.py:65-132):
+// np.clip(x, 0, 1) then (x*255).astype(np.uint8), CHW -> HWC, a 1-channel map
+// replicated to RGB.  NaN -> 0 (clip keeps NaN, the cast maps it to 0; here
+// the clamp already yields 0 -- same byte).
+// ---------------------------------------------------------------------------
+namespace upr {
+
+template <typename T>
+__global__ __launch_bounds__(256) void to_u8_hwc_kernel(const T* __restrict__ x, int C, size_t HW,
+                                                        uint8_t* __restrict__ out) {
+  const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= HW) return;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float v = ldf(x, (size_t)(C == 1 ? 0 : c) * HW + p);
+    out[p * 3 + c] = (uint8_t)quant_u8(fminf(fmaxf(v, 0.f), 1.f));
+  }
+}
+
+int launch_to_u8_hwc(const void* x, int C, int H, int W, int dtype, uint8_t* out, hipStream_t st) {
+  const size_t HW = (size_t)H * W;
+  const int grid = (int)((HW + 255) / 256);
+  if (dtype == kF16)
+    hipLaunchKernelGGL((to_u8_hwc_kernel<half_t>), dim3(grid), dim3(256), 0, st, (const half_t*)x, C, HW, out);
+  else
+    hipLaunchKernelGGL((to_u8_hwc_kernel<float>), dim3(grid), dim3(256), 0, st, (const float*)x, C, HW, out);
+  return (int)hipGetLastError();
+}
+
+}  // namespace upr

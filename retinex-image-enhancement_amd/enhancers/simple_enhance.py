@@ -40,13 +40,11 @@ def load_image(image_path, max_size=None, device=None):
 
 
 def _to_u8_hwc(t):
-    a = t.detach().float().cpu().numpy()
-    if a.shape[0] == 1:
-        a = np.clip(a[0], 0, 1)
-        a = (a * 255).astype(np.uint8)
-        return np.stack([a, a, a], axis=2)
-    a = np.clip(np.transpose(a, (1, 2, 0)), 0, 1)
-    return (a * 255).astype(np.uint8)
+    """(np.clip(x, 0, 1) * 255).astype(np.uint8) of one [C,H,W] image, 1-channel
+    maps replicated to RGB (reference :65-99): one device launch, then the
+    3 B/pixel copy to the host for the PNG encoder."""
+    from upr import runtime
+    return runtime.to_u8_hwc(t.detach()).cpu().numpy()
 
 
 def save_image(tensor, save_path):

@@ -59,6 +59,7 @@ SIGNATURES = {
     "upr_quantize_u8": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
     "upr_letterbox": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
                               c_void_p, c_int, c_void_p, c_int, c_void_p]),
+    "upr_to_u8_hwc": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "upr_rgb2lab_u8": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "upr_lab2rgb_u8": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "upr_clahe_u8": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_int, c_int, c_void_p]),

@@ -194,6 +194,18 @@ def quantize_u8(x):
     return out
 
 
+def to_u8_hwc(x):
+    """save_image pixels: one [C,H,W] image (C 1 or 3) -> u8 [H,W,3] on the device."""
+    _require_device(x)
+    x = x.contiguous()
+    C, H, W = x.shape
+    out = torch.empty((H, W, 3), dtype=torch.uint8, device=x.device)
+    with torch.cuda.device(x.device):
+        rc = L.lib().upr_to_u8_hwc(_ptr(x), C, H, W, dtype_code(x.dtype), _ptr(out), _stream(x.device))
+    L.check(rc, "upr_to_u8_hwc")
+    return out
+
+
 def rgb2lab_u8(rgb):
     """rgb: [..., 3] uint8 interleaved."""
     _require_device(rgb)

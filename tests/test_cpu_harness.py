@@ -50,16 +50,6 @@ def test_resize_linear_properties():
     assert up.min() >= a.min() and up.max() <= a.max()                # convex combination
 
 
-def test_save_and_compare(tmp_path):
-    from enhancers.simple_enhance import save_image, create_comparison
-    x = torch.rand(1, 3, 16, 24)
-    save_image(x, str(tmp_path / "a.png"))
-    save_image(x[:, :1], str(tmp_path / "b.png"))
-    create_comparison(x, x, str(tmp_path / "c.png"))
-    assert np.asarray(Image.open(tmp_path / "b.png")).shape == (16, 24, 3)
-    assert np.asarray(Image.open(tmp_path / "c.png")).shape == (16, 48, 3)
-
-
 def test_letterbox_refuses_without_device():
     import pytest
     from utils.letterbox import letterbox_tensor

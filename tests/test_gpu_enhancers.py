@@ -169,3 +169,28 @@ def test_load_image_on_device(tmp_path):
     assert img.is_cuda and img.shape == (1, 3, 16, 24) and size == (24, 16)
     expect = torch.from_numpy(np.asarray(Image.open(tmp_path / "a.png")).transpose(2, 0, 1).copy()).float() / 255
     assert torch.equal(img[0].cpu(), expect)
+
+
+def test_save_image_pixels_match_numpy(tmp_path):
+    """save_image / create_comparison write (np.clip(x,0,1)*255).astype(uint8)
+    (reference simple_enhance.py:65-132), computed on the device, 1-channel
+    maps replicated; out-of-range and NaN inputs included."""
+    from enhancers.simple_enhance import save_image, create_comparison
+    x = torch.rand(1, 3, 16, 24) * 1.4 - 0.2
+    x[0, 0, 0, 0] = float("nan")
+    xd = x.to(DEV)
+    save_image(xd, str(tmp_path / "a.png"))
+    save_image(xd[:, :1], str(tmp_path / "b.png"))
+    create_comparison(xd, xd.flip(-1), str(tmp_path / "c.png"))
+
+    def ref(t):
+        a = np.clip(t.numpy(), 0, 1)
+        with np.errstate(invalid="ignore"):
+            return (np.nan_to_num(a * np.float32(255), nan=0.0)).astype(np.uint8).transpose(1, 2, 0)
+
+    a = ref(x[0])
+    np.testing.assert_array_equal(np.asarray(Image.open(tmp_path / "a.png")), a)
+    b1 = ref(x[0, :1])
+    np.testing.assert_array_equal(np.asarray(Image.open(tmp_path / "b.png")), np.repeat(b1, 3, axis=2))
+    c = np.concatenate([a, ref(x[0].flip(-1))], axis=1)
+    np.testing.assert_array_equal(np.asarray(Image.open(tmp_path / "c.png")), c)
