@@ -319,7 +319,7 @@ __global__ __launch_bounds__(256) void conv3_mfma_kernel(const half_t* __restric
                                                          const float* __restrict__ bias, half_t* __restrict__ out0,
                                                          half_t* __restrict__ out1, half_t* __restrict__ out2,
                                                          const float* __restrict__ ps, const float* __restrict__ ph,
-                                                         int h, int wd, int tiles_x, int tiles_y) {
+                                                         int h, int wd, int tiles_x, int tiles_y, int nimg) {
   typedef _Float16 h8 __attribute__((ext_vector_type(8)));
   typedef _Float16 h4 __attribute__((ext_vector_type(4)));
   typedef float f4 __attribute__((ext_vector_type(4)));
@@ -327,15 +327,31 @@ __global__ __launch_bounds__(256) void conv3_mfma_kernel(const half_t* __restric
   __shared__ half_t reg[3 * RP];
   __shared__ __attribute__((aligned(16))) half_t tr[4][3][16 * 32];  // per-wave 16-pixel transpose, <= 3 outputs
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fg = lane >> 4;
-  const int tx = blockIdx.x % tiles_x, ty = (blockIdx.x / tiles_x) % tiles_y, b = blockIdx.x / (tiles_x * tiles_y);
-  const int oy0 = ty * 8, ox0 = tx * 32;
   const size_t HW = (size_t)h * wd;
-  for (int e = tid; e < 3 * RP; e += 256) {
-    const int c = e / RP, r = e - c * RP, hy = r / RW, hx = r - hy * RW;
-    const int iy = oy0 - 1 + hy, ix = ox0 - 1 + hx;
-    reg[e] = ((unsigned)iy < (unsigned)h && (unsigned)ix < (unsigned)wd) ? x[((size_t)b * 3 + c) * HW + (size_t)iy * wd + ix]
-                                                                         : (half_t)0.f;
-  }
+  const int ntiles = tiles_x * tiles_y * nimg;
+  // persistent: the filter / bias / tap offsets are set up once per block and
+  // the next tile's input region is prefetched into registers (4 halves per
+  // thread) while the current tile computes and stores
+  constexpr int RPT = (3 * RP + 255) / 256;
+  auto fetch = [&](int t, half_t (&pre)[RPT]) {
+    const int tx = t % tiles_x, ty = (t / tiles_x) % tiles_y, b = t / (tiles_x * tiles_y);
+    const int oy0 = ty * 8, ox0 = tx * 32;
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+      const int e = tid + j * 256;
+      half_t v = (half_t)0.f;
+      if (e < 3 * RP) {
+        const int c = e / RP, r = e - c * RP, hy = r / RW, hx = r - hy * RW;
+        const int iy = oy0 - 1 + hy, ix = ox0 - 1 + hx;
+        if ((unsigned)iy < (unsigned)h && (unsigned)ix < (unsigned)wd)
+          v = x[((size_t)b * 3 + c) * HW + (size_t)iy * wd + ix];
+      }
+      pre[j] = v;
+    }
+  };
+  half_t pre[RPT];
+  int t = blockIdx.x;
+  if (t < ntiles) fetch(t, pre);
   h8 wf[NT];
   float bv[NT][4];
 #pragma unroll
@@ -354,7 +370,15 @@ __global__ __launch_bounds__(256) void conv3_mfma_kernel(const half_t* __restric
     const int k = fg * 8 + e, c = k / 9, ky = (k % 9) / 3, kx = k % 3;
     koff[e] = k < 27 ? c * RP + ky * RW + kx : -1;
   }
+  for (; t < ntiles; t += gridDim.x) {
+  const int tx = t % tiles_x, ty = (t / tiles_x) % tiles_y, b = t / (tiles_x * tiles_y);
+  const int oy0 = ty * 8, ox0 = tx * 32;
+  __syncthreads();  // every wave is done with the previous tile's region
+#pragma unroll
+  for (int j = 0; j < RPT; ++j)
+    if (tid + j * 256 < 3 * RP) reg[tid + j * 256] = pre[j];
   __syncthreads();
+  if (t + (int)gridDim.x < ntiles) fetch(t + gridDim.x, pre);
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const int gy = wave * 2 + (g >> 1), gx = (g & 1) * 16 + fr;
@@ -393,6 +417,7 @@ __global__ __launch_bounds__(256) void conv3_mfma_kernel(const half_t* __restric
       if (out2) *(h8*)(out2 + off) = *(const h8*)(&tr[wave][2][lane * 8]);
     }
   }
+  }
 }
 
 int launch_conv3(const void* x, const float* w, const float* bias, void* out0, void* out1, int B, int h, int wd,
@@ -401,12 +426,14 @@ int launch_conv3(const void* x, const float* w, const float* bias, void* out0, v
   if (n <= 0) return kErrShape;
   if (dtype == kF16 && getenv("UPR_CONV3_DIRECT") == nullptr) {
     const int tx = cdiv(wd, 32), ty = cdiv(h, 8);
+    // persistent grid: one wave of resident blocks (108 / 80 VGPRs -> 4 / 6 blocks per CU)
+    const int grid = std::min(B * tx * ty, 256 * (out1 ? 4 : 6));
     if (out1)
-      hipLaunchKernelGGL((conv3_mfma_kernel<2>), dim3(B * tx * ty), dim3(256), 0, st, (const half_t*)x, w, bias,
-                         (half_t*)out0, (half_t*)out1, (half_t*)out2, ps, ph, h, wd, tx, ty);
+      hipLaunchKernelGGL((conv3_mfma_kernel<2>), dim3(grid), dim3(256), 0, st, (const half_t*)x, w, bias,
+                         (half_t*)out0, (half_t*)out1, (half_t*)out2, ps, ph, h, wd, tx, ty, B);
     else
-      hipLaunchKernelGGL((conv3_mfma_kernel<1>), dim3(B * tx * ty), dim3(256), 0, st, (const half_t*)x, w, bias,
-                         (half_t*)out0, (half_t*)nullptr, (half_t*)out2, ps, ph, h, wd, tx, ty);
+      hipLaunchKernelGGL((conv3_mfma_kernel<1>), dim3(grid), dim3(256), 0, st, (const half_t*)x, w, bias,
+                         (half_t*)out0, (half_t*)nullptr, (half_t*)out2, ps, ph, h, wd, tx, ty, B);
     return (int)hipGetLastError();
   }
   if (out2) return kErrUnsupported;  // the fused PreAct output exists on the MFMA path only

@@ -164,7 +164,7 @@ def test_letterbox_quantisation_wraps_like_numpy():
 def test_load_image_on_device(tmp_path):
     from enhancers.simple_enhance import load_image, save_image
     x = torch.rand(1, 3, 16, 24)
-    save_image(x, str(tmp_path / "a.png"))
+    save_image(x.to(DEV), str(tmp_path / "a.png"))
     img, size = load_image(str(tmp_path / "a.png"))
     assert img.is_cuda and img.shape == (1, 3, 16, 24) and size == (24, 16)
     expect = torch.from_numpy(np.asarray(Image.open(tmp_path / "a.png")).transpose(2, 0, 1).copy()).float() / 255
