@@ -1,6 +1,6 @@
 # Round validation of HEAD on the GPU box: all GPU tests, smoke, benches, rocprofv3 kernel stats
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/v9
+O=gpurun_out/v10
 mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1 && \
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \
