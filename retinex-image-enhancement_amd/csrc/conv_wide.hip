@@ -522,12 +522,15 @@ int launch_conv_wide(const ConvOp& op, hipStream_t st) {
     if ((uintptr_t)sg.src % 16) return kErrUnsupported;
   }
   if (op.N % 256 == 0) return launch_wide_any<256>(op, st);
-  // 128-channel tiles of pure stride-1 3x3 convs stay on the halo kernel (it
-  // stages each input pixel once for all 9 taps and measured faster there)
+  // 128-channel stride-1 3x3 convs (dec3) used to stay on the halo kernel;
+  // on the single-stage two-blocks-per-CU variant they are faster (dec3.conv.0
+  // 0.264 -> 0.191 ms, conv.3 0.276 -> 0.217).  UPR_WIDE128_S1=0 restores the
+  // halo routing (A/B timing).
   bool all_s1_3x3 = true;
   for (int s = 0; s < op.nseg; ++s)
     if (!(op.seg[s].kh == 3 && op.seg[s].stride == 1)) all_s1_3x3 = false;
-  if (all_s1_3x3 && op.Wo >= 24 && op.Ho >= 8) return kErrUnsupported;
+  static const int s1_wide = env_int("UPR_WIDE128_S1", 1);
+  if (all_s1_3x3 && op.Wo >= 24 && op.Ho >= 8 && !s1_wide) return kErrUnsupported;
   return launch_wide_any<128>(op, st);
 }
 
