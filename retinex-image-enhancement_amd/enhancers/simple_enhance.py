@@ -9,6 +9,7 @@ runs on the device.  Intentional divergences, each a reference bug:
     the reference behaviour: UP_Retinex() defaults, unseeded init).
 """
 import os
+from concurrent.futures import ThreadPoolExecutor
 import time
 
 import numpy as np
@@ -24,16 +25,22 @@ from utils.letterbox import letterbox_u8_image
 VALID_EXTENSIONS = {'.jpg', '.jpeg', '.png', '.bmp', '.tif', '.tiff'}
 
 
-def load_image(image_path, max_size=None, device=None):
+def _decode(image_path):
+    """PIL decode -> (uint8 HWC RGB array, (W, H)).  Runs on the harness's
+    prefetch thread for the next file of a batch."""
+    img = Image.open(image_path).convert('RGB')
+    return np.asarray(img, dtype=np.uint8), img.size
+
+
+def load_image(image_path, max_size=None, device=None, decoded=None):
     """Decode + letterbox (reference :23-62) -> ([1,3,H,W] float32, (W, H)).
 
     The decoded uint8 pixels go to the ROCm device as bytes and ToTensor +
     letterbox_tensor run there as one launch (utils/letterbox.py); the tensor is
     returned on that device (the reference returns it on the CPU and the caller
-    moves it -- the callers' .to(device) is then a no-op)."""
-    img = Image.open(image_path).convert('RGB')
-    original_size = img.size
-    a = np.asarray(img, dtype=np.uint8)
+    moves it -- the callers' .to(device) is then a no-op).  `decoded` takes an
+    already decoded (array, size) pair (the batch harness's prefetch)."""
+    a, original_size = decoded if decoded is not None else _decode(image_path)
     new_shape = max_size if max_size is not None else a.shape[:2]
     t, _, _ = letterbox_u8_image(a, new_shape=new_shape, auto=True, scaleup=False, device=device)
     return t.unsqueeze(0), original_size
@@ -47,28 +54,38 @@ def _to_u8_hwc(t):
     return runtime.to_u8_hwc(t.detach()).cpu().numpy()
 
 
-def save_image(tensor, save_path):
+def _write_png(arr, save_path, msg):
+    Image.fromarray(arr).save(save_path)
+    print(f"{msg}: {save_path}")
+
+
+def _emit(arr, save_path, msg, writer):
+    if writer is None:
+        _write_png(arr, save_path, msg)
+    else:  # PNG encode + file write on the batch harness's writer thread
+        writer.submit(_write_png, arr, save_path, msg)
+
+
+def save_image(tensor, save_path, writer=None):
     """[1,C,H,W] or [C,H,W] -> PNG; 1-channel maps are replicated to RGB (reference :65-99)."""
     if tensor.dim() == 4:
         tensor = tensor.squeeze(0)
-    Image.fromarray(_to_u8_hwc(tensor)).save(save_path)
-    print(f"已保存: {save_path}")
+    _emit(_to_u8_hwc(tensor), save_path, "已保存", writer)
 
 
-def create_comparison(img_low, img_enhanced, save_path):
+def create_comparison(img_low, img_enhanced, save_path, writer=None):
     """[input | enhanced] side by side (reference :102-132)."""
     a = _to_u8_hwc(img_low.squeeze(0))
     b = _to_u8_hwc(img_enhanced.squeeze(0))
-    Image.fromarray(np.concatenate([a, b], axis=1)).save(save_path)
-    print(f"已保存对比图像: {save_path}")
+    _emit(np.concatenate([a, b], axis=1), save_path, "已保存对比图像", writer)
 
 
 def enhance_single_image(model, image_path, output_dir, device, max_size=None, enable_multi_scale=False,
-                         enable_content_aware=False, adjuster=None, precision="fp32"):
+                         enable_content_aware=False, adjuster=None, precision="fp32", _decoded=None, _writer=None):
     """Enhance one file and write {name}_enhanced/_illumination/_comparison.png (reference :135-199).
     precision="fp16" runs the fp16 storage / fp16-MFMA graph (input cast to half)."""
     print(f"正在处理: {os.path.basename(image_path)}")
-    img_low, _ = load_image(image_path, max_size)
+    img_low, _ = load_image(image_path, max_size, decoded=_decoded)
     if precision == "fp16":
         img_low = img_low.half()
     adjuster = AdaptiveParameterAdjuster()
@@ -86,9 +103,9 @@ def enhance_single_image(model, image_path, output_dir, device, max_size=None, e
     print(f"增强耗时: {time.time() - start:.4f}s")
     os.makedirs(output_dir, exist_ok=True)
     name = os.path.splitext(os.path.basename(image_path))[0]
-    save_image(img_enhanced, os.path.join(output_dir, f"{name}_enhanced.png"))
-    save_image(illu_map, os.path.join(output_dir, f"{name}_illumination.png"))
-    create_comparison(img_low, img_enhanced, os.path.join(output_dir, f"{name}_comparison.png"))
+    save_image(img_enhanced, os.path.join(output_dir, f"{name}_enhanced.png"), _writer)
+    save_image(illu_map, os.path.join(output_dir, f"{name}_illumination.png"), _writer)
+    create_comparison(img_low, img_enhanced, os.path.join(output_dir, f"{name}_comparison.png"), _writer)
     print("图像增强完成！")
     return img_enhanced, illu_map
 
@@ -113,12 +130,21 @@ def enhance_batch_images(input_dir, output_dir, device, max_size=None, use_preac
     print(f"找到 {len(image_files)} 个图像文件")
     print("=" * 50)
     total = 0.0
-    for i, path in enumerate(image_files, 1):
-        print(f"[{i}/{len(image_files)}]")
-        t0 = time.time()
-        enhance_single_image(model, path, output_dir, device, max_size, precision=precision)
-        total += time.time() - t0
-        print("-" * 50)
+    # host pipeline around the device work: the next file is decoded on a
+    # prefetch thread and the PNG encodes run on writer threads while the GPU
+    # enhances the current image (the reference does all three serially)
+    with ThreadPoolExecutor(max_workers=1) as reader, ThreadPoolExecutor(max_workers=2) as writer:
+        nxt = reader.submit(_decode, image_files[0])
+        for i, path in enumerate(image_files, 1):
+            print(f"[{i}/{len(image_files)}]")
+            t0 = time.time()
+            decoded = nxt.result()
+            if i < len(image_files):
+                nxt = reader.submit(_decode, image_files[i])
+            enhance_single_image(model, path, output_dir, device, max_size, precision=precision, _decoded=decoded,
+                                 _writer=writer)
+            total += time.time() - t0
+            print("-" * 50)
     print("=" * 50)
     print(f"总共处理了 {len(image_files)} 张图像")
     print(f"总耗时: {total:.2f}s")

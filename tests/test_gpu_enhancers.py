@@ -194,3 +194,22 @@ def test_save_image_pixels_match_numpy(tmp_path):
     np.testing.assert_array_equal(np.asarray(Image.open(tmp_path / "b.png")), np.repeat(b1, 3, axis=2))
     c = np.concatenate([a, ref(x[0].flip(-1))], axis=1)
     np.testing.assert_array_equal(np.asarray(Image.open(tmp_path / "c.png")), c)
+
+
+def test_batch_harness_pipeline_matches_single(tmp_path):
+    """enhance_batch_images with decode prefetch and threaded PNG writes gives,
+    file for file, the bytes enhance_single_image writes serially."""
+    from enhancers.simple_enhance import enhance_single_image, enhance_batch_images
+    src = tmp_path / "in"
+    src.mkdir()
+    rng = np.random.default_rng(7)
+    for k, (h, w) in enumerate(((64, 96), (128, 64), (48, 48))):
+        Image.fromarray((rng.integers(0, 256, (h, w, 3)) * 0.4).astype(np.uint8)).save(src / f"im{k}.png")
+    enhance_batch_images(str(src), str(tmp_path / "batch"), DEV, use_preact=False, use_aspp=False, seed=0)
+    m = make_model(seed=0).to(DEV)
+    for k in range(3):
+        enhance_single_image(m, str(src / f"im{k}.png"), str(tmp_path / "single"), DEV)
+        for suffix in ("enhanced", "illumination", "comparison"):
+            a = np.asarray(Image.open(tmp_path / "batch" / f"im{k}_{suffix}.png"))
+            b = np.asarray(Image.open(tmp_path / "single" / f"im{k}_{suffix}.png"))
+            np.testing.assert_array_equal(a, b, err_msg=f"im{k}_{suffix}")
