@@ -22,6 +22,8 @@ from enhancers.multi_scale import MultiScaleEnhancer
 from enhancers.content_aware import ContentAwareEnhancer
 from utils.letterbox import letterbox_u8_image
 
+# PNG encoders running beside the GPU (PIL's zlib releases the GIL); 3 files per image
+_WRITERS = 6
 VALID_EXTENSIONS = {'.jpg', '.jpeg', '.png', '.bmp', '.tif', '.tiff'}
 
 
@@ -29,7 +31,7 @@ def _decode(image_path):
     """PIL decode -> (uint8 HWC RGB array, (W, H)).  Runs on the harness's
     prefetch thread for the next file of a batch."""
     img = Image.open(image_path).convert('RGB')
-    return np.asarray(img, dtype=np.uint8), img.size
+    return np.array(img, dtype=np.uint8), img.size
 
 
 def load_image(image_path, max_size=None, device=None, decoded=None):
@@ -133,7 +135,7 @@ def enhance_batch_images(input_dir, output_dir, device, max_size=None, use_preac
     # host pipeline around the device work: the next file is decoded on a
     # prefetch thread and the PNG encodes run on writer threads while the GPU
     # enhances the current image (the reference does all three serially)
-    with ThreadPoolExecutor(max_workers=1) as reader, ThreadPoolExecutor(max_workers=2) as writer:
+    with ThreadPoolExecutor(max_workers=1) as reader, ThreadPoolExecutor(max_workers=_WRITERS) as writer:
         nxt = reader.submit(_decode, image_files[0])
         for i, path in enumerate(image_files, 1):
             print(f"[{i}/{len(image_files)}]")
