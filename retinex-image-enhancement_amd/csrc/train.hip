@@ -7,6 +7,7 @@
 // NHWC activations, channel slices of concat buffers).  Everything computes in
 // fp32; per-channel / per-image reductions accumulate in fp64 (block partials
 // in registers + LDS, one fp64 atomic per block and channel).
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 
@@ -588,6 +589,51 @@ __global__ void bilinear_bwd_kernel(V dy, int B, int H, int W, int C, int Ho, in
     atomicAdd(dx.d + dx.at(b, y0, x1, c), g * (1.f - ly) * lx);
     atomicAdd(dx.d + dx.at(b, y1, x0, c), g * ly * (1.f - lx));
     atomicAdd(dx.d + dx.at(b, y1, x1, c), g * ly * lx);
+  }
+}
+
+// gather form of the bilinear backward: one thread per SOURCE element sums the
+// output gradients whose forward taps (bilin_src, the forward's own arithmetic)
+// land on it -- no atomics (the scatter form contends 16-256 ways on the 4x /
+// 16x head upsamplings).  Candidate outputs: those whose source coordinate lies
+// in [i-1, i+1]; the last row / column also collects the clamped tail.
+__device__ __forceinline__ void bilin_range(int i, int in, int out, float scale, int& lo, int& hi) {
+  lo = (int)floorf(((float)i - 0.5f) / scale - 0.5f) - 1;
+  hi = (int)ceilf(((float)i + 1.5f) / scale - 0.5f) + 1;
+  if (lo < 0) lo = 0;
+  if (i == in - 1 || hi > out - 1) hi = out - 1;
+}
+
+__device__ __forceinline__ float bilin_w(int o, int i, int in, float scale) {
+  int i0, i1;
+  float l;
+  bilin_src(o, in, scale, i0, i1, l);
+  return (i0 == i ? 1.f - l : 0.f) + (i1 == i ? l : 0.f);
+}
+
+__global__ void bilinear_bwd_gather_kernel(V dy, int B, int H, int W, int C, int Ho, int Wo, float sh, float sw, V dx) {
+  const long long n = (long long)B * H * W * C;
+  GSTRIDE(i, n) {
+    const int c = (int)(i % C);
+    long long r = i / C;
+    const int ix = (int)(r % W); r /= W;
+    const int iy = (int)(r % H);
+    const int b = (int)(r / H);
+    int ylo, yhi, xlo, xhi;
+    bilin_range(iy, H, Ho, sh, ylo, yhi);
+    bilin_range(ix, W, Wo, sw, xlo, xhi);
+    float acc = 0.f;
+    for (int oy = ylo; oy <= yhi; ++oy) {
+      const float wy = bilin_w(oy, iy, H, sh);
+      if (wy == 0.f) continue;
+      float row = 0.f;
+      for (int ox = xlo; ox <= xhi; ++ox) {
+        const float wx = bilin_w(ox, ix, W, sw);
+        if (wx != 0.f) row += wx * dy.d[dy.at(b, oy, ox, c)];
+      }
+      acc += wy * row;
+    }
+    dx.d[dx.at(b, iy, ix, c)] += acc;
   }
 }
 
@@ -1448,8 +1494,14 @@ int upr_t_bilinear_bwd(const UprView* dy, int B, int H, int W, int C, int Ho, in
                        void* stream) {
   if (!dy || !dx) return UPR_ERR_ARG;
   const long long n = (long long)B * Ho * Wo * C;
-  hipLaunchKernelGGL(bilinear_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), mkv(dy), B, H, W, C, Ho, Wo,
-                     (float)H / Ho, (float)W / Wo, mkv(dx));
+  if (getenv("UPR_BILINEAR_BWD_SCATTER")) {  // the atomic scatter form (A/B timing)
+    hipLaunchKernelGGL(bilinear_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), mkv(dy), B, H, W, C, Ho, Wo,
+                       (float)H / Ho, (float)W / Wo, mkv(dx));
+  } else {
+    const long long ns = (long long)B * H * W * C;
+    hipLaunchKernelGGL(bilinear_bwd_gather_kernel, dim3(grid_for(ns)), dim3(256), 0, ST(stream), mkv(dy), B, H, W, C,
+                       Ho, Wo, (float)H / Ho, (float)W / Wo, mkv(dx));
+  }
   LAUNCH_CHECK();
 }
 
