@@ -723,6 +723,70 @@ __global__ void fam_sa_bwd_kernel(const float* __restrict__ g, const float* __re
   }
 }
 
+// C == 32 forms of the three per-pixel attention kernels above: 8 lanes per
+// pixel, one float4 per lane (a wave reads 8 whole 128-byte pixel rows per
+// instruction instead of 64 lanes striding 128 B apart), the channel mean / max /
+// dot reduced over the 8-lane group by xor shuffles.  Groups of 8 are aligned
+// (n and blockDim multiples of 8), so a whole group leaves the loop together.
+__device__ __forceinline__ float nanmax(float a, float b) { return (b > a || isnan(b)) ? b : a; }
+
+__global__ void fam_ca_apply32_kernel(const float* __restrict__ o, const float* __restrict__ ca, int B, int HW,
+                                      float* __restrict__ o2, float* __restrict__ m) {
+  const long long n = (long long)B * HW * 8;
+  GSTRIDE(i, n) {
+    const long long pix = i >> 3;
+    const int q = (int)(i & 7);
+    const int b = (int)(pix / HW);
+    float4 v = ((const float4*)(o + pix * 32))[q];
+    const float4 w = ((const float4*)(ca + (size_t)b * 32))[q];
+    v.x *= w.x; v.y *= w.y; v.z *= w.z; v.w *= w.w;
+    ((float4*)(o2 + pix * 32))[q] = v;
+    float sm = (v.x + v.y) + (v.z + v.w);
+    float mx = nanmax(nanmax(v.x, v.y), nanmax(v.z, v.w));
+    for (int off = 1; off < 8; off <<= 1) {
+      sm += __shfl_xor(sm, off);
+      mx = nanmax(mx, __shfl_xor(mx, off));
+    }
+    if (q == 0) {
+      m[pix * 2] = sm / 32.f;
+      m[pix * 2 + 1] = mx;
+    }
+  }
+}
+
+__global__ void fam_sa_apply32_kernel(const float* __restrict__ o2, const float* __restrict__ s_pre, int B, int HW,
+                                      float* __restrict__ sa, float* __restrict__ out) {
+  const long long n = (long long)B * HW * 8;
+  GSTRIDE(i, n) {
+    const long long pix = i >> 3;
+    const int q = (int)(i & 7);
+    const float a = 1.f / (1.f + expf(-s_pre[pix]));
+    if (q == 0) sa[pix] = a;
+    float4 v = ((const float4*)(o2 + pix * 32))[q];
+    v.x *= a; v.y *= a; v.z *= a; v.w *= a;
+    ((float4*)(out + pix * 32))[q] = v;
+  }
+}
+
+__global__ void fam_sa_bwd32_kernel(const float* __restrict__ g, const float* __restrict__ o2,
+                                    const float* __restrict__ sa, int B, int HW, float* __restrict__ g_o2,
+                                    float* __restrict__ g_spre) {
+  const long long n = (long long)B * HW * 8;
+  GSTRIDE(i, n) {
+    const long long pix = i >> 3;
+    const int q = (int)(i & 7);
+    const float a = sa[pix];
+    const float4 gv = ((const float4*)(g + pix * 32))[q];
+    const float4 ov = ((const float4*)(o2 + pix * 32))[q];
+    float t = (gv.x * ov.x + gv.y * ov.y) + (gv.z * ov.z + gv.w * ov.w);
+    ((float4*)(g_o2 + pix * 32))[q] = make_float4(gv.x * a, gv.y * a, gv.z * a, gv.w * a);
+    for (int off = 1; off < 8; off <<= 1) t += __shfl_xor(t, off);
+    if (q == 0) g_spre[pix] = t * a * (1.f - a);
+  }
+}
+
+static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
 // g_ca[b][c] partials go through LDS: a block covers a pixel range of one image
 __global__ __launch_bounds__(256) void fam_ca_bwd_kernel(const float* __restrict__ g_o2, const float* __restrict__ g_m,
                                                          const float* __restrict__ o, const float* __restrict__ o2,
@@ -1526,6 +1590,11 @@ int upr_t_broadcast(const float* v, int B, int HW, int C, float scale, float* y,
 
 int upr_t_fam_ca_apply(const float* o, const float* ca, int B, int HW, int C, float* o2, float* m, void* stream) {
   if (!o || !ca || !o2 || !m) return UPR_ERR_ARG;
+  if (C == 32 && al16(o) && al16(ca) && al16(o2)) {
+    hipLaunchKernelGGL(fam_ca_apply32_kernel, dim3(grid_for((long long)B * HW * 8)), dim3(256), 0, ST(stream), o, ca,
+                       B, HW, o2, m);
+    LAUNCH_CHECK();
+  }
   hipLaunchKernelGGL(fam_ca_apply_kernel, dim3(grid_for((long long)B * HW)), dim3(256), 0, ST(stream), o, ca, B, HW,
                      C, o2, m);
   LAUNCH_CHECK();
@@ -1534,6 +1603,11 @@ int upr_t_fam_ca_apply(const float* o, const float* ca, int B, int HW, int C, fl
 int upr_t_fam_sa_apply(const float* o2, const float* s_pre, int B, int HW, int C, float* sa, float* out,
                        void* stream) {
   if (!o2 || !s_pre || !sa || !out) return UPR_ERR_ARG;
+  if (C == 32 && al16(o2) && al16(out)) {
+    hipLaunchKernelGGL(fam_sa_apply32_kernel, dim3(grid_for((long long)B * HW * 8)), dim3(256), 0, ST(stream), o2,
+                       s_pre, B, HW, sa, out);
+    LAUNCH_CHECK();
+  }
   hipLaunchKernelGGL(fam_sa_apply_kernel, dim3(grid_for((long long)B * HW)), dim3(256), 0, ST(stream), o2, s_pre, B,
                      HW, C, sa, out);
   LAUNCH_CHECK();
@@ -1542,6 +1616,11 @@ int upr_t_fam_sa_apply(const float* o2, const float* s_pre, int B, int HW, int C
 int upr_t_fam_sa_bwd(const float* g, const float* o2, const float* sa, int B, int HW, int C, float* g_o2,
                      float* g_spre, void* stream) {
   if (!g || !o2 || !sa || !g_o2 || !g_spre) return UPR_ERR_ARG;
+  if (C == 32 && al16(g) && al16(o2) && al16(g_o2)) {
+    hipLaunchKernelGGL(fam_sa_bwd32_kernel, dim3(grid_for((long long)B * HW * 8)), dim3(256), 0, ST(stream), g, o2, sa,
+                       B, HW, g_o2, g_spre);
+    LAUNCH_CHECK();
+  }
   hipLaunchKernelGGL(fam_sa_bwd_kernel, dim3(grid_for((long long)B * HW)), dim3(256), 0, ST(stream), g, o2, sa, B,
                      HW, C, g_o2, g_spre);
   LAUNCH_CHECK();
