@@ -369,6 +369,67 @@ __global__ __launch_bounds__(256) void chan_reduce_kernel(const float* __restric
 
 static int reduce_grid(int M) { return grid_for(M, 512, 2048); }
 
+// float4 form of chan_reduce_kernel (C % 4 == 0, C <= 1024, 16-byte aligned
+// rows): a thread owns 4 consecutive channels, so a wave reads whole 16-byte
+// chunks of 64 / (C/4) rows per instruction (same per-channel fp64 sums)
+__global__ __launch_bounds__(256) void chan_reduce4_kernel(const float* __restrict__ a, int a_cs, int a_coff,
+                                                           const float* __restrict__ x, int x_cs, int x_coff,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd, int M, int C, int mode,
+                                                           double* __restrict__ acc, float* __restrict__ fout) {
+  __shared__ double s1[256 * 4], s2[256 * 4];
+  const int rows_per_block = (M + gridDim.x - 1) / gridDim.x;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(M, r0 + rows_per_block);
+  const int C4 = C >> 2;
+  const int R = 256 / C4;
+  const int q = threadIdx.x % C4, rg = threadIdx.x / C4;
+  double u[4] = {0.0, 0.0, 0.0, 0.0}, v[4] = {0.0, 0.0, 0.0, 0.0};
+  if (rg < R) {
+    float4 mu = make_float4(0.f, 0.f, 0.f, 0.f), is = mu;
+    if (mode == 1) { mu = ((const float4*)mean)[q]; is = ((const float4*)invstd)[q]; }
+    for (int r = r0 + rg; r < r1; r += R) {
+      const float4 av = *(const float4*)(a + (size_t)r * a_cs + a_coff + 4 * q);
+      const float ae[4] = {av.x, av.y, av.z, av.w};
+      if (mode == 1) {
+        const float4 xv = *(const float4*)(x + (size_t)r * x_cs + x_coff + 4 * q);
+        const float xh[4] = {(xv.x - mu.x) * is.x, (xv.y - mu.y) * is.y, (xv.z - mu.z) * is.z, (xv.w - mu.w) * is.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { u[e] += ae[e]; v[e] += (double)ae[e] * xh[e]; }
+      } else if (mode == 0) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { u[e] += ae[e]; v[e] += (double)ae[e] * ae[e]; }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) u[e] += ae[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) { s1[threadIdx.x * 4 + e] = u[e]; s2[threadIdx.x * 4 + e] = v[e]; }
+  __syncthreads();
+  if (threadIdx.x < C4) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      double t1 = 0.0, t2 = 0.0;
+      for (int k = 0; k < R; ++k) { t1 += s1[(k * C4 + threadIdx.x) * 4 + e]; t2 += s2[(k * C4 + threadIdx.x) * 4 + e]; }
+      const int cc = 4 * threadIdx.x + e;
+      if (mode == 2) atomicAdd(fout + cc, (float)t1);
+      else { atomicAdd(acc + cc, t1); atomicAdd(acc + C + cc, t2); }
+    }
+  }
+}
+
+static bool reduce4_ok(int C, int cs, int coff, const void* p) {
+  static const bool off = [] {  // UPR_REDUCE4=0: the scalar form (A/B timing)
+    const char* e = getenv("UPR_REDUCE4");
+    return e && e[0] == '0';
+  }();
+  return !off && C % 4 == 0 && C <= 1024 && cs % 4 == 0 && coff % 4 == 0 && ((uintptr_t)p & 15) == 0;
+}
+
+
+
 __global__ void bn_finalize_kernel(const double* __restrict__ acc, int M, int C, float momentum, float eps,
                                    float* __restrict__ rm, float* __restrict__ rv, long long* nbt,
                                    float* __restrict__ mean, float* __restrict__ invstd) {
@@ -1450,8 +1511,12 @@ int upr_t_zero_upsample(const float* dy, int B, int Ho, int Wo, int C, int dy_cs
 
 int upr_t_bn_stats(const float* x, int M, int C, int cs, int coff, double* acc, void* stream) {
   if (!x || !acc || M <= 0 || C <= 0) return UPR_ERR_ARG;
-  hipLaunchKernelGGL(chan_reduce_kernel, dim3(reduce_grid(M)), dim3(256), 0, ST(stream), x, cs, coff, nullptr, 0, 0,
-                     nullptr, nullptr, M, C, 0, acc, nullptr);
+  if (reduce4_ok(C, cs, coff, x))
+    hipLaunchKernelGGL(chan_reduce4_kernel, dim3(reduce_grid(M)), dim3(256), 0, ST(stream), x, cs, coff, nullptr, 0,
+                       0, nullptr, nullptr, M, C, 0, acc, nullptr);
+  else
+    hipLaunchKernelGGL(chan_reduce_kernel, dim3(reduce_grid(M)), dim3(256), 0, ST(stream), x, cs, coff, nullptr, 0, 0,
+                       nullptr, nullptr, M, C, 0, acc, nullptr);
   LAUNCH_CHECK();
 }
 
@@ -1476,8 +1541,13 @@ int upr_t_bn_apply(const float* x, int M, int C, int x_cs, int x_coff, const flo
 int upr_t_bn_bwd_reduce(const float* g, int g_cs, int g_coff, const float* x, int x_cs, int x_coff, const float* mean,
                         const float* invstd, int M, int C, double* acc, void* stream) {
   if (!g || !x || !acc) return UPR_ERR_ARG;
-  hipLaunchKernelGGL(chan_reduce_kernel, dim3(reduce_grid(M)), dim3(256), 0, ST(stream), g, g_cs, g_coff, x, x_cs,
-                     x_coff, mean, invstd, M, C, 1, acc, nullptr);
+  if (reduce4_ok(C, g_cs, g_coff, g) && reduce4_ok(C, x_cs, x_coff, x) && ((uintptr_t)mean & 15) == 0 &&
+      ((uintptr_t)invstd & 15) == 0)
+    hipLaunchKernelGGL(chan_reduce4_kernel, dim3(reduce_grid(M)), dim3(256), 0, ST(stream), g, g_cs, g_coff, x,
+                       x_cs, x_coff, mean, invstd, M, C, 1, acc, nullptr);
+  else
+    hipLaunchKernelGGL(chan_reduce_kernel, dim3(reduce_grid(M)), dim3(256), 0, ST(stream), g, g_cs, g_coff, x, x_cs,
+                       x_coff, mean, invstd, M, C, 1, acc, nullptr);
   LAUNCH_CHECK();
 }
 
