@@ -79,6 +79,45 @@ __global__ __launch_bounds__(256) void conv_direct_kernel(V x, int B, int H, int
   }
 }
 
+// 3-input-channel 3x3 stride-1 dilation-1 form (the input layers 3->32 and
+// VGG-19 conv1_1 3->64 at full resolution): compile-time tap loops, the 27
+// weights in registers, one base pointer per tap row -- the generic kernel's
+// per-access 64-bit four-stride index arithmetic dominated its time
+__global__ __launch_bounds__(256) void conv_direct_c3k3_kernel(V x, int B, int H, int W, const float* __restrict__ w,
+                                                               const float* __restrict__ bias, int Cout, int p, V y,
+                                                               int Ho, int Wo, int relu, int accum) {
+  const long long n = (long long)B * Ho * Wo * Cout;
+  GSTRIDE(i, n) {
+    const int co = (int)(i % Cout);
+    long long r = i / Cout;
+    const int ox = (int)(r % Wo); r /= Wo;
+    const int oy = (int)(r % Ho);
+    const int b = (int)(r / Ho);
+    const float* wc = w + (size_t)co * 27;
+    float a = bias ? bias[co] : 0.f;
+    // same accumulation order as conv_direct_kernel: ci outer, then ky, kx
+#pragma unroll
+    for (int ci = 0; ci < 3; ++ci) {
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        const int iy = oy - p + ky;
+        if (iy < 0 || iy >= H) continue;
+        const float* row = x.d + b * x.sb + iy * x.sh + ci * x.sc;
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const int ix = ox - p + kx;
+          if (ix < 0 || ix >= W) continue;
+          a = fmaf(row[ix * x.sw], wc[(ci * 3 + ky) * 3 + kx], a);
+        }
+      }
+    }
+    float* yp = y.d + y.at(b, oy, ox, co);
+    if (accum) a += *yp;
+    if (relu) a = fmaxf(a, 0.f);
+    *yp = a;
+  }
+}
+
 __global__ __launch_bounds__(256) void conv_direct_dgrad_kernel(V dy, int Ho, int Wo, const float* __restrict__ w,
                                                                 int B, int H, int W, int Cin, int Cout, int kh,
                                                                 int kw, int s, int p, int d, V dx, int accum) {
@@ -1415,6 +1454,11 @@ int upr_t_conv_direct(const UprView* x, int B, int H, int W, int Cin, const floa
   if (Ho != (H + 2 * pad - dil * (kh - 1) - 1) / stride + 1 || Wo != (W + 2 * pad - dil * (kw - 1) - 1) / stride + 1)
     return UPR_ERR_SHAPE;
   const long long n = (long long)B * Ho * Wo * Cout;
+  if (Cin == 3 && kh == 3 && kw == 3 && stride == 1 && dil == 1) {
+    hipLaunchKernelGGL(conv_direct_c3k3_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), mkv(x), B, H, W, w, bias,
+                       Cout, pad, mkv(y), Ho, Wo, relu, accumulate);
+    LAUNCH_CHECK();
+  }
   hipLaunchKernelGGL(conv_direct_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), mkv(x), B, H, W, Cin, w, bias,
                      Cout, kh, kw, stride, pad, dil, mkv(y), Ho, Wo, relu, accumulate);
   LAUNCH_CHECK();
