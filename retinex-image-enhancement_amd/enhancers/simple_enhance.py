@@ -75,11 +75,14 @@ def save_image(tensor, save_path, writer=None):
     _emit(_to_u8_hwc(tensor), save_path, "已保存", writer)
 
 
-def create_comparison(img_low, img_enhanced, save_path, writer=None):
-    """[input | enhanced] side by side (reference :102-132)."""
-    a = _to_u8_hwc(img_low.squeeze(0))
-    b = _to_u8_hwc(img_enhanced.squeeze(0))
-    _emit(np.concatenate([a, b], axis=1), save_path, "已保存对比图像", writer)
+def create_comparison(img_low, img_enhanced, save_path, writer=None, illu_map=None):
+    """[input | enhanced] side by side (reference :102-132); with `illu_map`
+    the predictor's 3-panel form [input | enhanced | illumination]
+    (reference predictors/predict.py:102-140)."""
+    panels = [_to_u8_hwc(img_low.squeeze(0)), _to_u8_hwc(img_enhanced.squeeze(0))]
+    if illu_map is not None:
+        panels.append(_to_u8_hwc(illu_map.squeeze(0)))
+    _emit(np.concatenate(panels, axis=1), save_path, "已保存对比图像", writer)
 
 
 def enhance_single_image(model, image_path, output_dir, device, max_size=None, enable_multi_scale=False,

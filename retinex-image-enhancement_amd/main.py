@@ -7,8 +7,11 @@ never seeds its random init, main.py:229) and --precision {fp32,fp16}.
 Intentional divergences (reference bugs): a single-file --mode enhance works
 (reference main.py:240-249 raises TypeError); --mode predict unpacks the
 model's 3-tuple (reference predict.py:163 raises ValueError).
---mode train is not implemented on the HIP path yet (training kernels are the
-next scope row) and exits with an error.
+--mode train: the training STEP runs on the HIP path through the drop-in
+trainers/train.py (train_step / train_one_epoch, losses/loss.py TotalLoss);
+the reference's epoch driver around it (datasets, augmentation, schedulers,
+TensorBoard, checkpoint files; reference trainers/train.py:134-330) is outside
+this build's scope, so the CLI mode exits with that message.
 """
 import argparse
 import os
@@ -85,6 +88,9 @@ def _place(model, args):
 
 
 def _predict_one(model, path, args):
+    """predictors/predict.py:144-191 predict_single_image: enhanced, illumination
+    and the 3-panel [input | enhanced | illumination] comparison (:102-140; the
+    1-channel map's channel mean is the map itself, replicated to RGB)."""
     x, _ = load_image(path, args.max_size)
     x = x.to(args.device)
     if args.precision == 'fp16':
@@ -96,7 +102,7 @@ def _predict_one(model, path, args):
     save_image(enh, os.path.join(args.output_dir, f"{name}_enhanced.png"))
     save_image(illu, os.path.join(args.output_dir, f"{name}_illumination.png"))
     if not args.no_comparison:
-        create_comparison(x, enh, os.path.join(args.output_dir, f"{name}_comparison.png"))
+        create_comparison(x, enh, os.path.join(args.output_dir, f"{name}_comparison.png"), illu_map=illu)
 
 
 def main(argv=None):
@@ -106,8 +112,9 @@ def main(argv=None):
     print(f"使用设备: {args.device}")
     print(f"运行模式: {args.mode}")
     if args.mode == 'train':
-        raise SystemExit("--mode train: the HIP training step (backward kernels, losses) is not implemented yet; "
-                         "inference modes (enhance, predict) run on the MI355X path")
+        raise SystemExit("--mode train: the reference's epoch driver (datasets, augmentation, schedulers, "
+                         "checkpoint files) is outside this build; the HIP training step itself is the drop-in "
+                         "trainers.train.train_step / train_one_epoch with losses.loss.TotalLoss")
     if args.mode == 'predict':
         if not os.path.exists(args.checkpoint):
             print(f"错误: 找不到模型检查点文件 '{args.checkpoint}'")

@@ -67,8 +67,6 @@ def allreduce_grads(optimizer, group=None):
     rank, as the reference has no SyncBN.  Call between the backward and the
     unscale / clip (trainers.train.train_step's grad_hook)."""
     world = dist.get_world_size(group)
-    if world == 1:
-        return
     g = optimizer.flat.grad
     dist.all_reduce(g, op=dist.ReduceOp.SUM, group=group)
     g.div_(world)

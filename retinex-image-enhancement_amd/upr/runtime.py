@@ -37,16 +37,25 @@ def _stream(dev):
 
 
 class _Workspace:
-    """Grow-only per-device scratch buffer (torch-allocated device bytes)."""
+    """Grow-only scratch buffer per (device, HIP stream), torch-allocated.
+
+    Keyed by the caller's current stream: work issued on two streams never
+    shares scratch, and a buffer is allocated on (and, when it grows, released
+    to torch's caching allocator from) the stream that uses it, so the
+    allocator's stream ordering keeps a replaced buffer alive until the work
+    queued on that stream has drained (include/upr.h: thread-safe across
+    distinct handles or streams)."""
 
     def __init__(self):
         self.buf = {}
 
     def get(self, dev, nbytes):
-        key = (dev.type, dev.index)
+        stream = torch.cuda.current_stream(dev)
+        key = (dev.type, dev.index, stream.cuda_stream)
         b = self.buf.get(key)
         if b is None or b.numel() < nbytes:
-            b = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
+            with torch.cuda.stream(stream):
+                b = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
             self.buf[key] = b
         return b
 

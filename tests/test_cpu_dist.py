@@ -78,3 +78,23 @@ def test_gloo_allreduce_grads_world2():
     for p in procs:
         p.join(timeout=60)
     assert sorted(res) == [(0, True), (1, True)]
+
+
+def test_bench_gpus2_launches_two_gloo_ranks():
+    """`bench.py --gpus 2` run directly is a launcher: it starts torch.distributed.run
+    with 2 ranks (here with --dry-run: gloo, CPU step) and rank 0 reports
+    n_gpus 2 with the max-over-ranks time; both ranks are distinct processes."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "3",
+                        "--warmup", "1"], capture_output=True, text=True, timeout=240, cwd=repo)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == 3
+    ranks = out["ranks"]
+    assert sorted(rk for rk, _ in ranks) == [0, 1]
+    assert len({pid for _, pid in ranks}) == 2 and os.getpid() not in {pid for _, pid in ranks}

@@ -75,8 +75,15 @@ def test_fused_submodules_raise():
         m.retinex_decompose(torch.rand(1, 3, 8, 8), torch.rand(1, 1, 8, 8))
 
 
-def test_training_mode_raises():
+def test_training_mode_cpu_input_raises_and_ienet_train_unsupported():
+    """Training mode is supported on the device (upr/autograd.model_train_forward,
+    tests/test_gpu_train.py); on a CPU tensor it raises like eval mode (no CPU
+    path), and a standalone ResidualIENet training forward is refused."""
     m = M.UP_Retinex(use_preact=False, use_aspp=False)  # .train() by default
-    x = torch.rand(1, 3, 32, 32)
-    with pytest.raises((NotImplementedError, RuntimeError)):
-        m(x)
+    assert m.training
+    with pytest.raises(RuntimeError, match="ROCm"):
+        m(torch.rand(1, 3, 32, 32))
+    ie = M.ResidualIENet()
+    assert ie.training
+    with pytest.raises(RuntimeError, match="ROCm"):
+        ie(torch.rand(1, 3, 32, 32))
