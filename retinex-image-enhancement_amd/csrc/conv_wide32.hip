@@ -50,18 +50,21 @@ constexpr int Q_BK = 32;  // fp32 channels per K step = one 128-byte LDS row
 
 template <int BM, int BN>
 struct Q32Cfg {
-  static constexpr int WAVES_N = BN / 64;
+  static constexpr int WN = BN >= 64 ? 4 : BN / 16;  // 16-column tiles per wave
+  static constexpr int WAVES_N = BN / (16 * WN);
   static constexpr int WAVES_M = 8 / WAVES_N;
   static constexpr int WM = BM / WAVES_M / 16;  // 16-row tiles per wave
-  static constexpr int WN = 4;                  // 16-column tiles per wave
   static constexpr int A_BYTES = BM * 128;
   static constexpr int B_BYTES = BN * 128;
   static constexpr int STAGE = A_BYTES + B_BYTES;
-  static constexpr int AI = BM / 64;  // A DMA instructions per wave per step (8 rows each)
-  static constexpr int BJ = BN / 64;  // B DMA instructions per wave per step
-  static constexpr int EPI = 64 * (BN + 4) * 4;
+  static constexpr int AI = BM / 64;            // A DMA instructions per wave per step (8 rows each)
+  static constexpr int BJ = (BN / 8 + 7) / 8;   // B DMA instructions per wave per step (<= BN / 8 in all)
+  static constexpr int CPR = BN / 8;            // epilogue: 8-channel chunks per row
+  static constexpr int RPI = 512 / CPR;         // epilogue rows per iteration
+  static constexpr int PH = RPI > 64 ? RPI : 64;  // epilogue rows per LDS pass
+  static constexpr int EPI = PH * (BN + 4) * 4;
   static constexpr int LDS = 2 * STAGE > EPI ? 2 * STAGE : EPI;
-  static_assert(WAVES_M * WAVES_N == 8 && WM >= 1, "tile");
+  static_assert(WAVES_M * WAVES_N == 8 && WM >= 1 && BM % PH == 0, "tile");
 };
 
 __device__ __forceinline__ int q_xcd_remap(int bid, int nwg) {
@@ -120,7 +123,7 @@ struct Q32Cursor {
 };
 
 template <int BM, int BN>
-__device__ __forceinline__ void q32_epilogue(const ConvOp& op, f32x4_q (&acc)[Q32Cfg<BM, BN>::WM][4],
+__device__ __forceinline__ void q32_epilogue(const ConvOp& op, f32x4_q (&acc)[Q32Cfg<BM, BN>::WM][Q32Cfg<BM, BN>::WN],
                                              unsigned char* smem, int m0, int n0, int M, int HW) {
   using C = Q32Cfg<BM, BN>;
   const int tid = threadIdx.x;
@@ -131,8 +134,8 @@ __device__ __forceinline__ void q32_epilogue(const ConvOp& op, f32x4_q (&acc)[Q3
   const int fr = lane & 15;
   const int fg = lane >> 4;
   constexpr int EST = BN + 4;
-  constexpr int CPR = BN / 8;     // 8-channel chunks per row
-  constexpr int RPI = 512 / CPR;  // rows per iteration
+  constexpr int CPR = C::CPR, RPI = C::RPI, PH = C::PH;
+  constexpr int WN = C::WN;
   float* Es = (float*)smem;
   const int col8 = tid % CPR;
   const int nch = n0 + col8 * 8;
@@ -149,23 +152,23 @@ __device__ __forceinline__ void q32_epilogue(const ConvOp& op, f32x4_q (&acc)[Q3
   float* out = (float*)op.out;
   __syncthreads();  // every wave is done with the last stage
 #pragma unroll 1
-  for (int p = 0; p < BM / 64; ++p) {
+  for (int p = 0; p < BM / PH; ++p) {
 #pragma unroll
     for (int a = 0; a < C::WM; ++a) {
       const int t16 = wm * C::WM + a;  // 16-row tile index within the block tile
-      if (t16 / 4 == p) {
+      if (t16 / (PH / 16) == p) {
 #pragma unroll
-        for (int b = 0; b < 4; ++b)
+        for (int b = 0; b < WN; ++b)
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            Es[((t16 % 4) * 16 + fg * 4 + i) * EST + wn * 64 + b * 16 + fr] = acc[a][b][i];
+            Es[((t16 % (PH / 16)) * 16 + fg * 4 + i) * EST + wn * WN * 16 + b * 16 + fr] = acc[a][b][i];
       }
     }
     __syncthreads();
 #pragma unroll
-    for (int it = 0; it < 64 / RPI; ++it) {
+    for (int it = 0; it < PH / RPI; ++it) {
       const int row = tid / CPR + it * RPI;
-      const int m = m0 + p * 64 + row;
+      const int m = m0 + p * PH + row;
       if (m < M) {
         const f32x4_q lo = *(const f32x4_q*)(Es + row * EST + col8 * 8);
         const f32x4_q hi = *(const f32x4_q*)(Es + row * EST + col8 * 8 + 4);
@@ -292,46 +295,50 @@ __global__ __launch_bounds__(512, 2 * OCC) void conv_wide32_kernel(ConvOp op) {
     const int kb = cur.kb();
 #pragma unroll
     for (int j = 0; j < C::BJ; ++j) {
-      const int n = wave * (BN / 8) + j * 8 + q8;
-      const int ch = qc ^ ((n >> 1) & 7);  // (BN / 8 = 8: the wave term does not vanish)
-      q_glds16(Wt + (size_t)(n0 + n) * op.Kpad + kb + ch * 4, Bs + (wave * (BN / 8) + j * 8) * 128);
+      const int t = wave + 8 * j;  // 8-row group of B rows
+      if (BN / 8 >= 8 * (j + 1) || t < BN / 8) {
+        const int n = t * 8 + q8;
+        const int ch = qc ^ ((n >> 1) & 7);
+        q_glds16(Wt + (size_t)(n0 + n) * op.Kpad + kb + ch * 4, Bs + t * 8 * 128);
+      }
     }
     cur.advance();
   };
 
-  f32x4_q acc[WM][4];
+  constexpr int WN = C::WN;
+  f32x4_q acc[WM][WN];
 #pragma unroll
   for (int a = 0; a < WM; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4_q{0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < WN; ++b) acc[a][b] = f32x4_q{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15;
   const int fg = lane >> 4;
   const int rsw = (fr >> 1) & 7;
 
   // fragments of one half step (chunk kk*4 + fg of each row)
-  auto rd = [&](int buf, int kk, f32x4_q (&af)[WM], f32x4_q (&bf)[4]) {
+  auto rd = [&](int buf, int kk, f32x4_q (&af)[WM], f32x4_q (&bf)[WN]) {
     const float* As = (const float*)(smem + buf * C::STAGE);
     const float* Bs = As + C::A_BYTES / 4;
     const int pc = ((kk * 4 + fg) ^ rsw) * 4;
 #pragma unroll
-    for (int b = 0; b < 4; ++b) bf[b] = *(const f32x4_q*)(Bs + (wn * 64 + b * 16 + fr) * 32 + pc);
+    for (int b = 0; b < WN; ++b) bf[b] = *(const f32x4_q*)(Bs + (wn * WN * 16 + b * 16 + fr) * 32 + pc);
 #pragma unroll
     for (int a = 0; a < WM; ++a) af[a] = *(const f32x4_q*)(As + (wm * WM * 16 + a * 16 + fr) * 32 + pc);
   };
-  auto mm = [&](const f32x4_q (&af)[WM], const f32x4_q (&bf)[4]) {
+  auto mm = [&](const f32x4_q (&af)[WM], const f32x4_q (&bf)[WN]) {
 #pragma unroll
     for (int e = 0; e < 4; ++e)
 #pragma unroll
       for (int a = 0; a < WM; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b)
+        for (int b = 0; b < WN; ++b)
           acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[a][e], bf[b][e], acc[a][b], 0, 0, 0);
   };
   // one fragment read of the next half beside each group of MFMAs of this one
   auto interleave = [&]() {
-    constexpr int NR = WM + 4;
-    constexpr int NM = 4 * WM * 4;
+    constexpr int NR = WM + WN;
+    constexpr int NM = 4 * WM * WN;
 #pragma unroll
     for (int k = 0; k < NR; ++k) {
       __builtin_amdgcn_sched_group_barrier(0x008, NM / NR, 0);
@@ -339,7 +346,7 @@ __global__ __launch_bounds__(512, 2 * OCC) void conv_wide32_kernel(ConvOp op) {
     }
   };
 
-  f32x4_q a0[WM], b0[4], a1[WM], b1[4];
+  f32x4_q a0[WM], b0[WN], a1[WM], b1[WN];
   if constexpr (!PIPE) {
     if (total_steps > 0) issue(0);
     for (int step = 0; step < total_steps; ++step) {
@@ -415,7 +422,9 @@ static int w32_env(const char* name, int dflt) {
 int launch_conv_wide32(const ConvOp& op, hipStream_t st) {
   static const int mode = w32_env("UPR_WIDE32", -1);
   if (mode == 0) return kErrUnsupported;
-  if (op.store == kStoreHeadIllu || op.N % 64) return kErrUnsupported;
+  if (op.store == kStoreHeadIllu || op.N % 32) return kErrUnsupported;
+  static const int n32 = w32_env("UPR_WIDE32_N32", 0);
+  if (op.N % 64 && !n32) return kErrUnsupported;
   if (op.store == kStoreConvT2x2 && (op.N / 4) % 8) return kErrUnsupported;
   if (op.Kpad % 4 || ((uintptr_t)op.W % 16) || op.scale) return kErrUnsupported;
   if (op.out_cs % 4 || op.out_coff % 4 || ((uintptr_t)op.out % 16)) return kErrUnsupported;
@@ -430,6 +439,11 @@ int launch_conv_wide32(const ConvOp& op, hipStream_t st) {
     steps += sg.kh * sg.kw * (sg.C / Q_BK);
   }
   const bool n128 = op.N % 128 == 0;
+  if (op.N % 64) {  // 32-wide (UPR_WIDE32_N32=1: 1 = 256 x 32 one block per CU, 2 = 256 x 32 two, 3 = 512 x 32 one)
+    if (n32 == 2) return launch_w32<256, 32, 2>(op, steps, st);
+    if (n32 == 3) return launch_w32<512, 32, 1>(op, steps, st);
+    return launch_w32<256, 32, 1>(op, steps, st);
+  }
   switch (mode) {
     case 1: if (n128) return launch_w32<256, 128, 1>(op, steps, st); break;
     case 2: if (n128) return launch_w32<128, 128, 2>(op, steps, st); break;

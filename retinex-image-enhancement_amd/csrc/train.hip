@@ -45,6 +45,36 @@ static inline int grid_for(long long n, int per = 256, int cap = 65536) {
 
 #define LAUNCH_CHECK() return (int)hipGetLastError()
 
+// train_small.hip: pixel-tiled / MFMA forms of the small-channel convs
+int small_conv_fwd(const UprView* xv, int B, int H, int W, int Cin, const float* w, const float* bias, int Cout,
+                   int kh, int kw, int stride, int pad, int dil, const UprView* yv, int Ho, int Wo, int relu,
+                   int accumulate, hipStream_t st);
+int small_conv_dgrad(const UprView* dyv, int Ho, int Wo, const float* w, int B, int H, int W, int Cin, int Cout,
+                     int kh, int kw, int stride, int pad, int dil, const UprView* dxv, int accumulate, hipStream_t st);
+int small_conv_wgrad(const UprView* xv, const UprView* dyv, int B, int H, int W, int Cin, int Ho, int Wo, int Cout,
+                     int kh, int kw, int stride, int pad, int dil, float* dw, float* dbias, hipStream_t st);
+// train_wgrad.hip: split-K GEMM weight gradient (UPR_WGRAD_GEMM=0: round-1 kernel)
+int wgrad_gemm(const float* x, int B, int H, int W, int Cin, int x_cs, int x_coff, const float* dy, int Ho, int Wo,
+               int Cout, int dy_cs, int dy_coff, int kh, int kw, int stride, int pad, int dil, float* dwp,
+               hipStream_t st);
+static bool wgrad_gemm_on() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("UPR_WGRAD_GEMM");
+    on = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  return on == 1;
+}
+// UPR_TRAIN_SMALL=0 keeps the round-1 per-element kernels (A/B timing)
+static bool small_kernels_on() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("UPR_TRAIN_SMALL");
+    on = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  return on == 1;
+}
+
 // ---------------------------------------------------------------------------
 // Direct convolution (small channel counts): forward / dgrad / wgrad
 // ---------------------------------------------------------------------------
@@ -1453,6 +1483,11 @@ int upr_t_conv_direct(const UprView* x, int B, int H, int W, int Cin, const floa
     return UPR_ERR_ARG;
   if (Ho != (H + 2 * pad - dil * (kh - 1) - 1) / stride + 1 || Wo != (W + 2 * pad - dil * (kw - 1) - 1) / stride + 1)
     return UPR_ERR_SHAPE;
+  if (small_kernels_on()) {
+    const int rc = small_conv_fwd(x, B, H, W, Cin, w, bias, Cout, kh, kw, stride, pad, dil, y, Ho, Wo, relu,
+                                  accumulate, ST(stream));
+    if (rc != kErrUnsupported) return rc;
+  }
   const long long n = (long long)B * Ho * Wo * Cout;
   if (Cin == 3 && kh == 3 && kw == 3 && stride == 1 && dil == 1) {
     hipLaunchKernelGGL(conv_direct_c3k3_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), mkv(x), B, H, W, w, bias,
@@ -1468,6 +1503,11 @@ int upr_t_conv_direct_dgrad(const UprView* dy, int Ho, int Wo, const float* w, i
                             int kh, int kw, int stride, int pad, int dil, const UprView* dx, int accumulate,
                             void* stream) {
   if (!dy || !dx || !dy->data || !dx->data || !w || B <= 0 || stride <= 0 || dil <= 0) return UPR_ERR_ARG;
+  if (small_kernels_on()) {
+    const int rc = small_conv_dgrad(dy, Ho, Wo, w, B, H, W, Cin, Cout, kh, kw, stride, pad, dil, dx, accumulate,
+                                    ST(stream));
+    if (rc != kErrUnsupported) return rc;
+  }
   const long long n = (long long)B * H * W * Cin;
   hipLaunchKernelGGL(conv_direct_dgrad_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), mkv(dy), Ho, Wo, w, B, H,
                      W, Cin, Cout, kh, kw, stride, pad, dil, mkv(dx), accumulate);
@@ -1478,6 +1518,10 @@ int upr_t_conv_direct_wgrad(const UprView* x, const UprView* dy, int B, int H, i
                             int Cout, int kh, int kw, int stride, int pad, int dil, float* dw, float* dbias,
                             void* stream) {
   if (!x || !dy || !dw || B <= 0) return UPR_ERR_ARG;
+  if (small_kernels_on()) {
+    const int rc = small_conv_wgrad(x, dy, B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pad, dil, dw, dbias, ST(stream));
+    if (rc != kErrUnsupported) return rc;
+  }
   const int KC = kh * kw * Cin;
   const int nE = Cout * KC + (dbias ? Cout : 0);
   if (nE > 16 * 256) return UPR_ERR_UNSUPPORTED;
@@ -1518,6 +1562,11 @@ int upr_t_conv_wgrad(const float* x, int B, int H, int W, int Cin, int x_cs, int
                      int Wo, int Cout, int dy_cs, int dy_coff, int kh, int kw, int stride, int pad, int dil,
                      float* dwp, void* stream) {
   if (!x || !dy || !dwp || B <= 0 || Cin % 32 || Cout % 32 || Cin <= 0 || Cout <= 0) return UPR_ERR_ARG;
+  if (wgrad_gemm_on()) {
+    const int rc = wgrad_gemm(x, B, H, W, Cin, x_cs, x_coff, dy, Ho, Wo, Cout, dy_cs, dy_coff, kh, kw, stride, pad, dil,
+                              dwp, ST(stream));
+    if (rc != kErrUnsupported) return rc;
+  }
   const long long P = (long long)B * Ho * Wo;
   const long long chunks = (P + WG_PPB - 1) / WG_PPB;
   if (chunks > 0x7fffffff) return UPR_ERR_SHAPE;

@@ -1,0 +1,474 @@
+// Small-channel convolutions of the training step (the convs whose Cin or Cout
+// is not a multiple of 32, so they cannot take the MFMA implicit-GEMM path):
+// the 3-channel 3x3 input convs (ResidualIENet.input_layer and the three
+// multi-scale branch convs, models/model.py:293,419-425; VGG-19 conv1_1 of the
+// perceptual loss, losses/loss.py:198-211), the 32->3 / 32->1 heads
+// (model.py:402,326), the 7x7 2->1 spatial attention and the channel-attention
+// squeeze convs of EnhancedFAM (model.py:47-59).
+//
+// Round 1 ran them as one thread per OUTPUT ELEMENT with 64-bit index math
+// (26 % of the bs-8 512^2 step).  Here:
+//   * forward (3 -> COUT 3x3): one thread per output PIXEL computes all COUT
+//     channels from its 27 inputs (weights broadcast from LDS), the tile's
+//     outputs are transposed through LDS and leave as 16-byte row stores;
+//   * input gradient (stride 1): one thread per input pixel accumulates all
+//     CIN input-channel gradients over (tap, Cout), weights broadcast from LDS;
+//   * weight gradient (Cout <= 32): a GEMM over pixels on
+//     v_mfma_f32_32x32x2_f32 (D[co][k] += dy[p][co] * im2col[p][k], two
+//     pixels per MFMA, k = ci*kh*kw + ky*kw + kx = PyTorch's weight layout,
+//     plus a ones column for the bias), per-block LDS reduction, one atomic
+//     per weight per block.
+// All fp32 (exact-fp32 MFMA); only the summation order differs from a serial
+// loop.
+#include <cstdlib>
+#include <cstring>
+
+#include "upr_common.h"
+#include "../../include/upr.h"
+#include "../../include/upr_train.h"
+
+namespace upr {
+
+typedef float f32x4_t2 __attribute__((ext_vector_type(4)));
+typedef float f32x16_t2 __attribute__((ext_vector_type(16)));
+
+struct SV {
+  float* d;
+  long long sb, sh, sw, sc;
+  __device__ __forceinline__ long long at(int b, int y, int x, int c) const {
+    return b * sb + y * sh + x * sw + c * sc;
+  }
+};
+
+static SV mksv(const UprView* u) {
+  SV v;
+  v.d = (float*)u->data;
+  v.sb = u->sb; v.sh = u->sh; v.sw = u->sw; v.sc = u->sc;
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// forward: 3 -> COUT, 3x3, stride 1, dilation 1, padding p
+// ---------------------------------------------------------------------------
+template <int COUT>
+__global__ __launch_bounds__(256) void c3k3_fwd_kernel(SV x, int B, int H, int W, const float* __restrict__ w,
+                                                      const float* __restrict__ bias, int p, SV y, int Ho, int Wo,
+                                                      int relu, int accum) {
+  constexpr int TS = COUT + 4;  // LDS row stride (floats): 16-byte aligned rows, spread banks
+  extern __shared__ __attribute__((aligned(16))) float sm3[];
+  float* sw_ = sm3;                  // [27][COUT] weights, k-major (broadcast reads)
+  float* sb_ = sm3 + 27 * COUT;      // [COUT]
+  float* tile = sb_ + COUT;          // [256][TS]
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 27 * COUT; i += 256) {
+    const int co = i / 27, k = i - co * 27;
+    sw_[k * COUT + co] = w[i];
+  }
+  for (int i = tid; i < COUT; i += 256) sb_[i] = bias ? bias[i] : 0.f;
+  __syncthreads();
+  const int P = B * Ho * Wo;
+  const int p0 = blockIdx.x * 256;
+  const int pix = p0 + tid;
+  if (pix < P) {
+    const int ox = pix % Wo;
+    const int r = pix / Wo;
+    const int oy = r % Ho, b = r / Ho;
+    float in[27];
+#pragma unroll
+    for (int ci = 0; ci < 3; ++ci)
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        const int iy = oy - p + ky;
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const int ix = ox - p + kx;
+          const bool ok = iy >= 0 && iy < H && ix >= 0 && ix < W;
+          in[(ci * 3 + ky) * 3 + kx] = ok ? x.d[x.at(b, iy, ix, ci)] : 0.f;
+        }
+      }
+    float acc[COUT];
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) acc[co] = sb_[co];
+    // same accumulation order as the serial form: ci, ky, kx
+#pragma unroll
+    for (int k = 0; k < 27; ++k) {
+#pragma unroll
+      for (int co = 0; co < COUT; co += 4) {
+        const f32x4_t2 wv = *(const f32x4_t2*)(sw_ + k * COUT + co);
+        acc[co] = fmaf(in[k], wv[0], acc[co]);
+        acc[co + 1] = fmaf(in[k], wv[1], acc[co + 1]);
+        acc[co + 2] = fmaf(in[k], wv[2], acc[co + 2]);
+        acc[co + 3] = fmaf(in[k], wv[3], acc[co + 3]);
+      }
+    }
+#pragma unroll
+    for (int co = 0; co < COUT; co += 4)
+      *(f32x4_t2*)(tile + tid * TS + co) = f32x4_t2{acc[co], acc[co + 1], acc[co + 2], acc[co + 3]};
+  }
+  __syncthreads();
+  // copy-out: consecutive lanes store consecutive 16-byte chunks of a pixel's
+  // channel run (y.sc == 1, checked by the host)
+  constexpr int CQ = COUT / 4;
+  for (int it = tid; it < 256 * CQ; it += 256) {
+    const int lp = it / CQ, q = it - lp * CQ;
+    const int pp = p0 + lp;
+    if (pp >= P) break;
+    const int ox = pp % Wo;
+    const int r = pp / Wo;
+    const int oy = r % Ho, b = r / Ho;
+    f32x4_t2 v = *(const f32x4_t2*)(tile + lp * TS + q * 4);
+    f32x4_t2* dst = (f32x4_t2*)(y.d + y.at(b, oy, ox, q * 4));
+    if (accum) v += *dst;
+    if (relu) {
+      v[0] = fmaxf(v[0], 0.f); v[1] = fmaxf(v[1], 0.f); v[2] = fmaxf(v[2], 0.f); v[3] = fmaxf(v[3], 0.f);
+    }
+    *dst = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// forward, COUT <= 4 output channels (32->3 / 32->1 1x1 heads, 7x7 2->1
+// spatial attention): one thread per output pixel, all taps and input channels
+// (16-byte loads when the input rows are channel-contiguous and aligned)
+// ---------------------------------------------------------------------------
+template <int COUT>
+__global__ __launch_bounds__(256) void small_fwd_kernel(SV x, int B, int H, int W, int Cin,
+                                                        const float* __restrict__ w, const float* __restrict__ bias,
+                                                        int kh, int kw, int s, int p, int d, SV y, int Ho, int Wo,
+                                                        int relu, int accum, int xvec) {
+  extern __shared__ __attribute__((aligned(16))) float smf[];  // [tap][ci][COUT]
+  const int taps = kh * kw;
+  const int nw = COUT * Cin * taps;
+  for (int i = threadIdx.x; i < nw; i += 256) {
+    const int co = i / (Cin * taps);
+    const int rem = i - co * Cin * taps;
+    const int ci = rem / taps, tap = rem - ci * taps;
+    smf[(tap * Cin + ci) * COUT + co] = w[i];
+  }
+  __syncthreads();
+  const int P = B * Ho * Wo;
+  const int pix = blockIdx.x * 256 + threadIdx.x;
+  if (pix >= P) return;
+  const int ox = pix % Wo;
+  const int r = pix / Wo;
+  const int oy = r % Ho, b = r / Ho;
+  float acc[COUT];
+#pragma unroll
+  for (int c = 0; c < COUT; ++c) acc[c] = bias ? bias[c] : 0.f;
+  for (int ky = 0; ky < kh; ++ky) {
+    const int iy = oy * s - p + ky * d;
+    if (iy < 0 || iy >= H) continue;
+    for (int kx = 0; kx < kw; ++kx) {
+      const int ix = ox * s - p + kx * d;
+      if (ix < 0 || ix >= W) continue;
+      const float* xp = x.d + x.at(b, iy, ix, 0);
+      const float* wt = smf + (ky * kw + kx) * Cin * COUT;
+      int ci = 0;
+      if (xvec) {
+        for (; ci + 4 <= Cin; ci += 4) {
+          const f32x4_t2 v = *(const f32x4_t2*)(xp + ci);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int c = 0; c < COUT; ++c) acc[c] = fmaf(v[e], wt[(ci + e) * COUT + c], acc[c]);
+        }
+      }
+      for (; ci < Cin; ++ci) {
+        const float v = xp[ci * x.sc];
+#pragma unroll
+        for (int c = 0; c < COUT; ++c) acc[c] = fmaf(v, wt[ci * COUT + c], acc[c]);
+      }
+    }
+  }
+  float* yp = y.d + y.at(b, oy, ox, 0);
+#pragma unroll
+  for (int c = 0; c < COUT; ++c) {
+    float v = acc[c];
+    if (accum) v += yp[c * y.sc];
+    if (relu) v = fmaxf(v, 0.f);
+    yp[c * y.sc] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// input gradient, stride 1: dx[b,iy,ix,ci] (+)= sum_{ky,kx,co} dy[b,iy+p-ky*d,ix+p-kx*d,co] w[co][ci][ky][kx]
+// ---------------------------------------------------------------------------
+template <int CIN, int COUTT>
+__global__ __launch_bounds__(256) void small_dgrad_kernel(SV dy, int Ho, int Wo, const float* __restrict__ w, int B,
+                                                          int H, int W, int Cout, int kh, int kw, int p, int d, SV dx,
+                                                          int accum, int vec, int dvec) {
+  extern __shared__ __attribute__((aligned(16))) float smd[];  // [tap][co][CIN]
+  const int taps = kh * kw;
+  const int nw = Cout * taps * CIN;
+  for (int i = threadIdx.x; i < nw; i += 256) {
+    const int co = i / (CIN * taps);
+    const int rem = i - co * CIN * taps;
+    const int ci = rem / taps, tap = rem - ci * taps;
+    smd[(tap * Cout + co) * CIN + ci] = w[i];
+  }
+  __syncthreads();
+  const int P = B * H * W;
+  const int pix = blockIdx.x * 256 + threadIdx.x;
+  if (pix >= P) return;
+  const int ix = pix % W;
+  const int r = pix / W;
+  const int iy = r % H, b = r / H;
+  float acc[CIN];
+#pragma unroll
+  for (int c = 0; c < CIN; ++c) acc[c] = 0.f;
+  for (int ky = 0; ky < kh; ++ky) {
+    const int oy = iy + p - ky * d;
+    if (oy < 0 || oy >= Ho) continue;
+    for (int kx = 0; kx < kw; ++kx) {
+      const int ox = ix + p - kx * d;
+      if (ox < 0 || ox >= Wo) continue;
+      const float* dyp = dy.d + dy.at(b, oy, ox, 0);
+      const float* wt = smd + (ky * kw + kx) * Cout * CIN;
+      int co = 0;
+      if (COUTT > 0 && dvec) {  // compile-time Cout: the tap's loads all in flight, then the FMAs
+        f32x4_t2 g4[COUTT > 0 ? COUTT / 4 : 1];
+#pragma unroll
+        for (int q = 0; q < COUTT / 4; ++q) g4[q] = *(const f32x4_t2*)(dyp + 4 * q);
+#pragma unroll
+        for (int q = 0; q < COUTT / 4; ++q)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int c = 0; c < CIN; ++c) acc[c] = fmaf(g4[q][e], wt[(4 * q + e) * CIN + c], acc[c]);
+        co = COUTT;
+      }
+      if (dvec) {  // channel-contiguous, 16-byte aligned dy rows: 4 channels per load
+        for (; co + 4 <= Cout; co += 4) {
+          const f32x4_t2 g4 = *(const f32x4_t2*)(dyp + co);
+          const float* wc = wt + co * CIN;
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int c = 0; c < CIN; ++c) acc[c] = fmaf(g4[q], wc[q * CIN + c], acc[c]);
+        }
+      }
+      for (; co < Cout; ++co) {
+        const float g = dyp[co * dy.sc];
+        const float* wc = wt + co * CIN;
+#pragma unroll
+        for (int c = 0; c < CIN; ++c) acc[c] = fmaf(g, wc[c], acc[c]);
+      }
+    }
+  }
+  float* xp = dx.d + dx.at(b, iy, ix, 0);
+  if (CIN % 4 == 0 && vec) {  // channel-contiguous, 16-byte aligned rows (host-checked)
+#pragma unroll
+    for (int c = 0; c < CIN; c += 4) {
+      f32x4_t2 v = f32x4_t2{acc[c], acc[c + 1], acc[c + 2], acc[c + 3]};
+      if (accum) v += *(const f32x4_t2*)(xp + c);
+      *(f32x4_t2*)(xp + c) = v;
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < CIN; ++c) {
+      float v = acc[c];
+      if (accum) v += xp[c * dx.sc];
+      xp[c * dx.sc] = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// weight gradient, Cout <= 32: D[co][k] = sum_p dy[p][co] * col[p][k] on
+// v_mfma_f32_32x32x2_f32 (A = dy rows, B = im2col rows, K = 2 pixels)
+// ---------------------------------------------------------------------------
+constexpr int SW_UNROLL = 8;  // pixel pairs in flight per wave
+
+template <int NT>
+__global__ __launch_bounds__(256) void small_wgrad_mfma_kernel(SV x, SV dy, int B, int H, int W, int Cin, int Ho,
+                                                               int Wo, int Cout, int kh, int kw, int s, int p, int d,
+                                                               int pairs_per_wave, float* __restrict__ dw,
+                                                               float* __restrict__ dbias) {
+  __shared__ __attribute__((aligned(16))) float red[4][NT][16][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int j = lane & 31, half = lane >> 5;
+  const int taps = kh * kw;
+  const int KC = Cin * taps;
+  const int P = B * Ho * Wo;
+  // per lane, per 32-column tile: this lane's im2col column k = t*32 + j
+  int c_off[NT], c_dy[NT], c_dx[NT], c_kind[NT];  // kind: 0 zero, 1 pixel value, 2 ones (bias)
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int k = t * 32 + j;
+    c_kind[t] = 0; c_off[t] = 0; c_dy[t] = 0; c_dx[t] = 0;
+    if (k < KC) {
+      const int ci = k / taps, tap = k - ci * taps;
+      const int ky = tap / kw, kx = tap - ky * kw;
+      c_kind[t] = 1;
+      c_off[t] = ci;
+      c_dy[t] = ky * d - p;
+      c_dx[t] = kx * d - p;
+    } else if (k == KC && dbias) {
+      c_kind[t] = 2;
+    }
+  }
+  f32x16_t2 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
+  const long long gw = (long long)blockIdx.x * 4 + wave;
+  const long long pair0 = gw * pairs_per_wave;
+  for (int u0 = 0; u0 < pairs_per_wave; u0 += SW_UNROLL) {
+    float av[SW_UNROLL], bv[SW_UNROLL][NT];
+#pragma unroll
+    for (int u = 0; u < SW_UNROLL; ++u) {
+      const long long pix = (pair0 + u0 + u) * 2 + half;
+      av[u] = 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) bv[u][t] = 0.f;
+      if (u0 + u < pairs_per_wave && pix < P) {
+        const int ox = (int)(pix % Wo);
+        const int r = (int)(pix / Wo);
+        const int oy = r % Ho, b = r / Ho;
+        if (j < Cout) av[u] = dy.d[dy.at(b, oy, ox, j)];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          if (c_kind[t] == 1) {
+            const int iy = oy * s + c_dy[t], ix = ox * s + c_dx[t];
+            if (iy >= 0 && iy < H && ix >= 0 && ix < W) bv[u][t] = x.d[x.at(b, iy, ix, c_off[t])];
+          } else if (c_kind[t] == 2) {
+            bv[u][t] = 1.f;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < SW_UNROLL; ++u)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u][t], acc[t], 0, 0, 0);
+  }
+  // block reduction over the 4 waves, then one atomic per (co, k)
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) red[wave][t][e][lane] = acc[t][e];
+  __syncthreads();
+  for (int idx = tid; idx < NT * 16 * 64; idx += 256) {
+    const int t = idx / (16 * 64);
+    const int rem = idx - t * 16 * 64;
+    const int e = rem / 64, l = rem - e * 64;
+    const float v = red[0][t][e][l] + red[1][t][e][l] + red[2][t][e][l] + red[3][t][e][l];
+    // 32x32 accumulator map: column = l & 31, row = (e & 3) + 8 * (e >> 2) + 4 * (l >> 5)
+    const int co = (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
+    const int k = t * 32 + (l & 31);
+    if (co >= Cout) continue;
+    if (k < KC) atomicAdd(dw + (size_t)co * KC + k, v);
+    else if (k == KC && dbias) atomicAdd(dbias + co, v);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host entries (called from train.hip's upr_t_conv_direct*; kErrUnsupported
+// sends the caller to the generic kernels)
+// ---------------------------------------------------------------------------
+int small_conv_fwd(const UprView* xv, int B, int H, int W, int Cin, const float* w, const float* bias, int Cout,
+                   int kh, int kw, int stride, int pad, int dil, const UprView* yv, int Ho, int Wo, int relu,
+                   int accumulate, hipStream_t st) {
+  if (Cout <= 4) {
+    if ((long long)B * Ho * Wo >= (1ll << 31)) return kErrUnsupported;
+    const size_t lds = sizeof(float) * (size_t)Cout * Cin * kh * kw;
+    if (lds > 48 * 1024) return kErrUnsupported;
+    const SV x = mksv(xv), y = mksv(yv);
+    const int xvec = x.sc == 1 && x.sw % 4 == 0 && x.sh % 4 == 0 && x.sb % 4 == 0 && (uintptr_t)x.d % 16 == 0;
+    const int grid = (B * Ho * Wo + 255) / 256;
+#define UPR_SMALL_FWD(C)                                                                                         \
+  hipLaunchKernelGGL(small_fwd_kernel<C>, dim3(grid), dim3(256), lds, st, x, B, H, W, Cin, w, bias, kh, kw, stride, \
+                     pad, dil, y, Ho, Wo, relu, accumulate, xvec)
+    switch (Cout) {
+      case 1: UPR_SMALL_FWD(1); break;
+      case 2: UPR_SMALL_FWD(2); break;
+      case 3: UPR_SMALL_FWD(3); break;
+      default: UPR_SMALL_FWD(4); break;
+    }
+#undef UPR_SMALL_FWD
+    return (int)hipGetLastError();
+  }
+  if (Cin != 3 || kh != 3 || kw != 3 || stride != 1 || dil != 1) return kErrUnsupported;
+  if (Cout != 32 && Cout != 64) return kErrUnsupported;
+  if (yv->sc != 1 || yv->sw % 4 || yv->sh % 4 || yv->sb % 4 || ((uintptr_t)yv->data % 16)) return kErrUnsupported;
+  if ((long long)B * Ho * Wo >= (1ll << 31)) return kErrUnsupported;
+  const SV x = mksv(xv), y = mksv(yv);
+  const int P = B * Ho * Wo;
+  const int grid = (P + 255) / 256;
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)c3k3_fwd_kernel<64>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  if (Cout == 32) {
+    const size_t lds = sizeof(float) * (27 * 32 + 32 + 256 * 36);
+    hipLaunchKernelGGL(c3k3_fwd_kernel<32>, dim3(grid), dim3(256), lds, st, x, B, H, W, w, bias, pad, y, Ho, Wo, relu,
+                       accumulate);
+  } else {
+    const size_t lds = sizeof(float) * (27 * 64 + 64 + 256 * 68);
+    hipLaunchKernelGGL(c3k3_fwd_kernel<64>, dim3(grid), dim3(256), lds, st, x, B, H, W, w, bias, pad, y, Ho, Wo, relu,
+                       accumulate);
+  }
+  return (int)hipGetLastError();
+}
+
+int small_conv_dgrad(const UprView* dyv, int Ho, int Wo, const float* w, int B, int H, int W, int Cin, int Cout,
+                     int kh, int kw, int stride, int pad, int dil, const UprView* dxv, int accumulate, hipStream_t st) {
+  if (stride != 1) return kErrUnsupported;
+  if ((long long)B * H * W >= (1ll << 31)) return kErrUnsupported;
+  const size_t lds = sizeof(float) * (size_t)Cout * kh * kw * Cin;
+  if (lds > 64 * 1024) return kErrUnsupported;
+  const SV dy = mksv(dyv), dx = mksv(dxv);
+  const int grid = (B * H * W + 255) / 256;
+  const int vec = dx.sc == 1 && dx.sw % 4 == 0 && dx.sh % 4 == 0 && dx.sb % 4 == 0 && (uintptr_t)dx.d % 16 == 0;
+  const int dvec = dy.sc == 1 && dy.sw % 4 == 0 && dy.sh % 4 == 0 && dy.sb % 4 == 0 && (uintptr_t)dy.d % 16 == 0;
+#define UPR_SMALL_DGRAD(C, CO)                                                                                       \
+  hipLaunchKernelGGL((small_dgrad_kernel<C, CO>), dim3(grid), dim3(256), lds, st, dy, Ho, Wo, w, B, H, W, Cout, kh, kw, \
+                     pad, dil, dx, accumulate, vec, dvec)
+  switch (Cin) {
+    case 1: UPR_SMALL_DGRAD(1, 0); break;
+    case 2: UPR_SMALL_DGRAD(2, 0); break;
+    case 3:
+      if (Cout == 64) UPR_SMALL_DGRAD(3, 64);  // VGG-19 conv1_1 (loss.py:198-211)
+      else UPR_SMALL_DGRAD(3, 0);
+      break;
+    case 32: UPR_SMALL_DGRAD(32, 0); break;
+    default: return kErrUnsupported;
+  }
+#undef UPR_SMALL_DGRAD
+  return (int)hipGetLastError();
+}
+
+int small_conv_wgrad(const UprView* xv, const UprView* dyv, int B, int H, int W, int Cin, int Ho, int Wo, int Cout,
+                     int kh, int kw, int stride, int pad, int dil, float* dw, float* dbias, hipStream_t st) {
+  if (Cout > 32) return kErrUnsupported;
+  const int KC = Cin * kh * kw + (dbias ? 1 : 0);
+  const int nt = (KC + 31) / 32;
+  if (nt > 4) return kErrUnsupported;
+  const long long P = (long long)B * Ho * Wo;
+  if (P >= (1ll << 31)) return kErrUnsupported;
+  const long long pairs = (P + 1) / 2;
+  // ~2048 waves (8 per CU), pairs per wave a multiple of the unroll
+  long long ppw = (pairs + 2047) / 2048;
+  ppw = (ppw + SW_UNROLL - 1) / SW_UNROLL * SW_UNROLL;
+  if (ppw < SW_UNROLL) ppw = SW_UNROLL;
+  const long long waves = (pairs + ppw - 1) / ppw;
+  const int grid = (int)((waves + 3) / 4);
+  const SV x = mksv(xv), dy = mksv(dyv);
+#define UPR_SMALL_WGRAD(T)                                                                                          \
+  hipLaunchKernelGGL(small_wgrad_mfma_kernel<T>, dim3(grid), dim3(256), 0, st, x, dy, B, H, W, Cin, Ho, Wo, Cout, kh, \
+                     kw, stride, pad, dil, (int)ppw, dw, dbias)
+  switch (nt) {
+    case 1: UPR_SMALL_WGRAD(1); break;
+    case 2: UPR_SMALL_WGRAD(2); break;
+    case 3: UPR_SMALL_WGRAD(3); break;
+    default: UPR_SMALL_WGRAD(4); break;
+  }
+#undef UPR_SMALL_WGRAD
+  return (int)hipGetLastError();
+}
+
+}  // namespace upr

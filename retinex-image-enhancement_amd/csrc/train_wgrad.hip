@@ -1,0 +1,242 @@
+// Weight gradient of the MFMA-path convs of the training step as a split-K
+// GEMM over pixels (replaces round 1's per-tap 32x32 kernel with fp32
+// atomics, 17 % of the bs-8 512^2 step at 0.27 of the fp32 MFMA peak):
+//
+//   dW[co][k] = sum_p dy[p][co] * im2col(x)[p][k],   k = (ky, kx, ci)
+//
+// * M = Cout, N = kh*kw*Cin, K = the B*Ho*Wo output pixels, split into
+//   `splits` contiguous pixel ranges.  Block tile BM x BN (4 waves, each a
+//   32 x 64 block of v_mfma_f32_32x32x2_f32 accumulators), K step = 32
+//   pixels.
+// * Both operands global -> LDS by LDS-DMA into two stages (one barrier per
+//   step): A = the dy rows of the step's pixels (BM channels each), B = their
+//   im2col rows (BN/32 runs of 32 channels, each at its tap's shifted pixel;
+//   padded taps / pixels past the range read a zero line).  The MFMA
+//   fragments are single floats: lane l takes row (pixel) 2s + l/32, column
+//   l%32 -- ds_read_b32 over consecutive addresses, conflict free.
+// * Each block writes its partial tile to its split's slab (plain stores);
+//   a second kernel sums the slabs in split order and adds them to dwp:
+//   deterministic (no float atomics), one pass over the slabs.
+// * The slabs live in stream-ordered scratch (hipMallocAsync / hipFreeAsync on
+//   the caller's stream), so concurrent streams never share them.
+#include <cstdlib>
+#include <cstring>
+
+#include "upr_common.h"
+#include "../../include/upr_train.h"
+
+namespace upr {
+
+typedef float f32x4_w2 __attribute__((ext_vector_type(4)));
+typedef float f32x16_w2 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void* lds_void_ptr_w2;
+
+__device__ __attribute__((aligned(128))) uint4 g_wg_zero[8];
+
+constexpr int WG_KP = 32;  // pixels per K step
+
+struct WgArgs {
+  const float* x;
+  int B, H, W, Cin, x_cs, x_coff;
+  const float* dy;
+  int Ho, Wo, Cout, dy_cs, dy_coff;
+  int kh, kw, s, p, d;
+  int KT;       // kh*kw*Cin
+  int P;        // B*Ho*Wo
+  int splits, pix_per_split, mtiles, ntiles, ldn;  // ldn: slab row length (ntiles*BN)
+  float* slab;  // [splits][Cout][ldn]
+};
+
+__device__ __forceinline__ void wg_glds16(const void* g, unsigned char* lds) {
+  __builtin_amdgcn_global_load_lds(g, (lds_void_ptr_w2)lds, 16, 0, 0);
+}
+
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void wgrad_gemm_kernel(WgArgs a) {
+  constexpr int WAVES_N = BN / 64;
+  constexpr int WAVES_M = 4 / WAVES_N;
+  static_assert(WAVES_M * 32 == BM, "tile");
+  constexpr int A_BYTES = WG_KP * BM * 4, B_BYTES = WG_KP * BN * 4, STAGE = A_BYTES + B_BYTES;
+  constexpr int AI = WG_KP * BM / 4 / 256;  // A DMA instructions per wave per step (64 lanes x 16 B each)
+  constexpr int BI = WG_KP * BN / 4 / 256;
+  extern __shared__ __attribute__((aligned(16))) unsigned char wsm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WAVES_M, wn = wave / WAVES_M;
+  int bid = blockIdx.x;
+  const int nt = bid % a.ntiles; bid /= a.ntiles;
+  const int mt = bid % a.mtiles;
+  const int split = bid / a.mtiles;
+  const int co0 = mt * BM, k0 = nt * BN;
+  const int pb = split * a.pix_per_split;
+  const int pe = min(a.P, pb + a.pix_per_split);
+  const int steps = (pe - pb + WG_KP - 1) / WG_KP;
+  const float* zero = (const float*)g_wg_zero;
+  const int HWo = a.Ho * a.Wo;
+  const int cinq = a.Cin / 32;
+
+  auto issue = [&](int step, int stage) {
+    unsigned char* As = wsm + stage * STAGE;
+    unsigned char* Bs = As + A_BYTES;
+    const int ps = pb + step * WG_KP;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int c = (wave * AI + i) * 64 + lane;  // 16-byte chunk of the A tile
+      const int pr = c / (BM / 4), q = c % (BM / 4);
+      const int pix = ps + pr;
+      const float* src = pix < pe ? a.dy + (size_t)pix * a.dy_cs + a.dy_coff + co0 + q * 4 : zero;
+      wg_glds16(src, As + (wave * AI + i) * 1024);
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int c = (wave * BI + i) * 64 + lane;
+      const int pr = c / (BN / 4), q = c % (BN / 4);
+      const int pix = ps + pr;
+      const int k = k0 + q * 4;
+      const float* src = zero;
+      if (pix < pe && k < a.KT) {
+        const int kq = k >> 5;  // 32-channel run: (tap, ci chunk)
+        const int tap = kq / cinq, ci = (kq - tap * cinq) * 32 + (k & 31);
+        const int ky = tap / a.kw, kx = tap - ky * a.kw;
+        const int b = pix / HWo, r = pix - b * HWo;
+        const int oy = r / a.Wo, ox = r - oy * a.Wo;
+        const int iy = oy * a.s - a.p + ky * a.d, ix = ox * a.s - a.p + kx * a.d;
+        if ((unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
+          src = a.x + (size_t)((b * a.H + iy) * a.W + ix) * a.x_cs + a.x_coff + ci;
+      }
+      wg_glds16(src, Bs + (wave * BI + i) * 1024);
+    }
+  };
+
+  f32x16_w2 acc0, acc1;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) { acc0[e] = 0.f; acc1[e] = 0.f; }
+  const int half = lane >> 5, col = lane & 31;
+
+  if (steps > 0) issue(0, 0);
+  for (int step = 0; step < steps; ++step) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (step + 1 < steps) issue(step + 1, (step + 1) & 1);
+    const float* As = (const float*)(wsm + (step & 1) * STAGE);
+    const float* Bs = As + A_BYTES / 4;
+#pragma unroll
+    for (int s = 0; s < WG_KP / 2; ++s) {
+      const int row = 2 * s + half;
+      const float av = As[row * BM + wm * 32 + col];
+      const float b0 = Bs[row * BN + wn * 64 + col];
+      const float b1 = Bs[row * BN + wn * 64 + 32 + col];
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, b0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, b1, acc1, 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // partial tile -> this split's slab; D row = (e&3) + 8*(e>>2) + 4*half, column = lane & 31
+  float* sl = a.slab + ((size_t)split * a.Cout + co0 + wm * 32) * a.ldn + k0 + wn * 64 + col;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int row = (e & 3) + 8 * (e >> 2) + 4 * half;
+    sl[(size_t)row * a.ldn] = acc0[e];
+    sl[(size_t)row * a.ldn + 32] = acc1[e];
+  }
+}
+
+// out[g][co][k] = sum of slabs [g*G, min((g+1)*G, splits)) in order (grid.y = group)
+constexpr int WG_GROUP = 16;
+__global__ __launch_bounds__(256) void wgrad_group_kernel(const float* __restrict__ slab, int splits, int Cout, int KT,
+                                                          int ldn, float* __restrict__ out) {
+  const int n4 = Cout * KT / 4;
+  const int g = blockIdx.y;
+  const int s0 = g * WG_GROUP, s1 = min(splits, s0 + WG_GROUP);
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n4; i += gridDim.x * 256) {
+    const int e = i * 4;
+    const int co = e / KT, k = e - co * KT;  // KT % 4 == 0: a quad never crosses rows
+    f32x4_w2 acc = *(const f32x4_w2*)(slab + ((size_t)s0 * Cout + co) * ldn + k);
+    for (int sp = s0 + 1; sp < s1; ++sp) acc += *(const f32x4_w2*)(slab + ((size_t)sp * Cout + co) * ldn + k);
+    *(f32x4_w2*)(out + ((size_t)g * Cout + co) * ldn + k) = acc;
+  }
+}
+
+// dwp[co][k] += sum over n partial slabs (in order)
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int n, int Cout, int KT,
+                                                           int ldn, float* __restrict__ dwp) {
+  const int n4 = Cout * KT / 4;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n4; i += gridDim.x * 256) {
+    const int e = i * 4;
+    const int co = e / KT, k = e - co * KT;
+    f32x4_w2 acc = *(const f32x4_w2*)(part + (size_t)co * ldn + k);
+    for (int sp = 1; sp < n; ++sp) acc += *(const f32x4_w2*)(part + ((size_t)sp * Cout + co) * ldn + k);
+    f32x4_w2* o = (f32x4_w2*)(dwp + e);
+    *o = *o + acc;
+  }
+}
+
+template <int BM, int BN>
+static int launch_wgrad_gemm(WgArgs a, float* dwp, hipStream_t st) {
+  constexpr int LDS = 2 * WG_KP * (BM + BN) * 4;
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e =
+        hipFuncSetAttribute((const void*)wgrad_gemm_kernel<BM, BN>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  a.mtiles = a.Cout / BM;
+  a.ntiles = (a.KT + BN - 1) / BN;
+  a.ldn = a.ntiles * BN;
+  const int tiles = a.mtiles * a.ntiles;
+  // ~1024 blocks (4 per CU), >= 4 K steps each
+  int splits = (1024 + tiles - 1) / tiles;
+  const int max_splits = (a.P + 4 * WG_KP - 1) / (4 * WG_KP);
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  int pps = (a.P + splits - 1) / splits;
+  pps = (pps + WG_KP - 1) / WG_KP * WG_KP;
+  splits = (a.P + pps - 1) / pps;
+  a.splits = splits;
+  a.pix_per_split = pps;
+  const int groups = splits > WG_GROUP ? (splits + WG_GROUP - 1) / WG_GROUP : 0;
+  const size_t slab_elems = (size_t)a.Cout * a.ldn;
+  void* buf = nullptr;
+  hipError_t e = hipMallocAsync(&buf, (size_t)(splits + groups) * slab_elems * sizeof(float), st);
+  if (e != hipSuccess) return (int)e;
+  a.slab = (float*)buf;
+  hipLaunchKernelGGL((wgrad_gemm_kernel<BM, BN>), dim3(tiles * splits), dim3(256), LDS, st, a);
+  const int n4 = a.Cout * a.KT / 4;
+  const int g1 = (n4 + 255) / 256 < 1024 ? (n4 + 255) / 256 : 1024;
+  const float* part = a.slab;
+  int nparts = splits;
+  if (groups) {
+    float* out = a.slab + (size_t)splits * slab_elems;
+    hipLaunchKernelGGL(wgrad_group_kernel, dim3(g1, groups), dim3(256), 0, st, (const float*)a.slab, splits, a.Cout,
+                       a.KT, a.ldn, out);
+    part = out;
+    nparts = groups;
+  }
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(g1), dim3(256), 0, st, part, nparts, a.Cout, a.KT, a.ldn, dwp);
+  e = hipGetLastError();
+  const hipError_t f = hipFreeAsync(buf, st);
+  return (int)(e != hipSuccess ? e : f);
+}
+
+// Entry from train.hip's upr_t_conv_wgrad (same contract: dwp += ...).
+int wgrad_gemm(const float* x, int B, int H, int W, int Cin, int x_cs, int x_coff, const float* dy, int Ho, int Wo,
+               int Cout, int dy_cs, int dy_coff, int kh, int kw, int stride, int pad, int dil, float* dwp,
+               hipStream_t st) {
+  if (x_cs % 4 || x_coff % 4 || dy_cs % 4 || dy_coff % 4 || ((uintptr_t)x % 16) || ((uintptr_t)dy % 16) ||
+      ((uintptr_t)dwp % 16))
+    return kErrUnsupported;
+  const long long P = (long long)B * Ho * Wo;
+  if (P >= (1ll << 30) || (long long)B * H * W >= (1ll << 31)) return kErrUnsupported;
+  WgArgs a;
+  memset(&a, 0, sizeof(a));
+  a.x = x; a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.x_cs = x_cs; a.x_coff = x_coff;
+  a.dy = dy; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout; a.dy_cs = dy_cs; a.dy_coff = dy_coff;
+  a.kh = kh; a.kw = kw; a.s = stride; a.p = pad; a.d = dil;
+  a.KT = kh * kw * Cin;
+  a.P = (int)P;
+  if (Cout % 128 == 0) return launch_wgrad_gemm<128, 64>(a, dwp, st);
+  if (Cout % 64 == 0) return launch_wgrad_gemm<64, 128>(a, dwp, st);
+  return launch_wgrad_gemm<32, 256>(a, dwp, st);
+}
+
+}  // namespace upr
