@@ -16,8 +16,7 @@ GPU work by a small CPU step over gloo (tests the launcher / rank plumbing on
 a machine without a GPU).
 
 Extra objects on the JSON line:
-  roofline      the conv kernel family (conv_halo_kernel<*>, conv_igemm_kernel<*>,
-                ~97% of device time), timed live with HIP events around every
+  roofline      the conv kernel family (CONV_KERNELS below, ~97% of device time), timed live with HIP events around every
                 launch on the model's stream inside the timed region
                 (upr_model_profile); traffic from rocprofv3 FETCH_SIZE/WRITE_SIZE
                 child passes run before this process touches the GPU
@@ -104,8 +103,8 @@ def parity_vs_cpu(sd, pre, aspp, x, outs, precision):
             "sample": "image 0 of the last timed batch vs oracle/net.py fp32 on host cores"}
 
 
-CONV_KERNELS = ("conv_halo_kernel", "conv_igemm_kernel", "conv_wide_kernel", "conv_stream_kernel",
-                "conv_stream_fam_kernel")
+CONV_KERNELS = ("conv_halo_kernel", "conv_igemm_kernel", "conv_wide_kernel", "conv_wide32_kernel",
+                "conv_stream_kernel", "conv_stream_fam_kernel")
 
 
 def pmc_traffic(args):
@@ -432,7 +431,7 @@ def main():
             "traffic_unit": "bytes per conv launch (rocprofv3 FETCH_SIZE*2 + WRITE_SIZE)",
             "traffic_per_img_GB": traffic["bytes_per_forward"] / B / 1e9 if traffic else None,
             "alg_bytes_per_launch": g_bytes / max(g_calls, 1),
-            "kernel": "conv family: conv_wide/conv_stream/conv_stream_fam/conv_halo/conv_igemm (all conv launches of the step)",
+            "kernel": "conv family: conv_wide/conv_wide32/conv_stream/conv_stream_fam/conv_halo/conv_igemm (all conv launches of the step)",
             "launches_per_step": g_calls / args.steps,
             "avg_launch_us": 1000.0 * g_ms / max(g_calls, 1),
             "gemm_gflop_per_img": g_flops / (args.steps * B) / 1e9,
