@@ -90,6 +90,10 @@ int upr_t_bn_stats(const float* x, int M, int C, int cs, int coff, double* acc, 
  * unbiased variance and momentum; *nbt += 1 (num_batches_tracked). */
 int upr_t_bn_finalize(const double* acc, int M, int C, float momentum, float eps, float* running_mean,
                       float* running_var, int64_t* nbt, float* mean, float* invstd, void* stream);
+/* Eval-mode BatchNorm (nn.BatchNorm2d.eval(), model.py's BN in a standalone
+ * submodule forward): mean = running_mean, invstd = 1/sqrt(running_var + eps). */
+int upr_t_bn_eval_stats(const float* running_mean, const float* running_var, int C, float eps, float* mean,
+                        float* invstd, void* stream);
 /* y = [relu](gamma*(x-mean)*invstd + beta + res_pre) + res_post  (res nullable). */
 int upr_t_bn_apply(const float* x, int M, int C, int x_cs, int x_coff, const float* mean, const float* invstd,
                    const float* gamma, const float* beta, const float* res, int res_cs, int res_coff, int res_post,

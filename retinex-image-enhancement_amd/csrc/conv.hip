@@ -394,6 +394,7 @@ static int launch_t(const ConvOp& op, hipStream_t stream) {
 int launch_conv_halo(const ConvOp& op, int dtype, hipStream_t st);
 int launch_conv_wide(const ConvOp& op, hipStream_t st);
 int launch_conv_stream(const ConvOp& op, hipStream_t st);
+int launch_conv_ring(const ConvOp& op, hipStream_t st);
 int launch_conv_wide32(const ConvOp& op, hipStream_t st);
 
 // UPR_CONV_IMPL=generic forces the implicit-GEMM kernel everywhere (A/B tests);
@@ -414,6 +415,8 @@ int launch_conv(const ConvOp& op, int dtype, hipStream_t stream) {
   if (conv_impl_mode() == 0) {
     if (dtype == kF16) {
       int rc = launch_conv_wide(op, stream);
+      if (rc != kErrUnsupported) return rc;
+      rc = launch_conv_ring(op, stream);
       if (rc != kErrUnsupported) return rc;
       rc = launch_conv_stream(op, stream);
       if (rc != kErrUnsupported) return rc;

@@ -1059,7 +1059,11 @@ int upr_conv2d_nhwc(const void* x, int B, int H, int W, int Cin, const void* w, 
   s.src = x; s.C = Cin; s.cs = Cin; s.coff = 0; s.Hin = H; s.Win = W;
   s.kh = kh; s.kw = kw; s.stride = stride; s.pad = pad; s.dil = dil; s.pre = kPreNone; s.kbase = 0;
   c.B = B; c.Ho = Ho; c.Wo = Wo; c.N = Cout; c.Kpad = kh * kw * Cin;
-  c.W = w; c.bias = bias; c.res1 = residual; c.res1_cs = Cout; c.relu = relu;
+  c.W = w; c.bias = bias; c.relu = relu;
+  // without ReLU, "added before" and "added after" coincide: use the post-ReLU
+  // slot, which every kernel family takes
+  if (relu) { c.res1 = residual; c.res1_cs = Cout; }
+  else { c.res2 = residual; c.res2_cs = Cout; }
   c.out = y; c.out_cs = Cout; c.out_coff = 0; c.store = kStoreNHWC;
   return launch_conv(c, dtype, (hipStream_t)stream);
 }

@@ -517,6 +517,15 @@ __global__ void bn_finalize_kernel(const double* __restrict__ acc, int M, int C,
   }
 }
 
+// eval-mode BatchNorm statistics: mean = running_mean, invstd = 1/sqrt(running_var + eps)
+__global__ void bn_eval_stats_kernel(const float* __restrict__ rm, const float* __restrict__ rv, int C, float eps,
+                                     float* __restrict__ mean, float* __restrict__ invstd) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  mean[c] = rm[c];
+  invstd[c] = (float)(1.0 / sqrt((double)rv[c] + (double)eps));
+}
+
 __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__ x, int M, int C, int x_cs,
                                                        int x_coff, const float* __restrict__ mean,
                                                        const float* __restrict__ invstd,
@@ -1618,6 +1627,14 @@ int upr_t_bn_finalize(const double* acc, int M, int C, float momentum, float eps
   if (!acc || !mean || !invstd || M <= 0) return UPR_ERR_ARG;
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, ST(stream), acc, M, C, momentum, eps,
                      running_mean, running_var, (long long*)nbt, mean, invstd);
+  LAUNCH_CHECK();
+}
+
+int upr_t_bn_eval_stats(const float* running_mean, const float* running_var, int C, float eps, float* mean,
+                        float* invstd, void* stream) {
+  if (!running_mean || !running_var || !mean || !invstd || C <= 0) return UPR_ERR_ARG;
+  hipLaunchKernelGGL(bn_eval_stats_kernel, dim3((C + 255) / 256), dim3(256), 0, ST(stream), running_mean, running_var, C,
+                     eps, mean, invstd);
   LAUNCH_CHECK();
 }
 

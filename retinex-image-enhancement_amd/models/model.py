@@ -8,8 +8,10 @@ device `MultiScaleUP_Retinex.forward` / `ResidualIENet.forward` run the fused
 gfx950 kernel graph of libupr.so (BatchNorm folded, implicit-GEMM MFMA convs,
 fused FAM attention and Retinex tail).  In training mode the forward runs the
 HIP training engine (upr/train.py: batch-statistics BatchNorm, Dropout, an
-explicit backward reached through `loss.backward()`).  There is no eager
-fallback: CPU tensors and the fused submodules' own forward() raise.
+explicit backward reached through `loss.backward()`).  The submodules
+(EnhancedFAM, ResBlock, PreActResBlock, ASPPModule, UpBlock) called on their own
+run on the per-module HIP layer objects (upr/modules.py), in eval or training
+mode.  There is no eager fallback: CPU tensors raise.
 """
 import torch
 import torch.nn as nn
@@ -21,10 +23,13 @@ _FUSED_MSG = ("{} executes only inside the fused UP-Retinex HIP graph; call the 
 
 
 class _FusedModule(nn.Module):
-    """Submodules whose computation lives inside the fused HIP graph."""
+    """Submodules: fused into the model's HIP graph inside MultiScaleUP_Retinex;
+    a direct call runs the module alone on the HIP layer kernels
+    (upr/modules.py: NCHW float32 in / out, eval or training mode)."""
 
-    def forward(self, *args, **kwargs):  # pragma: no cover - guarded path
-        raise NotImplementedError(_FUSED_MSG.format(type(self).__name__))
+    def forward(self, x):
+        from upr.modules import submodule_forward
+        return submodule_forward(self, x)
 
 
 class EnhancedFAM(_FusedModule):

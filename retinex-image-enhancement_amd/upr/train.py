@@ -304,7 +304,9 @@ class ConvT:
 
 
 class BN:
-    """nn.BatchNorm2d in training mode (batch statistics, running-stat update)."""
+    """nn.BatchNorm2d: training mode (batch statistics, running-stat update) or,
+    when the module is in eval mode, the running statistics (a standalone
+    submodule forward, upr/modules.py)."""
 
     def __init__(self, m):
         self.m = m
@@ -317,11 +319,15 @@ class BN:
     def fwd(self, x, relu=False, out=None, res=None, res_post=False):
         lib, st = L.lib(), _stream()
         m = self.m
-        zero(self.acc)
-        _chk(lib.upr_t_bn_stats(x.ptr(), x.M, self.C, x.cs, 0, _p(self.acc), st), "bn_stats")
-        _chk(lib.upr_t_bn_finalize(_p(self.acc), x.M, self.C, ctypes.c_float(m.momentum), ctypes.c_float(m.eps),
-                                   _p(m.running_mean), _p(m.running_var), _p(m.num_batches_tracked), _p(self.mean),
-                                   _p(self.invstd), st), "bn_finalize")
+        if m.training:
+            zero(self.acc)
+            _chk(lib.upr_t_bn_stats(x.ptr(), x.M, self.C, x.cs, 0, _p(self.acc), st), "bn_stats")
+            _chk(lib.upr_t_bn_finalize(_p(self.acc), x.M, self.C, ctypes.c_float(m.momentum), ctypes.c_float(m.eps),
+                                       _p(m.running_mean), _p(m.running_var), _p(m.num_batches_tracked),
+                                       _p(self.mean), _p(self.invstd), st), "bn_finalize")
+        else:
+            _chk(lib.upr_t_bn_eval_stats(_p(m.running_mean), _p(m.running_var), self.C, ctypes.c_float(m.eps),
+                                         _p(self.mean), _p(self.invstd), st), "bn_eval_stats")
         if out is None:
             out = Act.new(x.B, x.H, x.W, self.C, x.t.device, fresh=False)
         _chk(lib.upr_t_bn_apply(x.ptr(), x.M, self.C, x.cs, 0, _p(self.mean), _p(self.invstd), _p(m.weight),
@@ -453,6 +459,11 @@ class ASPPT:
         self.p = m.fusion[3].p
         self.C = self.c1.Cout
         self.seed = 0
+        self.mod = m
+
+    @property
+    def training(self):
+        return self.mod.training
 
     def convs(self):
         return [self.c1, self.gc, self.fc] + [c for c, _ in self.br]
@@ -474,6 +485,8 @@ class ASPPT:
         _chk(L.lib().upr_t_broadcast(_fp(self.gp.t), x.B, x.H * x.W, C, ctypes.c_float(1.0), _fp(cat.t), cat.cs,
                                      C * (nb - 1), 0, _stream()), "broadcast")
         self.a = self.fb.fwd(self.fc.fwd(cat), relu=True)
+        if not self.training:
+            return self.a  # nn.Dropout in eval mode is the identity
         out = Act.new(x.B, x.H, x.W, C, dev, fresh=False)
         self.mask = torch.empty((out.t.numel(),), dtype=torch.uint8, device=dev)
         self.seed = int(torch.randint(0, 2 ** 62, (1,)).item())
@@ -522,18 +535,22 @@ class UpBlockT:
     def convs(self):
         return [self.up, self.c1, self.c2]
 
-    def fwd(self, x, skip):
+    def fwd(self, x, skip=None):
+        """skip=None: UpBlock.forward alone (model.py:271-274, no skip add)."""
         self.x = x
         self.u = self.up.fwd(x)
         self.a1 = self.b1.fwd(self.c1.fwd(self.u), relu=True)
         self.a2 = self.b2.fwd(self.c2.fwd(self.a1), relu=True)
+        if skip is None:
+            return self.a2
         out = Act.new(self.a2.B, self.a2.H, self.a2.W, self.a2.C, x.t.device, fresh=False)
         pointwise(self.a2.t, skip.t, out.t, out.t.numel(), 4)
         return out
 
-    def bwd(self, g, gx, g_skip):
+    def bwd(self, g, gx, g_skip=None):
         dev = g.t.device
-        add_into(g_skip, g)
+        if g_skip is not None:
+            add_into(g_skip, g)
         relu_mask(g, self.a2)
         g_c2 = Act.new(g.B, g.H, g.W, g.C, dev)
         self.b2.bwd(g, g_c2)

@@ -64,12 +64,13 @@ def test_cpu_forward_raises_no_fallback():
         m.ie_net(torch.rand(1, 3, 32, 32))
 
 
-def test_fused_submodules_raise():
-    fam = M.EnhancedFAM(32, 32)
-    with pytest.raises(NotImplementedError):
-        fam(torch.rand(1, 32, 8, 8))
-    with pytest.raises(NotImplementedError):
-        M.ResBlock(32, 64, 2)(torch.rand(1, 32, 8, 8))
+def test_submodules_have_no_cpu_path():
+    """Standalone submodule forwards run on the device (tests/test_gpu_modules.py);
+    a CPU tensor raises like the top-level model."""
+    for mod, c in ((M.EnhancedFAM(32, 32), 32), (M.ResBlock(32, 64, 2), 32), (M.PreActResBlock(32, 64, 2), 32),
+                   (M.ASPPModule(64, 64), 64), (M.UpBlock(64, 32), 64)):
+        with pytest.raises(RuntimeError, match="ROCm"):
+            mod.eval()(torch.rand(1, c, 8, 8))
     m = M.UP_Retinex()
     with pytest.raises(NotImplementedError):
         m.retinex_decompose(torch.rand(1, 3, 8, 8), torch.rand(1, 1, 8, 8))

@@ -63,6 +63,11 @@ CONV_CASES = [
     (2, 20, 45, 32, 32, 3, 1, 1, 1, True, False),
     (1, 9, 70, 32, 64, 3, 1, 1, 1, False, False),
     (3, 13, 29, 64, 64, 3, 1, 1, 1, True, False),
+    # row-ring streaming kernel (fp16): several strips / row bands, partial strips, residual
+    (2, 20, 45, 32, 32, 3, 1, 1, 1, False, True),
+    (1, 37, 70, 64, 64, 3, 1, 1, 1, False, True),
+    (2, 66, 96, 32, 64, 3, 1, 1, 1, True, False),
+    (4, 130, 40, 32, 32, 3, 1, 1, 1, True, False),
 ]
 
 
