@@ -303,10 +303,11 @@ def train_main(args):
         "metric": f"train images/sec at {S}x{S} bs={B} (UP-Retinex fwd + TotalLoss + bwd + clip + Adam)",
         "value": imgs / elapsed, "unit": "images/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "scaling": "weak", "vs_baseline": None,
+        "dtype": "f16 convs under autocast (fp32 accumulate; fp32 BN / loss / wgrad / Adam)" if args.amp else "f32",
         "data": "synthetic torch.rand inputs, random-init weights (seed 0), seeded random-init VGG19 (seed 1234)",
         "config": {"workload": f"configs[4]: bs={B}/GPU {S}x{S} {args.variant} train step"
-                               + (" with GradScaler (AMP control flow, fp32 arithmetic)" if args.amp else " (fp32)"),
+                               + (" AMP: autocast (fp16 MFMA convs) + GradScaler" if args.amp else " (fp32)"),
                    "global_batch": world * B, "image_size": S, "variant": args.variant,
                    "parallelism": f"data-parallel x{world} (per-rank shard"
                                   + (", RCCL all-reduce of the flat gradient buffer)" if world > 1 else ")")},

@@ -64,6 +64,20 @@ int upr_t_conv_direct_wgrad(const UprView* x, const UprView* dy, int B, int H, i
 int upr_t_conv_mfma(const float* x, int B, int H, int W, int Cin, int x_cs, int x_coff, const float* wp,
                     const float* bias, int N, int kh, int kw, int stride, int pad, int dil, const float* res,
                     int res_cs, int relu, float* y, int y_cs, int y_coff, int store, void* stream);
+/* Autocast (AMP) form of upr_t_conv_mfma (reference trainers/train.py:72 runs
+ * the step under torch.cuda.amp.autocast(): convs in fp16).  x (fp32 view) is
+ * cast into x16 (dense fp16 [B,H,W,Cin], caller-allocated) unless x16_ready;
+ * wp16 = the packed weights in fp16 (upr_t_cast_f16); the fp16 MFMA conv
+ * (fp32 accumulate, bias, ReLU) writes y16 (dense fp16 [B,Ho,Wo,N], or the
+ * ConvTranspose layout for store 1), then y = float(y16) (+ res, in fp32,
+ * indexed like upr_t_conv_mfma's: res == y accumulates).  res and relu are
+ * exclusive. */
+int upr_t_conv_mfma16(const float* x, int B, int H, int W, int Cin, int x_cs, int x_coff, const void* wp16,
+                      const float* bias, int N, int kh, int kw, int stride, int pad, int dil, const float* res,
+                      int res_cs, int relu, float* y, int y_cs, int y_coff, int store, void* x16, int x16_ready,
+                      void* y16, void* stream);
+/* y[i] = (fp16) x[i], n elements. */
+int upr_t_cast_f16(const float* x, void* y, size_t n, void* stream);
 /* Weight gradient of an NHWC conv as an MFMA GEMM over pixels:
  * dwp[co][(ky,kx,ci)] += sum_p dy[p][co] * x[window(p, ky, kx)][ci]
  * (packed layout of upr_t_pack_weight mode 0).  Cin, Cout multiples of 32. */

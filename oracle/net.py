@@ -17,7 +17,7 @@ BN_MOMENTUM = 0.1
 # and updates the running buffers in place, Dropout draws its mask from
 # MODE["dropout_mask"] (a callable shape -> {0,1} mask, so the checker can
 # replay the product's mask) — nn.BatchNorm2d / nn.Dropout train semantics.
-MODE = {"train": False, "dropout_mask": None}
+MODE = {"train": False, "dropout_mask": None, "amp": False}
 
 
 def _bn(sd, p, x):
@@ -35,8 +35,25 @@ def _dropout(x, p=0.1):
     return x * mask / (1.0 - p)
 
 
+def _r16(t):
+    """fp16 rounding (autocast's cast): its backward rounds the gradient too."""
+    return t.to(torch.float16).to(t.dtype)
+
+
+def amp_conv(fn, x, w, b, cin, cout, **kw):
+    """MODE["amp"]: the product's autocast arithmetic for MFMA-shaped convs
+    (Cin, Cout multiples of 32; upr/train.py Conv / ConvT with autocast on):
+    fp16 operands, wide accumulation, bias in fp32, fp16-rounded output.
+    Otherwise a plain conv."""
+    if MODE["amp"] and cin % 32 == 0 and cout % 32 == 0:
+        return _r16(fn(_r16(x), _r16(w), b, **kw))
+    return fn(x, w, b, **kw)
+
+
 def _conv(sd, p, x, stride=1, padding=0, dilation=1):
-    return F.conv2d(x, sd[p + ".weight"], sd.get(p + ".bias"), stride, padding, dilation)
+    w = sd[p + ".weight"]
+    return amp_conv(F.conv2d, x, w, sd.get(p + ".bias"), w.shape[1], w.shape[0], stride=stride, padding=padding,
+                    dilation=dilation)
 
 
 def fam(sd, p, x):
@@ -97,7 +114,8 @@ def aspp(sd, p, x, dilations=(1, 6, 12, 18)):
 
 def upblock(sd, p, x):
     """UpBlock.forward — models/model.py:271-274."""
-    u = F.conv_transpose2d(x, sd[p + ".up.weight"], sd[p + ".up.bias"], stride=2)
+    w = sd[p + ".up.weight"]
+    u = amp_conv(F.conv_transpose2d, x, w, sd[p + ".up.bias"], w.shape[0], w.shape[1], stride=2)
     u = F.relu(_bn(sd, p + ".conv.1", _conv(sd, p + ".conv.0", u, padding=1)))
     return F.relu(_bn(sd, p + ".conv.4", _conv(sd, p + ".conv.3", u, padding=1)))
 

@@ -137,7 +137,8 @@ def vgg_features(vgg_sd, x):
         for layer in sl:
             if layer[0] == "conv":
                 i = layer[1]
-                h = F.relu(F.conv2d(h, vgg_sd[f"{i}.weight"], vgg_sd[f"{i}.bias"], padding=1))
+                w = vgg_sd[f"{i}.weight"]
+                h = F.relu(net.amp_conv(F.conv2d, h, w, vgg_sd[f"{i}.bias"], w.shape[1], w.shape[0], padding=1))
             else:
                 h = F.max_pool2d(h, 2, 2)
         feats.append(h)
@@ -208,10 +209,13 @@ def total_loss(vgg_sd, low, enh, illu, refl, use_freq=True, texture_method="tv",
 
 
 @contextlib.contextmanager
-def train_mode(dropout_mask=None):
+def train_mode(dropout_mask=None, amp=False):
+    """Training-mode BatchNorm / Dropout; amp: the autocast conv arithmetic
+    (net.amp_conv) for the model and the VGG convs."""
     old = dict(net.MODE)
     net.MODE["train"] = True
     net.MODE["dropout_mask"] = dropout_mask
+    net.MODE["amp"] = amp
     try:
         yield
     finally:

@@ -1567,6 +1567,88 @@ int upr_t_conv_mfma(const float* x, int B, int H, int W, int Cin, int x_cs, int 
   return launch_conv(c, kF32, ST(stream));
 }
 
+// ---- autocast (AMP) convs: fp16 operands, fp32 accumulate, fp32 activations ----
+// x[m][coff + c] (fp32, pixel stride cs) -> dense fp16 [m][C], 8 channels per thread
+__global__ __launch_bounds__(256) void cast_act_f16_kernel(const float* __restrict__ x, long long M, int C, int cs,
+                                                           int coff, half_t* __restrict__ y) {
+  const int C8 = C / 8;
+  GSTRIDE(i, M * C8) {
+    const long long m = i / C8;
+    const int c = (int)(i - m * C8) * 8;
+    const float4* src = (const float4*)(x + m * cs + coff + c);
+    const float4 a = src[0], b = src[1];
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    h8 o = {(half_t)a.x, (half_t)a.y, (half_t)a.z, (half_t)a.w, (half_t)b.x, (half_t)b.y, (half_t)b.z, (half_t)b.w};
+    *(h8*)(y + m * C + c) = o;
+  }
+}
+// dense fp16 [m][C] -> y[m][coff + c] (fp32) (+ res[m * res_cs + c], fp32; res may alias y)
+__global__ __launch_bounds__(256) void cast_act_f32_kernel(const half_t* __restrict__ x, long long M, int C,
+                                                           const float* res, int res_cs, float* y, int cs, int coff) {
+  const int C4 = C / 4;
+  GSTRIDE(i, M * C4) {
+    const long long m = i / C4;
+    const int c = (int)(i - m * C4) * 4;
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    const h4 v = *(const h4*)(x + m * C + c);
+    float4 o = make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
+    if (res) {
+      const float4 r = *(const float4*)(res + m * res_cs + c);
+      o.x += r.x; o.y += r.y; o.z += r.z; o.w += r.w;
+    }
+    *(float4*)(y + m * cs + coff + c) = o;
+  }
+}
+__global__ __launch_bounds__(256) void cast_f16_kernel(const float* __restrict__ x, long long n, half_t* __restrict__ y) {
+  GSTRIDE(i, n) y[i] = (half_t)x[i];
+}
+
+int upr_t_cast_f16(const float* x, void* y, size_t n, void* stream) {
+  if (!x || !y) return UPR_ERR_ARG;
+  hipLaunchKernelGGL(cast_f16_kernel, dim3(grid_for((long long)n)), dim3(256), 0, ST(stream), x, (long long)n,
+                     (half_t*)y);
+  LAUNCH_CHECK();
+}
+
+int upr_t_conv_mfma16(const float* x, int B, int H, int W, int Cin, int x_cs, int x_coff, const void* wp16,
+                      const float* bias, int N, int kh, int kw, int stride, int pad, int dil, const float* res,
+                      int res_cs, int relu, float* y, int y_cs, int y_coff, int store, void* x16, int x16_ready,
+                      void* y16, void* stream) {
+  if (!x16 || !wp16 || !y || !y16 || B <= 0 || Cin % 32 || N % 32 || Cin <= 0 || N <= 0) return UPR_ERR_ARG;
+  if (!x16_ready && !x) return UPR_ERR_ARG;
+  if (kh <= 0 || kw <= 0 || stride <= 0 || dil <= 0 || pad < 0) return UPR_ERR_ARG;
+  if (x_cs % 4 || x_coff % 4 || y_cs % 4 || y_coff % 4 || (res && res_cs % 4)) return UPR_ERR_ARG;
+  if (res && relu) return UPR_ERR_ARG;  // the residual is added in fp32 after the fp16 GEMM
+  if (store == 1 && ((N / 4) % 32)) return UPR_ERR_SHAPE;
+  const int Ho = (H + 2 * pad - dil * (kh - 1) - 1) / stride + 1;
+  const int Wo = (W + 2 * pad - dil * (kw - 1) - 1) / stride + 1;
+  if (Ho <= 0 || Wo <= 0) return UPR_ERR_SHAPE;
+  hipStream_t st = ST(stream);
+  const long long Mi = (long long)B * H * W;
+  if (!x16_ready) {
+    if ((uintptr_t)x % 16 || x_cs % 8 || x_coff % 8) return UPR_ERR_ARG;
+    hipLaunchKernelGGL(cast_act_f16_kernel, dim3(grid_for(Mi * (Cin / 8))), dim3(256), 0, st, x, Mi, Cin, x_cs, x_coff,
+                       (half_t*)x16);
+    UPR_CHECK_HIP(hipGetLastError());
+  }
+  ConvOp c;
+  memset(&c, 0, sizeof(c));
+  c.nseg = 1;
+  ConvSeg& s = c.seg[0];
+  s.src = x16; s.C = Cin; s.cs = Cin; s.coff = 0; s.Hin = H; s.Win = W;
+  s.kh = kh; s.kw = kw; s.stride = stride; s.pad = pad; s.dil = dil; s.pre = kPreNone; s.kbase = 0;
+  c.B = B; c.Ho = Ho; c.Wo = Wo; c.N = N; c.Kpad = kh * kw * Cin;
+  c.W = wp16; c.bias = bias; c.relu = relu;
+  c.out = y16; c.out_cs = store == 1 ? N / 4 : N; c.out_coff = 0; c.store = store == 1 ? kStoreConvT2x2 : kStoreNHWC;
+  const int rc = launch_conv(c, kF16, st);
+  if (rc != 0) return rc;
+  const long long Mo = store == 1 ? (long long)B * 4 * Ho * Wo : (long long)B * Ho * Wo;
+  const int Co = store == 1 ? N / 4 : N;
+  hipLaunchKernelGGL(cast_act_f32_kernel, dim3(grid_for(Mo * (Co / 4))), dim3(256), 0, st, (const half_t*)y16, Mo, Co,
+                     res, res_cs, y, y_cs, y_coff);
+  LAUNCH_CHECK();
+}
+
 int upr_t_conv_wgrad(const float* x, int B, int H, int W, int Cin, int x_cs, int x_coff, const float* dy, int Ho,
                      int Wo, int Cout, int dy_cs, int dy_coff, int kh, int kw, int stride, int pad, int dil,
                      float* dwp, void* stream) {

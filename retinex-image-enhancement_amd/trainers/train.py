@@ -8,8 +8,12 @@ clip + Adam), and `clip_grad_norm_` is upr.optim's.  With `use_amp` and a
 scaler the step follows the reference's AMP branch (train.py:71-89): scaled
 backward, unscale_ (one launch over the flat gradient buffer), clip, a step
 skipped on inf/nan, scale update — upr.amp.GradScaler (a torch.amp.GradScaler
-handed in is mirrored by one with its settings).  The arithmetic stays fp32
-(precision >= autocast's).
+handed in is mirrored by one with its settings).  As in the reference, the
+forward and the loss of that branch run under torch.autocast: the engine then
+computes its MFMA convolutions (and their input gradients) in fp16 with fp32
+accumulation (upr/train.py, autocast_active); weight gradients, BatchNorm, the
+losses and the optimiser stay fp32.  `amp_fp16=False` keeps the GradScaler
+control flow with fp32 arithmetic.
 """
 import time
 
@@ -37,14 +41,16 @@ def make_optimizer(model, lr=1e-4, weight_decay=1e-5):
     return uoptim.Adam(model.parameters(), lr=lr, weight_decay=weight_decay)
 
 
-def train_step(model, img_low, criterion, optimizer, max_norm=1.0, scaler=None, use_amp=False, grad_hook=None):
+def train_step(model, img_low, criterion, optimizer, max_norm=1.0, scaler=None, use_amp=False, grad_hook=None,
+               amp_fp16=True):
     """One step body (train.py:63-103).  Returns (loss, loss_dict).  grad_hook
     (e.g. upr.dist.allreduce_grads for data parallelism) runs between the
     backward and the unscale / clip."""
     optimizer.zero_grad()
-    img_enhanced, reflectance, illu_map = model(img_low)
-    loss, loss_dict = criterion(img_low, img_enhanced, illu_map, reflectance)
     scaler = _as_upr_scaler(scaler) if use_amp else None
+    with torch.autocast("cuda", dtype=torch.float16, enabled=scaler is not None and amp_fp16):
+        img_enhanced, reflectance, illu_map = model(img_low)
+        loss, loss_dict = criterion(img_low, img_enhanced, illu_map, reflectance)
     if scaler is not None:
         scaler.scale(loss).backward()
         if grad_hook is not None:

@@ -95,6 +95,9 @@ SIGNATURES.update({
     "upr_t_conv_direct_wgrad": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p]),
     "upr_t_conv_mfma": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _p, _i, _i, _i, _i, _i, _i, _p, _i, _i, _p, _i, _i,
                              _i, _p]),
+    "upr_t_conv_mfma16": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _p, _i, _i, _i, _i, _i, _i, _p, _i, _i, _p, _i, _i,
+                               _i, _p, _i, _p, _p]),
+    "upr_t_cast_f16": (_i, [_p, _p, c_size_t, _p]),
     "upr_t_conv_wgrad": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p]),
     "upr_t_pack_weight": (_i, [_p, _p, _i, _i, _i, _i, _i, _p]),
     "upr_t_unpack_grad": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p]),

@@ -21,7 +21,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib as L
-from .train import Act, Conv, _chk, _fp, _p, _stream, empty, relu_mask, zero
+from .train import Act, Conv, _chk, _fp, _p, _stream, autocast_active, empty, relu_mask, set_amp, zero
 
 WEIGHTS = dict(exposure=10.0, smoothness=1.0, color=0.5, spatial=1.0, decouple=0.1, perceptual=1.0,
                frequency=0.5)
@@ -151,7 +151,8 @@ class TotalLossEngine:
                                   TEXTURE[self.texture_method], st), "loss_pixel")
         acc = torch.empty(4, dtype=torch.float64, device=dev)
         zero(acc)
-        # ---- perceptual ----
+        # ---- perceptual (VGG convs in fp16 under the caller's autocast, as the reference's) ----
+        set_amp(autocast_active())
         self.vgg.pack()
         ne = Act.new(B, H, W, 3, dev, fresh=False)
         nl = Act.new(B, H, W, 3, dev, fresh=False)

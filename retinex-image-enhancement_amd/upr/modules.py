@@ -21,7 +21,8 @@ import ctypes
 import torch
 
 from . import _lib as L
-from .train import (FAMT, ASPPT, Act, PreActResBlockT, ResBlockT, UpBlockT, _chk, _stream, empty, nchw_view)
+from .train import (FAMT, ASPPT, Act, PreActResBlockT, ResBlockT, UpBlockT, _chk, _stream, autocast_active, empty,
+                    nchw_view, set_amp)
 
 _LAYERS = {"EnhancedFAM": FAMT, "ResBlock": ResBlockT, "PreActResBlock": PreActResBlockT, "ASPPModule": ASPPT,
            "UpBlock": UpBlockT}
@@ -50,6 +51,7 @@ def _layer(module, dev):
 
 
 def _run(layer, x):
+    set_amp(autocast_active())
     for c in layer.convs():
         c.pack()
     return layer.fwd(_to_nhwc(x))

@@ -45,6 +45,32 @@ def empty(shape, dev):
     return torch.empty(shape, dtype=F32, device=dev)
 
 
+# Autocast (AMP) arithmetic.  The reference runs the model forward and the
+# loss under torch.cuda.amp.autocast() when use_amp (trainers/train.py:71-75),
+# i.e. its convolutions in fp16.  The graph / loss engine set this flag from
+# the caller's autocast state at forward time; while set, MFMA convs (and the
+# input gradients of their backward) run on the fp16 kernels with fp32
+# accumulation and fp32 activations in between (upr_t_conv_mfma16).  Weight
+# gradients, BatchNorm, losses, FFTs and the optimiser stay fp32.
+_AMP = [False]
+
+
+def autocast_active():
+    """True inside torch.autocast('cuda') (any half dtype: the kernels compute fp16)."""
+    try:
+        return bool(torch.is_autocast_enabled("cuda"))
+    except TypeError:  # older signature
+        return bool(torch.is_autocast_enabled())
+
+
+def set_amp(on):
+    _AMP[0] = bool(on)
+
+
+def _h16(n, dev):
+    return torch.empty((n,), dtype=torch.float16, device=dev)
+
+
 class Act:
     """NHWC activation: channels [coff, coff+C) of a [B,H,W,cs] fp32 tensor.
 
@@ -167,6 +193,8 @@ class Conv:
         self.mfma = self.Cin % 32 == 0 and self.Cout % 32 == 0
         self.frozen = frozen
         self.wp = self.wt = None
+        self.wp16 = self.wt16 = None
+        self.amp = False  # fp16 arithmetic of the last forward (its backward follows it)
 
     def out_hw(self, H, W):
         return ((H + 2 * self.p - self.d * (self.kh - 1) - 1) // self.s + 1,
@@ -183,6 +211,23 @@ class Conv:
             self.gp = torch.empty_like(w).view(-1)
         _chk(lib.upr_t_pack_weight(_p(w), _p(self.wp), self.Cout, self.Cin, self.kh, self.kw, 0, st), "pack")
         _chk(lib.upr_t_pack_weight(_p(w), _p(self.wt), self.Cout, self.Cin, self.kh, self.kw, 1, st), "pack")
+        if _AMP[0]:
+            if self.wp16 is None:
+                self.wp16, self.wt16 = _h16(w.numel(), w.device), _h16(w.numel(), w.device)
+            _chk(lib.upr_t_cast_f16(_p(self.wp), _p(self.wp16), w.numel(), st), "cast_w")
+            _chk(lib.upr_t_cast_f16(_p(self.wt), _p(self.wt16), w.numel(), st), "cast_w")
+
+    def _mfma16(self, x, B, H, W, C, cs, coff, w16, bias, N, kh, kw, s, p, d, res, relu, out, store=0):
+        """fp16 MFMA conv with fp32 in / out (upr_t_conv_mfma16); res: Act or None."""
+        Ho = (H + 2 * p - d * (kh - 1) - 1) // s + 1
+        Wo = (W + 2 * p - d * (kw - 1) - 1) // s + 1
+        dev = x.device
+        x16 = _h16(B * H * W * C, dev)
+        y16 = _h16(B * Ho * Wo * N, dev)
+        _chk(L.lib().upr_t_conv_mfma16(_fp(x, 0), B, H, W, C, cs, coff, _p(w16), _p(bias), N, kh, kw, s, p, d,
+                                       res.ptr() if res is not None else None, res.cs if res is not None else 0,
+                                       int(relu), _fp(out.t), out.cs, out.coff, store, _p(x16), 0, _p(y16),
+                                       _stream()), "conv_mfma16")
 
     def fwd(self, x, relu=False, out=None, res=None, x_view=None):
         """x: Act (or x_view: (UprView, B, H, W) for an NCHW network input)."""
@@ -195,7 +240,11 @@ class Conv:
         if out is None:
             out = Act.new(B, Ho, Wo, self.Cout, x.t.device, fresh=False)
         out.fresh = False
-        if self.mfma and x_view is None:
+        self.amp = _AMP[0] and self.mfma and x_view is None
+        if self.amp:
+            self._mfma16(x.t, B, H, W, self.Cin, x.cs, x.coff, self.wp16, self.bias, self.Cout, self.kh, self.kw,
+                         self.s, self.p, self.d, res, relu, out)
+        elif self.mfma and x_view is None:
             _chk(lib.upr_t_conv_mfma(_fp(x.t), B, H, W, self.Cin, x.cs, x.coff, _p(self.wp),
                                      _p(self.bias), self.Cout, self.kh, self.kw, self.s, self.p, self.d,
                                      res.ptr() if res is not None else None, res.cs if res is not None else 0,
@@ -247,9 +296,13 @@ class Conv:
                                              _p(z), st), "zero_upsample")
                 src, sH, sW, scs, scoff = z, H, W, self.Cout, 0
             pad_t = self.d * (self.kh - 1) - self.p
-            _chk(lib.upr_t_conv_mfma(_fp(src), B, sH, sW, self.Cout, scs, scoff, _p(self.wt), None, self.Cin,
-                                     self.kh, self.kw, 1, pad_t, self.d, gx.ptr() if acc else None,
-                                     gx.cs if acc else 0, 0, _fp(gx.t), gx.cs, gx.coff, 0, st), "conv_dgrad")
+            if self.amp:
+                self._mfma16(src, B, sH, sW, self.Cout, scs, scoff, self.wt16, None, self.Cin, self.kh, self.kw, 1,
+                             pad_t, self.d, gx if acc else None, False, gx)
+            else:
+                _chk(lib.upr_t_conv_mfma(_fp(src), B, sH, sW, self.Cout, scs, scoff, _p(self.wt), None, self.Cin,
+                                         self.kh, self.kw, 1, pad_t, self.d, gx.ptr() if acc else None,
+                                         gx.cs if acc else 0, 0, _fp(gx.t), gx.cs, gx.coff, 0, st), "conv_dgrad")
         else:
             acc = gx.consume_fresh()
             _chk(lib.upr_t_conv_direct_dgrad(ctypes.byref(gy.view()), Ho, Wo, _p(self.m.weight), B, H, W, self.Cin,
@@ -266,6 +319,8 @@ class ConvT:
         self.m = m
         self.Cin, self.Cout = m.weight.shape[0], m.weight.shape[1]
         self.wp = None
+        self.wp16 = self.wd16 = None
+        self.amp = False
 
     def pack(self):
         lib, st = L.lib(), _stream()
@@ -277,15 +332,25 @@ class ConvT:
             self.b4 = empty((4 * self.Cout,), w.device)
         _chk(lib.upr_t_pack_weight(_p(w), _p(self.wp), self.Cout, self.Cin, 2, 2, 2, st), "pack")
         _chk(lib.upr_t_pack_weight(_p(w), _p(self.wd), self.Cout, self.Cin, 2, 2, 3, st), "pack")
+        if _AMP[0]:
+            if self.wp16 is None:
+                self.wp16, self.wd16 = _h16(w.numel(), w.device), _h16(w.numel(), w.device)
+            _chk(lib.upr_t_cast_f16(_p(self.wp), _p(self.wp16), w.numel(), st), "cast_w")
+            _chk(lib.upr_t_cast_f16(_p(self.wd), _p(self.wd16), w.numel(), st), "cast_w")
         src = L.UprView(self.m.bias.data_ptr(), 0, 0, 0, 1)
         dst = L.UprView(self.b4.data_ptr(), 0, 0, self.Cout, 1)
         _chk(lib.upr_t_copy(ctypes.byref(src), ctypes.byref(dst), 1, 1, 4, self.Cout, 0, st), "bias4")
 
     def fwd(self, x):
         out = Act.new(x.B, 2 * x.H, 2 * x.W, self.Cout, x.t.device, fresh=False)
-        _chk(L.lib().upr_t_conv_mfma(x.ptr(), x.B, x.H, x.W, self.Cin, x.cs, 0, _p(self.wp), _p(self.b4),
-                                     4 * self.Cout, 1, 1, 1, 0, 1, None, 0, 0, _fp(out.t), out.cs, 0, 1, _stream()),
-             "convT")
+        self.amp = _AMP[0]
+        if self.amp:
+            Conv._mfma16(self, x.t, x.B, x.H, x.W, self.Cin, x.cs, x.coff, self.wp16, self.b4, 4 * self.Cout, 1, 1,
+                         1, 0, 1, None, False, out, store=1)
+        else:
+            _chk(L.lib().upr_t_conv_mfma(x.ptr(), x.B, x.H, x.W, self.Cin, x.cs, 0, _p(self.wp), _p(self.b4),
+                                         4 * self.Cout, 1, 1, 1, 0, 1, None, 0, 0, _fp(out.t), out.cs, 0, 1,
+                                         _stream()), "convT")
         return out
 
     def bwd(self, x, gy, gx):
@@ -298,9 +363,13 @@ class ConvT:
              "unpack")
         _chk(lib.upr_t_chan_sum(gy.ptr(), gy.M, self.Cout, gy.cs, 0, _p(self.m.bias.grad), 1, st), "dbias")
         acc = gx.consume_fresh()
-        _chk(lib.upr_t_conv_mfma(gy.ptr(), gy.B, gy.H, gy.W, self.Cout, gy.cs, 0, _p(self.wd), None, self.Cin, 2, 2,
-                                 2, 0, 1, gx.ptr() if acc else None, gx.cs if acc else 0, 0, _fp(gx.t), gx.cs,
-                                 gx.coff, 0, st), "convT_dgrad")
+        if self.amp:
+            Conv._mfma16(self, gy.t, gy.B, gy.H, gy.W, self.Cout, gy.cs, gy.coff, self.wd16, None, self.Cin, 2, 2, 2,
+                         0, 1, gx if acc else None, False, gx)
+        else:
+            _chk(lib.upr_t_conv_mfma(gy.ptr(), gy.B, gy.H, gy.W, self.Cout, gy.cs, 0, _p(self.wd), None, self.Cin, 2,
+                                     2, 2, 0, 1, gx.ptr() if acc else None, gx.cs if acc else 0, 0, _fp(gx.t),
+                                     gx.cs, gx.coff, 0, st), "convT_dgrad")
 
 
 class BN:
@@ -749,6 +818,7 @@ class UPRetinexTrainGraph:
         B, _, H, W = x.shape
         dev = x.device
         self.x = x
+        set_amp(autocast_active())
         self.pack()
         illu = self.ie.fwd(x)
         self.illu = illu

@@ -350,16 +350,17 @@ def _amp_setup(seed=0):
 
 
 def test_amp_gradscaler_step_equals_fp32_step():
-    """The AMP branch (train.py:71-89) with a power-of-two loss scale: scaling
-    commutes exactly with every rounding, so after unscale_ the gradients, the
-    clipped Adam update and the parameters equal the no-AMP step's."""
+    """The AMP branch's control flow (train.py:71-89) with fp32 arithmetic
+    (amp_fp16=False) and a power-of-two loss scale: scaling commutes exactly
+    with every rounding, so after unscale_ the gradients, the clipped Adam
+    update and the parameters equal the no-AMP step's."""
     from trainers.train import GradScaler, train_step
     x = (torch.rand(2, 3, 64, 64, generator=torch.Generator().manual_seed(11)) * 0.5).to(DEV)
     m1, c1, o1 = _amp_setup()
     train_step(m1, x, c1, o1)
     m2, c2, o2 = _amp_setup()
     scaler = GradScaler(init_scale=2.0 ** 16)
-    l2, d2 = train_step(m2, x, c2, o2, scaler=scaler, use_amp=True)
+    l2, d2 = train_step(m2, x, c2, o2, scaler=scaler, use_amp=True, amp_fp16=False)
     torch.cuda.synchronize()
     assert scaler.get_scale() == 2.0 ** 16  # finite step, growth interval not reached
     p1 = dict(m1.named_parameters())
@@ -395,3 +396,111 @@ def test_amp_gradscaler_skips_nonfinite_step():
     assert opt.step_count == 1 and scaler.get_scale() == 512.0
     moved = sum(int(not torch.equal(p.detach(), before[n])) for n, p in model.named_parameters())
     assert moved > 0
+
+
+def test_amp_autocast_fp16_gradients_vs_oracle():
+    """The reference's AMP step runs forward + loss under autocast (train.py:72):
+    convs in fp16.  With autocast on, the engine computes every MFMA conv (and its
+    input gradient, model and VGG) with fp16 operands and fp32 accumulation.
+
+    Oracle: oracle/net.py + oracle/train.py in fp64, plain (g64) and with the
+    autocast conv arithmetic emulated (net.amp_conv: fp16-rounded operands and
+    outputs, g16).  g16 - g64 is the perturbation fp16 convs cause by
+    themselves; BatchNorm over a small batch amplifies it (B = 4 here).  Per
+    parameter the device gradient must lie within max(2 x that band, 2 x its
+    median over the model, 1e-3) of g64 (rel-L2), and the loss terms within
+    rel 1e-3 of the emulation's."""
+    from oracle import net as onet
+    from oracle import train as otrain
+    from losses.loss import TotalLoss
+    B = 4
+    model = _model(False, False, seed=3)
+    sd_cpu = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    model = model.to(DEV).train()
+    crit = TotalLoss(use_freq_loss=True).to(DEV)
+    x = torch.rand(B, 3, 64, 64, generator=torch.Generator().manual_seed(5)) * 0.6
+    with torch.autocast("cuda", dtype=torch.float16):
+        enh, refl, illu = model(x.to(DEV))
+        total, d = crit(x.to(DEV), enh, illu, refl)
+    total.backward()
+    torch.cuda.synchronize()
+    g = model.__dict__["_upr_train"]["graph"]
+    assert all(c.amp for c in g._convs if getattr(c, "mfma", True)), "autocast step did not use the fp16 conv path"
+    names = otrain.param_names(sd_cpu)
+    vgg = otrain.vgg19_state(VGG_SEED)
+
+    def oracle(amp):
+        s2 = {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in sd_cpu.items()}
+        params = {k: s2[k].clone().requires_grad_(True) for k in names}
+        work = dict(s2)
+        work.update(params)
+        with otrain.train_mode(amp=amp):
+            e_r, r_r, i_r = onet.forward(work, x.double(), False, False)
+            t_r, d_r = otrain.total_loss({k: v.double() for k, v in vgg.items()}, x.double(), e_r, i_r, r_r)
+        t_r.backward()
+        return d_r, {k: params[k].grad for k in names}
+
+    d64, g64 = oracle(False)
+    d16, g16 = oracle(True)
+    for k in ("total", "exposure", "smoothness", "color", "spatial", "decouple", "perceptual", "frequency"):
+        np.testing.assert_allclose(d[k], d16[k], rtol=1e-3, atol=1e-9, err_msg=k)
+    dev_params = dict(model.named_parameters())
+    gmax = max(v.abs().max().item() for v in g64.values())
+    rows = []
+    for n in names:
+        ref = g64[n]
+        if ref.abs().max().item() < 1e-9 * gmax:
+            continue  # BN-fed conv bias: zero true gradient
+        rn = ref.norm().item()
+        dev = (dev_params[n].grad.double().cpu() - ref).norm().item() / rn
+        band = (g16[n] - ref).norm().item() / rn
+        rows.append((n, dev, band))
+    floor = 2.0 * float(np.median([r[2] for r in rows]))
+    for n, dev, band in rows:
+        print(f"{n}: rel-L2 vs fp64 device-AMP {dev:.3e}, emulated autocast {band:.3e}")
+        tol = max(2.0 * band, floor, 1e-3)
+        assert dev <= tol, f"{n}: AMP gradient rel-L2 {dev:.3e} > {tol:.3e} (autocast band {band:.3e})"
+
+
+@pytest.mark.parametrize("amp", [False, True])
+def test_train_step_full_size_bs8_512(amp):
+    """configs[4] at full size (B=8, 512x512, plain model, TotalLoss with the
+    frequency term): the loss and every gradient are finite and the step moves
+    the parameters.  The loss dict of the first two images (B=2 at 512x512) is
+    checked against the CPU oracle's (oracle/train.py, fp32 torch autograd):
+    rel 1e-4 in fp32, 1e-2 with autocast fp16 arithmetic."""
+    from losses.loss import TotalLoss
+    from oracle import net as onet
+    from oracle import train as otrain
+    from trainers.train import GradScaler, make_optimizer, train_step
+    x = torch.rand(8, 3, 512, 512, generator=torch.Generator().manual_seed(2))
+    # B = 2 loss dict vs the oracle
+    model = _model(False, False, seed=0)
+    sd_cpu = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    model = model.to(DEV).train()
+    crit = TotalLoss(use_freq_loss=True).to(DEV)
+    with torch.autocast("cuda", dtype=torch.float16, enabled=amp):
+        enh, refl, illu = model(x[:2].to(DEV))
+        _, d = crit(x[:2].to(DEV), enh, illu, refl)
+    torch.cuda.synchronize()
+    names = otrain.param_names(sd_cpu)
+    work = dict(sd_cpu)
+    with otrain.train_mode():
+        e_r, r_r, i_r = onet.forward(work, x[:2], False, False)
+    with torch.no_grad():
+        _, d_r = otrain.total_loss(otrain.vgg19_state(VGG_SEED), x[:2], e_r, i_r, r_r)
+    for k in ("total", "exposure", "smoothness", "color", "spatial", "decouple", "perceptual", "frequency"):
+        np.testing.assert_allclose(d[k], d_r[k], rtol=1e-2 if amp else 1e-4, atol=1e-8, err_msg=k)
+    # full B = 8 step
+    model = _model(False, False, seed=0).to(DEV).train()
+    before = {n: p.detach().clone() for n, p in model.named_parameters()}
+    opt = make_optimizer(model, lr=1e-4, weight_decay=1e-5)
+    scaler = GradScaler() if amp else None
+    loss, d8 = train_step(model, x.to(DEV), crit, opt, scaler=scaler, use_amp=amp)
+    torch.cuda.synchronize()
+    assert all(np.isfinite(v) for v in d8.values()), d8
+    gn = sum(float(p.grad.double().norm() ** 2) for p in model.parameters()) ** 0.5
+    assert np.isfinite(gn) and gn > 0
+    moved = sum(int(not torch.equal(p.detach(), before[n])) for n, p in model.named_parameters())
+    assert moved > len(before) // 2
+    print(f"bs8 512^2 step (amp={amp}): loss {d8['total']:.6g}, gradient norm before clipping {gn:.4g}")
