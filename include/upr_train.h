@@ -185,8 +185,22 @@ int upr_t_retinex_bwd(const float* x, const float* illu, const float* e, const f
                       void* stream);
 
 /* ---- TotalLoss (losses/loss.py:586-753) -------------------------------- */
+/* The loss modules' constructor arguments (reference defaults in brackets). */
+typedef struct UprLossParams {
+  int patch;              /* AdaptiveExposureLoss patch_size [16] (loss.py:24) */
+  float base_exposure;    /* base_target_exposure [0.6] */
+  float smooth_lambda;    /* EdgeAwareSmoothnessLoss lambda_val [10] (:76) */
+  float smooth_alpha;     /* alpha [1] */
+  float decouple_lambda;  /* IlluminationReflectanceDecouplingLoss lambda_val [0.1] (:271) */
+  float freq_high;        /* FrequencyLoss weight_high [1] (:442) */
+  float freq_low;         /* weight_low [0.5] */
+  int dynamic_smooth;     /* TotalLoss use_dynamic_smooth_weight [1] (:617) */
+} UprLossParams;
 /* Loss workspace bytes for a B x 3 x H x W batch (H, W multiples of 16). */
 size_t upr_t_loss_workspace(int B, int H, int W);
+/* ... for exposure patch size `patch` (H, W >= patch; floor(H/patch) x
+ * floor(W/patch) patches, as F.avg_pool2d). */
+size_t upr_t_loss_workspace_p(int B, int H, int W, int patch);
 /* Every non-perceptual, non-frequency term: exposure (:29-58), edge-aware
  * smoothness (:138-176), colour (:351-371), spatial (:408-427), decoupling
  * (:275-334), texture complexity of img_low (:523-583; texture 0 = 'tv',
@@ -198,6 +212,12 @@ size_t upr_t_loss_workspace(int B, int H, int W);
 int upr_t_loss_pixel(const float* low, const float* enh, const float* illu, const float* refl, int B, int H, int W,
                      void* ws, float* terms, float* g_enh, float* g_illu, float* g_refl, int grads, float w_exp,
                      float w_col, float w_spa, float w_dec, float w_smooth, int texture, void* stream);
+/* The same with the loss modules' arguments (upr_t_loss_pixel = the defaults);
+ * dynamic_smooth = 0 makes terms[8] = w_smooth (no texture pass). */
+int upr_t_loss_pixel_p(const float* low, const float* enh, const float* illu, const float* refl, int B, int H, int W,
+                       void* ws, float* terms, float* g_enh, float* g_illu, float* g_refl, int grads, float w_exp,
+                       float w_col, float w_spa, float w_dec, float w_smooth, int texture,
+                       const UprLossParams* params, void* stream);
 /* Perceptual MSE level (F.mse_loss): acc (fp64) += sum (a-b)^2 / n; with
  * g != NULL, g = scale*2*(a-b) (scale = weight/n). */
 int upr_t_mse(const float* a, const float* b, size_t n, double* acc, float* g, float scale, void* stream);
@@ -209,6 +229,9 @@ int upr_t_vgg_norm_bwd(const float* g_y, float* g_x, int B, int H, int W, void* 
  * with G != NULL, G = scale*2*w*(|Ze|-|Zl|) * Ze/|Ze| (0 where |Ze| = 0). */
 int upr_t_freq(const float* Ze, const float* Zl, int BC, int H, int W, double* acc, float* G, float scale,
                void* stream);
+/* ... with FrequencyLoss(weight_high, weight_low) (upr_t_freq: 1, 0.5). */
+int upr_t_freq_p(const float* Ze, const float* Zl, int BC, int H, int W, double* acc, float* G, float scale,
+                 float w_high, float w_low, void* stream);
 /* g (+)= scale * Re(z) (z interleaved complex, n elements). */
 int upr_t_add_real(const float* z, float* g, size_t n, float scale, void* stream);
 /* out[i] = scale * acc[i], i < n (device-side finalisation of a reduction). */

@@ -182,10 +182,10 @@ def texture_complexity(img, method="tv"):
     return (e > thr).float().mean((1, 2, 3))
 
 
-def total_loss(vgg_sd, low, enh, illu, refl, use_freq=True, texture_method="tv", weight_smooth=1.0):
-    """TotalLoss.forward — loss.py:656-753 (adaptive_weights=False,
-    use_dynamic_smooth_weight=True; weight_smooth scales the dynamic smooth
-    weight, :713).  Returns (total, dict of python floats)."""
+def total_loss(vgg_sd, low, enh, illu, refl, use_freq=True, texture_method="tv", weight_smooth=1.0, dynamic=True):
+    """TotalLoss.forward — loss.py:656-753 (adaptive_weights=False; with
+    use_dynamic_smooth_weight (dynamic) weight_smooth scales the dynamic smooth
+    weight, :705-720, else it is used as is).  Returns (total, dict of python floats)."""
     terms = {
         "exposure": exposure_loss(enh, low),
         "smoothness": smoothness_loss(illu, low),
@@ -196,8 +196,11 @@ def total_loss(vgg_sd, low, enh, illu, refl, use_freq=True, texture_method="tv",
         "frequency": frequency_loss(enh, low) if use_freq else torch.tensor(0.0),
     }
     w = dict(WEIGHTS)
-    tc = texture_complexity(low, texture_method).mean()
-    w["smoothness"] = torch.clamp(weight_smooth * (1.0 - tc * 0.8), 0.1, 5.0)
+    if dynamic:
+        tc = texture_complexity(low, texture_method).mean()
+        w["smoothness"] = torch.clamp(weight_smooth * (1.0 - tc * 0.8), 0.1, 5.0)
+    else:
+        w["smoothness"] = torch.tensor(float(weight_smooth), dtype=enh.dtype)
     total = (w["exposure"] * terms["exposure"] + w["smoothness"] * terms["smoothness"] +
              w["color"] * terms["color"] + w["spatial"] * terms["spatial"] +
              w["decouple"] * terms["decouple"] + w["perceptual"] * terms["perceptual"] +

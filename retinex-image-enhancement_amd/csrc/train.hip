@@ -1048,26 +1048,32 @@ enum {
 
 struct LossWS {
   double* acc;     // LA_FIXED + 7B
-  double* patch;   // B * (H/16) * (W/16) sums of gray(enh)
+  double* patch;   // B * (H/ps) * (W/ps) sums of gray(enh) (ps = exposure patch size)
   double* rowsum;  // B*H   sum_{x<W-1} edge
   double* colsum;  // B*W   sum_{y<H-1} edge
   double* ed;      // 2B    texture 'edge_density': per image sum of |Sobel|, count above threshold
   float* scal;     // finalised scalars for the gradient pass
+  // loss module arguments (UprLossParams)
+  int ps;          // AdaptiveExposureLoss patch_size
+  float base_exp;  // base_target_exposure
+  float lam_s, alpha;  // EdgeAwareSmoothnessLoss lambda_val, alpha
+  float lam_d;     // IlluminationReflectanceDecouplingLoss lambda_val
+  int dynamic;     // TotalLoss use_dynamic_smooth_weight
 };
 
-static LossWS loss_ws(void* ws, int B, int H, int W) {
+static LossWS loss_ws(void* ws, int B, int H, int W, int ps) {
   LossWS l;
   char* p = (char*)ws;
   l.acc = (double*)p; p += align_up(sizeof(double) * (LA_FIXED + 7 * B), 256);
-  l.patch = (double*)p; p += align_up(sizeof(double) * B * (H / 16) * (W / 16), 256);
+  l.patch = (double*)p; p += align_up(sizeof(double) * B * (H / ps) * (W / ps), 256);
   l.rowsum = (double*)p; p += align_up(sizeof(double) * B * H, 256);
   l.colsum = (double*)p; p += align_up(sizeof(double) * B * W, 256);
   l.ed = (double*)p; p += align_up(sizeof(double) * 2 * B, 256);
   l.scal = (float*)p;
   return l;
 }
-static size_t loss_ws_bytes(int B, int H, int W) {
-  return align_up(sizeof(double) * (LA_FIXED + 7 * B), 256) + align_up(sizeof(double) * B * (H / 16) * (W / 16), 256) +
+static size_t loss_ws_bytes(int B, int H, int W, int ps) {
+  return align_up(sizeof(double) * (LA_FIXED + 7 * B), 256) + align_up(sizeof(double) * B * (H / ps) * (W / ps), 256) +
          align_up(sizeof(double) * B * H, 256) + align_up(sizeof(double) * B * W, 256) +
          align_up(sizeof(double) * 2 * B, 256) + align_up(sizeof(float) * (64 + 8 * B), 256);
 }
@@ -1130,7 +1136,7 @@ __global__ __launch_bounds__(256) void loss_pass1_kernel(const float* __restrict
   double v[17];
 #pragma unroll
   for (int k = 0; k < 17; ++k) v[k] = 0.0;
-  const int PW = W / 16;
+  const int ps = ws.ps, PH = H / ps, PW = W / ps;
   for (int q = p0 + threadIdx.x; q < p1; q += 256) {
     const int y = q / W, x = q - y * W;
     float le[3], ll[3];
@@ -1160,7 +1166,8 @@ __global__ __launch_bounds__(256) void loss_pass1_kernel(const float* __restrict
     }
     // exposure patches, edge row / column sums (per-pixel atomics on small arrays)
     const float ge = (le[0] + le[1] + le[2]) / 3.f;
-    atomicAdd(ws.patch + ((size_t)b * (H / 16) + y / 16) * PW + x / 16, (double)ge);
+    // F.avg_pool2d(kernel = stride = ps): floor(H/ps) x floor(W/ps) patches, the remainder ignored
+    if (y < PH * ps && x < PW * ps) atomicAdd(ws.patch + ((size_t)b * PH + y / ps) * PW + x / ps, (double)ge);
     const float ed = edge_at(low, base, H, W, y, x);
     if (x < W - 1) atomicAdd(ws.rowsum + (size_t)b * H + y, (double)ed);
     if (y < H - 1) atomicAdd(ws.colsum + (size_t)b * W + x, (double)ed);
@@ -1187,15 +1194,15 @@ __global__ __launch_bounds__(256) void loss_pass2_kernel(const float* __restrict
     if (x < W - 1) {
       float s = 0.f;
       for (int c = 0; c < 3; ++c) s += fabsf(low[base + c * HW + q] - low[base + c * HW + q + 1]);
-      const float wh = expf(-10.f * (s / 3.f));
-      const float ef = 1.f + (float)(ws.rowsum[(size_t)b * H + y] / (W - 1));
+      const float wh = expf(-ws.lam_s * (s / 3.f));
+      const float ef = 1.f + ws.alpha * (float)(ws.rowsum[(size_t)b * H + y] / (W - 1));
       v[0] += wh * ef * fabsf(il - illu[(size_t)b * HW + q + 1]);
     }
     if (y < H - 1) {
       float s = 0.f;
       for (int c = 0; c < 3; ++c) s += fabsf(low[base + c * HW + q] - low[base + c * HW + q + W]);
-      const float wv = expf(-10.f * (s / 3.f));
-      const float ef = 1.f + (float)(ws.colsum[(size_t)b * W + x] / (H - 1));
+      const float wv = expf(-ws.lam_s * (s / 3.f));
+      const float ef = 1.f + ws.alpha * (float)(ws.colsum[(size_t)b * W + x] / (H - 1));
       v[1] += wv * ef * fabsf(il - illu[(size_t)b * HW + q + W]);
     }
   }
@@ -1230,10 +1237,12 @@ __global__ void loss_final_kernel(int B, int H, int W, LossWS ws, float* __restr
   __shared__ double ex[256];
   const int HW = H * W;
   const double N = (double)B * HW;
-  const double T = 0.6 + 0.2 * (1.0 - ws.acc[LA_GLOW] / N);
-  const int NP = B * (H / 16) * (W / 16);
+  // adaptive target base + (0.8 - base) * (1 - mean gray(low)) (loss.py:49)
+  const double T = ws.base_exp + (0.8 - (double)ws.base_exp) * (1.0 - ws.acc[LA_GLOW] / N);
+  const int NP = B * (H / ws.ps) * (W / ws.ps);
+  const double parea = (double)ws.ps * ws.ps;
   double e = 0.0;
-  for (int k = threadIdx.x; k < NP; k += blockDim.x) e += fabs(ws.patch[k] / 256.0 - T);
+  for (int k = threadIdx.x; k < NP; k += blockDim.x) e += fabs(ws.patch[k] / parea - T);
   ex[threadIdx.x] = e;
   __syncthreads();
   for (int s = 128; s > 0; s >>= 1) {
@@ -1253,8 +1262,11 @@ __global__ void loss_final_kernel(int B, int H, int W, LossWS ws, float* __restr
     for (int b = 0; b < B; ++b) tc += ws.ed[B + b] / HW;
     tc /= B;
   }
-  double wsm = (double)w_smooth * (1.0 - tc * 0.8);
-  wsm = wsm < 0.1 ? 0.1 : (wsm > 5.0 ? 5.0 : wsm);
+  double wsm = (double)w_smooth;
+  if (ws.dynamic) {  // loss.py:705-720
+    wsm = (double)w_smooth * (1.0 - tc * 0.8);
+    wsm = wsm < 0.1 ? 0.1 : (wsm > 5.0 ? 5.0 : wsm);
+  }
   double frob = 0.0, md = 0.0;
   for (int b = 0; b < B; ++b) {
     const double* a = ws.acc + LA_FIXED + b * 7;
@@ -1270,7 +1282,7 @@ __global__ void loss_final_kernel(int B, int H, int W, LossWS ws, float* __restr
     ws.scal[LS_DEC + b * 5 + 3] = (float)(im - rmm);
     ws.scal[LS_DEC + b * 5 + 4] = (float)im;
   }
-  const double dec = frob + 0.1 * md;
+  const double dec = frob + (double)ws.lam_d * md;
   terms[0] = (float)(ex[0] / NP);
   terms[1] = (float)smo;
   terms[2] = (float)col;
@@ -1303,15 +1315,19 @@ __global__ __launch_bounds__(256) void loss_grad_kernel(const float* __restrict_
                          -2.f * (mu0 - mu2) - 2.f * (mu1 - mu2)};
   const float nh = (float)B * 3 * H * (W - 1), nv = (float)B * 3 * (H - 1) * W;
   const float nh1 = (float)B * H * (W - 1), nv1 = (float)B * (H - 1) * W;
-  const int PW = W / 16;
+  const int ps = ws.ps, PH = H / ps, PW = W / ps;
+  const float parea = (float)(ps * ps);
   GSTRIDE(i, n) {
     const int b = (int)(i / HW), q = (int)(i - (long long)b * HW);
     const int y = q / W, x = q - y * W;
     const size_t base = (size_t)b * 3 * HW;
-    // exposure: sign(P - T) / NP / 256 / 3
-    const float P = (float)(ws.patch[((size_t)b * (H / 16) + y / 16) * PW + x / 16] / 256.0);
-    const float dp = P - T;
-    const float gexp = w_exp * (dp > 0.f ? 1.f : (dp < 0.f ? -1.f : 0.f)) / NP / 256.f / 3.f;
+    // exposure: sign(P - T) / NP / ps^2 / 3 (pixels outside the pooled area: 0)
+    float gexp = 0.f;
+    if (y < PH * ps && x < PW * ps) {
+      const float P = (float)(ws.patch[((size_t)b * PH + y / ps) * PW + x / ps] / parea);
+      const float dp = P - T;
+      gexp = w_exp * (dp > 0.f ? 1.f : (dp < 0.f ? -1.f : 0.f)) / NP / parea / 3.f;
+    }
     for (int c = 0; c < 3; ++c) {
       const size_t k = base + c * HW + q;
       float g = gexp + w_col * dcol[c] / N;
@@ -1331,17 +1347,16 @@ __global__ __launch_bounds__(256) void loss_grad_kernel(const float* __restrict_
     auto wgt = [&](int qa, int qb) {
       float s = 0.f;
       for (int c = 0; c < 3; ++c) s += fabsf(low[base + c * HW + qa] - low[base + c * HW + qb]);
-      return expf(-10.f * (s / 3.f));
+      return expf(-ws.lam_s * (s / 3.f));
     };
-    const float efh = 1.f + (float)(ws.rowsum[(size_t)b * H + y] / (W - 1));
+    const float efh = 1.f + ws.alpha * (float)(ws.rowsum[(size_t)b * H + y] / (W - 1));
     if (x < W - 1) gi += wgt(q, q + 1) * efh * sgn(il - illu[ii + 1]) / nh1;
     if (x > 0) gi -= wgt(q - 1, q) * efh * sgn(illu[ii - 1] - il) / nh1;
-    if (y < H - 1) gi += wgt(q, q + W) * (1.f + (float)(ws.colsum[(size_t)b * W + x] / (H - 1))) *
-                         sgn(il - illu[ii + W]) / nv1;
-    if (y > 0) gi -= wgt(q - W, q) * (1.f + (float)(ws.colsum[(size_t)b * W + x] / (H - 1))) *
-                     sgn(illu[ii - W] - il) / nv1;
+    const float efv = 1.f + ws.alpha * (float)(ws.colsum[(size_t)b * W + x] / (H - 1));
+    if (y < H - 1) gi += wgt(q, q + W) * efv * sgn(il - illu[ii + W]) / nv1;
+    if (y > 0) gi -= wgt(q - W, q) * efv * sgn(illu[ii - W] - il) / nv1;
     gi *= wsm;
-    // decoupling: 3*sum_j cov_j^2 + 0.1*(imean - rmean)^2 / B
+    // decoupling: 3*sum_j cov_j^2 + lam_d*(imean - rmean)^2 / B
     const float* sc = ws.scal + LS_DEC + b * 5;
     const float md = sc[3], imean = sc[4];
     const float inv = 1.f / (float)(HW - 1);
@@ -1351,9 +1366,9 @@ __global__ __launch_bounds__(256) void loss_grad_kernel(const float* __restrict_
       const float rmj = (float)(a[1 + j] / HW);
       const float r = refl[base + j * HW + q];
       gd += 6.f * sc[j] * (r - rmj) * inv;
-      g_refl[base + j * HW + q] = w_dec * (6.f * sc[j] * (il - imean) * inv - 0.1f * 2.f * md / (B * 3.f * HW));
+      g_refl[base + j * HW + q] = w_dec * (6.f * sc[j] * (il - imean) * inv - ws.lam_d * 2.f * md / (B * 3.f * HW));
     }
-    gd += 0.1f * 2.f * md / ((float)B * HW);
+    gd += ws.lam_d * 2.f * md / ((float)B * HW);
     g_illu[ii] = gi + w_dec * gd;
   }
 }
@@ -1396,7 +1411,8 @@ __global__ void vgg_norm_bwd_kernel(const float* __restrict__ gy, float* __restr
 }
 
 __global__ __launch_bounds__(256) void freq_kernel(const float2* __restrict__ ze, const float2* __restrict__ zl, int BC,
-                                                   int H, int W, double* acc, float2* G, float scale) {
+                                                   int H, int W, double* acc, float2* G, float scale, float w_high,
+                                                   float w_low) {
   const long long n = (long long)BC * H * W;
   const int ch = H / 2, cw = W / 2, rad = min(H, W) / 4;
   double v[1] = {0.0};
@@ -1404,7 +1420,7 @@ __global__ __launch_bounds__(256) void freq_kernel(const float2* __restrict__ ze
     const int q = (int)(i % ((long long)H * W));
     const int y = q / W, x = q - y * W;
     const float dist = sqrtf((float)((x - cw) * (x - cw)) + (float)((y - ch) * (y - ch)));
-    const float w = dist <= (float)rad ? 0.5f : 1.f;
+    const float w = dist <= (float)rad ? w_low : w_high;
     const float2 a = ze[i], c = zl[i];
     const float me = sqrtf(a.x * a.x + a.y * a.y), ml = sqrtf(c.x * c.x + c.y * c.y);
     const float d = me - ml;
@@ -1930,29 +1946,48 @@ int upr_t_retinex_bwd(const float* x, const float* illu, const float* e, const f
   LAUNCH_CHECK();
 }
 
-size_t upr_t_loss_workspace(int B, int H, int W) {
-  if (B <= 0 || H < 16 || W < 16) return 0;
-  return loss_ws_bytes(B, H, W);
+static const UprLossParams kLossDefaults = {16, 0.6f, 10.f, 1.f, 0.1f, 1.f, 0.5f, 1};
+
+size_t upr_t_loss_workspace(int B, int H, int W) { return upr_t_loss_workspace_p(B, H, W, 16); }
+
+size_t upr_t_loss_workspace_p(int B, int H, int W, int patch) {
+  if (B <= 0 || patch <= 0 || H < patch || W < patch || H < 2 || W < 2) return 0;
+  return loss_ws_bytes(B, H, W, patch);
 }
 
 int upr_t_loss_pixel(const float* low, const float* enh, const float* illu, const float* refl, int B, int H, int W,
                      void* ws, float* terms, float* g_enh, float* g_illu, float* g_refl, int grads, float w_exp,
                      float w_col, float w_spa, float w_dec, float w_smooth, int texture, void* stream) {
-  if (!low || !enh || !illu || !refl || !ws || !terms || B <= 0) return UPR_ERR_ARG;
+  if (H % 16 || W % 16) return UPR_ERR_SHAPE;
+  return upr_t_loss_pixel_p(low, enh, illu, refl, B, H, W, ws, terms, g_enh, g_illu, g_refl, grads, w_exp, w_col,
+                            w_spa, w_dec, w_smooth, texture, &kLossDefaults, stream);
+}
+
+int upr_t_loss_pixel_p(const float* low, const float* enh, const float* illu, const float* refl, int B, int H, int W,
+                       void* ws, float* terms, float* g_enh, float* g_illu, float* g_refl, int grads, float w_exp,
+                       float w_col, float w_spa, float w_dec, float w_smooth, int texture,
+                       const UprLossParams* prm, void* stream) {
+  if (!low || !enh || !illu || !refl || !ws || !terms || !prm || B <= 0) return UPR_ERR_ARG;
   if (texture != 0 && texture != 1) return UPR_ERR_ARG;
-  if (H % 16 || W % 16 || H < 16 || W < 16) return UPR_ERR_SHAPE;
+  if (prm->patch <= 0 || H < prm->patch || W < prm->patch || H < 2 || W < 2) return UPR_ERR_SHAPE;
   if (grads && (!g_enh || !g_illu || !g_refl)) return UPR_ERR_ARG;
   hipStream_t st = ST(stream);
-  const size_t zero_bytes = loss_ws_bytes(B, H, W) - align_up(sizeof(float) * (64 + 8 * B), 256);
+  const size_t zero_bytes = loss_ws_bytes(B, H, W, prm->patch) - align_up(sizeof(float) * (64 + 8 * B), 256);
   UPR_CHECK_HIP(hipMemsetAsync(ws, 0, zero_bytes, st));
-  LossWS l = loss_ws(ws, B, H, W);
+  LossWS l = loss_ws(ws, B, H, W, prm->patch);
+  l.ps = prm->patch;
+  l.base_exp = prm->base_exposure;
+  l.lam_s = prm->smooth_lambda;
+  l.alpha = prm->smooth_alpha;
+  l.lam_d = prm->decouple_lambda;
+  l.dynamic = prm->dynamic_smooth ? 1 : 0;
   int chunks = (H * W) / 4096;
   chunks = chunks < 1 ? 1 : (chunks > 128 ? 128 : chunks);
   hipLaunchKernelGGL(loss_pass1_kernel, dim3(chunks, B), dim3(256), 0, st, low, enh, illu, refl, H, W, l);
   UPR_CHECK_HIP(hipGetLastError());
   hipLaunchKernelGGL(loss_pass2_kernel, dim3(chunks, B), dim3(256), 0, st, low, illu, H, W, l);
   UPR_CHECK_HIP(hipGetLastError());
-  if (texture == 1) {
+  if (texture == 1 && l.dynamic) {
     for (int mode = 0; mode < 2; ++mode) {
       hipLaunchKernelGGL(edge_density_kernel, dim3(chunks, B), dim3(256), 0, st, low, H, W, l, mode);
       UPR_CHECK_HIP(hipGetLastError());
@@ -1997,9 +2032,14 @@ int upr_t_vgg_norm_bwd(const float* g_y, float* g_x, int B, int H, int W, void* 
 
 int upr_t_freq(const float* Ze, const float* Zl, int BC, int H, int W, double* acc, float* G, float scale,
                void* stream) {
+  return upr_t_freq_p(Ze, Zl, BC, H, W, acc, G, scale, 1.f, 0.5f, stream);
+}
+
+int upr_t_freq_p(const float* Ze, const float* Zl, int BC, int H, int W, double* acc, float* G, float scale,
+                 float w_high, float w_low, void* stream) {
   if (!Ze || !Zl || !acc) return UPR_ERR_ARG;
   hipLaunchKernelGGL(freq_kernel, dim3(grid_for((long long)BC * H * W, 256, 4096)), dim3(256), 0, ST(stream),
-                     (const float2*)Ze, (const float2*)Zl, BC, H, W, acc, (float2*)G, scale);
+                     (const float2*)Ze, (const float2*)Zl, BC, H, W, acc, (float2*)G, scale, w_high, w_low);
   LAUNCH_CHECK();
 }
 

@@ -4,8 +4,10 @@ Same classes, constructor arguments and forward signatures; the arithmetic
 runs on the gfx950 kernels of upr/loss_engine.py (include/upr_train.h).
 `TotalLoss.forward` returns `(total_loss, loss_dict)` like the reference
 (:656-753); `total_loss.backward()` sends the loss gradients into the model's
-HIP backward.  The individual term classes evaluate their value only (they
-are not used inside the reference's training step; no autograd through them).
+HIP backward.  The individual term classes are differentiable modules too
+(the engine with weight 1 on their term), with the reference's constructor
+arguments (patch_size, base_target_exposure, lambda_val, alpha, weight_high,
+weight_low) passed to the kernels (include/upr_train.h UprLossParams).
 
 Differences, all forced by the environment and recorded in DESIGN.md:
   * PerceptualLoss loads torchvision's pretrained VGG-19 in the reference
@@ -13,9 +15,9 @@ Differences, all forced by the environment and recorded in DESIGN.md:
     (e.g. a local copy of torchvision's vgg19 weights); without one the VGG is
     PyTorch-default-initialised under `vgg_seed` (1234, the seed the parity
     fixtures use).
-  * use_dynamic_smooth_weight=False is not implemented on the device and
-    raises.  adaptive_weights=True (DWA, :755-798) keeps the reference's host
-    loss history; texture_method 'tv' and 'edge_density' both run on the device.
+  * adaptive_weights=True (DWA, :755-798) keeps the reference's host loss
+    history; texture_method 'tv' and 'edge_density' both run on the device;
+    use_dynamic_smooth_weight=False uses weight_smooth as is.
 """
 import torch
 import torch.nn as nn
@@ -44,109 +46,155 @@ def _features(vgg_weights, vgg_seed):
 
 
 class _EngineHolder(nn.Module):
+    _weights = None
+    _params = None
+    use_freq_loss = True
+    texture_method = "tv"
+
     def _engine(self, dev):
         eng = self.__dict__.get("_eng")
         if eng is None or eng[0] != dev:
-            feats = self.features.to(dev) if hasattr(self, "features") else E.vgg19_features(_VGG_SEED).to(dev)
-            eng = (dev, E.TotalLossEngine(feats, weights=getattr(self, "_weights", None),
-                                          use_freq_loss=getattr(self, "use_freq_loss", True),
-                                          texture_method=getattr(self, "texture_method", "tv")))
+            feats = self.features.to(dev) if hasattr(self, "features") else None
+            eng = (dev, E.TotalLossEngine(feats, weights=self._weights, use_freq_loss=self.use_freq_loss,
+                                          texture_method=self.texture_method, params=self._params))
             self.__dict__["_eng"] = eng
         return eng[1]
 
 
-def _term(mod, idx, low, enh, illu, refl):
-    for t, n in ((low, "img_low"), (enh, "img_enhanced"), (illu, "illu_map"), (refl, "reflectance")):
-        _require(t, n)
-    with torch.no_grad():
-        _, terms = loss_forward(mod._engine(enh.device), low.contiguous(), enh.contiguous(), illu.contiguous(),
+class _Term(_EngineHolder):
+    """One loss term as its own differentiable module: the loss engine with
+    weight 1 on this term and 0 elsewhere (the smoothness weight fixed, not
+    dynamic), so the returned 0-dim tensor IS the term and its backward is the
+    term's gradient w.r.t. the module's differentiable inputs."""
+
+    _term = None
+
+    def _setup(self, **params):
+        w = {k: 0.0 for k in E.WEIGHTS}
+        w[self._term] = 1.0
+        self._weights = w
+        p = dict(E.PARAMS)
+        p.update(params)
+        p["dynamic_smooth"] = False
+        self._params = p
+        self.use_freq_loss = self._term == "frequency"
+
+    def _eval(self, low, enh, illu, refl):
+        for t, n in ((low, "img_low"), (enh, "img_enhanced"), (illu, "illu_map"), (refl, "reflectance")):
+            _require(t, n)
+        total, _ = loss_forward(self._engine(enh.device), low.contiguous(), enh.contiguous(), illu.contiguous(),
                                 refl.contiguous())
-    return terms[idx].clone()
+        return total
 
 
 def _dummy_illu(x):
     return x[:, :1].contiguous()
 
 
-class AdaptiveExposureLoss(_EngineHolder):
-    """L_exp (reference :12-58): mean |avgpool16(gray(R)) - (0.6 + 0.2(1 - mean gray(S)))|."""
+class AdaptiveExposureLoss(_Term):
+    """L_exp (reference :12-58): mean |avgpool_ps(gray(R)) - (b + (0.8 - b)(1 - mean gray(S)))|."""
+
+    _term = "exposure"
 
     def __init__(self, patch_size=16, base_target_exposure=0.6):
         super().__init__()
-        if patch_size != 16 or base_target_exposure != 0.6:
-            raise NotImplementedError("the device kernel implements the reference defaults (16, 0.6)")
+        if int(patch_size) != patch_size or patch_size < 1:
+            raise ValueError(f"patch_size must be a positive integer, got {patch_size}")
         self.patch_size, self.base_target_exposure = patch_size, base_target_exposure
+        self._setup(patch=int(patch_size), base_exposure=float(base_target_exposure))
 
     def forward(self, img_enhanced, img_low):
-        return _term(self, 0, img_low, img_enhanced, _dummy_illu(img_enhanced), img_enhanced)
+        return self._eval(img_low, img_enhanced, _dummy_illu(img_enhanced), img_enhanced)
 
 
-class EdgeAwareSmoothnessLoss(_EngineHolder):
-    """L_smooth (reference :61-176)."""
+class EdgeAwareSmoothnessLoss(_Term):
+    """L_smooth (reference :61-176): exp(-lambda |grad S|) x (1 + alpha x row / column edge means) x |grad I|."""
+
+    _term = "smoothness"
 
     def __init__(self, lambda_val=10.0, alpha=1.0):
         super().__init__()
-        if lambda_val != 10.0 or alpha != 1.0:
-            raise NotImplementedError("the device kernel implements the reference defaults (10, 1)")
         self.lambda_val, self.alpha = lambda_val, alpha
+        self._setup(smooth_lambda=float(lambda_val), smooth_alpha=float(alpha))
 
     def forward(self, illu_map, img_low):
-        return _term(self, 1, img_low, img_low, illu_map, img_low)
+        if illu_map.dim() != 4 or illu_map.shape[1] != 1:
+            raise NotImplementedError("device smoothness loss: illumination [B,1,H,W] (the model's)")
+        return self._eval(img_low, img_low, illu_map, img_low)
 
 
-class ColorLoss(_EngineHolder):
+class ColorLoss(_Term):
     """L_col gray-world (reference :337-371)."""
 
+    _term = "color"
+
+    def __init__(self):
+        super().__init__()
+        self._setup()
+
     def forward(self, img_enhanced):
-        return _term(self, 2, img_enhanced, img_enhanced, _dummy_illu(img_enhanced), img_enhanced)
+        return self._eval(img_enhanced, img_enhanced, _dummy_illu(img_enhanced), img_enhanced)
 
 
-class SpatialConsistencyLoss(_EngineHolder):
+class SpatialConsistencyLoss(_Term):
     """L_spa (reference :374-427)."""
 
+    _term = "spatial"
+
+    def __init__(self):
+        super().__init__()
+        self._setup()
+
     def forward(self, img_enhanced, img_low):
-        return _term(self, 3, img_low, img_enhanced, _dummy_illu(img_enhanced), img_enhanced)
+        return self._eval(img_low, img_enhanced, _dummy_illu(img_enhanced), img_enhanced)
 
 
-class IlluminationReflectanceDecouplingLoss(_EngineHolder):
-    """L_decouple (reference :258-334), the model's case C_illu = 1, C_refl = 3."""
+class IlluminationReflectanceDecouplingLoss(_Term):
+    """L_decouple (reference :258-334), the model's case C_illu = 1, C_refl = 3:
+    ||cov||_F^2 + lambda x mse(mean I, mean R)."""
+
+    _term = "decouple"
 
     def __init__(self, lambda_val=0.1):
         super().__init__()
-        if lambda_val != 0.1:
-            raise NotImplementedError("the device kernel implements the reference default (0.1)")
         self.lambda_val = lambda_val
+        self._setup(decouple_lambda=float(lambda_val))
 
     def forward(self, illu_map, reflectance):
         if illu_map.shape[1] != 1 or reflectance.shape[1] != 3:
             raise NotImplementedError("device decoupling loss: illumination [B,1,H,W], reflectance [B,3,H,W]")
-        return _term(self, 4, reflectance, reflectance, illu_map, reflectance)
+        return self._eval(reflectance, reflectance, illu_map, reflectance)
 
 
-class PerceptualLoss(_EngineHolder):
+class PerceptualLoss(_Term):
     """L_perceptual (reference :179-255): VGG-19 slices to pool3, summed MSEs."""
+
+    _term = "perceptual"
 
     def __init__(self, device='cpu', vgg_weights=None, vgg_seed=_VGG_SEED):
         super().__init__()
         self.features = _features(vgg_weights, vgg_seed)
         self.register_buffer('mean', torch.tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1))
         self.register_buffer('std', torch.tensor([0.229, 0.224, 0.225]).view(1, 3, 1, 1))
+        self._setup()
 
     def forward(self, img_enhanced, img_low):
-        return _term(self, 5, img_low, img_enhanced, _dummy_illu(img_enhanced), img_enhanced)
+        return self._eval(img_low, img_enhanced, _dummy_illu(img_enhanced), img_enhanced)
 
 
-class FrequencyLoss(_EngineHolder):
-    """L_freq (reference :430-520)."""
+class FrequencyLoss(_Term):
+    """L_freq (reference :430-520): weighted MSE of FFT magnitudes (weight_high
+    outside radius min(H, W)/4 of the unshifted centre, weight_low inside)."""
+
+    _term = "frequency"
 
     def __init__(self, weight_high=1.0, weight_low=0.5):
         super().__init__()
-        if weight_high != 1.0 or weight_low != 0.5:
-            raise NotImplementedError("the device kernel implements the reference defaults (1.0, 0.5)")
         self.weight_high, self.weight_low = weight_high, weight_low
+        self._setup(freq_high=float(weight_high), freq_low=float(weight_low))
 
     def forward(self, img_enhanced, img_low):
-        return _term(self, 6, img_low, img_enhanced, _dummy_illu(img_enhanced), img_enhanced)
+        return self._eval(img_low, img_enhanced, _dummy_illu(img_enhanced), img_enhanced)
 
 
 class TotalLoss(_EngineHolder):
@@ -156,9 +204,6 @@ class TotalLoss(_EngineHolder):
                  weight_perceptual=1.0, weight_freq=0.5, use_freq_loss=True, adaptive_weights=False,
                  use_dynamic_smooth_weight=True, texture_method='tv', vgg_weights=None, vgg_seed=_VGG_SEED):
         super().__init__()
-        if not use_dynamic_smooth_weight:
-            raise NotImplementedError("the device loss implements the dynamic smooth weight "
-                                      "(use_dynamic_smooth_weight=True, the reference training default)")
         if texture_method not in E.TEXTURE:
             raise ValueError(f"不支持的纹理复杂度计算方法: {texture_method}")
         self.features = _features(vgg_weights, vgg_seed)
@@ -168,6 +213,8 @@ class TotalLoss(_EngineHolder):
         self.texture_method = texture_method
         self._weights = dict(exposure=weight_exp, smoothness=weight_smooth, color=weight_col, spatial=weight_spa,
                              decouple=weight_decouple, perceptual=weight_perceptual, frequency=weight_freq)
+        # TotalLoss builds its terms with their default arguments (loss.py:620-626)
+        self._params = dict(E.PARAMS, dynamic_smooth=bool(use_dynamic_smooth_weight))
         if adaptive_weights:
             self.loss_history = {k: [] for k in _DWA_KEYS}
 

@@ -83,6 +83,13 @@ class UprView(ctypes.Structure):
                 ("sw", ctypes.c_int64), ("sc", ctypes.c_int64)]
 
 
+class UprLossParams(ctypes.Structure):
+    """include/upr_train.h UprLossParams: the loss modules' constructor arguments."""
+    _fields_ = [("patch", ctypes.c_int), ("base_exposure", ctypes.c_float), ("smooth_lambda", ctypes.c_float),
+                ("smooth_alpha", ctypes.c_float), ("decouple_lambda", ctypes.c_float), ("freq_high", ctypes.c_float),
+                ("freq_low", ctypes.c_float), ("dynamic_smooth", ctypes.c_int)]
+
+
 _vp = ctypes.POINTER(UprView)
 c_u64, c_i64p = ctypes.c_uint64, ctypes.c_void_p
 _i, _p, _f = c_int, c_void_p, c_float
@@ -127,11 +134,14 @@ SIGNATURES.update({
     "upr_t_retinex_fwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _p]),
     "upr_t_retinex_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p]),
     "upr_t_loss_workspace": (c_size_t, [_i, _i, _i]),
+    "upr_t_loss_workspace_p": (c_size_t, [_i, _i, _i, _i]),
+    "upr_t_loss_pixel_p": (_i, [_p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p, _i, _f, _f, _f, _f, _f, _i, _p, _p]),
     "upr_t_loss_pixel": (_i, [_p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p, _i, _f, _f, _f, _f, _f, _i, _p]),
     "upr_t_mse": (_i, [_p, _p, c_size_t, _p, _p, _f, _p]),
     "upr_t_vgg_norm": (_i, [_p, _p, _i, _i, _i, _p]),
     "upr_t_vgg_norm_bwd": (_i, [_p, _p, _i, _i, _i, _p]),
     "upr_t_freq": (_i, [_p, _p, _i, _i, _i, _p, _p, _f, _p]),
+    "upr_t_freq_p": (_i, [_p, _p, _i, _i, _i, _p, _p, _f, _f, _f, _p]),
     "upr_t_add_real": (_i, [_p, _p, c_size_t, _f, _p]),
     "upr_t_scale_acc": (_i, [_p, _i, _f, _p, _p]),
     "upr_t_loss_total": (_i, [_p, _f, _f, _f, _f, _f, _f, _p]),

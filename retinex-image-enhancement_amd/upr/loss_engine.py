@@ -25,6 +25,9 @@ from .train import Act, Conv, _chk, _fp, _p, _stream, autocast_active, empty, re
 
 WEIGHTS = dict(exposure=10.0, smoothness=1.0, color=0.5, spatial=1.0, decouple=0.1, perceptual=1.0,
                frequency=0.5)
+# the loss modules' constructor arguments (reference defaults; include/upr_train.h UprLossParams)
+PARAMS = dict(patch=16, base_exposure=0.6, smooth_lambda=10.0, smooth_alpha=1.0, decouple_lambda=0.1,
+              freq_high=1.0, freq_low=0.5, dynamic_smooth=True)
 TEXTURE = {"tv": 0, "edge_density": 1}  # calculate_texture_complexity methods (loss.py:523-583)
 TERM_ORDER = ("exposure", "smoothness", "color", "spatial", "decouple", "perceptual", "frequency", "total")
 
@@ -114,12 +117,15 @@ class VGGPerceptual:
 
 
 class TotalLossEngine:
-    """losses/loss.py TotalLoss with use_dynamic_smooth_weight=True
-    (train.py:224-234).  `w` holds the weights of the current step (the DWA
-    weights when TotalLoss adapts them); `w_smooth` is the constructor's
-    weight_smooth, which the dynamic smooth weight scales (loss.py:713)."""
+    """losses/loss.py TotalLoss (train.py:224-234).  `w` holds the weights of
+    the current step (the DWA weights when TotalLoss adapts them); `w_smooth`
+    is the constructor's weight_smooth, which the dynamic smooth weight scales
+    (loss.py:713) when params['dynamic_smooth'].  `params`: the loss modules'
+    arguments (PARAMS).  A term whose weight is 0 still has its value computed,
+    except perceptual (the VGG passes are skipped: value 0) — the single-term
+    modules of losses/loss.py use that."""
 
-    def __init__(self, vgg_features, weights=None, use_freq_loss=True, texture_method="tv"):
+    def __init__(self, vgg_features, weights=None, use_freq_loss=True, texture_method="tv", params=None):
         if texture_method not in TEXTURE:
             raise ValueError(f"不支持的纹理复杂度计算方法: {texture_method}")
         self.w = dict(WEIGHTS)
@@ -128,8 +134,17 @@ class TotalLossEngine:
         self.w_smooth = self.w["smoothness"]
         self.texture_method = texture_method
         self.use_freq = use_freq_loss
-        self.vgg = VGGPerceptual(vgg_features)
+        self.params = dict(PARAMS)
+        if params:
+            self.params.update(params)
+        self.vgg = VGGPerceptual(vgg_features) if vgg_features is not None else None
         self.features = vgg_features
+
+    def _cparams(self):
+        p = self.params
+        return L.UprLossParams(int(p["patch"]), float(p["base_exposure"]), float(p["smooth_lambda"]),
+                               float(p["smooth_alpha"]), float(p["decouple_lambda"]), float(p["freq_high"]),
+                               float(p["freq_low"]), int(bool(p["dynamic_smooth"])))
 
     def __call__(self, low, enh, illu, refl, grads=True):
         """All NCHW fp32 device tensors.  Returns (terms [9] device tensor in
@@ -140,17 +155,29 @@ class TotalLossEngine:
         w = self.w
         terms = torch.empty(9, dtype=torch.float32, device=dev)
         zero(terms)
-        ws = torch.empty(lib.upr_t_loss_workspace(B, H, W), dtype=torch.uint8, device=dev)
+        prm = self._cparams()
+        nws = lib.upr_t_loss_workspace_p(B, H, W, prm.patch)
+        if nws == 0:
+            raise ValueError(f"loss: a {H}x{W} image is smaller than the exposure patch ({prm.patch})")
+        ws = torch.empty(nws, dtype=torch.uint8, device=dev)
         g_enh = g_illu = g_refl = None
         if grads:
             g_enh, g_illu, g_refl = empty(enh.shape, dev), empty(illu.shape, dev), empty(refl.shape, dev)
-        _chk(lib.upr_t_loss_pixel(_p(low), _p(enh), _p(illu), _p(refl), B, H, W, _p(ws), _p(terms), _p(g_enh),
-                                  _p(g_illu), _p(g_refl), int(grads), ctypes.c_float(w["exposure"]),
-                                  ctypes.c_float(w["color"]), ctypes.c_float(w["spatial"]),
-                                  ctypes.c_float(w["decouple"]), ctypes.c_float(self.w_smooth),
-                                  TEXTURE[self.texture_method], st), "loss_pixel")
+        _chk(lib.upr_t_loss_pixel_p(_p(low), _p(enh), _p(illu), _p(refl), B, H, W, _p(ws), _p(terms), _p(g_enh),
+                                    _p(g_illu), _p(g_refl), int(grads), ctypes.c_float(w["exposure"]),
+                                    ctypes.c_float(w["color"]), ctypes.c_float(w["spatial"]),
+                                    ctypes.c_float(w["decouple"]), ctypes.c_float(self.w_smooth),
+                                    TEXTURE[self.texture_method], ctypes.byref(prm), st), "loss_pixel")
         acc = torch.empty(4, dtype=torch.float64, device=dev)
         zero(acc)
+        if self.vgg is not None and w["perceptual"] != 0.0:
+            self._perceptual(lib, st, low, enh, B, H, W, terms, acc, grads, g_enh)
+        self._frequency(lib, st, low, enh, B, C, H, W, terms, acc, grads, g_enh, prm)
+        return terms, ((g_enh, g_illu, g_refl) if grads else None)
+
+    def _perceptual(self, lib, st, low, enh, B, H, W, terms, acc, grads, g_enh):
+        w = self.w
+        dev = enh.device
         # ---- perceptual (VGG convs in fp16 under the caller's autocast, as the reference's) ----
         set_amp(autocast_active())
         self.vgg.pack()
@@ -171,14 +198,18 @@ class TotalLossEngine:
         if grads:
             g_in = self.vgg.backward(trace, gfe)
             _chk(lib.upr_t_vgg_norm_bwd(_fp(g_in.t), _p(g_enh), B, H, W, st), "vgg_norm_bwd")
+
+    def _frequency(self, lib, st, low, enh, B, C, H, W, terms, acc, grads, g_enh, prm):
+        w = self.w
         # ---- frequency ----
         if self.use_freq:
             ze = torch.fft.fft2(enh, dim=(-2, -1))
             zl = torch.fft.fft2(low, dim=(-2, -1))
             n = enh.numel()
             G = torch.empty_like(ze) if grads else None
-            _chk(lib.upr_t_freq(_p(ze), _p(zl), B * C, H, W, _p(acc[2:3]), _p(G),
-                                ctypes.c_float(w["frequency"] / n), st), "freq")
+            _chk(lib.upr_t_freq_p(_p(ze), _p(zl), B * C, H, W, _p(acc[2:3]), _p(G),
+                                  ctypes.c_float(w["frequency"] / n), ctypes.c_float(prm.freq_high),
+                                  ctypes.c_float(prm.freq_low), st), "freq")
             _chk(lib.upr_t_scale_acc(_p(acc[2:3]), 1, ctypes.c_float(1.0 / n), _fp(terms, 6), st), "scale")
             if grads:
                 gx = torch.fft.ifft2(G, dim=(-2, -1))
@@ -187,7 +218,6 @@ class TotalLossEngine:
                                   ctypes.c_float(w["spatial"]), ctypes.c_float(w["decouple"]),
                                   ctypes.c_float(w["perceptual"]), ctypes.c_float(w["frequency"] if self.use_freq
                                                                                   else 0.0), st), "total")
-        return terms, ((g_enh, g_illu, g_refl) if grads else None)
 
 
 def terms_dict(terms):

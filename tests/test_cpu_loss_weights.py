@@ -35,5 +35,23 @@ def test_totalloss_arguments():
     TotalLoss(texture_method="edge_density", weight_smooth=2.0, adaptive_weights=True)
     with pytest.raises(ValueError):
         TotalLoss(texture_method="sobel")
-    with pytest.raises(NotImplementedError):
-        TotalLoss(use_dynamic_smooth_weight=False)
+    t = TotalLoss(use_dynamic_smooth_weight=False, weight_smooth=3.0)
+    assert t._params["dynamic_smooth"] is False and t._weights["smoothness"] == 3.0
+
+
+def test_loss_term_module_arguments():
+    """The term modules keep the reference's constructor arguments and pass them
+    to the device engine (values vs the oracle: tests/test_gpu_losses.py)."""
+    from losses import loss as L
+    m = L.AdaptiveExposureLoss(patch_size=8, base_target_exposure=0.5)
+    assert (m.patch_size, m.base_target_exposure) == (8, 0.5)
+    assert m._params["patch"] == 8 and m._params["base_exposure"] == 0.5 and m._weights["exposure"] == 1.0
+    assert sum(m._weights.values()) == 1.0 and m._params["dynamic_smooth"] is False
+    s = L.EdgeAwareSmoothnessLoss(lambda_val=5.0, alpha=0.5)
+    assert s._params["smooth_lambda"] == 5.0 and s._params["smooth_alpha"] == 0.5
+    assert L.IlluminationReflectanceDecouplingLoss(lambda_val=0.3)._params["decouple_lambda"] == 0.3
+    f = L.FrequencyLoss(weight_high=2.0, weight_low=0.25)
+    assert f._params["freq_high"] == 2.0 and f._params["freq_low"] == 0.25 and f.use_freq_loss
+    assert not L.ColorLoss().use_freq_loss
+    with pytest.raises(ValueError):
+        L.AdaptiveExposureLoss(patch_size=0)

@@ -40,8 +40,7 @@ def test_losses_refuse_cpu_tensors():
 
 
 def test_unsupported_options_raise():
-    with pytest.raises(NotImplementedError):
-        L.TotalLoss(use_dynamic_smooth_weight=False)
+    L.TotalLoss(use_dynamic_smooth_weight=False)  # supported (tests/test_gpu_losses.py)
     with pytest.raises(ValueError):
         L.TotalLoss(texture_method="laplacian")
 
