@@ -395,6 +395,7 @@ int launch_conv_halo(const ConvOp& op, int dtype, hipStream_t st);
 int launch_conv_wide(const ConvOp& op, hipStream_t st);
 int launch_conv_stream(const ConvOp& op, hipStream_t st);
 int launch_conv_ring(const ConvOp& op, hipStream_t st);
+int launch_conv_ring32(const ConvOp& op, hipStream_t st);
 int launch_conv_wide32(const ConvOp& op, hipStream_t st);
 
 // UPR_CONV_IMPL=generic forces the implicit-GEMM kernel everywhere (A/B tests);
@@ -421,7 +422,9 @@ int launch_conv(const ConvOp& op, int dtype, hipStream_t stream) {
       rc = launch_conv_stream(op, stream);
       if (rc != kErrUnsupported) return rc;
     } else {
-      const int rc = launch_conv_wide32(op, stream);
+      int rc = launch_conv_wide32(op, stream);
+      if (rc != kErrUnsupported) return rc;
+      rc = launch_conv_ring32(op, stream);
       if (rc != kErrUnsupported) return rc;
     }
     const int rc = launch_conv_halo(op, dtype, stream);

@@ -660,6 +660,277 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, RingCfg<MODE, C, NB, FL
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// ---------------------------------------------------------------------------
+// fp32 form (the configs[1] graph): the same ring / step / DMA structure for the
+// 32-channel stride-1 3x3 convs at 512^2 (UpBlock dec1 convs, residual head,
+// FAM branch3/4 first convs), on v_mfma_f32_16x16x4_f32.  A 16-byte chunk holds
+// 4 channels, so a 32-channel slice is 8 chunk planes; each MFMA contracts 4
+// channels and the slice's 8 MFMAs use the k order "lane group fg takes
+// channels fg*8 .. fg*8+7" for both operands (any permutation of k shared by A
+// and B leaves the sum unchanged): a lane reads its pixel's 8 channels as two
+// conflict-free ds_read_b128 (planes 2fg, 2fg+1) per tap and feeds 8 MFMAs.
+// fp32 MFMA time (32 cycles per 16x16x4) bounds these layers, not HBM.
+// ---------------------------------------------------------------------------
+template <int MODE, int NB, int FL>
+struct Ring32Cfg {
+  static constexpr bool HEAD = MODE == kRingHead;
+  static constexpr bool RES = FL & kRingRes, RELU = (FL & kRingRelu) != 0;
+  static constexpr int C = 32, NT = NB / 16, NG = 2;
+  using RA = Ring<8, 34, 4>;                        // 32 fp32 channels = 8 chunk planes, 1-pixel halo
+  static constexpr bool WREG = NT == 2;             // 9 taps x 2 tiles x 8 floats = 144 VGPRs
+  static constexpr int WBYTES = WREG ? 0 : 9 * NB * 32 * 4;  // [tap][n][32 k] fp32
+  static constexpr int EW = RES ? 32 * NB * 4 : HEAD ? 512 : 0;
+  static constexpr int E = RES ? NB / 8 : HEAD ? 1 : 0;
+  static constexpr int LDS = WBYTES + RA::BYTES + 4 * EW;
+  static constexpr int G = RA::G;
+  static constexpr int S = HEAD ? NG : NG * NT;
+  static constexpr int W0 = G, W1 = E + G + S, WK = 2 * S + E + G;
+  static_assert(WK <= 63, "vmcnt immediate");
+};
+
+template <int MODE, int NB, int FL>
+__global__ __launch_bounds__(256) void conv_ring32_kernel(RingArgs a) {
+  using K = Ring32Cfg<MODE, NB, FL>;
+  using RA = typename K::RA;
+  constexpr bool HEAD = K::HEAD, RES = K::RES;
+  constexpr int NT = K::NT, NG = K::NG;
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  const ConvOp& op = a.op;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* Wl = smem;
+  unsigned char* ringA = smem + K::WBYTES;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fg = lane >> 4;
+  unsigned char* epi = ringA + RA::BYTES + wave * K::EW;
+  const int H = op.Ho, W = op.Wo;
+  const ConvSeg& sa = op.seg[0];
+  const int per_xcd = gridDim.x >> 3;
+  const int v0 = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+  const int nu = v0 < a.nunits ? (a.nunits - 1 - v0) / (int)gridDim.x + 1 : 0;
+  const int KT = nu * a.steps;
+
+  // filter: lane (fr = n within tile, fg) holds W[nt*16 + fr][tap*32 + fg*8 .. +7]
+  f32x4 wr[K::WREG ? 9 : 1][NT][2];
+  if constexpr (K::WREG) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          wr[t][nt][h] = *(const f32x4*)((const float*)op.W + (size_t)(nt * 16 + fr) * op.Kpad + t * 32 + fg * 8 + h * 4);
+  } else {
+    // LDS [tap][n][32 floats], the 8-float run of lane group fg at 32*fg bytes (+ h*16)
+    for (int i = tid; i < 9 * NB * 8; i += 256) {
+      const int c4 = i & 7, n = (i >> 3) % NB, t = (i >> 3) / NB;
+      *(f32x4*)(Wl + (size_t)i * 16) = *(const f32x4*)((const float*)op.W + (size_t)n * op.Kpad + t * 32 + c4 * 4);
+    }
+  }
+  const half_t* srcA = (const half_t*)((const float*)sa.src + sa.coff);  // element offsets in halves below
+  const int csA = sa.cs * 2;                                           // pixel stride in halves
+  const half_t* zero = (const half_t*)g_ring_zero;
+  RingLanes<RA> la;
+  la.init(lane, sa.Win, csA);
+
+  auto unit_of = [&](int j, int& b, int& y0, int& x0) {
+    const int u = v0 + j * (int)gridDim.x;
+    const int sx = u % a.nstrips, r = u / a.nstrips;
+    b = r / a.nseg;
+    y0 = (r % a.nseg) * a.rs;
+    x0 = sx * 32;
+  };
+  const int S = a.steps - 1;
+  struct Cursor {
+    int j, s, b, y0, x0;
+  };
+  Cursor cc{0, -1, 0, 0, 0};
+  if (nu > 0) unit_of(0, cc.b, cc.y0, cc.x0);
+  Cursor dc = cc;
+  auto advance = [&](Cursor& c) {
+    if (++c.s == S) {
+      c.s = -1;
+      if (++c.j < nu) unit_of(c.j, c.b, c.y0, c.x0);
+    }
+  };
+  // RingLanes addresses half_t elements: an fp32 chunk c (4 channels) is at
+  // half offset 8c, i.e. plane c <-> chunk c of the pixel
+  auto issue = [&](int k) {
+    const bool live = dc.j < nu;
+    la.issue(srcA, csA, dc.b, sa.Hin, sa.Win, dc.y0 + 4 * dc.s + 1, dc.x0 - 1, live, zero, ringA, (k + 1) & 3, wave);
+    advance(dc);
+  };
+
+  __syncthreads();
+  issue(0);
+  issue(1);
+
+  float bv[NT][4];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bv[nt][i] = op.bias ? op.bias[nt * 16 + fg * 4 + i] : 0.f;
+  float hw2[NT][4];
+  if constexpr (HEAD) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) hw2[nt][i] = op.head_w[nt * 16 + fg * 4 + i];
+  }
+  const int abase = 2 * fg * RA::PLANE + fr * 16;  // planes 2fg, 2fg+1 (channels fg*8 .. +7)
+  const int ocs = op.out_cs, rcs = RES ? op.res2_cs : 0;
+  const size_t HWs = (size_t)H * W;
+
+  for (int kk = 0; kk < KT; ++kk) {
+    if (kk == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K::W0) : "memory");
+    else if (kk == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K::W1) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K::WK) : "memory");
+    __builtin_amdgcn_s_barrier();
+    const int s = cc.s, b = cc.b, x0 = cc.x0;
+    const int yend = min(H, cc.y0 + a.rs);
+    const int y = cc.y0 + 4 * s + wave;
+    const bool rowok = s >= 0 && y < yend;
+    const size_t prow = (size_t)(b * H + (rowok ? y : 0)) * W + x0;
+    bool ovalid[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) ovalid[g] = rowok && x0 + g * 16 + fr < W;
+    if constexpr (RES) {
+      // 32 px x NB fp32 channels, pixel-major
+      constexpr int CPP = NB / 4;
+#pragma unroll
+      for (int i = 0; i < K::E; ++i) {
+        const int q = i * 64 + lane, px = q / CPP;
+        const bool ok = rowok && x0 + px < W;
+        const void* p = ok ? (const void*)((const float*)op.res2 + (prow + px) * rcs + (q % CPP) * 4) : (const void*)zero;
+        __builtin_amdgcn_global_load_lds(p, (lds_void_ptr_r)(epi + i * 1024), 16, 0, 0);
+      }
+    }
+    if constexpr (HEAD) {
+      const int ppc = op.x_f16 ? 8 : 4, cpr = 32 / ppc;
+      if (lane < 3 * cpr) {
+        const int c = lane / cpr, k = lane % cpr;
+        const bool ok = rowok && x0 + k * ppc < W;
+        const size_t e = (size_t)b * 2 * HWs + prow + c * HWs + k * ppc;
+        const void* p = !ok ? (const void*)zero
+                            : op.x_f16 ? (const void*)((const half_t*)op.x_nchw + e) : (const void*)(op.x_nchw + e);
+        __builtin_amdgcn_global_load_lds(p, (lds_void_ptr_r)epi, 16, 0, 0);
+      }
+    }
+    issue(kk + 2);
+
+    f32x4 acc[NT][NG];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int g = 0; g < NG; ++g) acc[nt][g] = f32x4{bv[nt][0], bv[nt][1], bv[nt][2], bv[nt][3]};
+#define RING_FENCE __builtin_amdgcn_sched_barrier(0)
+#define RING_LDS_DONE                                                               \
+  do {                                                                              \
+    RING_FENCE;                                                                     \
+    __builtin_amdgcn_s_waitcnt(0xC07F); /* lgkmcnt(0); vmcnt / expcnt untouched */ \
+    RING_FENCE;                                                                     \
+  } while (0)
+    if (s >= 0) {
+      // chunk = one tap row r: 3 taps x 2 groups x 2 halves of X (+ 3 x NT x 2 of W from LDS)
+      auto rowA = [&](int r) { return ((4 * kk + 4 + wave - 1 + r - 1) & 15) * (RA::RW * 16); };
+      constexpr int NW = K::WREG ? 1 : 3;
+      f32x4 bx[2][3][NG][2], bw[2][NW][NT][2];
+      auto ld = [&](int r, f32x4 (&x)[3][NG][2], f32x4 (&w)[NW][NT][2]) {
+        const unsigned char* xr = ringA + abase + rowA(r);
+#pragma unroll
+        for (int sc = 0; sc < 3; ++sc)
+#pragma unroll
+          for (int g = 0; g < NG; ++g)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) x[sc][g][h] = *(const f32x4*)(xr + h * RA::PLANE + (g * 16 + sc) * 16);
+        if constexpr (!K::WREG) {
+#pragma unroll
+          for (int sc = 0; sc < 3; ++sc)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+              for (int h = 0; h < 2; ++h)
+                w[sc][nt][h] = *(const f32x4*)(Wl + ((size_t)((r * 3 + sc) * NB + nt * 16 + fr) * 32 + fg * 8 + h * 4) * 4);
+        }
+      };
+      auto mm = [&](int r, const f32x4 (&x)[3][NG][2], const f32x4 (&w)[NW][NT][2]) {
+#pragma unroll
+        for (int sc = 0; sc < 3; ++sc)
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+#pragma unroll
+            for (int g = 0; g < NG; ++g)
+#pragma unroll
+              for (int nt = 0; nt < NT; ++nt) {
+                const float wv = K::WREG ? wr[r * 3 + sc][nt][j >> 2][j & 3] : w[K::WREG ? 0 : sc][nt][j >> 2][j & 3];
+                acc[nt][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv, x[sc][g][j >> 2][j & 3], acc[nt][g], 0, 0, 0);
+              }
+      };
+      ld(0, bx[0], bw[0]);
+      ld(1, bx[1], bw[1]);
+      RING_LDS_DONE;
+      mm(0, bx[0], bw[0]);
+      RING_FENCE;
+      ld(2, bx[0], bw[0]);
+      RING_FENCE;
+      mm(1, bx[1], bw[1]);
+      RING_LDS_DONE;
+      mm(2, bx[0], bw[0]);
+    }
+#undef RING_LDS_DONE
+#undef RING_FENCE
+
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K::G) : "memory");
+    if constexpr (HEAD) {
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        float part = 0.f;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) part += fmaxf(acc[nt][g][i], 0.f) * hw2[nt][i];
+        part += __shfl_xor(part, 16);
+        part += __shfl_xor(part, 32);
+        const int xp = g * 16 + fr;
+        float x0f, x1f, x2f;
+        if (op.x_f16) {
+          const half_t* xl = (const half_t*)epi;
+          x0f = (float)xl[xp];
+          x1f = (float)xl[32 + xp];
+          x2f = (float)xl[64 + xp];
+        } else {
+          const float* xl = (const float*)epi;
+          x0f = xl[xp];
+          x1f = xl[32 + xp];
+          x2f = xl[64 + xp];
+        }
+        const float z = (x0f + x1f + x2f) / 3.f + (part + op.head_b);
+        const float il = 1.f / (1.f + expf(-z));
+        float* dst = (ovalid[g] && fg == 0) ? op.illu + prow + g * 16 + fr : (float*)(g_ring_sink + tid);
+        *dst = il;
+      }
+    } else {
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        float* dg = ovalid[g] ? (float*)op.out + prow * ocs + op.out_coff + (g * 16 + fr) * ocs + fg * 4
+                              : (float*)(g_ring_sink + tid * 16);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          f32x4 v = acc[nt][g];
+          if constexpr (K::RELU) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = fmaxf(v[i], 0.f);
+          }
+          if constexpr (RES) v += *(const f32x4*)(epi + ((g * 16 + fr) * NB + nt * 16 + fg * 4) * 4);
+          *(f32x4*)(dg + nt * 16) = v;
+        }
+      }
+    }
+    advance(cc);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 static int ring_cus() {
   static int cus = 0;
   if (!cus) {
@@ -669,6 +940,25 @@ static int ring_cus() {
       cus = 256;
   }
   return cus;
+}
+
+// row bands: minimise the makespan ceil(units / grid) * steps per unit
+static void ring_bands(RingArgs& a, const ConvOp& op, int grid) {
+  const int per_band = op.B * a.nstrips;
+  long best = -1;
+  for (int nb = 1; nb <= 16; ++nb) {
+    int rs = (cdiv(op.Ho, nb) + 3) / 4 * 4;
+    if (rs < 8) rs = 8;
+    const int nseg = cdiv(op.Ho, rs);
+    const long cost = (long)cdiv(per_band * nseg, grid) * (rs / 4 + 1);
+    if (best < 0 || cost < best) {
+      best = cost;
+      a.rs = rs;
+      a.nseg = nseg;
+    }
+  }
+  a.nunits = per_band * a.nseg;
+  a.steps = a.rs / 4 + 1;
 }
 
 template <int MODE, int C, int NB, int FL>
@@ -687,25 +977,32 @@ static int launch_ring_cfg(const ConvOp& op, hipStream_t st) {
   a.op = op;
   a.nstrips = cdiv(op.Wo, K::TW);
   const int grid = ring_cus() * occ;  // a multiple of 8 (XCD-contiguous unit order)
-  const int per_band = op.B * a.nstrips;
-  // row bands: minimise the makespan ceil(units / grid) * steps per unit
-  long best = -1;
-  for (int nb = 1; nb <= 16; ++nb) {
-    int rs = (cdiv(op.Ho, nb) + 3) / 4 * 4;
-    if (rs < 8) rs = 8;
-    const int nseg = cdiv(op.Ho, rs);
-    const long cost = (long)cdiv(per_band * nseg, grid) * (rs / 4 + 1);
-    if (best < 0 || cost < best) {
-      best = cost;
-      a.rs = rs;
-      a.nseg = nseg;
-    }
-  }
-  a.nunits = per_band * a.nseg;
-  a.steps = a.rs / 4 + 1;
+  ring_bands(a, op, grid);
   int g = std::min(grid, cdiv(a.nunits, 8) * 8);
   g = std::max(8, g / 8 * 8);
   hipLaunchKernelGGL(kern, dim3(g), dim3(K::THREADS), K::LDS, st, a);
+  return (int)hipGetLastError();
+}
+
+template <int MODE, int NB, int FL>
+static int launch_ring32_cfg(const ConvOp& op, hipStream_t st) {
+  using K = Ring32Cfg<MODE, NB, FL>;
+  auto kern = conv_ring32_kernel<MODE, NB, FL>;
+  static int occ = 0;
+  if (!occ) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, K::LDS);
+    if (e != hipSuccess) return (int)e;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)kern, 256, K::LDS);
+    if (e != hipSuccess) return (int)e;
+    if (occ < 1) occ = 1;
+  }
+  RingArgs a;
+  a.op = op;
+  a.nstrips = cdiv(op.Wo, 32);
+  ring_bands(a, op, ring_cus() * occ);
+  int g = std::min(ring_cus() * occ, cdiv(a.nunits, 8) * 8);
+  g = std::max(8, g / 8 * 8);
+  hipLaunchKernelGGL(kern, dim3(g), dim3(256), K::LDS, st, a);
   return (int)hipGetLastError();
 }
 
@@ -782,6 +1079,31 @@ int launch_conv_ring(const ConvOp& op, hipStream_t st) {
   if (s.C == 32 && op.N == 32) return res ? ring_relu<kRingConv, 32, 32, kRingRes>(op, st) : ring_relu<kRingConv, 32, 32, 0>(op, st);
   if (s.C == 32 && op.N == 64) return res ? ring_relu<kRingConv, 32, 64, kRingRes>(op, st) : ring_relu<kRingConv, 32, 64, 0>(op, st);
   if (s.C == 64 && op.N == 64) return res ? ring_relu<kRingConv, 64, 64, kRingRes>(op, st) : ring_relu<kRingConv, 64, 64, 0>(op, st);
+  return kErrUnsupported;
+}
+
+template <int MODE, int NB, int FL>
+static int ring32_relu(const ConvOp& op, hipStream_t st) {
+  return op.relu ? launch_ring32_cfg<MODE, NB, FL | kRingRelu>(op, st) : launch_ring32_cfg<MODE, NB, FL>(op, st);
+}
+
+// fp32: stride-1 3x3 over 32 channels (-> 32 / 64, head); kErrUnsupported otherwise
+int launch_conv_ring32(const ConvOp& op, hipStream_t st) {
+  if (!ring_enabled()) return kErrUnsupported;
+  if (op.Ho < 4 || op.Wo < 16 || op.nseg != 1) return kErrUnsupported;
+  if (op.res1 || op.img_bias || op.pool || op.scale || op.Kpad != 288) return kErrUnsupported;
+  const ConvSeg& s = op.seg[0];
+  if (!ring_seg_ok(s) || s.C != 32 || s.stride != 1 || s.Hin != op.Ho || s.Win != op.Wo) return kErrUnsupported;
+  if (s.cs % 4 || s.coff % 4) return kErrUnsupported;
+  if (op.store == kStoreHeadIllu) {
+    if (op.N != 32 || op.res2 || op.illu_f16 || op.Wo % 8) return kErrUnsupported;
+    return launch_ring32_cfg<kRingHead, 32, 0>(op, st);
+  }
+  if (op.store != kStoreNHWC || op.out_cs % 4 || op.out_coff % 4) return kErrUnsupported;
+  if (op.res2 && op.res2_cs % 4) return kErrUnsupported;
+  const bool res = op.res2 != nullptr;
+  if (op.N == 32) return res ? ring32_relu<kRingConv, 32, kRingRes>(op, st) : ring32_relu<kRingConv, 32, 0>(op, st);
+  if (op.N == 64) return res ? ring32_relu<kRingConv, 64, kRingRes>(op, st) : ring32_relu<kRingConv, 64, 0>(op, st);
   return kErrUnsupported;
 }
 
