@@ -1,0 +1,12 @@
+# round checkpoint: full -m gpu suite, smoke, default bench (traffic + cpu baseline), kernel stats of the default bench
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out/ck
+timeout -k 10 700 python -u -m pytest tests -m gpu -v -s --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/ck/gpu_tests.log 2>&1
+rc=$?
+echo "pytest rc=$rc"; tail -5 gpurun_out/ck/gpu_tests.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/ck/smoke.log 2>&1 || exit $?
+timeout -k 10 400 python bench.py > gpurun_out/ck/bench_default.json 2> gpurun_out/ck/bench_default.err || exit $?
+cat gpurun_out/ck/bench_default.json
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/ck/prof -o p --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-traffic --cpu-seconds 0 > gpurun_out/ck/bench_prof.json 2>&1 || exit $?
+exit $rc
