@@ -154,15 +154,28 @@ __device__ __forceinline__ void wide_epilogue(const ConvOp& op, f32x4_w (&acc)[W
   float* Es = (float*)smem;
   const int col8 = tid % CPR;
   const int nch = n0 + col8 * 8;
-  float sc[8], bi[8], psum[8];
+  // scale / bias are re-read per row (L1 hits) rather than held: with the
+  // accumulators of the later passes still live, 16 more registers spill
+  float psum[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    sc[e] = op.scale ? op.scale[nch + e] : 1.f;
-    bi[e] = op.bias ? op.bias[nch + e] : 0.f;
-    psum[e] = 0.f;
-  }
+  for (int e = 0; e < 8; ++e) psum[e] = 0.f;
   const bool one_image = (m0 / HW) == (min(m0 + WBM, M) - 1) / HW;
   const bool convt = op.store == kStoreConvT2x2;
+  // the row a thread finishes advances by exactly RPI per iteration (passes of
+  // 64 rows, 64 / RPI iterations each): (image, y, x) of that row are carried
+  // along instead of divided out per row (three integer divisions per
+  // 16-byte store made the K = 64 ConvTranspose GEMM VALU-bound)
+  int img, py, px;
+  {
+    const int mfirst = m0 + tid / CPR;
+    img = mfirst / HW;
+    const int r = mfirst - img * HW;
+    py = r / op.Wo;
+    px = r - py * op.Wo;
+  }
+  const int cout4 = op.N >> 2;
+  const int cq = convt ? nch / cout4 : 0;
+  const int cco = convt ? nch - cq * cout4 : 0;
   __syncthreads();  // every wave is done with the last stage
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
@@ -180,13 +193,27 @@ __device__ __forceinline__ void wide_epilogue(const ConvOp& op, f32x4_w (&acc)[W
     for (int it = 0; it < 64 / RPI; ++it) {
       const int row = tid / CPR + it * RPI;
       const int m = m0 + p * 64 + row;
+      if (p + it > 0) {
+        px += RPI;
+        while (px >= op.Wo) {
+          px -= op.Wo;
+          if (++py >= op.Ho) { py = 0; ++img; }
+        }
+      }
       if (m < M) {
         const f32x4_w lo = *(const f32x4_w*)(Es + row * EST + col8 * 8);
         const f32x4_w hi = *(const f32x4_w*)(Es + row * EST + col8 * 8 + 4);
         float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        const int img = m / HW;
+        if (op.scale) {
+          const f32x4_w s0 = *(const f32x4_w*)(op.scale + nch), s1 = *(const f32x4_w*)(op.scale + nch + 4);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = v[e] * sc[e] + bi[e];
+          for (int e = 0; e < 4; ++e) { v[e] *= s0[e]; v[e + 4] *= s1[e]; }
+        }
+        if (op.bias) {
+          const f32x4_w b0 = *(const f32x4_w*)(op.bias + nch), b1 = *(const f32x4_w*)(op.bias + nch + 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { v[e] += b0[e]; v[e + 4] += b1[e]; }
+        }
         if (op.img_bias) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += op.img_bias[img * op.N + nch + e];
@@ -210,12 +237,8 @@ __device__ __forceinline__ void wide_epilogue(const ConvOp& op, f32x4_w (&acc)[W
         for (int e = 0; e < 8; ++e) o[e] = (half_t)v[e];
         size_t off;
         if (convt) {
-          const int cout = op.N >> 2;
-          const int q = nch / cout, co = nch - q * cout;
-          const int pix = m - img * HW;
-          const int oy = pix / op.Wo, ox = pix - oy * op.Wo;
-          const size_t opix = ((size_t)img * 2 * op.Ho + 2 * oy + (q >> 1)) * (2 * op.Wo) + 2 * ox + (q & 1);
-          off = opix * op.out_cs + op.out_coff + co;
+          const size_t opix = ((size_t)img * 2 * op.Ho + 2 * py + (cq >> 1)) * (2 * op.Wo) + 2 * px + (cq & 1);
+          off = opix * op.out_cs + op.out_coff + cco;
         } else {
           off = (size_t)m * op.out_cs + op.out_coff + nch;
         }

@@ -150,6 +150,19 @@ __device__ __forceinline__ void q32_epilogue(const ConvOp& op, f32x4_q (&acc)[Q3
   const float* res1 = (const float*)op.res1;
   const float* res2 = (const float*)op.res2;
   float* out = (float*)op.out;
+  // (image, y, x) of the finished row, carried by RPI per iteration (no
+  // per-row integer divisions; see wide_epilogue)
+  int img, py, px;
+  {
+    const int mfirst = m0 + tid / CPR;
+    img = mfirst / HW;
+    const int r = mfirst - img * HW;
+    py = r / op.Wo;
+    px = r - py * op.Wo;
+  }
+  const int cout4 = op.N >> 2;
+  const int cq = convt ? nch / cout4 : 0;
+  const int cco = convt ? nch - cq * cout4 : 0;
   __syncthreads();  // every wave is done with the last stage
 #pragma unroll 1
   for (int p = 0; p < BM / PH; ++p) {
@@ -169,12 +182,18 @@ __device__ __forceinline__ void q32_epilogue(const ConvOp& op, f32x4_q (&acc)[Q3
     for (int it = 0; it < PH / RPI; ++it) {
       const int row = tid / CPR + it * RPI;
       const int m = m0 + p * PH + row;
+      if (p + it > 0) {
+        px += RPI;
+        while (px >= op.Wo) {
+          px -= op.Wo;
+          if (++py >= op.Ho) { py = 0; ++img; }
+        }
+      }
       if (m < M) {
         const f32x4_q lo = *(const f32x4_q*)(Es + row * EST + col8 * 8);
         const f32x4_q hi = *(const f32x4_q*)(Es + row * EST + col8 * 8 + 4);
         float v[8] = {lo[0] + bi[0], lo[1] + bi[1], lo[2] + bi[2], lo[3] + bi[3],
                       hi[0] + bi[4], hi[1] + bi[5], hi[2] + bi[6], hi[3] + bi[7]};
-        const int img = m / HW;
         if (op.img_bias) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += op.img_bias[img * op.N + nch + e];
@@ -197,12 +216,8 @@ __device__ __forceinline__ void q32_epilogue(const ConvOp& op, f32x4_q (&acc)[Q3
         }
         size_t off;
         if (convt) {
-          const int cout = op.N >> 2;
-          const int q = nch / cout, co = nch - q * cout;
-          const int pix = m - img * HW;
-          const int oy = pix / op.Wo, ox = pix - oy * op.Wo;
-          const size_t opix = ((size_t)img * 2 * op.Ho + 2 * oy + (q >> 1)) * (2 * op.Wo) + 2 * ox + (q & 1);
-          off = opix * op.out_cs + op.out_coff + co;
+          const size_t opix = ((size_t)img * 2 * op.Ho + 2 * py + (cq >> 1)) * (2 * op.Wo) + 2 * px + (cq & 1);
+          off = opix * op.out_cs + op.out_coff + cco;
         } else {
           off = (size_t)m * op.out_cs + op.out_coff + nch;
         }
