@@ -69,7 +69,9 @@ __device__ __attribute__((aligned(256))) unsigned g_ring_ninf[64] = {
 };
 
 enum RingMode : int { kRingConv = 0, kRingHead = 1, kRingFam = 2, kRingS2 = 3 };
-enum RingFlags : int { kRingRes = 1, kRingRelu = 2, kRingSc = 4 };
+// kRingOcc3: 4-wave blocks compiled for 3 waves per SIMD (<= 168 VGPRs, three
+// blocks per CU); only the configs that fit without spilling (no residual / head)
+enum RingFlags : int { kRingRes = 1, kRingRelu = 2, kRingSc = 4, kRingOcc3 = 8 };
 
 // A ring of NPL chunk planes: 4 groups of GROWS rows of RW pixels.  DEINT:
 // ring column p holds source column 2p (p < (RW+1)/2) or 2(p - (RW+1)/2) + 1.
@@ -152,6 +154,15 @@ struct RingArgs {
   int nunits, steps;      // units; steps per unit = rs / 4 + 1 (first = DMA only)
 };
 
+// chunk permutation of landing pixel l (CPP 16-byte chunks per pixel) for
+// conflict-free epilogue reads: 8-byte reads (fp16, CPP 4/8) spread 16 pixels
+// over the 256-byte bank row; 16-byte reads (fp32, CPP 8/16) over its 16 slots
+template <int CPP>
+__device__ __forceinline__ int ring_res_swz(int l) {
+  if constexpr (CPP == 16) return l & 15;
+  else return ((l * CPP) >> 4) & (CPP - 1);
+}
+
 template <int MODE, int C, int NB, int FL>
 struct RingCfg {
   static constexpr bool FAM = MODE == kRingFam, HEAD = MODE == kRingHead, S2 = MODE == kRingS2;
@@ -174,7 +185,7 @@ struct RingCfg {
   static constexpr int NWV = NG == 2 && !(C == 32 && NB == 32 && !FAM) ? 8 : 4;
   static constexpr int THREADS = NWV * 64;
   // waves per SIMD the register budget is sized for (one 8-wave block per CU)
-  static constexpr int MINW = NWV == 8 ? 2 : 1;
+  static constexpr int MINW = NWV == 8 ? 2 : (FL & kRingOcc3) ? 3 : 1;
   static constexpr int GPW = NG * 4 / NWV;         // pixel groups per wave
   static constexpr int EPX = 16 * GPW;             // output pixels per wave per step
   // per-wave LDS landing zone of the epilogue inputs of its pixels (DMA'd at
@@ -357,13 +368,17 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, RingCfg<MODE, C, NB, FL
 #pragma unroll
     for (int g = 0; g < GPW; ++g) ovalid[g] = rowok && xw + g * 16 + fr < W;
     if constexpr (RES) {
-      // EPX px x NB channels, pixel-major (the residual's own NHWC layout)
+      // EPX px x NB channels, pixel-major; the 16-byte chunks of landing pixel
+      // l are XOR-permuted by ring_res_swz(l) so the epilogue's 8-byte reads
+      // (16 pixels x 2 channel quads per 32-lane group) hit 32 distinct bank
+      // pairs (the plain layout was 4-8-way: 56% of this kernel's LDS cycles)
       constexpr int CPP = NB / 8;  // 16-byte chunks per pixel
 #pragma unroll
       for (int i = 0; i < K::E; ++i) {
-        const int q = i * 64 + lane, px = g0 * 16 + q / CPP;
+        const int q = i * 64 + lane, l = q / CPP, px = g0 * 16 + l;
         const bool ok = rowok && x0 + px < W;
-        const half_t* p = ok ? (const half_t*)op.res2 + (prow + px) * rcs + (q % CPP) * 8 : zero;
+        const half_t* p =
+            ok ? (const half_t*)op.res2 + (prow + px) * rcs + ((q % CPP) ^ ring_res_swz<CPP>(l)) * 8 : zero;
         __builtin_amdgcn_global_load_lds(p, (lds_void_ptr_r)(epi + i * 1024), 16, 0, 0);
       }
     }
@@ -621,7 +636,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, RingCfg<MODE, C, NB, FL
             if constexpr (K::RELU) v[i] = fmaxf(v[i], 0.f);
           }
           if constexpr (RES) {
-            const f16x4_r rr = *(const f16x4_r*)(epi + ((g * 16 + fr) * NB + nt * 16 + fg * 4) * 2);
+            const int k = nt * 2 + (fg >> 1);  // logical 16-byte chunk of this lane's 4 channels
+            const f16x4_r rr = *(const f16x4_r*)(epi + (g * 16 + fr) * NB * 2 + ((k ^ ring_res_swz<NB / 8>(fr)) * 16) +
+                                                 (fg & 1) * 8);
 #pragma unroll
             for (int i = 0; i < 4; ++i) v[i] += (float)rr[i];
           }
@@ -671,6 +688,15 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, RingCfg<MODE, C, NB, FL
 // conflict-free ds_read_b128 (planes 2fg, 2fg+1) per tap and feeds 8 MFMAs.
 // fp32 MFMA time (32 cycles per 16x16x4) bounds these layers, not HBM.
 // ---------------------------------------------------------------------------
+// fp32 landing zone: rows of CPP 16-byte chunks read by ds_read_b128 lane
+// groups {fr 0-3, 12-15 | fg 0} + {fr 4-11 | fg 1}: (l >> 1) & 7 for 8-chunk
+// rows (the aligned-row swizzle of the wide kernels), l & 15 for 16-chunk rows
+template <int CPP>
+__device__ __forceinline__ int ring32_res_swz(int l) {
+  if constexpr (CPP == 8) return (l >> 1) & 7;
+  else return l & 15;
+}
+
 template <int MODE, int NB, int FL>
 struct Ring32Cfg {
   static constexpr bool HEAD = MODE == kRingHead;
@@ -795,13 +821,15 @@ __global__ __launch_bounds__(256) void conv_ring32_kernel(RingArgs a) {
 #pragma unroll
     for (int g = 0; g < NG; ++g) ovalid[g] = rowok && x0 + g * 16 + fr < W;
     if constexpr (RES) {
-      // 32 px x NB fp32 channels, pixel-major
+      // 32 px x NB fp32 channels, pixel-major, chunks XOR-permuted per pixel
+      // (conflict-free 16-byte epilogue reads)
       constexpr int CPP = NB / 4;
 #pragma unroll
       for (int i = 0; i < K::E; ++i) {
         const int q = i * 64 + lane, px = q / CPP;
         const bool ok = rowok && x0 + px < W;
-        const void* p = ok ? (const void*)((const float*)op.res2 + (prow + px) * rcs + (q % CPP) * 4) : (const void*)zero;
+        const void* p = ok ? (const void*)((const float*)op.res2 + (prow + px) * rcs + ((q % CPP) ^ ring32_res_swz<CPP>(px)) * 4)
+                           : (const void*)zero;
         __builtin_amdgcn_global_load_lds(p, (lds_void_ptr_r)(epi + i * 1024), 16, 0, 0);
       }
     }
@@ -921,7 +949,8 @@ __global__ __launch_bounds__(256) void conv_ring32_kernel(RingArgs a) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) v[i] = fmaxf(v[i], 0.f);
           }
-          if constexpr (RES) v += *(const f32x4*)(epi + ((g * 16 + fr) * NB + nt * 16 + fg * 4) * 4);
+          if constexpr (RES)
+            v += *(const f32x4*)(epi + (g * 16 + fr) * NB * 4 + (((nt * 4 + fg) ^ ring32_res_swz<NB / 4>(fr)) * 16));
           *(f32x4*)(dg + nt * 16) = v;
         }
       }
@@ -1042,6 +1071,15 @@ static int ring_relu(const ConvOp& op, hipStream_t st) {
   return op.relu ? launch_ring_cfg<MODE, C, NB, FL | kRingRelu>(op, st) : launch_ring_cfg<MODE, C, NB, FL>(op, st);
 }
 
+// UPR_RING_OCC3=0 keeps the plain 32 -> 32 conv at two blocks per CU (A/B timing)
+static bool ring_occ3() {
+  static const int v = [] {
+    const char* e = getenv("UPR_RING_OCC3");
+    return (e && atoi(e) == 0) ? 0 : 1;
+  }();
+  return v == 1;
+}
+
 // fp16 only; kErrUnsupported for every op this kernel does not take
 int launch_conv_ring(const ConvOp& op, hipStream_t st) {
   if (!ring_enabled()) return kErrUnsupported;
@@ -1076,7 +1114,10 @@ int launch_conv_ring(const ConvOp& op, hipStream_t st) {
     return ring_relu<kRingConv, 64, 64, kRingSc>(op, st);
   }
   if (op.nseg != 1) return kErrUnsupported;
-  if (s.C == 32 && op.N == 32) return res ? ring_relu<kRingConv, 32, 32, kRingRes>(op, st) : ring_relu<kRingConv, 32, 32, 0>(op, st);
+  if (s.C == 32 && op.N == 32) {
+    if (res) return ring_relu<kRingConv, 32, 32, kRingRes>(op, st);
+    return ring_occ3() ? ring_relu<kRingConv, 32, 32, kRingOcc3>(op, st) : ring_relu<kRingConv, 32, 32, 0>(op, st);
+  }
   if (s.C == 32 && op.N == 64) return res ? ring_relu<kRingConv, 32, 64, kRingRes>(op, st) : ring_relu<kRingConv, 32, 64, 0>(op, st);
   if (s.C == 64 && op.N == 64) return res ? ring_relu<kRingConv, 64, 64, kRingRes>(op, st) : ring_relu<kRingConv, 64, 64, 0>(op, st);
   return kErrUnsupported;

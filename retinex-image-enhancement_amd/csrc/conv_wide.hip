@@ -450,6 +450,479 @@ __global__ __launch_bounds__(512, MINW) void conv_wide_kernel(ConvOp op) {
   wide_epilogue<BN, C::WM, C::WN, C::WAVES_M>(op, acc, smem, m0, n0, M, HW);
 }
 
+// ---------------------------------------------------------------------------
+// Halo-tiled A operand: stride-1 3x3 (dilation 1) single-segment convs whose
+// 256-pixel tile is whole image rows (W = 64: 4 rows, W = 128: 2 rows) --
+// the bottleneck ResBlock convs (64^2 x 256) and the dec3 UpBlock convs
+// (128^2 x 128), models/model.py:100-178, :261-269.
+//
+// The gathered-A kernel above DMAs every input pixel 9 times (once per tap)
+// from L2; with both operands at 32 KB per K step the L2 -> LDS gather (~70
+// GB/s per CU) and the MFMAs run at about the same rate and serialise.  Here
+// the K loop is chunk-major, tap-minor: the tile's input REGION (its TR
+// output rows plus the two halo rows, W pixels wide) of one 64-channel chunk
+// is DMA'd once, and the 9 taps read their A fragments from it at a per-tap
+// pixel offset.  A traffic per chunk: 48 KB (W 64) / 64 KB (W 128) instead of
+// 9 x 32 KB.
+// * LDS: two region buffers (chunk parity) + two B stages = 160 KiB for
+//   (BN 256, W 64) and (BN 128, W 128).  The next chunk's region is DMA'd one
+//   1-KiB piece per wave per step during the first RI taps of the current
+//   chunk; B is double-buffered per step as in the gathered kernel, and the
+//   same half-step software pipeline runs across the one barrier per step.
+// * A region pixel is a 128-byte LDS row; its logical 16-byte chunk q sits at
+//   q ^ T[p & 15].  The tap shift starts a fragment's 16 pixels at p = 16k +
+//   tx (tx in {-1, 0, 1}); T (exhaustive search over the ds_read_b128 lane
+//   groups {0-3,12-15,20-27}, ...) keeps all three shifts conflict-free, where
+//   the aligned-row swizzle (p >> 1) & 7 would be 2-way at tx = +-1.
+// * No padding columns: the one lane of an edge fragment whose tap leaves
+//   the image row is zeroed after the read (top / bottom halo rows outside
+//   the image are DMA'd from the zero line).
+// ---------------------------------------------------------------------------
+static int env_int(const char* name, int dflt);
+constexpr unsigned long long kHaloSwz = 0x7662265544022100ull;  // T[p] = 0,0,1,2,2,0,4,4,5,5,6,2,2,6,6,7
+__device__ __forceinline__ int halo_swz(int p) { return (int)(kHaloSwz >> ((p & 15) * 4)) & 7; }
+
+template <int BN, int W>
+struct HaloCfg {
+  using C = WideCfg<BN>;
+  static constexpr int TR = WBM / W;        // output rows per tile
+  static constexpr int RPX = (TR + 2) * W;  // region pixels
+  static constexpr int R_BYTES = RPX * 128;
+  static constexpr int RI = RPX / 64;       // region DMA pieces per wave per chunk
+  static constexpr int LDS = 2 * R_BYTES + 2 * C::B_BYTES;
+  // wave row offsets (wm * WM * 16) are multiples of GW modulo W: fragment a
+  // can start a row (left edge) only if a * 16 % GW == 0
+  static constexpr int GW = (C::WM * 16) % W == 0 ? W : (C::WM * 16) % W;
+  static_assert(LDS <= 163840, "LDS");
+  static_assert(RI <= 8, "a chunk's region pieces go out during taps 0..RI-1 of the previous chunk");
+  static_assert(W % 16 == 0 && WBM % W == 0, "tiles of whole rows");
+};
+
+// ABL (timing ablations, results wrong): 1 = no B DMA, 2 = no DMA at all, 3 = no MFMAs
+template <int BN, int W, int ABL = 0>
+__global__ __launch_bounds__(512, 2) void conv_hwide_kernel(ConvOp op) {
+  using C = WideCfg<BN>;
+  using HC = HaloCfg<BN, W>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave % C::WAVES_M;
+  const int wn = wave / C::WAVES_M;
+
+  const int HW = op.Ho * W;
+  const int M = op.B * HW;
+  const int mtiles = M / WBM;
+  const int ntiles = op.N / BN;
+  const int L = wide_xcd_remap(blockIdx.x, mtiles * ntiles);
+  const int ntile = L % ntiles;
+  const int mtile = L / ntiles;
+  const int m0 = mtile * WBM;
+  const int n0 = ntile * BN;
+  const int img = m0 / HW;
+  const int oy0 = (m0 - img * HW) / W;
+  const ConvSeg& sg = op.seg[0];
+  const int cs = sg.cs, Cin = sg.C, H = op.Ho;
+  const int nchunks = Cin / WBK;
+  const int total = nchunks * 9;
+  const half_t* zero = (const half_t*)g_wide_zero;
+
+  // region DMA: piece i of wave w covers region pixels (8i + w) * 8 .. +7; lane
+  // -> pixel w * 8 + lane / 8 of the 64-pixel slab, logical chunk (lane & 7) ^ T[p]
+  const int rpx = wave * 8 + (lane >> 3);
+  const half_t* rsrc =
+      (const half_t*)sg.src + sg.coff + ((size_t)img * HW + rpx) * cs + (((lane & 7) ^ halo_swz(rpx)) * 8);
+  auto region_piece = [&](int c, int i) {
+    const int r = i * 64 / W, col = i * 64 % W;
+    const int iy = oy0 - 1 + r;
+    const half_t* g = (unsigned)iy < (unsigned)H ? rsrc + ((size_t)iy * W + col) * cs + c * WBK : zero;
+    if (ABL != 2) glds16(g, smem + (c & 1) * HC::R_BYTES + (i * 8 + wave) * 1024);
+  };
+
+  const int q8 = lane >> 3;
+  const int qc = lane & 7;
+  const int sw_lane = lane >> 4;
+  const half_t* Wt = (const half_t*)op.W;
+  auto issue_b = [&](int buf, int c, int t) {
+    unsigned char* Bs = smem + 2 * HC::R_BYTES + buf * C::B_BYTES;
+    const int kb = sg.kbase + t * Cin + c * WBK;
+#pragma unroll
+    for (int j = 0; j < C::BJ; ++j) {
+      const int n = wave * (BN / 8) + j * 8 + q8;
+      const int ch = qc ^ ((4 * j + sw_lane) & 7);
+      if (ABL == 0 || ABL == 3) glds16(Wt + (size_t)(n0 + n) * op.Kpad + kb + ch * 8, Bs + (wave * (BN / 8) + j * 8) * 128);
+    }
+  };
+
+  f32x4_w acc[C::WM][C::WN];
+#pragma unroll
+  for (int a = 0; a < C::WM; ++a)
+#pragma unroll
+    for (int b = 0; b < C::WN; ++b) acc[a][b] = f32x4_w{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15;
+  const int fg = lane >> 4;
+  const int rsw = (fr >> 1) & 7;
+  const bool lane_l = fr == 0, lane_r = fr == 15;
+  // fragments of read step (c, t): B from stage bbuf, A from region c & 1 at tap (t / 3, t % 3)
+  auto rd = [&](int bbuf, int c, int ty, int tx, int kk, f16x8_w (&af)[C::WM], f16x8_w (&bf)[C::WN]) {
+    const half_t* Bs = (const half_t*)(smem + 2 * HC::R_BYTES + bbuf * C::B_BYTES);
+    const int pc = ((kk * 4 + fg) ^ rsw) * 8;
+#pragma unroll
+    for (int b = 0; b < C::WN; ++b) bf[b] = *(const f16x8_w*)(Bs + (wn * C::WN * 16 + b * 16 + fr) * 64 + pc);
+    const int p = fr + tx - 1;  // lane pixel relative to the fragment's first output pixel
+    const unsigned char* Rs = smem + (c & 1) * HC::R_BYTES + p * 128 + (((kk * 4 + fg) ^ halo_swz(p)) * 16);
+    const bool zl = tx == 0 && lane_l, zr = tx == 2 && lane_r;
+#pragma unroll
+    for (int a = 0; a < C::WM; ++a) {
+      const int m = wm * C::WM * 16 + a * 16;
+      const int oy = m / W, ox = m % W;
+      f16x8_w v = *(const f16x8_w*)(Rs + ((oy + ty) * W + ox) * 128);
+      if ((a * 16) % HC::GW == 0) {
+        if (zl && ox == 0) v = f16x8_w{};
+      }
+      if ((a * 16 + 16) % HC::GW == 0) {
+        if (zr && ox == W - 16) v = f16x8_w{};
+      }
+      af[a] = v;
+    }
+  };
+  auto mm = [&](const f16x8_w (&af)[C::WM], const f16x8_w (&bf)[C::WN]) {
+    if constexpr (ABL == 3) {
+#pragma unroll
+      for (int a = 0; a < C::WM; ++a) asm volatile("" ::"v"(af[a]));
+#pragma unroll
+      for (int b = 0; b < C::WN; ++b) asm volatile("" ::"v"(bf[b]));
+      return;
+    }
+#pragma unroll
+    for (int a = 0; a < C::WM; ++a)
+#pragma unroll
+      for (int b = 0; b < C::WN; ++b)
+        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a], bf[b], acc[a][b], 0, 0, 0);
+  };
+  auto interleave = [&]() {
+    if constexpr (ABL == 3) return;
+#pragma unroll
+    for (int a = 0; a < C::WN; ++a) {
+      __builtin_amdgcn_sched_group_barrier(0x008, C::WN, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    }
+#pragma unroll
+    for (int a = C::WN; a < C::WM; ++a) {
+      __builtin_amdgcn_sched_group_barrier(0x008, C::WN, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+  };
+
+  // step cursors: (chunk, tap row, tap column) of the read step and of the B DMA
+  int rc = 0, ry = 0, rx = 0;
+  int bc = 0, by = 0, bx = 1;
+  auto adv = [](int& c, int& y, int& x) {
+    if (++x == 3) {
+      x = 0;
+      if (++y == 3) { y = 0; ++c; }
+    }
+  };
+  f16x8_w a0[C::WM], b0[C::WN], a1[C::WM], b1[C::WN];
+#pragma unroll
+  for (int i = 0; i < HC::RI; ++i) region_piece(0, i);
+  issue_b(0, 0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  issue_b(1, bc, by * 3 + bx);
+  adv(bc, by, bx);
+  if (nchunks > 1) region_piece(1, 0);
+  rd(0, rc, ry, rx, 0, a0, b0);
+  for (int step = 0; step < total - 1; ++step) {
+    rd(step & 1, rc, ry, rx, 1, a1, b1);
+    mm(a0, b0);
+    interleave();
+    // RAW: own DMA (B of step + 1, region pieces) retired before the barrier;
+    // WAR: own reads of B stage step & 1 (and of region (c - 1) & 1) retired
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    adv(rc, ry, rx);  // read cursor -> step + 1
+    if (step + 2 < total) {
+      issue_b(step & 1, bc, by * 3 + bx);
+      adv(bc, by, bx);
+    }
+    const int t = ry * 3 + rx;
+    if (t < HC::RI && rc + 1 < nchunks) region_piece(rc + 1, t);
+    rd((step + 1) & 1, rc, ry, rx, 0, a0, b0);
+    mm(a1, b1);
+    interleave();
+  }
+  rd((total - 1) & 1, rc, ry, rx, 1, a1, b1);
+  mm(a0, b0);
+  mm(a1, b1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave is done with the regions and stages before the epilogue reuses LDS
+
+  wide_epilogue<BN, C::WM, C::WN, C::WAVES_M>(op, acc, smem, m0, n0, M, HW);
+}
+
+template <int BN, int W, int ABL>
+static int launch_hwide_abl(const ConvOp& op, hipStream_t st) {
+  using HC = HaloCfg<BN, W>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    const hipError_t e = hipFuncSetAttribute((const void*)conv_hwide_kernel<BN, W, ABL>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, HC::LDS);
+    if (e != hipSuccess) return (int)e;
+    attr_set = true;
+  }
+  const int grid = (op.B * op.Ho * W / WBM) * (op.N / BN);
+  hipLaunchKernelGGL((conv_hwide_kernel<BN, W, ABL>), dim3(grid), dim3(512), HC::LDS, st, op);
+  return (int)hipGetLastError();
+}
+
+// UPR_HALO_ABL=1/2/3: timing ablations (wrong results; convbench only)
+template <int BN, int W>
+static int launch_hwide(const ConvOp& op, hipStream_t st) {
+  static const int abl = env_int("UPR_HALO_ABL", 0);
+  if (abl == 1) return launch_hwide_abl<BN, W, 1>(op, st);
+  if (abl == 2) return launch_hwide_abl<BN, W, 2>(op, st);
+  if (abl == 3) return launch_hwide_abl<BN, W, 3>(op, st);
+  return launch_hwide_abl<BN, W, 0>(op, st);
+}
+
+// ---------------------------------------------------------------------------
+// Halo A with a region ROW RING and three B stages (BN 256, W 64: the 64^2 x
+// 256-channel bottleneck convs).  The two-stage form above waits for each
+// step's B DMA within one step (vmcnt(0) before every barrier); measured on
+// bneck, its B DMA alone costs 10% (no-B-DMA ablation 0.170 -> 0.153 ms) and
+// all DMA 27% (-> 0.124).  Here:
+// * Region rows live in an 8-row ring (64 KB) instead of two 6-row buffers
+//   (96 KB): chunk c's region row r is ring row (6c + r) & 7, so the next
+//   chunk's rows 0-3 reuse the two spare rows and chunk c's rows 0 / 1 once
+//   taps 0-2 / 3-5 are done, and its rows 4 / 5 overwrite chunk c's rows 2 /
+//   3 at the start of the next chunk (needed from taps 3 / 6 on).
+// * The freed 32 KB hold a third B stage: B(s + 3) goes out after barrier s,
+//   and the wait before barrier s leaves the previous iteration's DMAs in
+//   flight (counted vmcnt, never 0 in the loop): two steps of lookahead for
+//   every operand.
+// * Edge masks (tap column outside the image row) are applied to the A
+//   fragments right before their MFMAs, not at the read (a select on freshly
+//   read registers stalls the wave on the LDS read).
+// ---------------------------------------------------------------------------
+template <int BN>
+struct Halo3Cfg {
+  using C = WideCfg<BN>;
+  static constexpr int W = 64;
+  static constexpr int ROW = W * 128;        // one region row of one 64-channel chunk
+  static constexpr int RING = 8 * ROW;       // 8-row ring
+  static constexpr int LDS = RING + 3 * C::B_BYTES;
+  static_assert(LDS <= 163840, "LDS");
+};
+
+template <int BN>
+__global__ __launch_bounds__(512, 2) void conv_hwide3_kernel(ConvOp op) {
+  using C = WideCfg<BN>;
+  using HC = Halo3Cfg<BN>;
+  constexpr int W = HC::W;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave % C::WAVES_M;
+  const int wn = wave / C::WAVES_M;
+
+  const int HW = op.Ho * W;
+  const int M = op.B * HW;
+  const int mtiles = M / WBM;
+  const int ntiles = op.N / BN;
+  const int L = wide_xcd_remap(blockIdx.x, mtiles * ntiles);
+  const int ntile = L % ntiles;
+  const int mtile = L / ntiles;
+  const int m0 = mtile * WBM;
+  const int n0 = ntile * BN;
+  const int img = m0 / HW;
+  const int oy0 = (m0 - img * HW) / W;
+  const ConvSeg& sg = op.seg[0];
+  const int cs = sg.cs, Cin = sg.C, H = op.Ho;
+  const int nchunks = Cin / WBK;
+  const int total = nchunks * 9;
+  const half_t* zero = (const half_t*)g_wide_zero;
+
+  // region row r of chunk cc: one 1-KiB piece per wave (pixels wave*8 .. +7)
+  const int rpx = wave * 8 + (lane >> 3);
+  const half_t* rsrc =
+      (const half_t*)sg.src + sg.coff + ((size_t)img * HW + rpx) * cs + (((lane & 7) ^ halo_swz(rpx)) * 8);
+  auto region_row = [&](int cc, int r) {
+    const int iy = oy0 - 1 + r;
+    const half_t* g = (unsigned)iy < (unsigned)H ? rsrc + (size_t)iy * W * cs + cc * WBK : zero;
+    glds16(g, smem + ((6 * cc + r) & 7) * HC::ROW + wave * 1024);
+  };
+  // pieces issued before the reads of step (c, t): this chunk's rows 4 / 5 at
+  // t 0 / 1, the next chunk's rows 0, 2, 1, 3 at t 2, 3, 4, 6
+  auto pieces = [&](int c, int t) -> int {
+    if (t < 2) return 1;
+    return (t <= 4 || t == 6) && c + 1 < nchunks ? 1 : 0;
+  };
+  auto issue_pieces = [&](int c, int t) {
+    if (t < 2) region_row(c, 4 + t);
+    else if (c + 1 < nchunks) {
+      if (t == 2) region_row(c + 1, 0);
+      else if (t == 3) region_row(c + 1, 2);
+      else if (t == 4) region_row(c + 1, 1);
+      else if (t == 6) region_row(c + 1, 3);
+    }
+  };
+
+  const int q8 = lane >> 3;
+  const int qc = lane & 7;
+  const int sw_lane = lane >> 4;
+  const half_t* Wt = (const half_t*)op.W;
+  // B of step (c, t) into stage `st`; steps past the end re-read the last
+  // step's rows into a stage nobody reads again (keeps the DMA count uniform)
+  auto issue_b = [&](int stg, int c, int t) {
+    unsigned char* Bs = smem + HC::RING + stg * C::B_BYTES;
+    const int kb = sg.kbase + t * Cin + c * WBK;
+#pragma unroll
+    for (int j = 0; j < C::BJ; ++j) {
+      const int n = wave * (BN / 8) + j * 8 + q8;
+      const int ch = qc ^ ((4 * j + sw_lane) & 7);
+      glds16(Wt + (size_t)(n0 + n) * op.Kpad + kb + ch * 8, Bs + (wave * (BN / 8) + j * 8) * 128);
+    }
+  };
+
+  f32x4_w acc[C::WM][C::WN];
+#pragma unroll
+  for (int a = 0; a < C::WM; ++a)
+#pragma unroll
+    for (int b = 0; b < C::WN; ++b) acc[a][b] = f32x4_w{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15;
+  const int fg = lane >> 4;
+  const int rsw = (fr >> 1) & 7;
+  const bool lane_l = fr == 0, lane_r = fr == 15;
+  // fragments of step (c, ty, tx), half kk; B from stage stg
+  auto rd = [&](int stg, int c, int ty, int tx, int kk, f16x8_w (&af)[C::WM], f16x8_w (&bf)[C::WN]) {
+    const half_t* Bs = (const half_t*)(smem + HC::RING + stg * C::B_BYTES);
+    const int pc = ((kk * 4 + fg) ^ rsw) * 8;
+#pragma unroll
+    for (int b = 0; b < C::WN; ++b) bf[b] = *(const f16x8_w*)(Bs + (wn * C::WN * 16 + b * 16 + fr) * 64 + pc);
+    const int p = fr + tx - 1;
+    const int lofs = p * 128 + (((kk * 4 + fg) ^ halo_swz(p)) * 16);
+    const int rbase = 6 * c + ty + 2 * wm;  // ring row of the wave's first output row, before & 7
+#pragma unroll
+    for (int a = 0; a < C::WM; ++a) {
+      const int rr = (rbase + a / 4) & 7;
+      af[a] = *(const f16x8_w*)(smem + rr * HC::ROW + (a % 4) * 16 * 128 + lofs);
+    }
+  };
+  // MFMAs of one half; edge lanes of the first / last 16-pixel group of a row
+  // are zeroed when the tap column leaves the image
+  auto mm = [&](f16x8_w (&af)[C::WM], const f16x8_w (&bf)[C::WN], int tx) {
+    const bool zl = tx == 0 && lane_l, zr = tx == 2 && lane_r;
+#pragma unroll
+    for (int a = 0; a < C::WM; ++a) {
+      if (a % 4 == 0 && zl) af[a] = f16x8_w{};
+      if (a % 4 == 3 && zr) af[a] = f16x8_w{};
+#pragma unroll
+      for (int b = 0; b < C::WN; ++b)
+        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a], bf[b], acc[a][b], 0, 0, 0);
+    }
+  };
+  auto interleave = [&]() {
+#pragma unroll
+    for (int a = 0; a < C::WN; ++a) {
+      __builtin_amdgcn_sched_group_barrier(0x008, C::WN, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    }
+#pragma unroll
+    for (int a = C::WN; a < C::WM; ++a) {
+      __builtin_amdgcn_sched_group_barrier(0x008, C::WN, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+  };
+  auto adv = [](int& c, int& y, int& x) {
+    if (++x == 3) {
+      x = 0;
+      if (++y == 3) { y = 0; ++c; }
+    }
+  };
+  // cursors: read step (rc, ry, rx) in B stage rs; B DMA step (bc, by, bx) into stage bs
+  int rc = 0, ry = 0, rx = 0, rs = 0;
+  int bc = 0, by = 0, bx = 2, bs = 2;
+  const int lc = nchunks - 1;  // clamp for B past the end
+  f16x8_w a0[C::WM], b0[C::WN], a1[C::WM], b1[C::WN];
+  region_row(0, 0);
+  region_row(0, 1);
+  region_row(0, 2);
+  region_row(0, 3);
+  issue_b(0, 0, 0);
+  issue_b(1, 0, 1);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::BJ) : "memory");  // rows 0-3 and B(0) landed
+  __builtin_amdgcn_s_barrier();
+  issue_b(2, 0, 2);  // B(2)
+  adv(bc, by, bx);   // -> step 3
+  bs = 0;
+  issue_pieces(0, 0);
+  rd(0, 0, 0, 0, 0, a0, b0);
+  int tx0 = 0;
+  for (int step = 0; step < total - 1; ++step) {
+    rd(rs, rc, ry, rx, 1, a1, b1);
+    const int tx1 = rx;
+    mm(a0, b0, tx0);
+    interleave();
+    // RAW: every DMA older than the previous iteration's (B(step + 2) and the
+    // pieces issued before step's reads) has landed -> B(step + 1) and the
+    // region rows step + 1 reads.  WAR: own fragment reads of step retired.
+    if (pieces(rc, ry * 3 + rx)) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(C::BJ + 1) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(C::BJ) : "memory");
+    __builtin_amdgcn_s_barrier();
+    adv(rc, ry, rx);  // -> step + 1
+    rs = rs == 2 ? 0 : rs + 1;
+    issue_b(bs, bc > lc ? lc : bc, bc > lc ? 8 : by * 3 + bx);  // B(step + 3) into the stage step read
+    adv(bc, by, bx);
+    bs = bs == 2 ? 0 : bs + 1;
+    issue_pieces(rc, ry * 3 + rx);
+    rd(rs, rc, ry, rx, 0, a0, b0);
+    tx0 = rx;
+    mm(a1, b1, tx1);
+    interleave();
+  }
+  rd(rs, rc, ry, rx, 1, a1, b1);
+  mm(a0, b0, tx0);
+  mm(a1, b1, rx);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave is done with the ring and stages before the epilogue reuses LDS
+
+  wide_epilogue<BN, C::WM, C::WN, C::WAVES_M>(op, acc, smem, m0, n0, M, HW);
+}
+
+template <int BN>
+static int launch_hwide3(const ConvOp& op, hipStream_t st) {
+  using HC = Halo3Cfg<BN>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    const hipError_t e =
+        hipFuncSetAttribute((const void*)conv_hwide3_kernel<BN>, hipFuncAttributeMaxDynamicSharedMemorySize, HC::LDS);
+    if (e != hipSuccess) return (int)e;
+    attr_set = true;
+  }
+  const int grid = (op.B * op.Ho * HC::W / WBM) * (op.N / BN);
+  hipLaunchKernelGGL((conv_hwide3_kernel<BN>), dim3(grid), dim3(512), HC::LDS, st, op);
+  return (int)hipGetLastError();
+}
+
+// UPR_WIDE_HALO=0 routes these convs to the gathered-A kernel, =1 to the
+// two-stage halo kernel (A/B timing); default: the ring / three-stage form
+// for W 64 x N 256, two-stage halo for W 64 x N 128, gathered for W 128
+static int halo_route(const ConvOp& op, hipStream_t st) {
+  static const int mode = env_int("UPR_WIDE_HALO", 2);
+  if (!mode || op.nseg != 1 || op.store != kStoreNHWC) return kErrUnsupported;
+  const ConvSeg& s = op.seg[0];
+  if (s.kh != 3 || s.kw != 3 || s.stride != 1 || s.pad != 1 || s.dil != 1 || s.pre != kPreNone) return kErrUnsupported;
+  if (s.Hin != op.Ho || s.Win != op.Wo || s.C % WBK || (op.Ho * op.Wo) % WBM) return kErrUnsupported;
+  if (op.Wo == 64 && op.N % 256 == 0) return mode == 1 ? launch_hwide<256, 64>(op, st) : launch_hwide3<256>(op, st);
+  if (op.Wo == 64) return launch_hwide<128, 64>(op, st);
+  if (op.Wo == 128 && mode == 1) return launch_hwide<128, 128>(op, st);
+  return kErrUnsupported;
+}
+
 
 template <int BN, bool PIPE>
 static int launch_wide_bn(const ConvOp& op, hipStream_t st) {
@@ -543,6 +1016,10 @@ int launch_conv_wide(const ConvOp& op, hipStream_t st) {
     const ConvSeg& sg = op.seg[s];
     if (sg.pre != kPreNone || sg.C % WBK || sg.cs % 8 || sg.coff % 8 || sg.kbase % 8) return kErrUnsupported;
     if ((uintptr_t)sg.src % 16) return kErrUnsupported;
+  }
+  {
+    const int rc = halo_route(op, st);
+    if (rc != kErrUnsupported) return rc;
   }
   if (op.N % 256 == 0) return launch_wide_any<256>(op, st);
   // 128-channel stride-1 3x3 convs (dec3) used to stay on the halo kernel;

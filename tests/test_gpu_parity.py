@@ -68,9 +68,16 @@ CONV_CASES = [
     (1, 37, 70, 64, 64, 3, 1, 1, 1, False, True),
     (2, 66, 96, 32, 64, 3, 1, 1, 1, True, False),
     (4, 130, 40, 32, 32, 3, 1, 1, 1, True, False),
+    (2, 24, 50, 32, 64, 3, 1, 1, 1, False, True),
     # row-ring stride-2 (enc1.conv1 shape class): de-interleaved ring rows, partial strips
     (2, 36, 70, 32, 64, 3, 2, 1, 1, True, False),
     (1, 64, 128, 32, 64, 3, 2, 1, 1, False, False),
+    # halo-tiled A operand of the wide kernel (fp16; 3x3 s1 d1, W 64 / 128, tiles of whole rows):
+    # BN 256 x W 64 over 4 chunks (region double buffer), BN 128 x W 64, BN 128 x W 128, one chunk
+    (2, 64, 64, 256, 256, 3, 1, 1, 1, True, True),
+    (1, 32, 64, 128, 128, 3, 1, 1, 1, False, True),
+    (2, 16, 128, 128, 128, 3, 1, 1, 1, True, False),
+    (1, 8, 64, 64, 256, 3, 1, 1, 1, False, False),
 ]
 
 
