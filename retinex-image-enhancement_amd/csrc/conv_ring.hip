@@ -71,7 +71,9 @@ __device__ __attribute__((aligned(256))) unsigned g_ring_ninf[64] = {
 enum RingMode : int { kRingConv = 0, kRingHead = 1, kRingFam = 2, kRingS2 = 3 };
 // kRingOcc3: 4-wave blocks compiled for 3 waves per SIMD (<= 168 VGPRs, three
 // blocks per CU); only the configs that fit without spilling (no residual / head)
-enum RingFlags : int { kRingRes = 1, kRingRelu = 2, kRingSc = 4, kRingOcc3 = 8 };
+// kRingWide: 64-pixel strips (4 pixel groups per wave row): twice the MFMAs per
+// step for the same per-step barrier / DMA / cursor work (32 -> 32 convs)
+enum RingFlags : int { kRingRes = 1, kRingRelu = 2, kRingSc = 4, kRingOcc3 = 8, kRingWide = 16 };
 
 // A ring of NPL chunk planes: 4 groups of GROWS rows of RW pixels.  DEINT:
 // ring column p holds source column 2p (p < (RW+1)/2) or 2(p - (RW+1)/2) + 1.
@@ -168,7 +170,7 @@ struct RingCfg {
   static constexpr bool FAM = MODE == kRingFam, HEAD = MODE == kRingHead, S2 = MODE == kRingS2;
   static constexpr bool RES = FL & kRingRes, RELU = FAM || (FL & kRingRelu), SC = FL & kRingSc;
   static constexpr int HA = FAM ? 2 : 1;           // main ring halo (stride 1)
-  static constexpr int TW = S2 ? 16 : 32;          // strip width (output pixels)
+  static constexpr int TW = S2 ? 16 : (FL & kRingWide) ? 64 : 32;  // strip width (output pixels)
   static constexpr int NG = TW / 16;               // 16-pixel groups per output row
   using RA = Ring<FAM ? 8 : C / 8, S2 ? 2 * TW + 1 : TW + 2 * HA, S2 ? 8 : 4, S2>;
   using RB = Ring<4, TW + 2, 4>;                   // FAM: x (32 channels, -inf outside)
@@ -185,7 +187,7 @@ struct RingCfg {
   static constexpr int NWV = NG == 2 && !(C == 32 && NB == 32 && !FAM) ? 8 : 4;
   static constexpr int THREADS = NWV * 64;
   // waves per SIMD the register budget is sized for (one 8-wave block per CU)
-  static constexpr int MINW = NWV == 8 ? 2 : (FL & kRingOcc3) ? 3 : 1;
+  static constexpr int MINW = NWV == 8 || (FL & kRingWide) ? 2 : (FL & kRingOcc3) ? 3 : 1;
   static constexpr int GPW = NG * 4 / NWV;         // pixel groups per wave
   static constexpr int EPX = 16 * GPW;             // output pixels per wave per step
   // per-wave LDS landing zone of the epilogue inputs of its pixels (DMA'd at
@@ -1071,6 +1073,15 @@ static int ring_relu(const ConvOp& op, hipStream_t st) {
   return op.relu ? launch_ring_cfg<MODE, C, NB, FL | kRingRelu>(op, st) : launch_ring_cfg<MODE, C, NB, FL>(op, st);
 }
 
+// UPR_RING_WIDE=0 keeps the 32 -> 32 convs (and the head) on 32-pixel strips (A/B timing)
+static bool ring_wide() {
+  static const int v = [] {
+    const char* e = getenv("UPR_RING_WIDE");
+    return (e && atoi(e) == 0) ? 0 : 1;
+  }();
+  return v == 1;
+}
+
 // UPR_RING_OCC3=0 keeps the plain 32 -> 32 conv at two blocks per CU (A/B timing)
 static bool ring_occ3() {
   static const int v = [] {
@@ -1091,7 +1102,7 @@ int launch_conv_ring(const ConvOp& op, hipStream_t st) {
   if (op.store == kStoreHeadIllu) {
     if (op.nseg != 1 || s.stride != 1 || s.Hin != op.Ho || s.Win != op.Wo) return kErrUnsupported;
     if (op.N != 32 || s.C != 32 || op.res2 || op.illu_f16 || op.Wo % 8) return kErrUnsupported;
-    return launch_ring_cfg<kRingHead, 32, 32, 0>(op, st);
+    return ring_wide() ? launch_ring_cfg<kRingHead, 32, 32, kRingWide>(op, st) : launch_ring_cfg<kRingHead, 32, 32, 0>(op, st);
   }
   if (op.store != kStoreNHWC || op.out_cs % 4 || op.out_coff % 4) return kErrUnsupported;
   if (op.res2 && op.res2_cs % 4) return kErrUnsupported;
@@ -1115,7 +1126,10 @@ int launch_conv_ring(const ConvOp& op, hipStream_t st) {
   }
   if (op.nseg != 1) return kErrUnsupported;
   if (s.C == 32 && op.N == 32) {
+    // 64-pixel strips for the plain conv only: with the residual landing zone
+    // (4 KB per wave) they measured slower (dec1.conv.3 0.301 -> 0.308 ms)
     if (res) return ring_relu<kRingConv, 32, 32, kRingRes>(op, st);
+    if (ring_wide() && op.Wo >= 48) return ring_relu<kRingConv, 32, 32, kRingWide>(op, st);
     return ring_occ3() ? ring_relu<kRingConv, 32, 32, kRingOcc3>(op, st) : ring_relu<kRingConv, 32, 32, 0>(op, st);
   }
   if (s.C == 32 && op.N == 64) return res ? ring_relu<kRingConv, 32, 64, kRingRes>(op, st) : ring_relu<kRingConv, 32, 64, 0>(op, st);
