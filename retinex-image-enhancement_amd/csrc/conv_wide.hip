@@ -128,7 +128,11 @@ struct SegCursor {
 
 // Epilogue shared by the wide kernels: 256 x BN accumulator tile -> LDS ->
 // scale / bias / per-image bias / residuals / ReLU -> 16-byte fp16 stores.
-template <int BN, int WM, int WN, int WAVES_M>
+// RPF: the tile's residual rows (res1, else res2) are loaded into registers
+// before the accumulators are parked -- one batch of independent loads
+// instead of one exposed HBM round trip per 16-byte store (a residual cost
+// the bottleneck / dec3 convs 10-25% of their time)
+template <int BN, int WM, int WN, int WAVES_M, int BM = WBM, bool RPF = false>
 __device__ __forceinline__ void wide_epilogue(const ConvOp& op, f32x4_w (&acc)[WM][WN], unsigned char* smem, int m0,
                                               int n0, int M, int HW) {
   const int tid = threadIdx.x;
@@ -139,7 +143,7 @@ __device__ __forceinline__ void wide_epilogue(const ConvOp& op, f32x4_w (&acc)[W
   const int fr = lane & 15;
   const int fg = lane >> 4;
   // ---- epilogue through LDS ---------------------------------------------------
-  // Four passes of 64 tile rows: the waves owning those rows park their raw
+  // BM / 64 passes of 64 tile rows: the waves owning those rows park their raw
   // fp32 accumulators in LDS ([64][BN + 4] floats: conflict-free 4-byte
   // writes), then every thread finishes 8 consecutive channels of one pixel
   // per iteration (scale / bias / per-image bias / residuals / ReLU, 16-byte
@@ -159,7 +163,7 @@ __device__ __forceinline__ void wide_epilogue(const ConvOp& op, f32x4_w (&acc)[W
   float psum[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) psum[e] = 0.f;
-  const bool one_image = (m0 / HW) == (min(m0 + WBM, M) - 1) / HW;
+  const bool one_image = (m0 / HW) == (min(m0 + BM, M) - 1) / HW;
   const bool convt = op.store == kStoreConvT2x2;
   // the row a thread finishes advances by exactly RPI per iteration (passes of
   // 64 rows, 64 / RPI iterations each): (image, y, x) of that row are carried
@@ -176,9 +180,20 @@ __device__ __forceinline__ void wide_epilogue(const ConvOp& op, f32x4_w (&acc)[W
   const int cout4 = op.N >> 2;
   const int cq = convt ? nch / cout4 : 0;
   const int cco = convt ? nch - cq * cout4 : 0;
+  constexpr int NQ = RPF ? BM / RPI : 1;  // rows this thread finishes (q = p * 64 / RPI + it)
+  const half_t* rpf = (const half_t*)(op.res1 ? op.res1 : op.res2);
+  const int rpf_cs = op.res1 ? op.res1_cs : op.res2_cs;
+  f16x8_w rv[NQ];
+  if (RPF && rpf) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int m = m0 + tid / CPR + q * RPI;
+      rv[q] = m < M ? *(const f16x8_w*)(rpf + (size_t)m * rpf_cs + nch) : f16x8_w{};
+    }
+  }
   __syncthreads();  // every wave is done with the last stage
 #pragma unroll
-  for (int p = 0; p < 4; ++p) {
+  for (int p = 0; p < BM / 64; ++p) {
     if (wm == p / PPW) {
 #pragma unroll
       for (int a = 0; a < APP; ++a)
@@ -218,8 +233,9 @@ __device__ __forceinline__ void wide_epilogue(const ConvOp& op, f32x4_w (&acc)[W
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += op.img_bias[img * op.N + nch + e];
         }
+        const int q = RPF ? p * (64 / RPI) + it : 0;
         if (op.res1) {
-          const f16x8_w r = *(const f16x8_w*)((const half_t*)op.res1 + (size_t)m * op.res1_cs + nch);
+          const f16x8_w r = RPF ? rv[q] : *(const f16x8_w*)((const half_t*)op.res1 + (size_t)m * op.res1_cs + nch);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += (float)r[e];
         }
@@ -228,7 +244,7 @@ __device__ __forceinline__ void wide_epilogue(const ConvOp& op, f32x4_w (&acc)[W
           for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
         }
         if (op.res2) {
-          const f16x8_w r = *(const f16x8_w*)((const half_t*)op.res2 + (size_t)m * op.res2_cs + nch);
+          const f16x8_w r = RPF && !op.res1 ? rv[q] : *(const f16x8_w*)((const half_t*)op.res2 + (size_t)m * op.res2_cs + nch);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += (float)r[e];
         }
@@ -447,7 +463,7 @@ __global__ __launch_bounds__(512, MINW) void conv_wide_kernel(ConvOp op) {
     __syncthreads();  // every wave is done with both stages before the epilogue reuses LDS
   }
 
-  wide_epilogue<BN, C::WM, C::WN, C::WAVES_M>(op, acc, smem, m0, n0, M, HW);
+  wide_epilogue<BN, C::WM, C::WN, C::WAVES_M, WBM, !ONE>(op, acc, smem, m0, n0, M, HW);
 }
 
 // ---------------------------------------------------------------------------
@@ -706,36 +722,43 @@ static int launch_hwide(const ConvOp& op, hipStream_t st) {
 //   fragments right before their MFMAs, not at the read (a select on freshly
 //   read registers stalls the wave on the LDS read).
 // ---------------------------------------------------------------------------
-template <int BN>
+template <int BN, int W>
 struct Halo3Cfg {
-  using C = WideCfg<BN>;
-  static constexpr int W = 64;
+  static constexpr int TR = 4;               // output rows per tile
+  static constexpr int BM = TR * W;          // 256 (W 64) / 512 (W 128) pixels
+  static constexpr int WAVES_M = BM / 128;   // each wave: 128 pixels x 64 channels
+  static constexpr int WAVES_N = 8 / WAVES_M;
+  static constexpr int WM = 8, WN = BN / WAVES_N / 16;
   static constexpr int ROW = W * 128;        // one region row of one 64-channel chunk
+  static constexpr int RP = W / 64;          // DMA pieces per wave per region row
   static constexpr int RING = 8 * ROW;       // 8-row ring
-  static constexpr int LDS = RING + 3 * C::B_BYTES;
+  static constexpr int B_BYTES = BN * WBK * 2;
+  static constexpr int BJ = BN / 64;         // B DMA instructions per wave per step
+  static constexpr int NBS = RING + 3 * B_BYTES <= 163840 ? 3 : 2;  // B stages
+  static constexpr int LDS = RING + NBS * B_BYTES;
+  static_assert(WN == 4 && WAVES_M * WAVES_N == 8, "wave tile 128 x 64");
   static_assert(LDS <= 163840, "LDS");
 };
 
-template <int BN>
+template <int BN, int W>
 __global__ __launch_bounds__(512, 2) void conv_hwide3_kernel(ConvOp op) {
-  using C = WideCfg<BN>;
-  using HC = Halo3Cfg<BN>;
-  constexpr int W = HC::W;
+  using HC = Halo3Cfg<BN, W>;
+  constexpr int WM = HC::WM, WN = HC::WN, BM = HC::BM;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wm = wave % C::WAVES_M;
-  const int wn = wave / C::WAVES_M;
+  const int wm = wave % HC::WAVES_M;
+  const int wn = wave / HC::WAVES_M;
 
   const int HW = op.Ho * W;
   const int M = op.B * HW;
-  const int mtiles = M / WBM;
+  const int mtiles = M / BM;
   const int ntiles = op.N / BN;
   const int L = wide_xcd_remap(blockIdx.x, mtiles * ntiles);
   const int ntile = L % ntiles;
   const int mtile = L / ntiles;
-  const int m0 = mtile * WBM;
+  const int m0 = mtile * BM;
   const int n0 = ntile * BN;
   const int img = m0 / HW;
   const int oy0 = (m0 - img * HW) / W;
@@ -745,22 +768,25 @@ __global__ __launch_bounds__(512, 2) void conv_hwide3_kernel(ConvOp op) {
   const int total = nchunks * 9;
   const half_t* zero = (const half_t*)g_wide_zero;
 
-  // region row r of chunk cc: one 1-KiB piece per wave (pixels wave*8 .. +7)
+  // region row r of chunk cc: RP 1-KiB pieces per wave (pixels (wave + 8k) * 8 .. +7)
   const int rpx = wave * 8 + (lane >> 3);
   const half_t* rsrc =
       (const half_t*)sg.src + sg.coff + ((size_t)img * HW + rpx) * cs + (((lane & 7) ^ halo_swz(rpx)) * 8);
   auto region_row = [&](int cc, int r) {
     const int iy = oy0 - 1 + r;
-    const half_t* g = (unsigned)iy < (unsigned)H ? rsrc + (size_t)iy * W * cs + cc * WBK : zero;
-    glds16(g, smem + ((6 * cc + r) & 7) * HC::ROW + wave * 1024);
+    const bool in = (unsigned)iy < (unsigned)H;
+    unsigned char* dst = smem + ((6 * cc + r) & 7) * HC::ROW + wave * 1024;
+#pragma unroll
+    for (int k = 0; k < HC::RP; ++k)
+      glds16(in ? rsrc + ((size_t)iy * W + 64 * k) * cs + cc * WBK : zero, dst + k * 8192);
   };
-  // pieces issued before the reads of step (c, t): this chunk's rows 4 / 5 at
+  // rows issued before the reads of step (c, t): this chunk's rows 4 / 5 at
   // t 0 / 1, the next chunk's rows 0, 2, 1, 3 at t 2, 3, 4, 6
-  auto pieces = [&](int c, int t) -> int {
+  auto rows_at = [&](int c, int t) -> int {
     if (t < 2) return 1;
     return (t <= 4 || t == 6) && c + 1 < nchunks ? 1 : 0;
   };
-  auto issue_pieces = [&](int c, int t) {
+  auto issue_rows = [&](int c, int t) {
     if (t < 2) region_row(c, 4 + t);
     else if (c + 1 < nchunks) {
       if (t == 2) region_row(c + 1, 0);
@@ -774,66 +800,67 @@ __global__ __launch_bounds__(512, 2) void conv_hwide3_kernel(ConvOp op) {
   const int qc = lane & 7;
   const int sw_lane = lane >> 4;
   const half_t* Wt = (const half_t*)op.W;
-  // B of step (c, t) into stage `st`; steps past the end re-read the last
+  // B of step (c, t) into stage stg; steps past the end re-read the last
   // step's rows into a stage nobody reads again (keeps the DMA count uniform)
   auto issue_b = [&](int stg, int c, int t) {
-    unsigned char* Bs = smem + HC::RING + stg * C::B_BYTES;
+    unsigned char* Bs = smem + HC::RING + stg * HC::B_BYTES;
     const int kb = sg.kbase + t * Cin + c * WBK;
 #pragma unroll
-    for (int j = 0; j < C::BJ; ++j) {
+    for (int j = 0; j < HC::BJ; ++j) {
       const int n = wave * (BN / 8) + j * 8 + q8;
       const int ch = qc ^ ((4 * j + sw_lane) & 7);
       glds16(Wt + (size_t)(n0 + n) * op.Kpad + kb + ch * 8, Bs + (wave * (BN / 8) + j * 8) * 128);
     }
   };
 
-  f32x4_w acc[C::WM][C::WN];
+  f32x4_w acc[WM][WN];
 #pragma unroll
-  for (int a = 0; a < C::WM; ++a)
+  for (int a = 0; a < WM; ++a)
 #pragma unroll
-    for (int b = 0; b < C::WN; ++b) acc[a][b] = f32x4_w{0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < WN; ++b) acc[a][b] = f32x4_w{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15;
   const int fg = lane >> 4;
   const int rsw = (fr >> 1) & 7;
   const bool lane_l = fr == 0, lane_r = fr == 15;
+  const int wrow = wm * 128 / W;  // the wave's first output row in the tile
   // fragments of step (c, ty, tx), half kk; B from stage stg
-  auto rd = [&](int stg, int c, int ty, int tx, int kk, f16x8_w (&af)[C::WM], f16x8_w (&bf)[C::WN]) {
-    const half_t* Bs = (const half_t*)(smem + HC::RING + stg * C::B_BYTES);
+  auto rd = [&](int stg, int c, int ty, int tx, int kk, f16x8_w (&af)[WM], f16x8_w (&bf)[WN]) {
+    const half_t* Bs = (const half_t*)(smem + HC::RING + stg * HC::B_BYTES);
     const int pc = ((kk * 4 + fg) ^ rsw) * 8;
 #pragma unroll
-    for (int b = 0; b < C::WN; ++b) bf[b] = *(const f16x8_w*)(Bs + (wn * C::WN * 16 + b * 16 + fr) * 64 + pc);
+    for (int b = 0; b < WN; ++b) bf[b] = *(const f16x8_w*)(Bs + (wn * WN * 16 + b * 16 + fr) * 64 + pc);
     const int p = fr + tx - 1;
     const int lofs = p * 128 + (((kk * 4 + fg) ^ halo_swz(p)) * 16);
-    const int rbase = 6 * c + ty + 2 * wm;  // ring row of the wave's first output row, before & 7
+    const int rbase = 6 * c + ty + wrow;  // ring row of the wave's first output row, before & 7
 #pragma unroll
-    for (int a = 0; a < C::WM; ++a) {
-      const int rr = (rbase + a / 4) & 7;
-      af[a] = *(const f16x8_w*)(smem + rr * HC::ROW + (a % 4) * 16 * 128 + lofs);
+    for (int a = 0; a < WM; ++a) {
+      const int rr = (rbase + a * 16 / W) & 7;
+      af[a] = *(const f16x8_w*)(smem + rr * HC::ROW + (a * 16 % W) * 128 + lofs);
     }
   };
-  // MFMAs of one half; edge lanes of the first / last 16-pixel group of a row
-  // are zeroed when the tap column leaves the image
-  auto mm = [&](f16x8_w (&af)[C::WM], const f16x8_w (&bf)[C::WN], int tx) {
+  // MFMAs of one half; the edge lane of a row's first / last 16-pixel group
+  // is zeroed when the tap column leaves the image
+  auto mm = [&](f16x8_w (&af)[WM], const f16x8_w (&bf)[WN], int tx) {
     const bool zl = tx == 0 && lane_l, zr = tx == 2 && lane_r;
 #pragma unroll
-    for (int a = 0; a < C::WM; ++a) {
-      if (a % 4 == 0 && zl) af[a] = f16x8_w{};
-      if (a % 4 == 3 && zr) af[a] = f16x8_w{};
+    for (int a = 0; a < WM; ++a) {
+      if ((a * 16) % W == 0 && zl) af[a] = f16x8_w{};
+      if ((a * 16 + 16) % W == 0 && zr) af[a] = f16x8_w{};
 #pragma unroll
-      for (int b = 0; b < C::WN; ++b)
+      for (int b = 0; b < WN; ++b)
         acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a], bf[b], acc[a][b], 0, 0, 0);
     }
   };
   auto interleave = [&]() {
 #pragma unroll
-    for (int a = 0; a < C::WN; ++a) {
-      __builtin_amdgcn_sched_group_barrier(0x008, C::WN, 0);
+    for (int a = 0; a < WN; ++a) {
+      __builtin_amdgcn_sched_group_barrier(0x008, WN, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
     }
 #pragma unroll
-    for (int a = C::WN; a < C::WM; ++a) {
-      __builtin_amdgcn_sched_group_barrier(0x008, C::WN, 0);
+    for (int a = WN; a < WM; ++a) {
+      __builtin_amdgcn_sched_group_barrier(0x008, WN, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
   };
@@ -843,23 +870,28 @@ __global__ __launch_bounds__(512, 2) void conv_hwide3_kernel(ConvOp op) {
       if (++y == 3) { y = 0; ++c; }
     }
   };
+  constexpr int NBS = HC::NBS;
   // cursors: read step (rc, ry, rx) in B stage rs; B DMA step (bc, by, bx) into stage bs
   int rc = 0, ry = 0, rx = 0, rs = 0;
-  int bc = 0, by = 0, bx = 2, bs = 2;
+  int bc = 0, by = 0, bx = NBS - 1, bs = NBS - 1;
   const int lc = nchunks - 1;  // clamp for B past the end
-  f16x8_w a0[C::WM], b0[C::WN], a1[C::WM], b1[C::WN];
+  f16x8_w a0[WM], b0[WN], a1[WM], b1[WN];
   region_row(0, 0);
   region_row(0, 1);
   region_row(0, 2);
   region_row(0, 3);
   issue_b(0, 0, 0);
-  issue_b(1, 0, 1);
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::BJ) : "memory");  // rows 0-3 and B(0) landed
+  if constexpr (NBS == 3) {
+    issue_b(1, 0, 1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(HC::BJ) : "memory");  // rows 0-3 and B(0) landed
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __builtin_amdgcn_s_barrier();
-  issue_b(2, 0, 2);  // B(2)
-  adv(bc, by, bx);   // -> step 3
+  issue_b(bs, 0, NBS - 1);  // B(NBS - 1)
+  adv(bc, by, bx);          // -> step NBS
   bs = 0;
-  issue_pieces(0, 0);
+  issue_rows(0, 0);
   rd(0, 0, 0, 0, 0, a0, b0);
   int tx0 = 0;
   for (int step = 0; step < total - 1; ++step) {
@@ -867,18 +899,20 @@ __global__ __launch_bounds__(512, 2) void conv_hwide3_kernel(ConvOp op) {
     const int tx1 = rx;
     mm(a0, b0, tx0);
     interleave();
-    // RAW: every DMA older than the previous iteration's (B(step + 2) and the
-    // pieces issued before step's reads) has landed -> B(step + 1) and the
-    // region rows step + 1 reads.  WAR: own fragment reads of step retired.
-    if (pieces(rc, ry * 3 + rx)) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(C::BJ + 1) : "memory");
-    else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(C::BJ) : "memory");
+    // RAW: B(step + 1) and the region rows step + 1 reads have landed: the
+    // only DMAs allowed in flight are the previous iteration's region rows
+    // (issued two steps ahead of their first reader) and, with three stages,
+    // its B(step + 2).  WAR: own fragment reads of step retired.
+    constexpr int VB = NBS == 3 ? HC::BJ : 0;
+    if (rows_at(rc, ry * 3 + rx)) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(VB + HC::RP) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(VB) : "memory");
     __builtin_amdgcn_s_barrier();
     adv(rc, ry, rx);  // -> step + 1
-    rs = rs == 2 ? 0 : rs + 1;
-    issue_b(bs, bc > lc ? lc : bc, bc > lc ? 8 : by * 3 + bx);  // B(step + 3) into the stage step read
+    rs = rs == NBS - 1 ? 0 : rs + 1;
+    issue_b(bs, bc > lc ? lc : bc, bc > lc ? 8 : by * 3 + bx);  // B(step + NBS) into the stage step read
     adv(bc, by, bx);
-    bs = bs == 2 ? 0 : bs + 1;
-    issue_pieces(rc, ry * 3 + rx);
+    bs = bs == NBS - 1 ? 0 : bs + 1;
+    issue_rows(rc, ry * 3 + rx);
     rd(rs, rc, ry, rx, 0, a0, b0);
     tx0 = rx;
     mm(a1, b1, tx1);
@@ -890,21 +924,21 @@ __global__ __launch_bounds__(512, 2) void conv_hwide3_kernel(ConvOp op) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // every wave is done with the ring and stages before the epilogue reuses LDS
 
-  wide_epilogue<BN, C::WM, C::WN, C::WAVES_M>(op, acc, smem, m0, n0, M, HW);
+  wide_epilogue<BN, WM, WN, HC::WAVES_M, BM, true>(op, acc, smem, m0, n0, M, HW);
 }
 
-template <int BN>
+template <int BN, int W>
 static int launch_hwide3(const ConvOp& op, hipStream_t st) {
-  using HC = Halo3Cfg<BN>;
+  using HC = Halo3Cfg<BN, W>;
   static bool attr_set = false;
   if (!attr_set) {
-    const hipError_t e =
-        hipFuncSetAttribute((const void*)conv_hwide3_kernel<BN>, hipFuncAttributeMaxDynamicSharedMemorySize, HC::LDS);
+    const hipError_t e = hipFuncSetAttribute((const void*)conv_hwide3_kernel<BN, W>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, HC::LDS);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
-  const int grid = (op.B * op.Ho * HC::W / WBM) * (op.N / BN);
-  hipLaunchKernelGGL((conv_hwide3_kernel<BN>), dim3(grid), dim3(512), HC::LDS, st, op);
+  const int grid = (op.B * op.Ho * W / HC::BM) * (op.N / BN);
+  hipLaunchKernelGGL((conv_hwide3_kernel<BN, W>), dim3(grid), dim3(512), HC::LDS, st, op);
   return (int)hipGetLastError();
 }
 
@@ -917,9 +951,10 @@ static int halo_route(const ConvOp& op, hipStream_t st) {
   const ConvSeg& s = op.seg[0];
   if (s.kh != 3 || s.kw != 3 || s.stride != 1 || s.pad != 1 || s.dil != 1 || s.pre != kPreNone) return kErrUnsupported;
   if (s.Hin != op.Ho || s.Win != op.Wo || s.C % WBK || (op.Ho * op.Wo) % WBM) return kErrUnsupported;
-  if (op.Wo == 64 && op.N % 256 == 0) return mode == 1 ? launch_hwide<256, 64>(op, st) : launch_hwide3<256>(op, st);
+  if (op.Wo == 64 && op.N % 256 == 0) return mode == 1 ? launch_hwide<256, 64>(op, st) : launch_hwide3<256, 64>(op, st);
   if (op.Wo == 64) return launch_hwide<128, 64>(op, st);
   if (op.Wo == 128 && mode == 1) return launch_hwide<128, 128>(op, st);
+  if (op.Wo == 128 && mode == 2 && (op.Ho * op.Wo) % 512 == 0) return launch_hwide3<128, 128>(op, st);
   return kErrUnsupported;
 }
 
