@@ -103,8 +103,10 @@ def parity_vs_cpu(sd, pre, aspp, x, outs, precision):
             "sample": "image 0 of the last timed batch vs oracle/net.py fp32 on host cores"}
 
 
+# every kernel launch_conv dispatches to (the bench's conv family = the executor's GEMM ops)
 CONV_KERNELS = ("conv_halo_kernel", "conv_igemm_kernel", "conv_wide_kernel", "conv_wide32_kernel",
-                "conv_stream_kernel", "conv_stream_fam_kernel")
+                "conv_stream_kernel", "conv_stream_fam_kernel", "conv_ring_kernel", "conv_ring32_kernel",
+                "conv_hwide_kernel", "conv_hwide3_kernel")
 
 
 def pmc_traffic(args):
@@ -435,7 +437,7 @@ def main():
             "traffic_unit": "bytes per conv launch (rocprofv3 FETCH_SIZE*2 + WRITE_SIZE)",
             "traffic_per_img_GB": traffic["bytes_per_forward"] / B / 1e9 if traffic else None,
             "alg_bytes_per_launch": g_bytes / max(g_calls, 1),
-            "kernel": "conv family: conv_wide/conv_wide32/conv_stream/conv_stream_fam/conv_halo/conv_igemm (all conv launches of the step)",
+            "kernel": "conv family: " + "/".join(k[:-7] for k in CONV_KERNELS) + " (all conv launches of the step)",
             "profiled_steps": 1,
             "launches_per_step": g_calls,
             "avg_launch_us": 1000.0 * g_ms / max(g_calls, 1),

@@ -514,8 +514,7 @@ struct HaloCfg {
   static_assert(W % 16 == 0 && WBM % W == 0, "tiles of whole rows");
 };
 
-// ABL (timing ablations, results wrong): 1 = no B DMA, 2 = no DMA at all, 3 = no MFMAs
-template <int BN, int W, int ABL = 0>
+template <int BN, int W>
 __global__ __launch_bounds__(512, 2) void conv_hwide_kernel(ConvOp op) {
   using C = WideCfg<BN>;
   using HC = HaloCfg<BN, W>;
@@ -552,7 +551,7 @@ __global__ __launch_bounds__(512, 2) void conv_hwide_kernel(ConvOp op) {
     const int r = i * 64 / W, col = i * 64 % W;
     const int iy = oy0 - 1 + r;
     const half_t* g = (unsigned)iy < (unsigned)H ? rsrc + ((size_t)iy * W + col) * cs + c * WBK : zero;
-    if (ABL != 2) glds16(g, smem + (c & 1) * HC::R_BYTES + (i * 8 + wave) * 1024);
+    glds16(g, smem + (c & 1) * HC::R_BYTES + (i * 8 + wave) * 1024);
   };
 
   const int q8 = lane >> 3;
@@ -566,7 +565,7 @@ __global__ __launch_bounds__(512, 2) void conv_hwide_kernel(ConvOp op) {
     for (int j = 0; j < C::BJ; ++j) {
       const int n = wave * (BN / 8) + j * 8 + q8;
       const int ch = qc ^ ((4 * j + sw_lane) & 7);
-      if (ABL == 0 || ABL == 3) glds16(Wt + (size_t)(n0 + n) * op.Kpad + kb + ch * 8, Bs + (wave * (BN / 8) + j * 8) * 128);
+      glds16(Wt + (size_t)(n0 + n) * op.Kpad + kb + ch * 8, Bs + (wave * (BN / 8) + j * 8) * 128);
     }
   };
 
@@ -604,13 +603,6 @@ __global__ __launch_bounds__(512, 2) void conv_hwide_kernel(ConvOp op) {
     }
   };
   auto mm = [&](const f16x8_w (&af)[C::WM], const f16x8_w (&bf)[C::WN]) {
-    if constexpr (ABL == 3) {
-#pragma unroll
-      for (int a = 0; a < C::WM; ++a) asm volatile("" ::"v"(af[a]));
-#pragma unroll
-      for (int b = 0; b < C::WN; ++b) asm volatile("" ::"v"(bf[b]));
-      return;
-    }
 #pragma unroll
     for (int a = 0; a < C::WM; ++a)
 #pragma unroll
@@ -618,7 +610,6 @@ __global__ __launch_bounds__(512, 2) void conv_hwide_kernel(ConvOp op) {
         acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a], bf[b], acc[a][b], 0, 0, 0);
   };
   auto interleave = [&]() {
-    if constexpr (ABL == 3) return;
 #pragma unroll
     for (int a = 0; a < C::WN; ++a) {
       __builtin_amdgcn_sched_group_barrier(0x008, C::WN, 0);
@@ -678,29 +669,19 @@ __global__ __launch_bounds__(512, 2) void conv_hwide_kernel(ConvOp op) {
   wide_epilogue<BN, C::WM, C::WN, C::WAVES_M>(op, acc, smem, m0, n0, M, HW);
 }
 
-template <int BN, int W, int ABL>
-static int launch_hwide_abl(const ConvOp& op, hipStream_t st) {
+template <int BN, int W>
+static int launch_hwide(const ConvOp& op, hipStream_t st) {
   using HC = HaloCfg<BN, W>;
   static bool attr_set = false;
   if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute((const void*)conv_hwide_kernel<BN, W, ABL>,
+    const hipError_t e = hipFuncSetAttribute((const void*)conv_hwide_kernel<BN, W>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, HC::LDS);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
   const int grid = (op.B * op.Ho * W / WBM) * (op.N / BN);
-  hipLaunchKernelGGL((conv_hwide_kernel<BN, W, ABL>), dim3(grid), dim3(512), HC::LDS, st, op);
+  hipLaunchKernelGGL((conv_hwide_kernel<BN, W>), dim3(grid), dim3(512), HC::LDS, st, op);
   return (int)hipGetLastError();
-}
-
-// UPR_HALO_ABL=1/2/3: timing ablations (wrong results; convbench only)
-template <int BN, int W>
-static int launch_hwide(const ConvOp& op, hipStream_t st) {
-  static const int abl = env_int("UPR_HALO_ABL", 0);
-  if (abl == 1) return launch_hwide_abl<BN, W, 1>(op, st);
-  if (abl == 2) return launch_hwide_abl<BN, W, 2>(op, st);
-  if (abl == 3) return launch_hwide_abl<BN, W, 3>(op, st);
-  return launch_hwide_abl<BN, W, 0>(op, st);
 }
 
 // ---------------------------------------------------------------------------

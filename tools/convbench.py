@@ -21,6 +21,7 @@ from upr import runtime  # noqa: E402
 SHAPES = {
     "dec1": (32, 512, 512, 32, 32, 3, 1, 1, 1, True),     # dec1.conv.3-like, 512^2 32ch
     "dec1p": (32, 512, 512, 32, 32, 3, 1, 1, 1, False),   # dec1.conv.0-like (ReLU, no residual)
+    "fam64": (32, 512, 512, 64, 32, 3, 1, 1, 1, False),   # FAM fusion-like 32-wide GEMM, K = 576
     "fam_h": (32, 512, 512, 32, 64, 3, 1, 1, 1, False),   # FAM branch3/4 conv1 fused, N=64
     "dec2": (32, 256, 256, 64, 64, 3, 1, 1, 1, True),
     "dec3": (32, 128, 128, 128, 128, 3, 1, 1, 1, True),
