@@ -409,8 +409,28 @@ static int conv_impl_mode() {
   return mode;
 }
 
+int launch_preact_f16(const void* x, const float* sc, const float* sh, void* o, size_t npix, int C, hipStream_t st);
+
 int launch_conv(const ConvOp& op, int dtype, hipStream_t stream) {
   if (op.nseg < 1 || op.nseg > 4 || op.B <= 0 || op.Ho <= 0 || op.Wo <= 0) return kErrArg;
+  if (op.out2) {
+    // fused second output: only the wide-tile and row-ring epilogues write it;
+    // any other kernel runs the plain op and the PreAct pass separately
+    if (dtype != kF16 || op.store != kStoreNHWC || op.out_coff || op.out_cs != op.N || op.out2_cs != op.N ||
+        !op.pre2_scale || !op.pre2_shift)
+      return kErrArg;
+    if (conv_impl_mode() == 0) {
+      int rc = launch_conv_wide(op, stream);
+      if (rc != kErrUnsupported) return rc;
+      rc = launch_conv_ring(op, stream);
+      if (rc != kErrUnsupported) return rc;
+    }
+    ConvOp c = op;
+    c.out2 = nullptr;
+    const int rc = launch_conv(c, dtype, stream);
+    if (rc != kOk) return rc;
+    return launch_preact_f16(op.out, op.pre2_scale, op.pre2_shift, op.out2, (size_t)op.B * op.Ho * op.Wo, op.N, stream);
+  }
   for (int s = 0; s < op.nseg; ++s)
     if (op.seg[s].C % 32 || op.seg[s].src == nullptr) return kErrShape;
   if (conv_impl_mode() == 0) {

@@ -73,7 +73,8 @@ enum RingMode : int { kRingConv = 0, kRingHead = 1, kRingFam = 2, kRingS2 = 3 };
 // blocks per CU); only the configs that fit without spilling (no residual / head)
 // kRingWide: 64-pixel strips (4 pixel groups per wave row): twice the MFMAs per
 // step for the same per-step barrier / DMA / cursor work (32 -> 32 convs)
-enum RingFlags : int { kRingRes = 1, kRingRelu = 2, kRingSc = 4, kRingOcc3 = 8, kRingWide = 16 };
+// kRingOut2: the epilogue also writes relu(fma(o, pre2_scale, pre2_shift)) (ConvOp::out2)
+enum RingFlags : int { kRingRes = 1, kRingRelu = 2, kRingSc = 4, kRingOcc3 = 8, kRingWide = 16, kRingOut2 = 32 };
 
 // A ring of NPL chunk planes: 4 groups of GROWS rows of RW pixels.  DEINT:
 // ring column p holds source column 2p (p < (RW+1)/2) or 2(p - (RW+1)/2) + 1.
@@ -198,7 +199,8 @@ struct RingCfg {
   static constexpr int E = RES ? EPX * NB / 512 : SC ? EPX / 16 : HEAD ? 1 : 0;  // DMA instructions per wave per step
   static constexpr int LDS = WBYTES + RA::BYTES + (FAM ? RB::BYTES : 0) + NWV * EW;
   static constexpr int G = RA::G + (FAM ? RB::G : 0);              // ring DMA per step (waves 0-3)
-  static constexpr int S = HEAD ? GPW : GPW * NT;                  // stores per wave per step
+  static constexpr bool OUT2 = (FL & kRingOut2) != 0;
+  static constexpr int S = HEAD ? GPW : GPW * NT * (OUT2 ? 2 : 1);  // stores per wave per step
   // vmcnt waits, waves 0-3 (ring DMA) / waves 4-7 (none): DMA(kk) has landed
   // at step 0 / step 1 / steps >= 2 / after a FAM pool flush (its atomics)
   static constexpr int W0 = G, W1 = E + G + S, WK = 2 * S + E + G, WF = WK + (FAM ? 4 * NT : 0);
@@ -318,6 +320,16 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, RingCfg<MODE, C, NB, FL
     for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
       for (int i = 0; i < 4; ++i) hw2[nt][i] = op.head_w[nt * 16 + fg * 4 + i];
+  }
+  float p2s[K::OUT2 ? NT : 1][4], p2h[K::OUT2 ? NT : 1][4];
+  if constexpr (K::OUT2) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        p2s[nt][i] = op.pre2_scale[nt * 16 + fg * 4 + i];
+        p2h[nt][i] = op.pre2_shift[nt * 16 + fg * 4 + i];
+      }
   }
   const int abase = fg * RA::PLANE + fr * 16;  // chunk plane fg, pixel fr of a ring row
   const int bbase = fg * RB::PLANE + fr * 16;
@@ -653,6 +665,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, RingCfg<MODE, C, NB, FL
               if (ovalid[g]) pool[nt][i] += (float)o[i];
           }
           *(uint2*)(dg + nt * 16) = __builtin_bit_cast(uint2, o);
+          if constexpr (K::OUT2) {
+            f16x4_r q;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) q[i] = (half_t)fmaxf(__builtin_fmaf((float)o[i], p2s[nt][i], p2h[nt][i]), 0.f);
+            half_t* d2 = ovalid[g] ? (half_t*)op.out2 + prow * ocs + oloff[g] : (half_t*)(g_ring_sink + tid * 16);
+            *(uint2*)(d2 + nt * 16) = __builtin_bit_cast(uint2, q);
+          }
         }
       }
     }
@@ -1095,6 +1114,7 @@ static bool ring_occ3() {
 int launch_conv_ring(const ConvOp& op, hipStream_t st) {
   if (!ring_enabled()) return kErrUnsupported;
   if (op.Ho < 4 || op.Wo < 16) return kErrUnsupported;
+  if (op.out2 && op.nseg != 2) return kErrUnsupported;  // fused PreAct output: enc1.conv2 program only
   if (ring_fam_program(op)) return launch_ring_cfg<kRingFam, 32, 32, 0>(op, st);
   if (op.res1 || op.img_bias || op.pool || op.scale || op.Kpad % 8) return kErrUnsupported;
   const ConvSeg& s = op.seg[0];
@@ -1122,6 +1142,7 @@ int launch_conv_ring(const ConvOp& op, hipStream_t st) {
       return kErrUnsupported;
     if (q.Hin != 2 * op.Ho || q.Win != 2 * op.Wo || q.cs % 8 || q.coff % 8 || (uintptr_t)q.src % 16 || op.Kpad != 608)
       return kErrUnsupported;
+    if (op.out2) return ring_relu<kRingConv, 64, 64, kRingSc | kRingOut2>(op, st);
     return ring_relu<kRingConv, 64, 64, kRingSc>(op, st);
   }
   if (op.nseg != 1) return kErrUnsupported;

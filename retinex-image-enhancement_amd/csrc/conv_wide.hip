@@ -259,6 +259,17 @@ __device__ __forceinline__ void wide_epilogue(const ConvOp& op, f32x4_w (&acc)[W
           off = (size_t)m * op.out_cs + op.out_coff + nch;
         }
         *(f16x8_w*)((half_t*)op.out + off) = o;
+        if (op.out2) {
+          const f32x4_w s0 = *(const f32x4_w*)(op.pre2_scale + nch), s1 = *(const f32x4_w*)(op.pre2_scale + nch + 4);
+          const f32x4_w h0 = *(const f32x4_w*)(op.pre2_shift + nch), h1 = *(const f32x4_w*)(op.pre2_shift + nch + 4);
+          f16x8_w q;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            q[e] = (half_t)fmaxf(__builtin_fmaf((float)o[e], s0[e], h0[e]), 0.f);
+            q[e + 4] = (half_t)fmaxf(__builtin_fmaf((float)o[e + 4], s1[e], h1[e]), 0.f);
+          }
+          *(f16x8_w*)((half_t*)op.out2 + (size_t)m * op.out2_cs + nch) = q;
+        }
         if (op.pool) {
           if (one_image) {
 #pragma unroll
@@ -1026,6 +1037,7 @@ static bool wide_enabled() {
 // fp16 only; returns kErrUnsupported for shapes this kernel does not take
 int launch_conv_wide(const ConvOp& op, hipStream_t st) {
   if (!wide_enabled()) return kErrUnsupported;
+  if (op.out2 && ((uintptr_t)op.out2 % 16 || op.store != kStoreNHWC)) return kErrUnsupported;
   if (op.store == kStoreHeadIllu || op.N % 128) return kErrUnsupported;
   if (op.Kpad % 8 || ((uintptr_t)op.W % 16)) return kErrUnsupported;
   for (int s = 0; s < op.nseg; ++s) {

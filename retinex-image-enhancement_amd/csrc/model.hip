@@ -464,14 +464,26 @@ struct Builder {
       Op* conv3_producer = nullptr;
       for (auto& o : m->ops)
         if (o.kind == OP_CONV3 && o.out == in) conv3_producer = &o;
+      // the GEMM that produced `in` as a whole NHWC tensor (the previous block's conv2, the ASPP fusion)
+      Op* gemm_producer = nullptr;
+      for (auto& o : m->ops)
+        if (o.kind == OP_GEMM && o.out == in && o.store == kStoreNHWC && o.out_coff == 0 && o.out_cs == cin &&
+            m->layers[o.layer].N == cin)
+          gemm_producer = &o;
+      const int pa = in_level == 0 ? B_PA1 : (in_level == 1 ? B_PA2 : (in_level == 2 ? B_PA3 : B_PA4));
       if (preact_materialised(m) && conv3_producer) {
         // enc1: the 3->32 input conv writes relu(bn1(x1)) beside x1 (one pass)
         conv3_producer->out2 = B_PA1; conv3_producer->ps = pre_s; conv3_producer->ph = pre_h;
         osrc = B_PA1; opre = kPreNone;
+      } else if (preact_materialised(m) && gemm_producer) {
+        // enc2 / enc3 / bottleneck: the producing conv's epilogue writes
+        // relu(bn1(x)) beside x (ConvOp::out2) -- no separate read of x
+        gemm_producer->out2 = pa; gemm_producer->ps = pre_s; gemm_producer->ph = pre_h;
+        osrc = pa; opre = kPreNone;
       } else if (preact_materialised(m)) {
         Op po;
         po.kind = OP_PREACT; po.name = p + ".bn1_relu"; po.in = in; po.level = in_level; po.w = pre_s; po.b = pre_h;
-        po.out = in_level == 0 ? B_PA1 : (in_level == 1 ? B_PA2 : (in_level == 2 ? B_PA3 : B_PA4));
+        po.out = pa;
         m->ops.push_back(po);
         osrc = po.out; opre = kPreNone;
       }
@@ -840,6 +852,10 @@ static int run_forward(UprModel* m, const void* x, int B, int H, int W, void* en
           c.out = buf(o.out); c.out_cs = o.out_cs; c.out_coff = o.out_coff;
         }
         c.pool = o.pool_slot >= 0 ? pool + (size_t)o.pool_slot * B * 256 : nullptr;
+        if (o.out2 >= 0) {
+          c.out2 = buf(o.out2); c.out2_cs = L.N;
+          c.pre2_scale = fptr(o.ps); c.pre2_shift = fptr(o.ph);
+        }
         rc = launch_conv(c, dt, st);
         if (m->prof) {
           // GEMM work of this launch: 2*M*N*K; algorithmic bytes: every source read once,
@@ -854,6 +870,7 @@ static int run_forward(UprModel* m, const void* x, int B, int H, int W, void* en
           bytes += Mpx * nout * (o.store == kStoreHeadIllu ? 4.0 : elt);
           if (c.res1) bytes += Mpx * L.N * elt;
           if (c.res2) bytes += Mpx * L.N * elt;
+          if (c.out2) bytes += Mpx * L.N * elt;
           m->cur_flops[oi] = 2.0 * Mpx * L.N * K;
           m->cur_bytes[oi] = bytes;
         }

@@ -507,7 +507,7 @@ __global__ __launch_bounds__(256) void preact_kernel(const half_t* __restrict__ 
     const h8 v = ((const h8*)x)[i];
     h8 r;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) r[e] = (half_t)fmaxf((float)v[e] * sc[c + e] + sh[c + e], 0.f);
+    for (int e = 0; e < 8; ++e) r[e] = (half_t)fmaxf(__builtin_fmaf((float)v[e], sc[c + e], sh[c + e]), 0.f);
     ((h8*)o)[i] = r;
   }
 }

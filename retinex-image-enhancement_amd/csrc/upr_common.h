@@ -86,6 +86,13 @@ struct ConvOp {
   int x_f16;
   float* illu;            // [B,1,Ho,Wo] fp32 output (or T when illu_f16)
   int illu_f16;
+  // second output (fp16, kStoreNHWC only; nullable): out2[m*out2_cs + n] =
+  // relu(fma(o, pre2_scale[n], pre2_shift[n])) of the fp16-rounded stored value
+  // o -- the next PreActResBlock's relu(bn1(x)) (models/model.py:164-166)
+  // written by the producer's epilogue instead of a separate pass
+  void* out2; int out2_cs;
+  const float* pre2_scale;
+  const float* pre2_shift;
 };
 
 int launch_conv(const ConvOp& op, int dtype, hipStream_t stream);
