@@ -306,7 +306,7 @@ def train_main(args):
         "value": imgs / elapsed, "unit": "images/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None,
-        "dtype": "f16 convs under autocast (fp32 accumulate; fp32 BN / loss / wgrad / Adam)" if args.amp else "f32",
+        "dtype": "f16 convs under autocast (fp32 accumulate; fp16-operand weight gradients; fp32 BN / loss / Adam)" if args.amp else "f32",
         "data": "synthetic torch.rand inputs, random-init weights (seed 0), seeded random-init VGG19 (seed 1234)",
         "config": {"workload": f"configs[4]: bs={B}/GPU {S}x{S} {args.variant} train step"
                                + (" AMP: autocast (fp16 MFMA convs) + GradScaler" if args.amp else " (fp32)"),

@@ -84,6 +84,15 @@ int upr_t_cast_f16(const float* x, void* y, size_t n, void* stream);
 int upr_t_conv_wgrad(const float* x, int B, int H, int W, int Cin, int x_cs, int x_coff, const float* dy, int Ho,
                      int Wo, int Cout, int dy_cs, int dy_coff, int kh, int kw, int stride, int pad, int dil,
                      float* dwp, void* stream);
+/* AMP weight gradient (trainers/train.py:72, convs under autocast): the same
+ * contract as upr_t_conv_wgrad with both operands rounded to fp16 and fp32
+ * accumulation (v_mfma_f32_16x16x32_f16).  x16: the compact fp16 copy
+ * [B][H][W][Cin] of x made by the AMP forward (upr_t_conv_mfma16), or NULL
+ * (x is cast into a stream-ordered temporary).  Shapes the fp16 kernel does
+ * not take (Wo % 64 != 0, ...) run the fp32 upr_t_conv_wgrad. */
+int upr_t_conv_wgrad16(const float* x, const void* x16, int B, int H, int W, int Cin, int x_cs, int x_coff,
+                       const float* dy, int Ho, int Wo, int Cout, int dy_cs, int dy_coff, int kh, int kw, int stride,
+                       int pad, int dil, float* dwp, void* stream);
 /* Weight layout transforms.  mode 0: [Co][Ci][kh][kw] -> [Co][(ky,kx,ci)];
  * mode 1: -> [Ci][(ky,kx,co)] spatially flipped (stride-1 dgrad as a conv);
  * mode 2: ConvTranspose [Ci][Co][2][2] -> [(a,b,co)][ci] (forward GEMM);

@@ -57,6 +57,8 @@ int small_conv_wgrad(const UprView* xv, const UprView* dyv, int B, int H, int W,
 int wgrad_gemm(const float* x, int B, int H, int W, int Cin, int x_cs, int x_coff, const float* dy, int Ho, int Wo,
                int Cout, int dy_cs, int dy_coff, int kh, int kw, int stride, int pad, int dil, float* dwp,
                hipStream_t st);
+int wgrad16_gemm(const void* x16, int B, int H, int W, int Cin, const float* dy, int Ho, int Wo, int Cout, int dy_cs,
+                 int dy_coff, int kh, int kw, int stride, int pad, int dil, float* dwp, hipStream_t st);
 static bool wgrad_gemm_on() {
   static int on = -1;
   if (on < 0) {
@@ -1681,6 +1683,32 @@ int upr_t_conv_wgrad(const float* x, int B, int H, int W, int Cin, int x_cs, int
   hipLaunchKernelGGL(conv_wgrad_kernel, grid, dim3(256), 0, ST(stream), x, B, H, W, Cin, x_cs, x_coff, dy, Ho, Wo,
                      Cout, dy_cs, dy_coff, kh, kw, stride, pad, dil, dwp);
   LAUNCH_CHECK();
+}
+
+int upr_t_conv_wgrad16(const float* x, const void* x16, int B, int H, int W, int Cin, int x_cs, int x_coff,
+                       const float* dy, int Ho, int Wo, int Cout, int dy_cs, int dy_coff, int kh, int kw, int stride,
+                       int pad, int dil, float* dwp, void* stream) {
+  if ((!x && !x16) || !dy || !dwp || B <= 0 || Cin % 32 || Cout % 32 || Cin <= 0 || Cout <= 0) return UPR_ERR_ARG;
+  hipStream_t st = ST(stream);
+  const bool fits = Wo % 64 == 0 && dy_cs % 4 == 0 && dy_coff % 4 == 0 && (uintptr_t)dy % 16 == 0 &&
+                    (uintptr_t)dwp % 16 == 0 && (x16 || (x && x_cs % 8 == 0 && x_coff % 8 == 0 && (uintptr_t)x % 16 == 0));
+  if (fits) {
+    void* tmp = nullptr;
+    const void* src = x16;
+    if (!src) {
+      const long long Mi = (long long)B * H * W;
+      UPR_CHECK_HIP(hipMallocAsync(&tmp, (size_t)Mi * Cin * sizeof(half_t), st));
+      hipLaunchKernelGGL(cast_act_f16_kernel, dim3(grid_for(Mi * (Cin / 8))), dim3(256), 0, st, x, Mi, Cin, x_cs, x_coff,
+                         (half_t*)tmp);
+      src = tmp;
+    }
+    const int rc = wgrad16_gemm(src, B, H, W, Cin, dy, Ho, Wo, Cout, dy_cs, dy_coff, kh, kw, stride, pad, dil, dwp, st);
+    if (tmp) UPR_CHECK_HIP(hipFreeAsync(tmp, st));
+    if (rc != kErrUnsupported) return rc;
+  }
+  if (!x) return UPR_ERR_ARG;
+  return upr_t_conv_wgrad(x, B, H, W, Cin, x_cs, x_coff, dy, Ho, Wo, Cout, dy_cs, dy_coff, kh, kw, stride, pad, dil, dwp,
+                          stream);
 }
 
 int upr_t_pack_weight(const float* w, float* out, int Co, int Ci, int kh, int kw, int mode, void* stream) {

@@ -106,6 +106,7 @@ SIGNATURES.update({
                                _i, _p, _i, _p, _p]),
     "upr_t_cast_f16": (_i, [_p, _p, c_size_t, _p]),
     "upr_t_conv_wgrad": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p]),
+    "upr_t_conv_wgrad16": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p]),
     "upr_t_pack_weight": (_i, [_p, _p, _i, _i, _i, _i, _i, _p]),
     "upr_t_unpack_grad": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p]),
     "upr_t_zero_upsample": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _p]),

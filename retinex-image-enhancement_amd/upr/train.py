@@ -228,6 +228,7 @@ class Conv:
                                        res.ptr() if res is not None else None, res.cs if res is not None else 0,
                                        int(relu), _fp(out.t), out.cs, out.coff, store, _p(x16), 0, _p(y16),
                                        _stream()), "conv_mfma16")
+        return x16
 
     def fwd(self, x, relu=False, out=None, res=None, x_view=None):
         """x: Act (or x_view: (UprView, B, H, W) for an NCHW network input)."""
@@ -242,8 +243,10 @@ class Conv:
         out.fresh = False
         self.amp = _AMP[0] and self.mfma and x_view is None
         if self.amp:
-            self._mfma16(x.t, B, H, W, self.Cin, x.cs, x.coff, self.wp16, self.bias, self.Cout, self.kh, self.kw,
-                         self.s, self.p, self.d, res, relu, out)
+            # the fp16 copy of x is the weight gradient's B operand (upr_t_conv_wgrad16)
+            x16 = self._mfma16(x.t, B, H, W, self.Cin, x.cs, x.coff, self.wp16, self.bias, self.Cout, self.kh,
+                               self.kw, self.s, self.p, self.d, res, relu, out)
+            self.x16 = None if self.frozen else x16
         elif self.mfma and x_view is None:
             _chk(lib.upr_t_conv_mfma(_fp(x.t), B, H, W, self.Cin, x.cs, x.coff, _p(self.wp),
                                      _p(self.bias), self.Cout, self.kh, self.kw, self.s, self.p, self.d,
@@ -271,9 +274,17 @@ class Conv:
             gw = self.m.weight.grad
             if self.mfma and x_view is None:
                 zero(self.gp)
-                _chk(lib.upr_t_conv_wgrad(_fp(x.t), B, H, W, self.Cin, x.cs, x.coff, _fp(gy.t), Ho, Wo, self.Cout,
-                                          gy.cs, gy.coff, self.kh, self.kw, self.s, self.p, self.d, _p(self.gp), st),
-                     "conv_wgrad")
+                x16 = getattr(self, "x16", None)
+                if self.amp and x16 is not None:
+                    # autocast: fp16 operands, fp32 accumulation (trainers/train.py:72)
+                    _chk(lib.upr_t_conv_wgrad16(_fp(x.t), _p(x16), B, H, W, self.Cin, x.cs, x.coff, _fp(gy.t), Ho,
+                                                Wo, self.Cout, gy.cs, gy.coff, self.kh, self.kw, self.s, self.p,
+                                                self.d, _p(self.gp), st), "conv_wgrad16")
+                    self.x16 = None
+                else:
+                    _chk(lib.upr_t_conv_wgrad(_fp(x.t), B, H, W, self.Cin, x.cs, x.coff, _fp(gy.t), Ho, Wo,
+                                              self.Cout, gy.cs, gy.coff, self.kh, self.kw, self.s, self.p, self.d,
+                                              _p(self.gp), st), "conv_wgrad")
                 _chk(lib.upr_t_unpack_grad(_p(self.gp), _p(gw), self.Cout, self.Cin, self.kh, self.kw, 0, 1, st),
                      "unpack")
                 if self.bias is not None:
@@ -357,8 +368,12 @@ class ConvT:
         lib, st = L.lib(), _stream()
         zero(self.gp)
         # dwp[ci][(a,b,co)] = sum_p x[p][ci] * gy[2y+a][2x+b][co]: a k2 s2 "conv" of gy producing x
-        _chk(lib.upr_t_conv_wgrad(gy.ptr(), gy.B, gy.H, gy.W, self.Cout, gy.cs, 0, x.ptr(), x.H, x.W, self.Cin,
-                                  x.cs, 0, 2, 2, 2, 0, 1, _p(self.gp), st), "convT_wgrad")
+        if self.amp:
+            _chk(lib.upr_t_conv_wgrad16(gy.ptr(), None, gy.B, gy.H, gy.W, self.Cout, gy.cs, 0, x.ptr(), x.H, x.W,
+                                        self.Cin, x.cs, 0, 2, 2, 2, 0, 1, _p(self.gp), st), "convT_wgrad16")
+        else:
+            _chk(lib.upr_t_conv_wgrad(gy.ptr(), gy.B, gy.H, gy.W, self.Cout, gy.cs, 0, x.ptr(), x.H, x.W, self.Cin,
+                                      x.cs, 0, 2, 2, 2, 0, 1, _p(self.gp), st), "convT_wgrad")
         _chk(lib.upr_t_unpack_grad(_p(self.gp), _p(self.m.weight.grad), self.Cout, self.Cin, 2, 2, 3, 1, st),
              "unpack")
         _chk(lib.upr_t_chan_sum(gy.ptr(), gy.M, self.Cout, gy.cs, 0, _p(self.m.bias.grad), 1, st), "dbias")

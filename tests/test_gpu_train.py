@@ -78,6 +78,45 @@ def test_conv_layer(cin, cout, k, s, p, d, bias):
         _close(md.bias.grad, m.bias.grad, 1e-4, "dbias")
 
 
+@pytest.mark.parametrize("B,cin,cout,H,W,k,s,p,d", [
+    (2, 32, 32, 64, 128, 3, 1, 1, 1),    # 32 -> 32 3x3 (dec1 / head / FAM class): BM 32, 9 runs per tile
+    (1, 64, 128, 128, 128, 3, 2, 1, 1),  # encoder stride-2 conv: BM 128, 4 runs
+    (1, 256, 256, 64, 64, 3, 1, 1, 1),   # bottleneck: BM 128, 72 runs (18 tiles)
+    (2, 32, 64, 128, 128, 1, 2, 0, 1),   # projecting shortcut 1x1 s2: BM 64, 1 run
+    (1, 32, 32, 64, 64, 3, 1, 2, 2),     # FAM branch4_conv2 (dilation 2)
+    (2, 64, 64, 64, 64, 3, 1, 1, 1),     # BM 64, 9 runs x 2 tiles
+    (1, 32, 32, 24, 24, 3, 1, 1, 1),     # Wo % 64 != 0: the fp32 path
+])
+def test_conv_wgrad16_vs_fp64(B, cin, cout, H, W, k, s, p, d):
+    """AMP weight gradient (upr_t_conv_wgrad16): fp16-rounded operands, fp32
+    accumulation -> vs the fp64 weight gradient of the same fp16-rounded x and
+    dy (autocast's operands, trainers/train.py:72), max|d| <= 1e-4 max|ref|.
+    Both the x16-provided and the cast-internally forms."""
+    import torch.nn.functional as F
+    from upr import _lib as L
+    torch.manual_seed(3)
+    x = torch.randn(B, cin, H, W)
+    Ho = (H + 2 * p - d * (k - 1) - 1) // s + 1
+    Wo = (W + 2 * p - d * (k - 1) - 1) // s + 1
+    dy = torch.randn(B, cout, Ho, Wo)
+    fp16_path = Wo % 64 == 0
+    xh, dyh = (x.half().double(), dy.half().double()) if fp16_path else (x.double(), dy.double())
+    ref = torch.nn.grad.conv2d_weight(xh, (cout, cin, k, k), dyh, stride=s, padding=p, dilation=d)
+    ref = ref.permute(0, 2, 3, 1).reshape(cout, -1).float()
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    dyd = dy.permute(0, 2, 3, 1).contiguous().to(DEV)
+    x16 = xd.half()
+    lib = L.lib()
+    st = torch.cuda.current_stream().cuda_stream
+    for use_x16 in (True, False):
+        dw = torch.zeros(cout, k * k * cin, device=DEV)
+        rc = lib.upr_t_conv_wgrad16(xd.data_ptr(), x16.data_ptr() if use_x16 else None, B, H, W, cin, cin, 0,
+                                    dyd.data_ptr(), Ho, Wo, cout, cout, 0, k, k, s, p, d, dw.data_ptr(), st)
+        assert rc == 0, rc
+        torch.cuda.synchronize()
+        _close(dw, ref, 1e-4, f"wgrad16 x16={use_x16}")
+
+
 def test_convT_layer():
     from upr.train import Act, ConvT
     torch.manual_seed(1)
