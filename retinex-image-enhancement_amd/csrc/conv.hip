@@ -411,8 +411,18 @@ static int conv_impl_mode() {
 
 int launch_preact_f16(const void* x, const float* sc, const float* sh, void* o, size_t npix, int C, hipStream_t st);
 
+int launch_conv_out32(const ConvOp& op, hipStream_t stream) {
+  if (!op.out32 || op.out || op.out2 || op.pool || op.store == kStoreHeadIllu) return kErrArg;
+  if (op.nseg < 1 || op.nseg > 4 || op.B <= 0 || op.Ho <= 0 || op.Wo <= 0) return kErrArg;
+  if (conv_impl_mode() != 0) return kErrUnsupported;
+  const int rc = launch_conv_wide(op, stream);
+  if (rc != kErrUnsupported) return rc;
+  return launch_conv_ring(op, stream);
+}
+
 int launch_conv(const ConvOp& op, int dtype, hipStream_t stream) {
   if (op.nseg < 1 || op.nseg > 4 || op.B <= 0 || op.Ho <= 0 || op.Wo <= 0) return kErrArg;
+  if (op.out32) return kErrArg;  // launch_conv_out32
   if (op.out2) {
     // fused second output: only the wide-tile and row-ring epilogues write it;
     // any other kernel runs the plain op and the PreAct pass separately

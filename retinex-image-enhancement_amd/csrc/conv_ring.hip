@@ -62,6 +62,7 @@ typedef __attribute__((address_space(3))) void* lds_void_ptr_r;
 // write sink for out-of-range outputs (128 bytes per thread, <= 512 threads)
 __device__ __attribute__((aligned(256))) uint4 g_ring_zero[16];
 __device__ __attribute__((aligned(256))) uint2 g_ring_sink[512 * 16];
+__device__ __attribute__((aligned(256))) float g_ring_sink32[512 * 64];  // fp32 outputs: 256 bytes per thread
 __device__ __attribute__((aligned(256))) unsigned g_ring_ninf[64] = {
 #define NINF4 0xFC00FC00u, 0xFC00FC00u, 0xFC00FC00u, 0xFC00FC00u
     NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4
@@ -74,7 +75,8 @@ enum RingMode : int { kRingConv = 0, kRingHead = 1, kRingFam = 2, kRingS2 = 3 };
 // kRingWide: 64-pixel strips (4 pixel groups per wave row): twice the MFMAs per
 // step for the same per-step barrier / DMA / cursor work (32 -> 32 convs)
 // kRingOut2: the epilogue also writes relu(fma(o, pre2_scale, pre2_shift)) (ConvOp::out2)
-enum RingFlags : int { kRingRes = 1, kRingRelu = 2, kRingSc = 4, kRingOcc3 = 8, kRingWide = 16, kRingOut2 = 32 };
+// kRingOut32: fp32 output (ConvOp::out32, no res32) instead of the fp16 store
+enum RingFlags : int { kRingRes = 1, kRingRelu = 2, kRingSc = 4, kRingOcc3 = 8, kRingWide = 16, kRingOut2 = 32, kRingOut32 = 64 };
 
 // A ring of NPL chunk planes: 4 groups of GROWS rows of RW pixels.  DEINT:
 // ring column p holds source column 2p (p < (RW+1)/2) or 2(p - (RW+1)/2) + 1.
@@ -200,6 +202,8 @@ struct RingCfg {
   static constexpr int LDS = WBYTES + RA::BYTES + (FAM ? RB::BYTES : 0) + NWV * EW;
   static constexpr int G = RA::G + (FAM ? RB::G : 0);              // ring DMA per step (waves 0-3)
   static constexpr bool OUT2 = (FL & kRingOut2) != 0;
+  static constexpr bool OUT32 = (FL & kRingOut32) != 0;
+  static_assert(!OUT32 || (!RES && !SC && !OUT2 && MODE != kRingHead && MODE != kRingFam), "fp32 output: plain convs");
   static constexpr int S = HEAD ? GPW : GPW * NT * (OUT2 ? 2 : 1);  // stores per wave per step
   // vmcnt waits, waves 0-3 (ring DMA) / waves 4-7 (none): DMA(kk) has landed
   // at step 0 / step 1 / steps >= 2 / after a FAM pool flush (its atomics)
@@ -664,7 +668,17 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, RingCfg<MODE, C, NB, FL
             for (int i = 0; i < 4; ++i)
               if (ovalid[g]) pool[nt][i] += (float)o[i];
           }
-          *(uint2*)(dg + nt * 16) = __builtin_bit_cast(uint2, o);
+          if constexpr (K::OUT32) {
+            f32x4_r o32;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o32[i] = (float)o[i];
+            float* d32 = ovalid[g] ? op.out32 + prow * op.out32_cs + op.out32_coff +
+                                         (size_t)((g0 + g) * 16 + fr) * op.out32_cs + fg * 4
+                                   : g_ring_sink32 + tid * 64;
+            *(f32x4_r*)(d32 + nt * 16) = o32;
+          } else {
+            *(uint2*)(dg + nt * 16) = __builtin_bit_cast(uint2, o);
+          }
           if constexpr (K::OUT2) {
             f16x4_r q;
 #pragma unroll
@@ -1115,6 +1129,26 @@ int launch_conv_ring(const ConvOp& op, hipStream_t st) {
   if (!ring_enabled()) return kErrUnsupported;
   if (op.Ho < 4 || op.Wo < 16) return kErrUnsupported;
   if (op.out2 && op.nseg != 2) return kErrUnsupported;  // fused PreAct output: enc1.conv2 program only
+  if (op.out32) {
+    // fp32 output (training autocast convs): plain single-segment programs without residuals
+    if (op.res32 || op.res1 || op.res2 || op.out2 || op.nseg != 1 || op.store != kStoreNHWC) return kErrUnsupported;
+    if (op.img_bias || op.pool || op.scale || op.Kpad % 8 || (uintptr_t)op.out32 % 16 || op.out32_cs % 4 ||
+        op.out32_coff % 4)
+      return kErrUnsupported;
+    const ConvSeg& s = op.seg[0];
+    if (!ring_seg_ok(s)) return kErrUnsupported;
+    if (s.stride == 2) {
+      if (s.C != 32 || op.N != 64 || s.Hin != 2 * op.Ho || s.Win != 2 * op.Wo) return kErrUnsupported;
+      return ring_relu<kRingS2, 32, 64, kRingOut32>(op, st);
+    }
+    if (s.stride != 1 || s.Hin != op.Ho || s.Win != op.Wo) return kErrUnsupported;
+    if (s.C == 32 && op.N == 32)
+      return op.Wo >= 48 && ring_wide() ? ring_relu<kRingConv, 32, 32, kRingWide | kRingOut32>(op, st)
+                                        : ring_relu<kRingConv, 32, 32, kRingOut32>(op, st);
+    if (s.C == 32 && op.N == 64) return ring_relu<kRingConv, 32, 64, kRingOut32>(op, st);
+    if (s.C == 64 && op.N == 64) return ring_relu<kRingConv, 64, 64, kRingOut32>(op, st);
+    return kErrUnsupported;
+  }
   if (ring_fam_program(op)) return launch_ring_cfg<kRingFam, 32, 32, 0>(op, st);
   if (op.res1 || op.img_bias || op.pool || op.scale || op.Kpad % 8) return kErrUnsupported;
   const ConvSeg& s = op.seg[0];

@@ -251,14 +251,29 @@ __device__ __forceinline__ void wide_epilogue(const ConvOp& op, f32x4_w (&acc)[W
         f16x8_w o;
 #pragma unroll
         for (int e = 0; e < 8; ++e) o[e] = (half_t)v[e];
-        size_t off;
+        // output pixel and its channel offset
+        size_t pix;
+        int ch;
         if (convt) {
-          const size_t opix = ((size_t)img * 2 * op.Ho + 2 * py + (cq >> 1)) * (2 * op.Wo) + 2 * px + (cq & 1);
-          off = opix * op.out_cs + op.out_coff + cco;
+          pix = ((size_t)img * 2 * op.Ho + 2 * py + (cq >> 1)) * (2 * op.Wo) + 2 * px + (cq & 1);
+          ch = cco;
         } else {
-          off = (size_t)m * op.out_cs + op.out_coff + nch;
+          pix = (size_t)m;
+          ch = nch;
         }
-        *(f16x8_w*)((half_t*)op.out + off) = o;
+        if (op.out32) {
+          float* d32 = op.out32 + pix * op.out32_cs + op.out32_coff + ch;
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {  // one 16-byte half at a time (register pressure of the 128-VGPR variant)
+            f32x4_w t;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) t[e] = (float)o[hh * 4 + e];
+            if (op.res32) t += *(const f32x4_w*)(op.res32 + pix * op.res32_cs + ch + hh * 4);
+            *(f32x4_w*)(d32 + hh * 4) = t;
+          }
+        } else {
+          *(f16x8_w*)((half_t*)op.out + pix * op.out_cs + op.out_coff + ch) = o;
+        }
         if (op.out2) {
           const f32x4_w s0 = *(const f32x4_w*)(op.pre2_scale + nch), s1 = *(const f32x4_w*)(op.pre2_scale + nch + 4);
           const f32x4_w h0 = *(const f32x4_w*)(op.pre2_shift + nch), h1 = *(const f32x4_w*)(op.pre2_shift + nch + 4);
@@ -1038,6 +1053,8 @@ static bool wide_enabled() {
 int launch_conv_wide(const ConvOp& op, hipStream_t st) {
   if (!wide_enabled()) return kErrUnsupported;
   if (op.out2 && ((uintptr_t)op.out2 % 16 || op.store != kStoreNHWC)) return kErrUnsupported;
+  if (op.out32 && ((uintptr_t)op.out32 % 16 || op.out32_cs % 4 || op.out32_coff % 4)) return kErrUnsupported;
+  if (op.res32 && ((uintptr_t)op.res32 % 16 || op.res32_cs % 4)) return kErrUnsupported;
   if (op.store == kStoreHeadIllu || op.N % 128) return kErrUnsupported;
   if (op.Kpad % 8 || ((uintptr_t)op.W % 16)) return kErrUnsupported;
   for (int s = 0; s < op.nseg; ++s) {

@@ -1628,6 +1628,16 @@ int upr_t_cast_f16(const float* x, void* y, size_t n, void* stream) {
   LAUNCH_CHECK();
 }
 
+// UPR_T_OUT32=0: fp16 conv output + separate fp32 cast pass (A/B timing)
+static bool out32_on() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("UPR_T_OUT32");
+    on = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  return on == 1;
+}
+
 int upr_t_conv_mfma16(const float* x, int B, int H, int W, int Cin, int x_cs, int x_coff, const void* wp16,
                       const float* bias, int N, int kh, int kw, int stride, int pad, int dil, const float* res,
                       int res_cs, int relu, float* y, int y_cs, int y_coff, int store, void* x16, int x16_ready,
@@ -1657,7 +1667,19 @@ int upr_t_conv_mfma16(const float* x, int B, int H, int W, int Cin, int x_cs, in
   s.kh = kh; s.kw = kw; s.stride = stride; s.pad = pad; s.dil = dil; s.pre = kPreNone; s.kbase = 0;
   c.B = B; c.Ho = Ho; c.Wo = Wo; c.N = N; c.Kpad = kh * kw * Cin;
   c.W = wp16; c.bias = bias; c.relu = relu;
-  c.out = y16; c.out_cs = store == 1 ? N / 4 : N; c.out_coff = 0; c.store = store == 1 ? kStoreConvT2x2 : kStoreNHWC;
+  c.store = store == 1 ? kStoreConvT2x2 : kStoreNHWC;
+  if (out32_on()) {
+    // the fp32 output (+ fp32 residual / accumulated gradient) straight from the conv epilogue
+    ConvOp c32 = c;
+    c32.out32 = y; c32.out32_cs = y_cs; c32.out32_coff = y_coff;
+    c32.res32 = res; c32.res32_cs = res_cs;
+    const int rc = launch_conv_out32(c32, st);
+    if (rc != kErrUnsupported) {
+      if (rc != 0) return rc;
+      LAUNCH_CHECK();
+    }
+  }
+  c.out = y16; c.out_cs = store == 1 ? N / 4 : N; c.out_coff = 0;
   const int rc = launch_conv(c, kF16, st);
   if (rc != 0) return rc;
   const long long Mo = store == 1 ? (long long)B * 4 * Ho * Wo : (long long)B * Ho * Wo;

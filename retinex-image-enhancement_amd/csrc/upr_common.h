@@ -93,7 +93,17 @@ struct ConvOp {
   void* out2; int out2_cs;
   const float* pre2_scale;
   const float* pre2_shift;
+  // fp32 output of an fp16 conv (the training step's autocast convs, nullable;
+  // launch_conv_out32 only): out32[pix * out32_cs + out32_coff + n] =
+  // (float)(fp16-rounded result) + res32[pix * res32_cs + n] (res32 nullable,
+  // may alias out32); `out` is not written
+  float* out32; int out32_cs, out32_coff;
+  const float* res32; int res32_cs;
 };
+
+// fp16 convs with an fp32 output (ConvOp::out32): the wide-tile and row-ring
+// kernels; kErrUnsupported when neither takes the op
+int launch_conv_out32(const ConvOp& op, hipStream_t stream);
 
 int launch_conv(const ConvOp& op, int dtype, hipStream_t stream);
 
