@@ -1864,13 +1864,135 @@ int upr_t_maxpool(const UprView* x, int B, int H, int W, int C, int k, int s, in
   LAUNCH_CHECK();
 }
 
+// Max-pool backward as two deterministic passes (the atomic scatter above --
+// up to k*k fp32 atomics per input element in arbitrary order -- stays behind
+// UPR_MAXPOOL_BWD_SCATTER=1 for A/B timing):
+//  1. per output element the window position of its max, PyTorch's rule
+//     (max_pool2d CPU kernel: the first in-bounds tap, then every tap with
+//     v > max or v NaN), as a byte code ky * k + kx;
+//  2. per input element, in output order, the dy of every window whose code
+//     points at it, added to dx.
+extern "C++" {
+template <int VEC>
+__global__ void maxpool_arg_kernel(V x, int B, int H, int W, int C, int k, int s, int p, int Ho, int Wo,
+                                   unsigned char* __restrict__ code) {
+  const int CV = C / VEC;
+  const long long n = (long long)B * Ho * Wo * CV;
+  GSTRIDE(i, n) {
+    const int c = (int)(i % CV) * VEC;
+    long long r = i / CV;
+    const int ox = (int)(r % Wo); r /= Wo;
+    const int oy = (int)(r % Ho);
+    const int b = (int)(r / Ho);
+    float m[VEC];
+    int best[VEC];
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) { m[v] = -INFINITY; best[v] = -1; }
+    for (int ky = 0; ky < k; ++ky) {
+      const int iy = oy * s - p + ky;
+      if (iy < 0 || iy >= H) continue;
+      for (int kx = 0; kx < k; ++kx) {
+        const int ix = ox * s - p + kx;
+        if (ix < 0 || ix >= W) continue;
+        float val[VEC];
+        if constexpr (VEC == 4) {
+          const float4 q = *(const float4*)(x.d + x.at(b, iy, ix, c));
+          val[0] = q.x; val[1] = q.y; val[2] = q.z; val[3] = q.w;
+        } else {
+          val[0] = x.d[x.at(b, iy, ix, c)];
+        }
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) {
+          if (best[v] < 0) best[v] = ky * k + kx;  // the first in-bounds tap is the default index
+          if (val[v] > m[v] || isnan(val[v])) {
+            m[v] = val[v];
+            best[v] = ky * k + kx;
+          }
+        }
+      }
+    }
+    unsigned char* o = code + (((long long)b * Ho + oy) * Wo + ox) * C + c;
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) o[v] = (unsigned char)(best[v] < 0 ? 255 : best[v]);
+  }
+}
+
+template <int VEC>
+__global__ void maxpool_bwd_gather_kernel(const unsigned char* __restrict__ code, V dy, int B, int H, int W, int C, int k,
+                                          int s, int p, int Ho, int Wo, V dx) {
+  const int CV = C / VEC;
+  const long long n = (long long)B * H * W * CV;
+  GSTRIDE(i, n) {
+    const int c = (int)(i % CV) * VEC;
+    long long r = i / CV;
+    const int ix = (int)(r % W); r /= W;
+    const int iy = (int)(r % H);
+    const int b = (int)(r / H);
+    float* dp = dx.d + dx.at(b, iy, ix, c);
+    float acc[VEC];
+    if constexpr (VEC == 4) {
+      const float4 q = *(const float4*)dp;
+      acc[0] = q.x; acc[1] = q.y; acc[2] = q.z; acc[3] = q.w;
+    } else {
+      acc[0] = *dp;
+    }
+    // windows containing (iy, ix): oy*s - p <= iy <= oy*s - p + k - 1
+    const int oy0 = max(0, (iy + p - k + 1 + s - 1 + s * k) / s - k), oy1 = min(Ho - 1, (iy + p) / s);
+    const int ox0 = max(0, (ix + p - k + 1 + s - 1 + s * k) / s - k), ox1 = min(Wo - 1, (ix + p) / s);
+    for (int oy = oy0; oy <= oy1; ++oy) {
+      const int ty = iy - (oy * s - p);
+      if (ty < 0 || ty >= k) continue;
+      for (int ox = ox0; ox <= ox1; ++ox) {
+        const int tx = ix - (ox * s - p);
+        if (tx < 0 || tx >= k) continue;
+        const unsigned char want = (unsigned char)(ty * k + tx);
+        const unsigned char* cd = code + (((long long)b * Ho + oy) * Wo + ox) * C + c;
+        const float* g = dy.d + dy.at(b, oy, ox, c);
+#pragma unroll
+        for (int v = 0; v < VEC; ++v)
+          if (cd[v] == want) acc[v] += g[v * dy.sc];
+      }
+    }
+    if constexpr (VEC == 4) {
+      *(float4*)dp = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    } else {
+      *dp = acc[0];
+    }
+  }
+}
+
+}  // extern "C++"
+
 int upr_t_maxpool_bwd(const UprView* x, const UprView* dy, int B, int H, int W, int C, int k, int s, int p, int Ho,
                       int Wo, const UprView* dx, void* stream) {
-  if (!x || !dy || !dx || k <= 0 || s <= 0) return UPR_ERR_ARG;
+  if (!x || !dy || !dx || k <= 0 || s <= 0 || k * k > 255) return UPR_ERR_ARG;
+  hipStream_t st = ST(stream);
   const long long n = (long long)B * Ho * Wo * C;
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), mkv(x), mkv(dy), B, H, W, C, k,
-                     s, p, Ho, Wo, mkv(dx));
-  LAUNCH_CHECK();
+  if (getenv("UPR_MAXPOOL_BWD_SCATTER")) {
+    hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, st, mkv(x), mkv(dy), B, H, W, C, k, s, p,
+                       Ho, Wo, mkv(dx));
+    LAUNCH_CHECK();
+  }
+  void* code = nullptr;
+  UPR_CHECK_HIP(hipMallocAsync(&code, (size_t)n, st));
+  const bool v4 = C % 4 == 0 && x->sc == 1 && dx->sc == 1 && (uintptr_t)x->data % 16 == 0 &&
+                  (uintptr_t)dx->data % 16 == 0 && x->sw % 4 == 0 && x->sh % 4 == 0 && x->sb % 4 == 0 &&
+                  dx->sw % 4 == 0 && dx->sh % 4 == 0 && dx->sb % 4 == 0;
+  const long long ni = (long long)B * H * W * C;
+  if (v4) {
+    hipLaunchKernelGGL(maxpool_arg_kernel<4>, dim3(grid_for(n / 4)), dim3(256), 0, st, mkv(x), B, H, W, C, k, s, p, Ho,
+                       Wo, (unsigned char*)code);
+    hipLaunchKernelGGL(maxpool_bwd_gather_kernel<4>, dim3(grid_for(ni / 4)), dim3(256), 0, st,
+                       (const unsigned char*)code, mkv(dy), B, H, W, C, k, s, p, Ho, Wo, mkv(dx));
+  } else {
+    hipLaunchKernelGGL(maxpool_arg_kernel<1>, dim3(grid_for(n)), dim3(256), 0, st, mkv(x), B, H, W, C, k, s, p, Ho, Wo,
+                       (unsigned char*)code);
+    hipLaunchKernelGGL(maxpool_bwd_gather_kernel<1>, dim3(grid_for(ni)), dim3(256), 0, st, (const unsigned char*)code,
+                       mkv(dy), B, H, W, C, k, s, p, Ho, Wo, mkv(dx));
+  }
+  UPR_CHECK_HIP(hipGetLastError());
+  UPR_CHECK_HIP(hipFreeAsync(code, st));
+  return UPR_OK;
 }
 
 int upr_t_bilinear(const UprView* x, int B, int H, int W, int C, const UprView* y, int Ho, int Wo, int accumulate,

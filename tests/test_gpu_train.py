@@ -117,6 +117,50 @@ def test_conv_wgrad16_vs_fp64(B, cin, cout, H, W, k, s, p, d):
         _close(dw, ref, 1e-4, f"wgrad16 x16={use_x16}")
 
 
+@pytest.mark.parametrize("B,C,H,W,k,s,p,nchw", [
+    (2, 32, 40, 56, 3, 1, 1, False),  # EnhancedFAM branch2 max-pool (vectorised path)
+    (2, 3, 64, 48, 2, 2, 0, True),    # scale2 MaxPool2d(2) on the NCHW input (scalar path)
+    (1, 3, 64, 64, 4, 4, 0, True),    # scale3 MaxPool2d(4)
+])
+def test_maxpool_bwd_matches_torch(B, C, H, W, k, s, p, nchw):
+    """upr_t_maxpool_bwd (argmax codes + deterministic gather) vs torch CPU
+    max_pool2d backward, with many ties (values on a 0.25 grid: PyTorch's rule,
+    the first maximal tap in window order, decides them) and one NaN window;
+    dx is accumulated into (+= like the scatter form)."""
+    import torch.nn.functional as F
+    from upr import _lib as L
+    torch.manual_seed(5)
+    x = (torch.randn(B, C, H, W) * 2).round() / 4
+    x[0, 0, 5, 7] = float("nan")
+    xr = x.clone().requires_grad_(True)
+    y = F.max_pool2d(xr, k, s, p)
+    gy = torch.randn(y.shape)
+    y.backward(gy)
+    base = torch.randn(B, C, H, W)
+    ref = xr.grad + base
+    Ho, Wo = y.shape[2], y.shape[3]
+    if nchw:
+        xd, gyd, dxd = x.to(DEV).contiguous(), gy.to(DEV).contiguous(), base.to(DEV).contiguous()
+        vx = L.UprView(xd.data_ptr(), C * H * W, W, 1, H * W)
+        vg = L.UprView(gyd.data_ptr(), C * Ho * Wo, Wo, 1, Ho * Wo)
+        vd = L.UprView(dxd.data_ptr(), C * H * W, W, 1, H * W)
+    else:
+        xd, gyd = x.permute(0, 2, 3, 1).contiguous().to(DEV), gy.permute(0, 2, 3, 1).contiguous().to(DEV)
+        dxd = base.permute(0, 2, 3, 1).contiguous().to(DEV)
+        vx = L.UprView(xd.data_ptr(), H * W * C, W * C, C, 1)
+        vg = L.UprView(gyd.data_ptr(), Ho * Wo * C, Wo * C, C, 1)
+        vd = L.UprView(dxd.data_ptr(), H * W * C, W * C, C, 1)
+    import ctypes
+    st = torch.cuda.current_stream().cuda_stream
+    assert L.lib().upr_t_maxpool_bwd(ctypes.byref(vx), ctypes.byref(vg), B, H, W, C, k, s, p, Ho, Wo,
+                                     ctypes.byref(vd), st) == 0
+    torch.cuda.synchronize()
+    out = dxd.cpu() if nchw else dxd.permute(0, 3, 1, 2).cpu()
+    assert torch.equal(torch.isnan(out), torch.isnan(ref))
+    m = ~torch.isnan(ref)
+    assert (out[m] - ref[m]).abs().max().item() <= 1e-6 * max(1.0, ref[m].abs().max().item())  # summation order
+
+
 def test_convT_layer():
     from upr.train import Act, ConvT
     torch.manual_seed(1)
