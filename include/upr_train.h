@@ -121,6 +121,11 @@ int upr_t_bn_eval_stats(const float* running_mean, const float* running_var, int
 int upr_t_bn_apply(const float* x, int M, int C, int x_cs, int x_coff, const float* mean, const float* invstd,
                    const float* gamma, const float* beta, const float* res, int res_cs, int res_coff, int res_post,
                    int relu, float* y, int y_cs, int y_coff, void* stream);
+/* upr_t_bn_apply that also writes y16[m][C] = (fp16) y (compact, nullable): the
+ * autocast conv consuming y reads it instead of casting y again. */
+int upr_t_bn_apply16(const float* x, int M, int C, int x_cs, int x_coff, const float* mean, const float* invstd,
+                     const float* gamma, const float* beta, const float* res, int res_cs, int res_coff, int res_post,
+                     int relu, float* y, int y_cs, int y_coff, void* y16, void* stream);
 /* acc[2C] (zeroed) += (sum g, sum g*xhat) per channel. */
 int upr_t_bn_bwd_reduce(const float* g, int g_cs, int g_coff, const float* x, int x_cs, int x_coff, const float* mean,
                         const float* invstd, int M, int C, double* acc, void* stream);

@@ -548,6 +548,40 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
   }
 }
 
+// the same arithmetic, 4 channels per thread (16-byte loads / stores), and
+// optionally the compact fp16 copy y16[m][C] the next autocast conv reads
+__global__ __launch_bounds__(256) void bn_apply4_kernel(const float* __restrict__ x, int M, int C, int x_cs, int x_coff,
+                                                        const float* __restrict__ mean,
+                                                        const float* __restrict__ invstd,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, const float* res, int res_cs,
+                                                        int res_coff, int res_post, int relu, float* y, int y_cs,
+                                                        int y_coff, half_t* __restrict__ y16) {
+  const int C4 = C / 4;
+  const long long n = (long long)M * C4;
+  GSTRIDE(i, n) {
+    const int c = (int)(i % C4) * 4;
+    const long long m = i / C4;
+    const float4 xv = *(const float4*)(x + m * x_cs + x_coff + c);
+    const float4 rv4 = res ? *(const float4*)(res + m * res_cs + res_coff + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float xa[4] = {xv.x, xv.y, xv.z, xv.w}, ra[4] = {rv4.x, rv4.y, rv4.z, rv4.w};
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float v = (xa[e] - mean[c + e]) * invstd[c + e] * gamma[c + e] + beta[c + e];
+      if (!res_post) v += ra[e];
+      if (relu) v = fmaxf(v, 0.f);
+      if (res_post) v += ra[e];
+      o[e] = v;
+    }
+    *(float4*)(y + m * y_cs + y_coff + c) = make_float4(o[0], o[1], o[2], o[3]);
+    if (y16) {
+      typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+      *(h4*)(y16 + m * C + c) = h4{(half_t)o[0], (half_t)o[1], (half_t)o[2], (half_t)o[3]};
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restrict__ g, int g_cs, int g_coff,
                                                            const float* __restrict__ x, int x_cs, int x_coff,
                                                            const float* __restrict__ mean,
@@ -1786,14 +1820,32 @@ int upr_t_bn_eval_stats(const float* running_mean, const float* running_var, int
   LAUNCH_CHECK();
 }
 
-int upr_t_bn_apply(const float* x, int M, int C, int x_cs, int x_coff, const float* mean, const float* invstd,
-                   const float* gamma, const float* beta, const float* res, int res_cs, int res_coff, int res_post,
-                   int relu, float* y, int y_cs, int y_coff, void* stream) {
+int upr_t_bn_apply16(const float* x, int M, int C, int x_cs, int x_coff, const float* mean, const float* invstd,
+                     const float* gamma, const float* beta, const float* res, int res_cs, int res_coff, int res_post,
+                     int relu, float* y, int y_cs, int y_coff, void* y16, void* stream) {
   if (!x || !y || !mean || !invstd || !gamma || !beta) return UPR_ERR_ARG;
+  const auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  const bool v4 = C % 4 == 0 && x_cs % 4 == 0 && x_coff % 4 == 0 && y_cs % 4 == 0 && y_coff % 4 == 0 && a16(x) &&
+                  a16(y) && (!res || (res_cs % 4 == 0 && res_coff % 4 == 0 && a16(res))) &&
+                  (!y16 || ((uintptr_t)y16 & 7) == 0);
+  if (v4) {
+    const long long n4 = (long long)M * (C / 4);
+    hipLaunchKernelGGL(bn_apply4_kernel, dim3(grid_for(n4)), dim3(256), 0, ST(stream), x, M, C, x_cs, x_coff, mean,
+                       invstd, gamma, beta, res, res_cs, res_coff, res_post, relu, y, y_cs, y_coff, (half_t*)y16);
+    LAUNCH_CHECK();
+  }
+  if (y16) return UPR_ERR_ARG;  // the fp16 copy needs the vectorised layout
   const long long n = (long long)M * C;
   hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), x, M, C, x_cs, x_coff, mean,
                      invstd, gamma, beta, res, res_cs, res_coff, res_post, relu, y, y_cs, y_coff);
   LAUNCH_CHECK();
+}
+
+int upr_t_bn_apply(const float* x, int M, int C, int x_cs, int x_coff, const float* mean, const float* invstd,
+                   const float* gamma, const float* beta, const float* res, int res_cs, int res_coff, int res_post,
+                   int relu, float* y, int y_cs, int y_coff, void* stream) {
+  return upr_t_bn_apply16(x, M, C, x_cs, x_coff, mean, invstd, gamma, beta, res, res_cs, res_coff, res_post, relu, y,
+                          y_cs, y_coff, nullptr, stream);
 }
 
 int upr_t_bn_bwd_reduce(const float* g, int g_cs, int g_coff, const float* x, int x_cs, int x_coff, const float* mean,

@@ -114,6 +114,7 @@ SIGNATURES.update({
     "upr_t_bn_finalize": (_i, [_p, _i, _i, _f, _f, _p, _p, _p, _p, _p, _p]),
     "upr_t_bn_eval_stats": (_i, [_p, _p, _i, _f, _p, _p, _p]),
     "upr_t_bn_apply": (_i, [_p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _i, _i, _p]),
+    "upr_t_bn_apply16": (_i, [_p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _i, _i, _p, _p]),
     "upr_t_bn_bwd_reduce": (_i, [_p, _i, _i, _p, _i, _i, _p, _p, _i, _i, _p, _p]),
     "upr_t_bn_bwd_apply": (_i, [_p, _i, _i, _p, _i, _i, _p, _p, _p, _p, _i, _i, _p, _p, _p, _i, _i, _i, _p]),
     "upr_t_chan_sum": (_i, [_p, _i, _i, _i, _i, _p, _i, _p]),

@@ -85,6 +85,7 @@ class Act:
         self.C = self.cs if C is None else C
         self.coff = coff
         self.fresh = False
+        self.t16 = None  # compact fp16 copy written by its producer (autocast conv input), or None
 
     @staticmethod
     def new(B, H, W, C, dev, fresh=True):
@@ -217,16 +218,19 @@ class Conv:
             _chk(lib.upr_t_cast_f16(_p(self.wp), _p(self.wp16), w.numel(), st), "cast_w")
             _chk(lib.upr_t_cast_f16(_p(self.wt), _p(self.wt16), w.numel(), st), "cast_w")
 
-    def _mfma16(self, x, B, H, W, C, cs, coff, w16, bias, N, kh, kw, s, p, d, res, relu, out, store=0):
-        """fp16 MFMA conv with fp32 in / out (upr_t_conv_mfma16); res: Act or None."""
+    def _mfma16(self, x, B, H, W, C, cs, coff, w16, bias, N, kh, kw, s, p, d, res, relu, out, store=0, x16=None):
+        """fp16 MFMA conv with fp32 in / out (upr_t_conv_mfma16); res: Act or None; x16: the
+        input's compact fp16 copy when its producer already wrote it."""
         Ho = (H + 2 * p - d * (kh - 1) - 1) // s + 1
         Wo = (W + 2 * p - d * (kw - 1) - 1) // s + 1
         dev = x.device
-        x16 = _h16(B * H * W * C, dev)
+        ready = x16 is not None
+        if not ready:
+            x16 = _h16(B * H * W * C, dev)
         y16 = _h16(B * Ho * Wo * N, dev)
         _chk(L.lib().upr_t_conv_mfma16(_fp(x, 0), B, H, W, C, cs, coff, _p(w16), _p(bias), N, kh, kw, s, p, d,
                                        res.ptr() if res is not None else None, res.cs if res is not None else 0,
-                                       int(relu), _fp(out.t), out.cs, out.coff, store, _p(x16), 0, _p(y16),
+                                       int(relu), _fp(out.t), out.cs, out.coff, store, _p(x16), int(ready), _p(y16),
                                        _stream()), "conv_mfma16")
         return x16
 
@@ -244,8 +248,9 @@ class Conv:
         self.amp = _AMP[0] and self.mfma and x_view is None
         if self.amp:
             # the fp16 copy of x is the weight gradient's B operand (upr_t_conv_wgrad16)
+            t16 = x.t16 if x.coff == 0 and x.C == x.cs == self.Cin else None
             x16 = self._mfma16(x.t, B, H, W, self.Cin, x.cs, x.coff, self.wp16, self.bias, self.Cout, self.kh,
-                               self.kw, self.s, self.p, self.d, res, relu, out)
+                               self.kw, self.s, self.p, self.d, res, relu, out, x16=t16)
             self.x16 = None if self.frozen else x16
         elif self.mfma and x_view is None:
             _chk(lib.upr_t_conv_mfma(_fp(x.t), B, H, W, self.Cin, x.cs, x.coff, _p(self.wp),
@@ -414,9 +419,12 @@ class BN:
                                          _p(self.mean), _p(self.invstd), st), "bn_eval_stats")
         if out is None:
             out = Act.new(x.B, x.H, x.W, self.C, x.t.device, fresh=False)
-        _chk(lib.upr_t_bn_apply(x.ptr(), x.M, self.C, x.cs, 0, _p(self.mean), _p(self.invstd), _p(m.weight),
-                                _p(m.bias), res.ptr() if res is not None else None, res.cs if res is not None else 0,
-                                0, int(res_post), int(relu), _fp(out.t), out.cs, out.coff, st), "bn_apply")
+        # under autocast the consumer is an fp16 conv: write its fp16 input copy here
+        y16 = _h16(out.M * self.C, out.t.device) if _AMP[0] and out.coff == 0 and out.cs == self.C else None
+        _chk(lib.upr_t_bn_apply16(x.ptr(), x.M, self.C, x.cs, 0, _p(self.mean), _p(self.invstd), _p(m.weight),
+                                  _p(m.bias), res.ptr() if res is not None else None, res.cs if res is not None else 0,
+                                  0, int(res_post), int(relu), _fp(out.t), out.cs, out.coff, _p(y16), st), "bn_apply")
+        out.t16 = y16
         self.x = x
         return out
 

@@ -1,4 +1,4 @@
-# deterministic max-pool backward: tests + AMP train bench
+# training GPU tests (train + modules) and the AMP train bench
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/sh16
 timeout -k 10 600 python -u -m pytest tests/test_gpu_train.py tests/test_gpu_modules.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/sh16/tests.log 2>&1
