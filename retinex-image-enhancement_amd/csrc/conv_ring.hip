@@ -1187,6 +1187,8 @@ int launch_conv_ring(const ConvOp& op, hipStream_t st) {
     if (ring_wide() && op.Wo >= 48) return ring_relu<kRingConv, 32, 32, kRingWide>(op, st);
     return ring_occ3() ? ring_relu<kRingConv, 32, 32, kRingOcc3>(op, st) : ring_relu<kRingConv, 32, 32, 0>(op, st);
   }
+  // (64-pixel strips do not fit here: a 32 -> 64 filter in registers spills, the
+  // 64 -> 64 ring + LDS filter needs 209 KB)
   if (s.C == 32 && op.N == 64) return res ? ring_relu<kRingConv, 32, 64, kRingRes>(op, st) : ring_relu<kRingConv, 32, 64, 0>(op, st);
   if (s.C == 64 && op.N == 64) return res ? ring_relu<kRingConv, 64, 64, kRingRes>(op, st) : ring_relu<kRingConv, 64, 64, 0>(op, st);
   return kErrUnsupported;

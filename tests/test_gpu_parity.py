@@ -72,6 +72,7 @@ CONV_CASES = [
     # 64-pixel strips (32 -> 32, W >= 48): partial last strip, residual / ReLU
     (2, 20, 100, 32, 32, 3, 1, 1, 1, False, True),
     (1, 33, 150, 32, 32, 3, 1, 1, 1, True, False),
+    (2, 20, 100, 64, 64, 3, 1, 1, 1, True, False),   # 64 -> 64, several 32-pixel strips
     # row-ring stride-2 (enc1.conv1 shape class): de-interleaved ring rows, partial strips
     (2, 36, 70, 32, 64, 3, 2, 1, 1, True, False),
     (1, 64, 128, 32, 64, 3, 2, 1, 1, False, False),

@@ -24,6 +24,7 @@ SHAPES = {
     "fam64": (32, 512, 512, 64, 32, 3, 1, 1, 1, False),   # FAM fusion-like 32-wide GEMM, K = 576
     "fam_h": (32, 512, 512, 32, 64, 3, 1, 1, 1, False),   # FAM branch3/4 conv1 fused, N=64
     "dec2": (32, 256, 256, 64, 64, 3, 1, 1, 1, True),
+    "dec2p": (32, 256, 256, 64, 64, 3, 1, 1, 1, False),  # dec2.conv.0-like (ReLU, no residual)
     "dec3": (32, 128, 128, 128, 128, 3, 1, 1, 1, True),
     "bneck": (32, 64, 64, 256, 256, 3, 1, 1, 1, False),
     "enc1s2": (32, 512, 512, 32, 64, 3, 2, 1, 1, False),
