@@ -423,6 +423,65 @@ def test_train_grads_variants_vs_oracle(pre, aspp):
         assert dev_err <= tol, f"grad {n}: device |d| {dev_err:.3e} vs fp64 > {tol:.3e} (fp32 CPU |d| {cpu_err:.3e})"
 
 
+@pytest.mark.parametrize("pre", [False, True])
+def test_train_grads_b8_vs_fp64(pre):
+    """The no-ASPP variants at B = 8, 64x64 against the fp64 oracle, per
+    parameter tensor, with the per-tensor fp32 CPU oracle as the yardstick and
+    NO network-wide floor: device rel-L2 <= max(4 x the fp32 oracle's, 2e-3),
+    max|d| <= max(4 x the fp32 oracle's, 2e-2 x max|g|).  Both are fp32 with
+    different reduction orders; the largest rel-L2 ratio seen on MI355X is 2.4x
+    (enc1.bn1.weight 5.0e-3 vs 2.3e-3, dec2.conv.0.weight 3.8e-3 vs 1.6e-3:
+    the tensors deepest in the backward pass carry the most accumulated
+    rounding); single elements are noisier (dec2.conv.3.weight 1.4e-2 of
+    max|g| vs 1.8e-3 on the CPU, dec3.conv.3.weight 3.1e-2 vs 2.1e-2)."""
+    from oracle import net as onet
+    from oracle import train as otrain
+    from losses.loss import TotalLoss
+    B = 8
+    model = _model(pre, False, seed=4)
+    sd_cpu = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    model = model.to(DEV).train()
+    crit = TotalLoss(use_freq_loss=True).to(DEV)
+    x = torch.rand(B, 3, 64, 64, generator=torch.Generator().manual_seed(6)) * 0.6
+    enh, refl, illu = model(x.to(DEV))
+    total, d = crit(x.to(DEV), enh, illu, refl)
+    total.backward()
+    torch.cuda.synchronize()
+    names = otrain.param_names(sd_cpu)
+    vgg = otrain.vgg19_state(VGG_SEED)
+
+    def oracle(dt):
+        s2 = {k: (v.to(dt) if v.is_floating_point() else v.clone()) for k, v in sd_cpu.items()}
+        params = {k: s2[k].clone().requires_grad_(True) for k in names}
+        work = dict(s2)
+        work.update(params)
+        with otrain.train_mode():
+            e_r, r_r, i_r = onet.forward(work, x.to(dt), pre, False)
+        t_r, d_r = otrain.total_loss({k: v.to(dt) for k, v in vgg.items()}, x.to(dt), e_r, i_r, r_r)
+        t_r.backward()
+        return d_r, {k: params[k].grad.double() for k in names}
+
+    d64, g64 = oracle(torch.float64)
+    _, g32 = oracle(torch.float32)
+    np.testing.assert_allclose(d["total"], d64["total"], rtol=1e-4)
+    dev_params = dict(model.named_parameters())
+    gmax = max(v.abs().max().item() for v in g64.values())
+    worst = (0.0, 0.0)
+    for n in names:
+        ref = g64[n]
+        if ref.abs().max().item() < 1e-9 * gmax:
+            continue  # BN-fed conv bias: zero true gradient
+        dev = dev_params[n].grad.double().cpu()
+        rn, rm = ref.norm().item(), ref.abs().max().item()
+        l2, l2c = (dev - ref).norm().item() / rn, (g32[n] - ref).norm().item() / rn
+        mx, mxc = (dev - ref).abs().max().item(), (g32[n] - ref).abs().max().item()
+        worst = max(worst, (l2, l2c))
+        print(f"{n}: rel-L2 dev {l2:.3e} cpu32 {l2c:.3e}; max|d| dev {mx / rm:.3e} cpu32 {mxc / rm:.3e} (of max|g|)")
+        assert l2 <= max(4.0 * l2c, 2e-3), f"grad {n}: rel-L2 {l2:.3e} (fp32 CPU {l2c:.3e})"
+        assert mx <= max(4.0 * mxc, 2e-2 * rm), f"grad {n}: max|d| {mx:.3e} (fp32 CPU {mxc:.3e})"
+    print(f"pre={pre}: worst (device, fp32 CPU) rel-L2 vs fp64 {worst}")
+
+
 def _amp_setup(seed=0):
     from losses.loss import TotalLoss
     from trainers.train import make_optimizer
