@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events")
     ap.add_argument("--breakdown", action="store_true", help="print per-layer stats to stderr")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC traffic passes")
+    ap.add_argument("--ceilings", action="store_true",
+                    help="after the timed steps, measure the chip's reachable fp16 MFMA and HBM-copy rates "
+                         "(upr/calib.py, ~5 s) and report the roofline fractions against them as well")
     ap.add_argument("--train", action="store_true",
                     help="configs[4]: one training step (fwd + TotalLoss + bwd + clip + Adam) per step, "
                          "bs=8 512x512 plain model (batch/size overridable)")
@@ -449,6 +452,20 @@ def main():
                                    f"{n_hbm} of {len(gemm)} conv ops are HBM-bound at {args.precision}",
             "ref_equiv_tflops": REF_GFLOP_PER_IMG[args.variant] * (S / 512) ** 2 * total_imgs / world / elapsed / 1e3,
         }
+        if args.ceilings:
+            from upr.calib import measure
+            cz = measure(dev)
+            # fp32 MFMA: MI355X_MICROARCH.md's measured 155 TF (99% of nominal), not re-measured here
+            mf = cz["mfma_f16_TF"] if args.precision == "fp16" else 155.0
+            hb = cz["hbm_copy_TBps"] * 1e3
+            t_meas = sum(max(s["flops"] / (mf * 1e12), s["bytes"] / (hb * 1e9)) for s in gemm)
+            out["roofline"]["measured_ceilings"] = {
+                "mfma_TFLOPs": mf, "hbm_GBs": hb, "detail": cz,
+                "frac_vs_measured_mfma": achieved / mf,
+                "layer_roofline_frac_vs_measured": (t_meas * 1e3) / g_ms if g_ms > 0 else None,
+                "note": "fp16: best of 1/2 waves per SIMD of back-to-back 16x16x32 MFMAs on random register "
+                        "operands after 2 s of load (DVFS-settled clock); HBM: best 16-B/lane copy of 1 GiB "
+                        "(read + write); measured in this process right after the timed steps"}
         if args.breakdown and rank == 0:
             for s in stats:
                 tf = s["flops"] / (s["ms"] * 1e-3) / 1e12 if s["ms"] else 0

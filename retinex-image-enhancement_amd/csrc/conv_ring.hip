@@ -221,7 +221,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, RingCfg<MODE, C, NB, FL
   using RA = typename K::RA;
   using RB = typename K::RB;
   constexpr bool FAM = K::FAM, HEAD = K::HEAD, S2 = K::S2, RES = K::RES, SC = K::SC;
-  constexpr int HA = K::HA, NT = K::NT, GPW = K::GPW, NWV = K::NWV;
+  constexpr int HA = K::HA, NT = K::NT, GPW = K::GPW;
   const ConvOp& op = a.op;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* Wl = smem;

@@ -292,7 +292,6 @@ __global__ __launch_bounds__(256) void wgrad16_kernel(Wg16Args a) {
   const int u1 = min(a.units, u0 + a.units_per_split);
   const int segs = a.Wo / W16_KP;
   const half_t* zero16 = (const half_t*)g_wg_zero;
-  const float* zero32 = (const float*)g_wg_zero;
 
   // A staging: chunk i of this thread = pixel tid / NQA + i * (256 / NQA), quad tid % NQA
   const int qa = tid % NQA;

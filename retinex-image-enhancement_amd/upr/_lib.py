@@ -39,6 +39,8 @@ class UprOpStat(ctypes.Structure):
 
 UPR_OP_CONV_IGEMM = 0
 UPR_OP_OTHER = 1
+UPR_CALIB_MFMA_F16 = 0
+UPR_CALIB_HBM_COPY = 1
 
 c_int, c_size_t, c_void_p, c_float = ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_float
 c_u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -74,6 +76,8 @@ SIGNATURES = {
     "upr_content_aware": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_int,
                                   c_int, c_int, c_void_p]),
     "upr_lab_tables": (None, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "upr_calib_run": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_size_t, c_int, ctypes.POINTER(c_float),
+                              c_void_p]),
 }
 
 
