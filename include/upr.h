@@ -181,8 +181,9 @@ void upr_lab_tables(uint16_t* gamma, uint16_t* cbrt, uint16_t* yf, uint16_t* inv
  *   UPR_CALIB_MFMA_F16: `iters` x 8 v_mfma_f32_16x16x32_f16 per wave on random
  *     fp16 operands held in registers (FLOPs = blocks * 4 * iters * 8 * 16384);
  *     src >= 1 MiB of fp16 (bytes), dst = blocks * 256 * 4 floats;
- *   UPR_CALIB_HBM_COPY: dst[0:bytes] = src[0:bytes], 16 B per lane, grid-stride
- *     (HBM bytes = 2 * bytes; 16-byte aligned).
+ *   UPR_CALIB_HBM_COPY: dst[0:bytes] = src[0:bytes], 16 B per lane (HBM bytes =
+ *     2 * bytes; 16-byte aligned); iters selects the access form: 0 grid-stride,
+ *     1 grid-stride non-temporal, 2 one contiguous slice per workgroup.
  * Stands in for no reference interface: the reference has no roofline. */
 enum { UPR_CALIB_MFMA_F16 = 0, UPR_CALIB_HBM_COPY = 1 };
 int upr_calib_run(int which, int blocks, int iters, const void* src, void* dst, size_t bytes, int reps,

@@ -43,10 +43,11 @@ def measure(dev, warm_s=2.0, copy_bytes=1 << 30):
         del sink
     a = torch.empty(copy_bytes, dtype=torch.uint8, device=dev).random_(0, 255, generator=g)
     b = torch.empty_like(a)
-    for blocks in (2048, 8192):
-        _run(lib, L.UPR_CALIB_HBM_COPY, blocks, 0, a, b, copy_bytes, 5, stream)
-        ms = _run(lib, L.UPR_CALIB_HBM_COPY, blocks, 0, a, b, copy_bytes, 100, stream)
-        out["hbm_copy"][f"grid_{blocks}"] = 2.0 * copy_bytes / (ms * 1e-3) / 1e12
+    for mode, name in ((0, "stride"), (1, "stride_nt"), (2, "slice")):
+        for blocks in (1024, 2048, 4096):
+            _run(lib, L.UPR_CALIB_HBM_COPY, blocks, mode, a, b, copy_bytes, 5, stream)
+            ms = _run(lib, L.UPR_CALIB_HBM_COPY, blocks, mode, a, b, copy_bytes, 50, stream)
+            out["hbm_copy"][f"{name}_grid_{blocks}"] = 2.0 * copy_bytes / (ms * 1e-3) / 1e12
     assert torch.equal(a[-4096:], b[-4096:])
     del a, b
     out["mfma_f16_TF"] = max(out["mfma_f16"].values())
