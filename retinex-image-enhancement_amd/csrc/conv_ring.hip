@@ -63,6 +63,11 @@ typedef __attribute__((address_space(3))) void* lds_void_ptr_r;
 __device__ __attribute__((aligned(256))) uint4 g_ring_zero[16];
 __device__ __attribute__((aligned(256))) uint2 g_ring_sink[512 * 16];
 __device__ __attribute__((aligned(256))) float g_ring_sink32[512 * 64];  // fp32 outputs: 256 bytes per thread
+__device__ __attribute__((aligned(256))) unsigned g_ring_ninf32[64] = {  // fp32 -inf line (16 chunks)
+#define NINF4 0xFF800000u, 0xFF800000u, 0xFF800000u, 0xFF800000u
+    NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4
+#undef NINF4
+};
 __device__ __attribute__((aligned(256))) unsigned g_ring_ninf[64] = {
 #define NINF4 0xFC00FC00u, 0xFC00FC00u, 0xFC00FC00u, 0xFC00FC00u
     NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4, NINF4
@@ -76,7 +81,16 @@ enum RingMode : int { kRingConv = 0, kRingHead = 1, kRingFam = 2, kRingS2 = 3 };
 // step for the same per-step barrier / DMA / cursor work (32 -> 32 convs)
 // kRingOut2: the epilogue also writes relu(fma(o, pre2_scale, pre2_shift)) (ConvOp::out2)
 // kRingOut32: fp32 output (ConvOp::out32, no res32) instead of the fp16 store
-enum RingFlags : int { kRingRes = 1, kRingRelu = 2, kRingSc = 4, kRingOcc3 = 8, kRingWide = 16, kRingOut2 = 32, kRingOut32 = 64 };
+// fp32 ring only: kRingDil2 = the segment is a 3x3 dilation-2 conv (2-pixel halo ring);
+// kRingResPre = the residual is ConvOp::res1 (added before the ReLU) instead of
+// res2 (after it); kRingPool = per-image channel sums of the output into ConvOp::pool
+enum RingFlags : int {
+  kRingRes = 1, kRingRelu = 2, kRingSc = 4, kRingOcc3 = 8, kRingWide = 16, kRingOut2 = 32, kRingOut32 = 64,
+  kRingDil2 = 128, kRingResPre = 256, kRingPool = 512, kRingXPool = 1024
+};
+// kRingXPool (fp32 ring): two more K slices after the 3x3 segment, a 1x1 over
+// x and a 1x1 over maxpool3x3(x) (EnhancedFAM branch1 / branch2 composed with
+// the fusion), x staged in a second ring with a -inf halo
 
 // A ring of NPL chunk planes: 4 groups of GROWS rows of RW pixels.  DEINT:
 // ring column p holds source column 2p (p < (RW+1)/2) or 2(p - (RW+1)/2) + 1.
@@ -736,17 +750,25 @@ template <int MODE, int NB, int FL>
 struct Ring32Cfg {
   static constexpr bool HEAD = MODE == kRingHead;
   static constexpr bool RES = FL & kRingRes, RELU = (FL & kRingRelu) != 0;
+  static constexpr bool RESPRE = (FL & kRingResPre) != 0, POOL = (FL & kRingPool) != 0;
+  static constexpr int DIL = (FL & kRingDil2) ? 2 : 1, HA = DIL;  // ring halo = the taps' reach
+  static constexpr bool XP = (FL & kRingXPool) != 0;
   static constexpr int C = 32, NT = NB / 16, NG = 2;
-  using RA = Ring<8, 34, 4>;                        // 32 fp32 channels = 8 chunk planes, 1-pixel halo
-  static constexpr bool WREG = NT == 2;             // 9 taps x 2 tiles x 8 floats = 144 VGPRs
+  using RA = Ring<8, 32 + 2 * HA, 4>;               // 32 fp32 channels = 8 chunk planes
+  using RB = Ring<8, 34, 4>;                        // kRingXPool: x, 1-pixel -inf halo
+  static constexpr int NSL = XP ? 11 : 9;           // K slices of 32 channels
+  static constexpr bool WREG = NT == 2;             // 9 (11) slices x 2 tiles x 8 floats = 144 (176) VGPRs
   static constexpr int WBYTES = WREG ? 0 : 9 * NB * 32 * 4;  // [tap][n][32 k] fp32
   static constexpr int EW = RES ? 32 * NB * 4 : HEAD ? 512 : 0;
   static constexpr int E = RES ? NB / 8 : HEAD ? 1 : 0;
-  static constexpr int LDS = WBYTES + RA::BYTES + 4 * EW;
-  static constexpr int G = RA::G;
+  static constexpr int LDS = WBYTES + RA::BYTES + (XP ? RB::BYTES : 0) + 4 * EW;
+  static constexpr int G = RA::G + (XP ? RB::G : 0);
   static constexpr int S = HEAD ? NG : NG * NT;
-  static constexpr int W0 = G, W1 = E + G + S, WK = 2 * S + E + G;
-  static_assert(WK <= 63, "vmcnt immediate");
+  static constexpr int W0 = G, W1 = E + G + S, WK = 2 * S + E + G, WF = WK + (POOL ? 4 * NT : 0);
+  static_assert(WF <= 63, "vmcnt immediate");
+  static_assert(!RESPRE || RES, "kRingResPre qualifies kRingRes");
+  static_assert(!(HEAD && (POOL || DIL == 2)), "head: plain 3x3");
+  static_assert(!XP || (WREG && DIL == 1 && !RES && !HEAD), "x / maxpool slices: the FAM h3 part");
 };
 
 template <int MODE, int NB, int FL>
@@ -754,7 +776,8 @@ __global__ __launch_bounds__(256) void conv_ring32_kernel(RingArgs a) {
   using K = Ring32Cfg<MODE, NB, FL>;
   using RA = typename K::RA;
   constexpr bool HEAD = K::HEAD, RES = K::RES;
-  constexpr int NT = K::NT, NG = K::NG;
+  constexpr int NT = K::NT, NG = K::NG, HA = K::HA, DIL = K::DIL;
+  using RB = typename K::RB;
   typedef float f32x4 __attribute__((ext_vector_type(4)));
   const ConvOp& op = a.op;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -763,7 +786,8 @@ __global__ __launch_bounds__(256) void conv_ring32_kernel(RingArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fg = lane >> 4;
-  unsigned char* epi = ringA + RA::BYTES + wave * K::EW;
+  unsigned char* ringB = ringA + RA::BYTES;
+  unsigned char* epi = ringA + RA::BYTES + (K::XP ? RB::BYTES : 0) + wave * K::EW;
   const int H = op.Ho, W = op.Wo;
   const ConvSeg& sa = op.seg[0];
   const int per_xcd = gridDim.x >> 3;
@@ -772,10 +796,10 @@ __global__ __launch_bounds__(256) void conv_ring32_kernel(RingArgs a) {
   const int KT = nu * a.steps;
 
   // filter: lane (fr = n within tile, fg) holds W[nt*16 + fr][tap*32 + fg*8 .. +7]
-  f32x4 wr[K::WREG ? 9 : 1][NT][2];
+  f32x4 wr[K::WREG ? K::NSL : 1][NT][2];
   if constexpr (K::WREG) {
 #pragma unroll
-    for (int t = 0; t < 9; ++t)
+    for (int t = 0; t < K::NSL; ++t)
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
@@ -793,6 +817,12 @@ __global__ __launch_bounds__(256) void conv_ring32_kernel(RingArgs a) {
   const half_t* zero = (const half_t*)g_ring_zero;
   RingLanes<RA> la;
   la.init(lane, sa.Win, csA);
+  const ConvSeg& sx = op.seg[K::XP ? 1 : 0];
+  const half_t* srcB = (const half_t*)((const float*)sx.src + sx.coff);
+  const int csB = sx.cs * 2;
+  const half_t* ninf = (const half_t*)g_ring_ninf32;
+  RingLanes<RB> lb;
+  if constexpr (K::XP) lb.init(lane, sx.Win, csB);
 
   auto unit_of = [&](int j, int& b, int& y0, int& x0) {
     const int u = v0 + j * (int)gridDim.x;
@@ -818,7 +848,9 @@ __global__ __launch_bounds__(256) void conv_ring32_kernel(RingArgs a) {
   // half offset 8c, i.e. plane c <-> chunk c of the pixel
   auto issue = [&](int k) {
     const bool live = dc.j < nu;
-    la.issue(srcA, csA, dc.b, sa.Hin, sa.Win, dc.y0 + 4 * dc.s + 1, dc.x0 - 1, live, zero, ringA, (k + 1) & 3, wave);
+    la.issue(srcA, csA, dc.b, sa.Hin, sa.Win, dc.y0 + 4 * dc.s + HA, dc.x0 - HA, live, zero, ringA, (k + 1) & 3, wave);
+    if constexpr (K::XP)
+      lb.issue(srcB, csB, dc.b, sx.Hin, sx.Win, dc.y0 + 4 * dc.s + 1, dc.x0 - 1, live, ninf, ringB, (k + 1) & 3, wave);
     advance(dc);
   };
 
@@ -839,14 +871,24 @@ __global__ __launch_bounds__(256) void conv_ring32_kernel(RingArgs a) {
       for (int i = 0; i < 4; ++i) hw2[nt][i] = op.head_w[nt * 16 + fg * 4 + i];
   }
   const int abase = 2 * fg * RA::PLANE + fr * 16;  // planes 2fg, 2fg+1 (channels fg*8 .. +7)
-  const int ocs = op.out_cs, rcs = RES ? op.res2_cs : 0;
+  const int ocs = op.out_cs, rcs = RES ? (K::RESPRE ? op.res1_cs : op.res2_cs) : 0;
+  const float* resp = RES ? (const float*)(K::RESPRE ? op.res1 : op.res2) : nullptr;
   const size_t HWs = (size_t)H * W;
+  float pool[K::POOL ? NT : 1][4];
+#pragma unroll
+  for (int nt = 0; nt < (K::POOL ? NT : 1); ++nt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pool[nt][i] = 0.f;
+  bool flushed = false;
 
   for (int kk = 0; kk < KT; ++kk) {
+    // (the previous step's pool atomics, when it ended a unit, are younger than DMA(kk) too)
     if (kk == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K::W0) : "memory");
     else if (kk == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K::W1) : "memory");
+    else if (K::POOL && flushed) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K::WF) : "memory");
     else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K::WK) : "memory");
     __builtin_amdgcn_s_barrier();
+    flushed = false;
     const int s = cc.s, b = cc.b, x0 = cc.x0;
     const int yend = min(H, cc.y0 + a.rs);
     const int y = cc.y0 + 4 * s + wave;
@@ -863,7 +905,7 @@ __global__ __launch_bounds__(256) void conv_ring32_kernel(RingArgs a) {
       for (int i = 0; i < K::E; ++i) {
         const int q = i * 64 + lane, px = q / CPP;
         const bool ok = rowok && x0 + px < W;
-        const void* p = ok ? (const void*)((const float*)op.res2 + (prow + px) * rcs + ((q % CPP) ^ ring32_res_swz<CPP>(px)) * 4)
+        const void* p = ok ? (const void*)(resp + (prow + px) * rcs + ((q % CPP) ^ ring32_res_swz<CPP>(px)) * 4)
                            : (const void*)zero;
         __builtin_amdgcn_global_load_lds(p, (lds_void_ptr_r)(epi + i * 1024), 16, 0, 0);
       }
@@ -895,7 +937,8 @@ __global__ __launch_bounds__(256) void conv_ring32_kernel(RingArgs a) {
   } while (0)
     if (s >= 0) {
       // chunk = one tap row r: 3 taps x 2 groups x 2 halves of X (+ 3 x NT x 2 of W from LDS)
-      auto rowA = [&](int r) { return ((4 * kk + 4 + wave - 1 + r - 1) & 15) * (RA::RW * 16); };
+      // ring row of tap row r (input row y + (r - 1) * DIL); ring column of tap sc below
+      auto rowA = [&](int r) { return ((4 * kk + 4 + wave - HA + (r - 1) * DIL) & 15) * (RA::RW * 16); };
       constexpr int NW = K::WREG ? 1 : 3;
       f32x4 bx[2][3][NG][2], bw[2][NW][NT][2];
       auto ld = [&](int r, f32x4 (&x)[3][NG][2], f32x4 (&w)[NW][NT][2]) {
@@ -905,7 +948,8 @@ __global__ __launch_bounds__(256) void conv_ring32_kernel(RingArgs a) {
 #pragma unroll
           for (int g = 0; g < NG; ++g)
 #pragma unroll
-            for (int h = 0; h < 2; ++h) x[sc][g][h] = *(const f32x4*)(xr + h * RA::PLANE + (g * 16 + sc) * 16);
+            for (int h = 0; h < 2; ++h)
+              x[sc][g][h] = *(const f32x4*)(xr + h * RA::PLANE + (g * 16 + HA + (sc - 1) * DIL) * 16);
         if constexpr (!K::WREG) {
 #pragma unroll
           for (int sc = 0; sc < 3; ++sc)
@@ -938,7 +982,60 @@ __global__ __launch_bounds__(256) void conv_ring32_kernel(RingArgs a) {
       RING_FENCE;
       mm(1, bx[1], bw[1]);
       RING_LDS_DONE;
-      mm(2, bx[0], bw[0]);
+      if constexpr (K::XP) {
+        // x rows y-1..y+1 of the x ring -> centre and 3x3 max per pixel group and channel half
+        const int bbase = 2 * fg * RB::PLANE + fr * 16;
+        auto rowB = [&](int dy) { return ((4 * kk + 4 + wave - 1 + dy) & 15) * (RB::RW * 16); };
+        f32x4 xr3[3][NG][2];
+#pragma unroll
+        for (int sc = 0; sc < 3; ++sc)
+#pragma unroll
+          for (int g = 0; g < NG; ++g)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+              xr3[sc][g][h] = *(const f32x4*)(ringB + bbase + rowB(-1) + h * RB::PLANE + (g * 16 + sc) * 16);
+        RING_FENCE;
+        mm(2, bx[0], bw[0]);
+        RING_LDS_DONE;
+        f32x4 ctr[NG][2], mx[NG][2];
+#pragma unroll
+        for (int g = 0; g < NG; ++g)
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            mx[g][h] = __builtin_elementwise_max(__builtin_elementwise_max(xr3[0][g][h], xr3[1][g][h]), xr3[2][g][h]);
+#pragma unroll
+        for (int dr = 1; dr < 3; ++dr) {
+#pragma unroll
+          for (int sc = 0; sc < 3; ++sc)
+#pragma unroll
+            for (int g = 0; g < NG; ++g)
+#pragma unroll
+              for (int h = 0; h < 2; ++h)
+                xr3[sc][g][h] = *(const f32x4*)(ringB + bbase + rowB(dr - 1) + h * RB::PLANE + (g * 16 + sc) * 16);
+          RING_LDS_DONE;
+#pragma unroll
+          for (int g = 0; g < NG; ++g)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              mx[g][h] = __builtin_elementwise_max(
+                  mx[g][h], __builtin_elementwise_max(__builtin_elementwise_max(xr3[0][g][h], xr3[1][g][h]), xr3[2][g][h]));
+              if (dr == 1) ctr[g][h] = xr3[1][g][h];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int g = 0; g < NG; ++g)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+              acc[nt][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[9][nt][j >> 2][j & 3], ctr[g][j >> 2][j & 3],
+                                                                acc[nt][g], 0, 0, 0);
+              acc[nt][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[10][nt][j >> 2][j & 3], mx[g][j >> 2][j & 3],
+                                                                acc[nt][g], 0, 0, 0);
+            }
+      } else {
+        mm(2, bx[0], bw[0]);
+      }
     }
 #undef RING_LDS_DONE
 #undef RING_FENCE
@@ -980,14 +1077,40 @@ __global__ __launch_bounds__(256) void conv_ring32_kernel(RingArgs a) {
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
           f32x4 v = acc[nt][g];
+          if constexpr (RES && K::RESPRE)
+            v += *(const f32x4*)(epi + (g * 16 + fr) * NB * 4 + (((nt * 4 + fg) ^ ring32_res_swz<NB / 4>(fr)) * 16));
           if constexpr (K::RELU) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) v[i] = fmaxf(v[i], 0.f);
           }
-          if constexpr (RES)
+          if constexpr (RES && !K::RESPRE)
             v += *(const f32x4*)(epi + (g * 16 + fr) * NB * 4 + (((nt * 4 + fg) ^ ring32_res_swz<NB / 4>(fr)) * 16));
+          if constexpr (K::POOL) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              if (ovalid[g]) pool[nt][i] += v[i];
+          }
           *(f32x4*)(dg + nt * 16) = v;
         }
+      }
+    }
+    // per-image channel sums, flushed at the last compute step of every unit
+    // (a unit lies in one image): one no-return atomic per (tile, channel quad)
+    if constexpr (K::POOL) {
+      if (s == a.steps - 2) {
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float v = pool[nt][i];
+            v += __shfl_xor(v, 1);
+            v += __shfl_xor(v, 2);
+            v += __shfl_xor(v, 4);
+            v += __shfl_xor(v, 8);
+            if (fr == 0) atomicAdd(op.pool + (size_t)cc.b * op.N + nt * 16 + fg * 4 + i, v);
+            pool[nt][i] = 0.f;
+          }
+        flushed = true;
       }
     }
     advance(cc);
@@ -1199,14 +1322,51 @@ static int ring32_relu(const ConvOp& op, hipStream_t st) {
   return op.relu ? launch_ring32_cfg<MODE, NB, FL | kRingRelu>(op, st) : launch_ring32_cfg<MODE, NB, FL>(op, st);
 }
 
-// fp32: stride-1 3x3 over 32 channels (-> 32 / 64, head); kErrUnsupported otherwise
+// fp32: stride-1 3x3 over 32 channels (-> 32 / 64, head), and the split
+// EnhancedFAM fusion's 3x3 parts (N 32: dilation 1 or 2, a pre-ReLU residual,
+// per-image pool sums); kErrUnsupported otherwise
 int launch_conv_ring32(const ConvOp& op, hipStream_t st) {
   if (!ring_enabled()) return kErrUnsupported;
-  if (op.Ho < 4 || op.Wo < 16 || op.nseg != 1) return kErrUnsupported;
-  if (op.res1 || op.img_bias || op.pool || op.scale || op.Kpad != 288) return kErrUnsupported;
+  if (op.Ho < 4 || op.Wo < 16) return kErrUnsupported;
   const ConvSeg& s = op.seg[0];
-  if (!ring_seg_ok(s) || s.C != 32 || s.stride != 1 || s.Hin != op.Ho || s.Win != op.Wo) return kErrUnsupported;
-  if (s.cs % 4 || s.coff % 4) return kErrUnsupported;
+  if (op.nseg == 3) {
+    // FAM fusion, h3 + x + maxpool3(x) part: conv(h3) + W1 x + W2 maxpool3(x) + bias (no ReLU)
+    const ConvSeg& x1 = op.seg[1];
+    const ConvSeg& x2 = op.seg[2];
+    if (op.Kpad != 352 || op.N != 32 || op.store != kStoreNHWC || op.relu || op.pool || op.res1 || op.res2 ||
+        op.img_bias || op.scale || op.out_cs % 4 || op.out_coff % 4)
+      return kErrUnsupported;
+    if (!ring_seg_ok(s) || s.C != 32 || s.stride != 1 || s.Hin != op.Ho || s.Win != op.Wo || s.cs % 4 || s.coff % 4)
+      return kErrUnsupported;
+    for (const ConvSeg* q : {&x1, &x2})
+      if (q->kh != 1 || q->kw != 1 || q->stride != 1 || q->pad != 0 || q->C != 32 || q->Hin != op.Ho ||
+          q->Win != op.Wo || q->src != x1.src || q->cs != x1.cs || q->coff != x1.coff)
+        return kErrUnsupported;
+    if (x1.pre != kPreNone || x2.pre != kPreMaxPool3 || x1.kbase != 288 || x2.kbase != 320 || x1.cs % 4 ||
+        x1.coff % 4 || (uintptr_t)x1.src % 16)
+      return kErrUnsupported;
+    return launch_ring32_cfg<kRingConv, 32, kRingXPool>(op, st);
+  }
+  if (op.nseg != 1) return kErrUnsupported;
+  if (op.img_bias || op.scale || op.Kpad != 288 || (op.res1 && op.res2)) return kErrUnsupported;
+  if (s.C != 32 || s.stride != 1 || s.Hin != op.Ho || s.Win != op.Wo || s.cs % 4 || s.coff % 4) return kErrUnsupported;
+  if (s.kh == 3 && s.kw == 3 && s.dil == 2 && s.pad == 2 && s.pre == kPreNone && s.kbase == 0 && s.cs % 8 == 0 &&
+      s.coff % 8 == 0 && (uintptr_t)s.src % 16 == 0) {
+    // FAM fusion, h4 part: relu(conv_d2(h4) + res1) (+ pool sums)
+    if (op.store != kStoreNHWC || op.N != 32 || op.res2 || !op.res1 || !op.relu || op.res1_cs % 4 || op.out_cs % 4 ||
+        op.out_coff % 4)
+      return kErrUnsupported;
+    return op.pool ? launch_ring32_cfg<kRingConv, 32, kRingDil2 | kRingRes | kRingResPre | kRingRelu | kRingPool>(op, st)
+                   : launch_ring32_cfg<kRingConv, 32, kRingDil2 | kRingRes | kRingResPre | kRingRelu>(op, st);
+  }
+  if (!ring_seg_ok(s)) return kErrUnsupported;
+  if (op.res1) {
+    // FAM fusion, h3 part: conv(h3) + res1 (no ReLU)
+    if (op.store != kStoreNHWC || op.N != 32 || op.relu || op.pool || op.res1_cs % 4 || op.out_cs % 4 || op.out_coff % 4)
+      return kErrUnsupported;
+    return launch_ring32_cfg<kRingConv, 32, kRingRes | kRingResPre>(op, st);
+  }
+  if (op.pool) return kErrUnsupported;
   if (op.store == kStoreHeadIllu) {
     if (op.N != 32 || op.res2 || op.illu_f16 || op.Wo % 8) return kErrUnsupported;
     return launch_ring32_cfg<kRingHead, 32, 0>(op, st);

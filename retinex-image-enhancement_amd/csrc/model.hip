@@ -249,6 +249,7 @@ enum BufId : int {
   B_IB,     // float ASPP per-image bias [B][256]
   B_ILLU32, // float illu when the model dtype is fp16 (head writes fp32 then tail reads)
   B_PA1, B_PA2, B_PA3, B_PA4,  // fp16 PreAct: materialised relu(bn1(x)) of the blocks at levels 0..3
+  B_FT,     // fp32 FAM fusion split: the partial sum between its parts (32 ch, level 0 size)
   B_COUNT
 };
 
@@ -346,6 +347,7 @@ static BufGeom buf_geom(int id, int use_aspp) {
     case B_PA2: return {64, 1, 0, 0};
     case B_PA3: return {128, 2, 0, 0};
     case B_PA4: return {256, 3, 0, 0};
+    case B_FT: return {32, 0, 0, 0};
     default: return {0, 0, 1, 0};
   }
 }
@@ -365,6 +367,21 @@ static void buf_dims(const BufGeom& g, int H, int W, int& h, int& w) {
 // (MFMA-bound there: the prologue is hidden).
 static bool preact_materialised(const UprModel* m) { return m->use_preact && m->dtype == kF16; }
 
+// fp32 EnhancedFAM fusion (K = 640, N = 32) as two launches instead of one
+// halo-kernel GEMM: y = relu(conv_d2(h4) + (conv(h3) + x-part + bias)), both on
+// the fp32 row ring with their filters in registers (the fused K = 640 filter
+// does not fit registers, and one ring with both halos and x does not fit
+// LDS); the x / maxpool3(x) 1x1 slices ride with the h3 part (second ring).
+// Same sum in a different association (fp32 rounding only).  UPR_FAM32_SPLIT=0
+// keeps the single launch (A/B timing).
+static bool fam32_split(const UprModel* m) {
+  static const int v = [] {
+    const char* e = getenv("UPR_FAM32_SPLIT");
+    return (e && atoi(e) == 0) ? 0 : 1;
+  }();
+  return v == 1 && m->dtype != kF16 && !(m->flags & UPR_MODEL_IENET_ONLY);
+}
+
 static size_t ws_layout(const UprModel* m, int B, int H, int W, size_t* offs) {
   size_t off = 0;
   const size_t elt = m->dtype == kF16 ? 2 : 4;
@@ -380,6 +397,7 @@ static size_t ws_layout(const UprModel* m, int B, int H, int W, size_t* offs) {
       bytes = (size_t)B * h * w * g.C * (g.is_f32 ? 4 : elt);
     }
     if (id >= B_PA1 && id <= B_PA4 && !preact_materialised(m)) bytes = 0;
+    if (id == B_FT && !fam32_split(m)) bytes = 0;
     if (m->flags & UPR_MODEL_IENET_ONLY) {
       const bool scale_buf = id == B_X2P || id == B_X3P || id == B_S1IN || id == B_S2IN || id == B_S3IN ||
                              (id >= B_H1 && id <= B_Q3);
@@ -642,7 +660,14 @@ struct Builder {
       for (int mm_ = 0; mm_ < C; ++mm_)
         fb[o] += F1[o * C + mm_] * bb1->v[mm_] + F2[o * C + mm_] * bb2->v[mm_] + F3[o * C + mm_] * b3b->v[mm_] +
                  F4[o * C + mm_] * b4b->v[mm_];
-    gemm(p + ".fusion", add_layer(C, sf, fb), lshift, ybuf, C, 1, -1, 0, -1, 0, kStoreNHWC, 0, k);
+    if (fam32_split(m)) {
+      std::vector<SegWeights> s3x{sf[0], sf[2], sf[3]}, s4(1, sf[1]);
+      const std::vector<double> nob;
+      gemm(p + ".fusion.h3x", add_layer(C, s3x, fb), lshift, B_FT, C, 0);
+      gemm(p + ".fusion.h4", add_layer(C, s4, nob), lshift, ybuf, C, 1, B_FT, C, -1, 0, kStoreNHWC, 0, k);
+    } else {
+      gemm(p + ".fusion", add_layer(C, sf, fb), lshift, ybuf, C, 1, -1, 0, -1, 0, kStoreNHWC, 0, k);
+    }
     // (3) channel attention, (4) mix + projection, (5) spatial attention
     Op oc;
     oc.kind = OP_FAM_CA; oc.name = p + ".channel_attention"; oc.fam = k; oc.lvl_shift = lshift;
