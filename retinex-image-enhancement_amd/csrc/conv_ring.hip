@@ -757,7 +757,10 @@ struct Ring32Cfg {
   using RA = Ring<8, 32 + 2 * HA, 4>;               // 32 fp32 channels = 8 chunk planes
   using RB = Ring<8, 34, 4>;                        // kRingXPool: x, 1-pixel -inf halo
   static constexpr int NSL = XP ? 11 : 9;           // K slices of 32 channels
-  static constexpr bool WREG = NT == 2;             // 9 (11) slices x 2 tiles x 8 floats = 144 (176) VGPRs
+  // filter in registers: 9 (11) slices x NT tiles x 8 floats = 144 (176) / 288
+  // VGPRs (one wave per SIMD: 32 -> 64 fits in 504 registers without spills;
+  // the residual variant does not)
+  static constexpr bool WREG = NT == 2 || (NT == 4 && !RES);
   static constexpr int WBYTES = WREG ? 0 : 9 * NB * 32 * 4;  // [tap][n][32 k] fp32
   static constexpr int EW = RES ? 32 * NB * 4 : HEAD ? 512 : 0;
   static constexpr int E = RES ? NB / 8 : HEAD ? 1 : 0;
