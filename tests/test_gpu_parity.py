@@ -331,10 +331,10 @@ def test_full_size_config(case):
 def test_two_streams_distinct_handles():
     """Two models (distinct handles) forwarding concurrently on two HIP streams:
     each stream gets its own workspace (upr/runtime.py _Workspace), so the
-    results equal the serial ones (include/upr.h threading rule): bit for bit
-    for the plain model; the ASPP global-pool sums are float atomics (summation
-    order varies run to run), so the ASPP model agrees to 1e-5, where a shared
-    workspace would corrupt whole activations."""
+    results equal the serial ones (include/upr.h threading rule) up to the
+    summation order of the per-image pool sums (EnhancedFAM channel attention,
+    ASPP global branch), which are float atomics: both models agree to 1e-5,
+    where a shared workspace would corrupt whole activations."""
     m1 = make_model(False, False).to(DEV)
     m2 = make_model(True, True).to(DEV)
     g = torch.Generator(device=DEV).manual_seed(13)
@@ -353,9 +353,8 @@ def test_two_streams_distinct_handles():
             with torch.cuda.stream(s2):
                 o2 = m2(x2)
     torch.cuda.synchronize()
-    for a, b in zip(o1, r1):
-        assert torch.equal(a, b)
-    for a, b in zip(o2, r2):
-        err = maxdiff(a, b)
-        print(f"two streams: preact+aspp max|d| vs serial {err:.2e}")
-        assert err <= 1e-5
+    for name, o, r in (("plain", o1, r1), ("preact+aspp", o2, r2)):
+        for a, b in zip(o, r):
+            err = maxdiff(a, b)
+            print(f"two streams: {name} max|d| vs serial {err:.2e}")
+            assert err <= 1e-5
