@@ -397,6 +397,7 @@ int launch_conv_stream(const ConvOp& op, hipStream_t st);
 int launch_conv_ring(const ConvOp& op, hipStream_t st);
 int launch_conv_ring32(const ConvOp& op, hipStream_t st);
 int launch_conv_wide32(const ConvOp& op, hipStream_t st);
+int launch_conv_t2(const ConvOp& op, hipStream_t st);
 
 // UPR_CONV_IMPL=generic forces the implicit-GEMM kernel everywhere (A/B tests);
 // default: halo-tiled kernel where the shape allows, implicit GEMM otherwise.
@@ -445,7 +446,9 @@ int launch_conv(const ConvOp& op, int dtype, hipStream_t stream) {
     if (op.seg[s].C % 32 || op.seg[s].src == nullptr) return kErrShape;
   if (conv_impl_mode() == 0) {
     if (dtype == kF16) {
-      int rc = launch_conv_wide(op, stream);
+      int rc = launch_conv_t2(op, stream);
+      if (rc != kErrUnsupported) return rc;
+      rc = launch_conv_wide(op, stream);
       if (rc != kErrUnsupported) return rc;
       rc = launch_conv_ring(op, stream);
       if (rc != kErrUnsupported) return rc;
