@@ -397,7 +397,7 @@ int launch_conv_stream(const ConvOp& op, hipStream_t st);
 int launch_conv_ring(const ConvOp& op, hipStream_t st);
 int launch_conv_ring32(const ConvOp& op, hipStream_t st);
 int launch_conv_wide32(const ConvOp& op, hipStream_t st);
-int launch_conv_t2(const ConvOp& op, hipStream_t st);
+int launch_conv_t2(const ConvOp& op, int dtype, hipStream_t st);
 
 // UPR_CONV_IMPL=generic forces the implicit-GEMM kernel everywhere (A/B tests);
 // default: halo-tiled kernel where the shape allows, implicit GEMM otherwise.
@@ -446,7 +446,7 @@ int launch_conv(const ConvOp& op, int dtype, hipStream_t stream) {
     if (op.seg[s].C % 32 || op.seg[s].src == nullptr) return kErrShape;
   if (conv_impl_mode() == 0) {
     if (dtype == kF16) {
-      int rc = launch_conv_t2(op, stream);
+      int rc = launch_conv_t2(op, dtype, stream);
       if (rc != kErrUnsupported) return rc;
       rc = launch_conv_wide(op, stream);
       if (rc != kErrUnsupported) return rc;
@@ -459,7 +459,7 @@ int launch_conv(const ConvOp& op, int dtype, hipStream_t stream) {
       // ring with its filter in registers first (measured 2.80 -> 2.53 ms at
       // 512^2 bs 32 against the wide32 tile)
       const bool ring_first = op.nseg == 1 && op.seg[0].C == 32 && op.N == 64 && !op.res1 && !op.res2;
-      int rc = ring_first ? launch_conv_ring32(op, stream) : kErrUnsupported;
+      int rc = ring_first ? launch_conv_ring32(op, stream) : launch_conv_t2(op, dtype, stream);
       if (rc != kErrUnsupported) return rc;
       rc = launch_conv_wide32(op, stream);
       if (rc != kErrUnsupported) return rc;

@@ -135,6 +135,120 @@ __global__ __launch_bounds__(256, (KC >= 256 ? 1 : 2)) void conv_t2_kernel(ConvO
   }
 }
 
+// fp32 form (v_mfma_f32_16x16x4_f32): the same streaming / staging; the k
+// order inside a pixel is permuted identically for both operands (lane group
+// fg takes channels fg*KC/4 .. +KC/4-1, so a lane's pixel operand is KC/16
+// 16-byte loads and its filter operand a contiguous run of one filter row).
+// KC 64 (dec1.up) and 128 (dec2.up): the filter slice is KC/4 x 8 floats per
+// lane (128 / 256 VGPRs).
+template <int KC, int COUT>
+__global__ __launch_bounds__(256, (KC >= 128 ? 1 : 2)) void conv_t2_f32_kernel(ConvOp op, int ngroups) {
+  using K = ConvT2Cfg<KC, COUT>;
+  constexpr int KJ = KC / 4;    // k steps of 4 (one MFMA each per n tile)
+  constexpr int KQ = KJ / 4;    // 16-byte chunks of a lane's pixel operand
+  constexpr int RSTR = COUT + 4;  // LDS stride (floats) of one output pixel (16-byte aligned)
+  constexpr int LDSW = K::ROWS * K::XS * RSTR * 4;
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) unsigned char stage[4 * LDSW];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fg = lane >> 4;
+  const int ns = wave % K::NSPLIT, team = wave / K::NSPLIT;
+  unsigned char* st = stage + wave * LDSW;
+  const ConvSeg& sg = op.seg[0];
+  const float* src = (const float*)sg.src + sg.coff;
+  const int cs = sg.cs;
+  const int H = op.Ho, W = op.Wo, gpr = W / 16;
+
+  f4 wf[K::NT][KQ];  // lane (fr, fg) of n tile nt: W[ns*128 + nt*16 + fr][fg*KJ .. +KJ-1]
+  f4 bias[K::NT];
+#pragma unroll
+  for (int nt = 0; nt < K::NT; ++nt) {
+    const int n = ns * 128 + nt * 16;
+#pragma unroll
+    for (int q = 0; q < KQ; ++q)
+      wf[nt][q] = *(const f4*)((const float*)op.W + (size_t)(n + fr) * op.Kpad + fg * KJ + q * 4);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias[nt][r] = op.bias ? op.bias[n + fg * 4 + r] : 0.f;
+  }
+  const int stride = gridDim.x * K::TEAMS;
+  int g = blockIdx.x * K::TEAMS + team;
+  auto load = [&](int gg, f4 (&x)[KQ]) {
+    if (gg < ngroups) {
+      const float* p = src + ((size_t)gg * 16 + fr) * cs + fg * KJ;
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) x[q] = *(const f4*)(p + q * 4);
+    }
+  };
+  f4 x0[KQ], x1[KQ];
+  load(g, x0);
+  for (; g < ngroups; g += stride) {
+    load(g + stride, x1);
+    f4 acc[K::NT];
+#pragma unroll
+    for (int nt = 0; nt < K::NT; ++nt) acc[nt] = bias[nt];
+#pragma unroll
+    for (int j = 0; j < KJ; ++j)
+#pragma unroll
+      for (int nt = 0; nt < K::NT; ++nt)
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[nt][j >> 2][j & 3], x0[j >> 2][j & 3], acc[nt], 0, 0, 0);
+#pragma unroll
+    for (int nt = 0; nt < K::NT; ++nt) {
+      const int nl = nt * 16 + fg * 4;
+      const int ql = nl / COUT, co = nl % COUT;
+      const int row = ql >> 1, xs = K::QPW >= 2 ? 2 * fr + (ql & 1) : fr;
+      f4 o = acc[nt];
+      if (op.relu) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = fmaxf(o[r], 0.f);
+      }
+      *(f4*)(st + ((row * K::XS + xs) * RSTR + co) * 4) = o;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int b = g / (H * gpr), rem = g - b * H * gpr, y = rem / gpr, xg = (rem - y * gpr) * 16;
+    const int q0 = ns * K::QPW, dy0 = q0 >> 1;
+    constexpr int CPP = COUT / 4;
+    constexpr int CHUNKS = K::ROWS * K::XS * CPP;
+#pragma unroll
+    for (int i = 0; i < CHUNKS / 64; ++i) {
+      const int c = i * 64 + lane;
+      const int row = c / (K::XS * CPP), xs = (c / CPP) % K::XS, part = c % CPP;
+      const int xo = K::QPW >= 2 ? 2 * xg + xs : 2 * (xg + xs) + (q0 & 1);
+      const f4 v = *(const f4*)(st + ((row * K::XS + xs) * RSTR + part * 4) * 4);
+      float* dst = (float*)op.out + ((size_t)(b * 2 * H + 2 * y + dy0 + row) * (2 * W) + xo) * op.out_cs +
+                   op.out_coff + part * 4;
+      *(f4*)dst = v;
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) x0[q] = x1[q];
+  }
+}
+
+template <int KC, int COUT>
+static int launch_t2_f32(const ConvOp& op, hipStream_t st) {
+  static int occ = 0;
+  if (!occ) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)conv_t2_f32_kernel<KC, COUT>, 256, 0) !=
+            hipSuccess ||
+        occ < 1)
+      occ = 1;
+  }
+  int cus = 256;
+  {
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  }
+  const int ngroups = op.B * op.Ho * (op.Wo / 16);
+  const int teams = ConvT2Cfg<KC, COUT>::TEAMS;
+  int grid = std::min(cus * occ, (ngroups + teams - 1) / teams);
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL((conv_t2_f32_kernel<KC, COUT>), dim3(grid), dim3(256), 0, st, op, ngroups);
+  return (int)hipGetLastError();
+}
+
 template <int KC, int COUT>
 static int launch_t2(const ConvOp& op, hipStream_t st) {
   static int occ = 0;
@@ -157,9 +271,9 @@ static int launch_t2(const ConvOp& op, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-// fp16 ConvT 2x2 ops this kernel takes; kErrUnsupported otherwise.
+// ConvT 2x2 ops these kernels take; kErrUnsupported otherwise.
 // UPR_CONVT_STREAM=0 leaves them on the tile kernels (A/B timing).
-int launch_conv_t2(const ConvOp& op, hipStream_t st) {
+int launch_conv_t2(const ConvOp& op, int dtype, hipStream_t st) {
   static const int en = [] {
     const char* e = getenv("UPR_CONVT_STREAM");
     return (e && atoi(e) == 0) ? 0 : 1;
@@ -172,6 +286,12 @@ int launch_conv_t2(const ConvOp& op, hipStream_t st) {
     return kErrUnsupported;
   if (op.out_cs % 8 || op.out_coff % 8 || (uintptr_t)op.out % 16 || (uintptr_t)op.W % 16 || op.Kpad % 8)
     return kErrUnsupported;
+  if (dtype != kF16) {
+    if (s.cs % 4 || s.coff % 4 || op.out_cs % 4 || op.out_coff % 4) return kErrUnsupported;
+    if (s.C == 64 && op.N == 128) return launch_t2_f32<64, 32>(op, st);
+    if (s.C == 128 && op.N == 256) return launch_t2_f32<128, 64>(op, st);
+    return kErrUnsupported;
+  }
   if (s.C == 64 && op.N == 128) return launch_t2<64, 32>(op, st);
   if (s.C == 128 && op.N == 256) return launch_t2<128, 64>(op, st);
   if (s.C == 256 && op.N == 512) return launch_t2<256, 128>(op, st);
