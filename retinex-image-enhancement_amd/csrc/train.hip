@@ -610,9 +610,67 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
   }
 }
 
+// the same arithmetic, 4 channels per thread (16-byte loads / stores)
+__global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(const float* __restrict__ g, int g_cs, int g_coff,
+                                                            const float* __restrict__ x, int x_cs, int x_coff,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ invstd,
+                                                            const float* __restrict__ gamma,
+                                                            const double* __restrict__ acc, int M, int C,
+                                                            float* dgamma, float* dbeta, float* dx, int dx_cs,
+                                                            int dx_coff, int accum) {
+  if (blockIdx.x == 0) {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      if (dgamma) dgamma[c] += (float)acc[C + c];
+      if (dbeta) dbeta[c] += (float)acc[c];
+    }
+  }
+  const int C4 = C / 4;
+  const long long n = (long long)M * C4;
+  GSTRIDE(i, n) {
+    const int c = (int)(i % C4) * 4;
+    const long long m = i / C4;
+    const float4 gv = *(const float4*)(g + m * g_cs + g_coff + c);
+    const float4 xv = *(const float4*)(x + m * x_cs + x_coff + c);
+    const float ga[4] = {gv.x, gv.y, gv.z, gv.w}, xa[4] = {xv.x, xv.y, xv.z, xv.w};
+    float4* o = (float4*)(dx + m * dx_cs + dx_coff + c);
+    float4 prev = accum ? *o : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float pa[4] = {prev.x, prev.y, prev.z, prev.w};
+    float r[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float is = invstd[c + e];
+      const float xh = (xa[e] - mean[c + e]) * is;
+      const float sg = (float)(acc[c + e] / M), sgx = (float)(acc[C + c + e] / M);
+      float v = gamma[c + e] * is * (ga[e] - sg - xh * sgx);
+      if (accum) v += pa[e];
+      r[e] = v;
+    }
+    *o = make_float4(r[0], r[1], r[2], r[3]);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // elementwise
 // ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void relu_mask4_kernel(float* g, int g_cs, int g_coff, const float* __restrict__ y,
+                                                         int y_cs, int y_coff, int M, int C) {
+  const int C4 = C / 4;
+  const long long n = (long long)M * C4;
+  GSTRIDE(i, n) {
+    const int c = (int)(i % C4) * 4;
+    const long long m = i / C4;
+    const float4 yv = *(const float4*)(y + m * y_cs + y_coff + c);
+    float4* gp = (float4*)(g + m * g_cs + g_coff + c);
+    float4 gv = *gp;
+    if (!(yv.x > 0.f)) gv.x = 0.f;
+    if (!(yv.y > 0.f)) gv.y = 0.f;
+    if (!(yv.z > 0.f)) gv.z = 0.f;
+    if (!(yv.w > 0.f)) gv.w = 0.f;
+    *gp = gv;
+  }
+}
+
 __global__ void relu_mask_kernel(float* g, int g_cs, int g_coff, const float* __restrict__ y, int y_cs, int y_coff,
                                  int M, int C) {
   const long long n = (long long)M * C;
@@ -1865,6 +1923,14 @@ int upr_t_bn_bwd_apply(const float* g, int g_cs, int g_coff, const float* x, int
                        const float* invstd, const float* gamma, const double* acc, int M, int C, float* dgamma,
                        float* dbeta, float* dx, int dx_cs, int dx_coff, int accumulate, void* stream) {
   if (!g || !x || !acc || !dx || !gamma) return UPR_ERR_ARG;
+  const auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (C % 4 == 0 && g_cs % 4 == 0 && g_coff % 4 == 0 && x_cs % 4 == 0 && x_coff % 4 == 0 && dx_cs % 4 == 0 &&
+      dx_coff % 4 == 0 && a16(g) && a16(x) && a16(dx)) {
+    const long long n4 = (long long)M * (C / 4);
+    hipLaunchKernelGGL(bn_bwd_apply4_kernel, dim3(grid_for(n4)), dim3(256), 0, ST(stream), g, g_cs, g_coff, x, x_cs,
+                       x_coff, mean, invstd, gamma, acc, M, C, dgamma, dbeta, dx, dx_cs, dx_coff, accumulate);
+    LAUNCH_CHECK();
+  }
   const long long n = (long long)M * C;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), g, g_cs, g_coff, x, x_cs,
                      x_coff, mean, invstd, gamma, acc, M, C, dgamma, dbeta, dx, dx_cs, dx_coff, accumulate);
@@ -1874,6 +1940,11 @@ int upr_t_bn_bwd_apply(const float* g, int g_cs, int g_coff, const float* x, int
 int upr_t_chan_sum(const float* g, int M, int C, int cs, int coff, float* out, int accumulate, void* stream) {
   if (!g || !out) return UPR_ERR_ARG;
   if (!accumulate) UPR_CHECK_HIP(hipMemsetAsync(out, 0, sizeof(float) * C, ST(stream)));
+  if (reduce4_ok(C, cs, coff, g)) {
+    hipLaunchKernelGGL(chan_reduce4_kernel, dim3(reduce_grid(M)), dim3(256), 0, ST(stream), g, cs, coff, nullptr, 0, 0,
+                       nullptr, nullptr, M, C, 2, nullptr, out);
+    LAUNCH_CHECK();
+  }
   hipLaunchKernelGGL(chan_reduce_kernel, dim3(reduce_grid(M)), dim3(256), 0, ST(stream), g, cs, coff, nullptr, 0, 0,
                      nullptr, nullptr, M, C, 2, nullptr, out);
   LAUNCH_CHECK();
@@ -1882,6 +1953,13 @@ int upr_t_chan_sum(const float* g, int M, int C, int cs, int coff, float* out, i
 int upr_t_relu_mask(float* g, int g_cs, int g_coff, const float* y, int y_cs, int y_coff, int M, int C,
                     void* stream) {
   if (!g || !y) return UPR_ERR_ARG;
+  if (C % 4 == 0 && g_cs % 4 == 0 && g_coff % 4 == 0 && y_cs % 4 == 0 && y_coff % 4 == 0 && ((uintptr_t)g & 15) == 0 &&
+      ((uintptr_t)y & 15) == 0) {
+    const long long n4 = (long long)M * (C / 4);
+    hipLaunchKernelGGL(relu_mask4_kernel, dim3(grid_for(n4)), dim3(256), 0, ST(stream), g, g_cs, g_coff, y, y_cs,
+                       y_coff, M, C);
+    LAUNCH_CHECK();
+  }
   const long long n = (long long)M * C;
   hipLaunchKernelGGL(relu_mask_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), g, g_cs, g_coff, y, y_cs, y_coff,
                      M, C);
