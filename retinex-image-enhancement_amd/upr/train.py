@@ -117,6 +117,7 @@ class Act:
         """Returns 1 (accumulate) or 0 (overwrite) for the next producer."""
         acc = 0 if self.fresh else 1
         self.fresh = False
+        self.t16 = None
         return acc
 
 
@@ -245,12 +246,16 @@ class Conv:
         if out is None:
             out = Act.new(B, Ho, Wo, self.Cout, x.t.device, fresh=False)
         out.fresh = False
+        out.t16 = None  # any fp16 copy of an earlier content is stale now
         self.amp = _AMP[0] and self.mfma and x_view is None
         if self.amp:
             # the fp16 copy of x is the weight gradient's B operand (upr_t_conv_wgrad16)
-            t16 = x.t16 if x.coff == 0 and x.C == x.cs == self.Cin else None
+            whole = x.coff == 0 and x.C == x.cs == self.Cin
+            t16 = x.t16 if whole else None
             x16 = self._mfma16(x.t, B, H, W, self.Cin, x.cs, x.coff, self.wp16, self.bias, self.Cout, self.kh,
                                self.kw, self.s, self.p, self.d, res, relu, out, x16=t16)
+            if whole:
+                x.t16 = x16  # the next autocast conv reading x (EnhancedFAM: three of them) reuses the copy
             self.x16 = None if self.frozen else x16
         elif self.mfma and x_view is None:
             _chk(lib.upr_t_conv_mfma(_fp(x.t), B, H, W, self.Cin, x.cs, x.coff, _p(self.wp),

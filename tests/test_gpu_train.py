@@ -161,16 +161,22 @@ def test_maxpool_bwd_matches_torch(B, C, H, W, k, s, p, nchw):
     assert (out[m] - ref[m]).abs().max().item() <= 1e-6 * max(1.0, ref[m].abs().max().item())  # summation order
 
 
-def test_convT_layer():
+@pytest.mark.parametrize("cin,cout,hw", [
+    (64, 32, 12),    # width not a multiple of 16: the tile GEMM
+    (64, 32, 32),    # dec1.up shape class: the streaming ConvT kernel (conv_t2.hip)
+    (128, 64, 16),   # dec2.up shape class: streaming, 2 waves per pixel group
+])
+def test_convT_layer(cin, cout, hw):
+    """fp32 ConvTranspose2d(2, 2) forward / dgrad / wgrad vs torch CPU."""
     from upr.train import Act, ConvT
     torch.manual_seed(1)
-    m = torch.nn.ConvTranspose2d(64, 32, 2, 2)
-    x = torch.randn(2, 64, 12, 12)
+    m = torch.nn.ConvTranspose2d(cin, cout, 2, 2)
+    x = torch.randn(2, cin, hw, hw)
     xr = x.clone().requires_grad_(True)
     y = m(xr)
     gy = torch.randn(y.shape)
     y.backward(gy)
-    md = torch.nn.ConvTranspose2d(64, 32, 2, 2).to(DEV)
+    md = torch.nn.ConvTranspose2d(cin, cout, 2, 2).to(DEV)
     md.load_state_dict(m.state_dict())
     md.weight.grad = torch.zeros_like(md.weight)
     md.bias.grad = torch.zeros_like(md.bias)
@@ -179,7 +185,7 @@ def test_convT_layer():
     xa = Act(x.permute(0, 2, 3, 1).contiguous().to(DEV))
     ya = c.fwd(xa)
     _close(ya.t.permute(0, 3, 1, 2), y, 1e-4, "fwd")
-    gxa = Act.new(2, 12, 12, 64, DEV)
+    gxa = Act.new(2, hw, hw, cin, DEV)
     c.bwd(xa, Act(gy.permute(0, 2, 3, 1).contiguous().to(DEV)), gxa)
     torch.cuda.synchronize()
     _close(gxa.t.permute(0, 3, 1, 2), xr.grad, 1e-4, "dgrad")
