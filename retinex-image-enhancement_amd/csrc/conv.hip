@@ -333,7 +333,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvOp op) {
           out[(size_t)m * op.out_cs + op.out_coff + n] = tv;
           if (op.pool) {
             if (one_image) psum += to_f(tv);
-            else atomicAdd(op.pool + img * op.N + n, to_f(tv));
+            else pool_add(op.pool, (size_t)img * op.N + n, to_f(tv));
           }
         }
       }
@@ -341,7 +341,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvOp op) {
     if (op.pool && one_image) {
       psum += __shfl_xor(psum, 16);
       psum += __shfl_xor(psum, 32);
-      if (lane < 16) atomicAdd(op.pool + (m0 / HW) * op.N + n, psum);
+      if (lane < 16) pool_add(op.pool, (size_t)(m0 / HW) * op.N + n, psum);
     }
   }
 }

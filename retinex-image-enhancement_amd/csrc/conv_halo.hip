@@ -689,7 +689,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
         const int cch = tid / EPC, e = tid % EPC;
         float s = 0.f;
         for (int q = cch; q < 256; q += CHN) s += Cs[q * (EPC + 1) + e];
-        atomicAdd(op.pool + b * op.N + n0 + tid, s);
+        pool_add(op.pool, (size_t)b * op.N + n0 + tid, s);
       }
     }
   }

@@ -715,7 +715,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, RingCfg<MODE, C, NB, FL
             v += __shfl_xor(v, 2);
             v += __shfl_xor(v, 4);
             v += __shfl_xor(v, 8);
-            if (fr == 0) atomicAdd(op.pool + (size_t)b * op.N + nt * 16 + fg * 4 + i, v);
+            if (fr == 0) pool_add(op.pool, (size_t)b * op.N + nt * 16 + fg * 4 + i, v);
             pool[nt][i] = 0.f;
           }
         flushed = true;
@@ -1110,7 +1110,7 @@ __global__ __launch_bounds__(256) void conv_ring32_kernel(RingArgs a) {
             v += __shfl_xor(v, 2);
             v += __shfl_xor(v, 4);
             v += __shfl_xor(v, 8);
-            if (fr == 0) atomicAdd(op.pool + (size_t)cc.b * op.N + nt * 16 + fg * 4 + i, v);
+            if (fr == 0) pool_add(op.pool, (size_t)cc.b * op.N + nt * 16 + fg * 4 + i, v);
             pool[nt][i] = 0.f;
           }
         flushed = true;

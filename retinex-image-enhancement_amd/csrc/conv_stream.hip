@@ -438,7 +438,7 @@ __global__ __launch_bounds__(256) void conv_stream_fam_kernel(StreamArgs args) {
         v += __shfl_xor(v, 2);
         v += __shfl_xor(v, 4);
         v += __shfl_xor(v, 8);
-        if (fr == 0) atomicAdd(op.pool + (size_t)pool_img * op.N + nt * 16 + fg * 4 + i, v);
+        if (fr == 0) pool_add(op.pool, (size_t)pool_img * op.N + nt * 16 + fg * 4 + i, v);
         pool[nt][i] = 0.f;
       }
   };

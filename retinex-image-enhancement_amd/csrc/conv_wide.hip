@@ -291,7 +291,7 @@ __device__ __forceinline__ void wide_epilogue(const ConvOp& op, f32x4_w (&acc)[W
             for (int e = 0; e < 8; ++e) psum[e] += (float)o[e];
           } else {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) atomicAdd(op.pool + img * op.N + nch + e, (float)o[e]);
+            for (int e = 0; e < 8; ++e) pool_add(op.pool, (size_t)img * op.N + nch + e, (float)o[e]);
           }
         }
       }
@@ -309,7 +309,7 @@ __device__ __forceinline__ void wide_epilogue(const ConvOp& op, f32x4_w (&acc)[W
     if (tid < BN) {
       float t = 0.f;
       for (int g = 0; g < RPI; ++g) t += Es[g * BN + tid];
-      atomicAdd(op.pool + (m0 / HW) * op.N + n0 + tid, t);
+      pool_add(op.pool, (size_t)(m0 / HW) * op.N + n0 + tid, t);
     }
   }
 }

@@ -58,7 +58,7 @@ __global__ void aspp_global_kernel(const float* __restrict__ pool, const float* 
   float* mean = sm;
   float* g = sm + C;
   const int b = blockIdx.x;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) mean[c] = pool[b * C + c] * inv_hw;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) mean[c] = pool_get(pool, (size_t)b * C + c) * inv_hw;
   __syncthreads();
   for (int o = threadIdx.x; o < C; o += blockDim.x) {
     float s = bg[o];
@@ -244,7 +244,7 @@ enum BufId : int {
   B_U3, B_V3, B_D3, B_U2, B_V2, B_D2, B_U1, B_V1, B_D1,
   B_H1, B_Y1, B_H2, B_Y2, B_H3, B_Y3,
   B_MM1, B_P1, B_Q1, B_MM2, B_P2, B_Q2, B_MM3, B_P3, B_Q3,
-  B_POOL,   // float pool sums (FAM x3 + ASPP), zeroed each forward
+  B_POOL,   // pool sums (FAM x3 + ASPP; 64-bit fixed point, upr_common.h pool_add), zeroed each forward
   B_CA,     // float ca [3][B][32]
   B_IB,     // float ASPP per-image bias [B][256]
   B_ILLU32, // float illu when the model dtype is fp16 (head writes fp32 then tail reads)
@@ -274,7 +274,7 @@ struct Op {
   int out = -1, out_cs = 0, out_coff = 0;
   int res1 = -1, res1_cs = 0, res2 = -1, res2_cs = 0;
   int relu = 0, store = kStoreNHWC;
-  int pool_slot = -1;   // index into pool buffer (units of B*256 floats)
+  int pool_slot = -1;   // index into pool buffer (units of B*256 8-byte entries)
   int img_bias = 0;
   size_t head_w = 0; float head_b = 0.f;
   // conv3 / fam
@@ -387,7 +387,7 @@ static size_t ws_layout(const UprModel* m, int B, int H, int W, size_t* offs) {
   const size_t elt = m->dtype == kF16 ? 2 : 4;
   for (int id = 1; id < B_COUNT; ++id) {
     size_t bytes = 0;
-    if (id == B_POOL) bytes = (size_t)4 * B * 256 * 4;
+    if (id == B_POOL) bytes = (size_t)4 * B * 256 * 8;
     else if (id == B_CA) bytes = (size_t)3 * B * 32 * 4;
     else if (id == B_IB) bytes = (size_t)B * 256 * 4;
     else {
@@ -802,7 +802,7 @@ static int run_forward(UprModel* m, const void* x, int B, int H, int W, void* en
   float* pool = (float*)buf(B_POOL);
   float* ca = (float*)buf(B_CA);
   float* ib = (float*)buf(B_IB);
-  UPR_CHECK_HIP(hipMemsetAsync(pool, 0, (size_t)4 * B * 256 * 4, st));
+  UPR_CHECK_HIP(hipMemsetAsync(pool, 0, (size_t)4 * B * 256 * 8, st));
   const int H4 = (H / 2) / 2, W4 = (W / 2) / 2, H16 = (H / 4) / 4, W16 = (W / 4) / 4;
   auto lvl_dims = [&](int lshift, int& h, int& w) {
     if (lshift == 2) { h = H4; w = W4; }
@@ -876,7 +876,7 @@ static int run_forward(UprModel* m, const void* x, int B, int H, int W, void* en
         } else {
           c.out = buf(o.out); c.out_cs = o.out_cs; c.out_coff = o.out_coff;
         }
-        c.pool = o.pool_slot >= 0 ? pool + (size_t)o.pool_slot * B * 256 : nullptr;
+        c.pool = o.pool_slot >= 0 ? pool + (size_t)o.pool_slot * B * 512 : nullptr;  // 8-byte entries
         if (o.out2 >= 0) {
           c.out2 = buf(o.out2); c.out2_cs = L.N;
           c.pre2_scale = fptr(o.ps); c.pre2_shift = fptr(o.ph);
@@ -912,7 +912,7 @@ static int run_forward(UprModel* m, const void* x, int B, int H, int W, void* en
       case OP_ASPP_G: {
         const int h = H >> 3, w = W >> 3;
         hipLaunchKernelGGL(aspp_global_kernel, dim3(B), dim3(256), 2 * 256 * sizeof(float), st,
-                           pool + (size_t)3 * B * 256, fptr(o.w), fptr(o.b), fptr(o.P), ib, 256,
+                           pool + (size_t)3 * B * 512, fptr(o.w), fptr(o.b), fptr(o.P), ib, 256,
                            1.f / (float)(h * w));
         rc = (int)hipGetLastError();
         break;
@@ -920,7 +920,7 @@ static int run_forward(UprModel* m, const void* x, int B, int H, int W, void* en
       case OP_FAM_CA: {
         int h, w;
         lvl_dims(o.lvl_shift, h, w);
-        rc = launch_fam_ca(pool + (size_t)o.fam * B * 256, fptr(o.ca_w1), fptr(o.ca_b1), fptr(o.ca_w2),
+        rc = launch_fam_ca(pool + (size_t)o.fam * B * 512, fptr(o.ca_w1), fptr(o.ca_b1), fptr(o.ca_w2),
                            fptr(o.ca_b2), ca + (size_t)o.fam * B * 32, B, h * w, st);
         break;
       }

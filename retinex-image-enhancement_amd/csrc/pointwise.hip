@@ -151,7 +151,7 @@ __global__ void fam_ca_kernel(const float* __restrict__ pool, const float* __res
   if (b >= B || c >= 32) return;
   __shared__ float g[32];
   __shared__ float hdn[2];
-  g[c] = pool[b * 32 + c] * inv_hw;
+  g[c] = pool_get(pool, (size_t)b * 32 + c) * inv_hw;
   __syncthreads();
   if (c < 2) {
     float s = b1[c];

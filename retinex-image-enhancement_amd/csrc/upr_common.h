@@ -108,6 +108,21 @@ int launch_conv_out32(const ConvOp& op, hipStream_t stream);
 int launch_conv(const ConvOp& op, int dtype, hipStream_t stream);
 
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+// Per-(image, channel) pool sums (ConvOp::pool: EnhancedFAM channel attention,
+// ASPP global branch) are accumulated as 64-bit fixed point (2^-24 units) with
+// integer atomics: the sum no longer depends on the order in which tiles /
+// units finish, so a forward is bit-for-bit reproducible.  A pool slot holds
+// 8 bytes per entry (the float* is only the carrier type).
+constexpr float kPoolScale = 16777216.f;  // 2^24
+#ifdef __HIPCC__
+__device__ __forceinline__ void pool_add(float* pool, size_t idx, float v) {
+  atomicAdd((unsigned long long*)pool + idx, (unsigned long long)__float2ll_rn(v * kPoolScale));
+}
+__device__ __forceinline__ float pool_get(const float* pool, size_t idx) {
+  return (float)((double)(long long)((const unsigned long long*)pool)[idx] * (1.0 / 16777216.0));
+}
+#endif
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 }  // namespace upr
