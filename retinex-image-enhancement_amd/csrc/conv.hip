@@ -416,9 +416,12 @@ int launch_conv_out32(const ConvOp& op, hipStream_t stream) {
   if (!op.out32 || op.out || op.out2 || op.pool || op.store == kStoreHeadIllu) return kErrArg;
   if (op.nseg < 1 || op.nseg > 4 || op.B <= 0 || op.Ho <= 0 || op.Wo <= 0) return kErrArg;
   if (conv_impl_mode() != 0) return kErrUnsupported;
-  const int rc = launch_conv_wide(op, stream);
+  int rc = launch_conv_wide(op, stream);
   if (rc != kErrUnsupported) return rc;
-  return launch_conv_ring(op, stream);
+  rc = launch_conv_ring(op, stream);
+  if (rc != kErrUnsupported) return rc;
+  static const int halo32 = getenv("UPR_HALO_OUT32") ? atoi(getenv("UPR_HALO_OUT32")) : 1;
+  return halo32 ? launch_conv_halo(op, kF16, stream) : kErrUnsupported;
 }
 
 int launch_conv(const ConvOp& op, int dtype, hipStream_t stream) {

@@ -667,6 +667,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
       T* ov = (T*)&o;
 #pragma unroll
       for (int e = 0; e < EPC; ++e) ov[e] = hfrom_f<T>(v[e]);
+      if constexpr (sizeof(T) == 2) {
+        if (op.out32) {
+          // fp32 output of the fp16 conv (training autocast): the fp16-rounded
+          // value (+ res32, fp32), NHWC only (launch_conv_halo checks)
+          float* d32 = op.out32 + m * op.out32_cs + op.out32_coff + n0 + nb0;
+          const float* r32 = op.res32 ? op.res32 + m * op.res32_cs + n0 + nb0 : nullptr;
+#pragma unroll
+          for (int e = 0; e < EPC; e += 4) {
+            f32x4_h w4 = {hto_f(ov[e]), hto_f(ov[e + 1]), hto_f(ov[e + 2]), hto_f(ov[e + 3])};
+            if (r32) w4 += *(const f32x4_h*)(r32 + e);
+            *(f32x4_h*)(d32 + e) = w4;
+          }
+          continue;
+        }
+      }
       if (op.store == kStoreConvT2x2) {
         // ConvTranspose2d(2, 2) pixel shuffle (model.py:167): n = (dy*2+dx)*Cout + co
         const int cout = op.N >> 2;
@@ -850,6 +865,13 @@ static void halo_choice(int dtype, int prog, int store, int N, int& th, int& occ
 // Returns kErrUnsupported when the op is not a halo-kernel shape (caller falls back).
 int launch_conv_halo(const ConvOp& op, int dtype, hipStream_t st) {
   if (op.Wo < 24 || op.Ho < 8) return kErrUnsupported;
+  if (op.out32) {
+    // fp32 output (training autocast convs): fp16 kernel, plain NHWC store, no pool / residual-before-ReLU
+    if (dtype != kF16 || op.out || op.store != kStoreNHWC || op.pool || op.res1 || op.res2 || op.img_bias ||
+        (uintptr_t)op.out32 % 16 || op.out32_cs % 4 || op.out32_coff % 4 || op.N % 4 ||
+        (op.res32 && ((uintptr_t)op.res32 % 16 || op.res32_cs % 4)))
+      return kErrUnsupported;
+  }
   const int elt = dtype == kF16 ? 2 : 4;
   if (op.out && ((op.out_cs * elt) % 16 || (op.out_coff * elt) % 16)) return kErrUnsupported;
   if (op.res1 && (op.res1_cs * elt) % 16) return kErrUnsupported;
