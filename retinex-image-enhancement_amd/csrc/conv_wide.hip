@@ -318,7 +318,7 @@ __device__ __forceinline__ void wide_epilogue(const ConvOp& op, f32x4_w (&acc)[W
 // 512-thread blocks per CU
 // (MINW 4 also selects ONE LDS stage: load -> compute per step, the other
 // block on the CU overlapping)
-template <int BN, bool PIPE, int MINW = 2>
+template <int BN, bool PIPE, int MINW = 2, int SCHED = 0>
 __global__ __launch_bounds__(512, MINW) void conv_wide_kernel(ConvOp op) {
   constexpr bool ONE = MINW >= 4;
   using C = WideCfg<BN>;
@@ -455,15 +455,25 @@ __global__ __launch_bounds__(512, MINW) void conv_wide_kernel(ConvOp op) {
     // MFMAs, so the fragments of the half being consumed free registers as the
     // next half's arrive
     auto interleave = [&]() {
+      if constexpr (SCHED == 2) {
+        // one fragment read after every two MFMAs, VALU between (measured on the halo-wide kernel)
 #pragma unroll
-      for (int a = 0; a < C::WN; ++a) {
-        __builtin_amdgcn_sched_group_barrier(0x008, C::WN, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-      }
+        for (int a = 0; a < (C::WM * C::WN) / 2; ++a) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+        }
+      } else {
 #pragma unroll
-      for (int a = C::WN; a < C::WM; ++a) {
-        __builtin_amdgcn_sched_group_barrier(0x008, C::WN, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        for (int a = 0; a < C::WN; ++a) {
+          __builtin_amdgcn_sched_group_barrier(0x008, C::WN, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        }
+#pragma unroll
+        for (int a = C::WN; a < C::WM; ++a) {
+          __builtin_amdgcn_sched_group_barrier(0x008, C::WN, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
       }
     };
     issue(0);
@@ -747,7 +757,7 @@ struct Halo3Cfg {
   static_assert(LDS <= 163840, "LDS");
 };
 
-template <int BN, int W>
+template <int BN, int W, int SCHED>
 __global__ __launch_bounds__(512, 2) void conv_hwide3_kernel(ConvOp op) {
   using HC = Halo3Cfg<BN, W>;
   constexpr int WM = HC::WM, WN = HC::WN, BM = HC::BM;
@@ -860,15 +870,25 @@ __global__ __launch_bounds__(512, 2) void conv_hwide3_kernel(ConvOp op) {
     }
   };
   auto interleave = [&]() {
+    if constexpr (SCHED == 0) {
 #pragma unroll
-    for (int a = 0; a < WN; ++a) {
-      __builtin_amdgcn_sched_group_barrier(0x008, WN, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-    }
+      for (int a = 0; a < WN; ++a) {
+        __builtin_amdgcn_sched_group_barrier(0x008, WN, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      }
 #pragma unroll
-    for (int a = WN; a < WM; ++a) {
-      __builtin_amdgcn_sched_group_barrier(0x008, WN, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      for (int a = WN; a < WM; ++a) {
+        __builtin_amdgcn_sched_group_barrier(0x008, WN, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+    } else if constexpr (SCHED == 2) {
+      // one fragment read after every two MFMAs, VALU between
+#pragma unroll
+      for (int a = 0; a < (WM * WN) / 2; ++a) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+      }
     }
   };
   auto adv = [](int& c, int& y, int& x) {
@@ -934,19 +954,29 @@ __global__ __launch_bounds__(512, 2) void conv_hwide3_kernel(ConvOp op) {
   wide_epilogue<BN, WM, WN, HC::WAVES_M, BM, true>(op, acc, smem, m0, n0, M, HW);
 }
 
-template <int BN, int W>
-static int launch_hwide3(const ConvOp& op, hipStream_t st) {
+template <int BN, int W, int SCHED>
+static int launch_hwide3_s(const ConvOp& op, hipStream_t st) {
   using HC = Halo3Cfg<BN, W>;
   static bool attr_set = false;
   if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute((const void*)conv_hwide3_kernel<BN, W>,
+    const hipError_t e = hipFuncSetAttribute((const void*)conv_hwide3_kernel<BN, W, SCHED>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, HC::LDS);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
   const int grid = (op.B * op.Ho * W / HC::BM) * (op.N / BN);
-  hipLaunchKernelGGL((conv_hwide3_kernel<BN, W>), dim3(grid), dim3(512), HC::LDS, st, op);
+  hipLaunchKernelGGL((conv_hwide3_kernel<BN, W, SCHED>), dim3(grid), dim3(512), HC::LDS, st, op);
   return (int)hipGetLastError();
+}
+// UPR_HW3_SCHED: 2 = one fragment read per two MFMAs, VALU between (default; measured
+// bneck 0.177 -> 0.172 ms, dec3 0.219 -> 0.214 on random operands), 0 = grouped
+// MFMA / fragment-read interleave, 1 = hipcc's own schedule (A/B timing)
+template <int BN, int W>
+static int launch_hwide3(const ConvOp& op, hipStream_t st) {
+  static const int v = getenv("UPR_HW3_SCHED") ? atoi(getenv("UPR_HW3_SCHED")) : 2;
+  if (v == 1) return launch_hwide3_s<BN, W, 1>(op, st);
+  if (v == 2) return launch_hwide3_s<BN, W, 2>(op, st);
+  return launch_hwide3_s<BN, W, 0>(op, st);
 }
 
 // UPR_WIDE_HALO=0 routes these convs to the gathered-A kernel, =1 to the
@@ -966,20 +996,27 @@ static int halo_route(const ConvOp& op, hipStream_t st) {
 }
 
 
-template <int BN, bool PIPE>
-static int launch_wide_bn(const ConvOp& op, hipStream_t st) {
+template <int BN, bool PIPE, int SCHED>
+static int launch_wide_bn_s(const ConvOp& op, hipStream_t st) {
   using C = WideCfg<BN>;
   static bool attr_set = false;
   if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute((const void*)conv_wide_kernel<BN, PIPE>,
+    const hipError_t e = hipFuncSetAttribute((const void*)conv_wide_kernel<BN, PIPE, 2, SCHED>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
   const int M = op.B * op.Ho * op.Wo;
   const int grid = ((M + WBM - 1) / WBM) * (op.N / BN);
-  hipLaunchKernelGGL((conv_wide_kernel<BN, PIPE>), dim3(grid), dim3(512), C::LDS, st, op);
+  hipLaunchKernelGGL((conv_wide_kernel<BN, PIPE, 2, SCHED>), dim3(grid), dim3(512), C::LDS, st, op);
   return (int)hipGetLastError();
+}
+
+// UPR_WIDE_SCHED: 2 = one fragment read per two MFMAs (default), 0 = grouped interleave (A/B timing)
+template <int BN, bool PIPE>
+static int launch_wide_bn(const ConvOp& op, hipStream_t st) {
+  static const int v = getenv("UPR_WIDE_SCHED") ? atoi(getenv("UPR_WIDE_SCHED")) : 2;
+  return v == 2 ? launch_wide_bn_s<BN, PIPE, 2>(op, st) : launch_wide_bn_s<BN, PIPE, 0>(op, st);
 }
 
 // UPR_WIDE_KIND=0 selects the plain main loop (A/B timing); default: the
