@@ -1036,7 +1036,8 @@ static int launch_wide_onestep128(const ConvOp& op, hipStream_t st);
 // fp16 preact+ASPP bs 32: it beats the one-block double-buffered kernel on
 // every 128-wide GEMM of the graph -- enc2.conv1 0.184 -> 0.160 ms, enc2.conv2
 // 0.255 -> 0.204, dec1.up 0.369 -> 0.258 -- and, as 128-wide halves, on the
-// 2-step 256-wide dec2.up 0.178 -> 0.157; 4-step 256-wide GEMMs break even).
+// 2-step 256-wide dec2.up 0.178 -> 0.157; the 4-step 256-wide ASPP conv1x1
+// 0.070 -> 0.053 ms; the 16-step ASPP fusion breaks even, so it stays whole).
 // UPR_WIDE_ONESTEP = max K steps for 128-wide GEMMs (0 = never; A/B timing),
 // UPR_WIDE_SPLIT256 = max K steps for splitting 256-wide GEMMs.
 static int env_int(const char* name, int dflt) {
@@ -1048,7 +1049,7 @@ static int onestep_max() {
   return v;
 }
 static int split256_max() {
-  static const int v = env_int("UPR_WIDE_SPLIT256", 2);
+  static const int v = env_int("UPR_WIDE_SPLIT256", 4);
   return v;
 }
 
