@@ -1057,7 +1057,13 @@ template <int BN>
 static int launch_wide_any(const ConvOp& op, hipStream_t st) {
   int steps = 0;
   for (int s = 0; s < op.nseg; ++s) steps += op.seg[s].kh * op.seg[s].kw * (op.seg[s].C / WBK);
-  if (steps <= (BN == 128 ? onestep_max() : split256_max())) return launch_wide_onestep128(op, st);
+  // stride-2 256-wide convs (enc3.conv1, 18 steps) also gain as halves: 0.125 -> 0.108 ms,
+  // where the 16-step 1x1 ASPP fusion loses (0.127 -> 0.156)
+  bool s2 = false;
+  for (int s = 0; s < op.nseg; ++s) s2 = s2 || op.seg[s].stride == 2;
+  static const int s2_split = env_int("UPR_WIDE_SPLIT256_S2", 1);
+  if (steps <= (BN == 128 ? onestep_max() : split256_max()) || (BN == 256 && s2 && s2_split))
+    return launch_wide_onestep128(op, st);
   if (steps < 2) return launch_wide_bn<BN, false>(op, st);
   return wide_kind() == 0 ? launch_wide_bn<BN, false>(op, st) : launch_wide_bn<BN, true>(op, st);
 }
