@@ -2,28 +2,37 @@
 """UP-Retinex hot-path benchmark (BASELINE.json metric: images/s at 512x512 bs=32).
 
 One step = one MultiScaleUP_Retinex forward over one resident batch of 32
-synthetic 512x512 images per GPU (configs[1]: random-init plain model, fp32;
---precision fp16 --variant preact_aspp gives configs[2]).  Multi-GPU: one
-process per GPU.  `--gpus N` (N > 1) run directly makes this process a pure
-launcher (it never touches the GPU): it starts `torch.distributed.run` with N
-ranks on 127.0.0.1 and exits with its code; run under torch.distributed.run
-(WORLD_SIZE set) it is one rank.  Each rank processes its own 32-image shard
-with no data-path collective (weak scaling); `--collect` adds the final
-collect of SURVEY §8e inside the timed region (one RCCL all_gather_into_tensor
-of the fp16 enhanced images per step).  Barrier + synchronize bracket the
-timed region and rank 0 reports the max over ranks.  `--dry-run` replaces the
-GPU work by a small CPU step over gloo (tests the launcher / rank plumbing on
-a machine without a GPU).
+synthetic 512x512 images per GPU.  The headline (`value`) is configs[1]
+(random-init plain model, fp32); `--precision fp16 --variant preact_aspp`
+makes configs[2] the headline instead.  A default run (no --no-nested) adds
+two nested objects to the same JSON line, each with its own roofline, parity
+and CPU baseline:
+  fp16_preact_aspp  configs[2]: bs 32 512^2 fp16 preact+ASPP forward
+  train_amp         configs[4]: bs 8 512^2 AMP training step (rank 0 of an N=1
+                    run only; `--train` makes it the headline)
+
+Multi-GPU: one process per GPU.  `--gpus N` (N > 1) run directly makes this
+process a pure launcher (it never touches the GPU): it starts
+`torch.distributed.run` with N ranks on 127.0.0.1 and exits with its code; run
+under torch.distributed.run (WORLD_SIZE set) it is one rank.  Each rank
+processes its own 32-image shard with no data-path collective (weak scaling);
+`--collect all|rank0` adds the final collect of SURVEY §8e inside the timed
+region (RCCL all_gather_into_tensor to every rank, or a gather to rank 0 only,
+of the fp16 enhanced images).  Barrier + synchronize bracket the timed region
+and rank 0 reports the max over ranks.  `--dry-run` replaces the GPU work by a
+small CPU step over gloo and emits the same keys (tests the launcher / rank /
+report plumbing on a machine without a GPU).
 
 Extra objects on the JSON line:
   roofline      the conv kernel family (CONV_KERNELS below, ~97% of device time), timed live with HIP events around every
                 launch of the last timed step on the model's stream
                 (upr_model_profile); traffic from rocprofv3 FETCH_SIZE/WRITE_SIZE
-                child passes run before this process touches the GPU;
+                child passes run before this process touches the GPU (N=1 only:
+                the numbers are per rank, and the passes need the whole GPU);
                 --ceilings adds the fractions against measured MFMA / HBM rates
-  cpu_baseline  the CPU oracle forward (oracle/net.py, torch-CPU fp32) on the
-                host cores, rank 0 only: the full timed batch in one forward
-                when a one-image warm-up predicts <= 30 s, else a bounded sample
+  parity        image 0 of rank 0's last timed batch vs the CPU oracle, at any world size
+  cpu_baseline  the CPU oracle (oracle/net.py, torch-CPU fp32) on the host cores this process may use,
+                rank 0 of an N=1 run only: 1 warm-up image, then the median of 3 timed repetitions of the sample
 """
 import argparse
 import json
@@ -42,9 +51,11 @@ import torch  # noqa: E402
 PEAK_TFLOPS = {"fp32": 157.3, "fp16": 2516.6}   # MI355X dense MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
 REF_GFLOP_PER_IMG = {"plain": 105.6, "preact_aspp": 123.4}
+TRAIN_GFLOP_PER_IMG = 668.0  # model fwd+bwd + VGG19 fwd x2 + dgrad, 512x512
+CPU_REPS = 3
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -53,56 +64,106 @@ def parse():
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--precision", choices=["fp32", "fp16"], default="fp32")
     ap.add_argument("--variant", choices=["plain", "preact_aspp"], default="plain")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline budget (0 = skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="0 = skip the CPU baselines")
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events")
     ap.add_argument("--breakdown", action="store_true", help="print per-layer stats to stderr")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC traffic passes")
+    ap.add_argument("--no-nested", action="store_true",
+                    help="only the headline config (no fp16_preact_aspp / train_amp objects)")
     ap.add_argument("--ceilings", action="store_true",
                     help="after the timed steps, measure the chip's reachable fp16 MFMA and HBM-copy rates "
                          "(upr/calib.py, ~5 s) and report the roofline fractions against them as well")
     ap.add_argument("--train", action="store_true",
-                    help="configs[4]: one training step (fwd + TotalLoss + bwd + clip + Adam) per step, "
-                         "bs=8 512x512 plain model (batch/size overridable)")
-    ap.add_argument("--collect", action="store_true",
-                    help="time the final collect too: all_gather_into_tensor of the fp16 enhanced images (RCCL)")
+                    help="configs[4] as the headline: one training step (fwd + TotalLoss + bwd + clip + Adam) per "
+                         "step, bs=8 512x512 plain model (batch/size overridable)")
+    ap.add_argument("--collect", nargs="?", const="all", default="none", choices=["none", "all", "rank0"],
+                    help="time the final collect too: fp16 enhanced images to every rank (all) or to rank 0")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: gloo ranks run a small CPU step through the same launch / barrier / report path")
     ap.add_argument("--amp", action="store_true",
-                    help="with --train: the reference's AMP branch (GradScaler: scaled backward, unscale_, "
-                         "skip on inf/nan, scale update); arithmetic stays fp32")
-    return ap.parse_args()
+                    help="with --train: the reference's AMP branch (autocast fp16 convs + GradScaler)")
+    return ap.parse_args(argv)
 
 
-def cpu_baseline(sd, pre, aspp, size, budget_s, batch):
-    """Oracle forward on host cores.  After a one-image warm-up, the full
-    `batch` (the timed GPU workload's shape) runs as one forward
-    when the warm-up predicts it fits in max(budget, 30 s); otherwise single
-    images until the budget is spent."""
-    from oracle import net as onet  # checker / baseline only
-    threads = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
-    x = torch.rand(1, 3, size, size, generator=torch.Generator().manual_seed(99))
-    with torch.no_grad():
+# ----------------------------------------------------------------------------
+# host CPU description and the CPU baselines (oracle = checker / baseline only)
+# ----------------------------------------------------------------------------
+def cpu_info():
+    """Cores this process may use: the affinity mask, capped by a cgroup CPU
+    quota when one is set (on the GPU box os.cpu_count() reports the whole
+    machine while the job's share is far smaller; threads beyond the share
+    only oversubscribe it)."""
+    total = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = total
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    usable = aff if quota is None else max(1, min(aff, int(quota + 0.5)))
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"threads": usable, "os_cpu_count": total, "affinity": aff, "cgroup_quota_cpus": quota,
+            "cpu_model": model}
+
+
+def _median_reps(fn, reps=CPU_REPS):
+    times = []
+    for _ in range(reps):
         t0 = time.perf_counter()
-        onet.forward(sd, x, pre, aspp)  # warm-up
-        t1 = time.perf_counter() - t0
-        if t1 * batch <= max(budget_s, 30.0):
-            xb = torch.rand(batch, 3, size, size, generator=torch.Generator().manual_seed(99))
-            t0 = time.perf_counter()
-            onet.forward(sd, xb, pre, aspp)
-            el = time.perf_counter() - t0
-            return {"value": batch / el, "unit": "images/s", "cores": threads, "kind": "port",
-                    "sample": f"one {batch}x3x{size}x{size} fp32 forward of oracle/net.py (torch-CPU, the full "
-                              f"timed batch) after a 1-image warm-up, {el:.1f}s"}
-        n, t0 = 0, time.perf_counter()
-        while True:
-            onet.forward(sd, x, pre, aspp)
-            n += 1
-            el = time.perf_counter() - t0
-            if el >= budget_s or n >= 64:
-                break
-    return {"value": n / el, "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{n} x 1x3x{size}x{size} fp32 forwards of oracle/net.py (torch-CPU), {el:.1f}s"}
+        fn()
+        times.append(time.perf_counter() - t0)
+    times.sort()
+    return times[len(times) // 2], times
+
+
+def cpu_baseline(sd, pre, aspp, size, sample, note):
+    """oracle/net.py forward (torch-CPU fp32) on `sample` images: 1 warm-up
+    image, then the median of CPU_REPS timed forwards of the whole sample."""
+    from oracle import net as onet  # checker / baseline only
+    ci = cpu_info()
+    torch.set_num_threads(ci["threads"])
+    x1 = torch.rand(1, 3, size, size, generator=torch.Generator().manual_seed(99))
+    xb = torch.rand(sample, 3, size, size, generator=torch.Generator().manual_seed(99))
+    with torch.no_grad():
+        onet.forward(sd, x1, pre, aspp)  # warm-up
+        med, times = _median_reps(lambda: onet.forward(sd, xb, pre, aspp))
+    return {"value": sample / med, "unit": "images/s", "cores": ci["threads"], "kind": "port",
+            "cpu": ci, "rep_seconds": times,
+            "sample": f"{sample}x3x{size}x{size} fp32 forward of oracle/net.py (torch-CPU, {note}); "
+                      f"1-image warm-up, median of {CPU_REPS}"}
+
+
+def cpu_train_baseline(sd, size):
+    """oracle/train.py step (torch-CPU fp32 autograd) on 1 image: 1 warm-up step,
+    then the median of CPU_REPS timed steps."""
+    from oracle import train as otrain  # checker / baseline only
+    ci = cpu_info()
+    torch.set_num_threads(ci["threads"])
+    vgg = otrain.vgg19_state(1234)
+    x = torch.rand(1, 3, size, size, generator=torch.Generator().manual_seed(98))
+
+    def one():
+        otrain.train_step({k: v.clone() for k, v in sd.items()}, vgg, x, False, False)
+    one()
+    med, times = _median_reps(one)
+    return {"value": 1.0 / med, "unit": "images/s", "cores": ci["threads"], "kind": "port",
+            "cpu": ci, "rep_seconds": times,
+            "sample": f"1x3x{size}x{size} training step of oracle/train.py (torch-CPU autograd, fp32); "
+                      f"1 warm-up step, median of {CPU_REPS}"}
 
 
 def parity_vs_cpu(sd, pre, aspp, x, outs, precision):
@@ -118,23 +179,26 @@ def parity_vs_cpu(sd, pre, aspp, x, outs, precision):
         d["reflectance"] /= max(1.0, ref[1].abs().max().item())
     tol = 1e-3  # fp32: north_star; fp16: tests/test_gpu_bn_parity.py FP16_TOL
     return {"max_abs_diff": d, "tol": tol, "pass": all(v <= tol for v in d.values()),
-            "sample": "image 0 of the last timed batch vs oracle/net.py fp32 on host cores"}
+            "sample": "image 0 of rank 0's last timed batch vs oracle/net.py fp32 on host cores"}
 
 
+# ----------------------------------------------------------------------------
+# PMC traffic (child passes before this process touches the GPU)
+# ----------------------------------------------------------------------------
 # every kernel launch_conv dispatches to (the bench's conv family = the executor's GEMM ops)
 CONV_KERNELS = ("conv_halo_kernel", "conv_igemm_kernel", "conv_wide_kernel", "conv_wide32_kernel",
                 "conv_stream_kernel", "conv_stream_fam_kernel", "conv_ring_kernel", "conv_ring32_kernel",
                 "conv_hwide_kernel", "conv_hwide3_kernel", "conv_t2_kernel", "conv_t2_f32_kernel")
 
 
-def pmc_traffic(args):
+def pmc_traffic(precision, variant, batch, size):
     """HBM bytes of the conv kernels per forward from rocprofv3 PMC counters.
 
-    Runs BEFORE this process touches the GPU: two child passes of this script
-    (one forward of warm-up + one timed) under `rocprofv3 --pmc FETCH_SIZE` and
-    `--pmc WRITE_SIZE` (separate passes: they do not fit one pass on gfx950).
-    FETCH_SIZE (KB) reports half the bytes of wide coalesced reads on gfx950, so
-    it is doubled (MI355X_MICROARCH.md, HBM section).  Returns None on failure."""
+    Two child passes of this script (one forward of warm-up + one timed) under
+    `rocprofv3 --pmc FETCH_SIZE` and `--pmc WRITE_SIZE` (separate passes: they
+    do not fit one pass on gfx950).  FETCH_SIZE (KB) reports half the bytes of
+    wide coalesced reads on gfx950, so it is doubled (MI355X_MICROARCH.md, HBM
+    section).  Returns None on failure."""
     import csv
     import shutil
     import subprocess
@@ -144,8 +208,8 @@ def pmc_traffic(args):
         return None
     out = {}
     base = [sys.executable, os.path.abspath(__file__), "--steps", "1", "--warmup", "1", "--cpu-seconds", "0",
-            "--no-profile", "--no-traffic", "--batch", str(args.batch), "--size", str(args.size),
-            "--precision", args.precision, "--variant", args.variant]
+            "--no-profile", "--no-traffic", "--no-nested", "--batch", str(batch), "--size", str(size),
+            "--precision", precision, "--variant", variant]
     env = dict(os.environ, TMPDIR="/tmp")
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix="upr_pmc_", dir="/tmp")
@@ -181,6 +245,9 @@ def pmc_traffic(args):
             "launches_per_forward": n_launch / 2.0}
 
 
+# ----------------------------------------------------------------------------
+# ranks
+# ----------------------------------------------------------------------------
 def launch_ranks(args):
     """`--gpus N` without WORLD_SIZE: this process is only the launcher and never
     initialises the GPU.  It runs torch.distributed.run with N ranks (one per
@@ -232,64 +299,206 @@ def max_over_ranks(world, dev, seconds):
     return t.item()
 
 
-def dry_run(args):
-    """The launcher / rank / barrier / max-over-ranks / report path with a small
-    CPU step in place of the forward (CPU test of --gpus N, gloo)."""
-    world, rank, dev = dist_setup(args)
-    torch.manual_seed(rank)
-    a = torch.rand(256, 256)
-    for _ in range(args.warmup):
-        a = torch.tanh(a @ a.T / 256)
+def timed_loop(world, dev, steps, warmup, step, profile_last=None):
+    """warmup untimed steps, then `steps` timed ones bracketed by barrier +
+    synchronize; returns (max-over-ranks seconds, last step's result).
+    profile_last(True/False) brackets the LAST timed step (per-launch events)."""
+    for _ in range(warmup):
+        step()
     sync(world, dev)
+    last = None
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        a = torch.tanh(a @ a.T / 256)
+    for i in range(steps):
+        if profile_last is not None and i == steps - 1:
+            profile_last(True)
+        last = step()
     sync(world, dev)
-    elapsed = max_over_ranks(world, dev, time.perf_counter() - t0)
-    ranks = [None] * world
-    if world > 1:
-        torch.distributed.all_gather_object(ranks, (rank, os.getpid()))
-    else:
-        ranks = [(rank, os.getpid())]
+    el = time.perf_counter() - t0
+    if profile_last is not None:
+        profile_last(False)
+    return max_over_ranks(world, dev, el), last
+
+
+def collect_fn(mode):
+    if mode == "none":
+        return None
+    from upr.dist import gather_shards, gather_to_rank0
+    return gather_shards if mode == "all" else gather_to_rank0
+
+
+# ----------------------------------------------------------------------------
+# forward leg (configs[1] / [2] / [3])
+# ----------------------------------------------------------------------------
+def _cfg_index(precision, variant, size):
+    """BASELINE.json configs[] entry a forward run corresponds to."""
+    if size == 1024 and variant == "preact_aspp":
+        return 3  # bs=256 1024^2 over 8 GPUs = 32 per GPU
+    return 1 if precision == "fp32" and variant == "plain" else 2
+
+
+def conv_roofline(stats, precision, B, traffic):
+    gemm = [s for s in stats if s["kind"] == "conv_igemm"]
+    g_ms = sum(s["ms"] for s in gemm)
+    g_calls = sum(s["calls"] for s in gemm)
+    g_flops = sum(s["flops"] for s in gemm)
+    g_bytes = sum(s["bytes"] for s in gemm)
+    all_ms = sum(s["ms"] for s in stats)
+    achieved = g_flops / (g_ms * 1e-3) / 1e12 if g_ms > 0 else 0.0
+    peak = PEAK_TFLOPS[precision]
+    # per-layer roofline: each conv launch is bounded by max(flops / MFMA
+    # peak, algorithmic bytes / HBM peak); layer_frac = sum of those bounds
+    # over the measured conv time (1.0 = every conv at its own roofline)
+    t_roof = sum(max(s["flops"] / (peak * 1e12), s["bytes"] / (PEAK_HBM_GBS * 1e9)) for s in gemm)
+    n_hbm = sum(1 for s in gemm if s["bytes"] / (PEAK_HBM_GBS * 1e9) > s["flops"] / (peak * 1e12))
+    # the MFMA-bound 3x3 convs on their own (north_star: >= 0.6 of the fp16 MFMA roofline on the 3x3 hot path)
+    mf = [s for s in gemm if s["flops"] / (peak * 1e12) >= s["bytes"] / (PEAK_HBM_GBS * 1e9)]
+    mf_ms = sum(s["ms"] for s in mf)
+    mf_fl = sum(s["flops"] for s in mf)
+    return {
+        "bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
+        "traffic": traffic["bytes_per_launch"] if traffic else None,
+        "traffic_unit": "bytes per conv launch (rocprofv3 FETCH_SIZE*2 + WRITE_SIZE; N=1 only, per rank)",
+        "traffic_per_img_GB": traffic["bytes_per_forward"] / B / 1e9 if traffic else None,
+        "alg_bytes_per_launch": g_bytes / max(g_calls, 1),
+        "kernel": "conv family: " + "/".join(k[:-7] for k in CONV_KERNELS) + " (all conv launches of the step)",
+        "profiled_steps": 1,
+        "launches_per_step": g_calls,
+        "avg_launch_us": 1000.0 * g_ms / max(g_calls, 1),
+        "gemm_gflop_per_img": g_flops / B / 1e9,
+        "gemm_alg_GB_per_img": g_bytes / B / 1e9,
+        "gemm_share_of_device_time": g_ms / all_ms if all_ms else None,
+        "layer_roofline_frac": (t_roof * 1e3) / g_ms if g_ms > 0 else None,
+        "layer_roofline_note": f"sum over conv launches of max(flops/MFMA peak, alg bytes/HBM peak) / measured; "
+                               f"{n_hbm} of {len(gemm)} conv ops are HBM-bound at {precision}",
+        "mfma_bound_layers": {"launches": len(mf), "ms": mf_ms,
+                              "achieved_TFLOPs": mf_fl / (mf_ms * 1e-3) / 1e12 if mf_ms > 0 else None,
+                              "frac": mf_fl / (mf_ms * 1e-3) / 1e12 / peak if mf_ms > 0 else None},
+    }
+
+
+def forward_leg(args, world, rank, dev, precision, variant, B, S, traffic, cpu_sample):
+    """One forward config: build the seeded model, time `args.steps` forwards of
+    this rank's resident shard, report roofline / parity / CPU baseline."""
+    from models.model import UP_Retinex
+    pre = aspp = variant == "preact_aspp"
+    torch.manual_seed(0)
+    model = UP_Retinex(use_preact=pre, use_aspp=aspp).eval()
+    sd_cpu = {k: v.clone() for k, v in model.state_dict().items()}
+    dt = torch.float16 if precision == "fp16" else torch.float32
+    model = model.to(dev)
+    if precision == "fp16":
+        model = model.half()
+    x = torch.rand(B, 3, S, S, generator=torch.Generator().manual_seed(1 + rank)).to(dev, dt)
+    collect = collect_fn(args.collect)
+
+    def step():
+        with torch.no_grad():
+            out = model(x)
+            if collect is not None:  # SURVEY §8e final collect: fp16 enhanced images
+                collect(out[0].half(), world * B)
+            return out
+
+    step()
+    torch.cuda.synchronize()
+    handle = next(iter(model.__dict__["_upr_cache"].values()))[1]
+    # per-launch HIP events in the LAST timed step only: events around every
+    # launch of every step cost ~5% of the fp16 step (two event packets per launch)
+    prof = None if args.no_profile else handle.profile
+    elapsed, last = timed_loop(world, dev, args.steps, args.warmup, step, prof)
+    stats = handle.profile_read() if not args.no_profile else []
+    handle.profile(False)
+    total = world * B * args.steps
+    out = {
+        "metric": f"images/sec at {S}x{S} bs={B} per GPU (UP-Retinex forward)",
+        "value": total / elapsed, "unit": "images/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None,
+        "dtype": "f32" if precision == "fp32" else "f16 (fp32 accumulate)",
+        "data": "synthetic torch.rand inputs, random-init weights (torch.manual_seed(0))",
+        "config": {"workload": f"configs[{_cfg_index(precision, variant, S)}]: bs={B}/GPU {S}x{S} "
+                               f"{variant} forward, {precision}",
+                   "global_batch": world * B, "image_size": S, "variant": variant,
+                   "parallelism": f"batch-shard x{world} " + {
+                       "none": "(no data-path collective)",
+                       "all": "(+ timed final collect: RCCL all_gather_into_tensor of fp16 enhanced to every rank)",
+                       "rank0": "(+ timed final collect: RCCL gather of fp16 enhanced to rank 0)"}[args.collect]},
+    }
+    if stats:
+        rf = conv_roofline(stats, precision, B, traffic)
+        rf["ref_equiv_tflops"] = REF_GFLOP_PER_IMG[variant] * (S / 512) ** 2 * total / world / elapsed / 1e3
+        if args.ceilings:
+            from upr.calib import measure
+            cz = measure(dev)
+            mf = cz["mfma_f16_TF"] if precision == "fp16" else 155.0  # fp32: MI355X_MICROARCH.md measured
+            hb = max(cz["hbm_copy_TBps"] * 1e3, 6290.0)
+            gemm = [s for s in stats if s["kind"] == "conv_igemm"]
+            g_ms = sum(s["ms"] for s in gemm)
+            t_meas = sum(max(s["flops"] / (mf * 1e12), s["bytes"] / (hb * 1e9)) for s in gemm)
+            rf["measured_ceilings"] = {
+                "mfma_TFLOPs": mf, "hbm_GBs": hb, "detail": cz, "frac_vs_measured_mfma": rf["achieved"] / mf,
+                "layer_roofline_frac_vs_measured": (t_meas * 1e3) / g_ms if g_ms > 0 else None,
+                "note": "fp16: best of 1/2 waves per SIMD of back-to-back 16x16x32 MFMAs on random register "
+                        "operands after 2 s of load; HBM: max(this run's best 16-B/lane copy of 1 GiB, "
+                        "MI355X_MICROARCH.md's measured 6.29 TB/s float4 copy)"}
+        out["roofline"] = rf
+        if args.breakdown and rank == 0:
+            for s in stats:
+                tf = s["flops"] / (s["ms"] * 1e-3) / 1e12 if s["ms"] else 0
+                gbs = s["bytes"] / (s["ms"] * 1e-3) / 1e9 if s["ms"] else 0
+                print(f"{s['name']:44s} {s['kind']:10s} {s['ms'] / max(s['calls'], 1):9.3f} ms "
+                      f"{tf:8.1f} TF/s {gbs:8.1f} GB/s", file=sys.stderr)
     if rank == 0:
-        print(json.dumps({"metric": "dry run (no GPU work)", "value": world * args.steps / elapsed, "unit": "steps/s",
-                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-                          "ms_per_step": 1000.0 * elapsed / args.steps, "ranks": ranks, "data": "none"}))
-    if world > 1:
-        torch.distributed.destroy_process_group()
+        out["parity"] = parity_vs_cpu(sd_cpu, pre, aspp, x, last, precision)
+        if world == 1 and args.cpu_seconds > 0 and cpu_sample:
+            n, note = cpu_sample
+            out["cpu_baseline"] = cpu_baseline(sd_cpu, pre, aspp, S, n, note)
+    del model, x, last
+    torch.cuda.empty_cache()
+    return out
 
 
-TRAIN_GFLOP_PER_IMG = 668.0  # SURVEY.md §8(d): model fwd+bwd + VGG19 fwd x2 + dgrad, 512x512
+# ----------------------------------------------------------------------------
+# training leg (configs[4])
+# ----------------------------------------------------------------------------
+def train_roofline(recs, step_ms, B, S):
+    """Convs of the profiled step against the peak of the arithmetic they ran
+    in (fp16 MFMA under autocast, fp32 MFMA otherwise); the rest of the step
+    (BatchNorm, ReLU masks, casts, losses, FFTs, clip + Adam: fp32, memory
+    bound) is reported as its time, not against an MFMA peak."""
+    by = {}
+    for kind, what, fl, ms in recs:
+        d = by.setdefault(kind, {"ms": 0.0, "gflop": 0.0, "calls": 0})
+        d["ms"] += ms
+        d["gflop"] += fl / 1e9
+        d["calls"] += 1
+    for k, d in by.items():
+        d["TFLOPs"] = d["gflop"] / d["ms"] if d["ms"] > 0 else None  # GF / ms = TF/s
+        d["peak"] = PEAK_TFLOPS["fp16"] if k == "mfma16" else PEAK_TFLOPS["fp32"]
+        d["frac"] = d["TFLOPs"] / d["peak"] if d["TFLOPs"] else None
+    main = "mfma16" if "mfma16" in by else "mfma32"
+    conv_ms = sum(d["ms"] for d in by.values())
+    m = by.get(main, {"ms": 0.0, "gflop": 0.0})
+    ach = m["gflop"] / m["ms"] if m["ms"] else 0.0
+    peak = PEAK_TFLOPS["fp16" if main == "mfma16" else "fp32"]
+    return {"bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s", "frac": ach / peak, "traffic": None,
+            "kernel": f"{main} conv calls of one profiled step (forward, input gradient, weight gradient; each call "
+                      f"timed with HIP events around its library call(s), algorithmic flops)",
+            "by_arithmetic": by,
+            "step_ms": step_ms, "conv_ms": conv_ms,
+            "non_conv_ms": step_ms - conv_ms,
+            "non_conv_note": "BatchNorm stats/apply, ReLU masks, fp32<->fp16 casts, pooling, losses, FFTs, "
+                             "clip + Adam: fp32 memory-bound passes, not priced against an MFMA peak",
+            "whole_step_TFLOPs": TRAIN_GFLOP_PER_IMG * (S / 512.0) ** 2 * B / step_ms,
+            "whole_step_frac_fp16_peak": TRAIN_GFLOP_PER_IMG * (S / 512.0) ** 2 * B / step_ms / PEAK_TFLOPS["fp16"]}
 
 
-def cpu_train_baseline(sd, size, budget_s):
-    """Oracle training step (oracle/train.py, torch-CPU fp32) on 1 image until the budget is spent."""
-    from oracle import train as otrain
-    threads = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
-    vgg = otrain.vgg19_state(1234)
-    x = torch.rand(1, 3, size, size, generator=torch.Generator().manual_seed(98))
-    n, t0 = 0, time.perf_counter()
-    while True:
-        sdc = {k: v.clone() for k, v in sd.items()}
-        otrain.train_step(sdc, vgg, x, False, False)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or n >= 16:
-            break
-    return {"value": n / el, "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{n} x 1x3x{size}x{size} training steps of oracle/train.py (torch-CPU autograd), {el:.1f}s"}
-
-
-def train_main(args):
-    world, rank, dev = dist_setup(args)
+def train_leg(args, world, rank, dev, B, S, amp, steps, warmup, variant):
     from models.model import UP_Retinex
     from losses.loss import TotalLoss
     from trainers.train import make_optimizer, train_step
-    B = args.batch if args.batch != 32 else 8
-    S = args.size
+    from upr import train as T
     torch.manual_seed(0)
-    model = UP_Retinex(use_preact=args.variant == "preact_aspp", use_aspp=args.variant == "preact_aspp")
+    model = UP_Retinex(use_preact=variant == "preact_aspp", use_aspp=variant == "preact_aspp")
     sd_cpu = {k: v.clone() for k, v in model.state_dict().items()}
     model = model.to(dev).train()
     crit = TotalLoss(use_freq_loss=True).to(dev)
@@ -297,201 +506,121 @@ def train_main(args):
     x = torch.rand(B, 3, S, S, generator=torch.Generator().manual_seed(2 + rank)).to(dev)
     from upr.dist import allreduce_grads
     scaler = None
-    if args.amp:
+    if amp:
         from trainers.train import GradScaler
         scaler = GradScaler()
 
     def tstep():
-        if world == 1:
-            return train_step(model, x, crit, opt, scaler=scaler, use_amp=args.amp)
-        return train_step(model, x, crit, opt, scaler=scaler, use_amp=args.amp,
-                          grad_hook=lambda: allreduce_grads(opt))
+        hook = (lambda: allreduce_grads(opt)) if world > 1 else None
+        return train_step(model, x, crit, opt, scaler=scaler, use_amp=amp, grad_hook=hook)
 
-    for _ in range(args.warmup):
-        tstep()
-    sync(world, dev)
+    elapsed, last = timed_loop(world, dev, steps, warmup, tstep)
+    # one more (untimed) step with per-conv HIP events for the roofline split
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
-    d = None
-    for _ in range(args.steps):
-        _, d = tstep()
-    sync(world, dev)
-    elapsed = max_over_ranks(world, dev, time.perf_counter() - t0)
-    imgs = world * B * args.steps
-    gf = TRAIN_GFLOP_PER_IMG * (S / 512.0) ** 2
-    achieved = gf * B * args.steps / elapsed / 1e3
+    T.profile_begin()
+    tstep()
+    recs = T.profile_end()
+    prof_ms = 1000.0 * (time.perf_counter() - t0)
+    step_ms = 1000.0 * elapsed / steps
+    imgs = world * B * steps
     out = {
         "metric": f"train images/sec at {S}x{S} bs={B} (UP-Retinex fwd + TotalLoss + bwd + clip + Adam)",
-        "value": imgs / elapsed, "unit": "images/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True,
+        "value": imgs / elapsed, "unit": "images/s", "n_gpus": world, "steps": steps,
+        "warmup": warmup, "ms_per_step": step_ms, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None,
-        "dtype": "f16 convs under autocast (fp32 accumulate; fp16-operand weight gradients; fp32 BN / loss / Adam)" if args.amp else "f32",
+        "dtype": "f16 convs under autocast (fp32 accumulate; fp16-operand weight gradients; fp32 BN / loss / Adam)"
+                 if amp else "f32",
         "data": "synthetic torch.rand inputs, random-init weights (seed 0), seeded random-init VGG19 (seed 1234)",
-        "config": {"workload": f"configs[4]: bs={B}/GPU {S}x{S} {args.variant} train step"
-                               + (" AMP: autocast (fp16 MFMA convs) + GradScaler" if args.amp else " (fp32)"),
-                   "global_batch": world * B, "image_size": S, "variant": args.variant,
+        "config": {"workload": f"configs[4]: bs={B}/GPU {S}x{S} {variant} train step"
+                               + (" AMP: autocast (fp16 MFMA convs) + GradScaler" if amp else " (fp32)"),
+                   "global_batch": world * B, "image_size": S, "variant": variant,
                    "parallelism": f"data-parallel x{world} (per-rank shard"
                                   + (", RCCL all-reduce of the flat gradient buffer)" if world > 1 else ")")},
-        "last_loss": d,
-        "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_TFLOPS["fp32"], "unit": "TFLOP/s",
-                     "frac": achieved / PEAK_TFLOPS["fp32"], "traffic": None,
-                     "kernel": "whole training step (algorithmic 668 GF/img at 512^2 over step time)"},
+        "last_loss": last[1] if last is not None else None,
+        "roofline": train_roofline(recs, step_ms, B, S),
+        "profiled_step_wall_ms": prof_ms,
     }
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        out["cpu_baseline"] = cpu_train_baseline(sd_cpu, S, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_train_baseline(sd_cpu, S)
+    del model, x, opt, crit
+    torch.cuda.empty_cache()
+    return out
+
+
+# ----------------------------------------------------------------------------
+# dry run: the same launch / rank / report path with a CPU stand-in step
+# ----------------------------------------------------------------------------
+def dry_run(args):
+    world, rank, dev = dist_setup(args)
+    torch.manual_seed(rank)
+    a = [torch.rand(256, 256)]
+
+    def step():
+        a[0] = torch.tanh(a[0] @ a[0].T / 256)
+        col = collect_fn(args.collect)
+        if col is not None:
+            col(a[0][:4].half(), 4 * world)
+        return a[0]
+
+    elapsed, _ = timed_loop(world, dev, args.steps, args.warmup, step)
+    ranks = [None] * world
+    if world > 1:
+        torch.distributed.all_gather_object(ranks, (rank, os.getpid()))
+    else:
+        ranks = [(rank, os.getpid())]
     if rank == 0:
+        stand_in = {"value": None, "note": "dry run: no GPU work"}
+        out = {"metric": "dry run (no GPU work)", "value": world * args.steps / elapsed, "unit": "steps/s",
+               "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": 1000.0 * elapsed / args.steps, "ranks": ranks, "data": "none",
+               "config": {"parallelism": f"batch-shard x{world} collect={args.collect}"},
+               "roofline": dict(stand_in, traffic=None), "parity": dict(stand_in, max_abs_diff=None)}
+        if world == 1:
+            out["cpu_baseline"] = dict(stand_in, cpu=cpu_info())
+        if not args.no_nested:
+            out["fp16_preact_aspp"] = {"value": None, "roofline": None, "parity": dict(stand_in)}
+            if world == 1:
+                out["train_amp"] = {"value": None, "roofline": None}
         print(json.dumps(out))
     if world > 1:
         torch.distributed.destroy_process_group()
 
 
-def _cfg_index(args):
-    """BASELINE.json configs[] entry a forward run corresponds to."""
-    if args.size == 1024 and args.variant == "preact_aspp":
-        return 3  # bs=256 1024^2 over 8 GPUs = 32 per GPU
-    return 1 if args.precision == "fp32" and args.variant == "plain" else 2
-
-
+# ----------------------------------------------------------------------------
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args))
     if args.dry_run:
         return dry_run(args)
-    if args.train:
-        return train_main(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    traffic = None
+    if args.train:
+        world, rank, dev = dist_setup(args)
+        out = train_leg(args, world, rank, dev, args.batch if args.batch != 32 else 8, args.size, args.amp,
+                        args.steps, args.warmup, args.variant)
+        if rank == 0:
+            print(json.dumps(out))
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
+    nested = not args.no_nested and not (args.precision == "fp16" and args.variant == "preact_aspp")
+    traffic = traffic16 = None
     if world == 1 and not args.no_traffic and not any(k.startswith("ROCPROF") for k in os.environ):
-        traffic = pmc_traffic(args)  # child processes, before this process initialises the GPU
+        # child processes, before this process initialises the GPU
+        traffic = pmc_traffic(args.precision, args.variant, args.batch, args.size)
+        if nested:
+            traffic16 = pmc_traffic("fp16", "preact_aspp", args.batch, args.size)
     world, rank, dev = dist_setup(args)
-
-    from models.model import UP_Retinex
-    pre = aspp = args.variant == "preact_aspp"
-    torch.manual_seed(0)
-    model = UP_Retinex(use_preact=pre, use_aspp=aspp).eval()
-    sd_cpu = {k: v.clone() for k, v in model.state_dict().items()}
-    dt = torch.float16 if args.precision == "fp16" else torch.float32
-    model = model.to(dev)
-    if args.precision == "fp16":
-        model = model.half()
     B, S = args.batch, args.size
-    g = torch.Generator().manual_seed(1 + rank)
-    x = torch.rand(B, 3, S, S, generator=g).to(dev, dt)
-
-    collect = None
-    if args.collect:
-        from upr.dist import gather_shards
-        collect = gather_shards
-
-    gathered = [None]
-
-    def step():
-        with torch.no_grad():
-            out = model(x)
-            if collect is not None:  # SURVEY §8e final collect: fp16 enhanced images of every rank
-                gathered[0] = collect(out[0].half(), world * B)
-            return out
-
-    last = [None]
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    handle = next(iter(model.__dict__["_upr_cache"].values()))[1]
-
-    # The per-launch HIP events of the roofline are recorded in the LAST timed
-    # step only (a sample inside the timed region): events around every launch
-    # of every step cost ~5% of the fp16 step (two event packets per launch).
-    sync(world, dev)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        if i == args.steps - 1 and not args.no_profile:
-            handle.profile(True)
-        last[0] = step()
-    sync(world, dev)
-    elapsed = time.perf_counter() - t0
-    stats = handle.profile_read() if not args.no_profile else []
-    handle.profile(False)
-    elapsed = max_over_ranks(world, dev, elapsed)
-
-    total_imgs = world * B * args.steps
-    out = {
-        "metric": f"images/sec at {S}x{S} bs={B} per GPU (UP-Retinex forward)",
-        "value": total_imgs / elapsed,
-        "unit": "images/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": 1000.0 * elapsed / args.steps,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f32" if args.precision == "fp32" else "f16 (fp32 accumulate)",
-        "data": "synthetic torch.rand inputs, random-init weights (torch.manual_seed(0))",
-        "config": {"workload": f"configs[{_cfg_index(args)}]: bs={B}/GPU {S}x{S} "
-                               f"{args.variant} forward, {args.precision}",
-                   "global_batch": world * B, "image_size": S, "variant": args.variant,
-                   "parallelism": f"batch-shard x{world} " + (
-                       "(+ timed final collect: RCCL all_gather_into_tensor of fp16 enhanced)" if args.collect
-                       else "(no data-path collective)")},
-    }
-    if stats:
-        gemm = [s for s in stats if s["kind"] == "conv_igemm"]
-        g_ms = sum(s["ms"] for s in gemm)
-        g_calls = sum(s["calls"] for s in gemm)
-        g_flops = sum(s["flops"] for s in gemm)
-        g_bytes = sum(s["bytes"] for s in gemm)
-        all_ms = sum(s["ms"] for s in stats)
-        achieved = g_flops / (g_ms * 1e-3) / 1e12 if g_ms > 0 else 0.0
-        peak = PEAK_TFLOPS[args.precision]
-        # per-layer roofline: each conv launch is bounded by max(flops / MFMA
-        # peak, algorithmic bytes / HBM peak); layer_frac = sum of those bounds
-        # over the measured conv time (1.0 = every conv at its own roofline)
-        t_roof = sum(max(s["flops"] / (peak * 1e12), s["bytes"] / (PEAK_HBM_GBS * 1e9)) for s in gemm)
-        n_hbm = sum(1 for s in gemm if s["bytes"] / (PEAK_HBM_GBS * 1e9) > s["flops"] / (peak * 1e12))
-        out["roofline"] = {
-            "bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
-            "traffic": traffic["bytes_per_launch"] if traffic else None,
-            "traffic_unit": "bytes per conv launch (rocprofv3 FETCH_SIZE*2 + WRITE_SIZE)",
-            "traffic_per_img_GB": traffic["bytes_per_forward"] / B / 1e9 if traffic else None,
-            "alg_bytes_per_launch": g_bytes / max(g_calls, 1),
-            "kernel": "conv family: " + "/".join(k[:-7] for k in CONV_KERNELS) + " (all conv launches of the step)",
-            "profiled_steps": 1,
-            "launches_per_step": g_calls,
-            "avg_launch_us": 1000.0 * g_ms / max(g_calls, 1),
-            "gemm_gflop_per_img": g_flops / B / 1e9,
-            "gemm_alg_GB_per_img": g_bytes / B / 1e9,
-            "gemm_share_of_device_time": g_ms / all_ms if all_ms else None,
-            "layer_roofline_frac": (t_roof * 1e3) / g_ms if g_ms > 0 else None,
-            "layer_roofline_note": f"sum over conv launches of max(flops/MFMA peak, alg bytes/HBM peak) / measured; "
-                                   f"{n_hbm} of {len(gemm)} conv ops are HBM-bound at {args.precision}",
-            "ref_equiv_tflops": REF_GFLOP_PER_IMG[args.variant] * (S / 512) ** 2 * total_imgs / world / elapsed / 1e3,
-        }
-        if args.ceilings:
-            from upr.calib import measure
-            cz = measure(dev)
-            # fp32 MFMA: MI355X_MICROARCH.md's measured 155 TF (99% of nominal), not re-measured here
-            mf = cz["mfma_f16_TF"] if args.precision == "fp16" else 155.0
-            # HBM: the better of this run's copy kernel and the guide's measured float4 copy (6.29 TB/s)
-            hb = max(cz["hbm_copy_TBps"] * 1e3, 6290.0)
-            t_meas = sum(max(s["flops"] / (mf * 1e12), s["bytes"] / (hb * 1e9)) for s in gemm)
-            out["roofline"]["measured_ceilings"] = {
-                "mfma_TFLOPs": mf, "hbm_GBs": hb, "detail": cz,
-                "frac_vs_measured_mfma": achieved / mf,
-                "layer_roofline_frac_vs_measured": (t_meas * 1e3) / g_ms if g_ms > 0 else None,
-                "note": "fp16: best of 1/2 waves per SIMD of back-to-back 16x16x32 MFMAs on random register "
-                        "operands after 2 s of load (DVFS-settled clock), measured in this process right after the timed "
-                        "steps; HBM: max(this run's best 16-B/lane copy of 1 GiB, read + write, and "
-                        "MI355X_MICROARCH.md's measured 6.29 TB/s float4 copy)"}
-        if args.breakdown and rank == 0:
-            for s in stats:
-                tf = s["flops"] / (s["ms"] * 1e-3) / 1e12 if s["ms"] else 0
-                gbs = s["bytes"] / (s["ms"] * 1e-3) / 1e9 if s["ms"] else 0
-                print(f"{s['name']:44s} {s['kind']:10s} {s['ms'] / max(s['calls'], 1):9.3f} ms "
-                      f"{tf:8.1f} TF/s {gbs:8.1f} GB/s", file=sys.stderr)
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        out["cpu_baseline"] = cpu_baseline(sd_cpu, pre, aspp, S, args.cpu_seconds, B)
-        out["parity"] = parity_vs_cpu(sd_cpu, pre, aspp, x, last[0], args.precision)
+    out = forward_leg(args, world, rank, dev, args.precision, args.variant, B, S, traffic,
+                      (B, "the full timed batch"))
+    if nested:
+        n16 = min(B, 8)
+        out["fp16_preact_aspp"] = forward_leg(args, world, rank, dev, "fp16", "preact_aspp", B, S, traffic16,
+                                              (n16, f"a bounded {n16}-image sample of the timed batch's shape"))
+        if world == 1:
+            out["train_amp"] = train_leg(args, world, rank, dev, 8, S, True, 5, 2, "plain")
     if rank == 0:
         print(json.dumps(out))
     if world > 1:

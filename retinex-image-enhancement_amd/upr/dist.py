@@ -50,6 +50,29 @@ def gather_shards(local, total, group=None):
     return torch.cat(keep)
 
 
+def gather_to_rank0(local, total, group=None, dst=0):
+    """Collect every rank's shard on rank `dst` only ("gather to
+    rank 0 if only rank 0 writes"): one gather, so the fabric carries each
+    shard once instead of to every rank as the all-gather does.  Returns the
+    [total, ...] tensor on `dst`, None elsewhere.  Shards are padded to the
+    largest size (dist.gather needs equal shapes); padding is dropped."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    per = -(-total // world)
+    pad = per - local.shape[0]
+    buf = local if pad == 0 else torch.cat([local, local.new_zeros((pad,) + tuple(local.shape[1:]))])
+    buf = buf.contiguous()
+    parts = [torch.empty_like(buf) for _ in range(world)] if rank == dst else None
+    dist.gather(buf, parts, dst=dst, group=group)
+    if rank != dst:
+        return None
+    keep = []
+    for r, p in enumerate(parts):
+        a, b = shard_bounds(total, world, r)
+        keep.append(p[: b - a])
+    return torch.cat(keep)
+
+
 def sharded_forward(model, x_local, total, collect=False, collect_dtype=None):
     """Run this rank's shard; optionally all-gather the enhanced images."""
     with torch.no_grad():

@@ -71,6 +71,50 @@ def _h16(n, dev):
     return torch.empty((n,), dtype=torch.float16, device=dev)
 
 
+# Per-call device timing of the conv launches (bench.py's training roofline).
+# While profile_begin() is active every conv call below records a HIP event
+# pair on the current stream around its library call(s), tagged with its
+# arithmetic ("mfma16": fp16 MFMA with fp32 accumulation, "mfma32": fp32
+# MFMA, "direct": FMA kernels) and its ALGORITHMIC flops 2*B*Ho*Wo*Cout*Cin*k^2
+# (forward, input gradient and weight gradient each count one such product;
+# the zero-upsampled stride-2 input gradient executes 4x that and is charged 1x).
+_PROF = [None]
+
+
+def profile_begin():
+    _PROF[0] = []
+
+
+def profile_end():
+    """Stops recording; returns [(kind, what, flops, ms)] (synchronises)."""
+    recs, _PROF[0] = _PROF[0], None
+    if not recs:
+        return []
+    torch.cuda.synchronize()
+    return [(k, w, f, e0.elapsed_time(e1)) for k, w, f, e0, e1 in recs]
+
+
+class _timed:
+    __slots__ = ("rec",)
+
+    def __init__(self, kind, what, flops):
+        self.rec = None
+        if _PROF[0] is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            self.rec = [kind, what, flops, e0, e1]
+
+    def __enter__(self):
+        if self.rec is not None:
+            self.rec[3].record()
+        return self
+
+    def __exit__(self, *exc):
+        if self.rec is not None:
+            self.rec[4].record()
+            _PROF[0].append(tuple(self.rec))
+        return False
+
+
 class Act:
     """NHWC activation: channels [coff, coff+C) of a [B,H,W,cs] fp32 tensor.
 
@@ -248,6 +292,18 @@ class Conv:
         out.fresh = False
         out.t16 = None  # any fp16 copy of an earlier content is stale now
         self.amp = _AMP[0] and self.mfma and x_view is None
+        kind = "mfma16" if self.amp else ("mfma32" if self.mfma and x_view is None else "direct")
+        with _timed(kind, "fwd", self.flops(B, Ho, Wo)):
+            self._fwd(x, B, H, W, Ho, Wo, relu, out, res, x_view)
+        return out
+
+    def flops(self, B, Ho, Wo):
+        return 2.0 * B * Ho * Wo * self.Cout * self.Cin * self.kh * self.kw
+
+    def _fwd(self, x, B, H, W, Ho, Wo, relu, out, res, x_view):
+        lib, st = L.lib(), _stream()
+        if x_view is not None:
+            xv = x_view[0]
         if self.amp:
             # the fp16 copy of x is the weight gradient's B operand (upr_t_conv_wgrad16)
             whole = x.coff == 0 and x.C == x.cs == self.Cin
@@ -268,7 +324,6 @@ class Conv:
             _chk(lib.upr_t_conv_direct(ctypes.byref(v), B, H, W, self.Cin, _p(self.m.weight), _p(self.bias),
                                        self.Cout, self.kh, self.kw, self.s, self.p, self.d,
                                        ctypes.byref(out.view()), Ho, Wo, int(relu), 0, st), "conv_direct")
-        return out
 
     def bwd(self, x, gy, gx=None, x_view=None):
         """gy: Act gradient of this conv's output (pre-activation).
@@ -280,55 +335,60 @@ class Conv:
         else:
             B, H, W = x.B, x.H, x.W
         Ho, Wo = gy.H, gy.W
-        if not self.frozen:
-            gw = self.m.weight.grad
-            if self.mfma and x_view is None:
-                zero(self.gp)
-                x16 = getattr(self, "x16", None)
-                if self.amp and x16 is not None:
-                    # autocast: fp16 operands, fp32 accumulation (trainers/train.py:72)
-                    _chk(lib.upr_t_conv_wgrad16(_fp(x.t), _p(x16), B, H, W, self.Cin, x.cs, x.coff, _fp(gy.t), Ho,
-                                                Wo, self.Cout, gy.cs, gy.coff, self.kh, self.kw, self.s, self.p,
-                                                self.d, _p(self.gp), st), "conv_wgrad16")
-                    self.x16 = None
+        F = self.flops(B, Ho, Wo)
+        mf = self.mfma and x_view is None
+        kw_ = ("mfma16" if self.amp and getattr(self, "x16", None) is not None else "mfma32") if mf else "direct"
+        with _timed(kw_, "wgrad", 0.0 if self.frozen else F):
+            if not self.frozen:
+                gw = self.m.weight.grad
+                if self.mfma and x_view is None:
+                    zero(self.gp)
+                    x16 = getattr(self, "x16", None)
+                    if self.amp and x16 is not None:
+                        # autocast: fp16 operands, fp32 accumulation (trainers/train.py:72)
+                        _chk(lib.upr_t_conv_wgrad16(_fp(x.t), _p(x16), B, H, W, self.Cin, x.cs, x.coff, _fp(gy.t), Ho,
+                                                    Wo, self.Cout, gy.cs, gy.coff, self.kh, self.kw, self.s, self.p,
+                                                    self.d, _p(self.gp), st), "conv_wgrad16")
+                        self.x16 = None
+                    else:
+                        _chk(lib.upr_t_conv_wgrad(_fp(x.t), B, H, W, self.Cin, x.cs, x.coff, _fp(gy.t), Ho, Wo,
+                                                  self.Cout, gy.cs, gy.coff, self.kh, self.kw, self.s, self.p, self.d,
+                                                  _p(self.gp), st), "conv_wgrad")
+                    _chk(lib.upr_t_unpack_grad(_p(self.gp), _p(gw), self.Cout, self.Cin, self.kh, self.kw, 0, 1, st),
+                         "unpack")
+                    if self.bias is not None:
+                        _chk(lib.upr_t_chan_sum(gy.ptr(), gy.M, self.Cout, gy.cs, 0, _p(self.bias.grad), 1, st), "dbias")
                 else:
-                    _chk(lib.upr_t_conv_wgrad(_fp(x.t), B, H, W, self.Cin, x.cs, x.coff, _fp(gy.t), Ho, Wo,
-                                              self.Cout, gy.cs, gy.coff, self.kh, self.kw, self.s, self.p, self.d,
-                                              _p(self.gp), st), "conv_wgrad")
-                _chk(lib.upr_t_unpack_grad(_p(self.gp), _p(gw), self.Cout, self.Cin, self.kh, self.kw, 0, 1, st),
-                     "unpack")
-                if self.bias is not None:
-                    _chk(lib.upr_t_chan_sum(gy.ptr(), gy.M, self.Cout, gy.cs, 0, _p(self.bias.grad), 1, st), "dbias")
-            else:
-                v = x.view() if x_view is None else xv
-                _chk(lib.upr_t_conv_direct_wgrad(ctypes.byref(v), ctypes.byref(gy.view()), B, H, W, self.Cin, Ho, Wo,
-                                                 self.Cout, self.kh, self.kw, self.s, self.p, self.d, _p(gw),
-                                                 _p(self.bias.grad) if self.bias is not None else None, st),
-                     "conv_direct_wgrad")
+                    v = x.view() if x_view is None else xv
+                    _chk(lib.upr_t_conv_direct_wgrad(ctypes.byref(v), ctypes.byref(gy.view()), B, H, W, self.Cin, Ho, Wo,
+                                                     self.Cout, self.kh, self.kw, self.s, self.p, self.d, _p(gw),
+                                                     _p(self.bias.grad) if self.bias is not None else None, st),
+                         "conv_direct_wgrad")
         if gx is None:
             return
-        if self.mfma:
-            acc = gx.consume_fresh()
-            src, sH, sW, scs, scoff = gy.t, Ho, Wo, gy.cs, gy.coff
-            if self.s != 1:
-                assert self.s == 2 and H == 2 * Ho and W == 2 * Wo, "stride-2 dgrad needs even sizes"
-                z = empty((B, H, W, self.Cout), gy.t.device)
-                _chk(lib.upr_t_zero_upsample(_fp(gy.t), B, Ho, Wo, self.Cout, gy.cs, gy.coff,
-                                             _p(z), st), "zero_upsample")
-                src, sH, sW, scs, scoff = z, H, W, self.Cout, 0
-            pad_t = self.d * (self.kh - 1) - self.p
-            if self.amp:
-                self._mfma16(src, B, sH, sW, self.Cout, scs, scoff, self.wt16, None, self.Cin, self.kh, self.kw, 1,
-                             pad_t, self.d, gx if acc else None, False, gx)
+        with _timed("mfma16" if self.amp else ("mfma32" if self.mfma else "direct"), "dgrad", F):
+            if self.mfma:
+                acc = gx.consume_fresh()
+                src, sH, sW, scs, scoff = gy.t, Ho, Wo, gy.cs, gy.coff
+                if self.s != 1:
+                    assert self.s == 2 and H == 2 * Ho and W == 2 * Wo, "stride-2 dgrad needs even sizes"
+                    z = empty((B, H, W, self.Cout), gy.t.device)
+                    _chk(lib.upr_t_zero_upsample(_fp(gy.t), B, Ho, Wo, self.Cout, gy.cs, gy.coff,
+                                                 _p(z), st), "zero_upsample")
+                    src, sH, sW, scs, scoff = z, H, W, self.Cout, 0
+                pad_t = self.d * (self.kh - 1) - self.p
+                if self.amp:
+                    self._mfma16(src, B, sH, sW, self.Cout, scs, scoff, self.wt16, None, self.Cin, self.kh, self.kw, 1,
+                                 pad_t, self.d, gx if acc else None, False, gx)
+                else:
+                    _chk(lib.upr_t_conv_mfma(_fp(src), B, sH, sW, self.Cout, scs, scoff, _p(self.wt), None, self.Cin,
+                                             self.kh, self.kw, 1, pad_t, self.d, gx.ptr() if acc else None,
+                                             gx.cs if acc else 0, 0, _fp(gx.t), gx.cs, gx.coff, 0, st), "conv_dgrad")
             else:
-                _chk(lib.upr_t_conv_mfma(_fp(src), B, sH, sW, self.Cout, scs, scoff, _p(self.wt), None, self.Cin,
-                                         self.kh, self.kw, 1, pad_t, self.d, gx.ptr() if acc else None,
-                                         gx.cs if acc else 0, 0, _fp(gx.t), gx.cs, gx.coff, 0, st), "conv_dgrad")
-        else:
-            acc = gx.consume_fresh()
-            _chk(lib.upr_t_conv_direct_dgrad(ctypes.byref(gy.view()), Ho, Wo, _p(self.m.weight), B, H, W, self.Cin,
-                                             self.Cout, self.kh, self.kw, self.s, self.p, self.d,
-                                             ctypes.byref(gx.view()), acc, st), "conv_direct_dgrad")
+                acc = gx.consume_fresh()
+                _chk(lib.upr_t_conv_direct_dgrad(ctypes.byref(gy.view()), Ho, Wo, _p(self.m.weight), B, H, W, self.Cin,
+                                                 self.Cout, self.kh, self.kw, self.s, self.p, self.d,
+                                                 ctypes.byref(gx.view()), acc, st), "conv_direct_dgrad")
 
 
 class ConvT:
@@ -365,36 +425,44 @@ class ConvT:
     def fwd(self, x):
         out = Act.new(x.B, 2 * x.H, 2 * x.W, self.Cout, x.t.device, fresh=False)
         self.amp = _AMP[0]
-        if self.amp:
-            Conv._mfma16(self, x.t, x.B, x.H, x.W, self.Cin, x.cs, x.coff, self.wp16, self.b4, 4 * self.Cout, 1, 1,
-                         1, 0, 1, None, False, out, store=1)
-        else:
-            _chk(L.lib().upr_t_conv_mfma(x.ptr(), x.B, x.H, x.W, self.Cin, x.cs, 0, _p(self.wp), _p(self.b4),
-                                         4 * self.Cout, 1, 1, 1, 0, 1, None, 0, 0, _fp(out.t), out.cs, 0, 1,
-                                         _stream()), "convT")
+        with _timed("mfma16" if self.amp else "mfma32", "fwd", self.flops(x)):
+            if self.amp:
+                Conv._mfma16(self, x.t, x.B, x.H, x.W, self.Cin, x.cs, x.coff, self.wp16, self.b4, 4 * self.Cout, 1, 1,
+                             1, 0, 1, None, False, out, store=1)
+            else:
+                _chk(L.lib().upr_t_conv_mfma(x.ptr(), x.B, x.H, x.W, self.Cin, x.cs, 0, _p(self.wp), _p(self.b4),
+                                             4 * self.Cout, 1, 1, 1, 0, 1, None, 0, 0, _fp(out.t), out.cs, 0, 1,
+                                             _stream()), "convT")
         return out
+
+    def flops(self, x):
+        return 2.0 * x.B * x.H * x.W * self.Cin * 4 * self.Cout
 
     def bwd(self, x, gy, gx):
         lib, st = L.lib(), _stream()
-        zero(self.gp)
-        # dwp[ci][(a,b,co)] = sum_p x[p][ci] * gy[2y+a][2x+b][co]: a k2 s2 "conv" of gy producing x
-        if self.amp:
-            _chk(lib.upr_t_conv_wgrad16(gy.ptr(), None, gy.B, gy.H, gy.W, self.Cout, gy.cs, 0, x.ptr(), x.H, x.W,
-                                        self.Cin, x.cs, 0, 2, 2, 2, 0, 1, _p(self.gp), st), "convT_wgrad16")
-        else:
-            _chk(lib.upr_t_conv_wgrad(gy.ptr(), gy.B, gy.H, gy.W, self.Cout, gy.cs, 0, x.ptr(), x.H, x.W, self.Cin,
-                                      x.cs, 0, 2, 2, 2, 0, 1, _p(self.gp), st), "convT_wgrad")
-        _chk(lib.upr_t_unpack_grad(_p(self.gp), _p(self.m.weight.grad), self.Cout, self.Cin, 2, 2, 3, 1, st),
-             "unpack")
-        _chk(lib.upr_t_chan_sum(gy.ptr(), gy.M, self.Cout, gy.cs, 0, _p(self.m.bias.grad), 1, st), "dbias")
-        acc = gx.consume_fresh()
-        if self.amp:
-            Conv._mfma16(self, gy.t, gy.B, gy.H, gy.W, self.Cout, gy.cs, gy.coff, self.wd16, None, self.Cin, 2, 2, 2,
-                         0, 1, gx if acc else None, False, gx)
-        else:
-            _chk(lib.upr_t_conv_mfma(gy.ptr(), gy.B, gy.H, gy.W, self.Cout, gy.cs, 0, _p(self.wd), None, self.Cin, 2,
-                                     2, 2, 0, 1, gx.ptr() if acc else None, gx.cs if acc else 0, 0, _fp(gx.t),
-                                     gx.cs, gx.coff, 0, st), "convT_dgrad")
+        F = self.flops(x)
+        kind = "mfma16" if self.amp else "mfma32"
+        with _timed(kind, "wgrad", F):
+            zero(self.gp)
+            # dwp[ci][(a,b,co)] = sum_p x[p][ci] * gy[2y+a][2x+b][co]: a k2 s2 "conv" of gy producing x
+            if self.amp:
+                _chk(lib.upr_t_conv_wgrad16(gy.ptr(), None, gy.B, gy.H, gy.W, self.Cout, gy.cs, 0, x.ptr(), x.H, x.W,
+                                            self.Cin, x.cs, 0, 2, 2, 2, 0, 1, _p(self.gp), st), "convT_wgrad16")
+            else:
+                _chk(lib.upr_t_conv_wgrad(gy.ptr(), gy.B, gy.H, gy.W, self.Cout, gy.cs, 0, x.ptr(), x.H, x.W, self.Cin,
+                                          x.cs, 0, 2, 2, 2, 0, 1, _p(self.gp), st), "convT_wgrad")
+            _chk(lib.upr_t_unpack_grad(_p(self.gp), _p(self.m.weight.grad), self.Cout, self.Cin, 2, 2, 3, 1, st),
+                 "unpack")
+            _chk(lib.upr_t_chan_sum(gy.ptr(), gy.M, self.Cout, gy.cs, 0, _p(self.m.bias.grad), 1, st), "dbias")
+        with _timed(kind, "dgrad", F):
+            acc = gx.consume_fresh()
+            if self.amp:
+                Conv._mfma16(self, gy.t, gy.B, gy.H, gy.W, self.Cout, gy.cs, gy.coff, self.wd16, None, self.Cin, 2, 2, 2,
+                             0, 1, gx if acc else None, False, gx)
+            else:
+                _chk(lib.upr_t_conv_mfma(gy.ptr(), gy.B, gy.H, gy.W, self.Cout, gy.cs, 0, _p(self.wd), None, self.Cin, 2,
+                                         2, 2, 0, 1, gx.ptr() if acc else None, gx.cs if acc else 0, 0, _fp(gx.t),
+                                         gx.cs, gx.coff, 0, st), "convT_dgrad")
 
 
 class BN:

@@ -6,7 +6,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from upr.dist import shard_bounds, gather_shards
+from upr.dist import shard_bounds, gather_shards, gather_to_rank0
 
 
 def test_shard_bounds_cover_exactly():
@@ -34,7 +34,10 @@ def _worker(rank, world, port, total, q):
     full = torch.arange(total * 6, dtype=torch.float32).reshape(total, 2, 3)
     a, b = shard_bounds(total, world, rank)
     got = gather_shards(full[a:b] * 1.0, total)
-    q.put((rank, bool(torch.equal(got, full))))
+    ok = bool(torch.equal(got, full))
+    g0 = gather_to_rank0(full[a:b] * 1.0, total)
+    ok = ok and (bool(torch.equal(g0, full)) if rank == 0 else g0 is None)
+    q.put((rank, ok))
     dist.destroy_process_group()
 
 
@@ -98,3 +101,37 @@ def test_bench_gpus2_launches_two_gloo_ranks():
     ranks = out["ranks"]
     assert sorted(rk for rk, _ in ranks) == [0, 1]
     assert len({pid for _, pid in ranks}) == 2 and os.getpid() not in {pid for _, pid in ranks}
+
+
+def _bench_json(args):
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=240, cwd=repo)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_gpus2_line_carries_evidence_keys():
+    """An N>1 line carries rank 0's parity, the roofline object and the nested
+    fp16 object; cpu_baseline and train_amp are N=1 only; --collect rank0 runs
+    the gather-to-rank-0 collect through the same timed loop (gloo here)."""
+    out = _bench_json(["--gpus", "2", "--dry-run", "--steps", "2", "--warmup", "1", "--collect", "rank0"])
+    assert out["n_gpus"] == 2
+    for k in ("roofline", "parity", "fp16_preact_aspp", "config"):
+        assert k in out, k
+    assert "parity" in out["fp16_preact_aspp"]
+    assert "cpu_baseline" not in out and "train_amp" not in out
+    assert "collect=rank0" in out["config"]["parallelism"]
+
+
+def test_bench_n1_line_carries_cpu_and_train_keys():
+    out = _bench_json(["--dry-run", "--steps", "2", "--warmup", "1"])
+    for k in ("roofline", "parity", "cpu_baseline", "fp16_preact_aspp", "train_amp"):
+        assert k in out, k
+    ci = out["cpu_baseline"]["cpu"]
+    assert ci["threads"] >= 1 and "cpu_model" in ci and ci["os_cpu_count"] >= ci["threads"]
