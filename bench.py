@@ -302,7 +302,8 @@ def max_over_ranks(world, dev, seconds):
 def timed_loop(world, dev, steps, warmup, step, profile_last=None):
     """warmup untimed steps, then `steps` timed ones bracketed by barrier +
     synchronize; returns (max-over-ranks seconds, last step's result).
-    profile_last(True/False) brackets the LAST timed step (per-launch events)."""
+    profile_last(True) is called before the LAST timed step (per-launch
+    events); the caller reads and disables the profile."""
     for _ in range(warmup):
         step()
     sync(world, dev)
@@ -314,13 +315,11 @@ def timed_loop(world, dev, steps, warmup, step, profile_last=None):
         last = step()
     sync(world, dev)
     el = time.perf_counter() - t0
-    if profile_last is not None:
-        profile_last(False)
     return max_over_ranks(world, dev, el), last
 
 
-def collect_fn(mode):
-    if mode == "none":
+def collect_fn(mode, world):
+    if mode == "none" or world == 1:  # one rank: nothing to collect
         return None
     from upr.dist import gather_shards, gather_to_rank0
     return gather_shards if mode == "all" else gather_to_rank0
@@ -389,7 +388,7 @@ def forward_leg(args, world, rank, dev, precision, variant, B, S, traffic, cpu_s
     if precision == "fp16":
         model = model.half()
     x = torch.rand(B, 3, S, S, generator=torch.Generator().manual_seed(1 + rank)).to(dev, dt)
-    collect = collect_fn(args.collect)
+    collect = collect_fn(args.collect, world)
 
     def step():
         with torch.no_grad():
@@ -398,13 +397,13 @@ def forward_leg(args, world, rank, dev, precision, variant, B, S, traffic, cpu_s
                 collect(out[0].half(), world * B)
             return out
 
-    step()
+    step()  # first warm-up step: builds the executor handle
     torch.cuda.synchronize()
     handle = next(iter(model.__dict__["_upr_cache"].values()))[1]
     # per-launch HIP events in the LAST timed step only: events around every
     # launch of every step cost ~5% of the fp16 step (two event packets per launch)
     prof = None if args.no_profile else handle.profile
-    elapsed, last = timed_loop(world, dev, args.steps, args.warmup, step, prof)
+    elapsed, last = timed_loop(world, dev, args.steps, max(args.warmup - 1, 0), step, prof)
     stats = handle.profile_read() if not args.no_profile else []
     handle.profile(False)
     total = world * B * args.steps
@@ -460,6 +459,25 @@ def forward_leg(args, world, rank, dev, precision, variant, B, S, traffic, cpu_s
 # ----------------------------------------------------------------------------
 # training leg (configs[4])
 # ----------------------------------------------------------------------------
+def train_parity(sd, x, d0, amp):
+    """The first step's loss terms (initial weights, train-mode BatchNorm over
+    the batch) against oracle/train.py's forward + TotalLoss (fp32 torch-CPU)
+    on the same images.  BatchNorm couples the images, so the oracle runs the
+    whole batch (forward and loss only, no backward)."""
+    from oracle import net as onet  # checker only
+    from oracle import train as otrain
+    work = {k: v.clone() for k, v in sd.items()}
+    with torch.no_grad(), otrain.train_mode():
+        e, r, i = onet.forward(work, x.float().cpu(), False, False)
+        _, dr = otrain.total_loss(otrain.vgg19_state(1234), x.float().cpu(), e, i, r)
+    keys = ("total", "exposure", "smoothness", "color", "spatial", "decouple", "perceptual", "frequency")
+    rel = {k: abs(d0[k] - dr[k]) / max(abs(dr[k]), 1e-12) for k in keys if k in d0 and k in dr}
+    tol = 1e-2 if amp else 1e-4  # tests/test_gpu_train.py::test_train_step_full_size_bs8_512
+    return {"rel_diff": rel, "tol": tol, "pass": all(v <= tol for v in rel.values()),
+            "sample": f"loss terms of the first step (initial weights) over rank 0's whole {x.shape[0]}-image batch "
+                      f"vs oracle/train.py forward + TotalLoss (fp32 torch-CPU, train-mode BatchNorm)"}
+
+
 def train_roofline(recs, step_ms, B, S):
     """Convs of the profiled step against the peak of the arithmetic they ran
     in (fp16 MFMA under autocast, fp32 MFMA otherwise); the rest of the step
@@ -471,6 +489,14 @@ def train_roofline(recs, step_ms, B, S):
         d["ms"] += ms
         d["gflop"] += fl / 1e9
         d["calls"] += 1
+    by_what = {}
+    for kind, what, fl, ms in recs:
+        d = by_what.setdefault(f"{kind}.{what}", {"ms": 0.0, "gflop": 0.0, "calls": 0})
+        d["ms"] += ms
+        d["gflop"] += fl / 1e9
+        d["calls"] += 1
+    for d in by_what.values():
+        d["TFLOPs"] = d["gflop"] / d["ms"] if d["ms"] > 0 else None
     for k, d in by.items():
         d["TFLOPs"] = d["gflop"] / d["ms"] if d["ms"] > 0 else None  # GF / ms = TF/s
         d["peak"] = PEAK_TFLOPS["fp16"] if k == "mfma16" else PEAK_TFLOPS["fp32"]
@@ -483,7 +509,7 @@ def train_roofline(recs, step_ms, B, S):
     return {"bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s", "frac": ach / peak, "traffic": None,
             "kernel": f"{main} conv calls of one profiled step (forward, input gradient, weight gradient; each call "
                       f"timed with HIP events around its library call(s), algorithmic flops)",
-            "by_arithmetic": by,
+            "by_arithmetic": by, "by_pass": by_what,
             "step_ms": step_ms, "conv_ms": conv_ms,
             "non_conv_ms": step_ms - conv_ms,
             "non_conv_note": "BatchNorm stats/apply, ReLU masks, fp32<->fp16 casts, pooling, losses, FFTs, "
@@ -514,7 +540,8 @@ def train_leg(args, world, rank, dev, B, S, amp, steps, warmup, variant):
         hook = (lambda: allreduce_grads(opt)) if world > 1 else None
         return train_step(model, x, crit, opt, scaler=scaler, use_amp=amp, grad_hook=hook)
 
-    elapsed, last = timed_loop(world, dev, steps, warmup, tstep)
+    _, d0 = tstep()  # first warm-up step: its loss dict (initial weights) is the parity sample
+    elapsed, last = timed_loop(world, dev, steps, max(warmup - 1, 0), tstep)
     # one more (untimed) step with per-conv HIP events for the roofline split
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -541,8 +568,10 @@ def train_leg(args, world, rank, dev, B, S, amp, steps, warmup, variant):
         "roofline": train_roofline(recs, step_ms, B, S),
         "profiled_step_wall_ms": prof_ms,
     }
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        out["cpu_baseline"] = cpu_train_baseline(sd_cpu, S)
+    if rank == 0:
+        out["parity"] = train_parity(sd_cpu, x, d0, amp)
+        if world == 1 and args.cpu_seconds > 0:
+            out["cpu_baseline"] = cpu_train_baseline(sd_cpu, S)
     del model, x, opt, crit
     torch.cuda.empty_cache()
     return out
@@ -558,7 +587,7 @@ def dry_run(args):
 
     def step():
         a[0] = torch.tanh(a[0] @ a[0].T / 256)
-        col = collect_fn(args.collect)
+        col = collect_fn(args.collect, world)
         if col is not None:
             col(a[0][:4].half(), 4 * world)
         return a[0]

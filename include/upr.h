@@ -38,8 +38,10 @@ enum {
   UPR_ERR_UNSUPPORTED = -5
 };
 
-/* model flags */
-enum { UPR_MODEL_IENET_ONLY = 1 };
+/* model flags: UPR_MODEL_IENET_ONLY = ResidualIENet alone; UPR_MODEL_HEAD_ONLY =
+ * MultiScaleUP_Retinex.multi_scale_enhance alone (the 3-scale FAM head, the
+ * enhancement map and R*E + (1-R)*E^2 with a caller-given reflectance). */
+enum { UPR_MODEL_IENET_ONLY = 1, UPR_MODEL_HEAD_ONLY = 2 };
 
 typedef struct UprModel UprModel;
 
@@ -68,7 +70,10 @@ size_t upr_model_workspace(const UprModel* model, int B, int H, int W);
  * x [B,3,H,W] in [0,1], H and W multiples of 8 (>= 16)  ->
  * enh [B,3,H,W], refl [B,3,H,W], illu [B,1,H,W] (all `dtype` of the model).
  * With UPR_MODEL_IENET_ONLY (ResidualIENet.forward, :333-360) only `illu` is
- * written and enh/refl may be NULL. */
+ * written and enh/refl may be NULL.  With UPR_MODEL_HEAD_ONLY
+ * (multi_scale_enhance(x, reflectance, illu), :415-443) `refl` is an INPUT
+ * [B,3,H,W], only `enh` is written and `illu` may be NULL (the reference
+ * method does not read it). */
 int upr_model_forward(UprModel* model, const void* x, int B, int H, int W, void* enh, void* refl, void* illu,
                       void* workspace, size_t workspace_bytes, void* stream);
 
@@ -94,6 +99,17 @@ int upr_model_profile(UprModel* model, int enable);
 int upr_model_profile_read(UprModel* model, UprOpStat* out, int max_ops, int* n_ops);
 
 const char* upr_status_string(int status);
+
+/* MultiScaleUP_Retinex.retinex_decompose (models/model.py:405-413) on its own:
+ * refl = x / (illu + 1e-6) for x [B,C,H,W] and illu [B,illu_c,H,W], illu_c 1
+ * (broadcast over C) or C; fp32 arithmetic rounded once to `dtype`.  The
+ * backward (autograd of the reference expression) writes dx = g / (illu + 1e-6)
+ * and dillu = -sum_c g * x / (illu + 1e-6)^2 (over c when broadcast) into the
+ * non-NULL of gx [B,C,H,W] / gillu [B,illu_c,H,W] (overwritten). */
+int upr_retinex_decompose(const void* x, const void* illu, void* refl, int B, int C, int H, int W, int illu_c,
+                          int dtype, void* stream);
+int upr_retinex_decompose_bwd(const void* x, const void* illu, const void* g, void* gx, void* gillu, int B, int C,
+                              int H, int W, int illu_c, int dtype, void* stream);
 
 /* Generic NHWC convolution (op-level hook used by the parity tests and by
  * callers composing their own graphs): y = act(conv(x, w) + bias [+ residual]).

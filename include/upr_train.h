@@ -129,10 +129,13 @@ int upr_t_bn_apply16(const float* x, int M, int C, int x_cs, int x_coff, const f
 /* acc[2C] (zeroed) += (sum g, sum g*xhat) per channel. */
 int upr_t_bn_bwd_reduce(const float* g, int g_cs, int g_coff, const float* x, int x_cs, int x_coff, const float* mean,
                         const float* invstd, int M, int C, double* acc, void* stream);
-/* dx = gamma*invstd*(g - sum_g/M - xhat*sum_gx/M); dgamma/dbeta (nullable) += sums. */
+/* batch_stats 1 (train-mode BN): dx = gamma*invstd*(g - sum_g/M - xhat*sum_gx/M); batch_stats 0 (an eval-mode
+ * BN inside a training graph: running statistics are constants): dx = gamma*invstd*g.  dgamma/dbeta
+ * (nullable) += sums either way. */
 int upr_t_bn_bwd_apply(const float* g, int g_cs, int g_coff, const float* x, int x_cs, int x_coff, const float* mean,
                        const float* invstd, const float* gamma, const double* acc, int M, int C, float* dgamma,
-                       float* dbeta, float* dx, int dx_cs, int dx_coff, int accumulate, void* stream);
+                       float* dbeta, float* dx, int dx_cs, int dx_coff, int accumulate, int batch_stats,
+                       void* stream);
 /* out[C] (+)= per-channel sum of g[M][cs] (conv bias gradients). */
 int upr_t_chan_sum(const float* g, int M, int C, int cs, int coff, float* out, int accumulate, void* stream);
 
@@ -215,6 +218,13 @@ size_t upr_t_loss_workspace(int B, int H, int W);
 /* ... for exposure patch size `patch` (H, W >= patch; floor(H/patch) x
  * floor(W/patch) patches, as F.avg_pool2d). */
 size_t upr_t_loss_workspace_p(int B, int H, int W, int patch);
+/* calculate_texture_complexity(img, method) (losses/loss.py:523-583) on its own:
+ * img [B,C,H,W] fp32 (H, W >= 2) -> out[B] fp32; method 0 'tv' (mean |horizontal
+ * difference| + mean |vertical difference|), 1 'edge_density' (share of pixels
+ * whose reflect-padded Sobel magnitude of the channel-mean gray exceeds 1.5x
+ * its per-image mean).  acc: 2B doubles of scratch. */
+int upr_t_texture_complexity(const float* img, int B, int C, int H, int W, int method, double* acc, float* out,
+                             void* stream);
 /* Every non-perceptual, non-frequency term: exposure (:29-58), edge-aware
  * smoothness (:138-176), colour (:351-371), spatial (:408-427), decoupling
  * (:275-334), texture complexity of img_low (:523-583; texture 0 = 'tv',

@@ -17,7 +17,15 @@ BN_MOMENTUM = 0.1
 # and updates the running buffers in place, Dropout draws its mask from
 # MODE["dropout_mask"] (a callable shape -> {0,1} mask, so the checker can
 # replay the product's mask) — nn.BatchNorm2d / nn.Dropout train semantics.
-MODE = {"train": False, "dropout_mask": None, "amp": False}
+# MODE["eval_prefixes"]: state_dict prefixes of submodules left in eval mode
+# inside a training graph (model.train() then module.eval(), nn.Module's
+# per-module `training` flag): their BatchNorms use the running statistics and
+# their Dropout is the identity.
+MODE = {"train": False, "dropout_mask": None, "amp": False, "eval_prefixes": ()}
+
+
+def _training(p):
+    return MODE["train"] and not any(p.startswith(e) for e in MODE["eval_prefixes"])
 
 
 def _bn(sd, p, x):
@@ -25,11 +33,11 @@ def _bn(sd, p, x):
     # train: batch mean / biased var normalise; running stats updated with the
     # unbiased var, momentum 0.1
     return F.batch_norm(x, sd[p + ".running_mean"], sd[p + ".running_var"],
-                        sd[p + ".weight"], sd[p + ".bias"], MODE["train"], BN_MOMENTUM, BN_EPS)
+                        sd[p + ".weight"], sd[p + ".bias"], _training(p), BN_MOMENTUM, BN_EPS)
 
 
-def _dropout(x, p=0.1):
-    if not MODE["train"] or p == 0.0:
+def _dropout(x, p=0.1, prefix=""):
+    if not _training(prefix) or p == 0.0:
         return x
     mask = MODE["dropout_mask"](x.shape)
     return x * mask / (1.0 - p)
@@ -109,7 +117,7 @@ def aspp(sd, p, x, dilations=(1, 6, 12, 18)):
     g = F.relu(_bn(sd, p + ".global_pool.2", _conv(sd, p + ".global_pool.1", g)))
     feats.append(F.interpolate(g, size=x.shape[2:], mode="bilinear", align_corners=False))
     o = _conv(sd, p + ".fusion.0", torch.cat(feats, 1))
-    return _dropout(F.relu(_bn(sd, p + ".fusion.1", o)), 0.1)
+    return _dropout(F.relu(_bn(sd, p + ".fusion.1", o)), 0.1, p + ".fusion.3")
 
 
 def upblock(sd, p, x):
@@ -160,16 +168,8 @@ def scale_branch(sd, p, x, pool):
     return fam(sd, famp, F.relu(_conv(sd, conv, x, padding=1)))
 
 
-def forward(sd, x, use_preact=None, use_aspp=None):
-    """MultiScaleUP_Retinex.forward — models/model.py:445-455 (+405-443).
-
-    Returns (enhanced, reflectance, illumination) in fp32 on CPU.
-    """
-    if use_preact is None or use_aspp is None:
-        use_preact, use_aspp = variant_of(sd)
-    x = x if x.dtype == torch.float64 else x.float()
-    illu = ienet(sd, x, use_preact, use_aspp)
-    refl = x / (illu + 1e-6)                                           # model.py:411-412
+def multi_scale_enhance(sd, x, refl):
+    """MultiScaleUP_Retinex.multi_scale_enhance — models/model.py:415-443."""
     x2 = F.interpolate(x, scale_factor=0.5, mode="bilinear", align_corners=False)
     x3 = F.interpolate(x, scale_factor=0.25, mode="bilinear", align_corners=False)
     f1 = scale_branch(sd, "scale1", x, 1)
@@ -180,5 +180,17 @@ def forward(sd, x, use_preact=None, use_aspp=None):
                        F.interpolate(f2, size=size, mode="bilinear", align_corners=False),
                        F.interpolate(f3, size=size, mode="bilinear", align_corners=False)], 1)
     e = torch.sigmoid(_conv(sd, "output_layer", _conv(sd, "fusion", fused)))
-    enh = refl * e + (1 - refl) * (e ** 2)                             # model.py:442
-    return enh, refl, illu
+    return refl * e + (1 - refl) * (e ** 2)                            # model.py:442
+
+
+def forward(sd, x, use_preact=None, use_aspp=None):
+    """MultiScaleUP_Retinex.forward — models/model.py:445-455 (+405-443).
+
+    Returns (enhanced, reflectance, illumination) in fp32 on CPU.
+    """
+    if use_preact is None or use_aspp is None:
+        use_preact, use_aspp = variant_of(sd)
+    x = x if x.dtype == torch.float64 else x.float()
+    illu = ienet(sd, x, use_preact, use_aspp)
+    refl = x / (illu + 1e-6)                                           # model.py:411-412
+    return multi_scale_enhance(sd, x, refl), refl, illu

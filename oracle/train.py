@@ -212,13 +212,15 @@ def total_loss(vgg_sd, low, enh, illu, refl, use_freq=True, texture_method="tv",
 
 
 @contextlib.contextmanager
-def train_mode(dropout_mask=None, amp=False):
+def train_mode(dropout_mask=None, amp=False, eval_prefixes=()):
     """Training-mode BatchNorm / Dropout; amp: the autocast conv arithmetic
-    (net.amp_conv) for the model and the VGG convs."""
+    (net.amp_conv) for the model and the VGG convs; eval_prefixes: submodules
+    left in eval mode (frozen BatchNorm, identity Dropout)."""
     old = dict(net.MODE)
     net.MODE["train"] = True
     net.MODE["dropout_mask"] = dropout_mask
     net.MODE["amp"] = amp
+    net.MODE["eval_prefixes"] = tuple(eval_prefixes)
     try:
         yield
     finally:

@@ -24,6 +24,10 @@ int launch_ms_features(const void* x, void* out, int B, int H, int W, int scale_
 size_t content_aware_ws(int B, int H, int W);
 int launch_content_aware(const void* x, const void* enh, void* out, float* sal_out, float* att_out, uint8_t* ws,
                          int B, int H, int W, int dtype, hipStream_t st);
+int launch_decompose(const void* x, const void* illu, void* refl, int B, int C, int HW, int illu_c, int dtype,
+                     hipStream_t st);
+int launch_decompose_bwd(const void* x, const void* illu, const void* g, void* gx, void* gillu, int B, int C, int HW,
+                         int illu_c, int dtype, hipStream_t st);
 }  // namespace upr
 
 using namespace upr;
@@ -117,6 +121,21 @@ int upr_content_aware(const void* x, const void* enh, void* out, float* saliency
   if (workspace_bytes < content_aware_ws(B, H, W)) return UPR_ERR_WORKSPACE;
   return launch_content_aware(x, enh, out, saliency, attention, (uint8_t*)workspace, B, H, W, dtype,
                               (hipStream_t)stream);
+}
+
+int upr_retinex_decompose(const void* x, const void* illu, void* refl, int B, int C, int H, int W, int illu_c,
+                          int dtype, void* stream) {
+  if (!x || !illu || !refl || !dtype_ok(dtype) || B <= 0 || C <= 0 || (illu_c != 1 && illu_c != C)) return UPR_ERR_ARG;
+  if (H <= 0 || W <= 0 || (long long)B * H * W * C >= (1LL << 40)) return UPR_ERR_SHAPE;
+  return launch_decompose(x, illu, refl, B, C, H * W, illu_c, dtype, (hipStream_t)stream);
+}
+
+int upr_retinex_decompose_bwd(const void* x, const void* illu, const void* g, void* gx, void* gillu, int B, int C,
+                              int H, int W, int illu_c, int dtype, void* stream) {
+  if (!x || !illu || !g || !dtype_ok(dtype) || B <= 0 || C <= 0 || (illu_c != 1 && illu_c != C)) return UPR_ERR_ARG;
+  if (H <= 0 || W <= 0) return UPR_ERR_SHAPE;
+  if (!gx && !gillu) return UPR_OK;
+  return launch_decompose_bwd(x, illu, g, gx, gillu, B, C, H * W, illu_c, dtype, (hipStream_t)stream);
 }
 
 void upr_lab_tables(uint16_t* gamma, uint16_t* cbrt, uint16_t* yf, uint16_t* invgamma, int32_t* rgb2xyz,

@@ -43,7 +43,7 @@ int launch_fam_sa(const float* mm, const float* p, const float* w, float bias, f
                   hipStream_t st);
 int launch_tail(const void* x, const float* illu_f32, const void* illu_t, const float* q1, const float* q2,
                 const float* q3, const float* cst, void* enh, void* refl, int B, int H, int W, int h2, int w2, int h3,
-                int w3, int dtype, hipStream_t st);
+                int w3, int dtype, hipStream_t st, int refl_in);
 
 // ---------------------------------------------------------------------------
 // ASPP global-pool branch -> per-image bias of the ASPP fusion GEMM
@@ -398,11 +398,10 @@ static size_t ws_layout(const UprModel* m, int B, int H, int W, size_t* offs) {
     }
     if (id >= B_PA1 && id <= B_PA4 && !preact_materialised(m)) bytes = 0;
     if (id == B_FT && !fam32_split(m)) bytes = 0;
-    if (m->flags & UPR_MODEL_IENET_ONLY) {
-      const bool scale_buf = id == B_X2P || id == B_X3P || id == B_S1IN || id == B_S2IN || id == B_S3IN ||
-                             (id >= B_H1 && id <= B_Q3);
-      if (scale_buf) bytes = 0;
-    }
+    const bool scale_buf = id == B_X2P || id == B_X3P || id == B_S1IN || id == B_S2IN || id == B_S3IN ||
+                           (id >= B_H1 && id <= B_Q3) || id == B_FT;
+    if ((m->flags & UPR_MODEL_IENET_ONLY) && scale_buf) bytes = 0;
+    if ((m->flags & UPR_MODEL_HEAD_ONLY) && !scale_buf && id != B_POOL && id != B_CA) bytes = 0;
     off = align_up(off, 256);
     if (offs) offs[id] = off;
     off += bytes;
@@ -690,8 +689,20 @@ static int build_model(UprModel* m, ParamSet& P) {
   Builder bd{P, blob, m, m->dtype};
   const int pre = m->use_preact;
   const std::string ie = "ie_net";
+  const bool head_only = (m->flags & UPR_MODEL_HEAD_ONLY) != 0;
+  if (head_only) {
+    // multi_scale_enhance alone (models/model.py:415-443): scale1's first conv
+    // on its own, no IENet ops; the tail reads the caller's reflectance
+    const HostTensor* ws = bd.T("scale1.0.weight");
+    const HostTensor* bs = bd.T("scale1.0.bias");
+    if (!bd.ok) return kErrMissingParam;
+    Op o;
+    o.kind = OP_CONV3; o.name = "scale1.0"; o.in = BX; o.out = B_S1IN; o.lvl_shift = 0;
+    o.w = blob.add_f32(conv3_kmajor(ws->v)); o.b = blob.add_f32(bs->v);
+    m->ops.push_back(o);
+  }
   // input layer (+ scale1's first conv, same input, one launch)
-  {
+  if (!head_only) {
     const HostTensor* wi = bd.T(ie + ".input_layer.weight");
     const HostTensor* bi = bd.T(ie + ".input_layer.bias");
     if (!bd.ok) return kErrMissingParam;
@@ -710,6 +721,7 @@ static int build_model(UprModel* m, ParamSet& P) {
     m->ops.push_back(o);
   }
   (void)pre;
+  if (!head_only) {
   bd.block(ie + ".enc1", B_X1, B_E1T, B_X2, 32, 64, 2, 0);
   bd.block(ie + ".enc2", B_X2, B_E2T, B_X3, 64, 128, 2, 1);
   bd.block(ie + ".enc3", B_X3, B_E3T, B_X4, 128, 256, 2, 2);
@@ -741,6 +753,7 @@ static int build_model(UprModel* m, ParamSet& P) {
     o.head_w = blob.add_f32(w2->v); o.head_b = (float)b2->v[0];
     m->ops.push_back(o);
   }
+  }  // !head_only
   if (!(m->flags & UPR_MODEL_IENET_ONLY)) {
     const HostTensor* wfu = bd.T("fusion.weight");   // [32][96]
     const HostTensor* bfu = bd.T("fusion.bias");
@@ -940,7 +953,8 @@ static int run_forward(UprModel* m, const void* x, int B, int H, int W, void* en
       }
       case OP_TAIL:
         rc = launch_tail(x, illu32, nullptr, (const float*)buf(B_Q1), (const float*)buf(B_Q2),
-                         (const float*)buf(B_Q3), fptr(o.cst), enh, refl, B, H, W, H4, W4, H16, W16, dt, st);
+                         (const float*)buf(B_Q3), fptr(o.cst), enh, refl, B, H, W, H4, W4, H16, W16, dt, st,
+                         (m->flags & UPR_MODEL_HEAD_ONLY) ? 1 : 0);
         break;
     }
     if (m->prof) UPR_CHECK_HIP(hipEventRecord(evs[2 * oi + 1], st));
@@ -954,7 +968,7 @@ static int run_forward(UprModel* m, const void* x, int B, int H, int W, void* en
     }
     for (size_t i = 0; i < nops; ++i) { m->st_flops[i] += m->cur_flops[i]; m->st_bytes[i] += m->cur_bytes[i]; }
   }
-  if (dt == kF16) {
+  if (dt == kF16 && !(m->flags & UPR_MODEL_HEAD_ONLY)) {
     // illumination in the model dtype
     extern int launch_cast_f32_to_f16(const float*, void*, size_t, hipStream_t);
     int rc = launch_cast_f32_to_f16(illu32, illu, (size_t)B * H * W, st);
@@ -1014,7 +1028,8 @@ size_t upr_model_workspace(const UprModel* model, int B, int H, int W) {
 
 int upr_model_forward(UprModel* model, const void* x, int B, int H, int W, void* enh, void* refl, void* illu,
                       void* workspace, size_t workspace_bytes, void* stream) {
-  if (!model || !x || !illu || B <= 0) return UPR_ERR_ARG;
+  const bool head_only = (model && (model->flags & UPR_MODEL_HEAD_ONLY));
+  if (!model || !x || (!illu && !head_only) || B <= 0) return UPR_ERR_ARG;
   if (!(model->flags & UPR_MODEL_IENET_ONLY) && (!enh || !refl)) return UPR_ERR_ARG;
   if (H % 8 || W % 8 || H < 16 || W < 16) return UPR_ERR_SHAPE;
   if ((long long)B * H * W > (1LL << 31) / 32) return UPR_ERR_SHAPE;  // 32-bit pixel indexing in kernels

@@ -261,7 +261,8 @@ __global__ __launch_bounds__(256) void retinex_tail_kernel(const T* __restrict__
                                                            const float* __restrict__ q1, const float* __restrict__ q2,
                                                            const float* __restrict__ q3, const float* __restrict__ cst,
                                                            T* __restrict__ enh, T* __restrict__ refl,
-                                                           int B, int H, int W, int h2, int w2, int h3, int w3) {
+                                                           int B, int H, int W, int h2, int w2, int h3, int w3,
+                                                           int refl_in) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= B * H * W) return;
   const int ox = idx % W, oy = (idx / W) % H, b = idx / (W * H);
@@ -271,7 +272,9 @@ __global__ __launch_bounds__(256) void retinex_tail_kernel(const T* __restrict__
   src_idx(ox, w2, (float)w2 / (float)W, ax0, ax1, alx);
   src_idx(oy, h3, (float)h3 / (float)H, by0, by1, bly);
   src_idx(ox, w3, (float)w3 / (float)W, bx0, bx1, blx);
-  const float il = illu_t ? ldf(illu_t, idx) : illu_f32[idx];
+  // refl_in (multi_scale_enhance, models/model.py:415-443): R is the caller's
+  // reflectance, read instead of x / (I + 1e-6) and not written
+  const float il = refl_in ? 0.f : (illu_t ? ldf(illu_t, idx) : illu_f32[idx]);
   const size_t HW = (size_t)H * W;
   const size_t pix = (size_t)oy * W + ox;
 #pragma unroll
@@ -280,9 +283,13 @@ __global__ __launch_bounds__(256) void retinex_tail_kernel(const T* __restrict__
               bilerp3(q3, b, h3, w3, c, by0, by1, bly, bx0, bx1, blx) + cst[c];
     const float e = sigmoidf_(z);
     const size_t o = ((size_t)b * 3 + c) * HW + pix;
-    const float xv = ldf(x, o);
-    const float r = xv / (il + 1e-6f);
-    stf(refl, o, r);
+    float r;
+    if (refl_in) {
+      r = ldf(refl, o);
+    } else {
+      r = ldf(x, o) / (il + 1e-6f);
+      stf(refl, o, r);
+    }
     stf(enh, o, r * e + (1.f - r) * (e * e));
   }
 }
@@ -496,14 +503,80 @@ int launch_fam_sa(const float* mm, const float* p, const float* w, float bias, f
 
 int launch_tail(const void* x, const float* illu_f32, const void* illu_t, const float* q1, const float* q2,
                 const float* q3, const float* cst, void* enh, void* refl, int B, int H, int W, int h2, int w2, int h3,
-                int w3, int dtype, hipStream_t st) {
+                int w3, int dtype, hipStream_t st, int refl_in) {
   const int n = B * H * W;
   if (dtype == kF16)
     hipLaunchKernelGGL((retinex_tail_kernel<half_t>), dim3(grid1d(n)), dim3(256), 0, st, (const half_t*)x, illu_f32,
-                       (const half_t*)illu_t, q1, q2, q3, cst, (half_t*)enh, (half_t*)refl, B, H, W, h2, w2, h3, w3);
+                       (const half_t*)illu_t, q1, q2, q3, cst, (half_t*)enh, (half_t*)refl, B, H, W, h2, w2, h3, w3,
+                       refl_in);
   else
     hipLaunchKernelGGL((retinex_tail_kernel<float>), dim3(grid1d(n)), dim3(256), 0, st, (const float*)x, illu_f32,
-                       (const float*)illu_t, q1, q2, q3, cst, (float*)enh, (float*)refl, B, H, W, h2, w2, h3, w3);
+                       (const float*)illu_t, q1, q2, q3, cst, (float*)enh, (float*)refl, B, H, W, h2, w2, h3, w3,
+                       refl_in);
+  return (int)hipGetLastError();
+}
+
+// MultiScaleUP_Retinex.retinex_decompose (models/model.py:405-413) called on
+// its own: refl = x / (illu + 1e-6) over [B,C,H,W], illu [B,illu_c,H,W] with
+// illu_c 1 (broadcast over C, the reference's use) or C; fp32 arithmetic, one
+// rounding to the tensor dtype.  Backward: dx = g / d, dillu = -sum_c g*x / d^2
+// (the sum over c when illu is broadcast), d = illu + 1e-6.  One thread per
+// (image, pixel) walks the channels.
+template <typename T>
+__global__ __launch_bounds__(256) void decompose_kernel(const T* __restrict__ x, const T* __restrict__ illu,
+                                                        T* __restrict__ refl, int B, int C, int HW, int illu_c) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)B * HW) return;
+  const long long b = i / HW, p = i - b * HW;
+  for (int c = 0; c < C; ++c) {
+    const long long o = (b * C + c) * HW + p;
+    const float d = ldf(illu, (b * illu_c + (illu_c == 1 ? 0 : c)) * HW + p) + 1e-6f;
+    stf(refl, o, ldf(x, o) / d);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void decompose_bwd_kernel(const T* __restrict__ x, const T* __restrict__ illu,
+                                                            const T* __restrict__ g, T* __restrict__ gx,
+                                                            T* __restrict__ gillu, int B, int C, int HW, int illu_c) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)B * HW) return;
+  const long long b = i / HW, p = i - b * HW;
+  float acc = 0.f;
+  for (int c = 0; c < C; ++c) {
+    const long long o = (b * C + c) * HW + p;
+    const long long io = (b * illu_c + (illu_c == 1 ? 0 : c)) * HW + p;
+    const float d = ldf(illu, io) + 1e-6f;
+    const float gv = ldf(g, o);
+    if (gx) stf(gx, o, gv / d);
+    const float gi = -gv * ldf(x, o) / (d * d);
+    if (illu_c == 1) acc += gi;
+    else if (gillu) stf(gillu, io, gi);
+  }
+  if (illu_c == 1 && gillu) stf(gillu, b * HW + p, acc);
+}
+
+int launch_decompose(const void* x, const void* illu, void* refl, int B, int C, int HW, int illu_c, int dtype,
+                     hipStream_t st) {
+  const int grid = (int)(((long long)B * HW + 255) / 256);
+  if (dtype == kF16)
+    hipLaunchKernelGGL((decompose_kernel<half_t>), dim3(grid), dim3(256), 0, st, (const half_t*)x, (const half_t*)illu,
+                       (half_t*)refl, B, C, HW, illu_c);
+  else
+    hipLaunchKernelGGL((decompose_kernel<float>), dim3(grid), dim3(256), 0, st, (const float*)x, (const float*)illu,
+                       (float*)refl, B, C, HW, illu_c);
+  return (int)hipGetLastError();
+}
+
+int launch_decompose_bwd(const void* x, const void* illu, const void* g, void* gx, void* gillu, int B, int C, int HW,
+                         int illu_c, int dtype, hipStream_t st) {
+  const int grid = (int)(((long long)B * HW + 255) / 256);
+  if (dtype == kF16)
+    hipLaunchKernelGGL((decompose_bwd_kernel<half_t>), dim3(grid), dim3(256), 0, st, (const half_t*)x,
+                       (const half_t*)illu, (const half_t*)g, (half_t*)gx, (half_t*)gillu, B, C, HW, illu_c);
+  else
+    hipLaunchKernelGGL((decompose_bwd_kernel<float>), dim3(grid), dim3(256), 0, st, (const float*)x,
+                       (const float*)illu, (const float*)g, (float*)gx, (float*)gillu, B, C, HW, illu_c);
   return (int)hipGetLastError();
 }
 

@@ -589,7 +589,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
                                                            const float* __restrict__ gamma,
                                                            const double* __restrict__ acc, int M, int C,
                                                            float* dgamma, float* dbeta, float* dx, int dx_cs,
-                                                           int dx_coff, int accum) {
+                                                           int dx_coff, int accum, int batch_stats) {
   if (blockIdx.x == 0) {
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
       if (dgamma) dgamma[c] += (float)acc[C + c];
@@ -602,7 +602,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
     const long long m = i / C;
     const float is = invstd[c];
     const float xh = (x[m * x_cs + x_coff + c] - mean[c]) * is;
-    const float sg = (float)(acc[c] / M), sgx = (float)(acc[C + c] / M);
+    // batch statistics: the mean / x-hat terms of the batch-statistics backward;
+    // running statistics (an eval-mode BN): the plain affine map g * gamma * invstd
+    const float sg = batch_stats ? (float)(acc[c] / M) : 0.f, sgx = batch_stats ? (float)(acc[C + c] / M) : 0.f;
     float v = gamma[c] * is * (g[m * g_cs + g_coff + c] - sg - xh * sgx);
     float* o = dx + m * dx_cs + dx_coff + c;
     if (accum) v += *o;
@@ -618,7 +620,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(const float* __restr
                                                             const float* __restrict__ gamma,
                                                             const double* __restrict__ acc, int M, int C,
                                                             float* dgamma, float* dbeta, float* dx, int dx_cs,
-                                                            int dx_coff, int accum) {
+                                                            int dx_coff, int accum, int batch_stats) {
   if (blockIdx.x == 0) {
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
       if (dgamma) dgamma[c] += (float)acc[C + c];
@@ -641,7 +643,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(const float* __restr
     for (int e = 0; e < 4; ++e) {
       const float is = invstd[c + e];
       const float xh = (xa[e] - mean[c + e]) * is;
-      const float sg = (float)(acc[c + e] / M), sgx = (float)(acc[C + c + e] / M);
+      const float sg = batch_stats ? (float)(acc[c + e] / M) : 0.f;
+      const float sgx = batch_stats ? (float)(acc[C + c + e] / M) : 0.f;
       float v = gamma[c + e] * is * (ga[e] - sg - xh * sgx);
       if (accum) v += pa[e];
       r[e] = v;
@@ -1325,6 +1328,72 @@ __global__ __launch_bounds__(256) void edge_density_kernel(const float* __restri
   block_sum_atomic<1>(v, dst);
 }
 
+// calculate_texture_complexity (losses/loss.py:523-583) called on its own, for
+// any channel count: img [B][C][H][W] fp32.  grid (chunks, B).
+//   method 0 'tv':  acc[b] += sum |x[..,w] - x[..,w+1]|, acc[B+b] += sum |x[h] - x[h+1]|
+//   method 1 'edge_density': gray = channel mean (torch.mean dim 1), reflect-
+//     padded Sobel magnitude; mode 0 acc[b] += sum of magnitudes, mode 1
+//     acc[B+b] += count of magnitudes > 1.5 * fp32 mean
+__device__ __forceinline__ float gray_mean_c(const float* img, size_t base, int C, int HW, int q) {
+  float s = img[base + q];
+  for (int c = 1; c < C; ++c) s += img[base + (size_t)c * HW + q];
+  return C > 1 ? s / (float)C : s;
+}
+
+__global__ __launch_bounds__(256) void texture_kernel(const float* __restrict__ img, int C, int H, int W, int method,
+                                                      int mode, double* __restrict__ acc) {
+  const int b = blockIdx.y, B = gridDim.y;
+  const int HW = H * W;
+  const size_t base = (size_t)b * C * HW;
+  const int per = (HW + gridDim.x - 1) / gridDim.x;
+  const int p0 = blockIdx.x * per, p1 = min(HW, p0 + per);
+  double v[2] = {0.0, 0.0};
+  const float thr = (method == 1 && mode == 1) ? (float)(acc[b] / HW) * 1.5f : 0.f;
+  for (int q = p0 + threadIdx.x; q < p1; q += 256) {
+    const int y = q / W, x = q - y * W;
+    if (method == 0) {
+      for (int c = 0; c < C; ++c) {
+        const float* pl = img + base + (size_t)c * HW;
+        const float a = pl[q];
+        if (x + 1 < W) v[0] += fabsf(a - pl[q + 1]);
+        if (y + 1 < H) v[1] += fabsf(a - pl[q + W]);
+      }
+    } else {
+      float g[3][3];
+      for (int dy = -1; dy <= 1; ++dy) {
+        int yy = y + dy;
+        yy = yy < 0 ? -yy : (yy >= H ? 2 * H - 2 - yy : yy);
+        for (int dx = -1; dx <= 1; ++dx) {
+          int xx = x + dx;
+          xx = xx < 0 ? -xx : (xx >= W ? 2 * W - 2 - xx : xx);
+          g[dy + 1][dx + 1] = gray_mean_c(img, base, C, HW, yy * W + xx);
+        }
+      }
+      const float gx = -g[0][0] + g[0][2] - 2.f * g[1][0] + 2.f * g[1][2] - g[2][0] + g[2][2];
+      const float gy = -g[0][0] - 2.f * g[0][1] - g[0][2] + g[2][0] + 2.f * g[2][1] + g[2][2];
+      const float e = sqrtf(gx * gx + gy * gy);
+      if (mode == 0) v[0] += (double)e;
+      else v[1] += e > thr ? 1.0 : 0.0;
+    }
+  }
+  double* dst[2] = {(method == 0 || mode == 0) ? acc + b : nullptr, (method == 0 || mode == 1) ? acc + B + b : nullptr};
+  block_sum_atomic<2>(v, dst);
+}
+
+__global__ void texture_final_kernel(const double* __restrict__ acc, int B, int C, int H, int W, int method,
+                                     float* __restrict__ out) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  if (method == 0) {
+    // torch.mean per direction (fp32 results), then their fp32 sum
+    const float th = (float)(acc[b] / ((double)C * H * (W - 1)));
+    const float tv = (float)(acc[B + b] / ((double)C * (H - 1) * W));
+    out[b] = th + tv;
+  } else {
+    out[b] = (float)(acc[B + b] / ((double)H * W));
+  }
+}
+
 // finalise: one block
 __global__ void loss_final_kernel(int B, int H, int W, LossWS ws, float* __restrict__ terms, int texture,
                                   float w_smooth) {
@@ -1921,19 +1990,22 @@ int upr_t_bn_bwd_reduce(const float* g, int g_cs, int g_coff, const float* x, in
 
 int upr_t_bn_bwd_apply(const float* g, int g_cs, int g_coff, const float* x, int x_cs, int x_coff, const float* mean,
                        const float* invstd, const float* gamma, const double* acc, int M, int C, float* dgamma,
-                       float* dbeta, float* dx, int dx_cs, int dx_coff, int accumulate, void* stream) {
+                       float* dbeta, float* dx, int dx_cs, int dx_coff, int accumulate, int batch_stats,
+                       void* stream) {
   if (!g || !x || !acc || !dx || !gamma) return UPR_ERR_ARG;
   const auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
   if (C % 4 == 0 && g_cs % 4 == 0 && g_coff % 4 == 0 && x_cs % 4 == 0 && x_coff % 4 == 0 && dx_cs % 4 == 0 &&
       dx_coff % 4 == 0 && a16(g) && a16(x) && a16(dx)) {
     const long long n4 = (long long)M * (C / 4);
     hipLaunchKernelGGL(bn_bwd_apply4_kernel, dim3(grid_for(n4)), dim3(256), 0, ST(stream), g, g_cs, g_coff, x, x_cs,
-                       x_coff, mean, invstd, gamma, acc, M, C, dgamma, dbeta, dx, dx_cs, dx_coff, accumulate);
+                       x_coff, mean, invstd, gamma, acc, M, C, dgamma, dbeta, dx, dx_cs, dx_coff, accumulate,
+                       batch_stats);
     LAUNCH_CHECK();
   }
   const long long n = (long long)M * C;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), g, g_cs, g_coff, x, x_cs,
-                     x_coff, mean, invstd, gamma, acc, M, C, dgamma, dbeta, dx, dx_cs, dx_coff, accumulate);
+                     x_coff, mean, invstd, gamma, acc, M, C, dgamma, dbeta, dx, dx_cs, dx_coff, accumulate,
+                       batch_stats);
   LAUNCH_CHECK();
 }
 
@@ -2301,6 +2373,22 @@ int upr_t_loss_pixel_p(const float* low, const float* enh, const float* illu, co
     hipLaunchKernelGGL(loss_grad_kernel, dim3(grid_for((long long)B * H * W)), dim3(256), 0, st, low, enh, illu, refl,
                        B, H, W, l, g_enh, g_illu, g_refl, w_exp, w_col, w_spa, w_dec);
   }
+  LAUNCH_CHECK();
+}
+
+int upr_t_texture_complexity(const float* img, int B, int C, int H, int W, int method, double* acc, float* out,
+                             void* stream) {
+  if (!img || !acc || !out || B <= 0 || C <= 0 || (method != 0 && method != 1)) return UPR_ERR_ARG;
+  if (H < 2 || W < 2) return UPR_ERR_SHAPE;  // a finite difference / a reflect pad needs two samples per axis
+  hipStream_t st = ST(stream);
+  UPR_CHECK_HIP(hipMemsetAsync(acc, 0, sizeof(double) * 2 * B, st));
+  int chunks = (H * W) / 4096;
+  chunks = chunks < 1 ? 1 : (chunks > 128 ? 128 : chunks);
+  for (int mode = 0; mode < (method == 1 ? 2 : 1); ++mode) {
+    hipLaunchKernelGGL(texture_kernel, dim3(chunks, B), dim3(256), 0, st, img, C, H, W, method, mode, acc);
+    UPR_CHECK_HIP(hipGetLastError());
+  }
+  hipLaunchKernelGGL(texture_final_kernel, dim3((B + 63) / 64), dim3(64), 0, st, acc, B, C, H, W, method, out);
   LAUNCH_CHECK();
 }
 

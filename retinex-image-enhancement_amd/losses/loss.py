@@ -133,7 +133,8 @@ class ColorLoss(_Term):
         self._setup()
 
     def forward(self, img_enhanced):
-        return self._eval(img_enhanced, img_enhanced, _dummy_illu(img_enhanced), img_enhanced)
+        # img_low is a placeholder here (the term does not read it)
+        return self._eval(img_enhanced.detach(), img_enhanced, _dummy_illu(img_enhanced), img_enhanced)
 
 
 class SpatialConsistencyLoss(_Term):
@@ -163,7 +164,7 @@ class IlluminationReflectanceDecouplingLoss(_Term):
     def forward(self, illu_map, reflectance):
         if illu_map.shape[1] != 1 or reflectance.shape[1] != 3:
             raise NotImplementedError("device decoupling loss: illumination [B,1,H,W], reflectance [B,3,H,W]")
-        return self._eval(reflectance, reflectance, illu_map, reflectance)
+        return self._eval(reflectance.detach(), reflectance, illu_map, reflectance)  # img_low: placeholder
 
 
 class PerceptualLoss(_Term):
@@ -263,6 +264,17 @@ def dwa_weights(history, defaults, temperature=2.0):
     return w
 
 
-def calculate_texture_complexity(img, method='tv'):  # pragma: no cover - not on the training hot path
-    raise NotImplementedError("calculate_texture_complexity is evaluated inside TotalLoss on the device "
-                              "(the dynamic smooth weight); no standalone device version")
+def calculate_texture_complexity(img, method='tv'):
+    """Texture complexity per image (reference losses/loss.py:523-583) on the
+    device (upr_t_texture_complexity): 'tv' = mean |horizontal difference| +
+    mean |vertical difference| over C, H, W; 'edge_density' = the share of
+    pixels whose reflect-padded Sobel magnitude of the channel-mean gray
+    exceeds 1.5x its image mean.  img [B,C,H,W] float32 on a ROCm device ->
+    [B] float32.  TotalLoss uses it for the dynamic smoothness weight without
+    gradient, and so does this function (no autograd history)."""
+    if method not in E.TEXTURE:
+        raise ValueError(f"不支持的纹理复杂度计算方法: {method}")
+    _require(img, "calculate_texture_complexity")
+    if img.dim() != 4:
+        raise RuntimeError(f"calculate_texture_complexity: expected [B,C,H,W], got {tuple(img.shape)}")
+    return E.texture_complexity(img.detach().contiguous(), E.TEXTURE[method])

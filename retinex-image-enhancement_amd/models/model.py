@@ -18,14 +18,10 @@ import torch.nn as nn
 
 from upr.runtime import ModelHandle
 
-_FUSED_MSG = ("{} executes only inside the fused UP-Retinex HIP graph; call the top-level "
-              "MultiScaleUP_Retinex / ResidualIENet forward()")
-
-
 class _FusedModule(nn.Module):
     """Submodules: fused into the model's HIP graph inside MultiScaleUP_Retinex;
     a direct call runs the module alone on the HIP layer kernels
-    (upr/modules.py: NCHW float32 in / out, eval or training mode)."""
+    (upr/modules.py: NCHW float32 / float16 in / out, eval or training mode)."""
 
     def forward(self, x):
         from upr.modules import submodule_forward
@@ -145,9 +141,8 @@ class _HipGraphMixin:
                 f"ROCm devices (gfx950 HIP kernels, no CPU path): use model.to('cuda') and a 'cuda' tensor.")
         if self.training:
             if self._ienet_only:
-                raise NotImplementedError(
-                    "ResidualIENet: standalone training-mode forward is not provided; train the full "
-                    "MultiScaleUP_Retinex (trainers/train.py) or call .eval()")
+                from upr.autograd import ienet_train_forward
+                return None, None, ienet_train_forward(self, x)
             from upr.autograd import model_train_forward
             return model_train_forward(self, x)
         key = (x.device, x.dtype)
@@ -218,11 +213,36 @@ class MultiScaleUP_Retinex(_HipGraphMixin, nn.Module):
         self.fusion = nn.Conv2d(96, 32, kernel_size=1)
         self.output_layer = nn.Conv2d(32, 3, kernel_size=1)
 
-    def retinex_decompose(self, x, illu):  # pragma: no cover - fused
-        raise NotImplementedError(_FUSED_MSG.format("retinex_decompose"))
+    def retinex_decompose(self, x, illu):
+        """Reflectance x / (illu + 1e-6) (reference :405-413); inside forward()
+        this is fused into the tail kernel, called on its own it is one device
+        kernel (upr_retinex_decompose), differentiable in x and illu."""
+        from upr.runtime import retinex_decompose
+        return retinex_decompose(x, illu)
 
-    def multi_scale_enhance(self, x, reflectance, illu):  # pragma: no cover - fused
-        raise NotImplementedError(_FUSED_MSG.format("multi_scale_enhance"))
+    def multi_scale_enhance(self, x, reflectance, illu):
+        """Enhanced image from the 3-scale FAM head of x and the given
+        reflectance: R*E + (1-R)*E^2 with E = sigmoid(output_layer(fusion(...)))
+        (reference :415-443; `illu` is not read there either).  Runs the head
+        alone on the HIP kernels (UPR_MODEL_HEAD_ONLY handle).  The head has no
+        BatchNorm or Dropout, so train and eval mode compute the same values;
+        like the eval-mode forward, the result records no autograd history
+        (training gradients flow through forward())."""
+        from upr.runtime import _require_device
+        _require_device(x)
+        _require_device(reflectance, "reflectance")
+        if torch.is_grad_enabled() and (reflectance.requires_grad or x.requires_grad) and self.training:
+            raise NotImplementedError("multi_scale_enhance: gradients through the head alone are not provided; "
+                                      "train through forward() (the full graph's backward covers the head)")
+        key = ("head", x.device, x.dtype)
+        sig = self._signature()
+        cache = self.__dict__.setdefault("_upr_cache", {})
+        ent = cache.get(key)
+        if ent is None or ent[0] != sig:
+            ent = (sig, ModelHandle(self.state_dict(), self._use_preact, self._use_aspp, x.dtype, x.device,
+                                    head_only=True))
+            cache[key] = ent
+        return ent[1].enhance(x, reflectance)
 
     def forward(self, x):
         """x [B,3,H,W] float32/float16 in [0,1] on a ROCm device, H, W multiples

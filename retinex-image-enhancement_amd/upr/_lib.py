@@ -12,6 +12,7 @@ LIB_PATH = os.environ.get("UPR_LIB", os.path.join(os.path.dirname(_HERE), "lib",
 UPR_F32 = 0
 UPR_F16 = 1
 UPR_MODEL_IENET_ONLY = 1
+UPR_MODEL_HEAD_ONLY = 2
 
 UPR_OK = 0
 UPR_ERR_ARG = -1
@@ -76,6 +77,10 @@ SIGNATURES = {
     "upr_content_aware": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_int,
                                   c_int, c_int, c_void_p]),
     "upr_lab_tables": (None, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "upr_retinex_decompose": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
+                                      c_void_p]),
+    "upr_retinex_decompose_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                                          c_int, c_int, c_int, c_void_p]),
     "upr_calib_run": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_size_t, c_int, ctypes.POINTER(c_float),
                               c_void_p]),
 }
@@ -120,11 +125,12 @@ SIGNATURES.update({
     "upr_t_bn_apply": (_i, [_p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _i, _i, _p]),
     "upr_t_bn_apply16": (_i, [_p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _i, _i, _p, _p]),
     "upr_t_bn_bwd_reduce": (_i, [_p, _i, _i, _p, _i, _i, _p, _p, _i, _i, _p, _p]),
-    "upr_t_bn_bwd_apply": (_i, [_p, _i, _i, _p, _i, _i, _p, _p, _p, _p, _i, _i, _p, _p, _p, _i, _i, _i, _p]),
+    "upr_t_bn_bwd_apply": (_i, [_p, _i, _i, _p, _i, _i, _p, _p, _p, _p, _i, _i, _p, _p, _p, _i, _i, _i, _i, _p]),
     "upr_t_chan_sum": (_i, [_p, _i, _i, _i, _i, _p, _i, _p]),
     "upr_t_relu_mask": (_i, [_p, _i, _i, _p, _i, _i, _i, _i, _p]),
     "upr_t_copy": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _p]),
     "upr_t_pointwise": (_i, [_p, _p, _p, c_size_t, _i, _p, _p, _f, c_u64, _p]),
+    "upr_t_texture_complexity": (_i, [_p, _i, _i, _i, _i, _i, _p, _p, _p]),
     "upr_t_maxpool": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _p]),
     "upr_t_maxpool_bwd": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _p]),
     "upr_t_bilinear": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _p]),

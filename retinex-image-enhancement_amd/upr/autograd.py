@@ -76,6 +76,59 @@ def model_train_forward(model, x):
     return _ModelStep.apply(x.contiguous(), st["anchor"], st["graph"])
 
 
+class _IENetStep(torch.autograd.Function):
+    """ResidualIENet.forward (models/model.py:333-360) in training mode on its
+    own: forward = the IENet layer objects of upr/train.py, backward = their
+    explicit backward from dL/d(illumination) (sigmoid backward on the device,
+    then the residual head and the network); parameter gradients accumulate
+    into the .grad views.  No gradient w.r.t. the network input (as the full
+    model's node)."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, ie, flat):
+        from .train import set_amp, autocast_active
+        set_amp(autocast_active())
+        for c in ie.convs():
+            c.pack()
+        illu = ie.fwd(x)
+        bump_weights_epoch()  # BatchNorm running stats were updated
+        ctx.ie, ctx.flat, ctx.illu = ie, flat, illu
+        return illu
+
+    @staticmethod
+    def backward(ctx, g_illu):
+        from .train import Act
+        ie, flat, illu = ctx.ie, ctx.flat, ctx.illu
+        if flat.attach_grads():
+            zero(flat.grad)
+        B, _, H, W = illu.shape
+        g_r = Act.new(B, H, W, 1, illu.device, fresh=False)
+        with torch.cuda.device(illu.device):
+            # illu = sigmoid(mean_c(x) + r): dL/dr = g * illu * (1 - illu)  ([B,1,H,W] == NHWC with C = 1)
+            _chk(L.lib().upr_t_pointwise(_p(g_illu.contiguous().to(torch.float32)), _p(illu), _p(g_r.t), illu.numel(),
+                                         1, None, None, ctypes.c_float(0), ctypes.c_uint64(0), _stream()),
+                 "sigmoid_bwd")
+            ie.bwd(g_r)
+        return None, None, None, None
+
+
+def ienet_train_forward(module, x):
+    """Training-mode ResidualIENet forward on the HIP engine.  Every call gets
+    its own layer objects (saved activations), like reference autograd."""
+    from .train import IENetT
+    if x.dtype != torch.float32:
+        raise TypeError("UP-Retinex HIP training computes in float32; pass a float32 batch")
+    ps = list(module.parameters())
+    flat = getattr(ps[0], "_upr_flat", None)
+    if flat is None or any(getattr(p, "_upr_flat", None) is not flat for p in ps) or flat.flat.device != x.device:
+        flat = FlatParams(module)
+    anchor = module.__dict__.get("_upr_anchor")
+    if anchor is None or anchor.device != x.device:
+        anchor = torch.empty(0, device=x.device, requires_grad=True)
+        module.__dict__["_upr_anchor"] = anchor
+    return _IENetStep.apply(x.contiguous(), anchor, IENetT(module), flat)
+
+
 class _LossStep(torch.autograd.Function):
     @staticmethod
     def forward(ctx, low, enh, illu, refl, engine):
@@ -109,7 +162,16 @@ def _scalar_of(terms, i):
 
 def loss_forward(engine, low, enh, illu, refl):
     """TotalLoss.forward on the HIP engine -> (total 0-dim tensor, device terms[9]).
-    With autograd recording (training), total carries the loss backward."""
+    With autograd recording (training), total carries the loss backward.
+
+    The engine produces the gradients w.r.t. (enh, illu, refl) only: the
+    reference's exposure target, smoothness edge weights and spatial /
+    frequency terms also depend on img_low, so an img_low that requires grad
+    is refused instead of silently getting no gradient."""
+    if torch.is_grad_enabled() and low.requires_grad:
+        raise NotImplementedError("UP-Retinex losses: no gradient w.r.t. img_low (the HIP loss engine "
+                                  "differentiates w.r.t. enhanced / illumination / reflectance); pass "
+                                  "img_low.detach() or run under torch.no_grad()")
     if torch.is_grad_enabled() and (enh.requires_grad or illu.requires_grad or refl.requires_grad):
         return _LossStep.apply(low, enh, illu, refl, engine)
     terms, _ = engine(low, enh, illu, refl, grads=False)

@@ -34,6 +34,17 @@ TERM_ORDER = ("exposure", "smoothness", "color", "spatial", "decouple", "percept
 VGG19_E = (64, 64, "M", 128, 128, "M", 256, 256, 256, 256, "M", 512, 512, 512, 512, "M", 512, 512, 512, 512, "M")
 
 
+def texture_complexity(img, method):
+    """img [B,C,H,W] float32 contiguous on the device -> [B] float32 (method 0 tv, 1 edge_density)."""
+    B, C, H, W = img.shape
+    acc = torch.empty((2 * B,), dtype=torch.float64, device=img.device)
+    out = torch.empty((B,), dtype=torch.float32, device=img.device)
+    with torch.cuda.device(img.device):
+        _chk(L.lib().upr_t_texture_complexity(_p(img), B, C, H, W, int(method), _p(acc), _p(out), _stream()),
+             "texture_complexity")
+    return out
+
+
 def vgg19_features(seed=None):
     """torchvision.models.vgg19().features layout (config "E"); with a seed,
     PyTorch's default Conv2d init drawn under torch.manual_seed(seed) — the

@@ -44,19 +44,27 @@ class _Workspace:
     to torch's caching allocator from) the stream that uses it, so the
     allocator's stream ordering keeps a replaced buffer alive until the work
     queued on that stream has drained (include/upr.h: thread-safe across
-    distinct handles or streams)."""
+    distinct handles or streams).  At most MAX_STREAMS buffers are kept (least
+    recently used evicted), so code that makes a new stream per request does
+    not pin a buffer per stream; an evicted buffer returns to torch's caching
+    allocator, which reuses it on its own stream only (stream-ordered safe)."""
+
+    MAX_STREAMS = 8
 
     def __init__(self):
-        self.buf = {}
+        from collections import OrderedDict
+        self.buf = OrderedDict()
 
     def get(self, dev, nbytes):
         stream = torch.cuda.current_stream(dev)
         key = (dev.type, dev.index, stream.cuda_stream)
-        b = self.buf.get(key)
+        b = self.buf.pop(key, None)
         if b is None or b.numel() < nbytes:
             with torch.cuda.stream(stream):
                 b = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
-            self.buf[key] = b
+        self.buf[key] = b  # most recently used last
+        while len(self.buf) > self.MAX_STREAMS:
+            self.buf.popitem(last=False)
         return b
 
 
@@ -66,11 +74,12 @@ _WS = _Workspace()
 class ModelHandle:
     """Owns one UprModel* (packed device weights) built from a state_dict."""
 
-    def __init__(self, state_dict, use_preact, use_aspp, dtype, device, ienet_only=False, prefix=""):
+    def __init__(self, state_dict, use_preact, use_aspp, dtype, device, ienet_only=False, prefix="", head_only=False):
         lib = L.lib()
         self.dtype = dtype
         self.device = device
         self.ienet_only = ienet_only
+        self.head_only = head_only
         names, descs, keep = [], [], []
         for k, v in state_dict.items():
             if not torch.is_floating_point(v):
@@ -88,7 +97,7 @@ class ModelHandle:
             descs.append(d)
         arr = (L.UprTensorDesc * len(descs))(*descs)
         out = ctypes.c_void_p()
-        flags = L.UPR_MODEL_IENET_ONLY if ienet_only else 0
+        flags = (L.UPR_MODEL_IENET_ONLY if ienet_only else 0) | (L.UPR_MODEL_HEAD_ONLY if head_only else 0)
         with torch.cuda.device(device):
             rc = lib.upr_model_create(arr, len(descs), int(bool(use_preact)), int(bool(use_aspp)),
                                       dtype_code(dtype), flags, ctypes.byref(out))
@@ -117,6 +126,27 @@ class ModelHandle:
         L.check(self._lib.upr_model_profile_read(self._h, arr, n.value, ctypes.byref(n)), "upr_model_profile_read")
         return [{"name": a.name.decode(), "kind": "conv_igemm" if a.kind == L.UPR_OP_CONV_IGEMM else "other",
                  "calls": a.calls, "ms": a.ms, "flops": a.flops, "bytes": a.bytes} for a in arr[:n.value]]
+
+    def enhance(self, x, refl):
+        """HEAD_ONLY handle: multi_scale_enhance(x, refl) -> enhanced [B,3,H,W]."""
+        _require_device(x)
+        _require_device(refl, "reflectance")
+        if x.dim() != 4 or x.shape[1] != 3 or refl.shape != x.shape:
+            raise RuntimeError(f"expected x and reflectance of one shape [B, 3, H, W], got {tuple(x.shape)} and "
+                               f"{tuple(refl.shape)}")
+        if x.dtype != self.dtype or refl.dtype != self.dtype:
+            raise RuntimeError(f"input dtypes {x.dtype}/{refl.dtype} do not match model dtype {self.dtype}")
+        x, refl = x.contiguous(), refl.contiguous()
+        B, _, H, W = x.shape
+        dev = x.device
+        with torch.cuda.device(dev):
+            enh = torch.empty_like(x)
+            nbytes = self._lib.upr_model_workspace(self._h, B, H, W)
+            ws = _WS.get(dev, nbytes)
+            rc = self._lib.upr_model_forward(self._h, _ptr(x), B, H, W, _ptr(enh), _ptr(refl), None,
+                                             _ptr(ws), ctypes.c_size_t(ws.numel()), _stream(dev))
+        L.check(rc, "upr_model_forward(head only)")
+        return enh
 
     def forward(self, x):
         _require_device(x)
@@ -327,3 +357,44 @@ def content_aware(x, enh=None, saliency=False, attention=False):
                                    ctypes.c_size_t(ws.numel()), B, H, W, dtype_code(x.dtype), _stream(dev))
     L.check(rc, "upr_content_aware")
     return out, sal, att
+
+
+class _Decompose(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, illu):
+        B, C, H, W = x.shape
+        refl = torch.empty_like(x)
+        with torch.cuda.device(x.device):
+            rc = L.lib().upr_retinex_decompose(_ptr(x), _ptr(illu), _ptr(refl), B, C, H, W, illu.shape[1],
+                                               dtype_code(x.dtype), _stream(x.device))
+        L.check(rc, "upr_retinex_decompose")
+        ctx.save_for_backward(x, illu)
+        return refl
+
+    @staticmethod
+    def backward(ctx, g):
+        x, illu = ctx.saved_tensors
+        B, C, H, W = x.shape
+        gx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        gi = torch.empty_like(illu) if ctx.needs_input_grad[1] else None
+        g = g.contiguous().to(x.dtype)
+        with torch.cuda.device(x.device):
+            rc = L.lib().upr_retinex_decompose_bwd(_ptr(x), _ptr(illu), _ptr(g), _ptr(gx), _ptr(gi), B, C, H, W,
+                                                   illu.shape[1], dtype_code(x.dtype), _stream(x.device))
+        L.check(rc, "upr_retinex_decompose_bwd")
+        return gx, gi
+
+
+def retinex_decompose(x, illu):
+    """x / (illu + 1e-6) (models/model.py:405-413) on the device, illu [B,1,H,W]
+    broadcast over the channels (or [B,C,H,W]); differentiable in x and illu."""
+    _require_device(x)
+    _require_device(illu, "illumination")
+    if x.dim() != 4 or illu.dim() != 4 or illu.shape[0] != x.shape[0] or illu.shape[2:] != x.shape[2:] or \
+            illu.shape[1] not in (1, x.shape[1]):
+        raise RuntimeError(f"retinex_decompose: shapes {tuple(x.shape)} and {tuple(illu.shape)} do not broadcast "
+                           f"as [B,C,H,W] / [B,1 or C,H,W]")
+    if x.dtype != illu.dtype:
+        raise RuntimeError(f"retinex_decompose: dtype mismatch {x.dtype} vs {illu.dtype}")
+    dtype_code(x.dtype)
+    return _Decompose.apply(x.contiguous(), illu.contiguous())

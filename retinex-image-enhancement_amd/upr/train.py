@@ -99,7 +99,7 @@ class _timed:
 
     def __init__(self, kind, what, flops):
         self.rec = None
-        if _PROF[0] is not None:
+        if _PROF[0] is not None and kind is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             self.rec = [kind, what, flops, e0, e1]
 
@@ -338,7 +338,7 @@ class Conv:
         F = self.flops(B, Ho, Wo)
         mf = self.mfma and x_view is None
         kw_ = ("mfma16" if self.amp and getattr(self, "x16", None) is not None else "mfma32") if mf else "direct"
-        with _timed(kw_, "wgrad", 0.0 if self.frozen else F):
+        with _timed(None if self.frozen else kw_, "wgrad", F):
             if not self.frozen:
                 gw = self.m.weight.grad
                 if self.mfma and x_view is None:
@@ -499,6 +499,7 @@ class BN:
                                   0, int(res_post), int(relu), _fp(out.t), out.cs, out.coff, _p(y16), st), "bn_apply")
         out.t16 = y16
         self.x = x
+        self.batch_stats = bool(m.training)  # the backward follows the statistics this forward used
         return out
 
     def bwd(self, g, gx):
@@ -511,7 +512,7 @@ class BN:
         acc = gx.consume_fresh()
         _chk(lib.upr_t_bn_bwd_apply(_fp(g.t), g.cs, g.coff, x.ptr(), x.cs, 0, _p(self.mean), _p(self.invstd),
                                     _p(m.weight), _p(self.acc), x.M, self.C, _p(m.weight.grad), _p(m.bias.grad),
-                                    _fp(gx.t), gx.cs, gx.coff, acc, st), "bn_bwd_apply")
+                                    _fp(gx.t), gx.cs, gx.coff, acc, int(self.batch_stats), st), "bn_bwd_apply")
 
 
 def relu_mask(g, y):
@@ -650,7 +651,9 @@ class ASPPT:
         _chk(L.lib().upr_t_broadcast(_fp(self.gp.t), x.B, x.H * x.W, C, ctypes.c_float(1.0), _fp(cat.t), cat.cs,
                                      C * (nb - 1), 0, _stream()), "broadcast")
         self.a = self.fb.fwd(self.fc.fwd(cat), relu=True)
-        if not self.training:
+        self.dropped = self.training  # the backward applies the mask only when this forward drew one
+        if not self.dropped:
+            self.mask = None
             return self.a  # nn.Dropout in eval mode is the identity
         out = Act.new(x.B, x.H, x.W, C, dev, fresh=False)
         self.mask = torch.empty((out.t.numel(),), dtype=torch.uint8, device=dev)
@@ -661,8 +664,12 @@ class ASPPT:
     def bwd(self, g, gx):
         dev = g.t.device
         C, nb, x = self.C, len(self.br) + 2, self.x
-        g_a = Act.new(g.B, g.H, g.W, C, dev, fresh=False)
-        pointwise(g.t, None, g_a.t, g.t.numel(), 3, mask_in=self.mask, p=self.p)
+        g_a = Act.new(g.B, g.H, g.W, C, dev)
+        if self.dropped:
+            pointwise(g.t, None, g_a.t, g.t.numel(), 3, mask_in=self.mask, p=self.p)
+            g_a.fresh = False
+        else:
+            add_into(g_a, g)
         relu_mask(g_a, self.a)
         g_cf = Act.new(g.B, g.H, g.W, C, dev)
         self.fb.bwd(g_a, g_cf)
@@ -839,6 +846,7 @@ class IENetT:
 
     def fwd(self, x):
         B, _, H, W = x.shape
+        self.x = x  # keeps the input alive: the backward reads it through the raw view below
         self.xin = (nchw_view(x), B, H, W)
         self.x1 = self.inp.fwd(None, relu=True, x_view=self.xin, out=Act.new(B, H, W, 32, x.device, fresh=False))
         self.x2 = self.enc[0].fwd(self.x1)

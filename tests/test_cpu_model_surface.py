@@ -72,14 +72,16 @@ def test_submodules_have_no_cpu_path():
         with pytest.raises(RuntimeError, match="ROCm"):
             mod.eval()(torch.rand(1, c, 8, 8))
     m = M.UP_Retinex()
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(RuntimeError, match="ROCm"):
         m.retinex_decompose(torch.rand(1, 3, 8, 8), torch.rand(1, 1, 8, 8))
+    with pytest.raises(RuntimeError, match="ROCm"):
+        m.eval().multi_scale_enhance(torch.rand(1, 3, 16, 16), torch.rand(1, 3, 16, 16), None)
 
 
-def test_training_mode_cpu_input_raises_and_ienet_train_unsupported():
-    """Training mode is supported on the device (upr/autograd.model_train_forward,
-    tests/test_gpu_train.py); on a CPU tensor it raises like eval mode (no CPU
-    path), and a standalone ResidualIENet training forward is refused."""
+def test_training_mode_cpu_input_raises():
+    """Training mode is supported on the device (upr/autograd.model_train_forward /
+    ienet_train_forward, tests/test_gpu_train.py, tests/test_gpu_api_surface.py);
+    on a CPU tensor it raises like eval mode (no CPU path)."""
     m = M.UP_Retinex(use_preact=False, use_aspp=False)  # .train() by default
     assert m.training
     with pytest.raises(RuntimeError, match="ROCm"):

@@ -72,10 +72,12 @@ def test_loss_term_module_value_and_grad(case):
     name, make, ref_fn, idx = case
     data = _inputs()
     mod = make(Lmod).to(DEV)
-    dev_in = _leaf(*[data[i] for i in idx])
     ref_in = _leaf(*[data[i] for i in idx], dev=False)
-    # only the first argument is differentiable for the (x, img_low) modules
+    # only the first argument is differentiable for the (x, img_low) modules:
+    # img_low goes in without requires_grad (the engine has no img_low gradient
+    # and refuses one that requires grad: test_loss_term_refuses_img_low_grad)
     diff = 2 if idx in ((2, 3),) or name == "color" else 1
+    dev_in = _leaf(*[data[i] for i in idx[:diff]]) + [data[i].to(DEV) for i in idx[diff:]]
     val = mod(*dev_in)
     assert val.dim() == 0 and val.requires_grad
     val.backward()
@@ -83,6 +85,17 @@ def test_loss_term_module_value_and_grad(case):
     ref = ref_fn(otrain, *ref_in)
     ref.backward()
     _check(name, val.detach().cpu(), ref.detach(), dev_in[:diff], ref_in[:diff])
+
+
+def test_loss_term_refuses_img_low_grad():
+    from losses import loss as Lmod
+    low, enh, _, _ = _inputs()
+    mod = Lmod.AdaptiveExposureLoss().to(DEV)
+    e_d, l_d = _leaf(enh, low)
+    with pytest.raises(NotImplementedError):
+        mod(e_d, l_d)
+    with torch.no_grad():
+        mod(e_d, l_d)  # no autograd recording: fine
 
 
 def test_perceptual_module_value_and_grad():

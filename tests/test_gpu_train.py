@@ -488,6 +488,70 @@ def test_train_grads_b8_vs_fp64(pre):
     print(f"pre={pre}: worst (device, fp32 CPU) rel-L2 vs fp64 {worst}")
 
 
+def test_train_graph_frozen_bn_and_eval_aspp_vs_oracle():
+    """model.train() followed by .eval() on one BatchNorm and on the ASPP module
+    (the fine-tuning pattern): those modules use their running statistics and
+    no Dropout in the forward, so their backward is the affine map (dx = g *
+    gamma * invstd, not the batch-statistics form) while dgamma / dbeta still
+    accumulate.  Forward + backward of a random projection of the outputs vs
+    the fp64 oracle with the same modules in eval mode: per tensor rel-L2 <=
+    max(4 x the fp32 oracle's, 2e-3).  The batch-statistics backward on those
+    modules would be off by O(1)."""
+    from oracle import net as onet
+    from oracle import train as otrain
+    B = 4
+    model = _model(True, True, seed=5)
+    with torch.no_grad():  # non-trivial running statistics for the frozen modules
+        for m in model.modules():
+            if isinstance(m, torch.nn.BatchNorm2d):
+                m.running_mean.uniform_(-0.2, 0.2)
+                m.running_var.uniform_(0.5, 1.5)
+    sd_cpu = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    sd0 = {k: v.clone() for k, v in sd_cpu.items()}  # the fp32 oracle run updates sd_cpu's buffers in place
+    model = model.to(DEV).train()
+    model.ie_net.enc2.bn1.eval()
+    model.ie_net.bottleneck[1].eval()
+    frozen = ("ie_net.enc2.bn1", "ie_net.bottleneck.1.")
+    x = torch.rand(B, 3, 64, 64, generator=torch.Generator().manual_seed(8)) * 0.6
+    gen = torch.Generator().manual_seed(9)
+    r = [torch.randn(s, generator=gen) for s in ((B, 3, 64, 64), (B, 3, 64, 64), (B, 1, 64, 64))]
+    outs = model(x.to(DEV))
+    sum((o * ri.to(DEV)).sum() for o, ri in zip(outs, r)).backward()
+    torch.cuda.synchronize()
+    names = otrain.param_names(sd_cpu)
+
+    def oracle(dt):
+        s2 = {k: (v.to(dt) if v.is_floating_point() else v.clone()) for k, v in sd_cpu.items()}
+        params = {k: s2[k].clone().requires_grad_(True) for k in names}
+        work = dict(s2)
+        work.update(params)
+        with otrain.train_mode(eval_prefixes=frozen):
+            o_r = onet.forward(work, x.to(dt), True, True)
+        sum((o * ri.to(dt)).sum() for o, ri in zip(o_r, r)).backward()
+        return o_r, {k: params[k].grad.double() for k in names}, work
+
+    o64, g64, w64 = oracle(torch.float64)
+    _, g32, _ = oracle(torch.float32)
+    for o, o_r in zip(outs, o64):
+        _close(o, o_r, 1e-4, "output")
+    # the frozen modules' running statistics are untouched, the others moved
+    for k, v in model.state_dict().items():
+        if k.endswith("running_mean"):
+            same = torch.equal(v.cpu(), sd0[k])
+            assert same == k.startswith(frozen), k
+            _close(v, w64[k], 1e-5, k)
+    dev_params = dict(model.named_parameters())
+    gmax = max(v.abs().max().item() for v in g64.values())
+    for n in names:
+        ref = g64[n]
+        if ref.abs().max().item() < 1e-9 * gmax:
+            continue  # BN-fed conv bias: zero true gradient
+        rn = ref.norm().item()
+        l2 = (dev_params[n].grad.double().cpu() - ref).norm().item() / rn
+        l2c = (g32[n] - ref).norm().item() / rn
+        assert l2 <= max(4.0 * l2c, 2e-3), f"grad {n}: rel-L2 {l2:.3e} (fp32 CPU {l2c:.3e})"
+
+
 def _amp_setup(seed=0):
     from losses.loss import TotalLoss
     from trainers.train import make_optimizer
