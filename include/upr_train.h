@@ -71,7 +71,9 @@ int upr_t_conv_mfma(const float* x, int B, int H, int W, int Cin, int x_cs, int 
  * (fp32 accumulate, bias, ReLU) writes y16 (dense fp16 [B,Ho,Wo,N], or the
  * ConvTranspose layout for store 1), then y = float(y16) (+ res, in fp32,
  * indexed like upr_t_conv_mfma's: res == y accumulates).  res and relu are
- * exclusive. */
+ * exclusive.  store | 2: y16 must afterwards hold (half)y exactly (no res):
+ * the next autocast conv reading y can take it as its x16 (x16_ready); without
+ * that bit y16 is scratch. */
 int upr_t_conv_mfma16(const float* x, int B, int H, int W, int Cin, int x_cs, int x_coff, const void* wp16,
                       const float* bias, int N, int kh, int kw, int stride, int pad, int dil, const float* res,
                       int res_cs, int relu, float* y, int y_cs, int y_coff, int store, void* x16, int x16_ready,
@@ -136,6 +138,21 @@ int upr_t_bn_bwd_apply(const float* g, int g_cs, int g_coff, const float* x, int
                        const float* invstd, const float* gamma, const double* acc, int M, int C, float* dgamma,
                        float* dbeta, float* dx, int dx_cs, int dx_coff, int accumulate, int batch_stats,
                        void* stream);
+/* upr_t_bn_bwd_reduce + upr_t_bn_bwd_apply in one call, with (relu != 0) the
+ * consumer ReLU of a relu(bn(x)) folded in: g counts only where bn(x) > 0,
+ * recomputed from x with the forward's expression (so no separate ReLU-mask
+ * pass), and (dx16 non-NULL) a compact [M][C] fp16 copy of dx for the
+ * autocast input-gradient conv that consumes it.  acc: 2C doubles of scratch
+ * (zeroed here).  Needs C % 4 == 0, C <= 1024, 16-byte aligned rows;
+ * UPR_ERR_UNSUPPORTED otherwise (the caller takes the separate kernels). */
+int upr_t_bn_bwd_fused(const float* g, int g_cs, int g_coff, const float* x, int x_cs, const float* mean,
+                       const float* invstd, const float* gamma, const float* beta, int relu, int M, int C,
+                       double* acc, float* dgamma, float* dbeta, float* dx, int dx_cs, int dx_coff, int accumulate,
+                       int batch_stats, void* dx16, void* stream);
+/* upr_t_zero_upsample with an fp16 result z16 [B,2Ho,2Wo,C] (dy rounded to
+ * fp16: the autocast stride-2 input-gradient conv's operand); C % 8 == 0. */
+int upr_t_zero_upsample16(const float* dy, int B, int Ho, int Wo, int C, int dy_cs, int dy_coff, void* z16,
+                          void* stream);
 /* out[C] (+)= per-channel sum of g[M][cs] (conv bias gradients). */
 int upr_t_chan_sum(const float* g, int M, int C, int cs, int coff, float* out, int accumulate, void* stream);
 

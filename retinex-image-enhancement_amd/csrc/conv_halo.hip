@@ -678,6 +678,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
             f32x4_h w4 = {hto_f(ov[e]), hto_f(ov[e + 1]), hto_f(ov[e + 2]), hto_f(ov[e + 3])};
             if (r32) w4 += *(const f32x4_h*)(r32 + e);
             *(f32x4_h*)(d32 + e) = w4;
+            if (op.out32_h16) {
+              typedef _Float16 h4h __attribute__((ext_vector_type(4)));
+              *(h4h*)((half_t*)op.out32_h16 + m * op.out32_h16_cs + n0 + nb0 + e) =
+                  h4h{(half_t)w4[0], (half_t)w4[1], (half_t)w4[2], (half_t)w4[3]};
+            }
           }
           continue;
         }

@@ -690,6 +690,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, RingCfg<MODE, C, NB, FL
                                          (size_t)((g0 + g) * 16 + fr) * op.out32_cs + fg * 4
                                    : g_ring_sink32 + tid * 64;
             *(f32x4_r*)(d32 + nt * 16) = o32;
+            if (op.out32_h16) {  // compact fp16 copy: o itself (no res32 on the ring)
+              half_t* d16 = ovalid[g] ? (half_t*)op.out32_h16 + prow * op.out32_h16_cs +
+                                            (size_t)((g0 + g) * 16 + fr) * op.out32_h16_cs + fg * 4
+                                      : (half_t*)(g_ring_sink + tid * 16);
+              *(uint2*)(d16 + nt * 16) = __builtin_bit_cast(uint2, o);
+            }
           } else {
             *(uint2*)(dg + nt * 16) = __builtin_bit_cast(uint2, o);
           }

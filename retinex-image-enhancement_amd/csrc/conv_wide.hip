@@ -270,6 +270,11 @@ __device__ __forceinline__ void wide_epilogue(const ConvOp& op, f32x4_w (&acc)[W
             for (int e = 0; e < 4; ++e) t[e] = (float)o[hh * 4 + e];
             if (op.res32) t += *(const f32x4_w*)(op.res32 + pix * op.res32_cs + ch + hh * 4);
             *(f32x4_w*)(d32 + hh * 4) = t;
+            if (op.out32_h16) {
+              typedef _Float16 h4w __attribute__((ext_vector_type(4)));
+              *(h4w*)((half_t*)op.out32_h16 + pix * op.out32_h16_cs + ch + hh * 4) =
+                  h4w{(half_t)t[0], (half_t)t[1], (half_t)t[2], (half_t)t[3]};
+            }
           }
         } else {
           *(f16x8_w*)((half_t*)op.out + pix * op.out_cs + op.out_coff + ch) = o;

@@ -274,7 +274,7 @@ struct Op {
   int out = -1, out_cs = 0, out_coff = 0;
   int res1 = -1, res1_cs = 0, res2 = -1, res2_cs = 0;
   int relu = 0, store = kStoreNHWC;
-  int pool_slot = -1;   // index into pool buffer (units of B*256 8-byte entries)
+  int pool_slot = -1;   // index into pool buffer (units of B*256 16-byte entries)
   int img_bias = 0;
   size_t head_w = 0; float head_b = 0.f;
   // conv3 / fam
@@ -387,7 +387,7 @@ static size_t ws_layout(const UprModel* m, int B, int H, int W, size_t* offs) {
   const size_t elt = m->dtype == kF16 ? 2 : 4;
   for (int id = 1; id < B_COUNT; ++id) {
     size_t bytes = 0;
-    if (id == B_POOL) bytes = (size_t)4 * B * 256 * 8;
+    if (id == B_POOL) bytes = (size_t)4 * B * 256 * 4 * kPoolEntryFloats;
     else if (id == B_CA) bytes = (size_t)3 * B * 32 * 4;
     else if (id == B_IB) bytes = (size_t)B * 256 * 4;
     else {
@@ -815,7 +815,7 @@ static int run_forward(UprModel* m, const void* x, int B, int H, int W, void* en
   float* pool = (float*)buf(B_POOL);
   float* ca = (float*)buf(B_CA);
   float* ib = (float*)buf(B_IB);
-  UPR_CHECK_HIP(hipMemsetAsync(pool, 0, (size_t)4 * B * 256 * 8, st));
+  UPR_CHECK_HIP(hipMemsetAsync(pool, 0, (size_t)4 * B * 256 * 4 * kPoolEntryFloats, st));
   const int H4 = (H / 2) / 2, W4 = (W / 2) / 2, H16 = (H / 4) / 4, W16 = (W / 4) / 4;
   auto lvl_dims = [&](int lshift, int& h, int& w) {
     if (lshift == 2) { h = H4; w = W4; }
@@ -889,7 +889,7 @@ static int run_forward(UprModel* m, const void* x, int B, int H, int W, void* en
         } else {
           c.out = buf(o.out); c.out_cs = o.out_cs; c.out_coff = o.out_coff;
         }
-        c.pool = o.pool_slot >= 0 ? pool + (size_t)o.pool_slot * B * 512 : nullptr;  // 8-byte entries
+        c.pool = o.pool_slot >= 0 ? pool + (size_t)o.pool_slot * B * 256 * kPoolEntryFloats : nullptr;
         if (o.out2 >= 0) {
           c.out2 = buf(o.out2); c.out2_cs = L.N;
           c.pre2_scale = fptr(o.ps); c.pre2_shift = fptr(o.ph);
@@ -925,7 +925,7 @@ static int run_forward(UprModel* m, const void* x, int B, int H, int W, void* en
       case OP_ASPP_G: {
         const int h = H >> 3, w = W >> 3;
         hipLaunchKernelGGL(aspp_global_kernel, dim3(B), dim3(256), 2 * 256 * sizeof(float), st,
-                           pool + (size_t)3 * B * 512, fptr(o.w), fptr(o.b), fptr(o.P), ib, 256,
+                           pool + (size_t)3 * B * 256 * kPoolEntryFloats, fptr(o.w), fptr(o.b), fptr(o.P), ib, 256,
                            1.f / (float)(h * w));
         rc = (int)hipGetLastError();
         break;
@@ -933,7 +933,7 @@ static int run_forward(UprModel* m, const void* x, int B, int H, int W, void* en
       case OP_FAM_CA: {
         int h, w;
         lvl_dims(o.lvl_shift, h, w);
-        rc = launch_fam_ca(pool + (size_t)o.fam * B * 512, fptr(o.ca_w1), fptr(o.ca_b1), fptr(o.ca_w2),
+        rc = launch_fam_ca(pool + (size_t)o.fam * B * 256 * kPoolEntryFloats, fptr(o.ca_w1), fptr(o.ca_b1), fptr(o.ca_w2),
                            fptr(o.ca_b2), ca + (size_t)o.fam * B * 32, B, h * w, st);
         break;
       }

@@ -395,6 +395,30 @@ __global__ void zero_upsample_kernel(const float* __restrict__ dy, int B, int Ho
   }
 }
 
+// fp16 form for the autocast stride-2 input gradient: dy (fp32) rounded to
+// fp16 as the conv's cast would, zero-upsampled, 8 channels per thread
+__global__ __launch_bounds__(256) void zero_upsample16_kernel(const float* __restrict__ dy, int B, int Ho, int Wo,
+                                                              int C, int cs, int coff, half_t* __restrict__ z) {
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  const int C8 = C / 8;
+  const long long n = (long long)B * 2 * Ho * 2 * Wo * C8;
+  GSTRIDE(i, n) {
+    const int c = (int)(i % C8) * 8;
+    long long r = i / C8;
+    const int X = (int)(r % (2 * Wo)); r /= 2 * Wo;
+    const int Y = (int)(r % (2 * Ho));
+    const int b = (int)(r / (2 * Ho));
+    h8 v = h8{};
+    if (!(X & 1) && !(Y & 1)) {
+      const float* src = dy + (((long long)b * Ho + (Y >> 1)) * Wo + (X >> 1)) * cs + coff + c;
+      const float4 lo = *(const float4*)src, hi = *(const float4*)(src + 4);
+      v = h8{(half_t)lo.x, (half_t)lo.y, (half_t)lo.z, (half_t)lo.w, (half_t)hi.x, (half_t)hi.y, (half_t)hi.z,
+             (half_t)hi.w};
+    }
+    *(h8*)(z + i * 8) = v;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // per-channel reductions over M rows: mode 0 (x, x^2), mode 1 (g, g*xhat),
 // mode 2 (g) -> float out via atomics
@@ -443,11 +467,21 @@ static int reduce_grid(int M) { return grid_for(M, 512, 2048); }
 // float4 form of chan_reduce_kernel (C % 4 == 0, C <= 1024, 16-byte aligned
 // rows): a thread owns 4 consecutive channels, so a wave reads whole 16-byte
 // chunks of 64 / (C/4) rows per instruction (same per-channel fp64 sums)
+// y = bn(x) of the forward (bn_apply kernels) and of the ReLU-mask recompute
+// in the fused backward: ONE expression, so the recomputed sign is the
+// forward's bit for bit
+__device__ __forceinline__ float bn_affine(float x, float mean, float invstd, float gamma, float beta) {
+  return __builtin_fmaf((x - mean) * invstd, gamma, beta);
+}
+
 __global__ __launch_bounds__(256) void chan_reduce4_kernel(const float* __restrict__ a, int a_cs, int a_coff,
                                                            const float* __restrict__ x, int x_cs, int x_coff,
                                                            const float* __restrict__ mean,
                                                            const float* __restrict__ invstd, int M, int C, int mode,
-                                                           double* __restrict__ acc, float* __restrict__ fout) {
+                                                           double* __restrict__ acc, float* __restrict__ fout,
+                                                           const float* __restrict__ gamma = nullptr,
+                                                           const float* __restrict__ beta = nullptr) {
+  // mode 3: mode 1 with the consumer ReLU folded in (g counts where bn(x) > 0)
   __shared__ double s1[256 * 4], s2[256 * 4];
   const int rows_per_block = (M + gridDim.x - 1) / gridDim.x;
   const int r0 = blockIdx.x * rows_per_block;
@@ -457,16 +491,22 @@ __global__ __launch_bounds__(256) void chan_reduce4_kernel(const float* __restri
   const int q = threadIdx.x % C4, rg = threadIdx.x / C4;
   double u[4] = {0.0, 0.0, 0.0, 0.0}, v[4] = {0.0, 0.0, 0.0, 0.0};
   if (rg < R) {
-    float4 mu = make_float4(0.f, 0.f, 0.f, 0.f), is = mu;
-    if (mode == 1) { mu = ((const float4*)mean)[q]; is = ((const float4*)invstd)[q]; }
-    for (int r = r0 + rg; r < r1; r += R) {
-      const float4 av = *(const float4*)(a + (size_t)r * a_cs + a_coff + 4 * q);
-      const float ae[4] = {av.x, av.y, av.z, av.w};
-      if (mode == 1) {
-        const float4 xv = *(const float4*)(x + (size_t)r * x_cs + x_coff + 4 * q);
-        const float xh[4] = {(xv.x - mu.x) * is.x, (xv.y - mu.y) * is.y, (xv.z - mu.z) * is.z, (xv.w - mu.w) * is.w};
+    float4 mu = make_float4(0.f, 0.f, 0.f, 0.f), is = mu, ga = mu, be = mu;
+    if (mode == 1 || mode == 3) { mu = ((const float4*)mean)[q]; is = ((const float4*)invstd)[q]; }
+    if (mode == 3) { ga = ((const float4*)gamma)[q]; be = ((const float4*)beta)[q]; }
+    auto acc_row = [&](const float4 av, const float4 xv) {
+      float ae[4] = {av.x, av.y, av.z, av.w};
+      if (mode == 1 || mode == 3) {
+        const float xe[4] = {xv.x, xv.y, xv.z, xv.w};
+        const float mue[4] = {mu.x, mu.y, mu.z, mu.w}, ise[4] = {is.x, is.y, is.z, is.w};
+        const float gae[4] = {ga.x, ga.y, ga.z, ga.w}, bee[4] = {be.x, be.y, be.z, be.w};
 #pragma unroll
-        for (int e = 0; e < 4; ++e) { u[e] += ae[e]; v[e] += (double)ae[e] * xh[e]; }
+        for (int e = 0; e < 4; ++e) {
+          if (mode == 3 && !(bn_affine(xe[e], mue[e], ise[e], gae[e], bee[e]) > 0.f)) ae[e] = 0.f;
+          const float xh = (xe[e] - mue[e]) * ise[e];
+          u[e] += ae[e];
+          v[e] += (double)ae[e] * xh;
+        }
       } else if (mode == 0) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) { u[e] += ae[e]; v[e] += (double)ae[e] * ae[e]; }
@@ -474,7 +514,26 @@ __global__ __launch_bounds__(256) void chan_reduce4_kernel(const float* __restri
 #pragma unroll
         for (int e = 0; e < 4; ++e) u[e] += ae[e];
       }
+    };
+    // four rows' loads issued before any is consumed (a single dependent load
+    // per iteration left the reduction latency-bound at ~1.2 TB/s)
+    const float* ap = a + a_coff + 4 * q;
+    const float* xp = x ? x + x_coff + 4 * q : nullptr;
+    int r = r0 + rg;
+    for (; r + 3 * R < r1; r += 4 * R) {
+      float4 av[4], xv[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) av[k] = *(const float4*)(ap + (size_t)(r + k * R) * a_cs);
+      if (mode == 1 || mode == 3) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) xv[k] = *(const float4*)(xp + (size_t)(r + k * R) * x_cs);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc_row(av[k], (mode == 1 || mode == 3) ? xv[k] : av[k]);
     }
+    for (; r < r1; r += R)
+      acc_row(*(const float4*)(ap + (size_t)r * a_cs),
+              (mode == 1 || mode == 3) ? *(const float4*)(xp + (size_t)r * x_cs) : make_float4(0.f, 0.f, 0.f, 0.f));
   }
 #pragma unroll
   for (int e = 0; e < 4; ++e) { s1[threadIdx.x * 4 + e] = u[e]; s2[threadIdx.x * 4 + e] = v[e]; }
@@ -539,7 +598,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
   GSTRIDE(i, n) {
     const int c = (int)(i % C);
     const long long m = i / C;
-    float v = (x[m * x_cs + x_coff + c] - mean[c]) * invstd[c] * gamma[c] + beta[c];
+    float v = bn_affine(x[m * x_cs + x_coff + c], mean[c], invstd[c], gamma[c], beta[c]);
     const float rv = res ? res[m * res_cs + res_coff + c] : 0.f;
     if (!res_post) v += rv;
     if (relu) v = fmaxf(v, 0.f);
@@ -568,7 +627,7 @@ __global__ __launch_bounds__(256) void bn_apply4_kernel(const float* __restrict_
     float o[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      float v = (xa[e] - mean[c + e]) * invstd[c + e] * gamma[c + e] + beta[c + e];
+      float v = bn_affine(xa[e], mean[c + e], invstd[c + e], gamma[c + e], beta[c + e]);
       if (!res_post) v += ra[e];
       if (relu) v = fmaxf(v, 0.f);
       if (res_post) v += ra[e];
@@ -620,7 +679,11 @@ __global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(const float* __restr
                                                             const float* __restrict__ gamma,
                                                             const double* __restrict__ acc, int M, int C,
                                                             float* dgamma, float* dbeta, float* dx, int dx_cs,
-                                                            int dx_coff, int accum, int batch_stats) {
+                                                            int dx_coff, int accum, int batch_stats,
+                                                            const float* __restrict__ beta = nullptr, int relu = 0,
+                                                            half_t* __restrict__ dx16 = nullptr) {
+  // relu: the consumer ReLU folded in (g counts where bn(x) > 0, recomputed);
+  // dx16: compact [M][C] fp16 copy of dx for the autocast input-gradient conv
   if (blockIdx.x == 0) {
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
       if (dgamma) dgamma[c] += (float)acc[C + c];
@@ -645,11 +708,17 @@ __global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(const float* __restr
       const float xh = (xa[e] - mean[c + e]) * is;
       const float sg = batch_stats ? (float)(acc[c + e] / M) : 0.f;
       const float sgx = batch_stats ? (float)(acc[C + c + e] / M) : 0.f;
-      float v = gamma[c + e] * is * (ga[e] - sg - xh * sgx);
+      float gg = ga[e];
+      if (relu && !(bn_affine(xa[e], mean[c + e], is, gamma[c + e], beta[c + e]) > 0.f)) gg = 0.f;
+      float v = gamma[c + e] * is * (gg - sg - xh * sgx);
       if (accum) v += pa[e];
       r[e] = v;
     }
     *o = make_float4(r[0], r[1], r[2], r[3]);
+    if (dx16) {
+      typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+      *(h4*)(dx16 + m * C + c) = h4{(half_t)r[0], (half_t)r[1], (half_t)r[2], (half_t)r[3]};
+    }
   }
 }
 
@@ -1805,6 +1874,8 @@ int upr_t_conv_mfma16(const float* x, int B, int H, int W, int Cin, int x_cs, in
                       void* y16, void* stream) {
   if (!x16 || !wp16 || !y || !y16 || B <= 0 || Cin % 32 || N % 32 || Cin <= 0 || N <= 0) return UPR_ERR_ARG;
   if (!x16_ready && !x) return UPR_ERR_ARG;
+  const bool want16 = (store & 2) != 0;  // y16 must end up holding (half)y
+  store &= 1;
   if (kh <= 0 || kw <= 0 || stride <= 0 || dil <= 0 || pad < 0) return UPR_ERR_ARG;
   if (x_cs % 4 || x_coff % 4 || y_cs % 4 || y_coff % 4 || (res && res_cs % 4)) return UPR_ERR_ARG;
   if (res && relu) return UPR_ERR_ARG;  // the residual is added in fp32 after the fp16 GEMM
@@ -1834,6 +1905,7 @@ int upr_t_conv_mfma16(const float* x, int B, int H, int W, int Cin, int x_cs, in
     ConvOp c32 = c;
     c32.out32 = y; c32.out32_cs = y_cs; c32.out32_coff = y_coff;
     c32.res32 = res; c32.res32_cs = res_cs;
+    if (want16) { c32.out32_h16 = y16; c32.out32_h16_cs = store == 1 ? N / 4 : N; }
     const int rc = launch_conv_out32(c32, st);
     if (rc != kErrUnsupported) {
       if (rc != 0) return rc;
@@ -2006,6 +2078,37 @@ int upr_t_bn_bwd_apply(const float* g, int g_cs, int g_coff, const float* x, int
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), g, g_cs, g_coff, x, x_cs,
                      x_coff, mean, invstd, gamma, acc, M, C, dgamma, dbeta, dx, dx_cs, dx_coff, accumulate,
                        batch_stats);
+  LAUNCH_CHECK();
+}
+
+int upr_t_bn_bwd_fused(const float* g, int g_cs, int g_coff, const float* x, int x_cs, const float* mean,
+                       const float* invstd, const float* gamma, const float* beta, int relu, int M, int C,
+                       double* acc, float* dgamma, float* dbeta, float* dx, int dx_cs, int dx_coff, int accumulate,
+                       int batch_stats, void* dx16, void* stream) {
+  if (!g || !x || !acc || !dx || !gamma || !beta || !mean || !invstd || M <= 0 || C <= 0) return UPR_ERR_ARG;
+  const auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (C % 4 || C > 1024 || g_cs % 4 || g_coff % 4 || x_cs % 4 || dx_cs % 4 || dx_coff % 4 || !a16(g) || !a16(x) ||
+      !a16(dx) || !a16(mean) || !a16(invstd) || !a16(gamma) || !a16(beta) || ((uintptr_t)dx16 & 7))
+    return UPR_ERR_UNSUPPORTED;
+  hipStream_t st = ST(stream);
+  UPR_CHECK_HIP(hipMemsetAsync(acc, 0, sizeof(double) * 2 * C, st));
+  hipLaunchKernelGGL(chan_reduce4_kernel, dim3(reduce_grid(M)), dim3(256), 0, st, g, g_cs, g_coff, x, x_cs, 0, mean,
+                     invstd, M, C, relu ? 3 : 1, acc, nullptr, gamma, beta);
+  UPR_CHECK_HIP(hipGetLastError());
+  const long long n4 = (long long)M * (C / 4);
+  hipLaunchKernelGGL(bn_bwd_apply4_kernel, dim3(grid_for(n4)), dim3(256), 0, st, g, g_cs, g_coff, x, x_cs, 0, mean,
+                     invstd, gamma, acc, M, C, dgamma, dbeta, dx, dx_cs, dx_coff, accumulate, batch_stats, beta, relu,
+                     (half_t*)dx16);
+  LAUNCH_CHECK();
+}
+
+int upr_t_zero_upsample16(const float* dy, int B, int Ho, int Wo, int C, int dy_cs, int dy_coff, void* z16,
+                          void* stream) {
+  if (!dy || !z16 || C % 8 || dy_cs % 4 || dy_coff % 4 || ((uintptr_t)dy & 15) || ((uintptr_t)z16 & 15))
+    return UPR_ERR_ARG;
+  const long long n = (long long)B * 4 * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(zero_upsample16_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), dy, B, Ho, Wo, C, dy_cs,
+                     dy_coff, (half_t*)z16);
   LAUNCH_CHECK();
 }
 

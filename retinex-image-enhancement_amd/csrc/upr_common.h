@@ -99,6 +99,10 @@ struct ConvOp {
   // may alias out32); `out` is not written
   float* out32; int out32_cs, out32_coff;
   const float* res32; int res32_cs;
+  // with out32 (nullable): a compact fp16 copy of the same outputs,
+  // out32_h16[pix * out32_h16_cs + n] = (half)(the fp32 value stored) -- the
+  // next autocast conv's operand, so it needs no cast pass of its own
+  void* out32_h16; int out32_h16_cs;
 };
 
 // fp16 convs with an fp32 output (ConvOp::out32): the wide-tile and row-ring
@@ -112,15 +116,26 @@ inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 // Per-(image, channel) pool sums (ConvOp::pool: EnhancedFAM channel attention,
 // ASPP global branch) are accumulated as 64-bit fixed point (2^-24 units) with
 // integer atomics: the sum no longer depends on the order in which tiles /
-// units finish, so a forward is bit-for-bit reproducible.  A pool slot holds
-// 8 bytes per entry (the float* is only the carrier type).
+// units finish, so a forward is bit-for-bit reproducible.  A pool entry is 16
+// bytes (the float* is only the carrier type): the int64 sum, then a uint32 of
+// non-finite flags (bit 0 a +inf, bit 1 a -inf, bit 2 a NaN contribution),
+// set with an atomic OR instead of converting the value, so pool_get returns
+// what torch's mean would (+inf, -inf, or NaN for NaN / +inf with -inf).
 constexpr float kPoolScale = 16777216.f;  // 2^24
+constexpr int kPoolEntryFloats = 4;       // 16-byte entries
 #ifdef __HIPCC__
 __device__ __forceinline__ void pool_add(float* pool, size_t idx, float v) {
-  atomicAdd((unsigned long long*)pool + idx, (unsigned long long)__float2ll_rn(v * kPoolScale));
+  if (__builtin_isfinite(v)) {
+    atomicAdd((unsigned long long*)pool + 2 * idx, (unsigned long long)__float2ll_rn(v * kPoolScale));
+  } else {
+    const unsigned f = __builtin_isnan(v) ? 4u : (v > 0.f ? 1u : 2u);
+    atomicOr((unsigned*)pool + 4 * idx + 2, f);
+  }
 }
 __device__ __forceinline__ float pool_get(const float* pool, size_t idx) {
-  return (float)((double)(long long)((const unsigned long long*)pool)[idx] * (1.0 / 16777216.0));
+  const unsigned f = ((const unsigned*)pool)[4 * idx + 2];
+  if (f) return (f & 4u) || (f & 3u) == 3u ? __builtin_nanf("") : ((f & 1u) ? __builtin_inff() : -__builtin_inff());
+  return (float)((double)(long long)((const unsigned long long*)pool)[2 * idx] * (1.0 / 16777216.0));
 }
 #endif
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }

@@ -127,6 +127,9 @@ SIGNATURES.update({
     "upr_t_bn_bwd_reduce": (_i, [_p, _i, _i, _p, _i, _i, _p, _p, _i, _i, _p, _p]),
     "upr_t_bn_bwd_apply": (_i, [_p, _i, _i, _p, _i, _i, _p, _p, _p, _p, _i, _i, _p, _p, _p, _i, _i, _i, _i, _p]),
     "upr_t_chan_sum": (_i, [_p, _i, _i, _i, _i, _p, _i, _p]),
+    "upr_t_bn_bwd_fused": (_i, [_p, _i, _i, _p, _i, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _i, _i, _i, _i, _p,
+                                _p]),
+    "upr_t_zero_upsample16": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _p]),
     "upr_t_relu_mask": (_i, [_p, _i, _i, _p, _i, _i, _i, _i, _p]),
     "upr_t_copy": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _p]),
     "upr_t_pointwise": (_i, [_p, _p, _p, c_size_t, _i, _p, _p, _f, c_u64, _p]),

@@ -130,6 +130,7 @@ class Act:
         self.coff = coff
         self.fresh = False
         self.t16 = None  # compact fp16 copy written by its producer (autocast conv input), or None
+        self.t16_grad = False  # t16 of a gradient: written by the fused BN backward (BN.bwd), trusted by dgrad
 
     @staticmethod
     def new(B, H, W, C, dev, fresh=True):
@@ -162,6 +163,7 @@ class Act:
         acc = 0 if self.fresh else 1
         self.fresh = False
         self.t16 = None
+        self.t16_grad = False
         return acc
 
 
@@ -263,20 +265,26 @@ class Conv:
             _chk(lib.upr_t_cast_f16(_p(self.wp), _p(self.wp16), w.numel(), st), "cast_w")
             _chk(lib.upr_t_cast_f16(_p(self.wt), _p(self.wt16), w.numel(), st), "cast_w")
 
-    def _mfma16(self, x, B, H, W, C, cs, coff, w16, bias, N, kh, kw, s, p, d, res, relu, out, store=0, x16=None):
+    def _mfma16(self, x, B, H, W, C, cs, coff, w16, bias, N, kh, kw, s, p, d, res, relu, out, store=0, x16=None,
+                keep16=False):
         """fp16 MFMA conv with fp32 in / out (upr_t_conv_mfma16); res: Act or None; x16: the
         input's compact fp16 copy when its producer already wrote it."""
         Ho = (H + 2 * p - d * (kh - 1) - 1) // s + 1
         Wo = (W + 2 * p - d * (kw - 1) - 1) // s + 1
-        dev = x.device
+        dev = out.t.device
         ready = x16 is not None
         if not ready:
             x16 = _h16(B * H * W * C, dev)
         y16 = _h16(B * Ho * Wo * N, dev)
         _chk(L.lib().upr_t_conv_mfma16(_fp(x, 0), B, H, W, C, cs, coff, _p(w16), _p(bias), N, kh, kw, s, p, d,
                                        res.ptr() if res is not None else None, res.cs if res is not None else 0,
-                                       int(relu), _fp(out.t), out.cs, out.coff, store, _p(x16), int(ready), _p(y16),
-                                       _stream()), "conv_mfma16")
+                                       int(relu), _fp(out.t), out.cs, out.coff, store | (2 if keep16 and res is None
+                                                                                         else 0),
+                                       _p(x16), int(ready), _p(y16), _stream()), "conv_mfma16")
+        # forward activations (keep16): without a residual y16 is (half)out exactly, and the next
+        # autocast conv reading out takes it (Act.t16); forward activations are not modified in place
+        whole = out.coff == 0 and out.cs == out.C == (N // 4 if store == 1 else N)
+        out.t16 = y16 if keep16 and res is None and whole else None
         return x16
 
     def fwd(self, x, relu=False, out=None, res=None, x_view=None):
@@ -309,7 +317,7 @@ class Conv:
             whole = x.coff == 0 and x.C == x.cs == self.Cin
             t16 = x.t16 if whole else None
             x16 = self._mfma16(x.t, B, H, W, self.Cin, x.cs, x.coff, self.wp16, self.bias, self.Cout, self.kh,
-                               self.kw, self.s, self.p, self.d, res, relu, out, x16=t16)
+                               self.kw, self.s, self.p, self.d, res, relu, out, x16=t16, keep16=True)
             if whole:
                 x.t16 = x16  # the next autocast conv reading x (EnhancedFAM: three of them) reuses the copy
             self.x16 = None if self.frozen else x16
@@ -370,16 +378,27 @@ class Conv:
             if self.mfma:
                 acc = gx.consume_fresh()
                 src, sH, sW, scs, scoff = gy.t, Ho, Wo, gy.cs, gy.coff
+                # autocast: the fp16 operand comes from gy's producer (gy.t16) or, for
+                # stride 2, straight from an fp16 zero-upsample (no fp32 pass + cast)
+                src16 = gy.t16 if self.amp and gy.t16_grad and gy.coff == 0 and gy.cs == gy.C == self.Cout else None
                 if self.s != 1:
                     assert self.s == 2 and H == 2 * Ho and W == 2 * Wo, "stride-2 dgrad needs even sizes"
-                    z = empty((B, H, W, self.Cout), gy.t.device)
-                    _chk(lib.upr_t_zero_upsample(_fp(gy.t), B, Ho, Wo, self.Cout, gy.cs, gy.coff,
-                                                 _p(z), st), "zero_upsample")
-                    src, sH, sW, scs, scoff = z, H, W, self.Cout, 0
+                    if self.amp and self.Cout % 8 == 0:
+                        src16 = _h16(B * H * W * self.Cout, gy.t.device)
+                        _chk(lib.upr_t_zero_upsample16(_fp(gy.t), B, Ho, Wo, self.Cout, gy.cs, gy.coff, _p(src16),
+                                                       st), "zero_upsample16")
+                        src = None
+                    else:
+                        src16 = None
+                        z = empty((B, H, W, self.Cout), gy.t.device)
+                        _chk(lib.upr_t_zero_upsample(_fp(gy.t), B, Ho, Wo, self.Cout, gy.cs, gy.coff,
+                                                     _p(z), st), "zero_upsample")
+                        src = z
+                    sH, sW, scs, scoff = H, W, self.Cout, 0
                 pad_t = self.d * (self.kh - 1) - self.p
                 if self.amp:
                     self._mfma16(src, B, sH, sW, self.Cout, scs, scoff, self.wt16, None, self.Cin, self.kh, self.kw, 1,
-                                 pad_t, self.d, gx if acc else None, False, gx)
+                                 pad_t, self.d, gx if acc else None, False, gx, x16=src16)
                 else:
                     _chk(lib.upr_t_conv_mfma(_fp(src), B, sH, sW, self.Cout, scs, scoff, _p(self.wt), None, self.Cin,
                                              self.kh, self.kw, 1, pad_t, self.d, gx.ptr() if acc else None,
@@ -428,7 +447,8 @@ class ConvT:
         with _timed("mfma16" if self.amp else "mfma32", "fwd", self.flops(x)):
             if self.amp:
                 Conv._mfma16(self, x.t, x.B, x.H, x.W, self.Cin, x.cs, x.coff, self.wp16, self.b4, 4 * self.Cout, 1, 1,
-                             1, 0, 1, None, False, out, store=1)
+                             1, 0, 1, None, False, out, store=1, x16=x.t16 if x.coff == 0 and x.cs == x.C == self.Cin
+                             else None, keep16=True)
             else:
                 _chk(L.lib().upr_t_conv_mfma(x.ptr(), x.B, x.H, x.W, self.Cin, x.cs, 0, _p(self.wp), _p(self.b4),
                                              4 * self.Cout, 1, 1, 1, 0, 1, None, 0, 0, _fp(out.t), out.cs, 0, 1,
@@ -499,13 +519,35 @@ class BN:
                                   0, int(res_post), int(relu), _fp(out.t), out.cs, out.coff, _p(y16), st), "bn_apply")
         out.t16 = y16
         self.x = x
+        self.out_act = out
         self.batch_stats = bool(m.training)  # the backward follows the statistics this forward used
+        self.relu_only = bool(relu) and res is None  # y = relu(bn(x)): the backward may fold the mask in
         return out
 
-    def bwd(self, g, gx):
-        """g: Act gradient of the BN output (ReLU already masked)."""
+    def bwd(self, g, gx, relu=False):
+        """g: Act gradient of the BN output; relu=True: g is the gradient of
+        relu(bn(x)) (this forward's relu=True, no residual), the ReLU mask is
+        folded into the BN backward (recomputed from x, no separate pass).
+        Under autocast the input gradient also gets its compact fp16 copy
+        (gx.t16) for the input-gradient conv that consumes it."""
         lib, st = L.lib(), _stream()
         m, x = self.m, self.x
+        assert not relu or self.relu_only, "ReLU fold needs a relu(bn(x)) forward"
+        if g.coff % 4 == 0 and gx.coff % 4 == 0:
+            whole = gx.coff == 0 and gx.cs == self.C
+            dx16 = _h16(gx.M * self.C, gx.t.device) if _AMP[0] and whole else None
+            acc = 0 if gx.fresh else 1
+            rc = lib.upr_t_bn_bwd_fused(_fp(g.t), g.cs, g.coff, x.ptr(), x.cs, _p(self.mean), _p(self.invstd),
+                                        _p(m.weight), _p(m.bias), int(relu), x.M, self.C, _p(self.acc),
+                                        _p(m.weight.grad), _p(m.bias.grad), _fp(gx.t), gx.cs, gx.coff, acc,
+                                        int(self.batch_stats), _p(dx16), st)
+            if rc != L.UPR_ERR_UNSUPPORTED:
+                _chk(rc, "bn_bwd_fused")
+                gx.consume_fresh()
+                gx.t16, gx.t16_grad = dx16, dx16 is not None
+                return
+        if relu:
+            relu_mask(g, self.out_act)
         zero(self.acc)
         _chk(lib.upr_t_bn_bwd_reduce(_fp(g.t), g.cs, g.coff, x.ptr(), x.cs, 0, _p(self.mean), _p(self.invstd), x.M,
                                      self.C, _p(self.acc), st), "bn_bwd_reduce")
@@ -516,6 +558,7 @@ class BN:
 
 
 def relu_mask(g, y):
+    g.t16, g.t16_grad = None, False  # masked in place: any fp16 copy is stale
     _chk(L.lib().upr_t_relu_mask(_fp(g.t), g.cs, g.coff, _fp(y.t), y.cs, y.coff, g.M, g.C, _stream()), "relu_mask")
 
 
@@ -567,9 +610,8 @@ class ResBlockT:
             add_into(gx, g)
         g_a1 = Act.new(self.a1.B, self.a1.H, self.a1.W, self.a1.C, g.t.device)
         self.conv2.bwd(self.a1, g_c2, g_a1)
-        relu_mask(g_a1, self.a1)
         g_c1 = Act.new(g_a1.B, g_a1.H, g_a1.W, g_a1.C, g.t.device)
-        self.bn1.bwd(g_a1, g_c1)
+        self.bn1.bwd(g_a1, g_c1, relu=True)
         self.conv1.bwd(self.x, g_c1, gx)
 
 
@@ -597,9 +639,8 @@ class PreActResBlockT:
         dev = g.t.device
         g_a2 = Act.new(self.a2.B, self.a2.H, self.a2.W, self.a2.C, dev)
         self.conv2.bwd(self.a2, g, g_a2)
-        relu_mask(g_a2, self.a2)
         g_c1 = Act.new(g_a2.B, g_a2.H, g_a2.W, g_a2.C, dev)
-        self.bn2.bwd(g_a2, g_c1)
+        self.bn2.bwd(g_a2, g_c1, relu=True)
         g_o = Act.new(self.o.B, self.o.H, self.o.W, self.o.C, dev)
         self.conv1.bwd(self.o, g_c1, g_o)
         if self.proj:
@@ -608,8 +649,7 @@ class PreActResBlockT:
             self.sconv.bwd(self.o, g_cs, g_o)
         else:
             add_into(gx, g)
-        relu_mask(g_o, self.o)
-        self.bn1.bwd(g_o, gx)
+        self.bn1.bwd(g_o, gx, relu=True)
 
 
 class ASPPT:
@@ -670,9 +710,8 @@ class ASPPT:
             g_a.fresh = False
         else:
             add_into(g_a, g)
-        relu_mask(g_a, self.a)
         g_cf = Act.new(g.B, g.H, g.W, C, dev)
-        self.fb.bwd(g_a, g_cf)
+        self.fb.bwd(g_a, g_cf, relu=True)
         g_cat = Act.new(g.B, g.H, g.W, C * nb, dev)
         self.fc.bwd(self.cat, g_cf, g_cat)
         # global branch
@@ -687,9 +726,8 @@ class ASPPT:
         # conv branches (the first one initialises gx)
         for i, (cv, bn) in enumerate([(self.c1, self.b1)] + self.br):
             gs = g_cat.slice(C * i, C)
-            relu_mask(gs, self.cat.slice(C * i, C))
             g_c = Act.new(g.B, g.H, g.W, C, dev)
-            bn.bwd(gs, g_c)
+            bn.bwd(gs, g_c, relu=True)
             cv.bwd(x, g_c, gx)
         acc = gx.consume_fresh()
         _chk(L.lib().upr_t_broadcast(_fp(g_gm.t), x.B, x.H * x.W, x.C, ctypes.c_float(1.0 / (x.H * x.W)), gx.ptr(),
@@ -723,14 +761,12 @@ class UpBlockT:
         dev = g.t.device
         if g_skip is not None:
             add_into(g_skip, g)
-        relu_mask(g, self.a2)
         g_c2 = Act.new(g.B, g.H, g.W, g.C, dev)
-        self.b2.bwd(g, g_c2)
+        self.b2.bwd(g, g_c2, relu=True)
         g_a1 = Act.new(g.B, g.H, g.W, g.C, dev)
         self.c2.bwd(self.a1, g_c2, g_a1)
-        relu_mask(g_a1, self.a1)
         g_c1 = Act.new(g.B, g.H, g.W, g.C, dev)
-        self.b1.bwd(g_a1, g_c1)
+        self.b1.bwd(g_a1, g_c1, relu=True)
         g_u = Act.new(g.B, g.H, g.W, g.C, dev)
         self.c1.bwd(self.u, g_c1, g_u)
         self.up.bwd(self.x, g_u, gx)
