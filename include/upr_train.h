@@ -73,11 +73,12 @@ int upr_t_conv_mfma(const float* x, int B, int H, int W, int Cin, int x_cs, int 
  * indexed like upr_t_conv_mfma's: res == y accumulates).  res and relu are
  * exclusive.  store | 2: y16 must afterwards hold (half)y exactly (no res):
  * the next autocast conv reading y can take it as its x16 (x16_ready); without
- * that bit y16 is scratch. */
+ * that bit y16 is scratch.  y16_cs: y16's channel stride (0 = compact: N, or
+ * N / 4 for store 1), e.g. a channel slice of a concat's fp16 copy. */
 int upr_t_conv_mfma16(const float* x, int B, int H, int W, int Cin, int x_cs, int x_coff, const void* wp16,
                       const float* bias, int N, int kh, int kw, int stride, int pad, int dil, const float* res,
                       int res_cs, int relu, float* y, int y_cs, int y_coff, int store, void* x16, int x16_ready,
-                      void* y16, void* stream);
+                      void* y16, int y16_cs, void* stream);
 /* y[i] = (fp16) x[i], n elements. */
 int upr_t_cast_f16(const float* x, void* y, size_t n, void* stream);
 /* Weight gradient of an NHWC conv as an MFMA GEMM over pixels:
@@ -109,7 +110,8 @@ int upr_t_zero_upsample(const float* dy, int B, int Ho, int Wo, int C, int dy_cs
                         void* stream);
 
 /* ---- BatchNorm2d, training mode (nn.BatchNorm2d, model.py:106-162,196-229) -- */
-/* acc[2C] (fp64, zeroed by the caller) += (sum x, sum x^2) per channel of x[M][cs]. */
+/* acc[2C] = (sum x, sum x^2) per channel of x[M][cs] (acc: upr_t_reduce_acc_doubles(C)
+ * doubles; the atomic fallback for C % 4 / unaligned rows adds to a zeroed acc). */
 int upr_t_bn_stats(const float* x, int M, int C, int cs, int coff, double* acc, void* stream);
 /* batch mean / 1/sqrt(var_biased + eps); running stats updated with the
  * unbiased variance and momentum; *nbt += 1 (num_batches_tracked). */
@@ -128,7 +130,9 @@ int upr_t_bn_apply(const float* x, int M, int C, int x_cs, int x_coff, const flo
 int upr_t_bn_apply16(const float* x, int M, int C, int x_cs, int x_coff, const float* mean, const float* invstd,
                      const float* gamma, const float* beta, const float* res, int res_cs, int res_coff, int res_post,
                      int relu, float* y, int y_cs, int y_coff, void* y16, void* stream);
-/* acc[2C] (zeroed) += (sum g, sum g*xhat) per channel. */
+/* acc[2C] = (sum g, sum g*xhat) per channel (acc: upr_t_reduce_acc_doubles(C)
+ * doubles; zeroed beforehand when C % 4 or the rows' alignment forces the
+ * atomic single-stage form, which adds). */
 int upr_t_bn_bwd_reduce(const float* g, int g_cs, int g_coff, const float* x, int x_cs, int x_coff, const float* mean,
                         const float* invstd, int M, int C, double* acc, void* stream);
 /* batch_stats 1 (train-mode BN): dx = gamma*invstd*(g - sum_g/M - xhat*sum_gx/M); batch_stats 0 (an eval-mode
@@ -153,6 +157,15 @@ int upr_t_bn_bwd_fused(const float* g, int g_cs, int g_coff, const float* x, int
  * fp16: the autocast stride-2 input-gradient conv's operand); C % 8 == 0. */
 int upr_t_zero_upsample16(const float* dy, int B, int Ho, int Wo, int C, int dy_cs, int dy_coff, void* z16,
                           void* stream);
+/* Doubles of `acc` that upr_t_bn_stats / upr_t_bn_bwd_reduce / upr_t_bn_bwd_fused
+ * need (and of `ws` for upr_t_chan_sum_ws): acc[0, 2C) receives the per-channel
+ * sums, the rest holds the per-block partial sums of the two-stage reduction
+ * (deterministic: slots added in a fixed order). */
+int upr_t_reduce_acc_doubles(int C);
+/* upr_t_chan_sum through the two-stage reduction (ws: upr_t_reduce_acc_doubles(C)
+ * doubles of scratch). */
+int upr_t_chan_sum_ws(const float* g, int M, int C, int cs, int coff, float* out, int accumulate, double* ws,
+                      void* stream);
 /* out[C] (+)= per-channel sum of g[M][cs] (conv bias gradients). */
 int upr_t_chan_sum(const float* g, int M, int C, int cs, int coff, float* out, int accumulate, void* stream);
 

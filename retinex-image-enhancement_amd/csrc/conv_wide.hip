@@ -38,6 +38,7 @@
 // register staging and stay on conv.hip / conv_halo.hip), C % 64 == 0.
 #include <cstdlib>
 #include <cstring>
+#include <utility>
 
 #include "upr_common.h"
 
@@ -132,7 +133,7 @@ struct SegCursor {
 // before the accumulators are parked -- one batch of independent loads
 // instead of one exposed HBM round trip per 16-byte store (a residual cost
 // the bottleneck / dec3 convs 10-25% of their time)
-template <int BN, int WM, int WN, int WAVES_M, int BM = WBM, bool RPF = false>
+template <int BN, int WM, int WN, int WAVES_M, int BM = WBM, bool RPF = false, int QW = 0>
 __device__ __forceinline__ void wide_epilogue(const ConvOp& op, f32x4_w (&acc)[WM][WN], unsigned char* smem, int m0,
                                               int n0, int M, int HW) {
   const int tid = threadIdx.x;
@@ -194,14 +195,36 @@ __device__ __forceinline__ void wide_epilogue(const ConvOp& op, f32x4_w (&acc)[W
   __syncthreads();  // every wave is done with the last stage
 #pragma unroll
   for (int p = 0; p < BM / 64; ++p) {
-    if (wm == p / PPW) {
+    if constexpr (QW == 0) {
+      if (wm == p / PPW) {
 #pragma unroll
-      for (int a = 0; a < APP; ++a)
+        for (int a = 0; a < APP; ++a)
 #pragma unroll
-        for (int b = 0; b < WN; ++b)
+          for (int b = 0; b < WN; ++b)
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-            Es[(a * 16 + fg * 4 + i) * EST + wn * WN * 16 + b * 16 + fr] = acc[(p % PPW) * APP + a][b][i];
+            for (int i = 0; i < 4; ++i)
+              Es[(a * 16 + fg * 4 + i) * EST + wn * WN * 16 + b * 16 + fr] = acc[(p % PPW) * APP + a][b][i];
+      }
+    } else {
+      // column-block wave mapping (conv_hwide4_kernel): wave wm owns columns
+      // [CW*wm, CW*wm + CW) of every image row of the tile, fragment a = image
+      // row a / FPR, columns CW*wm + (a % FPR)*16 ..; pass p = tile pixels
+      // [64p, 64p + 64) = image row 64p / QW, columns from (64p) % QW
+      constexpr int CW = QW / WAVES_M;
+      constexpr int FPR = CW / 16;
+      const int rr = (p * 64) / QW, cb = (p * 64) % QW;
+#pragma unroll
+      for (int a = 0; a < WM; ++a) {
+        if (a / FPR != rr) continue;
+        const int col = CW * wm + (a % FPR) * 16 - cb;
+        if (col >= 0 && col < 64) {
+#pragma unroll
+          for (int b = 0; b < WN; ++b)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              Es[(col + fg * 4 + i) * EST + wn * WN * 16 + b * 16 + fr] = acc[a][b][i];
+        }
+      }
     }
     __syncthreads();
 #pragma unroll
@@ -984,6 +1007,258 @@ static int launch_hwide3(const ConvOp& op, hipStream_t st) {
   return launch_hwide3_s<BN, W, 0>(op, st);
 }
 
+// ---------------------------------------------------------------------------
+// conv_hwide4_kernel: conv_hwide3's ring / three-B-stage algorithm with every
+// step's control decided at COMPILE time.  hwide3 walks (chunk, tap) with
+// runtime cursors, so its main loop carried ~170 SALU + ~88 VALU per 64 MFMAs
+// (branches on the tap for the region-row DMA and the counted waits, ring-row
+// arithmetic, the halo swizzle looked up from a 64-bit table per read, edge
+// masks selected on runtime taps).  Here:
+// * the Cin / 64 chunks x 9 taps are a template-unrolled sequence: ring rows,
+//   B stages, DMA schedule and vmcnt counts are constants, every LDS fragment
+//   read is a per-lane base register + an immediate offset;
+// * waves own COLUMN blocks (32 columns of all 4 tile rows) instead of row
+//   pairs, so a fragment's ring row depends on (chunk, tap, fragment) only --
+//   not on the wave -- and stays static (the epilogue parks accumulators with
+//   the matching mapping, wide_epilogue QW);
+// * the A / B fragment lane offsets (swizzle included) for the 3 tap columns x
+//   2 half-steps are computed once per block.
+// Same arithmetic as hwide3: identical operands, MFMA order and epilogue.
+// ---------------------------------------------------------------------------
+template <typename F, int... S>
+__device__ __forceinline__ void static_steps(F&& f, std::integer_sequence<int, S...>) {
+  (f(std::integral_constant<int, S>{}), ...);
+}
+
+// zero source of the out-of-image halo rows: a lane reads at its lane offset
+// (< 8 pixels x 1024 channels x 2 B), so a 16 KiB zero block
+__device__ __attribute__((aligned(256))) uint4 g_halo_zero[1024];
+
+template <int BN, int W, int NCH>
+__global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
+  using HC = Halo3Cfg<BN, W>;
+  constexpr int WM = HC::WM, WN = HC::WN, BM = HC::BM, NBS = HC::NBS;
+  constexpr int TOTAL = NCH * 9;
+  constexpr int CW = W / HC::WAVES_M;  // columns per wave
+  constexpr int FPR = CW / 16;         // fragments per tile row per wave
+  static_assert(CW % 16 == 0 && WM == HC::TR * FPR, "column blocks of whole 16-pixel fragments");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  // wave-uniform values live in SGPRs: every DMA address below is a uniform
+  // 64-bit base (scalar arithmetic per step) + a per-lane 32-bit offset fixed
+  // for the block, so the unrolled steps keep no per-step address registers
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % HC::WAVES_M;
+  const int wn = wave / HC::WAVES_M;
+
+  const int HW = op.Ho * W;
+  const int M = op.B * HW;
+  const int mtiles = M / BM;
+  const int ntiles = op.N / BN;
+  const int L = wide_xcd_remap(blockIdx.x, mtiles * ntiles);
+  const int ntile = L % ntiles;
+  const int mtile = L / ntiles;
+  const int m0 = mtile * BM;
+  const int n0 = ntile * BN;
+  const int img = m0 / HW;
+  const int oy0 = (m0 - img * HW) / W;
+  const ConvSeg& sg = op.seg[0];
+  const int cs = sg.cs, H = op.Ho;
+  constexpr int Cin = NCH * WBK;
+
+  // region row r of chunk cc: RP 1-KiB pieces per wave, wave w's piece k =
+  // pixels (w + 8k) * 8 .. +7 of the row; lane = (pixel, 16-byte chunk)
+  const int rpx = wave * 8 + (lane >> 3);
+  const unsigned voff_a = (unsigned)(((lane >> 3) * cs + (((lane & 7) ^ halo_swz(rpx)) * 8)) * 2);
+  const unsigned char* abase =
+      (const unsigned char*)((const half_t*)sg.src + sg.coff + ((size_t)img * HW + (size_t)wave * 8) * cs);
+  const size_t row_bytes = (size_t)W * cs * 2;
+  auto region_row = [&](int cc, int r) {  // cc, r compile-time at every call site
+    const int iy = oy0 - 1 + r;
+    const bool in = (unsigned)iy < (unsigned)H;
+    unsigned char* dst = smem + ((6 * cc + r) & 7) * HC::ROW + wave * 1024;
+#pragma unroll
+    for (int k = 0; k < HC::RP; ++k) {
+      const unsigned char* ub = in ? abase + (size_t)iy * row_bytes + (size_t)k * 64 * cs * 2 + cc * WBK * 2
+                                   : (const unsigned char*)g_halo_zero;
+      glds16(ub + voff_a, dst + k * 8192);
+    }
+  };
+  // region rows issued right before the reads of step (c, t): this chunk's
+  // rows 4 / 5 at t 0 / 1, the next chunk's rows 0, 2, 1, 3 at t 2, 3, 4, 6
+  constexpr auto rows_at = [](int c, int t) -> int {
+    if (t < 2) return 1;
+    return (t <= 4 || t == 6) && c + 1 < NCH ? 1 : 0;
+  };
+  auto issue_rows = [&](int c, int t) {
+    if (t < 2) region_row(c, 4 + t);
+    else if (c + 1 < NCH) {
+      if (t == 2) region_row(c + 1, 0);
+      else if (t == 3) region_row(c + 1, 2);
+      else if (t == 4) region_row(c + 1, 1);
+      else if (t == 6) region_row(c + 1, 3);
+    }
+  };
+
+  const int q8 = lane >> 3;
+  const int qc = lane & 7;
+  const int sw_lane = lane >> 4;
+  // B row n0 + wave*BN/8 + j*8 + q8, chunk qc ^ ((4j + sw_lane) & 7): the lane
+  // offset depends on j's parity only
+  const unsigned voff_b[2] = {(unsigned)((q8 * op.Kpad + ((qc ^ (sw_lane & 7)) * 8)) * 2),
+                              (unsigned)((q8 * op.Kpad + ((qc ^ ((4 + sw_lane) & 7)) * 8)) * 2)};
+  const unsigned char* bbase =
+      (const unsigned char*)((const half_t*)op.W + (size_t)(n0 + wave * (BN / 8)) * op.Kpad + sg.kbase);
+  // B of step (c, t) into stage stg; steps past the end re-read the last
+  // step's rows into a stage nobody reads again (uniform DMA count)
+  auto issue_b = [&](int stg, int c, int t) {
+    unsigned char* Bs = smem + HC::RING + stg * HC::B_BYTES;
+    const int kb = t * Cin + c * WBK;
+#pragma unroll
+    for (int j = 0; j < HC::BJ; ++j)
+      glds16(bbase + ((size_t)j * 8 * op.Kpad + kb) * 2 + voff_b[j & 1], Bs + (wave * (BN / 8) + j * 8) * 128);
+  };
+
+  f32x4_w acc[WM][WN];
+#pragma unroll
+  for (int a = 0; a < WM; ++a)
+#pragma unroll
+    for (int b = 0; b < WN; ++b) acc[a][b] = f32x4_w{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15;
+  const int fg = lane >> 4;
+  const int rsw = (fr >> 1) & 7;
+  // per-lane fragment offsets of half 0: A for tap column tx, B; half 1 is the
+  // same with chunk bit 2 flipped (XOR 64: the swizzles act on the chunk index).
+  // Edge lanes (a tap column outside the image row; ring rows have no padding
+  // columns) of a row's first / last fragment read through a base far beyond
+  // the block's LDS allocation: out-of-range LDS reads return zero, so no
+  // per-fragment select is needed (aofs_e[0] for tx 0, aofs_e[1] for tx 2).
+  constexpr int kLdsVoid = 1 << 30;
+  int aofs[3], aofs_e[2], bofs;
+#pragma unroll
+  for (int tx = 0; tx < 3; ++tx) {
+    const int p = CW * wm + fr + tx - 1;
+    aofs[tx] = p * 128 + ((fg ^ halo_swz(p)) * 16);
+  }
+  aofs_e[0] = (wm == 0 && fr == 0) ? kLdsVoid : aofs[0];
+  aofs_e[1] = (wm == HC::WAVES_M - 1 && fr == 15) ? kLdsVoid : aofs[2];
+  bofs = HC::RING + (wn * WN * 16 + fr) * 128 + ((fg ^ rsw) * 16);
+
+  // fragments of step S, half KK
+  auto rd = [&](auto S_, auto KK_, f16x8_w (&af)[WM], f16x8_w (&bf)[WN]) {
+    constexpr int S = decltype(S_)::value, KK = decltype(KK_)::value;
+    constexpr int c = S / 9, t = S % 9, ty = t / 3, tx = t % 3, stg = S % NBS;
+    const int bo = KK ? (bofs ^ 64) : bofs, ao = KK ? (aofs[tx] ^ 64) : aofs[tx];
+    int aoe = ao;
+    if constexpr (tx == 0) aoe = KK ? (aofs_e[0] ^ 64) : aofs_e[0];
+    if constexpr (tx == 2) aoe = KK ? (aofs_e[1] ^ 64) : aofs_e[1];
+#pragma unroll
+    for (int b = 0; b < WN; ++b)
+      bf[b] = *(const f16x8_w*)(smem + bo + stg * HC::B_BYTES + b * 16 * 128);
+#pragma unroll
+    for (int a = 0; a < WM; ++a) {
+      const int rr = (6 * c + ty + a / FPR) & 7;  // compile-time
+      const bool edge = (tx == 0 && a % FPR == 0) || (tx == 2 && a % FPR == FPR - 1);
+      af[a] = *(const f16x8_w*)(smem + (edge ? aoe : ao) + rr * HC::ROW + (a % FPR) * 16 * 128);
+    }
+  };
+  auto mm = [&](auto S_, f16x8_w (&af)[WM], const f16x8_w (&bf)[WN]) {
+#pragma unroll
+    for (int a = 0; a < WM; ++a) {
+#pragma unroll
+      for (int b = 0; b < WN; ++b)
+        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a], bf[b], acc[a][b], 0, 0, 0);
+    }
+  };
+  // hipcc's own MFMA / fragment-read schedule: the sched_group_barrier
+  // interleave of hwide3 made the straight-line steps spill (118 VGPRs)
+  f16x8_w a0[WM], b0[WN], a1[WM], b1[WN];
+  region_row(0, 0);
+  region_row(0, 1);
+  region_row(0, 2);
+  region_row(0, 3);
+  issue_b(0, 0, 0);
+  if constexpr (NBS == 3) {
+    issue_b(1, 0, 1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(HC::BJ) : "memory");  // rows 0-3 and B(0) landed
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  issue_b(NBS - 1, (NBS - 1) / 9, (NBS - 1) % 9);  // B(NBS - 1)
+  issue_rows(0, 0);
+  rd(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, a0, b0);
+  static_steps(
+      [&](auto S_) {
+        constexpr int S = decltype(S_)::value;
+        if constexpr (S + 1 < TOTAL) {
+          constexpr int c = S / 9, t = S % 9;
+          constexpr int n = S + 1, nc = n / 9, nt = n % 9;
+          // B DMA of step S + NBS (clamped past the end) into the stage step S read
+          constexpr int bstep = S + NBS;
+          constexpr int bc = bstep / 9 < NCH ? bstep / 9 : NCH - 1;
+          constexpr int bt = bstep / 9 < NCH ? bstep % 9 : 8;
+          rd(S_, std::integral_constant<int, 1>{}, a1, b1);
+          mm(S_, a0, b0);
+          // RAW: B(S + 1) and the region rows step S + 1 reads have landed: in
+          // flight may stay the previous iteration's region rows (issued two
+          // steps ahead of their first reader) and, with three stages, its
+          // B(S + 2).  WAR: own fragment reads of step S retired.
+          constexpr int VB = NBS == 3 ? HC::BJ : 0;
+          if constexpr (rows_at(c, t))
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(VB + HC::RP) : "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(VB) : "memory");
+          __builtin_amdgcn_s_barrier();
+          issue_b(S % NBS, bc, bt);
+          issue_rows(nc, nt);
+          rd(std::integral_constant<int, n>{}, std::integral_constant<int, 0>{}, a0, b0);
+          mm(S_, a1, b1);
+        } else {
+          rd(S_, std::integral_constant<int, 1>{}, a1, b1);
+          mm(S_, a0, b0);
+          mm(S_, a1, b1);
+        }
+      },
+      std::make_integer_sequence<int, TOTAL>{});
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave is done with the ring and stages before the epilogue reuses LDS
+
+  wide_epilogue<BN, WM, WN, HC::WAVES_M, BM, true, W>(op, acc, smem, m0, n0, M, HW);
+}
+
+template <int BN, int W, int NCH>
+static int launch_hwide4(const ConvOp& op, hipStream_t st) {
+  using HC = Halo3Cfg<BN, W>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    const hipError_t e = hipFuncSetAttribute((const void*)conv_hwide4_kernel<BN, W, NCH>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, HC::LDS);
+    if (e != hipSuccess) return (int)e;
+    attr_set = true;
+  }
+  const int grid = (op.B * op.Ho * W / HC::BM) * (op.N / BN);
+  hipLaunchKernelGGL((conv_hwide4_kernel<BN, W, NCH>), dim3(grid), dim3(512), HC::LDS, st, op);
+  return (int)hipGetLastError();
+}
+
+// UPR_HW4=0 keeps the runtime-cursor hwide3 kernel (A/B timing)
+template <int BN, int W>
+static int launch_hwide34(const ConvOp& op, hipStream_t st) {
+  static const int v = env_int("UPR_HW4", 0);
+  const int nch = op.seg[0].C / WBK;
+  if (v && op.seg[0].kbase == 0) {
+    // the graph's shapes: bottleneck (W 64, Cin 256), dec3 (W 128, Cin 128)
+    // (W 128 / 2 chunks still spills 40 VGPRs as a straight line: dec3 stays on hwide3)
+    if constexpr (W == 64) {
+      if (nch == 4) return launch_hwide4<BN, W, 4>(op, st);
+    }
+  }
+  return launch_hwide3<BN, W>(op, st);
+}
+
 // UPR_WIDE_HALO=0 routes these convs to the gathered-A kernel, =1 to the
 // two-stage halo kernel (A/B timing); default: the ring / three-stage form
 // for W 64 x N 256, two-stage halo for W 64 x N 128, gathered for W 128
@@ -993,10 +1268,10 @@ static int halo_route(const ConvOp& op, hipStream_t st) {
   const ConvSeg& s = op.seg[0];
   if (s.kh != 3 || s.kw != 3 || s.stride != 1 || s.pad != 1 || s.dil != 1 || s.pre != kPreNone) return kErrUnsupported;
   if (s.Hin != op.Ho || s.Win != op.Wo || s.C % WBK || (op.Ho * op.Wo) % WBM) return kErrUnsupported;
-  if (op.Wo == 64 && op.N % 256 == 0) return mode == 1 ? launch_hwide<256, 64>(op, st) : launch_hwide3<256, 64>(op, st);
+  if (op.Wo == 64 && op.N % 256 == 0) return mode == 1 ? launch_hwide<256, 64>(op, st) : launch_hwide34<256, 64>(op, st);
   if (op.Wo == 64) return launch_hwide<128, 64>(op, st);
   if (op.Wo == 128 && mode == 1) return launch_hwide<128, 128>(op, st);
-  if (op.Wo == 128 && mode == 2 && (op.Ho * op.Wo) % 512 == 0) return launch_hwide3<128, 128>(op, st);
+  if (op.Wo == 128 && mode == 2 && (op.Ho * op.Wo) % 512 == 0) return launch_hwide34<128, 128>(op, st);
   return kErrUnsupported;
 }
 

@@ -558,6 +558,137 @@ static bool reduce4_ok(int C, int cs, int coff, const void* p) {
   return !off && C % 4 == 0 && C <= 1024 && cs % 4 == 0 && coff % 4 == 0 && ((uintptr_t)p & 15) == 0;
 }
 
+// Two-stage per-channel reductions (the float4 path): kRedSlots blocks of 1024
+// threads each write their per-channel partial sums to a slot of their own
+// (plain stores), then one small kernel adds the slots in slot order.  The
+// single-stage form ended every block with 2C same-address fp64 atomics, which
+// serialised at the L2 (1.2-1.8 TB/s on the training shapes); this one is also
+// deterministic run to run.  Modes as chan_reduce4_kernel (0: x, x^2; 1: g,
+// g*xhat; 2: g; 3: mode 1 with the consumer ReLU folded in).
+constexpr int kRedSlots = 256;
+constexpr int kRedThreads = 1024;
+
+__global__ __launch_bounds__(kRedThreads) void chan_part_kernel(const float* __restrict__ a, int a_cs, int a_coff,
+                                                                const float* __restrict__ x, int x_cs, int x_coff,
+                                                                const float* __restrict__ mean,
+                                                                const float* __restrict__ invstd,
+                                                                const float* __restrict__ gamma,
+                                                                const float* __restrict__ beta, int M, int C, int mode,
+                                                                double* __restrict__ part) {
+  extern __shared__ double red_sm[];  // [R][2C]: R * C = 4096
+  const int C4 = C >> 2;
+  const int R = kRedThreads / C4;
+  const int q = threadIdx.x % C4, rg = threadIdx.x / C4;
+  const int rows_per_block = (M + gridDim.x - 1) / gridDim.x;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(M, r0 + rows_per_block);
+  const bool gx = mode == 1 || mode == 3;
+  double u[4] = {0.0, 0.0, 0.0, 0.0}, v[4] = {0.0, 0.0, 0.0, 0.0};
+  if (rg < R) {
+    float mu[4] = {0.f, 0.f, 0.f, 0.f}, is[4] = {0.f, 0.f, 0.f, 0.f}, ga[4] = {0.f, 0.f, 0.f, 0.f},
+          be[4] = {0.f, 0.f, 0.f, 0.f};
+    if (gx) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { mu[e] = mean[4 * q + e]; is[e] = invstd[4 * q + e]; }
+    }
+    if (mode == 3) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { ga[e] = gamma[4 * q + e]; be[e] = beta[4 * q + e]; }
+    }
+    const float* ap = a + a_coff + 4 * q;
+    const float* xp = x ? x + x_coff + 4 * q : nullptr;
+    auto row = [&](const float4 av, const float4 xv) {
+      float ae[4] = {av.x, av.y, av.z, av.w};
+      const float xe[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (gx) {
+          if (mode == 3 && !(bn_affine(xe[e], mu[e], is[e], ga[e], be[e]) > 0.f)) ae[e] = 0.f;
+          u[e] += ae[e];
+          v[e] += (double)ae[e] * ((xe[e] - mu[e]) * is[e]);
+        } else if (mode == 0) {
+          u[e] += ae[e];
+          v[e] += (double)ae[e] * ae[e];
+        } else {
+          u[e] += ae[e];
+        }
+      }
+    };
+    int r = r0 + rg;
+    for (; r + 3 * R < r1; r += 4 * R) {
+      float4 av[4], xv[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) av[k] = *(const float4*)(ap + (size_t)(r + k * R) * a_cs);
+      if (gx) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) xv[k] = *(const float4*)(xp + (size_t)(r + k * R) * x_cs);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) row(av[k], gx ? xv[k] : av[k]);
+    }
+    for (; r < r1; r += R)
+      row(*(const float4*)(ap + (size_t)r * a_cs), gx ? *(const float4*)(xp + (size_t)r * x_cs) : make_float4(0.f, 0.f, 0.f, 0.f));
+  }
+  if (rg < R) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      red_sm[rg * 2 * C + 4 * q + e] = u[e];
+      red_sm[rg * 2 * C + C + 4 * q + e] = v[e];
+    }
+  }
+  __syncthreads();
+  double* dst = part + (size_t)blockIdx.x * 2 * C;
+  for (int t = threadIdx.x; t < 2 * C; t += kRedThreads) {
+    double s = 0.0;
+    for (int k = 0; k < R; ++k) s += red_sm[k * 2 * C + t];
+    dst[t] = s;
+  }
+}
+
+// slot sums -> acc[2C] (modes 0/1/3, overwritten) or out[C] (+)= (mode 2), in
+// a fixed order: a block owns 64 outputs (one per lane), wave w adds slots
+// w, w + 4, ... with four independent partial sums (loads in flight instead
+// of one dependent load per slot), then the 4 x 4 partials are added in order
+__global__ __launch_bounds__(256) void chan_fin_kernel(const double* __restrict__ part, int slots, int C, int mode,
+                                                       double* __restrict__ acc, float* __restrict__ out,
+                                                       int accumulate) {
+  __shared__ double red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int t = blockIdx.x * 64 + lane;
+  const bool ok = t < 2 * C && !(mode == 2 && t >= C);
+  double s[4] = {0.0, 0.0, 0.0, 0.0};
+  if (ok) {
+    int k = w;
+    for (; k + 12 < slots; k += 16) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s[u] += part[(size_t)(k + 4 * u) * 2 * C + t];
+    }
+    for (int u = 0; k < slots; k += 4, ++u) s[u & 3] += part[(size_t)k * 2 * C + t];
+  }
+  red[w][lane] = (s[0] + s[1]) + (s[2] + s[3]);
+  __syncthreads();
+  if (w == 0 && ok) {
+    const double v = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    if (mode == 2) out[t] = (accumulate ? out[t] : 0.f) + (float)v;
+    else acc[t] = v;
+  }
+}
+
+static int chan_reduce2(const float* a, int a_cs, int a_coff, const float* x, int x_cs, int x_coff, const float* mean,
+                        const float* invstd, const float* gamma, const float* beta, int M, int C, int mode,
+                        double* part, double* acc, float* out, int accumulate, hipStream_t st) {
+  const int R = kRedThreads / (C / 4);
+  int slots = M / (R * 16);
+  slots = slots < 1 ? 1 : (slots > kRedSlots ? kRedSlots : slots);
+  hipLaunchKernelGGL(chan_part_kernel, dim3(slots), dim3(kRedThreads), (size_t)R * 2 * C * sizeof(double), st, a, a_cs,
+                     a_coff, x, x_cs, x_coff, mean, invstd, gamma, beta, M, C, mode, part);
+  UPR_CHECK_HIP(hipGetLastError());
+  hipLaunchKernelGGL(chan_fin_kernel, dim3((2 * C + 63) / 64), dim3(256), 0, st, part, slots, C, mode, acc, out,
+                     accumulate);
+  return (int)hipGetLastError();
+}
+
+
 
 
 __global__ void bn_finalize_kernel(const double* __restrict__ acc, int M, int C, float momentum, float eps,
@@ -1832,13 +1963,14 @@ __global__ __launch_bounds__(256) void cast_act_f16_kernel(const float* __restri
 }
 // dense fp16 [m][C] -> y[m][coff + c] (fp32) (+ res[m * res_cs + c], fp32; res may alias y)
 __global__ __launch_bounds__(256) void cast_act_f32_kernel(const half_t* __restrict__ x, long long M, int C,
-                                                           const float* res, int res_cs, float* y, int cs, int coff) {
+                                                           const float* res, int res_cs, float* y, int cs, int coff,
+                                                           int xcs) {
   const int C4 = C / 4;
   GSTRIDE(i, M * C4) {
     const long long m = i / C4;
     const int c = (int)(i - m * C4) * 4;
     typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-    const h4 v = *(const h4*)(x + m * C + c);
+    const h4 v = *(const h4*)(x + m * xcs + c);
     float4 o = make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
     if (res) {
       const float4 r = *(const float4*)(res + m * res_cs + c);
@@ -1871,11 +2003,13 @@ static bool out32_on() {
 int upr_t_conv_mfma16(const float* x, int B, int H, int W, int Cin, int x_cs, int x_coff, const void* wp16,
                       const float* bias, int N, int kh, int kw, int stride, int pad, int dil, const float* res,
                       int res_cs, int relu, float* y, int y_cs, int y_coff, int store, void* x16, int x16_ready,
-                      void* y16, void* stream) {
+                      void* y16, int y16_cs, void* stream) {
   if (!x16 || !wp16 || !y || !y16 || B <= 0 || Cin % 32 || N % 32 || Cin <= 0 || N <= 0) return UPR_ERR_ARG;
   if (!x16_ready && !x) return UPR_ERR_ARG;
   const bool want16 = (store & 2) != 0;  // y16 must end up holding (half)y
   store &= 1;
+  const int ycs16 = y16_cs > 0 ? y16_cs : (store == 1 ? N / 4 : N);  // y16's channel stride
+  if (ycs16 % 8 || ((uintptr_t)y16 & 15)) return UPR_ERR_ARG;
   if (kh <= 0 || kw <= 0 || stride <= 0 || dil <= 0 || pad < 0) return UPR_ERR_ARG;
   if (x_cs % 4 || x_coff % 4 || y_cs % 4 || y_coff % 4 || (res && res_cs % 4)) return UPR_ERR_ARG;
   if (res && relu) return UPR_ERR_ARG;  // the residual is added in fp32 after the fp16 GEMM
@@ -1905,20 +2039,20 @@ int upr_t_conv_mfma16(const float* x, int B, int H, int W, int Cin, int x_cs, in
     ConvOp c32 = c;
     c32.out32 = y; c32.out32_cs = y_cs; c32.out32_coff = y_coff;
     c32.res32 = res; c32.res32_cs = res_cs;
-    if (want16) { c32.out32_h16 = y16; c32.out32_h16_cs = store == 1 ? N / 4 : N; }
+    if (want16) { c32.out32_h16 = y16; c32.out32_h16_cs = ycs16; }
     const int rc = launch_conv_out32(c32, st);
     if (rc != kErrUnsupported) {
       if (rc != 0) return rc;
       LAUNCH_CHECK();
     }
   }
-  c.out = y16; c.out_cs = store == 1 ? N / 4 : N; c.out_coff = 0;
+  c.out = y16; c.out_cs = ycs16; c.out_coff = 0;
   const int rc = launch_conv(c, kF16, st);
   if (rc != 0) return rc;
   const long long Mo = store == 1 ? (long long)B * 4 * Ho * Wo : (long long)B * Ho * Wo;
   const int Co = store == 1 ? N / 4 : N;
   hipLaunchKernelGGL(cast_act_f32_kernel, dim3(grid_for(Mo * (Co / 4))), dim3(256), 0, st, (const half_t*)y16, Mo, Co,
-                     res, res_cs, y, y_cs, y_coff);
+                     res, res_cs, y, y_cs, y_coff, ycs16);
   LAUNCH_CHECK();
 }
 
@@ -1995,8 +2129,8 @@ int upr_t_zero_upsample(const float* dy, int B, int Ho, int Wo, int C, int dy_cs
 int upr_t_bn_stats(const float* x, int M, int C, int cs, int coff, double* acc, void* stream) {
   if (!x || !acc || M <= 0 || C <= 0) return UPR_ERR_ARG;
   if (reduce4_ok(C, cs, coff, x))
-    hipLaunchKernelGGL(chan_reduce4_kernel, dim3(reduce_grid(M)), dim3(256), 0, ST(stream), x, cs, coff, nullptr, 0,
-                       0, nullptr, nullptr, M, C, 0, acc, nullptr);
+    return chan_reduce2(x, cs, coff, nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr, M, C, 0, acc + 2 * C, acc,
+                        nullptr, 0, ST(stream));
   else
     hipLaunchKernelGGL(chan_reduce_kernel, dim3(reduce_grid(M)), dim3(256), 0, ST(stream), x, cs, coff, nullptr, 0, 0,
                        nullptr, nullptr, M, C, 0, acc, nullptr);
@@ -2050,10 +2184,9 @@ int upr_t_bn_apply(const float* x, int M, int C, int x_cs, int x_coff, const flo
 int upr_t_bn_bwd_reduce(const float* g, int g_cs, int g_coff, const float* x, int x_cs, int x_coff, const float* mean,
                         const float* invstd, int M, int C, double* acc, void* stream) {
   if (!g || !x || !acc) return UPR_ERR_ARG;
-  if (reduce4_ok(C, g_cs, g_coff, g) && reduce4_ok(C, x_cs, x_coff, x) && ((uintptr_t)mean & 15) == 0 &&
-      ((uintptr_t)invstd & 15) == 0)
-    hipLaunchKernelGGL(chan_reduce4_kernel, dim3(reduce_grid(M)), dim3(256), 0, ST(stream), g, g_cs, g_coff, x,
-                       x_cs, x_coff, mean, invstd, M, C, 1, acc, nullptr);
+  if (reduce4_ok(C, g_cs, g_coff, g) && reduce4_ok(C, x_cs, x_coff, x))
+    return chan_reduce2(g, g_cs, g_coff, x, x_cs, x_coff, mean, invstd, nullptr, nullptr, M, C, 1, acc + 2 * C, acc,
+                        nullptr, 0, ST(stream));
   else
     hipLaunchKernelGGL(chan_reduce_kernel, dim3(reduce_grid(M)), dim3(256), 0, ST(stream), g, g_cs, g_coff, x, x_cs,
                        x_coff, mean, invstd, M, C, 1, acc, nullptr);
@@ -2091,10 +2224,9 @@ int upr_t_bn_bwd_fused(const float* g, int g_cs, int g_coff, const float* x, int
       !a16(dx) || !a16(mean) || !a16(invstd) || !a16(gamma) || !a16(beta) || ((uintptr_t)dx16 & 7))
     return UPR_ERR_UNSUPPORTED;
   hipStream_t st = ST(stream);
-  UPR_CHECK_HIP(hipMemsetAsync(acc, 0, sizeof(double) * 2 * C, st));
-  hipLaunchKernelGGL(chan_reduce4_kernel, dim3(reduce_grid(M)), dim3(256), 0, st, g, g_cs, g_coff, x, x_cs, 0, mean,
-                     invstd, M, C, relu ? 3 : 1, acc, nullptr, gamma, beta);
-  UPR_CHECK_HIP(hipGetLastError());
+  const int rc = chan_reduce2(g, g_cs, g_coff, x, x_cs, 0, mean, invstd, gamma, beta, M, C, relu ? 3 : 1, acc + 2 * C,
+                              acc, nullptr, 0, st);
+  if (rc) return rc;
   const long long n4 = (long long)M * (C / 4);
   hipLaunchKernelGGL(bn_bwd_apply4_kernel, dim3(grid_for(n4)), dim3(256), 0, st, g, g_cs, g_coff, x, x_cs, 0, mean,
                      invstd, gamma, acc, M, C, dgamma, dbeta, dx, dx_cs, dx_coff, accumulate, batch_stats, beta, relu,
@@ -2124,6 +2256,16 @@ int upr_t_chan_sum(const float* g, int M, int C, int cs, int coff, float* out, i
                      nullptr, nullptr, M, C, 2, nullptr, out);
   LAUNCH_CHECK();
 }
+
+int upr_t_chan_sum_ws(const float* g, int M, int C, int cs, int coff, float* out, int accumulate, double* ws,
+                      void* stream) {
+  if (!g || !out || !ws || M <= 0 || C <= 0) return UPR_ERR_ARG;
+  if (!reduce4_ok(C, cs, coff, g)) return upr_t_chan_sum(g, M, C, cs, coff, out, accumulate, stream);
+  return chan_reduce2(g, cs, coff, nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr, M, C, 2, ws, nullptr, out,
+                      accumulate, ST(stream));
+}
+
+int upr_t_reduce_acc_doubles(int C) { return 2 * C * (1 + kRedSlots); }
 
 int upr_t_relu_mask(float* g, int g_cs, int g_coff, const float* y, int y_cs, int y_coff, int M, int C,
                     void* stream) {

@@ -112,7 +112,7 @@ SIGNATURES.update({
     "upr_t_conv_mfma": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _p, _i, _i, _i, _i, _i, _i, _p, _i, _i, _p, _i, _i,
                              _i, _p]),
     "upr_t_conv_mfma16": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _p, _i, _i, _i, _i, _i, _i, _p, _i, _i, _p, _i, _i,
-                               _i, _p, _i, _p, _p]),
+                               _i, _p, _i, _p, _i, _p]),
     "upr_t_cast_f16": (_i, [_p, _p, c_size_t, _p]),
     "upr_t_conv_wgrad": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p]),
     "upr_t_conv_wgrad16": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p]),
@@ -127,6 +127,8 @@ SIGNATURES.update({
     "upr_t_bn_bwd_reduce": (_i, [_p, _i, _i, _p, _i, _i, _p, _p, _i, _i, _p, _p]),
     "upr_t_bn_bwd_apply": (_i, [_p, _i, _i, _p, _i, _i, _p, _p, _p, _p, _i, _i, _p, _p, _p, _i, _i, _i, _i, _p]),
     "upr_t_chan_sum": (_i, [_p, _i, _i, _i, _i, _p, _i, _p]),
+    "upr_t_chan_sum_ws": (_i, [_p, _i, _i, _i, _i, _p, _i, _p, _p]),
+    "upr_t_reduce_acc_doubles": (_i, [_i]),
     "upr_t_bn_bwd_fused": (_i, [_p, _i, _i, _p, _i, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _i, _i, _i, _i, _p,
                                 _p]),
     "upr_t_zero_upsample16": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _p]),

@@ -266,29 +266,40 @@ class Conv:
             _chk(lib.upr_t_cast_f16(_p(self.wt), _p(self.wt16), w.numel(), st), "cast_w")
 
     def _mfma16(self, x, B, H, W, C, cs, coff, w16, bias, N, kh, kw, s, p, d, res, relu, out, store=0, x16=None,
-                keep16=False):
+                keep16=False, out16=None):
         """fp16 MFMA conv with fp32 in / out (upr_t_conv_mfma16); res: Act or None; x16: the
-        input's compact fp16 copy when its producer already wrote it."""
+        input's compact fp16 copy when its producer already wrote it; out16 = (fp16 tensor, channel
+        offset, channel stride): where the (half)out copy goes when `out` is a channel slice of a
+        concat whose fp16 copy the caller assembles (keep16)."""
         Ho = (H + 2 * p - d * (kh - 1) - 1) // s + 1
         Wo = (W + 2 * p - d * (kw - 1) - 1) // s + 1
         dev = out.t.device
         ready = x16 is not None
         if not ready:
             x16 = _h16(B * H * W * C, dev)
-        y16 = _h16(B * Ho * Wo * N, dev)
+        if out16 is not None:
+            t16, c16, cs16 = out16
+            y16p, y16cs = ctypes.c_void_p(t16.data_ptr() + 2 * c16), cs16
+        else:
+            y16 = _h16(B * Ho * Wo * N, dev)
+            y16p, y16cs = _p(y16), 0
         _chk(L.lib().upr_t_conv_mfma16(_fp(x, 0), B, H, W, C, cs, coff, _p(w16), _p(bias), N, kh, kw, s, p, d,
                                        res.ptr() if res is not None else None, res.cs if res is not None else 0,
                                        int(relu), _fp(out.t), out.cs, out.coff, store | (2 if keep16 and res is None
                                                                                          else 0),
-                                       _p(x16), int(ready), _p(y16), _stream()), "conv_mfma16")
+                                       _p(x16), int(ready), y16p, y16cs, _stream()), "conv_mfma16")
+        if out16 is not None:
+            out.t16 = None
+            return x16
         # forward activations (keep16): without a residual y16 is (half)out exactly, and the next
         # autocast conv reading out takes it (Act.t16); forward activations are not modified in place
         whole = out.coff == 0 and out.cs == out.C == (N // 4 if store == 1 else N)
         out.t16 = y16 if keep16 and res is None and whole else None
         return x16
 
-    def fwd(self, x, relu=False, out=None, res=None, x_view=None):
-        """x: Act (or x_view: (UprView, B, H, W) for an NCHW network input)."""
+    def fwd(self, x, relu=False, out=None, res=None, x_view=None, out16=None):
+        """x: Act (or x_view: (UprView, B, H, W) for an NCHW network input); out16: see _mfma16
+        (autocast MFMA convs only; False is returned when the copy was not written)."""
         lib, st = L.lib(), _stream()
         if x_view is not None:
             xv, B, H, W = x_view
@@ -302,13 +313,14 @@ class Conv:
         self.amp = _AMP[0] and self.mfma and x_view is None
         kind = "mfma16" if self.amp else ("mfma32" if self.mfma and x_view is None else "direct")
         with _timed(kind, "fwd", self.flops(B, Ho, Wo)):
-            self._fwd(x, B, H, W, Ho, Wo, relu, out, res, x_view)
+            self._fwd(x, B, H, W, Ho, Wo, relu, out, res, x_view, out16 if self.amp else None)
+        self.wrote16 = self.amp and out16 is not None and res is None
         return out
 
     def flops(self, B, Ho, Wo):
         return 2.0 * B * Ho * Wo * self.Cout * self.Cin * self.kh * self.kw
 
-    def _fwd(self, x, B, H, W, Ho, Wo, relu, out, res, x_view):
+    def _fwd(self, x, B, H, W, Ho, Wo, relu, out, res, x_view, out16=None):
         lib, st = L.lib(), _stream()
         if x_view is not None:
             xv = x_view[0]
@@ -317,7 +329,7 @@ class Conv:
             whole = x.coff == 0 and x.C == x.cs == self.Cin
             t16 = x.t16 if whole else None
             x16 = self._mfma16(x.t, B, H, W, self.Cin, x.cs, x.coff, self.wp16, self.bias, self.Cout, self.kh,
-                               self.kw, self.s, self.p, self.d, res, relu, out, x16=t16, keep16=True)
+                               self.kw, self.s, self.p, self.d, res, relu, out, x16=t16, keep16=True, out16=out16)
             if whole:
                 x.t16 = x16  # the next autocast conv reading x (EnhancedFAM: three of them) reuses the copy
             self.x16 = None if self.frozen else x16
@@ -365,7 +377,7 @@ class Conv:
                     _chk(lib.upr_t_unpack_grad(_p(self.gp), _p(gw), self.Cout, self.Cin, self.kh, self.kw, 0, 1, st),
                          "unpack")
                     if self.bias is not None:
-                        _chk(lib.upr_t_chan_sum(gy.ptr(), gy.M, self.Cout, gy.cs, 0, _p(self.bias.grad), 1, st), "dbias")
+                        chan_sum(gy, self.Cout, self.bias.grad, st)
                 else:
                     v = x.view() if x_view is None else xv
                     _chk(lib.upr_t_conv_direct_wgrad(ctypes.byref(v), ctypes.byref(gy.view()), B, H, W, self.Cin, Ho, Wo,
@@ -473,7 +485,7 @@ class ConvT:
                                           x.cs, 0, 2, 2, 2, 0, 1, _p(self.gp), st), "convT_wgrad")
             _chk(lib.upr_t_unpack_grad(_p(self.gp), _p(self.m.weight.grad), self.Cout, self.Cin, 2, 2, 3, 1, st),
                  "unpack")
-            _chk(lib.upr_t_chan_sum(gy.ptr(), gy.M, self.Cout, gy.cs, 0, _p(self.m.bias.grad), 1, st), "dbias")
+            chan_sum(gy, self.Cout, self.m.bias.grad, st)
         with _timed(kind, "dgrad", F):
             acc = gx.consume_fresh()
             if self.amp:
@@ -496,13 +508,14 @@ class BN:
         dev = m.weight.device
         self.mean = empty((self.C,), dev)
         self.invstd = empty((self.C,), dev)
-        self.acc = torch.empty((2 * self.C,), dtype=torch.float64, device=dev)
+        # per-channel sums + the two-stage reduction's partial slots (upr_t_reduce_acc_doubles)
+        self.acc = torch.empty((L.lib().upr_t_reduce_acc_doubles(self.C),), dtype=torch.float64, device=dev)
 
     def fwd(self, x, relu=False, out=None, res=None, res_post=False):
         lib, st = L.lib(), _stream()
         m = self.m
         if m.training:
-            zero(self.acc)
+            zero(self.acc[:2 * self.C])  # only the atomic fallback adds into acc
             _chk(lib.upr_t_bn_stats(x.ptr(), x.M, self.C, x.cs, 0, _p(self.acc), st), "bn_stats")
             _chk(lib.upr_t_bn_finalize(_p(self.acc), x.M, self.C, ctypes.c_float(m.momentum), ctypes.c_float(m.eps),
                                        _p(m.running_mean), _p(m.running_var), _p(m.num_batches_tracked),
@@ -548,13 +561,19 @@ class BN:
                 return
         if relu:
             relu_mask(g, self.out_act)
-        zero(self.acc)
+        zero(self.acc[:2 * self.C])
         _chk(lib.upr_t_bn_bwd_reduce(_fp(g.t), g.cs, g.coff, x.ptr(), x.cs, 0, _p(self.mean), _p(self.invstd), x.M,
                                      self.C, _p(self.acc), st), "bn_bwd_reduce")
         acc = gx.consume_fresh()
         _chk(lib.upr_t_bn_bwd_apply(_fp(g.t), g.cs, g.coff, x.ptr(), x.cs, 0, _p(self.mean), _p(self.invstd),
                                     _p(m.weight), _p(self.acc), x.M, self.C, _p(m.weight.grad), _p(m.bias.grad),
                                     _fp(gx.t), gx.cs, gx.coff, acc, int(self.batch_stats), st), "bn_bwd_apply")
+
+
+def chan_sum(g, C, out, st):
+    """out[C] += per-channel sum of the Act g (conv bias gradients; two-stage, deterministic)."""
+    ws = torch.empty((L.lib().upr_t_reduce_acc_doubles(C),), dtype=torch.float64, device=g.t.device)
+    _chk(L.lib().upr_t_chan_sum_ws(g.ptr(), g.M, C, g.cs, 0, _p(out), 1, _p(ws), st), "dbias")
 
 
 def relu_mask(g, y):
@@ -796,15 +815,23 @@ class FAMT:
         self.x = x
         cat = Act.new(B, H, W, 4 * C, dev, fresh=False)
         self.cat = cat
-        self.b1.fwd(x, out=cat.slice(0, C))
+        # under autocast the four branch convs also write the concat's fp16 copy (the fusion conv's operand)
+        cat16 = _h16(B * H * W * 4 * C, dev) if _AMP[0] else None
+        o16 = (lambda k: (cat16, k * C, 4 * C)) if cat16 is not None else (lambda k: None)
+        self.b1.fwd(x, out=cat.slice(0, C), out16=o16(0))
+        ok16 = self.b1.wrote16
         self.mp = Act.new(B, H, W, x.C, dev, fresh=False)
         _chk(lib.upr_t_maxpool(ctypes.byref(x.view()), B, H, W, x.C, 3, 1, 1, ctypes.byref(self.mp.view()), H, W, st),
              "maxpool")
-        self.b2.fwd(self.mp, out=cat.slice(C, C))
+        self.b2.fwd(self.mp, out=cat.slice(C, C), out16=o16(1))
+        ok16 = ok16 and self.b2.wrote16
         self.t3 = self.b3a.fwd(x, relu=True)
-        self.b3b.fwd(self.t3, out=cat.slice(2 * C, C))
+        self.b3b.fwd(self.t3, out=cat.slice(2 * C, C), out16=o16(2))
+        ok16 = ok16 and self.b3b.wrote16
         self.t4 = self.b4a.fwd(x, relu=True)
-        self.b4b.fwd(self.t4, out=cat.slice(3 * C, C))
+        self.b4b.fwd(self.t4, out=cat.slice(3 * C, C), out16=o16(3))
+        ok16 = ok16 and self.b4b.wrote16
+        cat.t16 = cat16 if ok16 else None
         self.o = self.fu.fwd(cat, relu=True)
         self.pool = Act.new(B, 1, 1, C, dev, fresh=False)
         _chk(lib.upr_t_pixel_sum(_fp(self.o.t), B, HW, C, C, 0, ctypes.c_float(1.0 / HW), _fp(self.pool.t), 0, st),

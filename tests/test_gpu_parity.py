@@ -79,6 +79,9 @@ CONV_CASES = [
     # halo-tiled A operand of the wide kernel (fp16; 3x3 s1 d1, W 64 / 128, tiles of whole rows):
     # BN 256 x W 64 over 4 chunks (region double buffer), BN 128 x W 64, BN 128 x W 128, one chunk
     (2, 64, 64, 256, 256, 3, 1, 1, 1, True, True),
+    # statically unrolled halo kernel (hwide4: bottleneck 64x64x256 -> 256): several images, ReLU only
+    (3, 64, 64, 256, 256, 3, 1, 1, 1, True, False),
+    (1, 64, 64, 256, 512, 3, 1, 1, 1, False, True),
     (1, 32, 64, 128, 128, 3, 1, 1, 1, False, True),
     (2, 16, 128, 128, 128, 3, 1, 1, 1, True, False),
     (1, 8, 64, 64, 256, 3, 1, 1, 1, False, False),
