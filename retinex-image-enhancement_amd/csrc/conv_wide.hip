@@ -1247,7 +1247,7 @@ static int launch_hwide4(const ConvOp& op, hipStream_t st) {
 // UPR_HW4=0 keeps the runtime-cursor hwide3 kernel (A/B timing)
 template <int BN, int W>
 static int launch_hwide34(const ConvOp& op, hipStream_t st) {
-  static const int v = env_int("UPR_HW4", 0);
+  static const int v = env_int("UPR_HW4", 1);
   const int nch = op.seg[0].C / WBK;
   if (v && op.seg[0].kbase == 0) {
     // the graph's shapes: bottleneck (W 64, Cin 256), dec3 (W 128, Cin 128)

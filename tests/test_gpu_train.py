@@ -439,7 +439,12 @@ def test_train_grads_b8_vs_fp64(pre):
     (enc1.bn1.weight 5.0e-3 vs 2.3e-3, dec2.conv.0.weight 3.8e-3 vs 1.6e-3:
     the tensors deepest in the backward pass carry the most accumulated
     rounding); single elements are noisier (dec2.conv.3.weight 1.4e-2 of
-    max|g| vs 1.8e-3 on the CPU, dec3.conv.3.weight 3.1e-2 vs 2.1e-2)."""
+    max|g| vs 1.8e-3 on the CPU, dec3.conv.3.weight 3.1e-2 vs 2.1e-2).
+
+    Plus a FIXED bound, independent of the CPU yardstick: every tensor's
+    rel-L2 <= 1e-2 (worst seen on MI355X 6.4e-3; the fp32 CPU oracle itself
+    reaches 4.0e-3 here, where fp32 rounding flips a loss-term branch), and
+    the median over the model's tensors <= 2e-3."""
     from oracle import net as onet
     from oracle import train as otrain
     from losses.loss import TotalLoss
@@ -472,7 +477,7 @@ def test_train_grads_b8_vs_fp64(pre):
     np.testing.assert_allclose(d["total"], d64["total"], rtol=1e-4)
     dev_params = dict(model.named_parameters())
     gmax = max(v.abs().max().item() for v in g64.values())
-    worst = (0.0, 0.0)
+    worst, l2s = (0.0, 0.0), []
     for n in names:
         ref = g64[n]
         if ref.abs().max().item() < 1e-9 * gmax:
@@ -482,10 +487,12 @@ def test_train_grads_b8_vs_fp64(pre):
         l2, l2c = (dev - ref).norm().item() / rn, (g32[n] - ref).norm().item() / rn
         mx, mxc = (dev - ref).abs().max().item(), (g32[n] - ref).abs().max().item()
         worst = max(worst, (l2, l2c))
+        l2s.append(l2)
         print(f"{n}: rel-L2 dev {l2:.3e} cpu32 {l2c:.3e}; max|d| dev {mx / rm:.3e} cpu32 {mxc / rm:.3e} (of max|g|)")
         assert l2 <= max(4.0 * l2c, 2e-3), f"grad {n}: rel-L2 {l2:.3e} (fp32 CPU {l2c:.3e})"
         assert mx <= max(4.0 * mxc, 2e-2 * rm), f"grad {n}: max|d| {mx:.3e} (fp32 CPU {mxc:.3e})"
-    print(f"pre={pre}: worst (device, fp32 CPU) rel-L2 vs fp64 {worst}")
+    print(f"pre={pre}: worst (device, fp32 CPU) rel-L2 vs fp64 {worst}; median device {np.median(l2s):.3e}")
+    assert max(l2s) <= 1e-2 and float(np.median(l2s)) <= 2e-3
 
 
 def test_train_graph_frozen_bn_and_eval_aspp_vs_oracle():
@@ -716,3 +723,84 @@ def test_train_step_full_size_bs8_512(amp):
     moved = sum(int(not torch.equal(p.detach(), before[n])) for n, p in model.named_parameters())
     assert moved > len(before) // 2
     print(f"bs8 512^2 step (amp={amp}): loss {d8['total']:.6g}, gradient norm before clipping {gn:.4g}")
+
+
+_G512 = {}
+
+
+def _oracle_grads_512(sd_cpu, x, amp):
+    """fp64 oracle gradients of TotalLoss at B=2 512x512 (plain model); amp:
+    with the autocast conv arithmetic emulated (net.amp_conv).  Cached per amp:
+    one oracle pass takes ~40 s on 16 host cores."""
+    from oracle import net as onet
+    from oracle import train as otrain
+    if amp not in _G512:
+        names = otrain.param_names(sd_cpu)
+        s2 = {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in sd_cpu.items()}
+        params = {k: s2[k].clone().requires_grad_(True) for k in names}
+        work = dict(s2)
+        work.update(params)
+        with otrain.train_mode(amp=amp):
+            e_r, r_r, i_r = onet.forward(work, x.double(), False, False)
+            t_r, d_r = otrain.total_loss({k: v.double() for k, v in otrain.vgg19_state(VGG_SEED).items()},
+                                         x.double(), e_r, i_r, r_r)
+        t_r.backward()
+        _G512[amp] = (d_r, {k: params[k].grad for k in names})
+    return _G512[amp]
+
+
+@pytest.mark.parametrize("amp", [False, True])
+def test_train_grads_512_b2_fixed_bound(amp):
+    """configs[4]'s arithmetic at its image size (reference trainers/train.py:63-103,
+    B=2 of the bs8 512x512 step, plain model, TotalLoss with the frequency term):
+    every parameter gradient vs the fp64 oracle under a FIXED bound.
+
+    fp32: per tensor rel-L2 <= 5e-3, median over the model <= 1e-3.
+    autocast fp16 (train.py:72): per tensor rel-L2 <= max(2 x the emulated
+    autocast band, 2 x the band's median, 5e-3), where the band is
+    |g_amp_emulated - g64| / |g64| from the fp64 oracle with fp16-rounded conv
+    operands and outputs (the perturbation fp16 convs cause by themselves)."""
+    from losses.loss import TotalLoss
+    from oracle import train as otrain
+    x = torch.rand(2, 3, 512, 512, generator=torch.Generator().manual_seed(21)) * 0.6
+    model = _model(False, False, seed=7)
+    sd_cpu = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    model = model.to(DEV).train()
+    crit = TotalLoss(use_freq_loss=True).to(DEV)
+    with torch.autocast("cuda", dtype=torch.float16, enabled=amp):
+        enh, refl, illu = model(x.to(DEV))
+        total, d = crit(x.to(DEV), enh, illu, refl)
+    total.backward()
+    torch.cuda.synchronize()
+    if amp:
+        g = model.__dict__["_upr_train"]["graph"]
+        assert all(c.amp for c in g._convs if getattr(c, "mfma", True)), "autocast step did not use the fp16 convs"
+    names = otrain.param_names(sd_cpu)
+    d64, g64 = _oracle_grads_512(sd_cpu, x, False)
+    if amp:
+        d16, g16 = _oracle_grads_512(sd_cpu, x, True)
+        for k in ("total", "exposure", "smoothness", "color", "spatial", "decouple", "perceptual", "frequency"):
+            np.testing.assert_allclose(d[k], d16[k], rtol=1e-3, atol=1e-9, err_msg=k)
+    else:
+        np.testing.assert_allclose(d["total"], d64["total"], rtol=1e-4)
+    dev_params = dict(model.named_parameters())
+    gmax = max(v.abs().max().item() for v in g64.values())
+    rows = []
+    for n in names:
+        ref = g64[n]
+        if ref.abs().max().item() < 1e-9 * gmax:
+            continue  # BN-fed conv bias: zero true gradient
+        rn = ref.norm().item()
+        l2 = (dev_params[n].grad.double().cpu() - ref).norm().item() / rn
+        band = (g16[n] - ref).norm().item() / rn if amp else 0.0
+        rows.append((n, l2, band))
+    med = float(np.median([r[1] for r in rows]))
+    bmed = float(np.median([r[2] for r in rows]))
+    for n, l2, band in rows:
+        print(f"{n}: rel-L2 vs fp64 {l2:.3e}" + (f" (emulated autocast band {band:.3e})" if amp else ""))
+    print(f"512^2 B=2 amp={amp}: worst rel-L2 {max(r[1] for r in rows):.3e}, median {med:.3e}")
+    for n, l2, band in rows:
+        tol = max(2.0 * band, 2.0 * bmed, 5e-3) if amp else 5e-3
+        assert l2 <= tol, f"{n}: rel-L2 {l2:.3e} > {tol:.3e}"
+    if not amp:
+        assert med <= 1e-3, med
