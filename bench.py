@@ -188,7 +188,7 @@ def parity_vs_cpu(sd, pre, aspp, x, outs, precision):
 # every kernel launch_conv dispatches to (the bench's conv family = the executor's GEMM ops)
 CONV_KERNELS = ("conv_halo_kernel", "conv_igemm_kernel", "conv_wide_kernel", "conv_wide32_kernel",
                 "conv_stream_kernel", "conv_stream_fam_kernel", "conv_ring_kernel", "conv_ring32_kernel",
-                "conv_hwide_kernel", "conv_hwide3_kernel", "conv_t2_kernel", "conv_t2_f32_kernel")
+                "conv_hwide_kernel", "conv_hwide3_kernel", "conv_hwide4_kernel", "conv_t2_kernel", "conv_t2_f32_kernel")
 
 
 def pmc_traffic(precision, variant, batch, size):
@@ -484,13 +484,13 @@ def train_roofline(recs, step_ms, B, S):
     (BatchNorm, ReLU masks, casts, losses, FFTs, clip + Adam: fp32, memory
     bound) is reported as its time, not against an MFMA peak."""
     by = {}
-    for kind, what, fl, ms in recs:
+    for kind, what, fl, ms, *_ in recs:
         d = by.setdefault(kind, {"ms": 0.0, "gflop": 0.0, "calls": 0})
         d["ms"] += ms
         d["gflop"] += fl / 1e9
         d["calls"] += 1
     by_what = {}
-    for kind, what, fl, ms in recs:
+    for kind, what, fl, ms, *_ in recs:
         d = by_what.setdefault(f"{kind}.{what}", {"ms": 0.0, "gflop": 0.0, "calls": 0})
         d["ms"] += ms
         d["gflop"] += fl / 1e9
@@ -510,6 +510,9 @@ def train_roofline(recs, step_ms, B, S):
             "kernel": f"{main} conv calls of one profiled step (forward, input gradient, weight gradient; each call "
                       f"timed with HIP events around its library call(s), algorithmic flops)",
             "by_arithmetic": by, "by_pass": by_what,
+            "slowest_calls": [{"kind": k, "pass": w, "shape": ("%d->%d k%d s%d %dx%d" % sh) if sh else None,
+                               "ms": round(ms, 4), "TFLOPs": round(fl / 1e9 / ms, 1) if ms > 0 else None}
+                              for k, w, fl, ms, sh in sorted(recs, key=lambda r: -r[3])[:16]],
             "step_ms": step_ms, "conv_ms": conv_ms,
             "non_conv_ms": step_ms - conv_ms,
             "non_conv_note": "BatchNorm stats/apply, ReLU masks, fp32<->fp16 casts, pooling, losses, FFTs, "

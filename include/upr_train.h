@@ -46,6 +46,18 @@ int upr_t_zero(void* p, size_t bytes, void* stream);
 int upr_t_conv_direct(const UprView* x, int B, int H, int W, int Cin, const float* w, const float* bias, int Cout,
                       int kh, int kw, int stride, int pad, int dil, const UprView* y, int Ho, int Wo, int relu,
                       int accumulate, void* stream);
+/* The same forward also writing y16 = (half)y compact [B*Ho*Wo][Cout] (the
+ * next autocast conv's operand): the 3 -> 32 / 64 3x3 kernel only, else
+ * UPR_ERR_UNSUPPORTED (nothing launched). */
+int upr_t_conv_direct16(const UprView* x, int B, int H, int W, int Cin, const float* w, const float* bias, int Cout,
+                        int kh, int kw, int stride, int pad, int dil, const UprView* y, int Ho, int Wo, int relu,
+                        int accumulate, void* y16, void* stream);
+/* Input gradient of a 3 -> Cout (32 / 64) 3x3 / stride 1 / pad 1 conv under
+ * autocast (VGG-19 conv1_1): dy16 = the fp16 output gradient, compact
+ * [B][H][W][Cout]; weights [Cout][3][3][3] fp32, rounded to fp16; fp32
+ * accumulation on MFMA.  dx [B][H][W][3] view (+= when accumulate). */
+int upr_t_conv_dgrad_c3_16(const void* dy16, int B, int H, int W, const float* w, int Cout, const UprView* dx,
+                           int accumulate, void* stream);
 /* d(loss)/d(input) of the same conv (autograd of F.conv2d). */
 int upr_t_conv_direct_dgrad(const UprView* dy, int Ho, int Wo, const float* w, int B, int H, int W, int Cin, int Cout,
                             int kh, int kw, int stride, int pad, int dil, const UprView* dx, int accumulate,
@@ -96,11 +108,31 @@ int upr_t_conv_wgrad(const float* x, int B, int H, int W, int Cin, int x_cs, int
 int upr_t_conv_wgrad16(const float* x, const void* x16, int B, int H, int W, int Cin, int x_cs, int x_coff,
                        const float* dy, int Ho, int Wo, int Cout, int dy_cs, int dy_coff, int kh, int kw, int stride,
                        int pad, int dil, float* dwp, void* stream);
+/* The weight gradient added straight into PyTorch's layout: dw[co][ci][ky][kx]
+ * += (no packed buffer, zero fill or unpack pass).  x16 non-NULL: the AMP
+ * arithmetic of upr_t_conv_wgrad16 (x may then be NULL when the fp16 path
+ * takes the shape); else the fp32 upr_t_conv_wgrad.  dw needs no alignment. */
+int upr_t_conv_wgrad_into(const float* x, const void* x16, int B, int H, int W, int Cin, int x_cs, int x_coff,
+                          const float* dy, int Ho, int Wo, int Cout, int dy_cs, int dy_coff, int kh, int kw,
+                          int stride, int pad, int dil, float* dw, void* stream);
 /* Weight layout transforms.  mode 0: [Co][Ci][kh][kw] -> [Co][(ky,kx,ci)];
  * mode 1: -> [Ci][(ky,kx,co)] spatially flipped (stride-1 dgrad as a conv);
  * mode 2: ConvTranspose [Ci][Co][2][2] -> [(a,b,co)][ci] (forward GEMM);
  * mode 3: ConvTranspose [Ci][Co][2][2] -> [ci][(a,b,co)] (dgrad = k2 s2 conv). */
 int upr_t_pack_weight(const float* w, float* out, int Co, int Ci, int kh, int kw, int mode, void* stream);
+/* Every re-pack of a training step in one launch (the per-conv pack + fp16
+ * cast launches were ~250 per step).  jobs: DEVICE array of njobs entries;
+ * each packs w ([Co][Ci][kh][kw], n = Co*Ci*kh*kw elements) with its mode
+ * (0-3 as upr_t_pack_weight; 4: replicate a bias of Co into out[q*Co + c],
+ * q < 4, n = Co) into out32 (fp32) and / or out16 (fp16, the same value
+ * rounded once), either may be NULL.  max_n: the largest n. */
+typedef struct UprPackJob {
+  const float* w;
+  float* out32;
+  void* out16;
+  int Co, Ci, kh, kw, mode, n;
+} UprPackJob;
+int upr_t_pack_weights(const UprPackJob* jobs, int njobs, int max_n, void* stream);
 /* Inverse of pack modes 0 and 3 for gradients; accumulate != 0 adds. */
 int upr_t_unpack_grad(const float* gp, float* g, int Co, int Ci, int kh, int kw, int mode, int accumulate,
                       void* stream);
@@ -173,6 +205,12 @@ int upr_t_chan_sum(const float* g, int M, int C, int cs, int coff, float* out, i
 /* g[m][c] *= (y[m][c] > 0)  (ReLU backward from the ReLU's output). */
 int upr_t_relu_mask(float* g, int g_cs, int g_coff, const float* y, int y_cs, int y_coff, int M, int C,
                     void* stream);
+/* The same mask also writing g16[m][c] = (half)(masked g), contiguous [M][C]
+ * (the autocast dgrad operand); g is rewritten only when write32.  Needs C,
+ * the strides and offsets multiples of 4 and 16-byte aligned g / y, else
+ * UPR_ERR_UNSUPPORTED. */
+int upr_t_relu_mask16(float* g, int g_cs, int g_coff, const float* y, int y_cs, int y_coff, int M, int C, void* g16,
+                      int write32, void* stream);
 /* dst (+)= src, any layouts (NCHW <-> NHWC, concat slices). */
 int upr_t_copy(const UprView* src, const UprView* dst, int B, int H, int W, int C, int accumulate, void* stream);
 /* n contiguous elements.  op 0: out = sigmoid(a); op 1: out = a*b*(1-b)
@@ -185,12 +223,36 @@ int upr_t_pointwise(const float* a, const float* b, float* out, size_t n, int op
                     uint8_t* mask_out, float p, uint64_t seed, void* stream);
 
 /* ---- pooling / resampling ---------------------------------------------- */
-/* nn.MaxPool2d(k, s, p) forward / backward (backward recomputes the argmax,
- * first maximum in scan order, and scatters with atomics; dx accumulated). */
+/* nn.MaxPool2d(k, s, p) forward / backward (backward recomputes the argmax
+ * codes below, then gathers them deterministically; dx accumulated). */
 int upr_t_maxpool(const UprView* x, int B, int H, int W, int C, int k, int s, int p, const UprView* y, int Ho, int Wo,
                   void* stream);
 int upr_t_maxpool_bwd(const UprView* x, const UprView* dy, int B, int H, int W, int C, int k, int s, int p, int Ho,
                       int Wo, const UprView* dx, void* stream);
+/* The same forward also writing code[b][oy][ox][c] = ky * k + kx of each
+ * window's maximum (PyTorch's rule: the first in-bounds tap, then every tap
+ * with v > max or v NaN; 255 for an empty window; code may be NULL), and the
+ * backward from those codes: dx[b][iy][ix][c] (+)= dy of every window whose
+ * code points at (iy, ix), in ascending (oy, ox) order (deterministic).
+ * code holds B*Ho*Wo*C bytes, 4-byte aligned.  3x3/1/1 and 2x2/2/0 on
+ * channel-contiguous views run 4 channels per thread.  y16 (nullable): also
+ * the compact fp16 copy of y ([B][Ho][Wo][C], the autocast consumer's
+ * operand) -- 4-channel path only, else UPR_ERR_UNSUPPORTED. */
+int upr_t_maxpool_code(const UprView* x, int B, int H, int W, int C, int k, int s, int p, const UprView* y, int Ho,
+                       int Wo, unsigned char* code, void* y16, void* stream);
+int upr_t_maxpool_bwd_code(const unsigned char* code, const UprView* dy, int B, int H, int W, int C, int k, int s,
+                           int p, int Ho, int Wo, const UprView* dx, int accumulate, void* stream);
+/* upr_t_copy / upr_t_bilinear also writing the fp16 copy of the result at
+ * dst16[pixel * dst16_cs + c] (dst16 points at the slice's first channel of
+ * a [B][H][W][dst16_cs] fp16 concat): 4-channel views only, else
+ * UPR_ERR_UNSUPPORTED (nothing launched). */
+int upr_t_copy16(const UprView* src, const UprView* dst, int B, int H, int W, int C, int accumulate, void* dst16,
+                 int dst16_cs, void* stream);
+int upr_t_bilinear16(const UprView* x, int B, int H, int W, int C, const UprView* y, int Ho, int Wo, int accumulate,
+                     void* y16, int y16_cs, void* stream);
+/* out = a + b (n floats) and out16 = (half)out; n % 4 == 0, 16-byte aligned
+ * fp32 / 8-byte aligned fp16, else UPR_ERR_UNSUPPORTED. */
+int upr_t_add16(const float* a, const float* b, float* out, size_t n, void* out16, void* stream);
 /* F.interpolate(mode='bilinear', align_corners=False) H x W -> Ho x Wo
  * (scale = in/out per axis) and its backward (dx accumulated, atomics). */
 int upr_t_bilinear(const UprView* x, int B, int H, int W, int C, const UprView* y, int Ho, int Wo, int accumulate,

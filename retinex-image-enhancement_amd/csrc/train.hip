@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
+#include <mutex>
 
 #include "upr_common.h"
 #include "../../include/upr.h"
@@ -34,6 +35,31 @@ static V mkv(const UprView* u) {
   return v;
 }
 
+// channel-contiguous view with 32-bit strides: the 4-channels-per-thread
+// resampling / copy kernels (the generic V kernels' 64-bit div/mod per element
+// run below 1 TB/s)
+struct V4 {
+  float* d;
+  int sb, sh, sw;
+  __device__ __forceinline__ float* at(int b, int y, int x, int c) const { return d + b * sb + y * sh + x * sw + c; }
+};
+
+// usable as a V4 over [B, H, W, C]: unit channel stride, C and the strides
+// multiples of 4, 16-byte aligned, every offset below 2^31
+static bool vec4_view_ok(const UprView* v, int B, int H, int W, int C) {
+  if (v->sc != 1 || C % 4 || (uintptr_t)v->data % 16 || v->sw % 4 || v->sh % 4 || v->sb % 4) return false;
+  if ((long long)B * H * W * C >= (1LL << 31)) return false;
+  const long long ext = (long long)(B - 1) * v->sb + (long long)(H - 1) * v->sh + (long long)(W - 1) * v->sw + C;
+  return ext < (1LL << 31) && v->sb < (1LL << 31) && v->sh < (1LL << 31) && v->sw < (1LL << 31);
+}
+
+static V4 mkv4(const UprView* u) {
+  V4 v;
+  v.d = (float*)u->data;
+  v.sb = (int)u->sb; v.sh = (int)u->sh; v.sw = (int)u->sw;
+  return v;
+}
+
 static inline int grid_for(long long n, int per = 256, int cap = 65536) {
   long long g = (n + per - 1) / per;
   if (g < 1) g = 1;
@@ -48,17 +74,20 @@ static inline int grid_for(long long n, int per = 256, int cap = 65536) {
 // train_small.hip: pixel-tiled / MFMA forms of the small-channel convs
 int small_conv_fwd(const UprView* xv, int B, int H, int W, int Cin, const float* w, const float* bias, int Cout,
                    int kh, int kw, int stride, int pad, int dil, const UprView* yv, int Ho, int Wo, int relu,
-                   int accumulate, hipStream_t st);
+                   int accumulate, hipStream_t st, void* y16 = nullptr);
 int small_conv_dgrad(const UprView* dyv, int Ho, int Wo, const float* w, int B, int H, int W, int Cin, int Cout,
                      int kh, int kw, int stride, int pad, int dil, const UprView* dxv, int accumulate, hipStream_t st);
+int small_conv_dgrad_c3_16(const void* dy16, int B, int H, int W, const float* w, int Cout, const UprView* dxv,
+                           int accumulate, hipStream_t st);
 int small_conv_wgrad(const UprView* xv, const UprView* dyv, int B, int H, int W, int Cin, int Ho, int Wo, int Cout,
                      int kh, int kw, int stride, int pad, int dil, float* dw, float* dbias, hipStream_t st);
 // train_wgrad.hip: split-K GEMM weight gradient (UPR_WGRAD_GEMM=0: round-1 kernel)
 int wgrad_gemm(const float* x, int B, int H, int W, int Cin, int x_cs, int x_coff, const float* dy, int Ho, int Wo,
                int Cout, int dy_cs, int dy_coff, int kh, int kw, int stride, int pad, int dil, float* dwp,
-               hipStream_t st);
+               hipStream_t st, int torch_ci = 0);
 int wgrad16_gemm(const void* x16, int B, int H, int W, int Cin, const float* dy, int Ho, int Wo, int Cout, int dy_cs,
-                 int dy_coff, int kh, int kw, int stride, int pad, int dil, float* dwp, hipStream_t st);
+                 int dy_coff, int kh, int kw, int stride, int pad, int dil, float* dwp, hipStream_t st,
+                 int torch_ci = 0);
 static bool wgrad_gemm_on() {
   static int on = -1;
   if (on < 0) {
@@ -75,6 +104,50 @@ static bool small_kernels_on() {
     on = (e && atoi(e) == 0) ? 0 : 1;
   }
   return on == 1;
+}
+
+// scratch(): see upr_common.h
+void* scratch(int slot, size_t bytes, hipStream_t st) {
+  struct Entry {
+    int dev;
+    hipStream_t st;
+    void* p[kSlotCount];
+    size_t n[kSlotCount];
+  };
+  static std::mutex mu;
+  static Entry tab[64];
+  static int used = 0;
+  if (slot < 0 || slot >= kSlotCount) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  Entry* e = nullptr;
+  for (int i = 0; i < used; ++i)
+    if (tab[i].dev == dev && tab[i].st == st) e = &tab[i];
+  if (!e) {
+    if (used == 64) return nullptr;
+    e = &tab[used++];
+    memset(e, 0, sizeof(*e));
+    e->dev = dev;
+    e->st = st;
+  }
+  if (bytes == 0) bytes = 16;
+  if (e->n[slot] < bytes) {
+    if (e->p[slot]) {
+      if (hipStreamSynchronize(st) != hipSuccess) return nullptr;  // earlier kernels may still read it
+      (void)hipFree(e->p[slot]);
+      e->p[slot] = nullptr;
+      e->n[slot] = 0;
+    }
+    const size_t grow = bytes + bytes / 4;  // headroom: one growth covers nearby sizes
+    if (hipMalloc(&e->p[slot], grow) != hipSuccess) {
+      (void)hipGetLastError();
+      e->p[slot] = nullptr;
+      return nullptr;
+    }
+    e->n[slot] = grow;
+  }
+  return e->p[slot];
 }
 
 // ---------------------------------------------------------------------------
@@ -356,6 +429,34 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, float* __restric
       if (mode == 2) o[((size_t)q * Co + co) * Ci + ci] = w[i];
       else o[((size_t)ci * 4 + q) * Co + co] = w[i];
     }
+  }
+}
+
+__global__ __launch_bounds__(256) void pack_batch_kernel(const UprPackJob* __restrict__ jobs) {
+  const UprPackJob j = jobs[blockIdx.y];
+  const int taps = j.kh * j.kw;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < j.n; i += gridDim.x * 256) {
+    const float v = j.w[i];
+    if (j.mode == 4) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (j.out32) j.out32[q * j.Co + i] = v;
+        if (j.out16) ((half_t*)j.out16)[q * j.Co + i] = (half_t)v;
+      }
+      continue;
+    }
+    int dst;
+    if (j.mode <= 1) {
+      const int tap = i % taps, r = i / taps;
+      const int ci = r % j.Ci, co = r / j.Ci;
+      dst = j.mode == 0 ? (co * taps + tap) * j.Ci + ci : (ci * taps + (taps - 1 - tap)) * j.Co + co;
+    } else {
+      const int q = i % 4, r = i / 4;
+      const int co = r % j.Co, ci = r / j.Co;
+      dst = j.mode == 2 ? (q * j.Co + co) * j.Ci + ci : (ci * 4 + q) * j.Co + co;
+    }
+    if (j.out32) j.out32[dst] = v;
+    if (j.out16) ((half_t*)j.out16)[dst] = (half_t)v;
   }
 }
 
@@ -874,6 +975,27 @@ __global__ __launch_bounds__(256) void relu_mask4_kernel(float* g, int g_cs, int
   }
 }
 
+// the mask fused with the fp16 copy of the masked gradient (the autocast
+// dgrad operand, trainers/train.py:72): g16[m][c] = half(g masked), g itself
+// rewritten only with write32 (a frozen conv's gradient has no fp32 reader)
+__global__ __launch_bounds__(256) void relu_mask16_kernel(float* g, int g_cs, int g_coff, const float* __restrict__ y,
+                                                          int y_cs, int y_coff, int M, int C4,
+                                                          half_t* __restrict__ g16, int write32) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= M * C4) return;
+  const int c = (i % C4) * 4, m = i / C4;
+  const float4 yv = *(const float4*)(y + (size_t)m * y_cs + y_coff + c);
+  float4* gp = (float4*)(g + (size_t)m * g_cs + g_coff + c);
+  float4 gv = *gp;
+  if (!(yv.x > 0.f)) gv.x = 0.f;
+  if (!(yv.y > 0.f)) gv.y = 0.f;
+  if (!(yv.z > 0.f)) gv.z = 0.f;
+  if (!(yv.w > 0.f)) gv.w = 0.f;
+  if (write32) *gp = gv;
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+  *(h4*)(g16 + (size_t)i * 4) = h4{(half_t)gv.x, (half_t)gv.y, (half_t)gv.z, (half_t)gv.w};
+}
+
 __global__ void relu_mask_kernel(float* g, int g_cs, int g_coff, const float* __restrict__ y, int y_cs, int y_coff,
                                  int M, int C) {
   const long long n = (long long)M * C;
@@ -1073,6 +1195,116 @@ __global__ void bilinear_bwd_gather_kernel(V dy, int B, int H, int W, int C, int
   }
 }
 
+// 4-channel forms (V4 views, one thread per pixel and 4 channels)
+__device__ __forceinline__ void dec4(int i, int CV, int W, int H, int& b, int& y, int& x, int& c) {
+  c = (i % CV) * 4;
+  int r = i / CV;
+  x = r % W;
+  r /= W;
+  y = r % H;
+  b = r / H;
+}
+
+// d16 (nullable): fp16 copy of the result at d16[pixel * cs16 + c] (pixel = (b*H + y)*W + x)
+__device__ __forceinline__ void store16(half_t* d16, int cs16, int pix, int c, float4 v) {
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+  *(h4*)(d16 + (size_t)pix * cs16 + c) = h4{(half_t)v.x, (half_t)v.y, (half_t)v.z, (half_t)v.w};
+}
+
+__global__ __launch_bounds__(256) void copy4_kernel(V4 s, V4 d, int H, int W, int CV, int n, int accum,
+                                                    half_t* __restrict__ d16, int cs16) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  int b, y, x, c;
+  dec4(i, CV, W, H, b, y, x, c);
+  float4 v = *(const float4*)s.at(b, y, x, c);
+  float4* o = (float4*)d.at(b, y, x, c);
+  if (accum) {
+    const float4 u = *o;
+    v = make_float4(u.x + v.x, u.y + v.y, u.z + v.z, u.w + v.w);
+  }
+  *o = v;
+  if (d16) store16(d16, cs16, i / CV, c, v);
+}
+
+__global__ __launch_bounds__(256) void bilinear4_kernel(V4 x, int H, int W, int CV, V4 y, int Ho, int Wo, float sh,
+                                                        float sw, int n, int accum, half_t* __restrict__ y16,
+                                                        int cs16) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  int b, oy, ox, c;
+  dec4(i, CV, Wo, Ho, b, oy, ox, c);
+  int y0, y1, x0, x1;
+  float ly, lx;
+  bilin_src(oy, H, sh, y0, y1, ly);
+  bilin_src(ox, W, sw, x0, x1, lx);
+  const float4 a = *(const float4*)x.at(b, y0, x0, c), bq = *(const float4*)x.at(b, y0, x1, c);
+  const float4 cq = *(const float4*)x.at(b, y1, x0, c), d = *(const float4*)x.at(b, y1, x1, c);
+  // the scalar kernel's expression per channel
+  float4 v;
+  v.x = (1.f - ly) * ((1.f - lx) * a.x + lx * bq.x) + ly * ((1.f - lx) * cq.x + lx * d.x);
+  v.y = (1.f - ly) * ((1.f - lx) * a.y + lx * bq.y) + ly * ((1.f - lx) * cq.y + lx * d.y);
+  v.z = (1.f - ly) * ((1.f - lx) * a.z + lx * bq.z) + ly * ((1.f - lx) * cq.z + lx * d.z);
+  v.w = (1.f - ly) * ((1.f - lx) * a.w + lx * bq.w) + ly * ((1.f - lx) * cq.w + lx * d.w);
+  float4* o = (float4*)y.at(b, oy, ox, c);
+  if (accum) {
+    const float4 u = *o;
+    v = make_float4(u.x + v.x, u.y + v.y, u.z + v.z, u.w + v.w);
+  }
+  *o = v;
+  if (y16) store16(y16, cs16, i / CV, c, v);
+}
+
+// bilinear backward, separable and in the gather kernel's summation order:
+// pass 1 row[b][oy][ix] = sum over ox (ascending, nonzero weights) of
+// wx * dy[b][oy][ox]; pass 2 dx[b][iy][ix] += sum over oy (ascending, nonzero
+// weights) of wy * row[b][oy][ix].  Each pass scans ~3/scale candidates
+// instead of the product of both axes.
+__global__ __launch_bounds__(256) void bilinear_bwd_rows4_kernel(V4 dy, int Ho, int Wo, int W, int CV, float sw,
+                                                                 float* __restrict__ row, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  int b, oy, ix, c;
+  dec4(i, CV, W, Ho, b, oy, ix, c);
+  int xlo, xhi;
+  bilin_range(ix, W, Wo, sw, xlo, xhi);
+  float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int ox = xlo; ox <= xhi; ++ox) {
+    const float wx = bilin_w(ox, ix, W, sw);
+    if (wx == 0.f) continue;
+    const float4 g = *(const float4*)dy.at(b, oy, ox, c);
+    r.x += wx * g.x;
+    r.y += wx * g.y;
+    r.z += wx * g.z;
+    r.w += wx * g.w;
+  }
+  *(float4*)(row + (size_t)i * 4) = r;
+}
+
+__global__ __launch_bounds__(256) void bilinear_bwd_cols4_kernel(const float* __restrict__ row, int Ho, int H, int W,
+                                                                 int CV, float sh, V4 dx, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  int b, iy, ix, c;
+  dec4(i, CV, W, H, b, iy, ix, c);
+  int ylo, yhi;
+  bilin_range(iy, H, Ho, sh, ylo, yhi);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int C = CV * 4;
+  for (int oy = ylo; oy <= yhi; ++oy) {
+    const float wy = bilin_w(oy, iy, H, sh);
+    if (wy == 0.f) continue;
+    const float4 r = *(const float4*)(row + (((size_t)b * Ho + oy) * W + ix) * C + c);
+    acc.x += wy * r.x;
+    acc.y += wy * r.y;
+    acc.z += wy * r.z;
+    acc.w += wy * r.w;
+  }
+  float4* o = (float4*)dx.at(b, iy, ix, c);
+  const float4 u = *o;
+  *o = make_float4(u.x + acc.x, u.y + acc.y, u.z + acc.z, u.w + acc.w);
+}
+
 // per-(image, channel) pixel sums: grid (chunks, B)
 __global__ __launch_bounds__(256) void pixel_sum_kernel(const float* __restrict__ x, int HW, int C, int cs, int coff,
                                                         float scale, float* __restrict__ out) {
@@ -1261,6 +1493,76 @@ __global__ __launch_bounds__(256) void fam_ca_bwd_kernel(const float* __restrict
     for (int k = 0; k < 256; ++k) t += sm[k][threadIdx.x];
     atomicAdd(g_ca + (size_t)b * C + threadIdx.x, t);
   }
+}
+
+// C = 32 form: 8 lanes per pixel (a float4 of channels each, coalesced rows),
+// the channel argmax reduced across the 8 lanes with the scan's rule (first
+// NaN, else first maximum), per-block partial sums of gt * o in a fixed order
+// to part[b][chunk][c] (summed in chunk order by fam_ca_fin_kernel: no atomics)
+__device__ __forceinline__ void argmax_pick(float& v, int& i, float v2, int i2) {
+  const bool second_is_later = i2 > i;
+  const float fv = second_is_later ? v : v2, sv = second_is_later ? v2 : v;
+  const int fi = second_is_later ? i : i2, si = second_is_later ? i2 : i;
+  const bool take_second = sv > fv || (isnan(sv) && !isnan(fv));
+  v = take_second ? sv : fv;
+  i = take_second ? si : fi;
+}
+
+__global__ __launch_bounds__(256) void fam_ca_bwd32_kernel(const float* __restrict__ g_o2,
+                                                           const float* __restrict__ g_m, const float* __restrict__ o,
+                                                           const float* __restrict__ o2, const float* __restrict__ ca,
+                                                           int HW, float* __restrict__ g_o, float* __restrict__ part) {
+  __shared__ float sm[32][33];
+  const int b = blockIdx.y, q = threadIdx.x & 7, pl = threadIdx.x >> 3;
+  const int per = (HW + gridDim.x - 1) / gridDim.x;
+  const int p0 = blockIdx.x * per, p1 = min(HW, p0 + per);
+  const float4 cav = *(const float4*)(ca + (size_t)b * 32 + q * 4);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int p = p0 + pl; p < p1; p += 32) {
+    const size_t i = (size_t)b * HW + p;
+    const float4 v = *(const float4*)(o2 + i * 32 + q * 4);
+    float mv = v.x;
+    int mi = q * 4;
+    argmax_pick(mv, mi, v.y, q * 4 + 1);
+    argmax_pick(mv, mi, v.z, q * 4 + 2);
+    argmax_pick(mv, mi, v.w, q * 4 + 3);
+#pragma unroll
+    for (int off = 1; off < 8; off <<= 1) {
+      const float v2 = __shfl_xor(mv, off);
+      const int i2 = __shfl_xor(mi, off);
+      argmax_pick(mv, mi, v2, i2);
+    }
+    const float gm0 = g_m[i * 2] / 32.f, gm1 = g_m[i * 2 + 1];
+    const float4 gv = *(const float4*)(g_o2 + i * 32 + q * 4);
+    const float4 ov = *(const float4*)(o + i * 32 + q * 4);
+    const int c0 = q * 4;
+    const float t0 = gv.x + gm0 + (mi == c0 ? gm1 : 0.f), t1 = gv.y + gm0 + (mi == c0 + 1 ? gm1 : 0.f);
+    const float t2 = gv.z + gm0 + (mi == c0 + 2 ? gm1 : 0.f), t3 = gv.w + gm0 + (mi == c0 + 3 ? gm1 : 0.f);
+    *(float4*)(g_o + i * 32 + q * 4) = make_float4(t0 * cav.x, t1 * cav.y, t2 * cav.z, t3 * cav.w);
+    acc.x += t0 * ov.x;
+    acc.y += t1 * ov.y;
+    acc.z += t2 * ov.z;
+    acc.w += t3 * ov.w;
+  }
+  sm[pl][q * 4] = acc.x;
+  sm[pl][q * 4 + 1] = acc.y;
+  sm[pl][q * 4 + 2] = acc.z;
+  sm[pl][q * 4 + 3] = acc.w;
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    float t = 0.f;
+    for (int k = 0; k < 32; ++k) t += sm[k][threadIdx.x];
+    part[((size_t)b * gridDim.x + blockIdx.x) * 32 + threadIdx.x] = t;
+  }
+}
+
+__global__ void fam_ca_fin_kernel(const float* __restrict__ part, int chunks, int n, float* __restrict__ g_ca) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;  // j = b * 32 + c
+  if (j >= n) return;
+  const int b = j >> 5, c = j & 31;
+  float t = 0.f;
+  for (int k = 0; k < chunks; ++k) t += part[((size_t)b * chunks + k) * 32 + c];
+  g_ca[j] = t;
 }
 
 __global__ void fam_pool_bwd_kernel(float* g_o, const float* __restrict__ g_pool, const float* __restrict__ o, int B,
@@ -1887,6 +2189,26 @@ int upr_t_conv_direct(const UprView* x, int B, int H, int W, int Cin, const floa
   LAUNCH_CHECK();
 }
 
+int upr_t_conv_dgrad_c3_16(const void* dy16, int B, int H, int W, const float* w, int Cout, const UprView* dx,
+                           int accumulate, void* stream) {
+  if (!dy16 || !w || !dx || !dx->data || B <= 0 || H <= 0 || W <= 0) return UPR_ERR_ARG;
+  const int rc = small_conv_dgrad_c3_16(dy16, B, H, W, w, Cout, dx, accumulate, ST(stream));
+  return rc == kErrUnsupported ? UPR_ERR_UNSUPPORTED : rc;
+}
+
+int upr_t_conv_direct16(const UprView* x, int B, int H, int W, int Cin, const float* w, const float* bias, int Cout,
+                        int kh, int kw, int stride, int pad, int dil, const UprView* y, int Ho, int Wo, int relu,
+                        int accumulate, void* y16, void* stream) {
+  if (!x || !y || !x->data || !y->data || !w || !y16 || B <= 0 || Cin <= 0 || Cout <= 0 || stride <= 0 || dil <= 0)
+    return UPR_ERR_ARG;
+  if (Ho != (H + 2 * pad - dil * (kh - 1) - 1) / stride + 1 || Wo != (W + 2 * pad - dil * (kw - 1) - 1) / stride + 1)
+    return UPR_ERR_SHAPE;
+  if (!small_kernels_on()) return UPR_ERR_UNSUPPORTED;
+  const int rc = small_conv_fwd(x, B, H, W, Cin, w, bias, Cout, kh, kw, stride, pad, dil, y, Ho, Wo, relu, accumulate,
+                                ST(stream), y16);
+  return rc == kErrUnsupported ? UPR_ERR_UNSUPPORTED : rc;
+}
+
 int upr_t_conv_direct_dgrad(const UprView* dy, int Ho, int Wo, const float* w, int B, int H, int W, int Cin, int Cout,
                             int kh, int kw, int stride, int pad, int dil, const UprView* dx, int accumulate,
                             void* stream) {
@@ -2086,13 +2408,13 @@ int upr_t_conv_wgrad16(const float* x, const void* x16, int B, int H, int W, int
     const void* src = x16;
     if (!src) {
       const long long Mi = (long long)B * H * W;
-      UPR_CHECK_HIP(hipMallocAsync(&tmp, (size_t)Mi * Cin * sizeof(half_t), st));
+      tmp = scratch(kSlotCast, (size_t)Mi * Cin * sizeof(half_t), st);
+      if (!tmp) return (int)hipErrorOutOfMemory;
       hipLaunchKernelGGL(cast_act_f16_kernel, dim3(grid_for(Mi * (Cin / 8))), dim3(256), 0, st, x, Mi, Cin, x_cs, x_coff,
                          (half_t*)tmp);
       src = tmp;
     }
     const int rc = wgrad16_gemm(src, B, H, W, Cin, dy, Ho, Wo, Cout, dy_cs, dy_coff, kh, kw, stride, pad, dil, dwp, st);
-    if (tmp) UPR_CHECK_HIP(hipFreeAsync(tmp, st));
     if (rc != kErrUnsupported) return rc;
   }
   if (!x) return UPR_ERR_ARG;
@@ -2100,11 +2422,49 @@ int upr_t_conv_wgrad16(const float* x, const void* x16, int B, int H, int W, int
                           stream);
 }
 
+int upr_t_conv_wgrad_into(const float* x, const void* x16, int B, int H, int W, int Cin, int x_cs, int x_coff,
+                          const float* dy, int Ho, int Wo, int Cout, int dy_cs, int dy_coff, int kh, int kw,
+                          int stride, int pad, int dil, float* dw, void* stream) {
+  if ((!x && !x16) || !dy || !dw || B <= 0 || Cin % 32 || Cout % 32 || Cin <= 0 || Cout <= 0) return UPR_ERR_ARG;
+  hipStream_t st = ST(stream);
+  if (x16) {
+    const int rc = wgrad16_gemm(x16, B, H, W, Cin, dy, Ho, Wo, Cout, dy_cs, dy_coff, kh, kw, stride, pad, dil, dw, st,
+                                Cin);
+    if (rc != kErrUnsupported) return rc;
+  }
+  if (!x) return UPR_ERR_ARG;
+  if (wgrad_gemm_on()) {
+    const int rc = wgrad_gemm(x, B, H, W, Cin, x_cs, x_coff, dy, Ho, Wo, Cout, dy_cs, dy_coff, kh, kw, stride, pad, dil,
+                              dw, st, Cin);
+    if (rc != kErrUnsupported) return rc;
+  }
+  // any other shape: the packed form into scratch, then added in PyTorch's layout
+  const size_t n = (size_t)Cout * Cin * kh * kw;
+  float* tmp = nullptr;
+  tmp = (float*)scratch(kSlotTmp, n * sizeof(float), st);
+  if (!tmp) return (int)hipErrorOutOfMemory;
+  UPR_CHECK_HIP(hipMemsetAsync(tmp, 0, n * sizeof(float), st));
+  int rc = x16 ? upr_t_conv_wgrad16(x, x16, B, H, W, Cin, x_cs, x_coff, dy, Ho, Wo, Cout, dy_cs, dy_coff, kh, kw, stride,
+                                    pad, dil, tmp, stream)
+               : upr_t_conv_wgrad(x, B, H, W, Cin, x_cs, x_coff, dy, Ho, Wo, Cout, dy_cs, dy_coff, kh, kw, stride, pad,
+                                  dil, tmp, stream);
+  if (rc == UPR_OK) rc = upr_t_unpack_grad(tmp, dw, Cout, Cin, kh, kw, 0, 1, stream);
+  return rc;
+}
+
 int upr_t_pack_weight(const float* w, float* out, int Co, int Ci, int kh, int kw, int mode, void* stream) {
   if (!w || !out || Co <= 0 || Ci <= 0 || mode < 0 || mode > 3) return UPR_ERR_ARG;
   if (mode >= 2 && (kh != 2 || kw != 2)) return UPR_ERR_SHAPE;
   const long long n = (long long)Co * Ci * kh * kw;
   hipLaunchKernelGGL(pack_weight_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), w, out, Co, Ci, kh, kw, mode);
+  LAUNCH_CHECK();
+}
+
+int upr_t_pack_weights(const UprPackJob* jobs, int njobs, int max_n, void* stream) {
+  if (!jobs || njobs < 0 || max_n < 0 || njobs > 65535) return UPR_ERR_ARG;
+  if (njobs == 0 || max_n == 0) return UPR_OK;
+  const int gx = (max_n + 255) / 256 < 64 ? (max_n + 255) / 256 : 64;
+  hipLaunchKernelGGL(pack_batch_kernel, dim3(gx, njobs), dim3(256), 0, ST(stream), jobs);
   LAUNCH_CHECK();
 }
 
@@ -2283,9 +2643,29 @@ int upr_t_relu_mask(float* g, int g_cs, int g_coff, const float* y, int y_cs, in
   LAUNCH_CHECK();
 }
 
+int upr_t_relu_mask16(float* g, int g_cs, int g_coff, const float* y, int y_cs, int y_coff, int M, int C, void* g16,
+                      int write32, void* stream) {
+  if (!g || !y || !g16) return UPR_ERR_ARG;
+  if (C % 4 || g_cs % 4 || g_coff % 4 || y_cs % 4 || y_coff % 4 || ((uintptr_t)g & 15) || ((uintptr_t)y & 15) ||
+      ((uintptr_t)g16 & 7) || (long long)M * C >= (1LL << 31))
+    return UPR_ERR_UNSUPPORTED;
+  const int n = M * (C / 4);
+  if (n == 0) return UPR_OK;
+  hipLaunchKernelGGL(relu_mask16_kernel, dim3((n + 255) / 256), dim3(256), 0, ST(stream), g, g_cs, g_coff, y, y_cs,
+                     y_coff, M, C / 4, (half_t*)g16, write32);
+  LAUNCH_CHECK();
+}
+
 int upr_t_copy(const UprView* src, const UprView* dst, int B, int H, int W, int C, int accumulate, void* stream) {
   if (!src || !dst || !src->data || !dst->data) return UPR_ERR_ARG;
   const long long n = (long long)B * H * W * C;
+  if (n == 0) return UPR_OK;
+  if (vec4_view_ok(src, B, H, W, C) && vec4_view_ok(dst, B, H, W, C)) {
+    const int nv = (int)(n / 4);
+    hipLaunchKernelGGL(copy4_kernel, dim3((nv + 255) / 256), dim3(256), 0, ST(stream), mkv4(src), mkv4(dst), H, W,
+                       C / 4, nv, accumulate, (half_t*)nullptr, 0);
+    LAUNCH_CHECK();
+  }
   hipLaunchKernelGGL(copy_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), mkv(src), mkv(dst), B, H, W, C,
                      accumulate);
   LAUNCH_CHECK();
@@ -2304,11 +2684,7 @@ int upr_t_pointwise(const float* a, const float* b, float* out, size_t n, int op
 
 int upr_t_maxpool(const UprView* x, int B, int H, int W, int C, int k, int s, int p, const UprView* y, int Ho, int Wo,
                   void* stream) {
-  if (!x || !y || k <= 0 || s <= 0) return UPR_ERR_ARG;
-  const long long n = (long long)B * Ho * Wo * C;
-  hipLaunchKernelGGL(maxpool_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), mkv(x), B, H, W, C, k, s, p, mkv(y),
-                     Ho, Wo);
-  LAUNCH_CHECK();
+  return upr_t_maxpool_code(x, B, H, W, C, k, s, p, y, Ho, Wo, nullptr, nullptr, stream);
 }
 
 // Max-pool backward as two deterministic passes (the atomic scatter above --
@@ -2408,6 +2784,102 @@ __global__ void maxpool_bwd_gather_kernel(const unsigned char* __restrict__ code
   }
 }
 
+// Fast paths for the two pools of the training step -- EnhancedFAM's 3x3/1/1
+// (models/model.py:32) and the VGG 2x2/2 (losses/loss.py perceptual
+// features[4], [9], [18]) -- on channel-contiguous views: 4 channels per
+// thread, 32-bit index math (the generic kernels' 64-bit div/mod per element
+// ran at <1 TB/s), compile-time windows.  The forward optionally writes the
+// argmax byte codes (PyTorch's rule, as maxpool_arg_kernel) so the backward
+// is the gather alone.
+template <int K, int S, int P>
+__global__ __launch_bounds__(256) void maxpool4_kernel(const float* __restrict__ x, int xsb, int xsh, int xsw, int H,
+                                                       int W, int CV, int Ho, int Wo, int n, float* __restrict__ y,
+                                                       int ysb, int ysh, int ysw, unsigned* __restrict__ code,
+                                                       half_t* __restrict__ y16) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int c = (i % CV) * 4;
+  int r = i / CV;
+  const int ox = r % Wo;
+  r /= Wo;
+  const int oy = r % Ho, b = r / Ho;
+  float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  int best[4] = {-1, -1, -1, -1};
+  const float* xb = x + b * xsb + c;
+#pragma unroll
+  for (int ky = 0; ky < K; ++ky) {
+    const int iy = oy * S - P + ky;
+    if ((unsigned)iy >= (unsigned)H) continue;
+#pragma unroll
+    for (int kx = 0; kx < K; ++kx) {
+      const int ix = ox * S - P + kx;
+      if ((unsigned)ix >= (unsigned)W) continue;
+      const float4 q = *(const float4*)(xb + iy * xsh + ix * xsw);
+      const float val[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        if (best[v] < 0) best[v] = ky * K + kx;
+        if (val[v] > m[v] || isnan(val[v])) {
+          m[v] = val[v];
+          best[v] = ky * K + kx;
+        }
+      }
+    }
+  }
+  *(float4*)(y + b * ysb + oy * ysh + ox * ysw + c) = make_float4(m[0], m[1], m[2], m[3]);
+  if (y16) {  // compact [b][oy][ox][C] fp16 copy: element index 4 i
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    *(h4*)(y16 + (size_t)i * 4) = h4{(half_t)m[0], (half_t)m[1], (half_t)m[2], (half_t)m[3]};
+  }
+  if (code) {
+    unsigned w = 0;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) w |= (unsigned)(best[v] < 0 ? 255 : best[v]) << (8 * v);
+    code[i] = w;
+  }
+}
+
+// dx[b][iy][ix][c..c+3] += dy of every window (ascending oy, then ox: the
+// generic gather's order) whose code points at (iy, ix)
+template <int K, int S, int P>
+__global__ __launch_bounds__(256) void maxpool_gather4_kernel(const unsigned* __restrict__ code,
+                                                              const float* __restrict__ dy, int dsb, int dsh, int dsw,
+                                                              int H, int W, int CV, int Ho, int Wo, int n,
+                                                              float* __restrict__ dx, int xsb, int xsh, int xsw,
+                                                              int accumulate) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int cv = i % CV, c = cv * 4;
+  int r = i / CV;
+  const int ix = r % W;
+  r /= W;
+  const int iy = r % H, b = r / H;
+  float* dp = dx + b * xsb + iy * xsh + ix * xsw + c;
+  float4 acc = accumulate ? *(const float4*)dp : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int t = 0; t < K; ++t) {
+    const int ky = K - 1 - t, ny = iy + P - ky;  // oy * S
+    if (ny < 0 || ny % S != 0 || ny / S >= Ho) continue;
+    const int oy = ny / S;
+#pragma unroll
+    for (int u = 0; u < K; ++u) {
+      const int kx = K - 1 - u, nx = ix + P - kx;
+      if (nx < 0 || nx % S != 0 || nx / S >= Wo) continue;
+      const int ox = nx / S;
+      const unsigned w = code[((b * Ho + oy) * Wo + ox) * CV + cv];
+      const unsigned want = (unsigned)(ky * K + kx) * 0x01010101u;
+      const unsigned hit = w ^ want;  // a zero byte marks a window whose max sits here
+      if (((hit - 0x01010101u) & ~hit & 0x80808080u) == 0) continue;
+      const float4 g = *(const float4*)(dy + b * dsb + oy * dsh + ox * dsw + c);
+      if ((hit & 0xffu) == 0) acc.x += g.x;
+      if ((hit & 0xff00u) == 0) acc.y += g.y;
+      if ((hit & 0xff0000u) == 0) acc.z += g.z;
+      if ((hit & 0xff000000u) == 0) acc.w += g.w;
+    }
+  }
+  *(float4*)dp = acc;
+}
+
 }  // extern "C++"
 
 int upr_t_maxpool_bwd(const UprView* x, const UprView* dy, int B, int H, int W, int C, int k, int s, int p, int Ho,
@@ -2421,7 +2893,8 @@ int upr_t_maxpool_bwd(const UprView* x, const UprView* dy, int B, int H, int W, 
     LAUNCH_CHECK();
   }
   void* code = nullptr;
-  UPR_CHECK_HIP(hipMallocAsync(&code, (size_t)n, st));
+  code = scratch(kSlotCode, (size_t)n, st);
+  if (!code) return (int)hipErrorOutOfMemory;
   const bool v4 = C % 4 == 0 && x->sc == 1 && dx->sc == 1 && (uintptr_t)x->data % 16 == 0 &&
                   (uintptr_t)dx->data % 16 == 0 && x->sw % 4 == 0 && x->sh % 4 == 0 && x->sb % 4 == 0 &&
                   dx->sw % 4 == 0 && dx->sh % 4 == 0 && dx->sb % 4 == 0;
@@ -2438,14 +2911,94 @@ int upr_t_maxpool_bwd(const UprView* x, const UprView* dy, int B, int H, int W, 
                        mkv(dy), B, H, W, C, k, s, p, Ho, Wo, mkv(dx));
   }
   UPR_CHECK_HIP(hipGetLastError());
-  UPR_CHECK_HIP(hipFreeAsync(code, st));
   return UPR_OK;
+}
+
+__global__ void zero_view_kernel(V v, int B, int H, int W, int C) {
+  const long long n = (long long)B * H * W * C;
+  GSTRIDE(i, n) {
+    const int c = (int)(i % C);
+    long long r = i / C;
+    const int x = (int)(r % W);
+    r /= W;
+    v.d[v.at((int)(r / H), (int)(r % H), x, c)] = 0.f;
+  }
+}
+
+// shape of a fast-path pool: (k, s, p) one of the two instantiated windows,
+// channel-contiguous 16-byte aligned views whose extents fit 32-bit offsets
+static int pool_fast_kind(int k, int s, int p) {
+  if (k == 3 && s == 1 && p == 1) return 1;
+  if (k == 2 && s == 2 && p == 0) return 2;
+  return 0;
+}
+
+int upr_t_maxpool_code(const UprView* x, int B, int H, int W, int C, int k, int s, int p, const UprView* y, int Ho,
+                       int Wo, unsigned char* code, void* y16, void* stream) {
+  if (!x || !y || k <= 0 || s <= 0 || k * k > 255) return UPR_ERR_ARG;
+  hipStream_t st = ST(stream);
+  const long long n = (long long)B * Ho * Wo * C;
+  if (n == 0) return UPR_OK;
+  const int kind = pool_fast_kind(k, s, p);
+  if (kind && vec4_view_ok(x, B, H, W, C) && vec4_view_ok(y, B, Ho, Wo, C) && (uintptr_t)code % 4 == 0 &&
+      (uintptr_t)y16 % 8 == 0 && n < (1LL << 31)) {
+    const int nv = (int)(n / 4), CV = C / 4;
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3((nv + 255) / 256), dim3(256), 0, st, (const float*)x->data, (int)x->sb,
+                         (int)x->sh, (int)x->sw, H, W, CV, Ho, Wo, nv, (float*)y->data, (int)y->sb, (int)y->sh,
+                         (int)y->sw, (unsigned*)code, (half_t*)y16);
+    };
+    if (kind == 1) go(maxpool4_kernel<3, 1, 1>);
+    else go(maxpool4_kernel<2, 2, 0>);
+    LAUNCH_CHECK();
+  }
+  if (y16) return UPR_ERR_UNSUPPORTED;  // the fp16 copy comes with the 4-channel path only
+  hipLaunchKernelGGL(maxpool_kernel, dim3(grid_for(n)), dim3(256), 0, st, mkv(x), B, H, W, C, k, s, p, mkv(y), Ho, Wo);
+  if (code)
+    hipLaunchKernelGGL(maxpool_arg_kernel<1>, dim3(grid_for(n)), dim3(256), 0, st, mkv(x), B, H, W, C, k, s, p, Ho,
+                       Wo, code);
+  LAUNCH_CHECK();
+}
+
+int upr_t_maxpool_bwd_code(const unsigned char* code, const UprView* dy, int B, int H, int W, int C, int k, int s,
+                           int p, int Ho, int Wo, const UprView* dx, int accumulate, void* stream) {
+  if (!code || !dy || !dx || k <= 0 || s <= 0 || k * k > 255) return UPR_ERR_ARG;
+  hipStream_t st = ST(stream);
+  const long long ni = (long long)B * H * W * C;
+  if (ni == 0) return UPR_OK;
+  const int kind = pool_fast_kind(k, s, p);
+  if (kind && vec4_view_ok(dy, B, Ho, Wo, C) && vec4_view_ok(dx, B, H, W, C) && (uintptr_t)code % 4 == 0 &&
+      ni < (1LL << 31)) {
+    const int nv = (int)(ni / 4), CV = C / 4;
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3((nv + 255) / 256), dim3(256), 0, st, (const unsigned*)code,
+                         (const float*)dy->data, (int)dy->sb, (int)dy->sh, (int)dy->sw, H, W, CV, Ho, Wo, nv,
+                         (float*)dx->data, (int)dx->sb, (int)dx->sh, (int)dx->sw, accumulate);
+    };
+    if (kind == 1) go(maxpool_gather4_kernel<3, 1, 1>);
+    else go(maxpool_gather4_kernel<2, 2, 0>);
+    LAUNCH_CHECK();
+  }
+  if (!accumulate) {
+    // the generic gather adds into dx: clear the view first
+    hipLaunchKernelGGL(zero_view_kernel, dim3(grid_for(ni)), dim3(256), 0, st, mkv(dx), B, H, W, C);
+  }
+  hipLaunchKernelGGL(maxpool_bwd_gather_kernel<1>, dim3(grid_for(ni)), dim3(256), 0, st, code, mkv(dy), B, H, W, C,
+                     k, s, p, Ho, Wo, mkv(dx));
+  LAUNCH_CHECK();
 }
 
 int upr_t_bilinear(const UprView* x, int B, int H, int W, int C, const UprView* y, int Ho, int Wo, int accumulate,
                    void* stream) {
   if (!x || !y || Ho <= 0 || Wo <= 0) return UPR_ERR_ARG;
   const long long n = (long long)B * Ho * Wo * C;
+  if (n == 0) return UPR_OK;
+  if (vec4_view_ok(x, B, H, W, C) && vec4_view_ok(y, B, Ho, Wo, C)) {
+    const int nv = (int)(n / 4);
+    hipLaunchKernelGGL(bilinear4_kernel, dim3((nv + 255) / 256), dim3(256), 0, ST(stream), mkv4(x), H, W, C / 4,
+                       mkv4(y), Ho, Wo, (float)H / Ho, (float)W / Wo, nv, accumulate, (half_t*)nullptr, 0);
+    LAUNCH_CHECK();
+  }
   hipLaunchKernelGGL(bilinear_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), mkv(x), B, H, W, C, mkv(y), Ho, Wo,
                      (float)H / Ho, (float)W / Wo, accumulate);
   LAUNCH_CHECK();
@@ -2458,11 +3011,74 @@ int upr_t_bilinear_bwd(const UprView* dy, int B, int H, int W, int C, int Ho, in
   if (getenv("UPR_BILINEAR_BWD_SCATTER")) {  // the atomic scatter form (A/B timing)
     hipLaunchKernelGGL(bilinear_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), mkv(dy), B, H, W, C, Ho, Wo,
                        (float)H / Ho, (float)W / Wo, mkv(dx));
+  } else if (n > 0 && vec4_view_ok(dy, B, Ho, Wo, C) && vec4_view_ok(dx, B, H, W, C) &&
+             (long long)B * Ho * W * C < (1LL << 31)) {
+    hipStream_t st = ST(stream);
+    const int nr = B * Ho * W * C / 4, ns = B * H * W * C / 4;
+    float* row = nullptr;
+    row = (float*)scratch(kSlotRows, sizeof(float) * 4 * (size_t)nr, st);
+    if (!row) return (int)hipErrorOutOfMemory;
+    hipLaunchKernelGGL(bilinear_bwd_rows4_kernel, dim3((nr + 255) / 256), dim3(256), 0, st, mkv4(dy), Ho, Wo, W, C / 4,
+                       (float)W / Wo, row, nr);
+    hipLaunchKernelGGL(bilinear_bwd_cols4_kernel, dim3((ns + 255) / 256), dim3(256), 0, st, (const float*)row, Ho, H,
+                       W, C / 4, (float)H / Ho, mkv4(dx), ns);
+    UPR_CHECK_HIP(hipGetLastError());
+    return UPR_OK;
   } else {
     const long long ns = (long long)B * H * W * C;
     hipLaunchKernelGGL(bilinear_bwd_gather_kernel, dim3(grid_for(ns)), dim3(256), 0, ST(stream), mkv(dy), B, H, W, C,
                        Ho, Wo, (float)H / Ho, (float)W / Wo, mkv(dx));
   }
+  LAUNCH_CHECK();
+}
+
+int upr_t_copy16(const UprView* src, const UprView* dst, int B, int H, int W, int C, int accumulate, void* dst16,
+                 int dst16_cs, void* stream) {
+  if (!src || !dst || !src->data || !dst->data || !dst16) return UPR_ERR_ARG;
+  const long long n = (long long)B * H * W * C;
+  if (n == 0) return UPR_OK;
+  if (!vec4_view_ok(src, B, H, W, C) || !vec4_view_ok(dst, B, H, W, C) || (uintptr_t)dst16 % 8 || dst16_cs % 4 ||
+      (long long)B * H * W * dst16_cs >= (1LL << 31))
+    return UPR_ERR_UNSUPPORTED;
+  const int nv = (int)(n / 4);
+  hipLaunchKernelGGL(copy4_kernel, dim3((nv + 255) / 256), dim3(256), 0, ST(stream), mkv4(src), mkv4(dst), H, W, C / 4,
+                     nv, accumulate, (half_t*)dst16, dst16_cs);
+  LAUNCH_CHECK();
+}
+
+int upr_t_bilinear16(const UprView* x, int B, int H, int W, int C, const UprView* y, int Ho, int Wo, int accumulate,
+                     void* y16, int y16_cs, void* stream) {
+  if (!x || !y || !y16 || Ho <= 0 || Wo <= 0) return UPR_ERR_ARG;
+  const long long n = (long long)B * Ho * Wo * C;
+  if (n == 0) return UPR_OK;
+  if (!vec4_view_ok(x, B, H, W, C) || !vec4_view_ok(y, B, Ho, Wo, C) || (uintptr_t)y16 % 8 || y16_cs % 4 ||
+      (long long)B * Ho * Wo * y16_cs >= (1LL << 31))
+    return UPR_ERR_UNSUPPORTED;
+  const int nv = (int)(n / 4);
+  hipLaunchKernelGGL(bilinear4_kernel, dim3((nv + 255) / 256), dim3(256), 0, ST(stream), mkv4(x), H, W, C / 4, mkv4(y),
+                     Ho, Wo, (float)H / Ho, (float)W / Wo, nv, accumulate, (half_t*)y16, y16_cs);
+  LAUNCH_CHECK();
+}
+
+// out = a + b with its fp16 copy (a residual / skip sum feeding an autocast conv)
+__global__ __launch_bounds__(256) void add16_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                    float* __restrict__ out, half_t* __restrict__ out16, int n4) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const float4 u = ((const float4*)a)[i], v = ((const float4*)b)[i];
+  const float4 r = make_float4(u.x + v.x, u.y + v.y, u.z + v.z, u.w + v.w);
+  ((float4*)out)[i] = r;
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+  ((h4*)out16)[i] = h4{(half_t)r.x, (half_t)r.y, (half_t)r.z, (half_t)r.w};
+}
+
+int upr_t_add16(const float* a, const float* b, float* out, size_t n, void* out16, void* stream) {
+  if (!a || !b || !out || !out16) return UPR_ERR_ARG;
+  if (n % 4 || n / 4 >= (1ULL << 31) || ((uintptr_t)a | (uintptr_t)b | (uintptr_t)out) % 16 || (uintptr_t)out16 % 8)
+    return UPR_ERR_UNSUPPORTED;
+  if (n == 0) return UPR_OK;
+  const int n4 = (int)(n / 4);
+  hipLaunchKernelGGL(add16_kernel, dim3((n4 + 255) / 256), dim3(256), 0, ST(stream), a, b, out, (half_t*)out16, n4);
   LAUNCH_CHECK();
 }
 
@@ -2526,6 +3142,19 @@ int upr_t_fam_sa_bwd(const float* g, const float* o2, const float* sa, int B, in
 int upr_t_fam_ca_bwd(const float* g_o2, const float* g_m, const float* o, const float* o2, const float* ca, int B,
                      int HW, int C, float* g_o, float* g_ca, void* stream) {
   if (!g_o2 || !g_m || !o || !o2 || !ca || !g_o || !g_ca || C > 32) return UPR_ERR_ARG;
+  if (C == 32 && al16(g_o2) && al16(o) && al16(o2) && al16(ca) && al16(g_o) && B > 0 && HW > 0) {
+    hipStream_t st = ST(stream);
+    int chunks = HW / 1024;
+    chunks = chunks < 1 ? 1 : (chunks > 256 ? 256 : chunks);
+    float* part = nullptr;
+    part = (float*)scratch(kSlotPart, sizeof(float) * 32 * B * chunks, st);
+    if (!part) return (int)hipErrorOutOfMemory;
+    hipLaunchKernelGGL(fam_ca_bwd32_kernel, dim3(chunks, B), dim3(256), 0, st, g_o2, g_m, o, o2, ca, HW, g_o, part);
+    hipLaunchKernelGGL(fam_ca_fin_kernel, dim3((B * 32 + 255) / 256), dim3(256), 0, st, (const float*)part, chunks,
+                       B * 32, g_ca);
+    UPR_CHECK_HIP(hipGetLastError());
+    return UPR_OK;
+  }
   UPR_CHECK_HIP(hipMemsetAsync(g_ca, 0, sizeof(float) * B * C, ST(stream)));
   int chunks = HW / 4096;
   chunks = chunks < 1 ? 1 : (chunks > 256 ? 256 : chunks);

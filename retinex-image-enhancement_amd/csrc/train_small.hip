@@ -53,7 +53,7 @@ static SV mksv(const UprView* u) {
 template <int COUT>
 __global__ __launch_bounds__(256) void c3k3_fwd_kernel(SV x, int B, int H, int W, const float* __restrict__ w,
                                                       const float* __restrict__ bias, int p, SV y, int Ho, int Wo,
-                                                      int relu, int accum) {
+                                                      int relu, int accum, half_t* __restrict__ y16) {
   constexpr int TS = COUT + 4;  // LDS row stride (floats): 16-byte aligned rows, spread banks
   extern __shared__ __attribute__((aligned(16))) float sm3[];
   float* sw_ = sm3;                  // [27][COUT] weights, k-major (broadcast reads)
@@ -123,6 +123,10 @@ __global__ __launch_bounds__(256) void c3k3_fwd_kernel(SV x, int B, int H, int W
       v[0] = fmaxf(v[0], 0.f); v[1] = fmaxf(v[1], 0.f); v[2] = fmaxf(v[2], 0.f); v[3] = fmaxf(v[3], 0.f);
     }
     *dst = v;
+    if (y16) {  // the autocast consumer's fp16 operand, [pixel][COUT] compact
+      typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+      *(h4*)(y16 + (size_t)pp * COUT + q * 4) = h4{(half_t)v[0], (half_t)v[1], (half_t)v[2], (half_t)v[3]};
+    }
   }
 }
 
@@ -277,7 +281,10 @@ __global__ __launch_bounds__(256) void small_dgrad_kernel(SV dy, int Ho, int Wo,
 // weight gradient, Cout <= 32: D[co][k] = sum_p dy[p][co] * col[p][k] on
 // v_mfma_f32_32x32x2_f32 (A = dy rows, B = im2col rows, K = 2 pixels)
 // ---------------------------------------------------------------------------
-constexpr int SW_UNROLL = 8;  // pixel pairs in flight per wave
+// pixel pairs in flight per wave: ~32 im2col loads per lane whatever NT (the
+// kernel is latency-bound: 8 pairs left the memory pipe mostly idle)
+template <int NT>
+constexpr int sw_unroll() { return NT == 1 ? 32 : NT == 2 ? 16 : 8; }
 
 template <int NT>
 __global__ __launch_bounds__(256) void small_wgrad_mfma_kernel(SV x, SV dy, int B, int H, int W, int Cin, int Ho,
@@ -312,19 +319,22 @@ __global__ __launch_bounds__(256) void small_wgrad_mfma_kernel(SV x, SV dy, int 
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
-  const long long gw = (long long)blockIdx.x * 4 + wave;
-  const long long pair0 = gw * pairs_per_wave;
+  // 32-bit pixel math (P < 2^31, host-checked): the 64-bit div / mod per
+  // pixel dominated these kernels
+  const int gw = blockIdx.x * 4 + wave;
+  const int pair0 = gw * pairs_per_wave;
+  constexpr int SW_UNROLL = sw_unroll<NT>();
   for (int u0 = 0; u0 < pairs_per_wave; u0 += SW_UNROLL) {
     float av[SW_UNROLL], bv[SW_UNROLL][NT];
 #pragma unroll
     for (int u = 0; u < SW_UNROLL; ++u) {
-      const long long pix = (pair0 + u0 + u) * 2 + half;
+      const int pix = (pair0 + u0 + u) * 2 + half;
       av[u] = 0.f;
 #pragma unroll
       for (int t = 0; t < NT; ++t) bv[u][t] = 0.f;
       if (u0 + u < pairs_per_wave && pix < P) {
-        const int ox = (int)(pix % Wo);
-        const int r = (int)(pix / Wo);
+        const int ox = pix % Wo;
+        const int r = pix / Wo;
         const int oy = r % Ho, b = r / Ho;
         if (j < Cout) av[u] = dy.d[dy.at(b, oy, ox, j)];
 #pragma unroll
@@ -364,12 +374,106 @@ __global__ __launch_bounds__(256) void small_wgrad_mfma_kernel(SV x, SV dy, int 
 }
 
 // ---------------------------------------------------------------------------
+// input gradient of a 3 -> COUT (32 / 64) 3x3 / s1 / p1 conv under autocast
+// (VGG-19 conv1_1's gradient w.r.t. the normalised enhanced image,
+// losses/loss.py:198-211): dy in fp16 (the masked gradient's copy,
+// upr_t_relu_mask16), weights rounded to fp16, fp32 accumulation on
+// v_mfma_f32_16x16x32_f16 -- D[ci][pixel] = sum over (tap, co) of
+// w[co][ci][tap'] * dy[pixel + tap][co] with the weights as A (rows 0..2 of
+// 16 used) and dy as B.  A block owns 4 rows x 64 columns of dx; the dy rows
+// and columns it needs (6 x 66 pixels x COUT channels) sit in LDS, the 16-byte
+// chunks of a pixel XOR-swizzled by its column (within the pixel's COUT / 8
+// chunks) so a fragment read (16 consecutive pixels, one chunk) spreads over
+// the banks.  Lanes 0..15 of each 16-pixel group end
+// with that pixel's 3 input-channel gradients: 12-byte runs, 192 contiguous
+// bytes per group.
+// ---------------------------------------------------------------------------
+template <int COUT>
+__global__ __launch_bounds__(256) void dgrad_c3_mfma_kernel(const half_t* __restrict__ dy, int B, int H, int W,
+                                                            const float* __restrict__ w, SV dx, int accum) {
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  constexpr int KC = COUT / 32, CH = COUT / 8;  // 32-channel k chunks, 16-byte chunks per pixel
+  constexpr int TR = 4, TC = 64, LR = TR + 2, LC = TC + 2;
+  __shared__ __attribute__((aligned(16))) half_t tile[LR * LC * COUT];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fg = lane >> 4;
+  const int tx = blockIdx.x, ty = blockIdx.y, b = blockIdx.z;
+  const int iy0 = ty * TR, ix0 = tx * TC;
+  // dy rows iy0-1 .. iy0+4, columns ix0-1 .. ix0+64 -> LDS
+  for (int q = tid; q < LR * LC * CH; q += 256) {
+    const int ch = q % CH, rc = q / CH, col = rc % LC, r = rc / LC;
+    const int gy = iy0 - 1 + r, gx = ix0 - 1 + col;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if ((unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
+      v = *(const uint4*)(dy + (((size_t)b * H + gy) * W + gx) * COUT + ch * 8);
+    *(uint4*)(tile + (r * LC + col) * COUT + ((ch ^ (col & (CH - 1))) * 8)) = v;
+  }
+  // A = weights: lane (fr = ci, fg) holds w[co = kc*32 + fg*8 + e][ci][tap], tap = 8 - (dr*3 + dc)
+  h8 wa[KC][9];
+#pragma unroll
+  for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        wa[kc][t][e] = fr < 3 ? (half_t)w[((kc * 32 + fg * 8 + e) * 3 + fr) * 9 + (8 - t)] : (half_t)0.f;
+  __syncthreads();
+  const int iy = iy0 + wave;
+  f4 acc[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) acc[g] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int dr = t / 3, dc = t % 3;
+      const int col = g * 16 + fr + dc;  // LDS column of this lane's pixel, shifted by the tap
+      const half_t* row = tile + ((wave + dr) * LC + col) * COUT;
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) {
+        const h8 bv = *(const h8*)(row + (((kc * 4 + fg) ^ (col & (CH - 1))) * 8));
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[kc][t], bv, acc[g], 0, 0, 0);
+      }
+    }
+  if (iy >= H || fg != 0) return;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int ix = ix0 + g * 16 + fr;
+    if (ix >= W) continue;
+    float* o = dx.d + dx.at(b, iy, ix, 0);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      float v = acc[g][c];
+      if (accum) v += o[c * dx.sc];
+      o[c * dx.sc] = v;
+    }
+  }
+}
+
+int small_conv_dgrad_c3_16(const void* dy16, int B, int H, int W, const float* w, int Cout, const UprView* dxv,
+                           int accumulate, hipStream_t st) {
+  if ((Cout != 32 && Cout != 64) || ((uintptr_t)dy16 % 16)) return kErrUnsupported;
+  if ((long long)B * H * W >= (1ll << 31)) return kErrUnsupported;
+  const dim3 grid((W + 63) / 64, (H + 3) / 4, B);
+  if (grid.y > 65535 || grid.z > 65535) return kErrUnsupported;
+  const SV dx = mksv(dxv);
+  if (Cout == 64)
+    hipLaunchKernelGGL(dgrad_c3_mfma_kernel<64>, grid, dim3(256), 0, st, (const half_t*)dy16, B, H, W, w, dx,
+                       accumulate);
+  else
+    hipLaunchKernelGGL(dgrad_c3_mfma_kernel<32>, grid, dim3(256), 0, st, (const half_t*)dy16, B, H, W, w, dx,
+                       accumulate);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // host entries (called from train.hip's upr_t_conv_direct*; kErrUnsupported
 // sends the caller to the generic kernels)
 // ---------------------------------------------------------------------------
 int small_conv_fwd(const UprView* xv, int B, int H, int W, int Cin, const float* w, const float* bias, int Cout,
                    int kh, int kw, int stride, int pad, int dil, const UprView* yv, int Ho, int Wo, int relu,
-                   int accumulate, hipStream_t st) {
+                   int accumulate, hipStream_t st, void* y16) {
+  if (y16 && (Cout <= 4 || (uintptr_t)y16 % 8)) return kErrUnsupported;  // fp16 copies: the 3 -> 32 / 64 kernel only
   if (Cout <= 4) {
     if ((long long)B * Ho * Wo >= (1ll << 31)) return kErrUnsupported;
     const size_t lds = sizeof(float) * (size_t)Cout * Cin * kh * kw;
@@ -406,11 +510,11 @@ int small_conv_fwd(const UprView* xv, int B, int H, int W, int Cin, const float*
   if (Cout == 32) {
     const size_t lds = sizeof(float) * (27 * 32 + 32 + 256 * 36);
     hipLaunchKernelGGL(c3k3_fwd_kernel<32>, dim3(grid), dim3(256), lds, st, x, B, H, W, w, bias, pad, y, Ho, Wo, relu,
-                       accumulate);
+                       accumulate, (half_t*)y16);
   } else {
     const size_t lds = sizeof(float) * (27 * 64 + 64 + 256 * 68);
     hipLaunchKernelGGL(c3k3_fwd_kernel<64>, dim3(grid), dim3(256), lds, st, x, B, H, W, w, bias, pad, y, Ho, Wo, relu,
-                       accumulate);
+                       accumulate, (half_t*)y16);
   }
   return (int)hipGetLastError();
 }
@@ -449,12 +553,13 @@ int small_conv_wgrad(const UprView* xv, const UprView* dyv, int B, int H, int W,
   const int nt = (KC + 31) / 32;
   if (nt > 4) return kErrUnsupported;
   const long long P = (long long)B * Ho * Wo;
-  if (P >= (1ll << 31)) return kErrUnsupported;
+  if (P >= (1ll << 30)) return kErrUnsupported;  // the kernel's 32-bit pair / pixel indices
   const long long pairs = (P + 1) / 2;
-  // ~2048 waves (8 per CU), pairs per wave a multiple of the unroll
-  long long ppw = (pairs + 2047) / 2048;
-  ppw = (ppw + SW_UNROLL - 1) / SW_UNROLL * SW_UNROLL;
-  if (ppw < SW_UNROLL) ppw = SW_UNROLL;
+  // ~4096 waves (16 per CU), pairs per wave a multiple of the unroll
+  long long ppw = (pairs + 4095) / 4096;
+  const int unroll = nt == 1 ? sw_unroll<1>() : nt == 2 ? sw_unroll<2>() : sw_unroll<4>();
+  ppw = (ppw + unroll - 1) / unroll * unroll;
+  if (ppw < unroll) ppw = unroll;
   const long long waves = (pairs + ppw - 1) / ppw;
   const int grid = (int)((waves + 3) / 4);
   const SV x = mksv(xv), dy = mksv(dyv);

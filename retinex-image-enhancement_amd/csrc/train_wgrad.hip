@@ -17,8 +17,8 @@
 // * Each block writes its partial tile to its split's slab (plain stores);
 //   a second kernel sums the slabs in split order and adds them to dwp:
 //   deterministic (no float atomics), one pass over the slabs.
-// * The slabs live in stream-ordered scratch (hipMallocAsync / hipFreeAsync on
-//   the caller's stream), so concurrent streams never share them.
+// * The slabs live in the caller stream's scratch slot (upr_common.h
+//   scratch()), so concurrent streams never share them.
 #include <cstdlib>
 #include <cstring>
 
@@ -156,22 +156,32 @@ __global__ __launch_bounds__(256) void wgrad_group_kernel(const float* __restric
   }
 }
 
-// dwp[co][k] += sum over n partial slabs (in order)
+// dwp[co][k] += sum over n partial slabs (in order); torch_ci > 0: the
+// gradient goes straight into PyTorch's [Co][Ci][kh][kw] layout instead
+// (k = tap * Ci + ci; the 4 k of a quad share the tap), no packed buffer /
+// unpack pass
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int n, int Cout, int KT,
-                                                           int ldn, float* __restrict__ dwp) {
+                                                           int ldn, float* __restrict__ dwp, int torch_ci) {
   const int n4 = Cout * KT / 4;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n4; i += gridDim.x * 256) {
     const int e = i * 4;
     const int co = e / KT, k = e - co * KT;
     f32x4_w2 acc = *(const f32x4_w2*)(part + (size_t)co * ldn + k);
     for (int sp = 1; sp < n; ++sp) acc += *(const f32x4_w2*)(part + ((size_t)sp * Cout + co) * ldn + k);
-    f32x4_w2* o = (f32x4_w2*)(dwp + e);
-    *o = *o + acc;
+    if (torch_ci) {
+      const int taps = KT / torch_ci, tap = k / torch_ci, ci = k - tap * torch_ci;
+      float* o = dwp + ((size_t)co * torch_ci + ci) * taps + tap;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[(size_t)j * taps] += acc[j];
+    } else {
+      f32x4_w2* o = (f32x4_w2*)(dwp + e);
+      *o = *o + acc;
+    }
   }
 }
 
 template <int BM, int BN>
-static int launch_wgrad_gemm(WgArgs a, float* dwp, hipStream_t st) {
+static int launch_wgrad_gemm(WgArgs a, float* dwp, hipStream_t st, int torch_ci) {
   constexpr int LDS = 2 * WG_KP * (BM + BN) * 4;
   static bool attr = false;
   if (!attr) {
@@ -196,9 +206,8 @@ static int launch_wgrad_gemm(WgArgs a, float* dwp, hipStream_t st) {
   a.pix_per_split = pps;
   const int groups = splits > WG_GROUP ? (splits + WG_GROUP - 1) / WG_GROUP : 0;
   const size_t slab_elems = (size_t)a.Cout * a.ldn;
-  void* buf = nullptr;
-  hipError_t e = hipMallocAsync(&buf, (size_t)(splits + groups) * slab_elems * sizeof(float), st);
-  if (e != hipSuccess) return (int)e;
+  void* buf = scratch(kSlotSlab, (size_t)(splits + groups) * slab_elems * sizeof(float), st);
+  if (!buf) return (int)hipErrorOutOfMemory;
   a.slab = (float*)buf;
   hipLaunchKernelGGL((wgrad_gemm_kernel<BM, BN>), dim3(tiles * splits), dim3(256), LDS, st, a);
   const int n4 = a.Cout * a.KT / 4;
@@ -212,10 +221,9 @@ static int launch_wgrad_gemm(WgArgs a, float* dwp, hipStream_t st) {
     part = out;
     nparts = groups;
   }
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(g1), dim3(256), 0, st, part, nparts, a.Cout, a.KT, a.ldn, dwp);
-  e = hipGetLastError();
-  const hipError_t f = hipFreeAsync(buf, st);
-  return (int)(e != hipSuccess ? e : f);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(g1), dim3(256), 0, st, part, nparts, a.Cout, a.KT, a.ldn, dwp,
+                     torch_ci);
+  return (int)hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
@@ -420,7 +428,7 @@ __global__ __launch_bounds__(256) void wgrad16_kernel(Wg16Args a) {
 }
 
 template <int BM, int NR>
-static int launch_wgrad16(Wg16Args a, float* dwp, hipStream_t st) {
+static int launch_wgrad16(Wg16Args a, float* dwp, hipStream_t st, int torch_ci) {
   constexpr int LDS = W16_KP * BM * 2 + 2 * NR * W16_KP * 64;
   static bool attr = false;
   if (!attr) {
@@ -444,9 +452,8 @@ static int launch_wgrad16(Wg16Args a, float* dwp, hipStream_t st) {
   a.units_per_split = ups;
   const int groups = splits > WG_GROUP ? (splits + WG_GROUP - 1) / WG_GROUP : 0;
   const size_t slab_elems = (size_t)a.Cout * a.ldn;
-  void* buf = nullptr;
-  hipError_t e = hipMallocAsync(&buf, (size_t)(splits + groups) * slab_elems * sizeof(float), st);
-  if (e != hipSuccess) return (int)e;
+  void* buf = scratch(kSlotSlab, (size_t)(splits + groups) * slab_elems * sizeof(float), st);
+  if (!buf) return (int)hipErrorOutOfMemory;
   a.slab = (float*)buf;
   hipLaunchKernelGGL((wgrad16_kernel<BM, NR>), dim3(tiles * splits), dim3(256), LDS, st, a);
   const int n4 = a.Cout * a.KT / 4;
@@ -460,28 +467,27 @@ static int launch_wgrad16(Wg16Args a, float* dwp, hipStream_t st) {
     part = out;
     nparts = groups;
   }
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(g1), dim3(256), 0, st, part, nparts, a.Cout, a.KT, a.ldn, dwp);
-  e = hipGetLastError();
-  const hipError_t f = hipFreeAsync(buf, st);
-  return (int)(e != hipSuccess ? e : f);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(g1), dim3(256), 0, st, part, nparts, a.Cout, a.KT, a.ldn, dwp,
+                     torch_ci);
+  return (int)hipGetLastError();
 }
 
 template <int BM>
-static int wgrad16_nr(const Wg16Args& a, float* dwp, hipStream_t st) {
+static int wgrad16_nr(const Wg16Args& a, float* dwp, hipStream_t st, int torch_ci) {
   const int nr = a.nruns;
-  if (BM <= 64 && nr % 9 == 0) return launch_wgrad16<BM, 9>(a, dwp, st);
-  if (BM <= 64 && nr % 8 == 0) return launch_wgrad16<BM, 8>(a, dwp, st);
-  if (nr % 4 == 0) return launch_wgrad16<BM, 4>(a, dwp, st);
-  if (nr % 2 == 0) return launch_wgrad16<BM, 2>(a, dwp, st);
-  return launch_wgrad16<BM, 1>(a, dwp, st);
+  if (BM <= 64 && nr % 9 == 0) return launch_wgrad16<BM, 9>(a, dwp, st, torch_ci);
+  if (BM <= 64 && nr % 8 == 0) return launch_wgrad16<BM, 8>(a, dwp, st, torch_ci);
+  if (nr % 4 == 0) return launch_wgrad16<BM, 4>(a, dwp, st, torch_ci);
+  if (nr % 2 == 0) return launch_wgrad16<BM, 2>(a, dwp, st, torch_ci);
+  return launch_wgrad16<BM, 1>(a, dwp, st, torch_ci);
 }
 
 // AMP entry (upr_t_conv_wgrad16): x16 = the compact fp16 copy of x ([B][H][W][Cin]);
 // kErrUnsupported when the shape does not fit (the caller falls back to fp32)
 int wgrad16_gemm(const void* x16, int B, int H, int W, int Cin, const float* dy, int Ho, int Wo, int Cout, int dy_cs,
-                 int dy_coff, int kh, int kw, int stride, int pad, int dil, float* dwp, hipStream_t st) {
+                 int dy_coff, int kh, int kw, int stride, int pad, int dil, float* dwp, hipStream_t st, int torch_ci) {
   if (Wo % W16_KP || Cin % 32 || Cout % 32 || dy_cs % 4 || dy_coff % 4 || ((uintptr_t)dy % 16) ||
-      ((uintptr_t)x16 % 16) || ((uintptr_t)dwp % 16))
+      ((uintptr_t)x16 % 16) || (!torch_ci && ((uintptr_t)dwp % 16)))
     return kErrUnsupported;
   const long long P = (long long)B * Ho * Wo;
   if (P >= (1ll << 30) || (long long)B * H * W * Cin >= (1ll << 31)) return kErrUnsupported;
@@ -493,17 +499,17 @@ int wgrad16_gemm(const void* x16, int B, int H, int W, int Cin, const float* dy,
   a.KT = kh * kw * Cin;
   a.nruns = a.KT / 32;
   a.units = (int)(P / W16_KP);
-  if (Cout % 128 == 0) return wgrad16_nr<128>(a, dwp, st);
-  if (Cout % 64 == 0) return wgrad16_nr<64>(a, dwp, st);
-  return wgrad16_nr<32>(a, dwp, st);
+  if (Cout % 128 == 0) return wgrad16_nr<128>(a, dwp, st, torch_ci);
+  if (Cout % 64 == 0) return wgrad16_nr<64>(a, dwp, st, torch_ci);
+  return wgrad16_nr<32>(a, dwp, st, torch_ci);
 }
 
 // Entry from train.hip's upr_t_conv_wgrad (same contract: dwp += ...).
 int wgrad_gemm(const float* x, int B, int H, int W, int Cin, int x_cs, int x_coff, const float* dy, int Ho, int Wo,
                int Cout, int dy_cs, int dy_coff, int kh, int kw, int stride, int pad, int dil, float* dwp,
-               hipStream_t st) {
+               hipStream_t st, int torch_ci) {
   if (x_cs % 4 || x_coff % 4 || dy_cs % 4 || dy_coff % 4 || ((uintptr_t)x % 16) || ((uintptr_t)dy % 16) ||
-      ((uintptr_t)dwp % 16))
+      (!torch_ci && ((uintptr_t)dwp % 16)))
     return kErrUnsupported;
   const long long P = (long long)B * Ho * Wo;
   if (P >= (1ll << 30) || (long long)B * H * W >= (1ll << 31)) return kErrUnsupported;
@@ -514,9 +520,9 @@ int wgrad_gemm(const float* x, int B, int H, int W, int Cin, int x_cs, int x_cof
   a.kh = kh; a.kw = kw; a.s = stride; a.p = pad; a.d = dil;
   a.KT = kh * kw * Cin;
   a.P = (int)P;
-  if (Cout % 128 == 0) return launch_wgrad_gemm<128, 64>(a, dwp, st);
-  if (Cout % 64 == 0) return launch_wgrad_gemm<64, 128>(a, dwp, st);
-  return launch_wgrad_gemm<32, 256>(a, dwp, st);
+  if (Cout % 128 == 0) return launch_wgrad_gemm<128, 64>(a, dwp, st, torch_ci);
+  if (Cout % 64 == 0) return launch_wgrad_gemm<64, 128>(a, dwp, st, torch_ci);
+  return launch_wgrad_gemm<32, 256>(a, dwp, st, torch_ci);
 }
 
 }  // namespace upr

@@ -140,4 +140,16 @@ __device__ __forceinline__ float pool_get(const float* pool, size_t idx) {
 #endif
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
+// Per-(device, stream) scratch of the training kernels (split-K slabs,
+// argmax codes, bilinear row sums, partial sums): one growable buffer per
+// slot, reused by every later call on that stream -- the calls are
+// stream-ordered, so a buffer is never live in two of them at once; buffers
+// that ARE live together (a nested call) take different slots.  Replaces
+// hipMallocAsync / hipFreeAsync, which cost 0.1-0.5 ms of host time per
+// call on this stack (13 of 36 ms per training step went to them) and
+// stalled the launch queue.  Growth (warm-up only) synchronises the stream
+// before freeing the smaller buffer.  Returns nullptr when out of memory.
+enum ScratchSlot { kSlotSlab = 0, kSlotCast, kSlotTmp, kSlotCode, kSlotRows, kSlotPart, kSlotCount };
+void* scratch(int slot, size_t bytes, hipStream_t st);
+
 }  // namespace upr

@@ -99,6 +99,13 @@ class UprLossParams(ctypes.Structure):
                 ("freq_low", ctypes.c_float), ("dynamic_smooth", ctypes.c_int)]
 
 
+class UprPackJob(ctypes.Structure):
+    """include/upr_train.h UprPackJob: one re-pack of upr_t_pack_weights."""
+    _fields_ = [("w", ctypes.c_void_p), ("out32", ctypes.c_void_p), ("out16", ctypes.c_void_p), ("Co", ctypes.c_int),
+                ("Ci", ctypes.c_int), ("kh", ctypes.c_int), ("kw", ctypes.c_int), ("mode", ctypes.c_int),
+                ("n", ctypes.c_int)]
+
+
 _vp = ctypes.POINTER(UprView)
 c_u64, c_i64p = ctypes.c_uint64, ctypes.c_void_p
 _i, _p, _f = c_int, c_void_p, c_float
@@ -107,6 +114,8 @@ _i, _p, _f = c_int, c_void_p, c_float
 SIGNATURES.update({
     "upr_t_zero": (_i, [_p, c_size_t, _p]),
     "upr_t_conv_direct": (_i, [_vp, _i, _i, _i, _i, _p, _p, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _p]),
+    "upr_t_conv_dgrad_c3_16": (_i, [_p, _i, _i, _i, _p, _i, _vp, _i, _p]),
+    "upr_t_conv_direct16": (_i, [_vp, _i, _i, _i, _i, _p, _p, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _p, _p]),
     "upr_t_conv_direct_dgrad": (_i, [_vp, _i, _i, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _p]),
     "upr_t_conv_direct_wgrad": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p]),
     "upr_t_conv_mfma": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _p, _i, _i, _i, _i, _i, _i, _p, _i, _i, _p, _i, _i,
@@ -116,7 +125,10 @@ SIGNATURES.update({
     "upr_t_cast_f16": (_i, [_p, _p, c_size_t, _p]),
     "upr_t_conv_wgrad": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p]),
     "upr_t_conv_wgrad16": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p]),
+    "upr_t_conv_wgrad_into": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p,
+                                   _p]),
     "upr_t_pack_weight": (_i, [_p, _p, _i, _i, _i, _i, _i, _p]),
+    "upr_t_pack_weights": (_i, [_p, _i, _i, _p]),
     "upr_t_unpack_grad": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p]),
     "upr_t_zero_upsample": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _p]),
     "upr_t_bn_stats": (_i, [_p, _i, _i, _i, _i, _p, _p]),
@@ -133,11 +145,17 @@ SIGNATURES.update({
                                 _p]),
     "upr_t_zero_upsample16": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _p]),
     "upr_t_relu_mask": (_i, [_p, _i, _i, _p, _i, _i, _i, _i, _p]),
+    "upr_t_relu_mask16": (_i, [_p, _i, _i, _p, _i, _i, _i, _i, _p, _i, _p]),
     "upr_t_copy": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _p]),
     "upr_t_pointwise": (_i, [_p, _p, _p, c_size_t, _i, _p, _p, _f, c_u64, _p]),
     "upr_t_texture_complexity": (_i, [_p, _i, _i, _i, _i, _i, _p, _p, _p]),
     "upr_t_maxpool": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _p]),
     "upr_t_maxpool_bwd": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _p]),
+    "upr_t_maxpool_code": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _p, _p, _p]),
+    "upr_t_copy16": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _p, _i, _p]),
+    "upr_t_bilinear16": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _p, _i, _p]),
+    "upr_t_add16": (_i, [_p, _p, _p, c_size_t, _p, _p]),
+    "upr_t_maxpool_bwd_code": (_i, [_p, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _p]),
     "upr_t_bilinear": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _p]),
     "upr_t_bilinear_bwd": (_i, [_vp, _i, _i, _i, _i, _i, _i, _vp, _p]),
     "upr_t_pixel_sum": (_i, [_p, _i, _i, _i, _i, _i, _f, _p, _i, _p]),

@@ -86,10 +86,9 @@ class _IENetStep(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, anchor, ie, flat):
-        from .train import set_amp, autocast_active
+        from .train import set_amp, autocast_active, pack_convs
         set_amp(autocast_active())
-        for c in ie.convs():
-            c.pack()
+        pack_convs(ie.convs(), ie)
         illu = ie.fwd(x)
         bump_weights_epoch()  # BatchNorm running stats were updated
         ctx.ie, ctx.flat, ctx.illu = ie, flat, illu

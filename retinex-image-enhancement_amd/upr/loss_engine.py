@@ -21,7 +21,8 @@ import torch
 import torch.nn as nn
 
 from . import _lib as L
-from .train import Act, Conv, _chk, _fp, _p, _stream, autocast_active, empty, relu_mask, set_amp, zero
+from .train import (Act, Conv, _chk, _fp, _p, _stream, autocast_active, empty, maxpool_into, pack_convs, relu_mask,
+                    set_amp, zero)
 
 WEIGHTS = dict(exposure=10.0, smoothness=1.0, color=0.5, spatial=1.0, decouple=0.1, perceptual=1.0,
                frequency=0.5)
@@ -71,8 +72,7 @@ class VGGPerceptual:
         self.convs = {i: Conv(features[i], frozen=True) for s in self.SLICES for i in s}
 
     def pack(self):
-        for c in self.convs.values():
-            c.pack()
+        pack_convs(list(self.convs.values()), self)
 
     def run(self, x_nhwc, keep):
         """x_nhwc: Act [B,H,W,3] (normalised).  Returns the three slice outputs;
@@ -89,10 +89,10 @@ class VGGPerceptual:
                 if keep:
                     trace.append(("conv", i, inp, h))
             p = Act.new(h.B, h.H // 2, h.W // 2, h.C, h.t.device, fresh=False)
-            _chk(lib.upr_t_maxpool(ctypes.byref(h.view()), h.B, h.H, h.W, h.C, 2, 2, 0, ctypes.byref(p.view()), p.H,
-                                   p.W, st), "vgg_pool")
+            code = torch.empty(p.B * p.H * p.W * p.C, dtype=torch.uint8, device=h.t.device) if keep else None
+            maxpool_into(h, p, 2, 2, 0, code)
             if keep:
-                trace.append(("pool", None, h, p))
+                trace.append(("pool", code, h, p))
             h = p
             feats.append(p)
         return feats, trace
@@ -102,7 +102,7 @@ class VGGPerceptual:
         lib, st = L.lib(), _stream()
         g = None
         level = 2
-        for kind, i, inp, out in reversed(trace):
+        for kind, i, inp, out in reversed(trace):  # i: conv index, or the pool's argmax codes
             if kind == "pool":
                 if g is None:
                     g = g_feats[level]
@@ -111,14 +111,15 @@ class VGGPerceptual:
                                              ctypes.c_float(0), ctypes.c_uint64(0), st), "add")
                 level -= 1
                 gi = Act.new(inp.B, inp.H, inp.W, inp.C, inp.t.device, fresh=False)
-                zero(gi.t)
-                _chk(lib.upr_t_maxpool_bwd(ctypes.byref(inp.view()), ctypes.byref(g.view()), inp.B, inp.H, inp.W,
-                                           inp.C, 2, 2, 0, out.H, out.W, ctypes.byref(gi.view()), st), "pool_bwd")
+                _chk(lib.upr_t_maxpool_bwd_code(_p(i), ctypes.byref(g.view()), inp.B, inp.H, inp.W, inp.C, 2, 2, 0,
+                                                out.H, out.W, ctypes.byref(gi.view()), 0, st), "pool_bwd")
                 g = gi
             else:
-                relu_mask(g, out)
-                gi = Act.new(inp.B, inp.H, inp.W, inp.C, inp.t.device)
                 c = self.convs[i]
+                # the frozen VGG conv's fp16 dgrad is the masked gradient's only reader
+                want16 = (c.amp and c.mfma) or c.dgrad16_c3
+                relu_mask(g, out, want16=want16, only16=c.frozen and want16)
+                gi = Act.new(inp.B, inp.H, inp.W, inp.C, inp.t.device)
                 if c.mfma:
                     c.bwd(inp, g, gi)
                 else:

@@ -86,22 +86,23 @@ def profile_begin():
 
 
 def profile_end():
-    """Stops recording; returns [(kind, what, flops, ms)] (synchronises)."""
+    """Stops recording; returns [(kind, what, flops, ms, shape)] (synchronises);
+    shape: (Cin, Cout, k, stride, H, W) of the conv's input, or None."""
     recs, _PROF[0] = _PROF[0], None
     if not recs:
         return []
     torch.cuda.synchronize()
-    return [(k, w, f, e0.elapsed_time(e1)) for k, w, f, e0, e1 in recs]
+    return [(k, w, f, e0.elapsed_time(e1), sh) for k, w, f, e0, e1, sh in recs]
 
 
 class _timed:
     __slots__ = ("rec",)
 
-    def __init__(self, kind, what, flops):
+    def __init__(self, kind, what, flops, shape=None):
         self.rec = None
         if _PROF[0] is not None and kind is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            self.rec = [kind, what, flops, e0, e1]
+            self.rec = [kind, what, flops, e0, e1, shape]
 
     def __enter__(self):
         if self.rec is not None:
@@ -131,6 +132,7 @@ class Act:
         self.fresh = False
         self.t16 = None  # compact fp16 copy written by its producer (autocast conv input), or None
         self.t16_grad = False  # t16 of a gradient: written by the fused BN backward (BN.bwd), trusted by dgrad
+        self.stale32 = False  # fp32 t left behind by relu_mask(only16): t16 is the gradient's only value
 
     @staticmethod
     def new(B, H, W, C, dev, fresh=True):
@@ -243,20 +245,40 @@ class Conv:
         self.wp = self.wt = None
         self.wp16 = self.wt16 = None
         self.amp = False  # fp16 arithmetic of the last forward (its backward follows it)
+        self.dgrad16_c3 = False
 
     def out_hw(self, H, W):
         return ((H + 2 * self.p - self.d * (self.kh - 1) - 1) // self.s + 1,
                 (W + 2 * self.p - self.d * (self.kw - 1) - 1) // self.s + 1)
+
+    def _buffers(self):
+        w = self.m.weight
+        if self.wp is None:
+            self.wp = torch.empty_like(w).view(-1)
+            self.wt = torch.empty_like(w).view(-1)
+            self.gp = torch.empty_like(w).view(-1)
+        if _AMP[0] and self.wp16 is None:
+            self.wp16, self.wt16 = _h16(w.numel(), w.device), _h16(w.numel(), w.device)
+
+    def pack_jobs(self):
+        """This conv's re-packs as UprPackJob tuples (pack_convs): the forward
+        and flipped dgrad layouts, fp16 only under autocast, else fp32."""
+        if not self.mfma:
+            return []
+        self._buffers()
+        w, amp = self.m.weight, _AMP[0]
+        n = w.numel()
+        return [(w.data_ptr(), 0 if amp else self.wp.data_ptr(), self.wp16.data_ptr() if amp else 0, self.Cout,
+                 self.Cin, self.kh, self.kw, 0, n),
+                (w.data_ptr(), 0 if amp else self.wt.data_ptr(), self.wt16.data_ptr() if amp else 0, self.Cout,
+                 self.Cin, self.kh, self.kw, 1, n)]
 
     def pack(self):
         if not self.mfma:
             return
         lib, st = L.lib(), _stream()
         w = self.m.weight
-        if self.wp is None:
-            self.wp = torch.empty_like(w).view(-1)
-            self.wt = torch.empty_like(w).view(-1)
-            self.gp = torch.empty_like(w).view(-1)
+        self._buffers()
         _chk(lib.upr_t_pack_weight(_p(w), _p(self.wp), self.Cout, self.Cin, self.kh, self.kw, 0, st), "pack")
         _chk(lib.upr_t_pack_weight(_p(w), _p(self.wt), self.Cout, self.Cin, self.kh, self.kw, 1, st), "pack")
         if _AMP[0]:
@@ -311,8 +333,11 @@ class Conv:
         out.fresh = False
         out.t16 = None  # any fp16 copy of an earlier content is stale now
         self.amp = _AMP[0] and self.mfma and x_view is None
+        # autocast 3 -> 32 / 64 3x3 convs: input gradient on MFMA from an fp16 dy (upr_t_conv_dgrad_c3_16)
+        self.dgrad16_c3 = _AMP[0] and self.Cin == 3 and self.Cout in (32, 64) and \
+            (self.kh, self.kw, self.s, self.p, self.d) == (3, 3, 1, 1, 1)
         kind = "mfma16" if self.amp else ("mfma32" if self.mfma and x_view is None else "direct")
-        with _timed(kind, "fwd", self.flops(B, Ho, Wo)):
+        with _timed(kind, "fwd", self.flops(B, Ho, Wo), (self.Cin, self.Cout, self.kh, self.s, H, W)):
             self._fwd(x, B, H, W, Ho, Wo, relu, out, res, x_view, out16 if self.amp else None)
         self.wrote16 = self.amp and out16 is not None and res is None
         return out
@@ -341,6 +366,18 @@ class Conv:
         else:
             assert res is None
             v = x.view() if x_view is None else xv
+            if _AMP[0] and self.Cin == 3 and self.Cout in (32, 64) and out.coff == 0 and out.cs == out.C:
+                # autocast: the 3-channel input convs also write their output's fp16 copy (the
+                # next conv's operand) instead of a separate cast pass
+                y16 = _h16(B * Ho * Wo * self.Cout, out.t.device)
+                rc = lib.upr_t_conv_direct16(ctypes.byref(v), B, H, W, self.Cin, _p(self.m.weight), _p(self.bias),
+                                             self.Cout, self.kh, self.kw, self.s, self.p, self.d,
+                                             ctypes.byref(out.view()), Ho, Wo, int(relu), 0, _p(y16), st)
+                if rc == 0:
+                    out.t16 = y16
+                    return
+                if rc != L.UPR_ERR_UNSUPPORTED:
+                    _chk(rc, "conv_direct16")
             _chk(lib.upr_t_conv_direct(ctypes.byref(v), B, H, W, self.Cin, _p(self.m.weight), _p(self.bias),
                                        self.Cout, self.kh, self.kw, self.s, self.p, self.d,
                                        ctypes.byref(out.view()), Ho, Wo, int(relu), 0, st), "conv_direct")
@@ -358,24 +395,17 @@ class Conv:
         F = self.flops(B, Ho, Wo)
         mf = self.mfma and x_view is None
         kw_ = ("mfma16" if self.amp and getattr(self, "x16", None) is not None else "mfma32") if mf else "direct"
-        with _timed(None if self.frozen else kw_, "wgrad", F):
+        with _timed(None if self.frozen else kw_, "wgrad", F, (self.Cin, self.Cout, self.kh, self.s, H, W)):
             if not self.frozen:
                 gw = self.m.weight.grad
                 if self.mfma and x_view is None:
-                    zero(self.gp)
                     x16 = getattr(self, "x16", None)
-                    if self.amp and x16 is not None:
-                        # autocast: fp16 operands, fp32 accumulation (trainers/train.py:72)
-                        _chk(lib.upr_t_conv_wgrad16(_fp(x.t), _p(x16), B, H, W, self.Cin, x.cs, x.coff, _fp(gy.t), Ho,
-                                                    Wo, self.Cout, gy.cs, gy.coff, self.kh, self.kw, self.s, self.p,
-                                                    self.d, _p(self.gp), st), "conv_wgrad16")
-                        self.x16 = None
-                    else:
-                        _chk(lib.upr_t_conv_wgrad(_fp(x.t), B, H, W, self.Cin, x.cs, x.coff, _fp(gy.t), Ho, Wo,
-                                                  self.Cout, gy.cs, gy.coff, self.kh, self.kw, self.s, self.p, self.d,
-                                                  _p(self.gp), st), "conv_wgrad")
-                    _chk(lib.upr_t_unpack_grad(_p(self.gp), _p(gw), self.Cout, self.Cin, self.kh, self.kw, 0, 1, st),
-                         "unpack")
+                    # autocast: fp16 operands, fp32 accumulation (trainers/train.py:72); added
+                    # straight into weight.grad's layout
+                    _chk(lib.upr_t_conv_wgrad_into(_fp(x.t), _p(x16) if self.amp else None, B, H, W, self.Cin, x.cs,
+                                                   x.coff, _fp(gy.t), Ho, Wo, self.Cout, gy.cs, gy.coff, self.kh,
+                                                   self.kw, self.s, self.p, self.d, _p(gw), st), "conv_wgrad")
+                    self.x16 = None
                     if self.bias is not None:
                         chan_sum(gy, self.Cout, self.bias.grad, st)
                 else:
@@ -386,7 +416,8 @@ class Conv:
                          "conv_direct_wgrad")
         if gx is None:
             return
-        with _timed("mfma16" if self.amp else ("mfma32" if self.mfma else "direct"), "dgrad", F):
+        with _timed("mfma16" if self.amp else ("mfma32" if self.mfma else "direct"), "dgrad", F,
+                    (self.Cin, self.Cout, self.kh, self.s, H, W)):
             if self.mfma:
                 acc = gx.consume_fresh()
                 src, sH, sW, scs, scoff = gy.t, Ho, Wo, gy.cs, gy.coff
@@ -417,6 +448,16 @@ class Conv:
                                              gx.cs if acc else 0, 0, _fp(gx.t), gx.cs, gx.coff, 0, st), "conv_dgrad")
             else:
                 acc = gx.consume_fresh()
+                if self.dgrad16_c3 and gy.t16 is not None and gy.t16_grad:
+                    # autocast (VGG conv1_1): fp16 dy from the fused ReLU mask, MFMA
+                    rc = lib.upr_t_conv_dgrad_c3_16(_p(gy.t16), B, H, W, _p(self.m.weight), self.Cout,
+                                                    ctypes.byref(gx.view()), int(acc), st)
+                    if rc == 0:
+                        return
+                    if rc != L.UPR_ERR_UNSUPPORTED:
+                        _chk(rc, "conv_dgrad_c3_16")
+                    if gy.stale32:
+                        raise RuntimeError("upr: fp16-only gradient without an fp16 dgrad path")
                 _chk(lib.upr_t_conv_direct_dgrad(ctypes.byref(gy.view()), Ho, Wo, _p(self.m.weight), B, H, W, self.Cin,
                                                  self.Cout, self.kh, self.kw, self.s, self.p, self.d,
                                                  ctypes.byref(gx.view()), acc, st), "conv_direct_dgrad")
@@ -434,14 +475,30 @@ class ConvT:
         self.wp16 = self.wd16 = None
         self.amp = False
 
-    def pack(self):
-        lib, st = L.lib(), _stream()
+    def _buffers(self):
         w = self.m.weight
         if self.wp is None:
             self.wp = torch.empty_like(w).view(-1)
             self.wd = torch.empty_like(w).view(-1)
             self.gp = torch.empty_like(w).view(-1)
             self.b4 = empty((4 * self.Cout,), w.device)
+        if _AMP[0] and self.wp16 is None:
+            self.wp16, self.wd16 = _h16(w.numel(), w.device), _h16(w.numel(), w.device)
+
+    def pack_jobs(self):
+        self._buffers()
+        w, amp = self.m.weight, _AMP[0]
+        n = w.numel()
+        return [(w.data_ptr(), 0 if amp else self.wp.data_ptr(), self.wp16.data_ptr() if amp else 0, self.Cout,
+                 self.Cin, 2, 2, 2, n),
+                (w.data_ptr(), 0 if amp else self.wd.data_ptr(), self.wd16.data_ptr() if amp else 0, self.Cout,
+                 self.Cin, 2, 2, 3, n),
+                (self.m.bias.data_ptr(), self.b4.data_ptr(), 0, self.Cout, 1, 1, 1, 4, self.Cout)]
+
+    def pack(self):
+        lib, st = L.lib(), _stream()
+        w = self.m.weight
+        self._buffers()
         _chk(lib.upr_t_pack_weight(_p(w), _p(self.wp), self.Cout, self.Cin, 2, 2, 2, st), "pack")
         _chk(lib.upr_t_pack_weight(_p(w), _p(self.wd), self.Cout, self.Cin, 2, 2, 3, st), "pack")
         if _AMP[0]:
@@ -576,9 +633,75 @@ def chan_sum(g, C, out, st):
     _chk(L.lib().upr_t_chan_sum_ws(g.ptr(), g.M, C, g.cs, 0, _p(out), 1, _p(ws), st), "dbias")
 
 
-def relu_mask(g, y):
-    g.t16, g.t16_grad = None, False  # masked in place: any fp16 copy is stale
+def relu_mask(g, y, want16=False, only16=False):
+    """g *= (y > 0) in place.  want16: also write the masked gradient's fp16 copy
+    (g.t16, the next autocast dgrad's operand) in the same pass; only16: the fp32
+    g is left unmasked (stale) -- for a gradient whose only reader is a frozen
+    conv's fp16 dgrad."""
+    g.t16, g.t16_grad, g.stale32 = None, False, False  # masked in place: any fp16 copy is stale
+    if want16 and g.coff == 0 and g.cs == g.C:
+        g16 = _h16(g.M * g.C, g.t.device)
+        rc = L.lib().upr_t_relu_mask16(_fp(g.t), g.cs, g.coff, _fp(y.t), y.cs, y.coff, g.M, g.C, _p(g16),
+                                       int(not only16), _stream())
+        if rc == 0:
+            g.t16, g.t16_grad, g.stale32 = g16, True, only16
+            return
+        if rc != L.UPR_ERR_UNSUPPORTED:
+            _chk(rc, "relu_mask16")
     _chk(L.lib().upr_t_relu_mask(_fp(g.t), g.cs, g.coff, _fp(y.t), y.cs, y.coff, g.M, g.C, _stream()), "relu_mask")
+
+
+def maxpool_into(x, y, k, s, p, code=None):
+    """nn.MaxPool2d(k, s, p) of Act x into Act y (argmax codes for the backward
+    when `code`); under autocast also y's fp16 copy (y.t16) in the same pass."""
+    lib, st = L.lib(), _stream()
+    if _AMP[0] and y.coff == 0 and y.cs == y.C:
+        y16 = _h16(y.M * y.C, y.t.device)
+        rc = lib.upr_t_maxpool_code(ctypes.byref(x.view()), x.B, x.H, x.W, x.C, k, s, p, ctypes.byref(y.view()), y.H,
+                                    y.W, _p(code), _p(y16), st)
+        if rc == 0:
+            y.t16 = y16
+            return
+        if rc != L.UPR_ERR_UNSUPPORTED:
+            _chk(rc, "maxpool")
+    _chk(lib.upr_t_maxpool_code(ctypes.byref(x.view()), x.B, x.H, x.W, x.C, k, s, p, ctypes.byref(y.view()), y.H, y.W,
+                                _p(code), None, st), "maxpool")
+    y.t16 = None
+
+
+def add_acts(a, b, out):
+    """out = a + b (contiguous Acts of one shape); under autocast with out's fp16 copy."""
+    n = out.t.numel()
+    if _AMP[0]:
+        o16 = _h16(n, out.t.device)
+        rc = L.lib().upr_t_add16(_fp(a.t), _fp(b.t), _fp(out.t), n, _p(o16), _stream())
+        if rc == 0:
+            out.t16 = o16
+            return
+        if rc != L.UPR_ERR_UNSUPPORTED:
+            _chk(rc, "add16")
+    pointwise(a.t, b.t, out.t, n, 4)
+    out.t16 = None
+
+
+def pack_convs(convs, owner):
+    """Re-pack every conv's weights for this step in ONE launch
+    (upr_t_pack_weights); the device job table is rebuilt only when a pointer,
+    shape or the autocast mode changed, and is kept alive on `owner`."""
+    jobs = []
+    for c in convs:
+        jobs += c.pack_jobs()
+    if not jobs:
+        return
+    key = tuple(jobs)
+    tab = getattr(owner, "_pack_tab", None)
+    if tab is None or tab[0] != key:
+        arr = (L.UprPackJob * len(jobs))(*[L.UprPackJob(*j) for j in jobs])
+        host = torch.frombuffer(bytearray(arr), dtype=torch.uint8)
+        dev = convs[0].m.weight.device
+        owner._pack_tab = (key, host.to(dev), len(jobs), max(j[-1] for j in jobs))
+    _, t, nj, mx = owner._pack_tab
+    _chk(L.lib().upr_t_pack_weights(_p(t), nj, mx, _stream()), "pack_weights")
 
 
 def add_into(dst, src):
@@ -773,7 +896,7 @@ class UpBlockT:
         if skip is None:
             return self.a2
         out = Act.new(self.a2.B, self.a2.H, self.a2.W, self.a2.C, x.t.device, fresh=False)
-        pointwise(self.a2.t, skip.t, out.t, out.t.numel(), 4)
+        add_acts(self.a2, skip, out)
         return out
 
     def bwd(self, g, gx, g_skip=None):
@@ -821,8 +944,8 @@ class FAMT:
         self.b1.fwd(x, out=cat.slice(0, C), out16=o16(0))
         ok16 = self.b1.wrote16
         self.mp = Act.new(B, H, W, x.C, dev, fresh=False)
-        _chk(lib.upr_t_maxpool(ctypes.byref(x.view()), B, H, W, x.C, 3, 1, 1, ctypes.byref(self.mp.view()), H, W, st),
-             "maxpool")
+        self.mp_code = torch.empty(B * H * W * x.C, dtype=torch.uint8, device=dev)  # argmax codes for the backward
+        maxpool_into(x, self.mp, 3, 1, 1, self.mp_code)
         self.b2.fwd(self.mp, out=cat.slice(C, C), out16=o16(1))
         ok16 = ok16 and self.b2.wrote16
         self.t3 = self.b3a.fwd(x, relu=True)
@@ -878,13 +1001,14 @@ class FAMT:
         g_mp = Act.new(B, H, W, self.x.C, dev)
         self.b2.bwd(self.mp, g_cat.slice(C, C), g_mp)
         gx.zero_if_fresh()
-        _chk(lib.upr_t_maxpool_bwd(ctypes.byref(self.x.view()), ctypes.byref(g_mp.view()), B, H, W, self.x.C, 3, 1, 1,
-                                   H, W, ctypes.byref(gx.view()), st), "maxpool_bwd")
+        _chk(lib.upr_t_maxpool_bwd_code(_p(self.mp_code), ctypes.byref(g_mp.view()), B, H, W, self.x.C, 3, 1, 1,
+                                        H, W, ctypes.byref(gx.view()), 1, st), "maxpool_bwd")
+        self.mp_code = None
         for (ca_, cb_, t) in ((self.b3a, self.b3b, self.t3), (self.b4a, self.b4b, self.t4)):
             k = 2 if cb_ is self.b3b else 3
             g_t = Act.new(B, H, W, t.C, dev)
             cb_.bwd(t, g_cat.slice(k * C, C), g_t)
-            relu_mask(g_t, t)
+            relu_mask(g_t, t, want16=ca_.amp and ca_.mfma)
             ca_.bwd(self.x, g_t, gx)
 
 
@@ -976,8 +1100,7 @@ class UPRetinexTrainGraph:
             self.s1f.convs() + self.s2f.convs() + self.s3f.convs()
 
     def pack(self):
-        for c in self._convs:
-            c.pack()
+        pack_convs(self._convs, self)
 
     def forward(self, x):
         """x [B,3,H,W] fp32 NCHW (H, W multiples of 16) -> (enh, refl, illu)."""
@@ -1009,11 +1132,31 @@ class UPRetinexTrainGraph:
         self.s3 = self.s3c.fwd(pyr[1], relu=True)
         f3 = self.s3f.fwd(self.s3)
         fused = Act.new(B, H, W, 96, dev, fresh=False)
-        _chk(lib.upr_t_copy(ctypes.byref(f1.view()), ctypes.byref(fused.slice(0, 32).view()), B, H, W, 32, 0, st),
-             "cat")
+        # under autocast the concat's fp16 copy (the fusion conv's operand) is written alongside
+        f16 = _h16(B * H * W * 96, dev) if _AMP[0] else None
+        ok16 = f16 is not None
+        if ok16:
+            rc = lib.upr_t_copy16(ctypes.byref(f1.view()), ctypes.byref(fused.slice(0, 32).view()), B, H, W, 32, 0,
+                                  _p(f16), 96, st)
+            ok16 = rc == 0
+            if rc not in (0, L.UPR_ERR_UNSUPPORTED):
+                _chk(rc, "cat16")
+        if not ok16:
+            _chk(lib.upr_t_copy(ctypes.byref(f1.view()), ctypes.byref(fused.slice(0, 32).view()), B, H, W, 32, 0, st),
+                 "cat")
         for i, f in enumerate((f2, f3)):
-            _chk(lib.upr_t_bilinear(ctypes.byref(f.view()), B, f.H, f.W, 32,
-                                    ctypes.byref(fused.slice(32 * (i + 1), 32).view()), H, W, 0, st), "upsample")
+            dst = fused.slice(32 * (i + 1), 32).view()
+            if ok16:
+                rc = lib.upr_t_bilinear16(ctypes.byref(f.view()), B, f.H, f.W, 32, ctypes.byref(dst), H, W, 0,
+                                          ctypes.c_void_p(f16.data_ptr() + 2 * 32 * (i + 1)), 96, st)
+                ok16 = rc == 0
+                if rc == 0:
+                    continue
+                if rc != L.UPR_ERR_UNSUPPORTED:
+                    _chk(rc, "upsample16")
+            _chk(lib.upr_t_bilinear(ctypes.byref(f.view()), B, f.H, f.W, 32, ctypes.byref(dst), H, W, 0, st),
+                 "upsample")
+        fused.t16 = f16 if ok16 else None
         self.fused = fused
         self.fz = self.fusion.fwd(fused)
         o = self.outc.fwd(self.fz)

@@ -116,6 +116,25 @@ def test_conv_wgrad16_vs_fp64(B, cin, cout, H, W, k, s, p, d):
         torch.cuda.synchronize()
         _close(dw, ref, 1e-4, f"wgrad16 x16={use_x16}")
 
+    # upr_t_conv_wgrad_into: the same gradient added straight into PyTorch's
+    # [Co][Ci][kh][kw] layout at an unaligned offset of a flat buffer (the
+    # data-parallel gradient bucket), fp16 (x16) and fp32 (no x16) arithmetic
+    ref_t = ref.view(cout, k, k, cin).permute(0, 3, 1, 2).contiguous()
+    ref32 = torch.nn.grad.conv2d_weight(x.double(), (cout, cin, k, k), dy.double(), stride=s, padding=p,
+                                        dilation=d).float()
+    for use_x16 in (True, False):
+        flat = torch.zeros(cout * cin * k * k + 1, device=DEV)
+        flat[0] = 7.0
+        base = torch.randn(cout, cin, k, k, generator=torch.Generator().manual_seed(4))
+        flat[1:] = base.reshape(-1).to(DEV)
+        rc = lib.upr_t_conv_wgrad_into(xd.data_ptr(), x16.data_ptr() if use_x16 else None, B, H, W, cin, cin, 0,
+                                       dyd.data_ptr(), Ho, Wo, cout, cout, 0, k, k, s, p, d, flat.data_ptr() + 4, st)
+        assert rc == 0, rc
+        torch.cuda.synchronize()
+        assert flat[0].item() == 7.0
+        want = (ref_t if use_x16 else ref32) + base
+        _close(flat[1:].view(cout, cin, k, k), want, 1e-4, f"wgrad_into x16={use_x16}")
+
 
 @pytest.mark.parametrize("B,C,H,W,k,s,p,nchw", [
     (2, 32, 40, 56, 3, 1, 1, False),  # EnhancedFAM branch2 max-pool (vectorised path)
@@ -159,6 +178,210 @@ def test_maxpool_bwd_matches_torch(B, C, H, W, k, s, p, nchw):
     assert torch.equal(torch.isnan(out), torch.isnan(ref))
     m = ~torch.isnan(ref)
     assert (out[m] - ref[m]).abs().max().item() <= 1e-6 * max(1.0, ref[m].abs().max().item())  # summation order
+
+
+@pytest.mark.parametrize("B,C,H,W,k,s,p,acc", [
+    (2, 32, 40, 56, 3, 1, 1, 1),   # EnhancedFAM branch2 (fast 3x3/1/1 path, dx accumulated)
+    (2, 64, 34, 50, 2, 2, 0, 0),   # VGG pool (fast 2x2/2 path, dx written)
+    (2, 64, 33, 51, 2, 2, 0, 0),   # odd extents: the uncovered last row / column get dx = 0
+    (1, 6, 20, 24, 3, 1, 1, 1),    # C % 4 != 0: generic kernels
+    (1, 3, 32, 32, 4, 4, 0, 0),    # generic window, written
+])
+def test_maxpool_code_fwd_bwd_matches_torch(B, C, H, W, k, s, p, acc):
+    """upr_t_maxpool_code (forward + argmax byte codes) and upr_t_maxpool_bwd_code
+    (gather from those codes) vs torch CPU max_pool2d forward / backward, NHWC,
+    with ties on a 0.25 grid, one NaN window and -inf entries; the forward
+    value is exact and the codes match upr_t_maxpool_bwd's recomputed ones."""
+    import ctypes
+    import torch.nn.functional as F
+    from upr import _lib as L
+    torch.manual_seed(6)
+    x = (torch.randn(B, C, H, W) * 2).round() / 4
+    x[0, 0, 5, 7] = float("nan")
+    x[-1, -1, 2, 3] = float("-inf")
+    xr = x.clone().requires_grad_(True)
+    y = F.max_pool2d(xr, k, s, p)
+    gy = torch.randn(y.shape)
+    y.backward(gy)
+    base = torch.randn(B, C, H, W)
+    ref = xr.grad + (base if acc else 0)
+    Ho, Wo = y.shape[2], y.shape[3]
+    xd, gyd = x.permute(0, 2, 3, 1).contiguous().to(DEV), gy.permute(0, 2, 3, 1).contiguous().to(DEV)
+    dxd = base.permute(0, 2, 3, 1).contiguous().to(DEV)
+    yd = torch.full((B, Ho, Wo, C), 7.0, device=DEV)
+    code = torch.full((B * Ho * Wo * C,), 77, dtype=torch.uint8, device=DEV)
+    vx = L.UprView(xd.data_ptr(), H * W * C, W * C, C, 1)
+    vy = L.UprView(yd.data_ptr(), Ho * Wo * C, Wo * C, C, 1)
+    vg = L.UprView(gyd.data_ptr(), Ho * Wo * C, Wo * C, C, 1)
+    vd = L.UprView(dxd.data_ptr(), H * W * C, W * C, C, 1)
+    st = torch.cuda.current_stream().cuda_stream
+    lib = L.lib()
+    assert lib.upr_t_maxpool_code(ctypes.byref(vx), B, H, W, C, k, s, p, ctypes.byref(vy), Ho, Wo,
+                                  ctypes.c_void_p(code.data_ptr()), None, st) == 0
+    assert lib.upr_t_maxpool_bwd_code(ctypes.c_void_p(code.data_ptr()), ctypes.byref(vg), B, H, W, C, k, s, p, Ho, Wo,
+                                      ctypes.byref(vd), acc, st) == 0
+    torch.cuda.synchronize()
+    yo = yd.permute(0, 3, 1, 2).cpu()
+    assert torch.equal(torch.isnan(yo), torch.isnan(y.detach()))
+    assert torch.equal(yo.nan_to_num(0.0), y.detach().nan_to_num(0.0))
+    # the codes point at the window's first maximal tap (PyTorch's index rule)
+    _, idx = F.max_pool2d(x, k, s, p, return_indices=True)
+    oy = torch.arange(Ho).view(1, 1, Ho, 1) * s - p
+    ox = torch.arange(Wo).view(1, 1, 1, Wo) * s - p
+    want = (idx // W - oy) * k + (idx % W - ox)
+    got = code.view(B, Ho, Wo, C).permute(0, 3, 1, 2).cpu().long()
+    assert torch.equal(got, want)
+    out = dxd.permute(0, 3, 1, 2).cpu()
+    assert torch.equal(torch.isnan(out), torch.isnan(ref))
+    m = ~torch.isnan(ref)
+    assert (out[m] - ref[m]).abs().max().item() <= 1e-6 * max(1.0, ref[m].abs().max().item())
+
+
+@pytest.mark.parametrize("B,C,H,W,Ho,Wo,sliced", [
+    (2, 32, 16, 12, 64, 48, True),   # scale3 -> full resolution (4x) into a channel slice of the concat (vec4 path)
+    (2, 32, 24, 20, 48, 40, False),  # scale2 -> full resolution (2x)
+    (2, 3, 64, 48, 32, 24, False),   # the input pyramid's 0.5x downsample (generic path, C = 3)
+    (1, 8, 10, 14, 37, 23, True),    # non-integer ratios
+])
+def test_bilinear_and_copy_vs_torch(B, C, H, W, Ho, Wo, sliced):
+    """upr_t_bilinear / upr_t_bilinear_bwd (accumulating into dx) / upr_t_copy
+    vs F.interpolate(mode='bilinear', align_corners=False) (models/model.py:
+    436-441) forward and backward on torch CPU fp32."""
+    import ctypes
+    import torch.nn.functional as F
+    from upr import _lib as L
+    gen = torch.Generator().manual_seed(H * W + C)
+    x = torch.randn(B, C, H, W, generator=gen)
+    gy = torch.randn(B, C, Ho, Wo, generator=gen)
+    base = torch.randn(B, C, H, W, generator=gen)
+    xr = x.clone().requires_grad_(True)
+    y = F.interpolate(xr, size=(Ho, Wo), mode="bilinear", align_corners=False)
+    y.backward(gy)
+    lib, st = L.lib(), torch.cuda.current_stream().cuda_stream
+    CT = 3 * C if sliced else C  # the output lives in channels [C, 2C) of a wider tensor when sliced
+    off = C if sliced else 0
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    yd = torch.full((B, Ho, Wo, CT), 5.0, device=DEV)
+    pre = torch.randn(B, Ho, Wo, C, generator=gen).to(DEV)
+    yd[..., off:off + C] = pre
+    vx = L.UprView(xd.data_ptr(), H * W * C, W * C, C, 1)
+    vy = L.UprView(yd.data_ptr() + 4 * off, Ho * Wo * CT, Wo * CT, CT, 1)
+    assert lib.upr_t_bilinear(ctypes.byref(vx), B, H, W, C, ctypes.byref(vy), Ho, Wo, 1, st) == 0  # accumulate
+    torch.cuda.synchronize()
+    ref = y.detach().permute(0, 2, 3, 1) + pre.cpu()
+    assert (yd[..., off:off + C].cpu() - ref).abs().max().item() <= 1e-5
+    if sliced:
+        assert torch.all(yd[..., :off] == 5.0) and torch.all(yd[..., off + C:] == 5.0)
+    # backward from a sliced gradient, accumulated into base
+    gd = torch.zeros(B, Ho, Wo, CT, device=DEV)
+    gd[..., off:off + C] = gy.permute(0, 2, 3, 1).to(DEV)
+    vg = L.UprView(gd.data_ptr() + 4 * off, Ho * Wo * CT, Wo * CT, CT, 1)
+    dxd = base.permute(0, 2, 3, 1).contiguous().to(DEV)
+    vd = L.UprView(dxd.data_ptr(), H * W * C, W * C, C, 1)
+    assert lib.upr_t_bilinear_bwd(ctypes.byref(vg), B, H, W, C, Ho, Wo, ctypes.byref(vd), st) == 0
+    torch.cuda.synchronize()
+    refg = (xr.grad + base).permute(0, 2, 3, 1)
+    assert (dxd.cpu() - refg).abs().max().item() <= 1e-5 * max(1.0, refg.abs().max().item())
+    # copy (overwrite, then accumulate) between a slice and a dense tensor
+    dst = torch.zeros(B, Ho, Wo, C, device=DEV)
+    vdst = L.UprView(dst.data_ptr(), Ho * Wo * C, Wo * C, C, 1)
+    assert lib.upr_t_copy(ctypes.byref(vy), ctypes.byref(vdst), B, Ho, Wo, C, 0, st) == 0
+    assert lib.upr_t_copy(ctypes.byref(vy), ctypes.byref(vdst), B, Ho, Wo, C, 1, st) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(dst, 2 * yd[..., off:off + C])
+
+
+@pytest.mark.parametrize("B,H,W,cout,acc", [(2, 40, 72, 64, 0), (1, 17, 130, 64, 1), (2, 24, 64, 32, 1)])
+def test_conv_dgrad_c3_16_vs_fp64(B, H, W, cout, acc):
+    """upr_t_conv_dgrad_c3_16 (VGG conv1_1's input gradient under autocast):
+    vs the fp64 input gradient of the fp16-rounded dy and weights; ragged tile
+    edges (H % 4, W % 64), dx accumulated or written."""
+    import ctypes
+    from upr import _lib as L
+    gen = torch.Generator().manual_seed(H + W)
+    w = torch.randn(cout, 3, 3, 3, generator=gen) * 0.2
+    dy = torch.randn(B, cout, H, W, generator=gen)
+    base = torch.randn(B, 3, H, W, generator=gen)
+    ref = torch.nn.grad.conv2d_input((B, 3, H, W), w.half().double(), dy.half().double(), padding=1).float()
+    if acc:
+        ref = ref + base
+    dy16 = dy.permute(0, 2, 3, 1).contiguous().half().to(DEV)
+    dx = base.permute(0, 2, 3, 1).contiguous().to(DEV)
+    wd = w.to(DEV)
+    vd = L.UprView(dx.data_ptr(), H * W * 3, W * 3, 3, 1)
+    rc = L.lib().upr_t_conv_dgrad_c3_16(ctypes.c_void_p(dy16.data_ptr()), B, H, W, ctypes.c_void_p(wd.data_ptr()),
+                                        cout, ctypes.byref(vd), acc, torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, rc
+    torch.cuda.synchronize()
+    _close(dx.permute(0, 3, 1, 2), ref, 1e-5, "dgrad_c3_16")
+
+
+def test_fp16_copy_producers():
+    """The autocast operand copies written by their producers (no cast pass):
+    upr_t_conv_direct16 (3 -> 32 / 64 3x3 + ReLU), upr_t_maxpool_code(y16),
+    upr_t_add16, upr_t_copy16 / upr_t_bilinear16 into a channel slice of an fp16
+    concat: each fp16 value == (half) of the fp32 result written alongside."""
+    import ctypes
+    from upr import _lib as L
+    lib, st = L.lib(), torch.cuda.current_stream().cuda_stream
+    gen = torch.Generator().manual_seed(9)
+    B, H, W = 2, 20, 36
+    # direct 3 -> 64 conv
+    x = torch.rand(B, 3, H, W, generator=gen).to(DEV)
+    w = (torch.randn(64, 3, 3, 3, generator=gen) * 0.3).to(DEV)
+    bias = torch.randn(64, generator=gen).to(DEV)
+    y = torch.empty(B, H, W, 64, device=DEV)
+    y16 = torch.empty(B * H * W * 64, dtype=torch.float16, device=DEV)
+    vx = L.UprView(x.data_ptr(), 3 * H * W, W, 1, H * W)
+    vy = L.UprView(y.data_ptr(), H * W * 64, W * 64, 64, 1)
+    assert lib.upr_t_conv_direct16(ctypes.byref(vx), B, H, W, 3, w.data_ptr(), bias.data_ptr(), 64, 3, 3, 1, 1, 1,
+                                   ctypes.byref(vy), H, W, 1, 0, y16.data_ptr(), st) == 0
+    torch.cuda.synchronize()
+    ref = torch.relu(torch.nn.functional.conv2d(x.cpu(), w.cpu(), bias.cpu(), padding=1)).permute(0, 2, 3, 1)
+    _close(y, ref, 1e-5, "direct16 fp32")
+    assert torch.equal(y16.view(B, H, W, 64), y.half())
+    # a 1 x 1 head has no fp16 form: UNSUPPORTED, nothing written
+    w1 = torch.randn(1, 3, 1, 1, device=DEV)
+    y1 = torch.full((B, H, W, 1), 3.0, device=DEV)
+    vy1 = L.UprView(y1.data_ptr(), H * W, W, 1, 1)
+    assert lib.upr_t_conv_direct16(ctypes.byref(vx), B, H, W, 3, w1.data_ptr(), None, 1, 1, 1, 1, 0, 1,
+                                   ctypes.byref(vy1), H, W, 0, 0, y16.data_ptr(), st) == L.UPR_ERR_UNSUPPORTED
+    assert torch.all(y1 == 3.0)
+    # max-pool 3x3/1/1 with the fp16 copy
+    mp = torch.empty_like(y)
+    mp16 = torch.empty_like(y16)
+    vmp = L.UprView(mp.data_ptr(), H * W * 64, W * 64, 64, 1)
+    assert lib.upr_t_maxpool_code(ctypes.byref(vy), B, H, W, 64, 3, 1, 1, ctypes.byref(vmp), H, W, None,
+                                  mp16.data_ptr(), st) == 0
+    torch.cuda.synchronize()
+    refp = torch.nn.functional.max_pool2d(y.permute(0, 3, 1, 2).cpu(), 3, 1, 1).permute(0, 2, 3, 1)
+    assert torch.equal(mp.cpu(), refp) and torch.equal(mp16.view(B, H, W, 64), mp.half())
+    # add16
+    s_ = torch.empty_like(y)
+    s16 = torch.empty_like(y16)
+    assert lib.upr_t_add16(y.data_ptr(), mp.data_ptr(), s_.data_ptr(), y.numel(), s16.data_ptr(), st) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(s_, y + mp) and torch.equal(s16.view(B, H, W, 64), s_.half())
+    # copy16 / bilinear16 into channels [32, 64) and [64, 96) of a 96-channel concat
+    cat = torch.zeros(B, H, W, 96, device=DEV)
+    cat16 = torch.zeros(B * H * W * 96, dtype=torch.float16, device=DEV)
+    src = y[..., :32].contiguous()
+    vs = L.UprView(src.data_ptr(), H * W * 32, W * 32, 32, 1)
+    vc1 = L.UprView(cat.data_ptr() + 4 * 32, H * W * 96, W * 96, 96, 1)
+    assert lib.upr_t_copy16(ctypes.byref(vs), ctypes.byref(vc1), B, H, W, 32, 0, cat16.data_ptr() + 2 * 32, 96,
+                            st) == 0
+    small = torch.randn(B, H // 4, W // 4, 32, generator=gen).to(DEV)
+    vsm = L.UprView(small.data_ptr(), (H // 4) * (W // 4) * 32, (W // 4) * 32, 32, 1)
+    vc2 = L.UprView(cat.data_ptr() + 4 * 64, H * W * 96, W * 96, 96, 1)
+    assert lib.upr_t_bilinear16(ctypes.byref(vsm), B, H // 4, W // 4, 32, ctypes.byref(vc2), H, W, 0,
+                                cat16.data_ptr() + 2 * 64, 96, st) == 0
+    torch.cuda.synchronize()
+    c16 = cat16.view(B, H, W, 96)
+    assert torch.equal(cat[..., 32:64], src) and torch.equal(c16[..., 32:96], cat[..., 32:96].half())
+    assert torch.all(c16[..., :32] == 0) and torch.all(cat[..., :32] == 0)
+    refb = torch.nn.functional.interpolate(small.permute(0, 3, 1, 2).cpu(), size=(H, W), mode="bilinear",
+                                           align_corners=False).permute(0, 2, 3, 1)
+    _close(cat[..., 64:96], refb, 1e-5, "bilinear16")
 
 
 @pytest.mark.parametrize("cin,cout,hw", [

@@ -1,0 +1,88 @@
+"""Host-side profile of the configs[4] AMP training step (bs 8, 512^2, plain
+model): per C-ABI function host time (every libupr call timed on the host),
+the Python hot spots (cProfile, by own time) and the device-idle estimate
+(step wall time vs the sum of the step's kernels is in the rocprofv3 trace,
+not here).  Run on the GPU box: python tools/host_prof.py"""
+import cProfile
+import collections
+import os
+import pstats
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "retinex-image-enhancement_amd"), REPO]
+
+import torch  # noqa: E402
+
+from upr import _lib as L  # noqa: E402
+
+
+class _Timed:
+    """Proxy over the ctypes library: each ABI call's host duration."""
+
+    def __init__(self, lib):
+        self._lib = lib
+        self.t = collections.Counter()
+        self.n = collections.Counter()
+
+    def __getattr__(self, name):
+        fn = getattr(self._lib, name)
+        if not callable(fn):
+            return fn
+
+        def call(*a):
+            t0 = time.perf_counter()
+            r = fn(*a)
+            self.t[name] += time.perf_counter() - t0
+            self.n[name] += 1
+            return r
+        return call
+
+
+def main():
+    from models.model import UP_Retinex
+    from losses.loss import TotalLoss
+    from trainers.train import GradScaler, make_optimizer, train_step
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = UP_Retinex(use_preact=False, use_aspp=False).to(dev).train()
+    crit = TotalLoss(use_freq_loss=True).to(dev)
+    opt = make_optimizer(model, lr=1e-4, weight_decay=1e-5)
+    scaler = GradScaler()
+    x = torch.rand(8, 3, 512, 512, device=dev)
+
+    def step():
+        return train_step(model, x, crit, opt, scaler=scaler, use_amp=True)
+
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    steps = 3
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / steps
+    prox = _Timed(L.lib())
+    L._lib = prox
+    pr = cProfile.Profile()
+    t0 = time.perf_counter()
+    pr.enable()
+    for _ in range(steps):
+        step()
+    pr.disable()
+    host = (time.perf_counter() - t0) / steps
+    torch.cuda.synchronize()
+    L._lib = prox._lib
+    abi = sum(prox.t.values()) / steps
+    print(f"step wall {wall * 1e3:.2f} ms; profiled host loop {host * 1e3:.2f} ms/step, "
+          f"of which C-ABI calls {abi * 1e3:.2f} ms ({sum(prox.n.values()) // steps} calls/step)")
+    for k, v in prox.t.most_common(25):
+        print(f"  {v / steps * 1e3:8.3f} ms {prox.n[k] // steps:5d} calls  {k}")
+    st = pstats.Stats(pr)
+    st.sort_stats("tottime").print_stats(30)
+
+
+if __name__ == "__main__":
+    main()
