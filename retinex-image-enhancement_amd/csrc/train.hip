@@ -849,6 +849,35 @@ __global__ __launch_bounds__(256) void bn_apply4_kernel(const float* __restrict_
                                                         int res_coff, int res_post, int relu, float* y, int y_cs,
                                                         int y_coff, half_t* __restrict__ y16) {
   const int C4 = C / 4;
+  if (256 % C4 == 0) {
+    // this thread's 4 channels are fixed (the grid stride is a multiple of C4):
+    // per-channel parameters once, row index by addition -- no div / mod per
+    // element (the 64-bit form ran at ~3 TB/s); 32-bit offsets (host-checked)
+    const int c = (threadIdx.x % C4) * 4, rpb = 256 / C4;
+    float mu[4], is[4], ga[4], be[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { mu[e] = mean[c + e]; is[e] = invstd[c + e]; ga[e] = gamma[c + e]; be[e] = beta[c + e]; }
+    for (int m = blockIdx.x * rpb + threadIdx.x / C4; m < M; m += gridDim.x * rpb) {
+      const float4 xv = *(const float4*)(x + (size_t)m * x_cs + x_coff + c);
+      const float4 rv4 = res ? *(const float4*)(res + (size_t)m * res_cs + res_coff + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float xa[4] = {xv.x, xv.y, xv.z, xv.w}, ra[4] = {rv4.x, rv4.y, rv4.z, rv4.w};
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = bn_affine(xa[e], mu[e], is[e], ga[e], be[e]);
+        if (!res_post) v += ra[e];
+        if (relu) v = fmaxf(v, 0.f);
+        if (res_post) v += ra[e];
+        o[e] = v;
+      }
+      *(float4*)(y + (size_t)m * y_cs + y_coff + c) = make_float4(o[0], o[1], o[2], o[3]);
+      if (y16) {
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        *(h4*)(y16 + (size_t)m * C + c) = h4{(half_t)o[0], (half_t)o[1], (half_t)o[2], (half_t)o[3]};
+      }
+    }
+    return;
+  }
   const long long n = (long long)M * C4;
   GSTRIDE(i, n) {
     const int c = (int)(i % C4) * 4;
@@ -923,6 +952,46 @@ __global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(const float* __restr
     }
   }
   const int C4 = C / 4;
+  if (256 % C4 == 0) {
+    // fixed channels per thread (see bn_apply4_kernel): the per-channel terms,
+    // fp64 divides included, once per thread instead of per element
+    const int c = (threadIdx.x % C4) * 4, rpb = 256 / C4;
+    float mu[4], is[4], ga[4], be[4], sg[4], sgx[4], gis[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      mu[e] = mean[c + e];
+      is[e] = invstd[c + e];
+      ga[e] = gamma[c + e];
+      be[e] = relu ? beta[c + e] : 0.f;
+      sg[e] = batch_stats ? (float)(acc[c + e] / M) : 0.f;
+      sgx[e] = batch_stats ? (float)(acc[C + c + e] / M) : 0.f;
+      gis[e] = ga[e] * is[e];
+    }
+    for (int m = blockIdx.x * rpb + threadIdx.x / C4; m < M; m += gridDim.x * rpb) {
+      const float4 gv = *(const float4*)(g + (size_t)m * g_cs + g_coff + c);
+      const float4 xv = *(const float4*)(x + (size_t)m * x_cs + x_coff + c);
+      const float ga4[4] = {gv.x, gv.y, gv.z, gv.w}, xa[4] = {xv.x, xv.y, xv.z, xv.w};
+      float4* o = (float4*)(dx + (size_t)m * dx_cs + dx_coff + c);
+      const float4 prev = accum ? *o : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float pa[4] = {prev.x, prev.y, prev.z, prev.w};
+      float r[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float xh = (xa[e] - mu[e]) * is[e];
+        float gg = ga4[e];
+        if (relu && !(bn_affine(xa[e], mu[e], is[e], ga[e], be[e]) > 0.f)) gg = 0.f;
+        float v = gis[e] * (gg - sg[e] - xh * sgx[e]);
+        if (accum) v += pa[e];
+        r[e] = v;
+      }
+      *o = make_float4(r[0], r[1], r[2], r[3]);
+      if (dx16) {
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        *(h4*)(dx16 + (size_t)m * C + c) = h4{(half_t)r[0], (half_t)r[1], (half_t)r[2], (half_t)r[3]};
+      }
+    }
+    return;
+  }
   const long long n = (long long)M * C4;
   GSTRIDE(i, n) {
     const int c = (int)(i % C4) * 4;
@@ -960,6 +1029,20 @@ __global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(const float* __restr
 __global__ __launch_bounds__(256) void relu_mask4_kernel(float* g, int g_cs, int g_coff, const float* __restrict__ y,
                                                          int y_cs, int y_coff, int M, int C) {
   const int C4 = C / 4;
+  if (256 % C4 == 0) {  // fixed channels per thread (see bn_apply4_kernel)
+    const int c = (threadIdx.x % C4) * 4, rpb = 256 / C4;
+    for (int m = blockIdx.x * rpb + threadIdx.x / C4; m < M; m += gridDim.x * rpb) {
+      const float4 yv = *(const float4*)(y + (size_t)m * y_cs + y_coff + c);
+      float4* gp = (float4*)(g + (size_t)m * g_cs + g_coff + c);
+      float4 gv = *gp;
+      if (!(yv.x > 0.f)) gv.x = 0.f;
+      if (!(yv.y > 0.f)) gv.y = 0.f;
+      if (!(yv.z > 0.f)) gv.z = 0.f;
+      if (!(yv.w > 0.f)) gv.w = 0.f;
+      *gp = gv;
+    }
+    return;
+  }
   const long long n = (long long)M * C4;
   GSTRIDE(i, n) {
     const int c = (int)(i % C4) * 4;
@@ -1556,13 +1639,20 @@ __global__ __launch_bounds__(256) void fam_ca_bwd32_kernel(const float* __restri
   }
 }
 
-__global__ void fam_ca_fin_kernel(const float* __restrict__ part, int chunks, int n, float* __restrict__ g_ca) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;  // j = b * 32 + c
-  if (j >= n) return;
+__global__ __launch_bounds__(256) void fam_ca_fin_kernel(const float* __restrict__ part, int chunks, int n,
+                                                         float* __restrict__ g_ca) {
+  __shared__ float red[256];
+  const int j = blockIdx.x;  // j = b * 32 + c: one block per output, fixed-order tree
   const int b = j >> 5, c = j & 31;
   float t = 0.f;
-  for (int k = 0; k < chunks; ++k) t += part[((size_t)b * chunks + k) * 32 + c];
-  g_ca[j] = t;
+  for (int k = threadIdx.x; k < chunks; k += 256) t += part[((size_t)b * chunks + k) * 32 + c];
+  red[threadIdx.x] = t;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) g_ca[j] = red[0];
 }
 
 __global__ void fam_pool_bwd_kernel(float* g_o, const float* __restrict__ g_pool, const float* __restrict__ o, int B,
@@ -2273,12 +2363,22 @@ int upr_t_conv_mfma(const float* x, int B, int H, int W, int Cin, int x_cs, int 
 __global__ __launch_bounds__(256) void cast_act_f16_kernel(const float* __restrict__ x, long long M, int C, int cs,
                                                            int coff, half_t* __restrict__ y) {
   const int C8 = C / 8;
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  if (256 % C8 == 0) {  // fixed channels per thread, rows by addition (no 64-bit div per element)
+    const int c = (threadIdx.x % C8) * 8, rpb = 256 / C8;
+    for (long long m = (long long)blockIdx.x * rpb + threadIdx.x / C8; m < M; m += (long long)gridDim.x * rpb) {
+      const float4* src = (const float4*)(x + m * cs + coff + c);
+      const float4 a = src[0], b = src[1];
+      *(h8*)(y + m * C + c) =
+          h8{(half_t)a.x, (half_t)a.y, (half_t)a.z, (half_t)a.w, (half_t)b.x, (half_t)b.y, (half_t)b.z, (half_t)b.w};
+    }
+    return;
+  }
   GSTRIDE(i, M * C8) {
     const long long m = i / C8;
     const int c = (int)(i - m * C8) * 8;
     const float4* src = (const float4*)(x + m * cs + coff + c);
     const float4 a = src[0], b = src[1];
-    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
     h8 o = {(half_t)a.x, (half_t)a.y, (half_t)a.z, (half_t)a.w, (half_t)b.x, (half_t)b.y, (half_t)b.z, (half_t)b.w};
     *(h8*)(y + m * C + c) = o;
   }
@@ -3150,8 +3250,7 @@ int upr_t_fam_ca_bwd(const float* g_o2, const float* g_m, const float* o, const 
     part = (float*)scratch(kSlotPart, sizeof(float) * 32 * B * chunks, st);
     if (!part) return (int)hipErrorOutOfMemory;
     hipLaunchKernelGGL(fam_ca_bwd32_kernel, dim3(chunks, B), dim3(256), 0, st, g_o2, g_m, o, o2, ca, HW, g_o, part);
-    hipLaunchKernelGGL(fam_ca_fin_kernel, dim3((B * 32 + 255) / 256), dim3(256), 0, st, (const float*)part, chunks,
-                       B * 32, g_ca);
+    hipLaunchKernelGGL(fam_ca_fin_kernel, dim3(B * 32), dim3(256), 0, st, (const float*)part, chunks, B * 32, g_ca);
     UPR_CHECK_HIP(hipGetLastError());
     return UPR_OK;
   }

@@ -16,8 +16,8 @@
 //   * weight gradient (Cout <= 32): a GEMM over pixels on
 //     v_mfma_f32_32x32x2_f32 (D[co][k] += dy[p][co] * im2col[p][k], two
 //     pixels per MFMA, k = ci*kh*kw + ky*kw + kx = PyTorch's weight layout,
-//     plus a ones column for the bias), per-block LDS reduction, one atomic
-//     per weight per block.
+//     plus a ones column for the bias), per-block LDS reduction into a
+//     partial row per block, summed in block order by a second kernel.
 // All fp32 (exact-fp32 MFMA); only the summation order differs from a serial
 // loop.
 #include <cstdlib>
@@ -281,16 +281,14 @@ __global__ __launch_bounds__(256) void small_dgrad_kernel(SV dy, int Ho, int Wo,
 // weight gradient, Cout <= 32: D[co][k] = sum_p dy[p][co] * col[p][k] on
 // v_mfma_f32_32x32x2_f32 (A = dy rows, B = im2col rows, K = 2 pixels)
 // ---------------------------------------------------------------------------
-// pixel pairs in flight per wave: ~32 im2col loads per lane whatever NT (the
-// kernel is latency-bound: 8 pairs left the memory pipe mostly idle)
+// pixel pairs in flight per wave
 template <int NT>
-constexpr int sw_unroll() { return NT == 1 ? 32 : NT == 2 ? 16 : 8; }
+constexpr int sw_unroll() { return NT == 2 ? 16 : 8; }
 
 template <int NT>
 __global__ __launch_bounds__(256) void small_wgrad_mfma_kernel(SV x, SV dy, int B, int H, int W, int Cin, int Ho,
                                                                int Wo, int Cout, int kh, int kw, int s, int p, int d,
-                                                               int pairs_per_wave, float* __restrict__ dw,
-                                                               float* __restrict__ dbias) {
+                                                               int pairs_per_wave, float* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) float red[4][NT][16][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int j = lane & 31, half = lane >> 5;
@@ -310,7 +308,7 @@ __global__ __launch_bounds__(256) void small_wgrad_mfma_kernel(SV x, SV dy, int 
       c_off[t] = ci;
       c_dy[t] = ky * d - p;
       c_dx[t] = kx * d - p;
-    } else if (k == KC && dbias) {
+    } else if (k == KC) {  // the bias column (kept only when the layer has a bias)
       c_kind[t] = 2;
     }
   }
@@ -353,7 +351,10 @@ __global__ __launch_bounds__(256) void small_wgrad_mfma_kernel(SV x, SV dy, int 
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u][t], acc[t], 0, 0, 0);
   }
-  // block reduction over the 4 waves, then one atomic per (co, k)
+  // block reduction over the 4 waves into this block's partial row
+  // part[block][co * (KC + 1) + k] (k == KC: the bias column); summed over the
+  // blocks in order by small_wgrad_fin_kernel -- deterministic, and no
+  // same-address atomics (which serialised ~1000 blocks per weight)
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -367,9 +368,33 @@ __global__ __launch_bounds__(256) void small_wgrad_mfma_kernel(SV x, SV dy, int 
     // 32x32 accumulator map: column = l & 31, row = (e & 3) + 8 * (e >> 2) + 4 * (l >> 5)
     const int co = (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
     const int k = t * 32 + (l & 31);
-    if (co >= Cout) continue;
-    if (k < KC) atomicAdd(dw + (size_t)co * KC + k, v);
-    else if (k == KC && dbias) atomicAdd(dbias + co, v);
+    if (co >= Cout || k > KC) continue;
+    part[((size_t)blockIdx.x * Cout + co) * (KC + 1) + k] = v;
+  }
+}
+
+// dw[co][k] += sum over blocks of part[block][co][k]; the bias column into
+// dbias.  One block per output: thread t adds blocks t, t + 256, ... in order,
+// then a fixed LDS tree -- deterministic, and no long serial load chain
+__global__ __launch_bounds__(256) void small_wgrad_fin_kernel(const float* __restrict__ part, int blocks, int Cout,
+                                                              int KC, float* __restrict__ dw,
+                                                              float* __restrict__ dbias) {
+  __shared__ float red[256];
+  const int i = blockIdx.x;  // co * (KC + 1) + k
+  const int n = Cout * (KC + 1);
+  const int co = i / (KC + 1), k = i - co * (KC + 1);
+  if (k == KC && !dbias) return;
+  float t = 0.f;
+  for (int b = threadIdx.x; b < blocks; b += 256) t += part[(size_t)b * n + i];
+  red[threadIdx.x] = t;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (k < KC) dw[(size_t)co * KC + k] += red[0];
+    else dbias[co] += red[0];
   }
 }
 
@@ -557,15 +582,18 @@ int small_conv_wgrad(const UprView* xv, const UprView* dyv, int B, int H, int W,
   const long long pairs = (P + 1) / 2;
   // ~4096 waves (16 per CU), pairs per wave a multiple of the unroll
   long long ppw = (pairs + 4095) / 4096;
-  const int unroll = nt == 1 ? sw_unroll<1>() : nt == 2 ? sw_unroll<2>() : sw_unroll<4>();
+  const int unroll = nt == 2 ? sw_unroll<2>() : sw_unroll<1>();
   ppw = (ppw + unroll - 1) / unroll * unroll;
   if (ppw < unroll) ppw = unroll;
   const long long waves = (pairs + ppw - 1) / ppw;
   const int grid = (int)((waves + 3) / 4);
   const SV x = mksv(xv), dy = mksv(dyv);
+  const int KC0 = Cin * kh * kw;
+  float* part = (float*)scratch(kSlotPart, sizeof(float) * (size_t)grid * Cout * (KC0 + 1), st);
+  if (!part) return (int)hipErrorOutOfMemory;
 #define UPR_SMALL_WGRAD(T)                                                                                          \
   hipLaunchKernelGGL(small_wgrad_mfma_kernel<T>, dim3(grid), dim3(256), 0, st, x, dy, B, H, W, Cin, Ho, Wo, Cout, kh, \
-                     kw, stride, pad, dil, (int)ppw, dw, dbias)
+                     kw, stride, pad, dil, (int)ppw, part)
   switch (nt) {
     case 1: UPR_SMALL_WGRAD(1); break;
     case 2: UPR_SMALL_WGRAD(2); break;
@@ -573,6 +601,9 @@ int small_conv_wgrad(const UprView* xv, const UprView* dyv, int B, int H, int W,
     default: UPR_SMALL_WGRAD(4); break;
   }
 #undef UPR_SMALL_WGRAD
+  const int nf = Cout * (KC0 + 1);
+  hipLaunchKernelGGL(small_wgrad_fin_kernel, dim3(nf), dim3(256), 0, st, (const float*)part, grid, Cout, KC0, dw,
+                     dbias);
   return (int)hipGetLastError();
 }
 
