@@ -9,9 +9,9 @@ if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${CK:-ck}/smoke.log 2>&1 || exit $?
 timeout -k 10 400 python bench.py > gpurun_out/${CK:-ck}/bench_default.json 2> gpurun_out/${CK:-ck}/bench_default.err || exit $?
 cat gpurun_out/${CK:-ck}/bench_default.json
-timeout -k 10 400 python bench.py --precision fp16 --variant preact_aspp --ceilings > gpurun_out/${CK:-ck}/bench_fp16.json 2> gpurun_out/${CK:-ck}/bench_fp16.err || exit $?
+timeout -k 10 400 python bench.py --precision fp16 --variant preact_aspp --ceilings --no-nested > gpurun_out/${CK:-ck}/bench_fp16.json 2> gpurun_out/${CK:-ck}/bench_fp16.err || exit $?
 cat gpurun_out/${CK:-ck}/bench_fp16.json
-timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/${CK:-ck}/prof -o p --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-traffic --cpu-seconds 0 > gpurun_out/${CK:-ck}/bench_prof.json 2>&1 || exit $?
-timeout -k 10 300 python bench.py --train --amp --steps 5 --warmup 2 > gpurun_out/${CK:-ck}/bench_train.json 2> gpurun_out/${CK:-ck}/bench_train.err || exit $?
-timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/${CK:-ck}/prof16 -o p --output-format csv -- python3 bench.py --precision fp16 --variant preact_aspp --steps 20 --warmup 3 --no-traffic --cpu-seconds 0 > gpurun_out/${CK:-ck}/bench_prof16.json 2>&1 || exit $?
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/${CK:-ck}/prof -o p --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-traffic --cpu-seconds 0 --no-nested > gpurun_out/${CK:-ck}/bench_prof.json 2>&1 || exit $?
+timeout -k 10 300 python bench.py --train --amp --steps 5 --warmup 2 --no-nested > gpurun_out/${CK:-ck}/bench_train.json 2> gpurun_out/${CK:-ck}/bench_train.err || exit $?
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/${CK:-ck}/prof16 -o p --output-format csv -- python3 bench.py --precision fp16 --variant preact_aspp --steps 20 --warmup 3 --no-traffic --cpu-seconds 0 --no-nested > gpurun_out/${CK:-ck}/bench_prof16.json 2>&1 || exit $?
 exit $rc
