@@ -108,13 +108,25 @@ int upr_t_conv_wgrad(const float* x, int B, int H, int W, int Cin, int x_cs, int
 int upr_t_conv_wgrad16(const float* x, const void* x16, int B, int H, int W, int Cin, int x_cs, int x_coff,
                        const float* dy, int Ho, int Wo, int Cout, int dy_cs, int dy_coff, int kh, int kw, int stride,
                        int pad, int dil, float* dwp, void* stream);
+/* Stride-1 input gradient on fp16 MFMA (x16 = the fp16 output gradient, wp16
+ * = the flipped weights of upr_t_pack_weight mode 1 in fp16) with the ReLU
+ * backward of the activation it flows into fused: y (fp32, skipped when
+ * skip32) and y16 (compact fp16, y16_cs) are zero where mask16[pix *
+ * mask16_cs + n] <= 0 (mask16 = that activation's fp16 copy).  No bias,
+ * residual or accumulation.  UPR_ERR_UNSUPPORTED when no out32 kernel takes
+ * the shape (nothing launched: run upr_t_conv_mfma16 + upr_t_relu_mask16). */
+int upr_t_conv_mfma16_relu_bwd(const void* x16, int B, int H, int W, int Cin, const void* wp16, int N, int kh, int kw,
+                               int pad, int dil, float* y, int y_cs, int y_coff, void* y16, int y16_cs,
+                               const void* mask16, int mask16_cs, int skip32, void* stream);
 /* The weight gradient added straight into PyTorch's layout: dw[co][ci][ky][kx]
  * += (no packed buffer, zero fill or unpack pass).  x16 non-NULL: the AMP
  * arithmetic of upr_t_conv_wgrad16 (x may then be NULL when the fp16 path
- * takes the shape); else the fp32 upr_t_conv_wgrad.  dw needs no alignment. */
+ * takes the shape); else the fp32 upr_t_conv_wgrad.  dy16 (nullable, AMP
+ * only): dy's compact [pixel][Cout] fp16 copy = (half)dy, read instead of dy
+ * (the same operand values, half the bytes).  dw needs no alignment. */
 int upr_t_conv_wgrad_into(const float* x, const void* x16, int B, int H, int W, int Cin, int x_cs, int x_coff,
-                          const float* dy, int Ho, int Wo, int Cout, int dy_cs, int dy_coff, int kh, int kw,
-                          int stride, int pad, int dil, float* dw, void* stream);
+                          const float* dy, const void* dy16, int Ho, int Wo, int Cout, int dy_cs, int dy_coff, int kh,
+                          int kw, int stride, int pad, int dil, float* dw, void* stream);
 /* Weight layout transforms.  mode 0: [Co][Ci][kh][kw] -> [Co][(ky,kx,ci)];
  * mode 1: -> [Ci][(ky,kx,co)] spatially flipped (stride-1 dgrad as a conv);
  * mode 2: ConvTranspose [Ci][Co][2][2] -> [(a,b,co)][ci] (forward GEMM);

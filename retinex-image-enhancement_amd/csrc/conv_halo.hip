@@ -677,7 +677,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
           for (int e = 0; e < EPC; e += 4) {
             f32x4_h w4 = {hto_f(ov[e]), hto_f(ov[e + 1]), hto_f(ov[e + 2]), hto_f(ov[e + 3])};
             if (r32) w4 += *(const f32x4_h*)(r32 + e);
-            *(f32x4_h*)(d32 + e) = w4;
+            if (op.mask16) {
+              typedef _Float16 h4m __attribute__((ext_vector_type(4)));
+              const h4m mk = *(const h4m*)((const half_t*)op.mask16 + m * op.mask16_cs + n0 + nb0 + e);
+#pragma unroll
+              for (int q = 0; q < 4; ++q) w4[q] = (float)mk[q] > 0.f ? w4[q] : 0.f;
+            }
+            if (!op.skip32) *(f32x4_h*)(d32 + e) = w4;
             if (op.out32_h16) {
               typedef _Float16 h4h __attribute__((ext_vector_type(4)));
               *(h4h*)((half_t*)op.out32_h16 + m * op.out32_h16_cs + n0 + nb0 + e) =

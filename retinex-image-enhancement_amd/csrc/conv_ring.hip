@@ -683,13 +683,21 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, RingCfg<MODE, C, NB, FL
               if (ovalid[g]) pool[nt][i] += (float)o[i];
           }
           if constexpr (K::OUT32) {
+            if (op.mask16 && ovalid[g]) {
+              const half_t* mk = (const half_t*)op.mask16 + prow * op.mask16_cs +
+                                 (size_t)((g0 + g) * 16 + fr) * op.mask16_cs + fg * 4 + nt * 16;
+              const uint2 mw = *(const uint2*)mk;
+              const f16x4_r mv = __builtin_bit_cast(f16x4_r, mw);
+#pragma unroll
+              for (int i = 0; i < 4; ++i) o[i] = (float)mv[i] > 0.f ? o[i] : (half_t)0.f;
+            }
             f32x4_r o32;
 #pragma unroll
             for (int i = 0; i < 4; ++i) o32[i] = (float)o[i];
             float* d32 = ovalid[g] ? op.out32 + prow * op.out32_cs + op.out32_coff +
                                          (size_t)((g0 + g) * 16 + fr) * op.out32_cs + fg * 4
                                    : g_ring_sink32 + tid * 64;
-            *(f32x4_r*)(d32 + nt * 16) = o32;
+            if (!op.skip32) *(f32x4_r*)(d32 + nt * 16) = o32;
             if (op.out32_h16) {  // compact fp16 copy: o itself (no res32 on the ring)
               half_t* d16 = ovalid[g] ? (half_t*)op.out32_h16 + prow * op.out32_h16_cs +
                                             (size_t)((g0 + g) * 16 + fr) * op.out32_h16_cs + fg * 4

@@ -292,7 +292,13 @@ __device__ __forceinline__ void wide_epilogue(const ConvOp& op, f32x4_w (&acc)[W
 #pragma unroll
             for (int e = 0; e < 4; ++e) t[e] = (float)o[hh * 4 + e];
             if (op.res32) t += *(const f32x4_w*)(op.res32 + pix * op.res32_cs + ch + hh * 4);
-            *(f32x4_w*)(d32 + hh * 4) = t;
+            if (op.mask16) {
+              typedef _Float16 h4m __attribute__((ext_vector_type(4)));
+              const h4m mk = *(const h4m*)((const half_t*)op.mask16 + pix * op.mask16_cs + ch + hh * 4);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) t[e] = (float)mk[e] > 0.f ? t[e] : 0.f;
+            }
+            if (!op.skip32) *(f32x4_w*)(d32 + hh * 4) = t;
             if (op.out32_h16) {
               typedef _Float16 h4w __attribute__((ext_vector_type(4)));
               *(h4w*)((half_t*)op.out32_h16 + pix * op.out32_h16_cs + ch + hh * 4) =

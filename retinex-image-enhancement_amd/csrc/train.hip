@@ -87,7 +87,7 @@ int wgrad_gemm(const float* x, int B, int H, int W, int Cin, int x_cs, int x_cof
                hipStream_t st, int torch_ci = 0);
 int wgrad16_gemm(const void* x16, int B, int H, int W, int Cin, const float* dy, int Ho, int Wo, int Cout, int dy_cs,
                  int dy_coff, int kh, int kw, int stride, int pad, int dil, float* dwp, hipStream_t st,
-                 int torch_ci = 0);
+                 int torch_ci = 0, const void* dy16 = nullptr);
 static bool wgrad_gemm_on() {
   static int on = -1;
   if (on < 0) {
@@ -2478,6 +2478,35 @@ int upr_t_conv_mfma16(const float* x, int B, int H, int W, int Cin, int x_cs, in
   LAUNCH_CHECK();
 }
 
+int upr_t_conv_mfma16_relu_bwd(const void* x16, int B, int H, int W, int Cin, const void* wp16, int N, int kh, int kw,
+                               int pad, int dil, float* y, int y_cs, int y_coff, void* y16, int y16_cs,
+                               const void* mask16, int mask16_cs, int skip32, void* stream) {
+  if (!x16 || !wp16 || !y || !y16 || !mask16 || B <= 0 || Cin % 32 || N % 32 || Cin <= 0 || N <= 0) return UPR_ERR_ARG;
+  if (kh <= 0 || kw <= 0 || dil <= 0 || pad < 0) return UPR_ERR_ARG;
+  if (((uintptr_t)x16 | (uintptr_t)y16 | (uintptr_t)mask16) % 16 || y16_cs % 8 || mask16_cs % 8 || y_cs % 4 ||
+      y_coff % 4 || (uintptr_t)y % 16)
+    return UPR_ERR_UNSUPPORTED;
+  if (!out32_on()) return UPR_ERR_UNSUPPORTED;
+  const int Ho = H + 2 * pad - dil * (kh - 1), Wo = W + 2 * pad - dil * (kw - 1);
+  if (Ho <= 0 || Wo <= 0) return UPR_ERR_SHAPE;
+  ConvOp c;
+  memset(&c, 0, sizeof(c));
+  c.nseg = 1;
+  ConvSeg& sg = c.seg[0];
+  sg.src = x16; sg.C = Cin; sg.cs = Cin; sg.coff = 0; sg.Hin = H; sg.Win = W;
+  sg.kh = kh; sg.kw = kw; sg.stride = 1; sg.pad = pad; sg.dil = dil; sg.pre = kPreNone; sg.kbase = 0;
+  c.B = B; c.Ho = Ho; c.Wo = Wo; c.N = N; c.Kpad = kh * kw * Cin;
+  c.W = wp16; c.bias = nullptr; c.relu = 0;
+  c.store = kStoreNHWC;
+  c.out32 = y; c.out32_cs = y_cs; c.out32_coff = y_coff;
+  c.out32_h16 = y16; c.out32_h16_cs = y16_cs;
+  c.mask16 = mask16; c.mask16_cs = mask16_cs; c.skip32 = skip32 ? 1 : 0;
+  const int rc = launch_conv_out32(c, ST(stream));
+  if (rc == kErrUnsupported) return UPR_ERR_UNSUPPORTED;
+  if (rc != 0) return rc;
+  LAUNCH_CHECK();
+}
+
 int upr_t_conv_wgrad(const float* x, int B, int H, int W, int Cin, int x_cs, int x_coff, const float* dy, int Ho,
                      int Wo, int Cout, int dy_cs, int dy_coff, int kh, int kw, int stride, int pad, int dil,
                      float* dwp, void* stream) {
@@ -2523,13 +2552,13 @@ int upr_t_conv_wgrad16(const float* x, const void* x16, int B, int H, int W, int
 }
 
 int upr_t_conv_wgrad_into(const float* x, const void* x16, int B, int H, int W, int Cin, int x_cs, int x_coff,
-                          const float* dy, int Ho, int Wo, int Cout, int dy_cs, int dy_coff, int kh, int kw,
-                          int stride, int pad, int dil, float* dw, void* stream) {
+                          const float* dy, const void* dy16, int Ho, int Wo, int Cout, int dy_cs, int dy_coff, int kh,
+                          int kw, int stride, int pad, int dil, float* dw, void* stream) {
   if ((!x && !x16) || !dy || !dw || B <= 0 || Cin % 32 || Cout % 32 || Cin <= 0 || Cout <= 0) return UPR_ERR_ARG;
   hipStream_t st = ST(stream);
   if (x16) {
     const int rc = wgrad16_gemm(x16, B, H, W, Cin, dy, Ho, Wo, Cout, dy_cs, dy_coff, kh, kw, stride, pad, dil, dw, st,
-                                Cin);
+                                Cin, dy16);
     if (rc != kErrUnsupported) return rc;
   }
   if (!x) return UPR_ERR_ARG;

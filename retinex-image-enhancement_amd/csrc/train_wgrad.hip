@@ -258,6 +258,7 @@ struct Wg16Args {
   const half_t* x16;   // [B][H][W][Cin] fp16
   int B, H, W, Cin;
   const float* dy;
+  const half_t* dy16;  // nullable: dy's compact [pixel][Cout] fp16 copy (its producer's), read instead of dy
   int Ho, Wo, Cout, dy_cs, dy_coff;
   int kh, kw, s, p, d;
   int KT, nruns;       // kh*kw*Cin, KT / 32
@@ -304,10 +305,22 @@ __global__ __launch_bounds__(256) void wgrad16_kernel(Wg16Args a) {
   // A staging: chunk i of this thread = pixel tid / NQA + i * (256 / NQA), quad tid % NQA
   const int qa = tid % NQA;
   f32x4_w2 areg[AC];
+  f16x4_w2 hreg[AC];
+  const bool a16 = a.dy16 != nullptr;  // uniform
   auto load_a = [&](int u) {
     const int b = u / (a.Ho * segs), r = u - b * a.Ho * segs;
     const int oy = r / segs, ox0 = (r - oy * segs) * W16_KP;
-    const float* base = a.dy + ((size_t)(b * a.Ho + oy) * a.Wo + ox0) * a.dy_cs + a.dy_coff + co0 + qa * 4;
+    const size_t pix0 = (size_t)(b * a.Ho + oy) * a.Wo + ox0;
+    if (a16) {  // the fp16 copy: half the bytes, the same RNE-rounded values
+      const half_t* base = a.dy16 + pix0 * a.Cout + co0 + qa * 4;
+#pragma unroll
+      for (int i = 0; i < AC; ++i) {
+        const int pr = tid / NQA + i * (256 / NQA);
+        hreg[i] = *(const f16x4_w2*)(base + (size_t)pr * a.Cout);
+      }
+      return;
+    }
+    const float* base = a.dy + pix0 * a.dy_cs + a.dy_coff + co0 + qa * 4;
 #pragma unroll
     for (int i = 0; i < AC; ++i) {
       const int pr = tid / NQA + i * (256 / NQA);
@@ -319,8 +332,12 @@ __global__ __launch_bounds__(256) void wgrad16_kernel(Wg16Args a) {
     for (int i = 0; i < AC; ++i) {
       const int pr = tid / NQA + i * (256 / NQA);
       f16x4_w2 h;
+      if (a16) {
+        h = hreg[i];
+      } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) h[e] = (half_t)areg[i][e];
+        for (int e = 0; e < 4; ++e) h[e] = (half_t)areg[i][e];
+      }
       *(f16x4_w2*)(As + pr * BM * 2 + ((qa ^ w16_swz<NQA>(pr)) * 8)) = h;
     }
   };
@@ -485,7 +502,8 @@ static int wgrad16_nr(const Wg16Args& a, float* dwp, hipStream_t st, int torch_c
 // AMP entry (upr_t_conv_wgrad16): x16 = the compact fp16 copy of x ([B][H][W][Cin]);
 // kErrUnsupported when the shape does not fit (the caller falls back to fp32)
 int wgrad16_gemm(const void* x16, int B, int H, int W, int Cin, const float* dy, int Ho, int Wo, int Cout, int dy_cs,
-                 int dy_coff, int kh, int kw, int stride, int pad, int dil, float* dwp, hipStream_t st, int torch_ci) {
+                 int dy_coff, int kh, int kw, int stride, int pad, int dil, float* dwp, hipStream_t st, int torch_ci,
+                 const void* dy16) {
   if (Wo % W16_KP || Cin % 32 || Cout % 32 || dy_cs % 4 || dy_coff % 4 || ((uintptr_t)dy % 16) ||
       ((uintptr_t)x16 % 16) || (!torch_ci && ((uintptr_t)dwp % 16)))
     return kErrUnsupported;
@@ -495,6 +513,7 @@ int wgrad16_gemm(const void* x16, int B, int H, int W, int Cin, const float* dy,
   memset(&a, 0, sizeof(a));
   a.x16 = (const half_t*)x16; a.B = B; a.H = H; a.W = W; a.Cin = Cin;
   a.dy = dy; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout; a.dy_cs = dy_cs; a.dy_coff = dy_coff;
+  a.dy16 = ((uintptr_t)dy16 % 8) ? nullptr : (const half_t*)dy16;
   a.kh = kh; a.kw = kw; a.s = stride; a.p = pad; a.d = dil;
   a.KT = kh * kw * Cin;
   a.nruns = a.KT / 32;

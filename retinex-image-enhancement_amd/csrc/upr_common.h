@@ -103,6 +103,11 @@ struct ConvOp {
   // out32_h16[pix * out32_h16_cs + n] = (half)(the fp32 value stored) -- the
   // next autocast conv's operand, so it needs no cast pass of its own
   void* out32_h16; int out32_h16_cs;
+  // with out32 (nullable): both outputs zeroed where mask16[pix * mask16_cs +
+  // n] <= 0 -- the ReLU backward of the activation this input gradient flows
+  // into, fused (mask16 = that activation's fp16 copy); skip32: out32 is not
+  // written, only out32_h16 (a gradient whose one reader takes the fp16 copy)
+  const void* mask16; int mask16_cs; int skip32;
 };
 
 // fp16 convs with an fp32 output (ConvOp::out32): the wide-tile and row-ring

@@ -125,8 +125,10 @@ SIGNATURES.update({
     "upr_t_cast_f16": (_i, [_p, _p, c_size_t, _p]),
     "upr_t_conv_wgrad": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p]),
     "upr_t_conv_wgrad16": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p]),
-    "upr_t_conv_wgrad_into": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p,
-                                   _p]),
+    "upr_t_conv_mfma16_relu_bwd": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p, _i, _i, _p, _i, _p, _i, _i,
+                                        _p]),
+    "upr_t_conv_wgrad_into": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i,
+                                   _p, _p]),
     "upr_t_pack_weight": (_i, [_p, _p, _i, _i, _i, _i, _i, _p]),
     "upr_t_pack_weights": (_i, [_p, _i, _i, _p]),
     "upr_t_unpack_grad": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p]),

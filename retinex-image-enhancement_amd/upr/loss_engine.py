@@ -102,7 +102,9 @@ class VGGPerceptual:
         lib, st = L.lib(), _stream()
         g = None
         level = 2
-        for kind, i, inp, out in reversed(trace):  # i: conv index, or the pool's argmax codes
+        entries = list(reversed(trace))
+        premasked = False  # g already carries its ReLU mask (fused into the producing dgrad)
+        for j, (kind, i, inp, out) in enumerate(entries):  # i: conv index, or the pool's argmax codes
             if kind == "pool":
                 if g is None:
                     g = g_feats[level]
@@ -114,16 +116,26 @@ class VGGPerceptual:
                 _chk(lib.upr_t_maxpool_bwd_code(_p(i), ctypes.byref(g.view()), inp.B, inp.H, inp.W, inp.C, 2, 2, 0,
                                                 out.H, out.W, ctypes.byref(gi.view()), 0, st), "pool_bwd")
                 g = gi
+                premasked = False
             else:
                 c = self.convs[i]
-                # the frozen VGG conv's fp16 dgrad is the masked gradient's only reader
-                want16 = (c.amp and c.mfma) or c.dgrad16_c3
-                relu_mask(g, out, want16=want16, only16=c.frozen and want16)
+                if not premasked:
+                    # the frozen VGG conv's fp16 dgrad is the masked gradient's only reader
+                    want16 = (c.amp and c.mfma) or c.dgrad16_c3
+                    relu_mask(g, out, want16=want16, only16=c.frozen and want16)
                 gi = Act.new(inp.B, inp.H, inp.W, inp.C, inp.t.device)
+                # inp is the previous conv's ReLU output: its mask goes into this dgrad's epilogue
+                nxt = entries[j + 1] if j + 1 < len(entries) else None
+                mask = None
+                if nxt is not None and nxt[0] == "conv" and inp.t16 is not None:
+                    cn = self.convs[nxt[1]]
+                    only16 = cn.frozen and ((cn.amp and cn.mfma) or cn.dgrad16_c3)
+                    mask = (inp.t16, inp.C, only16)
                 if c.mfma:
-                    c.bwd(inp, g, gi)
+                    premasked = bool(c.bwd(inp, g, gi, mask=mask))
                 else:
                     c.bwd(None, g, gi, x_view=(inp.view(), inp.B, inp.H, inp.W))
+                    premasked = False
                 g = gi
         return g
 

@@ -382,10 +382,14 @@ class Conv:
                                        self.Cout, self.kh, self.kw, self.s, self.p, self.d,
                                        ctypes.byref(out.view()), Ho, Wo, int(relu), 0, st), "conv_direct")
 
-    def bwd(self, x, gy, gx=None, x_view=None):
+    def bwd(self, x, gy, gx=None, x_view=None, mask=None):
         """gy: Act gradient of this conv's output (pre-activation).
         Accumulates the weight / bias gradients; gx (Act, nullable) receives
-        the input gradient (overwrite when fresh, else accumulate)."""
+        the input gradient (overwrite when fresh, else accumulate).
+        mask = (a16, cs, only16): the ReLU backward of the activation gx flows
+        into, fused into the input-gradient epilogue (a16 = that activation's
+        fp16 copy, channel stride cs); gx.t16 then holds the masked gradient and
+        gx.t is left stale when only16.  Returns True when the mask was applied."""
         lib, st = L.lib(), _stream()
         if x_view is not None:
             xv, B, H, W = x_view
@@ -402,9 +406,13 @@ class Conv:
                     x16 = getattr(self, "x16", None)
                     # autocast: fp16 operands, fp32 accumulation (trainers/train.py:72); added
                     # straight into weight.grad's layout
+                    # gy's fp16 copy (the fused BN backward's dx16) is the AMP A operand as is
+                    dy16 = gy.t16 if self.amp and gy.t16_grad and gy.coff == 0 and gy.cs == gy.C == self.Cout \
+                        else None
                     _chk(lib.upr_t_conv_wgrad_into(_fp(x.t), _p(x16) if self.amp else None, B, H, W, self.Cin, x.cs,
-                                                   x.coff, _fp(gy.t), Ho, Wo, self.Cout, gy.cs, gy.coff, self.kh,
-                                                   self.kw, self.s, self.p, self.d, _p(gw), st), "conv_wgrad")
+                                                   x.coff, _fp(gy.t), _p(dy16), Ho, Wo, self.Cout, gy.cs, gy.coff,
+                                                   self.kh, self.kw, self.s, self.p, self.d, _p(gw), st),
+                         "conv_wgrad")
                     self.x16 = None
                     if self.bias is not None:
                         chan_sum(gy, self.Cout, self.bias.grad, st)
@@ -421,6 +429,20 @@ class Conv:
             if self.mfma:
                 acc = gx.consume_fresh()
                 src, sH, sW, scs, scoff = gy.t, Ho, Wo, gy.cs, gy.coff
+                src16 = gy.t16 if self.amp and gy.t16_grad and gy.coff == 0 and gy.cs == gy.C == self.Cout else None
+                if mask is not None and self.amp and self.s == 1 and not acc and src16 is not None and \
+                        gx.coff == 0 and gx.cs == gx.C == self.Cin:
+                    a16, mcs, only16 = mask
+                    y16 = _h16(B * H * W * self.Cin, gx.t.device)
+                    rc = lib.upr_t_conv_mfma16_relu_bwd(_p(src16), B, Ho, Wo, self.Cout, _p(self.wt16), self.Cin,
+                                                        self.kh, self.kw, self.d * (self.kh - 1) - self.p, self.d,
+                                                        _fp(gx.t), gx.cs, 0, _p(y16), self.Cin, _p(a16), mcs,
+                                                        int(only16), st)
+                    if rc == 0:
+                        gx.t16, gx.t16_grad, gx.stale32 = y16, True, bool(only16)
+                        return True
+                    if rc != L.UPR_ERR_UNSUPPORTED:
+                        _chk(rc, "conv_mfma16_relu_bwd")
                 # autocast: the fp16 operand comes from gy's producer (gy.t16) or, for
                 # stride 2, straight from an fp16 zero-upsample (no fp32 pass + cast)
                 src16 = gy.t16 if self.amp and gy.t16_grad and gy.coff == 0 and gy.cs == gy.C == self.Cout else None

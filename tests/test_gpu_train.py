@@ -127,8 +127,10 @@ def test_conv_wgrad16_vs_fp64(B, cin, cout, H, W, k, s, p, d):
         flat[0] = 7.0
         base = torch.randn(cout, cin, k, k, generator=torch.Generator().manual_seed(4))
         flat[1:] = base.reshape(-1).to(DEV)
+        dy16 = dyd.half() if use_x16 else None  # the fp16 A operand as its producer would write it
         rc = lib.upr_t_conv_wgrad_into(xd.data_ptr(), x16.data_ptr() if use_x16 else None, B, H, W, cin, cin, 0,
-                                       dyd.data_ptr(), Ho, Wo, cout, cout, 0, k, k, s, p, d, flat.data_ptr() + 4, st)
+                                       dyd.data_ptr(), dy16.data_ptr() if use_x16 else None, Ho, Wo, cout, cout, 0,
+                                       k, k, s, p, d, flat.data_ptr() + 4, st)
         assert rc == 0, rc
         torch.cuda.synchronize()
         assert flat[0].item() == 7.0
@@ -314,6 +316,45 @@ def test_conv_dgrad_c3_16_vs_fp64(B, H, W, cout, acc):
     assert rc == 0, rc
     torch.cuda.synchronize()
     _close(dx.permute(0, 3, 1, 2), ref, 1e-5, "dgrad_c3_16")
+
+
+@pytest.mark.parametrize("cin,cout,H,W,skip32", [(64, 64, 32, 64, 0), (128, 64, 16, 64, 1), (256, 128, 16, 32, 1)])
+def test_conv_mfma16_relu_bwd_vs_fp64(cin, cout, H, W, skip32):
+    """upr_t_conv_mfma16_relu_bwd: the stride-1 input gradient of a 3x3 conv
+    (the VGG shapes) with the ReLU backward of the activation it flows into
+    fused into the epilogue, vs the fp64 input gradient of the fp16 dy and
+    weights masked by (a > 0); fp16 copy == (half) of the fp32 output;
+    skip32 leaves the fp32 buffer untouched."""
+    import ctypes
+    from upr import _lib as L
+    gen = torch.Generator().manual_seed(cin + H)
+    B = 2
+    w = torch.randn(cout, cin, 3, 3, generator=gen) * 0.05
+    dy = torch.randn(B, cout, H, W, generator=gen)
+    a = torch.randn(B, cin, H, W, generator=gen).clamp_min(0)  # a ReLU output: about half zeros
+    ref = torch.nn.grad.conv2d_input((B, cin, H, W), w.half().double(), dy.half().double(), padding=1)
+    ref = (ref * (a > 0)).float().permute(0, 2, 3, 1)
+    lib, st = L.lib(), torch.cuda.current_stream().cuda_stream
+    wd = w.to(DEV)
+    wt = torch.empty(w.numel(), device=DEV)
+    assert lib.upr_t_pack_weight(wd.data_ptr(), wt.data_ptr(), cout, cin, 3, 3, 1, st) == 0
+    wt16 = wt.half()
+    dy16 = dy.permute(0, 2, 3, 1).contiguous().half().to(DEV)
+    a16 = a.permute(0, 2, 3, 1).contiguous().half().to(DEV)
+    y = torch.full((B, H, W, cin), 9.0, device=DEV)
+    y16 = torch.empty(B * H * W * cin, dtype=torch.float16, device=DEV)
+    rc = lib.upr_t_conv_mfma16_relu_bwd(dy16.data_ptr(), B, H, W, cout, wt16.data_ptr(), cin, 3, 3, 1, 1,
+                                        y.data_ptr(), cin, 0, y16.data_ptr(), cin, a16.data_ptr(), cin, skip32, st)
+    assert rc == 0, rc
+    torch.cuda.synchronize()
+    g16 = y16.view(B, H, W, cin).float()
+    _close(g16, ref, 2e-3, "relu_bwd fp16")  # one fp16 rounding of the fp32 result
+    assert torch.all((g16 == 0) | (a16.float() > 0))
+    if skip32:
+        assert torch.all(y == 9.0)
+    else:
+        _close(y, ref, 1e-3, "relu_bwd fp32")
+        assert torch.equal(y.half().float(), g16)
 
 
 def test_fp16_copy_producers():
