@@ -1040,7 +1040,9 @@ __device__ __forceinline__ void static_steps(F&& f, std::integer_sequence<int, S
 // (< 8 pixels x 1024 channels x 2 B), so a 16 KiB zero block
 __device__ __attribute__((aligned(256))) uint4 g_halo_zero[1024];
 
-template <int BN, int W, int NCH>
+// ABL (timing ablations only, UPR_HW4_ABL; results are garbage): bit 0 drops
+// the main loop's DMA (region rows + B stages), bit 1 its LDS fragment reads
+template <int BN, int W, int NCH, int ABL = 0>
 __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
   using HC = Halo3Cfg<BN, W>;
   constexpr int WM = HC::WM, WN = HC::WN, BM = HC::BM, NBS = HC::NBS;
@@ -1196,6 +1198,7 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
   issue_b(NBS - 1, (NBS - 1) / 9, (NBS - 1) % 9);  // B(NBS - 1)
   issue_rows(0, 0);
   rd(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, a0, b0);
+  if constexpr ((ABL & 2) != 0) rd(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{}, a1, b1);
   static_steps(
       [&](auto S_) {
         constexpr int S = decltype(S_)::value;
@@ -1206,7 +1209,7 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
           constexpr int bstep = S + NBS;
           constexpr int bc = bstep / 9 < NCH ? bstep / 9 : NCH - 1;
           constexpr int bt = bstep / 9 < NCH ? bstep % 9 : 8;
-          rd(S_, std::integral_constant<int, 1>{}, a1, b1);
+          if constexpr (!(ABL & 2)) rd(S_, std::integral_constant<int, 1>{}, a1, b1);
           mm(S_, a0, b0);
           // RAW: B(S + 1) and the region rows step S + 1 reads have landed: in
           // flight may stay the previous iteration's region rows (issued two
@@ -1218,12 +1221,14 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
           else
             asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(VB) : "memory");
           __builtin_amdgcn_s_barrier();
-          issue_b(S % NBS, bc, bt);
-          issue_rows(nc, nt);
-          rd(std::integral_constant<int, n>{}, std::integral_constant<int, 0>{}, a0, b0);
+          if constexpr (!(ABL & 1)) {
+            issue_b(S % NBS, bc, bt);
+            issue_rows(nc, nt);
+          }
+          if constexpr (!(ABL & 2)) rd(std::integral_constant<int, n>{}, std::integral_constant<int, 0>{}, a0, b0);
           mm(S_, a1, b1);
         } else {
-          rd(S_, std::integral_constant<int, 1>{}, a1, b1);
+          if constexpr (!(ABL & 2)) rd(S_, std::integral_constant<int, 1>{}, a1, b1);
           mm(S_, a0, b0);
           mm(S_, a1, b1);
         }
@@ -1235,18 +1240,18 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
   wide_epilogue<BN, WM, WN, HC::WAVES_M, BM, true, W>(op, acc, smem, m0, n0, M, HW);
 }
 
-template <int BN, int W, int NCH>
+template <int BN, int W, int NCH, int ABL = 0>
 static int launch_hwide4(const ConvOp& op, hipStream_t st) {
   using HC = Halo3Cfg<BN, W>;
   static bool attr_set = false;
   if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute((const void*)conv_hwide4_kernel<BN, W, NCH>,
+    const hipError_t e = hipFuncSetAttribute((const void*)conv_hwide4_kernel<BN, W, NCH, ABL>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, HC::LDS);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
   const int grid = (op.B * op.Ho * W / HC::BM) * (op.N / BN);
-  hipLaunchKernelGGL((conv_hwide4_kernel<BN, W, NCH>), dim3(grid), dim3(512), HC::LDS, st, op);
+  hipLaunchKernelGGL((conv_hwide4_kernel<BN, W, NCH, ABL>), dim3(grid), dim3(512), HC::LDS, st, op);
   return (int)hipGetLastError();
 }
 
@@ -1259,6 +1264,10 @@ static int launch_hwide34(const ConvOp& op, hipStream_t st) {
     // the graph's shapes: bottleneck (W 64, Cin 256), dec3 (W 128, Cin 128)
     // (W 128 / 2 chunks still spills 40 VGPRs as a straight line: dec3 stays on hwide3)
     if constexpr (W == 64) {
+      static const int abl = env_int("UPR_HW4_ABL", 0);  // timing ablations (garbage results)
+      if (nch == 4 && abl == 1) return launch_hwide4<BN, W, 4, 1>(op, st);
+      if (nch == 4 && abl == 2) return launch_hwide4<BN, W, 4, 2>(op, st);
+      if (nch == 4 && abl == 3) return launch_hwide4<BN, W, 4, 3>(op, st);
       if (nch == 4) return launch_hwide4<BN, W, 4>(op, st);
     }
   }
