@@ -48,10 +48,11 @@ int upr_t_conv_direct(const UprView* x, int B, int H, int W, int Cin, const floa
                       int accumulate, void* stream);
 /* The same forward also writing y16 = (half)y compact [B*Ho*Wo][Cout] (the
  * next autocast conv's operand): the 3 -> 32 / 64 3x3 kernel only, else
- * UPR_ERR_UNSUPPORTED (nothing launched). */
+ * UPR_ERR_UNSUPPORTED (nothing launched).  skip32: y is not written (an
+ * activation whose readers all take y16; accumulate must be 0). */
 int upr_t_conv_direct16(const UprView* x, int B, int H, int W, int Cin, const float* w, const float* bias, int Cout,
                         int kh, int kw, int stride, int pad, int dil, const UprView* y, int Ho, int Wo, int relu,
-                        int accumulate, void* y16, void* stream);
+                        int accumulate, void* y16, int skip32, void* stream);
 /* Input gradient of a 3 -> Cout (32 / 64) 3x3 / stride 1 / pad 1 conv under
  * autocast (VGG-19 conv1_1): dy16 = the fp16 output gradient, compact
  * [B][H][W][Cout]; weights [Cout][3][3][3] fp32, rounded to fp16; fp32
@@ -86,7 +87,9 @@ int upr_t_conv_mfma(const float* x, int B, int H, int W, int Cin, int x_cs, int 
  * exclusive.  store | 2: y16 must afterwards hold (half)y exactly (no res):
  * the next autocast conv reading y can take it as its x16 (x16_ready); without
  * that bit y16 is scratch.  y16_cs: y16's channel stride (0 = compact: N, or
- * N / 4 for store 1), e.g. a channel slice of a concat's fp16 copy. */
+ * N / 4 for store 1), e.g. a channel slice of a concat's fp16 copy.
+ * store | 4 (with | 2): y need not be written (every reader takes y16); the
+ * fp32 store is skipped where the kernel allows it. */
 int upr_t_conv_mfma16(const float* x, int B, int H, int W, int Cin, int x_cs, int x_coff, const void* wp16,
                       const float* bias, int N, int kh, int kw, int stride, int pad, int dil, const float* res,
                       int res_cs, int relu, float* y, int y_cs, int y_coff, int store, void* x16, int x16_ready,
@@ -223,6 +226,10 @@ int upr_t_relu_mask(float* g, int g_cs, int g_coff, const float* y, int y_cs, in
  * UPR_ERR_UNSUPPORTED. */
 int upr_t_relu_mask16(float* g, int g_cs, int g_coff, const float* y, int y_cs, int y_coff, int M, int C, void* g16,
                       int write32, void* stream);
+/* The same with the mask taken from the activation's fp16 copy y16 (channel
+ * stride y16_cs). */
+int upr_t_relu_mask16h(float* g, int g_cs, int g_coff, const void* y16, int y16_cs, int M, int C, void* g16,
+                       int write32, void* stream);
 /* dst (+)= src, any layouts (NCHW <-> NHWC, concat slices). */
 int upr_t_copy(const UprView* src, const UprView* dst, int B, int H, int W, int C, int accumulate, void* stream);
 /* n contiguous elements.  op 0: out = sigmoid(a); op 1: out = a*b*(1-b)
@@ -254,6 +261,11 @@ int upr_t_maxpool_code(const UprView* x, int B, int H, int W, int C, int k, int 
                        int Wo, unsigned char* code, void* y16, void* stream);
 int upr_t_maxpool_bwd_code(const unsigned char* code, const UprView* dy, int B, int H, int W, int C, int k, int s,
                            int p, int Ho, int Wo, const UprView* dx, int accumulate, void* stream);
+/* upr_t_maxpool_code reading the input's compact fp16 copy x16 ([B][H][W][C];
+ * the autocast VGG activations exist in fp16 only): 3x3/1/1 and 2x2/2/0 with
+ * C % 4 == 0, else UPR_ERR_UNSUPPORTED. */
+int upr_t_maxpool16_code(const void* x16, int B, int H, int W, int C, int k, int s, int p, const UprView* y, int Ho,
+                         int Wo, unsigned char* code, void* y16, void* stream);
 /* upr_t_copy / upr_t_bilinear also writing the fp16 copy of the result at
  * dst16[pixel * dst16_cs + c] (dst16 points at the slice's first channel of
  * a [B][H][W][dst16_cs] fp16 concat): 4-channel views only, else

@@ -53,6 +53,14 @@ static bool vec4_view_ok(const UprView* v, int B, int H, int W, int C) {
   return ext < (1LL << 31) && v->sb < (1LL << 31) && v->sh < (1LL << 31) && v->sw < (1LL << 31);
 }
 
+// 4 consecutive channels as floats, from fp32 or an fp16 copy
+__device__ __forceinline__ float4 ld4f(const float* p) { return *(const float4*)p; }
+__device__ __forceinline__ float4 ld4f(const half_t* p) {
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+  const h4 v = *(const h4*)p;
+  return make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
+}
+
 static V4 mkv4(const UprView* u) {
   V4 v;
   v.d = (float*)u->data;
@@ -74,7 +82,7 @@ static inline int grid_for(long long n, int per = 256, int cap = 65536) {
 // train_small.hip: pixel-tiled / MFMA forms of the small-channel convs
 int small_conv_fwd(const UprView* xv, int B, int H, int W, int Cin, const float* w, const float* bias, int Cout,
                    int kh, int kw, int stride, int pad, int dil, const UprView* yv, int Ho, int Wo, int relu,
-                   int accumulate, hipStream_t st, void* y16 = nullptr);
+                   int accumulate, hipStream_t st, void* y16 = nullptr, int skip32 = 0);
 int small_conv_dgrad(const UprView* dyv, int Ho, int Wo, const float* w, int B, int H, int W, int Cin, int Cout,
                      int kh, int kw, int stride, int pad, int dil, const UprView* dxv, int accumulate, hipStream_t st);
 int small_conv_dgrad_c3_16(const void* dy16, int B, int H, int W, const float* w, int Cout, const UprView* dxv,
@@ -1061,13 +1069,16 @@ __global__ __launch_bounds__(256) void relu_mask4_kernel(float* g, int g_cs, int
 // the mask fused with the fp16 copy of the masked gradient (the autocast
 // dgrad operand, trainers/train.py:72): g16[m][c] = half(g masked), g itself
 // rewritten only with write32 (a frozen conv's gradient has no fp32 reader)
-__global__ __launch_bounds__(256) void relu_mask16_kernel(float* g, int g_cs, int g_coff, const float* __restrict__ y,
+// TY = half_t: the mask from the activation's fp16 copy (the autocast VGG
+// activations are fp16 only; (half)y > 0 <=> y > 0 for their fp16-exact values)
+template <typename TY = float>
+__global__ __launch_bounds__(256) void relu_mask16_kernel(float* g, int g_cs, int g_coff, const TY* __restrict__ y,
                                                           int y_cs, int y_coff, int M, int C4,
                                                           half_t* __restrict__ g16, int write32) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= M * C4) return;
   const int c = (i % C4) * 4, m = i / C4;
-  const float4 yv = *(const float4*)(y + (size_t)m * y_cs + y_coff + c);
+  const float4 yv = ld4f(y + (size_t)m * y_cs + y_coff + c);
   float4* gp = (float4*)(g + (size_t)m * g_cs + g_coff + c);
   float4 gv = *gp;
   if (!(yv.x > 0.f)) gv.x = 0.f;
@@ -2288,14 +2299,15 @@ int upr_t_conv_dgrad_c3_16(const void* dy16, int B, int H, int W, const float* w
 
 int upr_t_conv_direct16(const UprView* x, int B, int H, int W, int Cin, const float* w, const float* bias, int Cout,
                         int kh, int kw, int stride, int pad, int dil, const UprView* y, int Ho, int Wo, int relu,
-                        int accumulate, void* y16, void* stream) {
+                        int accumulate, void* y16, int skip32, void* stream) {
   if (!x || !y || !x->data || !y->data || !w || !y16 || B <= 0 || Cin <= 0 || Cout <= 0 || stride <= 0 || dil <= 0)
     return UPR_ERR_ARG;
   if (Ho != (H + 2 * pad - dil * (kh - 1) - 1) / stride + 1 || Wo != (W + 2 * pad - dil * (kw - 1) - 1) / stride + 1)
     return UPR_ERR_SHAPE;
   if (!small_kernels_on()) return UPR_ERR_UNSUPPORTED;
+  if (skip32 && accumulate) return UPR_ERR_ARG;
   const int rc = small_conv_fwd(x, B, H, W, Cin, w, bias, Cout, kh, kw, stride, pad, dil, y, Ho, Wo, relu, accumulate,
-                                ST(stream), y16);
+                                ST(stream), y16, skip32);
   return rc == kErrUnsupported ? UPR_ERR_UNSUPPORTED : rc;
 }
 
@@ -2429,6 +2441,7 @@ int upr_t_conv_mfma16(const float* x, int B, int H, int W, int Cin, int x_cs, in
   if (!x16 || !wp16 || !y || !y16 || B <= 0 || Cin % 32 || N % 32 || Cin <= 0 || N <= 0) return UPR_ERR_ARG;
   if (!x16_ready && !x) return UPR_ERR_ARG;
   const bool want16 = (store & 2) != 0;  // y16 must end up holding (half)y
+  const bool only16 = want16 && (store & 4) != 0;  // y itself not needed (written only on the fallback path)
   store &= 1;
   const int ycs16 = y16_cs > 0 ? y16_cs : (store == 1 ? N / 4 : N);  // y16's channel stride
   if (ycs16 % 8 || ((uintptr_t)y16 & 15)) return UPR_ERR_ARG;
@@ -2462,6 +2475,7 @@ int upr_t_conv_mfma16(const float* x, int B, int H, int W, int Cin, int x_cs, in
     c32.out32 = y; c32.out32_cs = y_cs; c32.out32_coff = y_coff;
     c32.res32 = res; c32.res32_cs = res_cs;
     if (want16) { c32.out32_h16 = y16; c32.out32_h16_cs = ycs16; }
+    c32.skip32 = only16 ? 1 : 0;
     const int rc = launch_conv_out32(c32, st);
     if (rc != kErrUnsupported) {
       if (rc != 0) return rc;
@@ -2780,8 +2794,21 @@ int upr_t_relu_mask16(float* g, int g_cs, int g_coff, const float* y, int y_cs, 
     return UPR_ERR_UNSUPPORTED;
   const int n = M * (C / 4);
   if (n == 0) return UPR_OK;
-  hipLaunchKernelGGL(relu_mask16_kernel, dim3((n + 255) / 256), dim3(256), 0, ST(stream), g, g_cs, g_coff, y, y_cs,
-                     y_coff, M, C / 4, (half_t*)g16, write32);
+  hipLaunchKernelGGL(relu_mask16_kernel<float>, dim3((n + 255) / 256), dim3(256), 0, ST(stream), g, g_cs, g_coff, y,
+                     y_cs, y_coff, M, C / 4, (half_t*)g16, write32);
+  LAUNCH_CHECK();
+}
+
+int upr_t_relu_mask16h(float* g, int g_cs, int g_coff, const void* y16, int y16_cs, int M, int C, void* g16,
+                       int write32, void* stream) {
+  if (!g || !y16 || !g16) return UPR_ERR_ARG;
+  if (C % 4 || g_cs % 4 || g_coff % 4 || y16_cs % 4 || ((uintptr_t)g & 15) || ((uintptr_t)y16 & 7) ||
+      ((uintptr_t)g16 & 7) || (long long)M * C >= (1LL << 31))
+    return UPR_ERR_UNSUPPORTED;
+  const int n = M * (C / 4);
+  if (n == 0) return UPR_OK;
+  hipLaunchKernelGGL(relu_mask16_kernel<half_t>, dim3((n + 255) / 256), dim3(256), 0, ST(stream), g, g_cs, g_coff,
+                     (const half_t*)y16, y16_cs, 0, M, C / 4, (half_t*)g16, write32);
   LAUNCH_CHECK();
 }
 
@@ -2920,8 +2947,10 @@ __global__ void maxpool_bwd_gather_kernel(const unsigned char* __restrict__ code
 // ran at <1 TB/s), compile-time windows.  The forward optionally writes the
 // argmax byte codes (PyTorch's rule, as maxpool_arg_kernel) so the backward
 // is the gather alone.
-template <int K, int S, int P>
-__global__ __launch_bounds__(256) void maxpool4_kernel(const float* __restrict__ x, int xsb, int xsh, int xsw, int H,
+// TI = half_t: the input is an activation's compact fp16 copy (the autocast
+// VGG activations live in fp16 only, as the reference's under autocast)
+template <int K, int S, int P, typename TI = float>
+__global__ __launch_bounds__(256) void maxpool4_kernel(const TI* __restrict__ x, int xsb, int xsh, int xsw, int H,
                                                        int W, int CV, int Ho, int Wo, int n, float* __restrict__ y,
                                                        int ysb, int ysh, int ysw, unsigned* __restrict__ code,
                                                        half_t* __restrict__ y16) {
@@ -2934,7 +2963,7 @@ __global__ __launch_bounds__(256) void maxpool4_kernel(const float* __restrict__
   const int oy = r % Ho, b = r / Ho;
   float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
   int best[4] = {-1, -1, -1, -1};
-  const float* xb = x + b * xsb + c;
+  const TI* xb = x + b * xsb + c;
 #pragma unroll
   for (int ky = 0; ky < K; ++ky) {
     const int iy = oy * S - P + ky;
@@ -2943,7 +2972,7 @@ __global__ __launch_bounds__(256) void maxpool4_kernel(const float* __restrict__
     for (int kx = 0; kx < K; ++kx) {
       const int ix = ox * S - P + kx;
       if ((unsigned)ix >= (unsigned)W) continue;
-      const float4 q = *(const float4*)(xb + iy * xsh + ix * xsw);
+      const float4 q = ld4f(xb + iy * xsh + ix * xsw);
       const float val[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
@@ -3086,6 +3115,26 @@ int upr_t_maxpool_code(const UprView* x, int B, int H, int W, int C, int k, int 
   if (code)
     hipLaunchKernelGGL(maxpool_arg_kernel<1>, dim3(grid_for(n)), dim3(256), 0, st, mkv(x), B, H, W, C, k, s, p, Ho,
                        Wo, code);
+  LAUNCH_CHECK();
+}
+
+int upr_t_maxpool16_code(const void* x16, int B, int H, int W, int C, int k, int s, int p, const UprView* y, int Ho,
+                         int Wo, unsigned char* code, void* y16, void* stream) {
+  if (!x16 || !y || k <= 0 || s <= 0 || k * k > 255) return UPR_ERR_ARG;
+  const long long n = (long long)B * Ho * Wo * C;
+  if (n == 0) return UPR_OK;
+  const int kind = pool_fast_kind(k, s, p);
+  if (!kind || C % 4 || (uintptr_t)x16 % 8 || !vec4_view_ok(y, B, Ho, Wo, C) || (uintptr_t)code % 4 ||
+      (uintptr_t)y16 % 8 || (long long)B * H * W * C >= (1LL << 31))
+    return UPR_ERR_UNSUPPORTED;
+  const int nv = (int)(n / 4), CV = C / 4;
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3((nv + 255) / 256), dim3(256), 0, ST(stream), (const half_t*)x16, H * W * C, W * C,
+                       C, H, W, CV, Ho, Wo, nv, (float*)y->data, (int)y->sb, (int)y->sh, (int)y->sw, (unsigned*)code,
+                       (half_t*)y16);
+  };
+  if (kind == 1) go(maxpool4_kernel<3, 1, 1, half_t>);
+  else go(maxpool4_kernel<2, 2, 0, half_t>);
   LAUNCH_CHECK();
 }
 

@@ -53,7 +53,7 @@ static SV mksv(const UprView* u) {
 template <int COUT>
 __global__ __launch_bounds__(256) void c3k3_fwd_kernel(SV x, int B, int H, int W, const float* __restrict__ w,
                                                       const float* __restrict__ bias, int p, SV y, int Ho, int Wo,
-                                                      int relu, int accum, half_t* __restrict__ y16) {
+                                                      int relu, int accum, half_t* __restrict__ y16, int skip32) {
   constexpr int TS = COUT + 4;  // LDS row stride (floats): 16-byte aligned rows, spread banks
   extern __shared__ __attribute__((aligned(16))) float sm3[];
   float* sw_ = sm3;                  // [27][COUT] weights, k-major (broadcast reads)
@@ -122,7 +122,7 @@ __global__ __launch_bounds__(256) void c3k3_fwd_kernel(SV x, int B, int H, int W
     if (relu) {
       v[0] = fmaxf(v[0], 0.f); v[1] = fmaxf(v[1], 0.f); v[2] = fmaxf(v[2], 0.f); v[3] = fmaxf(v[3], 0.f);
     }
-    *dst = v;
+    if (!skip32) *dst = v;
     if (y16) {  // the autocast consumer's fp16 operand, [pixel][COUT] compact
       typedef _Float16 h4 __attribute__((ext_vector_type(4)));
       *(h4*)(y16 + (size_t)pp * COUT + q * 4) = h4{(half_t)v[0], (half_t)v[1], (half_t)v[2], (half_t)v[3]};
@@ -497,8 +497,9 @@ int small_conv_dgrad_c3_16(const void* dy16, int B, int H, int W, const float* w
 // ---------------------------------------------------------------------------
 int small_conv_fwd(const UprView* xv, int B, int H, int W, int Cin, const float* w, const float* bias, int Cout,
                    int kh, int kw, int stride, int pad, int dil, const UprView* yv, int Ho, int Wo, int relu,
-                   int accumulate, hipStream_t st, void* y16) {
+                   int accumulate, hipStream_t st, void* y16, int skip32) {
   if (y16 && (Cout <= 4 || (uintptr_t)y16 % 8)) return kErrUnsupported;  // fp16 copies: the 3 -> 32 / 64 kernel only
+  if (skip32 && !y16) return kErrUnsupported;
   if (Cout <= 4) {
     if ((long long)B * Ho * Wo >= (1ll << 31)) return kErrUnsupported;
     const size_t lds = sizeof(float) * (size_t)Cout * Cin * kh * kw;
@@ -535,11 +536,11 @@ int small_conv_fwd(const UprView* xv, int B, int H, int W, int Cin, const float*
   if (Cout == 32) {
     const size_t lds = sizeof(float) * (27 * 32 + 32 + 256 * 36);
     hipLaunchKernelGGL(c3k3_fwd_kernel<32>, dim3(grid), dim3(256), lds, st, x, B, H, W, w, bias, pad, y, Ho, Wo, relu,
-                       accumulate, (half_t*)y16);
+                       accumulate, (half_t*)y16, skip32);
   } else {
     const size_t lds = sizeof(float) * (27 * 64 + 64 + 256 * 68);
     hipLaunchKernelGGL(c3k3_fwd_kernel<64>, dim3(grid), dim3(256), lds, st, x, B, H, W, w, bias, pad, y, Ho, Wo, relu,
-                       accumulate, (half_t*)y16);
+                       accumulate, (half_t*)y16, skip32);
   }
   return (int)hipGetLastError();
 }

@@ -115,7 +115,8 @@ SIGNATURES.update({
     "upr_t_zero": (_i, [_p, c_size_t, _p]),
     "upr_t_conv_direct": (_i, [_vp, _i, _i, _i, _i, _p, _p, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _p]),
     "upr_t_conv_dgrad_c3_16": (_i, [_p, _i, _i, _i, _p, _i, _vp, _i, _p]),
-    "upr_t_conv_direct16": (_i, [_vp, _i, _i, _i, _i, _p, _p, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _p, _p]),
+    "upr_t_conv_direct16": (_i, [_vp, _i, _i, _i, _i, _p, _p, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _p, _i,
+                                 _p]),
     "upr_t_conv_direct_dgrad": (_i, [_vp, _i, _i, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _p]),
     "upr_t_conv_direct_wgrad": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p]),
     "upr_t_conv_mfma": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _p, _i, _i, _i, _i, _i, _i, _p, _i, _i, _p, _i, _i,
@@ -154,6 +155,8 @@ SIGNATURES.update({
     "upr_t_maxpool": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _p]),
     "upr_t_maxpool_bwd": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _p]),
     "upr_t_maxpool_code": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _p, _p, _p]),
+    "upr_t_maxpool16_code": (_i, [_p, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _p, _p, _p]),
+    "upr_t_relu_mask16h": (_i, [_p, _i, _i, _p, _i, _i, _i, _p, _i, _p]),
     "upr_t_copy16": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _p, _i, _p]),
     "upr_t_bilinear16": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _p, _i, _p]),
     "upr_t_add16": (_i, [_p, _p, _p, c_size_t, _p, _p]),

@@ -83,9 +83,12 @@ class VGGPerceptual:
         for sl in self.SLICES:
             for i in sl:
                 inp = h
-                h = self.convs[i].fwd(h, relu=True) if self.convs[i].mfma else \
+                # autocast: the frozen VGG's activations are fp16 only (every reader takes the
+                # fp16 copy: the next conv, the pool, the backward's ReLU masks), as the reference's
+                h = self.convs[i].fwd(h, relu=True, only16=True) if self.convs[i].mfma else \
                     self.convs[i].fwd(None, relu=True, x_view=(h.view(), h.B, h.H, h.W),
-                                      out=Act.new(h.B, h.H, h.W, self.convs[i].Cout, h.t.device, fresh=False))
+                                      out=Act.new(h.B, h.H, h.W, self.convs[i].Cout, h.t.device, fresh=False),
+                                      only16=True)
                 if keep:
                     trace.append(("conv", i, inp, h))
             p = Act.new(h.B, h.H // 2, h.W // 2, h.C, h.t.device, fresh=False)

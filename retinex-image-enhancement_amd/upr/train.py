@@ -246,6 +246,7 @@ class Conv:
         self.wp16 = self.wt16 = None
         self.amp = False  # fp16 arithmetic of the last forward (its backward follows it)
         self.dgrad16_c3 = False
+        self.only16 = False
 
     def out_hw(self, H, W):
         return ((H + 2 * self.p - self.d * (self.kh - 1) - 1) // self.s + 1,
@@ -288,7 +289,7 @@ class Conv:
             _chk(lib.upr_t_cast_f16(_p(self.wt), _p(self.wt16), w.numel(), st), "cast_w")
 
     def _mfma16(self, x, B, H, W, C, cs, coff, w16, bias, N, kh, kw, s, p, d, res, relu, out, store=0, x16=None,
-                keep16=False, out16=None):
+                keep16=False, out16=None, only16=False):
         """fp16 MFMA conv with fp32 in / out (upr_t_conv_mfma16); res: Act or None; x16: the
         input's compact fp16 copy when its producer already wrote it; out16 = (fp16 tensor, channel
         offset, channel stride): where the (half)out copy goes when `out` is a channel slice of a
@@ -307,8 +308,9 @@ class Conv:
             y16p, y16cs = _p(y16), 0
         _chk(L.lib().upr_t_conv_mfma16(_fp(x, 0), B, H, W, C, cs, coff, _p(w16), _p(bias), N, kh, kw, s, p, d,
                                        res.ptr() if res is not None else None, res.cs if res is not None else 0,
-                                       int(relu), _fp(out.t), out.cs, out.coff, store | (2 if keep16 and res is None
-                                                                                         else 0),
+                                       int(relu), _fp(out.t), out.cs, out.coff,
+                                       store | (2 if keep16 and res is None else 0) |
+                                       (4 if only16 and keep16 and res is None and out16 is None else 0),
                                        _p(x16), int(ready), y16p, y16cs, _stream()), "conv_mfma16")
         if out16 is not None:
             out.t16 = None
@@ -317,11 +319,14 @@ class Conv:
         # autocast conv reading out takes it (Act.t16); forward activations are not modified in place
         whole = out.coff == 0 and out.cs == out.C == (N // 4 if store == 1 else N)
         out.t16 = y16 if keep16 and res is None and whole else None
+        out.stale32 = bool(only16 and out.t16 is not None)
         return x16
 
-    def fwd(self, x, relu=False, out=None, res=None, x_view=None, out16=None):
+    def fwd(self, x, relu=False, out=None, res=None, x_view=None, out16=None, only16=False):
         """x: Act (or x_view: (UprView, B, H, W) for an NCHW network input); out16: see _mfma16
-        (autocast MFMA convs only; False is returned when the copy was not written)."""
+        (autocast MFMA convs only; False is returned when the copy was not written).
+        only16: under autocast every reader of the output takes its fp16 copy (the
+        frozen VGG's activations): the fp32 output is not written (out.stale32)."""
         lib, st = L.lib(), _stream()
         if x_view is not None:
             xv, B, H, W = x_view
@@ -332,6 +337,8 @@ class Conv:
             out = Act.new(B, Ho, Wo, self.Cout, x.t.device, fresh=False)
         out.fresh = False
         out.t16 = None  # any fp16 copy of an earlier content is stale now
+        out.stale32 = False
+        self.only16 = bool(only16 and _AMP[0] and res is None and out.coff == 0 and out.cs == out.C)
         self.amp = _AMP[0] and self.mfma and x_view is None
         # autocast 3 -> 32 / 64 3x3 convs: input gradient on MFMA from an fp16 dy (upr_t_conv_dgrad_c3_16)
         self.dgrad16_c3 = _AMP[0] and self.Cin == 3 and self.Cout in (32, 64) and \
@@ -354,7 +361,8 @@ class Conv:
             whole = x.coff == 0 and x.C == x.cs == self.Cin
             t16 = x.t16 if whole else None
             x16 = self._mfma16(x.t, B, H, W, self.Cin, x.cs, x.coff, self.wp16, self.bias, self.Cout, self.kh,
-                               self.kw, self.s, self.p, self.d, res, relu, out, x16=t16, keep16=True, out16=out16)
+                               self.kw, self.s, self.p, self.d, res, relu, out, x16=t16, keep16=True, out16=out16,
+                               only16=self.only16)
             if whole:
                 x.t16 = x16  # the next autocast conv reading x (EnhancedFAM: three of them) reuses the copy
             self.x16 = None if self.frozen else x16
@@ -372,9 +380,11 @@ class Conv:
                 y16 = _h16(B * Ho * Wo * self.Cout, out.t.device)
                 rc = lib.upr_t_conv_direct16(ctypes.byref(v), B, H, W, self.Cin, _p(self.m.weight), _p(self.bias),
                                              self.Cout, self.kh, self.kw, self.s, self.p, self.d,
-                                             ctypes.byref(out.view()), Ho, Wo, int(relu), 0, _p(y16), st)
+                                             ctypes.byref(out.view()), Ho, Wo, int(relu), 0, _p(y16),
+                                             int(self.only16), st)
                 if rc == 0:
                     out.t16 = y16
+                    out.stale32 = self.only16
                     return
                 if rc != L.UPR_ERR_UNSUPPORTED:
                     _chk(rc, "conv_direct16")
@@ -663,13 +673,18 @@ def relu_mask(g, y, want16=False, only16=False):
     g.t16, g.t16_grad, g.stale32 = None, False, False  # masked in place: any fp16 copy is stale
     if want16 and g.coff == 0 and g.cs == g.C:
         g16 = _h16(g.M * g.C, g.t.device)
-        rc = L.lib().upr_t_relu_mask16(_fp(g.t), g.cs, g.coff, _fp(y.t), y.cs, y.coff, g.M, g.C, _p(g16),
-                                       int(not only16), _stream())
+        if y.stale32:  # y exists in fp16 only (frozen VGG activations under autocast)
+            rc = L.lib().upr_t_relu_mask16h(_fp(g.t), g.cs, g.coff, _p(y.t16), y.C, g.M, g.C, _p(g16),
+                                            int(not only16), _stream())
+        else:
+            rc = L.lib().upr_t_relu_mask16(_fp(g.t), g.cs, g.coff, _fp(y.t), y.cs, y.coff, g.M, g.C, _p(g16),
+                                           int(not only16), _stream())
         if rc == 0:
             g.t16, g.t16_grad, g.stale32 = g16, True, only16
             return
         if rc != L.UPR_ERR_UNSUPPORTED:
             _chk(rc, "relu_mask16")
+    assert not y.stale32, "fp16-only activation without an fp16 mask path"
     _chk(L.lib().upr_t_relu_mask(_fp(g.t), g.cs, g.coff, _fp(y.t), y.cs, y.coff, g.M, g.C, _stream()), "relu_mask")
 
 
@@ -679,6 +694,16 @@ def maxpool_into(x, y, k, s, p, code=None):
     lib, st = L.lib(), _stream()
     if _AMP[0] and y.coff == 0 and y.cs == y.C:
         y16 = _h16(y.M * y.C, y.t.device)
+        if x.t16 is not None and x.coff == 0 and x.cs == x.C:
+            # the activation's fp16 copy (its only value when x.stale32)
+            rc = lib.upr_t_maxpool16_code(_p(x.t16), x.B, x.H, x.W, x.C, k, s, p, ctypes.byref(y.view()), y.H, y.W,
+                                          _p(code), _p(y16), st)
+            if rc == 0:
+                y.t16 = y16
+                return
+            if rc != L.UPR_ERR_UNSUPPORTED:
+                _chk(rc, "maxpool16")
+        assert not x.stale32, "fp16-only activation without an fp16 max-pool path"
         rc = lib.upr_t_maxpool_code(ctypes.byref(x.view()), x.B, x.H, x.W, x.C, k, s, p, ctypes.byref(y.view()), y.H,
                                     y.W, _p(code), _p(y16), st)
         if rc == 0:

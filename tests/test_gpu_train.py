@@ -376,17 +376,25 @@ def test_fp16_copy_producers():
     vx = L.UprView(x.data_ptr(), 3 * H * W, W, 1, H * W)
     vy = L.UprView(y.data_ptr(), H * W * 64, W * 64, 64, 1)
     assert lib.upr_t_conv_direct16(ctypes.byref(vx), B, H, W, 3, w.data_ptr(), bias.data_ptr(), 64, 3, 3, 1, 1, 1,
-                                   ctypes.byref(vy), H, W, 1, 0, y16.data_ptr(), st) == 0
+                                   ctypes.byref(vy), H, W, 1, 0, y16.data_ptr(), 0, st) == 0
     torch.cuda.synchronize()
     ref = torch.relu(torch.nn.functional.conv2d(x.cpu(), w.cpu(), bias.cpu(), padding=1)).permute(0, 2, 3, 1)
     _close(y, ref, 1e-5, "direct16 fp32")
     assert torch.equal(y16.view(B, H, W, 64), y.half())
+    # skip32: the fp16 copy alone (the frozen VGG conv1_1 under autocast)
+    yk = torch.full_like(y, 4.0)
+    y16k = torch.empty_like(y16)
+    vyk = L.UprView(yk.data_ptr(), H * W * 64, W * 64, 64, 1)
+    assert lib.upr_t_conv_direct16(ctypes.byref(vx), B, H, W, 3, w.data_ptr(), bias.data_ptr(), 64, 3, 3, 1, 1, 1,
+                                   ctypes.byref(vyk), H, W, 1, 0, y16k.data_ptr(), 1, st) == 0
+    torch.cuda.synchronize()
+    assert torch.all(yk == 4.0) and torch.equal(y16k, y16)
     # a 1 x 1 head has no fp16 form: UNSUPPORTED, nothing written
     w1 = torch.randn(1, 3, 1, 1, device=DEV)
     y1 = torch.full((B, H, W, 1), 3.0, device=DEV)
     vy1 = L.UprView(y1.data_ptr(), H * W, W, 1, 1)
     assert lib.upr_t_conv_direct16(ctypes.byref(vx), B, H, W, 3, w1.data_ptr(), None, 1, 1, 1, 1, 0, 1,
-                                   ctypes.byref(vy1), H, W, 0, 0, y16.data_ptr(), st) == L.UPR_ERR_UNSUPPORTED
+                                   ctypes.byref(vy1), H, W, 0, 0, y16.data_ptr(), 0, st) == L.UPR_ERR_UNSUPPORTED
     assert torch.all(y1 == 3.0)
     # max-pool 3x3/1/1 with the fp16 copy
     mp = torch.empty_like(y)
@@ -397,6 +405,30 @@ def test_fp16_copy_producers():
     torch.cuda.synchronize()
     refp = torch.nn.functional.max_pool2d(y.permute(0, 3, 1, 2).cpu(), 3, 1, 1).permute(0, 2, 3, 1)
     assert torch.equal(mp.cpu(), refp) and torch.equal(mp16.view(B, H, W, 64), mp.half())
+    # the same pool from the fp16 copy (upr_t_maxpool16_code) with argmax codes
+    mpa = torch.empty_like(y)
+    codes = [torch.empty(B * H * W * 64, dtype=torch.uint8, device=DEV) for _ in range(2)]
+    vmpa = L.UprView(mpa.data_ptr(), H * W * 64, W * 64, 64, 1)
+    yh = y.half()
+    assert lib.upr_t_maxpool16_code(yh.data_ptr(), B, H, W, 64, 3, 1, 1, ctypes.byref(vmpa), H, W,
+                                    codes[0].data_ptr(), None, st) == 0
+    assert lib.upr_t_maxpool_code(ctypes.byref(vy), B, H, W, 64, 3, 1, 1, ctypes.byref(vmp), H, W,
+                                  codes[1].data_ptr(), None, st) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(mpa, torch.nn.functional.max_pool2d(yh.float().permute(0, 3, 1, 2), 3, 1, 1).permute(0, 2, 3, 1))
+    # codes: PyTorch's first-max index rule on the fp16 values
+    _, idx = torch.nn.functional.max_pool2d(yh.float().permute(0, 3, 1, 2).cpu(), 3, 1, 1, return_indices=True)
+    oy = torch.arange(H).view(1, 1, H, 1) - 1
+    ox = torch.arange(W).view(1, 1, 1, W) - 1
+    want = ((idx // W - oy) * 3 + (idx % W - ox)).permute(0, 2, 3, 1)
+    assert torch.equal(codes[0].view(B, H, W, 64).cpu().long(), want)
+    # ReLU mask from the fp16 copy (upr_t_relu_mask16h) == from fp32 where fp16 is exact
+    g = torch.randn(B, H, W, 64, generator=gen).to(DEV)
+    g16a = torch.empty(B * H * W * 64, dtype=torch.float16, device=DEV)
+    yr = (y - 0.5).half()
+    assert lib.upr_t_relu_mask16h(g.data_ptr(), 64, 0, yr.data_ptr(), 64, B * H * W, 64, g16a.data_ptr(), 0, st) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(g16a.view(B, H, W, 64), (g * (yr.float() > 0)).half())
     # add16
     s_ = torch.empty_like(y)
     s16 = torch.empty_like(y16)
