@@ -200,6 +200,19 @@ int upr_t_bn_bwd_fused(const float* g, int g_cs, int g_coff, const float* x, int
                        const float* invstd, const float* gamma, const float* beta, int relu, int M, int C,
                        double* acc, float* dgamma, float* dbeta, float* dx, int dx_cs, int dx_coff, int accumulate,
                        int batch_stats, void* dx16, void* stream);
+/* BatchNorm training passes reading x from its compact fp16 copy x16 ([M][C])
+ * instead of the fp32 tensor: under autocast the BN input is an fp16 conv's
+ * output, so both hold the same values (bit-identical statistics, outputs and
+ * gradients) at half the bytes.  C % 4 == 0 (and <= 1024 for the reductions),
+ * else UPR_ERR_UNSUPPORTED. */
+int upr_t_bn_stats16(const void* x16, int M, int C, double* acc, void* stream);
+int upr_t_bn_apply16h(const void* x16, int M, int C, const float* mean, const float* invstd, const float* gamma,
+                      const float* beta, const float* res, int res_cs, int res_coff, int res_post, int relu, float* y,
+                      int y_cs, int y_coff, void* y16, void* stream);
+int upr_t_bn_bwd_fused16(const float* g, int g_cs, int g_coff, const void* x16, const float* mean,
+                         const float* invstd, const float* gamma, const float* beta, int relu, int M, int C,
+                         double* acc, float* dgamma, float* dbeta, float* dx, int dx_cs, int dx_coff, int accumulate,
+                         int batch_stats, void* dx16, void* stream);
 /* upr_t_zero_upsample with an fp16 result z16 [B,2Ho,2Wo,C] (dy rounded to
  * fp16: the autocast stride-2 input-gradient conv's operand); C % 8 == 0. */
 int upr_t_zero_upsample16(const float* dy, int B, int Ho, int Wo, int C, int dy_cs, int dy_coff, void* z16,

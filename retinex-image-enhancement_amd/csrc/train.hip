@@ -677,8 +677,11 @@ static bool reduce4_ok(int C, int cs, int coff, const void* p) {
 constexpr int kRedSlots = 256;
 constexpr int kRedThreads = 1024;
 
-__global__ __launch_bounds__(kRedThreads) void chan_part_kernel(const float* __restrict__ a, int a_cs, int a_coff,
-                                                                const float* __restrict__ x, int x_cs, int x_coff,
+// TA / TX = half_t: the operand is an activation's compact fp16 copy (the
+// autocast conv output's exact values: BatchNorm reads half the bytes)
+template <typename TA = float, typename TX = float>
+__global__ __launch_bounds__(kRedThreads) void chan_part_kernel(const TA* __restrict__ a, int a_cs, int a_coff,
+                                                                const TX* __restrict__ x, int x_cs, int x_coff,
                                                                 const float* __restrict__ mean,
                                                                 const float* __restrict__ invstd,
                                                                 const float* __restrict__ gamma,
@@ -704,8 +707,8 @@ __global__ __launch_bounds__(kRedThreads) void chan_part_kernel(const float* __r
 #pragma unroll
       for (int e = 0; e < 4; ++e) { ga[e] = gamma[4 * q + e]; be[e] = beta[4 * q + e]; }
     }
-    const float* ap = a + a_coff + 4 * q;
-    const float* xp = x ? x + x_coff + 4 * q : nullptr;
+    const TA* ap = a + a_coff + 4 * q;
+    const TX* xp = x ? x + x_coff + 4 * q : nullptr;
     auto row = [&](const float4 av, const float4 xv) {
       float ae[4] = {av.x, av.y, av.z, av.w};
       const float xe[4] = {xv.x, xv.y, xv.z, xv.w};
@@ -727,16 +730,16 @@ __global__ __launch_bounds__(kRedThreads) void chan_part_kernel(const float* __r
     for (; r + 3 * R < r1; r += 4 * R) {
       float4 av[4], xv[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) av[k] = *(const float4*)(ap + (size_t)(r + k * R) * a_cs);
+      for (int k = 0; k < 4; ++k) av[k] = ld4f(ap + (size_t)(r + k * R) * a_cs);
       if (gx) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) xv[k] = *(const float4*)(xp + (size_t)(r + k * R) * x_cs);
+        for (int k = 0; k < 4; ++k) xv[k] = ld4f(xp + (size_t)(r + k * R) * x_cs);
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) row(av[k], gx ? xv[k] : av[k]);
     }
     for (; r < r1; r += R)
-      row(*(const float4*)(ap + (size_t)r * a_cs), gx ? *(const float4*)(xp + (size_t)r * x_cs) : make_float4(0.f, 0.f, 0.f, 0.f));
+      row(ld4f(ap + (size_t)r * a_cs), gx ? ld4f(xp + (size_t)r * x_cs) : make_float4(0.f, 0.f, 0.f, 0.f));
   }
   if (rg < R) {
 #pragma unroll
@@ -783,13 +786,14 @@ __global__ __launch_bounds__(256) void chan_fin_kernel(const double* __restrict_
   }
 }
 
-static int chan_reduce2(const float* a, int a_cs, int a_coff, const float* x, int x_cs, int x_coff, const float* mean,
+template <typename TA = float, typename TX = float>
+static int chan_reduce2(const TA* a, int a_cs, int a_coff, const TX* x, int x_cs, int x_coff, const float* mean,
                         const float* invstd, const float* gamma, const float* beta, int M, int C, int mode,
                         double* part, double* acc, float* out, int accumulate, hipStream_t st) {
   const int R = kRedThreads / (C / 4);
   int slots = M / (R * 16);
   slots = slots < 1 ? 1 : (slots > kRedSlots ? kRedSlots : slots);
-  hipLaunchKernelGGL(chan_part_kernel, dim3(slots), dim3(kRedThreads), (size_t)R * 2 * C * sizeof(double), st, a, a_cs,
+  hipLaunchKernelGGL((chan_part_kernel<TA, TX>), dim3(slots), dim3(kRedThreads), (size_t)R * 2 * C * sizeof(double), st, a, a_cs,
                      a_coff, x, x_cs, x_coff, mean, invstd, gamma, beta, M, C, mode, part);
   UPR_CHECK_HIP(hipGetLastError());
   hipLaunchKernelGGL(chan_fin_kernel, dim3((2 * C + 63) / 64), dim3(256), 0, st, part, slots, C, mode, acc, out,
@@ -849,7 +853,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
 
 // the same arithmetic, 4 channels per thread (16-byte loads / stores), and
 // optionally the compact fp16 copy y16[m][C] the next autocast conv reads
-__global__ __launch_bounds__(256) void bn_apply4_kernel(const float* __restrict__ x, int M, int C, int x_cs, int x_coff,
+template <typename TX = float>
+__global__ __launch_bounds__(256) void bn_apply4_kernel(const TX* __restrict__ x, int M, int C, int x_cs, int x_coff,
                                                         const float* __restrict__ mean,
                                                         const float* __restrict__ invstd,
                                                         const float* __restrict__ gamma,
@@ -866,7 +871,7 @@ __global__ __launch_bounds__(256) void bn_apply4_kernel(const float* __restrict_
 #pragma unroll
     for (int e = 0; e < 4; ++e) { mu[e] = mean[c + e]; is[e] = invstd[c + e]; ga[e] = gamma[c + e]; be[e] = beta[c + e]; }
     for (int m = blockIdx.x * rpb + threadIdx.x / C4; m < M; m += gridDim.x * rpb) {
-      const float4 xv = *(const float4*)(x + (size_t)m * x_cs + x_coff + c);
+      const float4 xv = ld4f(x + (size_t)m * x_cs + x_coff + c);
       const float4 rv4 = res ? *(const float4*)(res + (size_t)m * res_cs + res_coff + c) : make_float4(0.f, 0.f, 0.f, 0.f);
       const float xa[4] = {xv.x, xv.y, xv.z, xv.w}, ra[4] = {rv4.x, rv4.y, rv4.z, rv4.w};
       float o[4];
@@ -890,7 +895,7 @@ __global__ __launch_bounds__(256) void bn_apply4_kernel(const float* __restrict_
   GSTRIDE(i, n) {
     const int c = (int)(i % C4) * 4;
     const long long m = i / C4;
-    const float4 xv = *(const float4*)(x + m * x_cs + x_coff + c);
+    const float4 xv = ld4f(x + m * x_cs + x_coff + c);
     const float4 rv4 = res ? *(const float4*)(res + m * res_cs + res_coff + c) : make_float4(0.f, 0.f, 0.f, 0.f);
     const float xa[4] = {xv.x, xv.y, xv.z, xv.w}, ra[4] = {rv4.x, rv4.y, rv4.z, rv4.w};
     float o[4];
@@ -941,8 +946,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
 }
 
 // the same arithmetic, 4 channels per thread (16-byte loads / stores)
+template <typename TX = float>
 __global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(const float* __restrict__ g, int g_cs, int g_coff,
-                                                            const float* __restrict__ x, int x_cs, int x_coff,
+                                                            const TX* __restrict__ x, int x_cs, int x_coff,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ invstd,
                                                             const float* __restrict__ gamma,
@@ -977,7 +983,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(const float* __restr
     }
     for (int m = blockIdx.x * rpb + threadIdx.x / C4; m < M; m += gridDim.x * rpb) {
       const float4 gv = *(const float4*)(g + (size_t)m * g_cs + g_coff + c);
-      const float4 xv = *(const float4*)(x + (size_t)m * x_cs + x_coff + c);
+      const float4 xv = ld4f(x + (size_t)m * x_cs + x_coff + c);
       const float ga4[4] = {gv.x, gv.y, gv.z, gv.w}, xa[4] = {xv.x, xv.y, xv.z, xv.w};
       float4* o = (float4*)(dx + (size_t)m * dx_cs + dx_coff + c);
       const float4 prev = accum ? *o : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1005,7 +1011,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(const float* __restr
     const int c = (int)(i % C4) * 4;
     const long long m = i / C4;
     const float4 gv = *(const float4*)(g + m * g_cs + g_coff + c);
-    const float4 xv = *(const float4*)(x + m * x_cs + x_coff + c);
+    const float4 xv = ld4f(x + m * x_cs + x_coff + c);
     const float ga[4] = {gv.x, gv.y, gv.z, gv.w}, xa[4] = {xv.x, xv.y, xv.z, xv.w};
     float4* o = (float4*)(dx + m * dx_cs + dx_coff + c);
     float4 prev = accum ? *o : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -2632,8 +2638,8 @@ int upr_t_zero_upsample(const float* dy, int B, int Ho, int Wo, int C, int dy_cs
 int upr_t_bn_stats(const float* x, int M, int C, int cs, int coff, double* acc, void* stream) {
   if (!x || !acc || M <= 0 || C <= 0) return UPR_ERR_ARG;
   if (reduce4_ok(C, cs, coff, x))
-    return chan_reduce2(x, cs, coff, nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr, M, C, 0, acc + 2 * C, acc,
-                        nullptr, 0, ST(stream));
+    return chan_reduce2(x, cs, coff, (const float*)nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr, M, C, 0,
+                        acc + 2 * C, acc, nullptr, 0, ST(stream));
   else
     hipLaunchKernelGGL(chan_reduce_kernel, dim3(reduce_grid(M)), dim3(256), 0, ST(stream), x, cs, coff, nullptr, 0, 0,
                        nullptr, nullptr, M, C, 0, acc, nullptr);
@@ -2666,7 +2672,7 @@ int upr_t_bn_apply16(const float* x, int M, int C, int x_cs, int x_coff, const f
                   (!y16 || ((uintptr_t)y16 & 7) == 0);
   if (v4) {
     const long long n4 = (long long)M * (C / 4);
-    hipLaunchKernelGGL(bn_apply4_kernel, dim3(grid_for(n4)), dim3(256), 0, ST(stream), x, M, C, x_cs, x_coff, mean,
+    hipLaunchKernelGGL(bn_apply4_kernel<float>, dim3(grid_for(n4)), dim3(256), 0, ST(stream), x, M, C, x_cs, x_coff, mean,
                        invstd, gamma, beta, res, res_cs, res_coff, res_post, relu, y, y_cs, y_coff, (half_t*)y16);
     LAUNCH_CHECK();
   }
@@ -2705,7 +2711,7 @@ int upr_t_bn_bwd_apply(const float* g, int g_cs, int g_coff, const float* x, int
   if (C % 4 == 0 && g_cs % 4 == 0 && g_coff % 4 == 0 && x_cs % 4 == 0 && x_coff % 4 == 0 && dx_cs % 4 == 0 &&
       dx_coff % 4 == 0 && a16(g) && a16(x) && a16(dx)) {
     const long long n4 = (long long)M * (C / 4);
-    hipLaunchKernelGGL(bn_bwd_apply4_kernel, dim3(grid_for(n4)), dim3(256), 0, ST(stream), g, g_cs, g_coff, x, x_cs,
+    hipLaunchKernelGGL(bn_bwd_apply4_kernel<float>, dim3(grid_for(n4)), dim3(256), 0, ST(stream), g, g_cs, g_coff, x, x_cs,
                        x_coff, mean, invstd, gamma, acc, M, C, dgamma, dbeta, dx, dx_cs, dx_coff, accumulate,
                        batch_stats);
     LAUNCH_CHECK();
@@ -2731,9 +2737,53 @@ int upr_t_bn_bwd_fused(const float* g, int g_cs, int g_coff, const float* x, int
                               acc, nullptr, 0, st);
   if (rc) return rc;
   const long long n4 = (long long)M * (C / 4);
-  hipLaunchKernelGGL(bn_bwd_apply4_kernel, dim3(grid_for(n4)), dim3(256), 0, st, g, g_cs, g_coff, x, x_cs, 0, mean,
+  hipLaunchKernelGGL(bn_bwd_apply4_kernel<float>, dim3(grid_for(n4)), dim3(256), 0, st, g, g_cs, g_coff, x, x_cs, 0, mean,
                      invstd, gamma, acc, M, C, dgamma, dbeta, dx, dx_cs, dx_coff, accumulate, batch_stats, beta, relu,
                      (half_t*)dx16);
+  LAUNCH_CHECK();
+}
+
+// x read from its compact fp16 copy x16 ([M][C]; under autocast the BN input
+// is an fp16 conv's output, whose fp32 form holds the same values)
+int upr_t_bn_stats16(const void* x16, int M, int C, double* acc, void* stream) {
+  if (!x16 || !acc || M <= 0 || C <= 0) return UPR_ERR_ARG;
+  if (C % 4 || C > 1024 || (uintptr_t)x16 % 8) return UPR_ERR_UNSUPPORTED;
+  return chan_reduce2((const half_t*)x16, C, 0, (const float*)nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr, M, C,
+                      0, acc + 2 * C, acc, nullptr, 0, ST(stream));
+}
+
+int upr_t_bn_apply16h(const void* x16, int M, int C, const float* mean, const float* invstd, const float* gamma,
+                      const float* beta, const float* res, int res_cs, int res_coff, int res_post, int relu, float* y,
+                      int y_cs, int y_coff, void* y16, void* stream) {
+  if (!x16 || !y || !mean || !invstd || !gamma || !beta || M <= 0 || C <= 0) return UPR_ERR_ARG;
+  const auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (C % 4 || (uintptr_t)x16 % 8 || y_cs % 4 || y_coff % 4 || !a16(y) ||
+      (res && (res_cs % 4 || res_coff % 4 || !a16(res))) || ((uintptr_t)y16 & 7))
+    return UPR_ERR_UNSUPPORTED;
+  const long long n4 = (long long)M * (C / 4);
+  hipLaunchKernelGGL(bn_apply4_kernel<half_t>, dim3(grid_for(n4)), dim3(256), 0, ST(stream), (const half_t*)x16, M, C,
+                     C, 0, mean, invstd, gamma, beta, res, res_cs, res_coff, res_post, relu, y, y_cs, y_coff,
+                     (half_t*)y16);
+  LAUNCH_CHECK();
+}
+
+int upr_t_bn_bwd_fused16(const float* g, int g_cs, int g_coff, const void* x16, const float* mean,
+                         const float* invstd, const float* gamma, const float* beta, int relu, int M, int C,
+                         double* acc, float* dgamma, float* dbeta, float* dx, int dx_cs, int dx_coff, int accumulate,
+                         int batch_stats, void* dx16, void* stream) {
+  if (!g || !x16 || !acc || !dx || !gamma || !beta || !mean || !invstd || M <= 0 || C <= 0) return UPR_ERR_ARG;
+  const auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (C % 4 || C > 1024 || g_cs % 4 || g_coff % 4 || dx_cs % 4 || dx_coff % 4 || !a16(g) || (uintptr_t)x16 % 8 ||
+      !a16(dx) || !a16(mean) || !a16(invstd) || !a16(gamma) || !a16(beta) || ((uintptr_t)dx16 & 7))
+    return UPR_ERR_UNSUPPORTED;
+  hipStream_t st = ST(stream);
+  const int rc = chan_reduce2(g, g_cs, g_coff, (const half_t*)x16, C, 0, mean, invstd, gamma, beta, M, C,
+                              relu ? 3 : 1, acc + 2 * C, acc, nullptr, 0, st);
+  if (rc) return rc;
+  const long long n4 = (long long)M * (C / 4);
+  hipLaunchKernelGGL(bn_bwd_apply4_kernel<half_t>, dim3(grid_for(n4)), dim3(256), 0, st, g, g_cs, g_coff,
+                     (const half_t*)x16, C, 0, mean, invstd, gamma, acc, M, C, dgamma, dbeta, dx, dx_cs, dx_coff,
+                     accumulate, batch_stats, beta, relu, (half_t*)dx16);
   LAUNCH_CHECK();
 }
 
@@ -2764,7 +2814,7 @@ int upr_t_chan_sum_ws(const float* g, int M, int C, int cs, int coff, float* out
                       void* stream) {
   if (!g || !out || !ws || M <= 0 || C <= 0) return UPR_ERR_ARG;
   if (!reduce4_ok(C, cs, coff, g)) return upr_t_chan_sum(g, M, C, cs, coff, out, accumulate, stream);
-  return chan_reduce2(g, cs, coff, nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr, M, C, 2, ws, nullptr, out,
+  return chan_reduce2(g, cs, coff, (const float*)nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr, M, C, 2, ws, nullptr, out,
                       accumulate, ST(stream));
 }
 

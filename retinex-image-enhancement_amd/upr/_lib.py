@@ -146,6 +146,10 @@ SIGNATURES.update({
     "upr_t_reduce_acc_doubles": (_i, [_i]),
     "upr_t_bn_bwd_fused": (_i, [_p, _i, _i, _p, _i, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _i, _i, _i, _i, _p,
                                 _p]),
+    "upr_t_bn_stats16": (_i, [_p, _i, _i, _p, _p]),
+    "upr_t_bn_apply16h": (_i, [_p, _i, _i, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _i, _i, _p, _p]),
+    "upr_t_bn_bwd_fused16": (_i, [_p, _i, _i, _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _i, _i, _i, _i, _p,
+                                  _p]),
     "upr_t_zero_upsample16": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _p]),
     "upr_t_relu_mask": (_i, [_p, _i, _i, _p, _i, _i, _i, _i, _p]),
     "upr_t_relu_mask16": (_i, [_p, _i, _i, _p, _i, _i, _i, _i, _p, _i, _p]),

@@ -603,9 +603,17 @@ class BN:
     def fwd(self, x, relu=False, out=None, res=None, res_post=False):
         lib, st = L.lib(), _stream()
         m = self.m
+        # under autocast x is an fp16 conv's output: its fp16 copy holds the same values
+        x16 = x.t16 if _AMP[0] and x.t16 is not None and x.coff == 0 and x.cs == x.C == self.C else None
+        self.x16 = x16
         if m.training:
             zero(self.acc[:2 * self.C])  # only the atomic fallback adds into acc
-            _chk(lib.upr_t_bn_stats(x.ptr(), x.M, self.C, x.cs, 0, _p(self.acc), st), "bn_stats")
+            rc = lib.upr_t_bn_stats16(_p(x16), x.M, self.C, _p(self.acc), st) if x16 is not None \
+                else L.UPR_ERR_UNSUPPORTED
+            if rc == L.UPR_ERR_UNSUPPORTED:
+                assert not x.stale32, "fp16-only BN input without an fp16 statistics path"
+                rc = lib.upr_t_bn_stats(x.ptr(), x.M, self.C, x.cs, 0, _p(self.acc), st)
+            _chk(rc, "bn_stats")
             _chk(lib.upr_t_bn_finalize(_p(self.acc), x.M, self.C, ctypes.c_float(m.momentum), ctypes.c_float(m.eps),
                                        _p(m.running_mean), _p(m.running_var), _p(m.num_batches_tracked),
                                        _p(self.mean), _p(self.invstd), st), "bn_finalize")
@@ -616,9 +624,19 @@ class BN:
             out = Act.new(x.B, x.H, x.W, self.C, x.t.device, fresh=False)
         # under autocast the consumer is an fp16 conv: write its fp16 input copy here
         y16 = _h16(out.M * self.C, out.t.device) if _AMP[0] and out.coff == 0 and out.cs == self.C else None
-        _chk(lib.upr_t_bn_apply16(x.ptr(), x.M, self.C, x.cs, 0, _p(self.mean), _p(self.invstd), _p(m.weight),
-                                  _p(m.bias), res.ptr() if res is not None else None, res.cs if res is not None else 0,
-                                  0, int(res_post), int(relu), _fp(out.t), out.cs, out.coff, _p(y16), st), "bn_apply")
+        rc = L.UPR_ERR_UNSUPPORTED
+        if x16 is not None:
+            rc = lib.upr_t_bn_apply16h(_p(x16), x.M, self.C, _p(self.mean), _p(self.invstd), _p(m.weight),
+                                       _p(m.bias), res.ptr() if res is not None else None,
+                                       res.cs if res is not None else 0, 0, int(res_post), int(relu), _fp(out.t),
+                                       out.cs, out.coff, _p(y16), st)
+        if rc == L.UPR_ERR_UNSUPPORTED:
+            assert not x.stale32, "fp16-only BN input without an fp16 apply path"
+            rc = lib.upr_t_bn_apply16(x.ptr(), x.M, self.C, x.cs, 0, _p(self.mean), _p(self.invstd), _p(m.weight),
+                                      _p(m.bias), res.ptr() if res is not None else None,
+                                      res.cs if res is not None else 0, 0, int(res_post), int(relu), _fp(out.t),
+                                      out.cs, out.coff, _p(y16), st)
+        _chk(rc, "bn_apply")
         out.t16 = y16
         self.x = x
         self.out_act = out
@@ -639,10 +657,18 @@ class BN:
             whole = gx.coff == 0 and gx.cs == self.C
             dx16 = _h16(gx.M * self.C, gx.t.device) if _AMP[0] and whole else None
             acc = 0 if gx.fresh else 1
-            rc = lib.upr_t_bn_bwd_fused(_fp(g.t), g.cs, g.coff, x.ptr(), x.cs, _p(self.mean), _p(self.invstd),
-                                        _p(m.weight), _p(m.bias), int(relu), x.M, self.C, _p(self.acc),
-                                        _p(m.weight.grad), _p(m.bias.grad), _fp(gx.t), gx.cs, gx.coff, acc,
-                                        int(self.batch_stats), _p(dx16), st)
+            rc = L.UPR_ERR_UNSUPPORTED
+            if self.x16 is not None:
+                rc = lib.upr_t_bn_bwd_fused16(_fp(g.t), g.cs, g.coff, _p(self.x16), _p(self.mean), _p(self.invstd),
+                                              _p(m.weight), _p(m.bias), int(relu), x.M, self.C, _p(self.acc),
+                                              _p(m.weight.grad), _p(m.bias.grad), _fp(gx.t), gx.cs, gx.coff, acc,
+                                              int(self.batch_stats), _p(dx16), st)
+            if rc == L.UPR_ERR_UNSUPPORTED:
+                assert not x.stale32, "fp16-only BN input without an fp16 backward path"
+                rc = lib.upr_t_bn_bwd_fused(_fp(g.t), g.cs, g.coff, x.ptr(), x.cs, _p(self.mean), _p(self.invstd),
+                                            _p(m.weight), _p(m.bias), int(relu), x.M, self.C, _p(self.acc),
+                                            _p(m.weight.grad), _p(m.bias.grad), _fp(gx.t), gx.cs, gx.coff, acc,
+                                            int(self.batch_stats), _p(dx16), st)
             if rc != L.UPR_ERR_UNSUPPORTED:
                 _chk(rc, "bn_bwd_fused")
                 gx.consume_fresh()
@@ -781,9 +807,11 @@ class ResBlockT:
 
     def fwd(self, x):
         self.x = x
-        self.a1 = self.bn1.fwd(self.conv1.fwd(x), relu=True)
-        c2 = self.conv2.fwd(self.a1)
-        sc = self.sbn.fwd(self.sconv.fwd(x)) if self.proj else x
+        # a conv whose only reader is a BatchNorm keeps its output in fp16 only under
+        # autocast (the BN reads the fp16 copy: the same values)
+        self.a1 = self.bn1.fwd(self.conv1.fwd(x, only16=True), relu=True)
+        c2 = self.conv2.fwd(self.a1, only16=True)
+        sc = self.sbn.fwd(self.sconv.fwd(x, only16=True)) if self.proj else x
         self.out = self.bn2.fwd(c2, relu=True, res=sc)
         return self.out
 
@@ -820,8 +848,8 @@ class PreActResBlockT:
     def fwd(self, x):
         self.x = x
         self.o = self.bn1.fwd(x, relu=True)
-        sc = self.sbn.fwd(self.sconv.fwd(self.o)) if self.proj else x
-        self.a2 = self.bn2.fwd(self.conv1.fwd(self.o), relu=True)
+        sc = self.sbn.fwd(self.sconv.fwd(self.o, only16=True)) if self.proj else x
+        self.a2 = self.bn2.fwd(self.conv1.fwd(self.o, only16=True), relu=True)
         return self.conv2.fwd(self.a2, res=sc)
 
     def bwd(self, g, gx):
@@ -869,9 +897,9 @@ class ASPPT:
         self.x = x
         cat = Act.new(x.B, x.H, x.W, C * nb, dev, fresh=False)
         self.cat = cat
-        self.b1.fwd(self.c1.fwd(x), relu=True, out=cat.slice(0, C))
+        self.b1.fwd(self.c1.fwd(x, only16=True), relu=True, out=cat.slice(0, C))
         for i, (cv, bn) in enumerate(self.br):
-            bn.fwd(cv.fwd(x), relu=True, out=cat.slice(C * (i + 1), C))
+            bn.fwd(cv.fwd(x, only16=True), relu=True, out=cat.slice(C * (i + 1), C))
         # global branch: mean -> 1x1 -> BN (over the batch) -> ReLU -> broadcast
         self.gm = Act.new(x.B, 1, 1, x.C, dev, fresh=False)
         _chk(L.lib().upr_t_pixel_sum(x.ptr(), x.B, x.H * x.W, x.C, x.cs, 0, ctypes.c_float(1.0 / (x.H * x.W)),
@@ -879,7 +907,7 @@ class ASPPT:
         self.gp = self.gb.fwd(self.gc.fwd(self.gm), relu=True)
         _chk(L.lib().upr_t_broadcast(_fp(self.gp.t), x.B, x.H * x.W, C, ctypes.c_float(1.0), _fp(cat.t), cat.cs,
                                      C * (nb - 1), 0, _stream()), "broadcast")
-        self.a = self.fb.fwd(self.fc.fwd(cat), relu=True)
+        self.a = self.fb.fwd(self.fc.fwd(cat, only16=True), relu=True)
         self.dropped = self.training  # the backward applies the mask only when this forward drew one
         if not self.dropped:
             self.mask = None
@@ -938,8 +966,8 @@ class UpBlockT:
         """skip=None: UpBlock.forward alone (model.py:271-274, no skip add)."""
         self.x = x
         self.u = self.up.fwd(x)
-        self.a1 = self.b1.fwd(self.c1.fwd(self.u), relu=True)
-        self.a2 = self.b2.fwd(self.c2.fwd(self.a1), relu=True)
+        self.a1 = self.b1.fwd(self.c1.fwd(self.u, only16=True), relu=True)
+        self.a2 = self.b2.fwd(self.c2.fwd(self.a1, only16=True), relu=True)
         if skip is None:
             return self.a2
         out = Act.new(self.a2.B, self.a2.H, self.a2.W, self.a2.C, x.t.device, fresh=False)
