@@ -212,7 +212,15 @@ int upr_t_bn_apply16h(const void* x16, int M, int C, const float* mean, const fl
 int upr_t_bn_bwd_fused16(const float* g, int g_cs, int g_coff, const void* x16, const float* mean,
                          const float* invstd, const float* gamma, const float* beta, int relu, int M, int C,
                          double* acc, float* dgamma, float* dbeta, float* dx, int dx_cs, int dx_coff, int accumulate,
-                         int batch_stats, void* dx16, void* stream);
+                         int batch_stats, void* dx16, int skip32, void* stream);
+/* skip32 (needs dx16, no accumulate): dx itself is not written -- the input
+ * gradient's readers (the autocast conv's dgrad, weight gradient and bias sum)
+ * all take dx16.  Bias gradient from an fp16 gradient copy ([M][C] compact):
+ * out[c] (+)= sum over m (two-stage, ws = upr_t_reduce_acc_doubles(C)
+ * doubles). */
+int upr_t_chan_sum16(const void* g16, int M, int C, float* out, int accumulate, double* ws, void* stream);
+/* upr_t_zero_upsample16 from the gradient's compact fp16 copy dy16. */
+int upr_t_zero_upsample16h(const void* dy16, int B, int Ho, int Wo, int C, void* z16, void* stream);
 /* upr_t_zero_upsample with an fp16 result z16 [B,2Ho,2Wo,C] (dy rounded to
  * fp16: the autocast stride-2 input-gradient conv's operand); C % 8 == 0. */
 int upr_t_zero_upsample16(const float* dy, int B, int Ho, int Wo, int C, int dy_cs, int dy_coff, void* z16,

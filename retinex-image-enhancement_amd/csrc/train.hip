@@ -506,6 +506,22 @@ __global__ void zero_upsample_kernel(const float* __restrict__ dy, int B, int Ho
 
 // fp16 form for the autocast stride-2 input gradient: dy (fp32) rounded to
 // fp16 as the conv's cast would, zero-upsampled, 8 channels per thread
+// from the gradient's compact fp16 copy (dy16 [B][Ho][Wo][C]): 16-byte copies
+__global__ __launch_bounds__(256) void zero_upsample16h_kernel(const half_t* __restrict__ dy16, int B, int Ho, int Wo,
+                                                               int C, half_t* __restrict__ z, long long n) {
+  const int C8 = C / 8;
+  GSTRIDE(i, n) {
+    const int c = (int)(i % C8) * 8;
+    long long r = i / C8;
+    const int X = (int)(r % (2 * Wo)); r /= 2 * Wo;
+    const int Y = (int)(r % (2 * Ho));
+    const int b = (int)(r / (2 * Ho));
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (!(X & 1) && !(Y & 1)) v = *(const uint4*)(dy16 + (((long long)b * Ho + (Y >> 1)) * Wo + (X >> 1)) * C + c);
+    *(uint4*)(z + i * 8) = v;
+  }
+}
+
 __global__ __launch_bounds__(256) void zero_upsample16_kernel(const float* __restrict__ dy, int B, int Ho, int Wo,
                                                               int C, int cs, int coff, half_t* __restrict__ z) {
   typedef _Float16 h8 __attribute__((ext_vector_type(8)));
@@ -956,7 +972,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(const float* __restr
                                                             float* dgamma, float* dbeta, float* dx, int dx_cs,
                                                             int dx_coff, int accum, int batch_stats,
                                                             const float* __restrict__ beta = nullptr, int relu = 0,
-                                                            half_t* __restrict__ dx16 = nullptr) {
+                                                            half_t* __restrict__ dx16 = nullptr, int skip32 = 0) {
   // relu: the consumer ReLU folded in (g counts where bn(x) > 0, recomputed);
   // dx16: compact [M][C] fp16 copy of dx for the autocast input-gradient conv
   if (blockIdx.x == 0) {
@@ -998,7 +1014,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(const float* __restr
         if (accum) v += pa[e];
         r[e] = v;
       }
-      *o = make_float4(r[0], r[1], r[2], r[3]);
+      if (!skip32) *o = make_float4(r[0], r[1], r[2], r[3]);
       if (dx16) {
         typedef _Float16 h4 __attribute__((ext_vector_type(4)));
         *(h4*)(dx16 + (size_t)m * C + c) = h4{(half_t)r[0], (half_t)r[1], (half_t)r[2], (half_t)r[3]};
@@ -1029,7 +1045,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(const float* __restr
       if (accum) v += pa[e];
       r[e] = v;
     }
-    *o = make_float4(r[0], r[1], r[2], r[3]);
+    if (!skip32) *o = make_float4(r[0], r[1], r[2], r[3]);
     if (dx16) {
       typedef _Float16 h4 __attribute__((ext_vector_type(4)));
       *(h4*)(dx16 + m * C + c) = h4{(half_t)r[0], (half_t)r[1], (half_t)r[2], (half_t)r[3]};
@@ -2770,8 +2786,9 @@ int upr_t_bn_apply16h(const void* x16, int M, int C, const float* mean, const fl
 int upr_t_bn_bwd_fused16(const float* g, int g_cs, int g_coff, const void* x16, const float* mean,
                          const float* invstd, const float* gamma, const float* beta, int relu, int M, int C,
                          double* acc, float* dgamma, float* dbeta, float* dx, int dx_cs, int dx_coff, int accumulate,
-                         int batch_stats, void* dx16, void* stream) {
+                         int batch_stats, void* dx16, int skip32, void* stream) {
   if (!g || !x16 || !acc || !dx || !gamma || !beta || !mean || !invstd || M <= 0 || C <= 0) return UPR_ERR_ARG;
+  if (skip32 && (accumulate || !dx16)) return UPR_ERR_ARG;
   const auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
   if (C % 4 || C > 1024 || g_cs % 4 || g_coff % 4 || dx_cs % 4 || dx_coff % 4 || !a16(g) || (uintptr_t)x16 % 8 ||
       !a16(dx) || !a16(mean) || !a16(invstd) || !a16(gamma) || !a16(beta) || ((uintptr_t)dx16 & 7))
@@ -2783,7 +2800,7 @@ int upr_t_bn_bwd_fused16(const float* g, int g_cs, int g_coff, const void* x16, 
   const long long n4 = (long long)M * (C / 4);
   hipLaunchKernelGGL(bn_bwd_apply4_kernel<half_t>, dim3(grid_for(n4)), dim3(256), 0, st, g, g_cs, g_coff,
                      (const half_t*)x16, C, 0, mean, invstd, gamma, acc, M, C, dgamma, dbeta, dx, dx_cs, dx_coff,
-                     accumulate, batch_stats, beta, relu, (half_t*)dx16);
+                     accumulate, batch_stats, beta, relu, (half_t*)dx16, skip32);
   LAUNCH_CHECK();
 }
 
@@ -2794,6 +2811,14 @@ int upr_t_zero_upsample16(const float* dy, int B, int Ho, int Wo, int C, int dy_
   const long long n = (long long)B * 4 * Ho * Wo * (C / 8);
   hipLaunchKernelGGL(zero_upsample16_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), dy, B, Ho, Wo, C, dy_cs,
                      dy_coff, (half_t*)z16);
+  LAUNCH_CHECK();
+}
+
+int upr_t_zero_upsample16h(const void* dy16, int B, int Ho, int Wo, int C, void* z16, void* stream) {
+  if (!dy16 || !z16 || C % 8 || ((uintptr_t)dy16 & 15) || ((uintptr_t)z16 & 15)) return UPR_ERR_ARG;
+  const long long n = (long long)B * 4 * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(zero_upsample16h_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), (const half_t*)dy16, B, Ho,
+                     Wo, C, (half_t*)z16, n);
   LAUNCH_CHECK();
 }
 
@@ -2816,6 +2841,13 @@ int upr_t_chan_sum_ws(const float* g, int M, int C, int cs, int coff, float* out
   if (!reduce4_ok(C, cs, coff, g)) return upr_t_chan_sum(g, M, C, cs, coff, out, accumulate, stream);
   return chan_reduce2(g, cs, coff, (const float*)nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr, M, C, 2, ws, nullptr, out,
                       accumulate, ST(stream));
+}
+
+int upr_t_chan_sum16(const void* g16, int M, int C, float* out, int accumulate, double* ws, void* stream) {
+  if (!g16 || !out || !ws || M <= 0 || C <= 0) return UPR_ERR_ARG;
+  if (C % 4 || C > 1024 || (uintptr_t)g16 % 8) return UPR_ERR_UNSUPPORTED;
+  return chan_reduce2((const half_t*)g16, C, 0, (const float*)nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr, M, C,
+                      2, ws, nullptr, out, accumulate, ST(stream));
 }
 
 int upr_t_reduce_acc_doubles(int C) { return 2 * C * (1 + kRedSlots); }

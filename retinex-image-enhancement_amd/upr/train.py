@@ -166,6 +166,7 @@ class Act:
         self.fresh = False
         self.t16 = None
         self.t16_grad = False
+        self.stale32 = False
         return acc
 
 
@@ -343,6 +344,7 @@ class Conv:
         # autocast 3 -> 32 / 64 3x3 convs: input gradient on MFMA from an fp16 dy (upr_t_conv_dgrad_c3_16)
         self.dgrad16_c3 = _AMP[0] and self.Cin == 3 and self.Cout in (32, 64) and \
             (self.kh, self.kw, self.s, self.p, self.d) == (3, 3, 1, 1, 1)
+        self.out_wo = Wo
         kind = "mfma16" if self.amp else ("mfma32" if self.mfma and x_view is None else "direct")
         with _timed(kind, "fwd", self.flops(B, Ho, Wo), (self.Cin, self.Cout, self.kh, self.s, H, W)):
             self._fwd(x, B, H, W, Ho, Wo, relu, out, res, x_view, out16 if self.amp else None)
@@ -351,6 +353,17 @@ class Conv:
 
     def flops(self, B, Ho, Wo):
         return 2.0 * B * Ho * Wo * self.Cout * self.Cin * self.kh * self.kw
+
+    def takes16_grad(self):
+        """True when every reader of this conv's output gradient in its backward can
+        take the gradient's fp16 copy alone (autocast: input gradient on the fp16
+        MFMA, weight gradient on the fp16-operand GEMM, bias sum from fp16), so its
+        producer (the BatchNorm backward) may skip the fp32 store."""
+        if not (self.amp and self.mfma) or self.s not in (1, 2) or self.Cout % 8:
+            return False
+        if self.frozen:
+            return True
+        return getattr(self, "out_wo", 0) % 64 == 0 and getattr(self, "x16", None) is not None
 
     def _fwd(self, x, B, H, W, Ho, Wo, relu, out, res, x_view, out16=None):
         lib, st = L.lib(), _stream()
@@ -419,13 +432,20 @@ class Conv:
                     # gy's fp16 copy (the fused BN backward's dx16) is the AMP A operand as is
                     dy16 = gy.t16 if self.amp and gy.t16_grad and gy.coff == 0 and gy.cs == gy.C == self.Cout \
                         else None
+                    assert dy16 is not None or not gy.stale32, "fp16-only gradient without the fp16 weight gradient"
                     _chk(lib.upr_t_conv_wgrad_into(_fp(x.t), _p(x16) if self.amp else None, B, H, W, self.Cin, x.cs,
                                                    x.coff, _fp(gy.t), _p(dy16), Ho, Wo, self.Cout, gy.cs, gy.coff,
                                                    self.kh, self.kw, self.s, self.p, self.d, _p(gw), st),
                          "conv_wgrad")
                     self.x16 = None
                     if self.bias is not None:
-                        chan_sum(gy, self.Cout, self.bias.grad, st)
+                        if gy.stale32:
+                            ws = torch.empty((L.lib().upr_t_reduce_acc_doubles(self.Cout),), dtype=torch.float64,
+                                             device=gy.t.device)
+                            _chk(lib.upr_t_chan_sum16(_p(gy.t16), gy.M, self.Cout, _p(self.bias.grad), 1, _p(ws), st),
+                                 "dbias16")
+                        else:
+                            chan_sum(gy, self.Cout, self.bias.grad, st)
                 else:
                     v = x.view() if x_view is None else xv
                     _chk(lib.upr_t_conv_direct_wgrad(ctypes.byref(v), ctypes.byref(gy.view()), B, H, W, self.Cin, Ho, Wo,
@@ -459,10 +479,14 @@ class Conv:
                 if self.s != 1:
                     assert self.s == 2 and H == 2 * Ho and W == 2 * Wo, "stride-2 dgrad needs even sizes"
                     if self.amp and self.Cout % 8 == 0:
-                        src16 = _h16(B * H * W * self.Cout, gy.t.device)
-                        _chk(lib.upr_t_zero_upsample16(_fp(gy.t), B, Ho, Wo, self.Cout, gy.cs, gy.coff, _p(src16),
-                                                       st), "zero_upsample16")
-                        src = None
+                        z16 = _h16(B * H * W * self.Cout, gy.t.device)
+                        if gy.stale32:
+                            _chk(lib.upr_t_zero_upsample16h(_p(gy.t16), B, Ho, Wo, self.Cout, _p(z16), st),
+                                 "zero_upsample16h")
+                        else:
+                            _chk(lib.upr_t_zero_upsample16(_fp(gy.t), B, Ho, Wo, self.Cout, gy.cs, gy.coff, _p(z16),
+                                                           st), "zero_upsample16")
+                        src16, src = z16, None
                     else:
                         src16 = None
                         z = empty((B, H, W, self.Cout), gy.t.device)
@@ -471,6 +495,7 @@ class Conv:
                         src = z
                     sH, sW, scs, scoff = H, W, self.Cout, 0
                 pad_t = self.d * (self.kh - 1) - self.p
+                assert src16 is not None or not gy.stale32, "fp16-only gradient without the fp16 input gradient"
                 if self.amp:
                     self._mfma16(src, B, sH, sW, self.Cout, scs, scoff, self.wt16, None, self.Cin, self.kh, self.kw, 1,
                                  pad_t, self.d, gx if acc else None, False, gx, x16=src16)
@@ -644,12 +669,13 @@ class BN:
         self.relu_only = bool(relu) and res is None  # y = relu(bn(x)): the backward may fold the mask in
         return out
 
-    def bwd(self, g, gx, relu=False):
+    def bwd(self, g, gx, relu=False, only16=False):
         """g: Act gradient of the BN output; relu=True: g is the gradient of
         relu(bn(x)) (this forward's relu=True, no residual), the ReLU mask is
         folded into the BN backward (recomputed from x, no separate pass).
         Under autocast the input gradient also gets its compact fp16 copy
-        (gx.t16) for the input-gradient conv that consumes it."""
+        (gx.t16) for the input-gradient conv that consumes it; only16 (the
+        consumer's Conv.takes16_grad()): the fp32 gx is not written at all."""
         lib, st = L.lib(), _stream()
         m, x = self.m, self.x
         assert not relu or self.relu_only, "ReLU fold needs a relu(bn(x)) forward"
@@ -658,11 +684,16 @@ class BN:
             dx16 = _h16(gx.M * self.C, gx.t.device) if _AMP[0] and whole else None
             acc = 0 if gx.fresh else 1
             rc = L.UPR_ERR_UNSUPPORTED
+            skip32 = int(bool(only16) and dx16 is not None and acc == 0)
             if self.x16 is not None:
                 rc = lib.upr_t_bn_bwd_fused16(_fp(g.t), g.cs, g.coff, _p(self.x16), _p(self.mean), _p(self.invstd),
                                               _p(m.weight), _p(m.bias), int(relu), x.M, self.C, _p(self.acc),
                                               _p(m.weight.grad), _p(m.bias.grad), _fp(gx.t), gx.cs, gx.coff, acc,
-                                              int(self.batch_stats), _p(dx16), st)
+                                              int(self.batch_stats), _p(dx16), skip32, st)
+                if rc == 0:
+                    gx.consume_fresh()
+                    gx.t16, gx.t16_grad, gx.stale32 = dx16, dx16 is not None, bool(skip32)
+                    return
             if rc == L.UPR_ERR_UNSUPPORTED:
                 assert not x.stale32, "fp16-only BN input without an fp16 backward path"
                 rc = lib.upr_t_bn_bwd_fused(_fp(g.t), g.cs, g.coff, x.ptr(), x.cs, _p(self.mean), _p(self.invstd),
@@ -818,17 +849,17 @@ class ResBlockT:
     def bwd(self, g, gx):
         relu_mask(g, self.out)
         g_c2 = Act.new(g.B, g.H, g.W, self.conv2.Cout, g.t.device)
-        self.bn2.bwd(g, g_c2)
+        self.bn2.bwd(g, g_c2, only16=self.conv2.takes16_grad())
         if self.proj:
             g_cs = Act.new(g.B, g.H, g.W, self.sconv.Cout, g.t.device)
-            self.sbn.bwd(g, g_cs)
+            self.sbn.bwd(g, g_cs, only16=self.sconv.takes16_grad())
             self.sconv.bwd(self.x, g_cs, gx)
         else:
             add_into(gx, g)
         g_a1 = Act.new(self.a1.B, self.a1.H, self.a1.W, self.a1.C, g.t.device)
         self.conv2.bwd(self.a1, g_c2, g_a1)
         g_c1 = Act.new(g_a1.B, g_a1.H, g_a1.W, g_a1.C, g.t.device)
-        self.bn1.bwd(g_a1, g_c1, relu=True)
+        self.bn1.bwd(g_a1, g_c1, relu=True, only16=self.conv1.takes16_grad())
         self.conv1.bwd(self.x, g_c1, gx)
 
 
@@ -857,12 +888,12 @@ class PreActResBlockT:
         g_a2 = Act.new(self.a2.B, self.a2.H, self.a2.W, self.a2.C, dev)
         self.conv2.bwd(self.a2, g, g_a2)
         g_c1 = Act.new(g_a2.B, g_a2.H, g_a2.W, g_a2.C, dev)
-        self.bn2.bwd(g_a2, g_c1, relu=True)
+        self.bn2.bwd(g_a2, g_c1, relu=True, only16=self.conv1.takes16_grad())
         g_o = Act.new(self.o.B, self.o.H, self.o.W, self.o.C, dev)
         self.conv1.bwd(self.o, g_c1, g_o)
         if self.proj:
             g_cs = Act.new(g.B, g.H, g.W, self.sconv.Cout, dev)
-            self.sbn.bwd(g, g_cs)
+            self.sbn.bwd(g, g_cs, only16=self.sconv.takes16_grad())
             self.sconv.bwd(self.o, g_cs, g_o)
         else:
             add_into(gx, g)
@@ -979,11 +1010,11 @@ class UpBlockT:
         if g_skip is not None:
             add_into(g_skip, g)
         g_c2 = Act.new(g.B, g.H, g.W, g.C, dev)
-        self.b2.bwd(g, g_c2, relu=True)
+        self.b2.bwd(g, g_c2, relu=True, only16=self.c2.takes16_grad())
         g_a1 = Act.new(g.B, g.H, g.W, g.C, dev)
         self.c2.bwd(self.a1, g_c2, g_a1)
         g_c1 = Act.new(g.B, g.H, g.W, g.C, dev)
-        self.b1.bwd(g_a1, g_c1, relu=True)
+        self.b1.bwd(g_a1, g_c1, relu=True, only16=self.c1.takes16_grad())
         g_u = Act.new(g.B, g.H, g.W, g.C, dev)
         self.c1.bwd(self.u, g_c1, g_u)
         self.up.bwd(self.x, g_u, gx)
