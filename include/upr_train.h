@@ -208,12 +208,14 @@ int upr_t_bn_bwd_fused(const float* g, int g_cs, int g_coff, const float* x, int
 int upr_t_bn_stats16(const void* x16, int M, int C, double* acc, void* stream);
 int upr_t_bn_apply16h(const void* x16, int M, int C, const float* mean, const float* invstd, const float* gamma,
                       const float* beta, const float* res, int res_cs, int res_coff, int res_post, int relu, float* y,
-                      int y_cs, int y_coff, void* y16, void* stream);
-int upr_t_bn_bwd_fused16(const float* g, int g_cs, int g_coff, const void* x16, const float* mean,
+                      int y_cs, int y_coff, void* y16, int skip32, void* stream);
+/* g16 (nullable): g read from the input-gradient conv's fp16 output instead
+ * (compact [M][C]; g / g_cs / g_coff then unused). */
+int upr_t_bn_bwd_fused16(const float* g, const void* g16, int g_cs, int g_coff, const void* x16, const float* mean,
                          const float* invstd, const float* gamma, const float* beta, int relu, int M, int C,
                          double* acc, float* dgamma, float* dbeta, float* dx, int dx_cs, int dx_coff, int accumulate,
                          int batch_stats, void* dx16, int skip32, void* stream);
-/* skip32 (needs dx16, no accumulate): dx itself is not written -- the input
+/* skip32 (needs dx16 / y16; no accumulate): dx / y itself is not written -- the input
  * gradient's readers (the autocast conv's dgrad, weight gradient and bias sum)
  * all take dx16.  Bias gradient from an fp16 gradient copy ([M][C] compact):
  * out[c] (+)= sum over m (two-stage, ws = upr_t_reduce_acc_doubles(C)

@@ -876,7 +876,7 @@ __global__ __launch_bounds__(256) void bn_apply4_kernel(const TX* __restrict__ x
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, const float* res, int res_cs,
                                                         int res_coff, int res_post, int relu, float* y, int y_cs,
-                                                        int y_coff, half_t* __restrict__ y16) {
+                                                        int y_coff, half_t* __restrict__ y16, int skip32 = 0) {
   const int C4 = C / 4;
   if (256 % C4 == 0) {
     // this thread's 4 channels are fixed (the grid stride is a multiple of C4):
@@ -899,7 +899,7 @@ __global__ __launch_bounds__(256) void bn_apply4_kernel(const TX* __restrict__ x
         if (res_post) v += ra[e];
         o[e] = v;
       }
-      *(float4*)(y + (size_t)m * y_cs + y_coff + c) = make_float4(o[0], o[1], o[2], o[3]);
+      if (!skip32) *(float4*)(y + (size_t)m * y_cs + y_coff + c) = make_float4(o[0], o[1], o[2], o[3]);
       if (y16) {
         typedef _Float16 h4 __attribute__((ext_vector_type(4)));
         *(h4*)(y16 + (size_t)m * C + c) = h4{(half_t)o[0], (half_t)o[1], (half_t)o[2], (half_t)o[3]};
@@ -923,7 +923,7 @@ __global__ __launch_bounds__(256) void bn_apply4_kernel(const TX* __restrict__ x
       if (res_post) v += ra[e];
       o[e] = v;
     }
-    *(float4*)(y + m * y_cs + y_coff + c) = make_float4(o[0], o[1], o[2], o[3]);
+    if (!skip32) *(float4*)(y + m * y_cs + y_coff + c) = make_float4(o[0], o[1], o[2], o[3]);
     if (y16) {
       typedef _Float16 h4 __attribute__((ext_vector_type(4)));
       *(h4*)(y16 + m * C + c) = h4{(half_t)o[0], (half_t)o[1], (half_t)o[2], (half_t)o[3]};
@@ -962,8 +962,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
 }
 
 // the same arithmetic, 4 channels per thread (16-byte loads / stores)
-template <typename TX = float>
-__global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(const float* __restrict__ g, int g_cs, int g_coff,
+template <typename TX = float, typename TG = float>
+__global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(const TG* __restrict__ g, int g_cs, int g_coff,
                                                             const TX* __restrict__ x, int x_cs, int x_coff,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ invstd,
@@ -998,7 +998,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(const float* __restr
       gis[e] = ga[e] * is[e];
     }
     for (int m = blockIdx.x * rpb + threadIdx.x / C4; m < M; m += gridDim.x * rpb) {
-      const float4 gv = *(const float4*)(g + (size_t)m * g_cs + g_coff + c);
+      const float4 gv = ld4f(g + (size_t)m * g_cs + g_coff + c);
       const float4 xv = ld4f(x + (size_t)m * x_cs + x_coff + c);
       const float ga4[4] = {gv.x, gv.y, gv.z, gv.w}, xa[4] = {xv.x, xv.y, xv.z, xv.w};
       float4* o = (float4*)(dx + (size_t)m * dx_cs + dx_coff + c);
@@ -1026,7 +1026,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(const float* __restr
   GSTRIDE(i, n) {
     const int c = (int)(i % C4) * 4;
     const long long m = i / C4;
-    const float4 gv = *(const float4*)(g + m * g_cs + g_coff + c);
+    const float4 gv = ld4f(g + m * g_cs + g_coff + c);
     const float4 xv = ld4f(x + m * x_cs + x_coff + c);
     const float ga[4] = {gv.x, gv.y, gv.z, gv.w}, xa[4] = {xv.x, xv.y, xv.z, xv.w};
     float4* o = (float4*)(dx + m * dx_cs + dx_coff + c);
@@ -2727,7 +2727,7 @@ int upr_t_bn_bwd_apply(const float* g, int g_cs, int g_coff, const float* x, int
   if (C % 4 == 0 && g_cs % 4 == 0 && g_coff % 4 == 0 && x_cs % 4 == 0 && x_coff % 4 == 0 && dx_cs % 4 == 0 &&
       dx_coff % 4 == 0 && a16(g) && a16(x) && a16(dx)) {
     const long long n4 = (long long)M * (C / 4);
-    hipLaunchKernelGGL(bn_bwd_apply4_kernel<float>, dim3(grid_for(n4)), dim3(256), 0, ST(stream), g, g_cs, g_coff, x, x_cs,
+    hipLaunchKernelGGL((bn_bwd_apply4_kernel<float, float>), dim3(grid_for(n4)), dim3(256), 0, ST(stream), g, g_cs, g_coff, x, x_cs,
                        x_coff, mean, invstd, gamma, acc, M, C, dgamma, dbeta, dx, dx_cs, dx_coff, accumulate,
                        batch_stats);
     LAUNCH_CHECK();
@@ -2753,7 +2753,7 @@ int upr_t_bn_bwd_fused(const float* g, int g_cs, int g_coff, const float* x, int
                               acc, nullptr, 0, st);
   if (rc) return rc;
   const long long n4 = (long long)M * (C / 4);
-  hipLaunchKernelGGL(bn_bwd_apply4_kernel<float>, dim3(grid_for(n4)), dim3(256), 0, st, g, g_cs, g_coff, x, x_cs, 0, mean,
+  hipLaunchKernelGGL((bn_bwd_apply4_kernel<float, float>), dim3(grid_for(n4)), dim3(256), 0, st, g, g_cs, g_coff, x, x_cs, 0, mean,
                      invstd, gamma, acc, M, C, dgamma, dbeta, dx, dx_cs, dx_coff, accumulate, batch_stats, beta, relu,
                      (half_t*)dx16);
   LAUNCH_CHECK();
@@ -2770,8 +2770,9 @@ int upr_t_bn_stats16(const void* x16, int M, int C, double* acc, void* stream) {
 
 int upr_t_bn_apply16h(const void* x16, int M, int C, const float* mean, const float* invstd, const float* gamma,
                       const float* beta, const float* res, int res_cs, int res_coff, int res_post, int relu, float* y,
-                      int y_cs, int y_coff, void* y16, void* stream) {
+                      int y_cs, int y_coff, void* y16, int skip32, void* stream) {
   if (!x16 || !y || !mean || !invstd || !gamma || !beta || M <= 0 || C <= 0) return UPR_ERR_ARG;
+  if (skip32 && !y16) return UPR_ERR_ARG;
   const auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
   if (C % 4 || (uintptr_t)x16 % 8 || y_cs % 4 || y_coff % 4 || !a16(y) ||
       (res && (res_cs % 4 || res_coff % 4 || !a16(res))) || ((uintptr_t)y16 & 7))
@@ -2779,26 +2780,37 @@ int upr_t_bn_apply16h(const void* x16, int M, int C, const float* mean, const fl
   const long long n4 = (long long)M * (C / 4);
   hipLaunchKernelGGL(bn_apply4_kernel<half_t>, dim3(grid_for(n4)), dim3(256), 0, ST(stream), (const half_t*)x16, M, C,
                      C, 0, mean, invstd, gamma, beta, res, res_cs, res_coff, res_post, relu, y, y_cs, y_coff,
-                     (half_t*)y16);
+                     (half_t*)y16, skip32);
   LAUNCH_CHECK();
 }
 
-int upr_t_bn_bwd_fused16(const float* g, int g_cs, int g_coff, const void* x16, const float* mean,
+int upr_t_bn_bwd_fused16(const float* g, const void* g16, int g_cs, int g_coff, const void* x16, const float* mean,
                          const float* invstd, const float* gamma, const float* beta, int relu, int M, int C,
                          double* acc, float* dgamma, float* dbeta, float* dx, int dx_cs, int dx_coff, int accumulate,
                          int batch_stats, void* dx16, int skip32, void* stream) {
-  if (!g || !x16 || !acc || !dx || !gamma || !beta || !mean || !invstd || M <= 0 || C <= 0) return UPR_ERR_ARG;
+  if ((!g && !g16) || !x16 || !acc || !dx || !gamma || !beta || !mean || !invstd || M <= 0 || C <= 0)
+    return UPR_ERR_ARG;
   if (skip32 && (accumulate || !dx16)) return UPR_ERR_ARG;
   const auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-  if (C % 4 || C > 1024 || g_cs % 4 || g_coff % 4 || dx_cs % 4 || dx_coff % 4 || !a16(g) || (uintptr_t)x16 % 8 ||
-      !a16(dx) || !a16(mean) || !a16(invstd) || !a16(gamma) || !a16(beta) || ((uintptr_t)dx16 & 7))
+  if (C % 4 || C > 1024 || dx_cs % 4 || dx_coff % 4 || (uintptr_t)x16 % 8 || !a16(dx) || !a16(mean) ||
+      !a16(invstd) || !a16(gamma) || !a16(beta) || ((uintptr_t)dx16 & 7))
     return UPR_ERR_UNSUPPORTED;
+  if (g16 ? (uintptr_t)g16 % 8 != 0 : (g_cs % 4 || g_coff % 4 || !a16(g))) return UPR_ERR_UNSUPPORTED;
   hipStream_t st = ST(stream);
+  const long long n4 = (long long)M * (C / 4);
+  if (g16) {  // g = the input-gradient conv's fp16 output (compact [M][C])
+    const int rc = chan_reduce2((const half_t*)g16, C, 0, (const half_t*)x16, C, 0, mean, invstd, gamma, beta, M, C,
+                                relu ? 3 : 1, acc + 2 * C, acc, nullptr, 0, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL((bn_bwd_apply4_kernel<half_t, half_t>), dim3(grid_for(n4)), dim3(256), 0, st,
+                       (const half_t*)g16, C, 0, (const half_t*)x16, C, 0, mean, invstd, gamma, acc, M, C, dgamma,
+                       dbeta, dx, dx_cs, dx_coff, accumulate, batch_stats, beta, relu, (half_t*)dx16, skip32);
+    LAUNCH_CHECK();
+  }
   const int rc = chan_reduce2(g, g_cs, g_coff, (const half_t*)x16, C, 0, mean, invstd, gamma, beta, M, C,
                               relu ? 3 : 1, acc + 2 * C, acc, nullptr, 0, st);
   if (rc) return rc;
-  const long long n4 = (long long)M * (C / 4);
-  hipLaunchKernelGGL(bn_bwd_apply4_kernel<half_t>, dim3(grid_for(n4)), dim3(256), 0, st, g, g_cs, g_coff,
+  hipLaunchKernelGGL((bn_bwd_apply4_kernel<half_t, float>), dim3(grid_for(n4)), dim3(256), 0, st, g, g_cs, g_coff,
                      (const half_t*)x16, C, 0, mean, invstd, gamma, acc, M, C, dgamma, dbeta, dx, dx_cs, dx_coff,
                      accumulate, batch_stats, beta, relu, (half_t*)dx16, skip32);
   LAUNCH_CHECK();

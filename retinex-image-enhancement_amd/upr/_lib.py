@@ -147,9 +147,9 @@ SIGNATURES.update({
     "upr_t_bn_bwd_fused": (_i, [_p, _i, _i, _p, _i, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _i, _i, _i, _i, _p,
                                 _p]),
     "upr_t_bn_stats16": (_i, [_p, _i, _i, _p, _p]),
-    "upr_t_bn_apply16h": (_i, [_p, _i, _i, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _i, _i, _p, _p]),
-    "upr_t_bn_bwd_fused16": (_i, [_p, _i, _i, _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _i, _i, _i, _i, _p,
-                                  _i, _p]),
+    "upr_t_bn_apply16h": (_i, [_p, _i, _i, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _i, _i, _p, _i, _p]),
+    "upr_t_bn_bwd_fused16": (_i, [_p, _p, _i, _i, _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _i, _i, _i, _i,
+                                  _p, _i, _p]),
     "upr_t_chan_sum16": (_i, [_p, _i, _i, _p, _i, _p, _p]),
     "upr_t_zero_upsample16h": (_i, [_p, _i, _i, _i, _i, _p, _p]),
     "upr_t_zero_upsample16": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _p]),

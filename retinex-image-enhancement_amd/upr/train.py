@@ -354,6 +354,15 @@ class Conv:
     def flops(self, B, Ho, Wo):
         return 2.0 * B * Ho * Wo * self.Cout * self.Cin * self.kh * self.kw
 
+    def wgrad16_ok(self, W):
+        """Under autocast, this conv's weight gradient on an input of width W runs on
+        the fp16-operand GEMM (it reads the input's fp16 copy only)."""
+        if not (_AMP[0] and self.mfma):
+            return False
+        if self.frozen:
+            return True
+        return ((W + 2 * self.p - self.d * (self.kw - 1) - 1) // self.s + 1) % 64 == 0
+
     def takes16_grad(self):
         """True when every reader of this conv's output gradient in its backward can
         take the gradient's fp16 copy alone (autocast: input gradient on the fp16
@@ -405,14 +414,16 @@ class Conv:
                                        self.Cout, self.kh, self.kw, self.s, self.p, self.d,
                                        ctypes.byref(out.view()), Ho, Wo, int(relu), 0, st), "conv_direct")
 
-    def bwd(self, x, gy, gx=None, x_view=None, mask=None):
+    def bwd(self, x, gy, gx=None, x_view=None, mask=None, gx_only16=False):
         """gy: Act gradient of this conv's output (pre-activation).
         Accumulates the weight / bias gradients; gx (Act, nullable) receives
         the input gradient (overwrite when fresh, else accumulate).
         mask = (a16, cs, only16): the ReLU backward of the activation gx flows
         into, fused into the input-gradient epilogue (a16 = that activation's
         fp16 copy, channel stride cs); gx.t16 then holds the masked gradient and
-        gx.t is left stale when only16.  Returns True when the mask was applied."""
+        gx.t is left stale when only16.  Returns True when the mask was applied.
+        gx_only16: the input gradient's reader (a BatchNorm backward) takes its fp16
+        copy: under autocast gx gets gx.t16 and no fp32 store when fresh."""
         lib, st = L.lib(), _stream()
         if x_view is not None:
             xv, B, H, W = x_view
@@ -433,6 +444,7 @@ class Conv:
                     dy16 = gy.t16 if self.amp and gy.t16_grad and gy.coff == 0 and gy.cs == gy.C == self.Cout \
                         else None
                     assert dy16 is not None or not gy.stale32, "fp16-only gradient without the fp16 weight gradient"
+                    assert x16 is not None or not x.stale32, "fp16-only input without the fp16 weight gradient"
                     _chk(lib.upr_t_conv_wgrad_into(_fp(x.t), _p(x16) if self.amp else None, B, H, W, self.Cin, x.cs,
                                                    x.coff, _fp(gy.t), _p(dy16), Ho, Wo, self.Cout, gy.cs, gy.coff,
                                                    self.kh, self.kw, self.s, self.p, self.d, _p(gw), st),
@@ -497,8 +509,10 @@ class Conv:
                 pad_t = self.d * (self.kh - 1) - self.p
                 assert src16 is not None or not gy.stale32, "fp16-only gradient without the fp16 input gradient"
                 if self.amp:
+                    o16 = bool(gx_only16) and not acc and gx.coff == 0 and gx.cs == gx.C == self.Cin
                     self._mfma16(src, B, sH, sW, self.Cout, scs, scoff, self.wt16, None, self.Cin, self.kh, self.kw, 1,
-                                 pad_t, self.d, gx if acc else None, False, gx, x16=src16)
+                                 pad_t, self.d, gx if acc else None, False, gx, x16=src16, keep16=o16, only16=o16)
+                    gx.t16_grad = gx.t16 is not None
                 else:
                     _chk(lib.upr_t_conv_mfma(_fp(src), B, sH, sW, self.Cout, scs, scoff, _p(self.wt), None, self.Cin,
                                              self.kh, self.kw, 1, pad_t, self.d, gx.ptr() if acc else None,
@@ -625,7 +639,10 @@ class BN:
         # per-channel sums + the two-stage reduction's partial slots (upr_t_reduce_acc_doubles)
         self.acc = torch.empty((L.lib().upr_t_reduce_acc_doubles(self.C),), dtype=torch.float64, device=dev)
 
-    def fwd(self, x, relu=False, out=None, res=None, res_post=False):
+    def fwd(self, x, relu=False, out=None, res=None, res_post=False, only16=False):
+        """only16: under autocast every reader of the output takes its fp16 copy (convs
+        whose weight gradients run on the fp16-operand GEMM): the fp32 output is not
+        written (out.stale32)."""
         lib, st = L.lib(), _stream()
         m = self.m
         # under autocast x is an fp16 conv's output: its fp16 copy holds the same values
@@ -650,11 +667,14 @@ class BN:
         # under autocast the consumer is an fp16 conv: write its fp16 input copy here
         y16 = _h16(out.M * self.C, out.t.device) if _AMP[0] and out.coff == 0 and out.cs == self.C else None
         rc = L.UPR_ERR_UNSUPPORTED
+        skip32 = int(bool(only16) and y16 is not None)
         if x16 is not None:
             rc = lib.upr_t_bn_apply16h(_p(x16), x.M, self.C, _p(self.mean), _p(self.invstd), _p(m.weight),
                                        _p(m.bias), res.ptr() if res is not None else None,
                                        res.cs if res is not None else 0, 0, int(res_post), int(relu), _fp(out.t),
-                                       out.cs, out.coff, _p(y16), st)
+                                       out.cs, out.coff, _p(y16), skip32, st)
+            if rc != 0:
+                skip32 = 0
         if rc == L.UPR_ERR_UNSUPPORTED:
             assert not x.stale32, "fp16-only BN input without an fp16 apply path"
             rc = lib.upr_t_bn_apply16(x.ptr(), x.M, self.C, x.cs, 0, _p(self.mean), _p(self.invstd), _p(m.weight),
@@ -663,6 +683,7 @@ class BN:
                                       out.cs, out.coff, _p(y16), st)
         _chk(rc, "bn_apply")
         out.t16 = y16
+        out.stale32 = bool(skip32)
         self.x = x
         self.out_act = out
         self.batch_stats = bool(m.training)  # the backward follows the statistics this forward used
@@ -685,8 +706,11 @@ class BN:
             acc = 0 if gx.fresh else 1
             rc = L.UPR_ERR_UNSUPPORTED
             skip32 = int(bool(only16) and dx16 is not None and acc == 0)
+            # g's fp16 copy (the input-gradient conv's fp16 output) when it has one
+            g16 = g.t16 if g.t16_grad and g.coff == 0 and g.cs == g.C == self.C else None
             if self.x16 is not None:
-                rc = lib.upr_t_bn_bwd_fused16(_fp(g.t), g.cs, g.coff, _p(self.x16), _p(self.mean), _p(self.invstd),
+                rc = lib.upr_t_bn_bwd_fused16(_fp(g.t), _p(g16), g.cs, g.coff, _p(self.x16), _p(self.mean),
+                                              _p(self.invstd),
                                               _p(m.weight), _p(m.bias), int(relu), x.M, self.C, _p(self.acc),
                                               _p(m.weight.grad), _p(m.bias.grad), _fp(gx.t), gx.cs, gx.coff, acc,
                                               int(self.batch_stats), _p(dx16), skip32, st)
@@ -695,7 +719,7 @@ class BN:
                     gx.t16, gx.t16_grad, gx.stale32 = dx16, dx16 is not None, bool(skip32)
                     return
             if rc == L.UPR_ERR_UNSUPPORTED:
-                assert not x.stale32, "fp16-only BN input without an fp16 backward path"
+                assert not x.stale32 and not g.stale32, "fp16-only BN operand without an fp16 backward path"
                 rc = lib.upr_t_bn_bwd_fused(_fp(g.t), g.cs, g.coff, x.ptr(), x.cs, _p(self.mean), _p(self.invstd),
                                             _p(m.weight), _p(m.bias), int(relu), x.M, self.C, _p(self.acc),
                                             _p(m.weight.grad), _p(m.bias.grad), _fp(gx.t), gx.cs, gx.coff, acc,
@@ -840,7 +864,8 @@ class ResBlockT:
         self.x = x
         # a conv whose only reader is a BatchNorm keeps its output in fp16 only under
         # autocast (the BN reads the fp16 copy: the same values)
-        self.a1 = self.bn1.fwd(self.conv1.fwd(x, only16=True), relu=True)
+        c1 = self.conv1.fwd(x, only16=True)
+        self.a1 = self.bn1.fwd(c1, relu=True, only16=self.conv2.wgrad16_ok(c1.W))
         c2 = self.conv2.fwd(self.a1, only16=True)
         sc = self.sbn.fwd(self.sconv.fwd(x, only16=True)) if self.proj else x
         self.out = self.bn2.fwd(c2, relu=True, res=sc)
@@ -857,7 +882,7 @@ class ResBlockT:
         else:
             add_into(gx, g)
         g_a1 = Act.new(self.a1.B, self.a1.H, self.a1.W, self.a1.C, g.t.device)
-        self.conv2.bwd(self.a1, g_c2, g_a1)
+        self.conv2.bwd(self.a1, g_c2, g_a1, gx_only16=True)
         g_c1 = Act.new(g_a1.B, g_a1.H, g_a1.W, g_a1.C, g.t.device)
         self.bn1.bwd(g_a1, g_c1, relu=True, only16=self.conv1.takes16_grad())
         self.conv1.bwd(self.x, g_c1, gx)
@@ -880,13 +905,14 @@ class PreActResBlockT:
         self.x = x
         self.o = self.bn1.fwd(x, relu=True)
         sc = self.sbn.fwd(self.sconv.fwd(self.o, only16=True)) if self.proj else x
-        self.a2 = self.bn2.fwd(self.conv1.fwd(self.o, only16=True), relu=True)
+        c1 = self.conv1.fwd(self.o, only16=True)
+        self.a2 = self.bn2.fwd(c1, relu=True, only16=self.conv2.wgrad16_ok(c1.W))
         return self.conv2.fwd(self.a2, res=sc)
 
     def bwd(self, g, gx):
         dev = g.t.device
         g_a2 = Act.new(self.a2.B, self.a2.H, self.a2.W, self.a2.C, dev)
-        self.conv2.bwd(self.a2, g, g_a2)
+        self.conv2.bwd(self.a2, g, g_a2, gx_only16=True)
         g_c1 = Act.new(g_a2.B, g_a2.H, g_a2.W, g_a2.C, dev)
         self.bn2.bwd(g_a2, g_c1, relu=True, only16=self.conv1.takes16_grad())
         g_o = Act.new(self.o.B, self.o.H, self.o.W, self.o.C, dev)
@@ -997,7 +1023,8 @@ class UpBlockT:
         """skip=None: UpBlock.forward alone (model.py:271-274, no skip add)."""
         self.x = x
         self.u = self.up.fwd(x)
-        self.a1 = self.b1.fwd(self.c1.fwd(self.u, only16=True), relu=True)
+        c1 = self.c1.fwd(self.u, only16=True)
+        self.a1 = self.b1.fwd(c1, relu=True, only16=self.c2.wgrad16_ok(c1.W))
         self.a2 = self.b2.fwd(self.c2.fwd(self.a1, only16=True), relu=True)
         if skip is None:
             return self.a2
@@ -1012,7 +1039,7 @@ class UpBlockT:
         g_c2 = Act.new(g.B, g.H, g.W, g.C, dev)
         self.b2.bwd(g, g_c2, relu=True, only16=self.c2.takes16_grad())
         g_a1 = Act.new(g.B, g.H, g.W, g.C, dev)
-        self.c2.bwd(self.a1, g_c2, g_a1)
+        self.c2.bwd(self.a1, g_c2, g_a1, gx_only16=True)
         g_c1 = Act.new(g.B, g.H, g.W, g.C, dev)
         self.b1.bwd(g_a1, g_c1, relu=True, only16=self.c1.takes16_grad())
         g_u = Act.new(g.B, g.H, g.W, g.C, dev)
