@@ -1041,7 +1041,8 @@ __device__ __forceinline__ void static_steps(F&& f, std::integer_sequence<int, S
 __device__ __attribute__((aligned(256))) uint4 g_halo_zero[1024];
 
 // ABL (timing ablations only, UPR_HW4_ABL; results are garbage): bit 0 drops
-// the main loop's DMA (region rows + B stages), bit 1 its LDS fragment reads
+// the main loop's DMA (region rows + B stages), bit 1 its LDS fragment reads,
+// bit 2 the epilogue, bit 3 the MFMAs
 template <int BN, int W, int NCH, int ABL = 0>
 __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
   using HC = Halo3Cfg<BN, W>;
@@ -1173,6 +1174,7 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
     }
   };
   auto mm = [&](auto S_, f16x8_w (&af)[WM], const f16x8_w (&bf)[WN]) {
+    if constexpr ((ABL & 8) != 0) return;
 #pragma unroll
     for (int a = 0; a < WM; ++a) {
 #pragma unroll
@@ -1237,7 +1239,11 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // every wave is done with the ring and stages before the epilogue reuses LDS
 
-  wide_epilogue<BN, WM, WN, HC::WAVES_M, BM, true, W>(op, acc, smem, m0, n0, M, HW);
+  if constexpr ((ABL & 4) != 0) {
+    if (acc[0][0][0] == 12345.f) wide_epilogue<BN, WM, WN, HC::WAVES_M, BM, true, W>(op, acc, smem, m0, n0, M, HW);
+  } else {
+    wide_epilogue<BN, WM, WN, HC::WAVES_M, BM, true, W>(op, acc, smem, m0, n0, M, HW);
+  }
 }
 
 template <int BN, int W, int NCH, int ABL = 0>
@@ -1268,6 +1274,10 @@ static int launch_hwide34(const ConvOp& op, hipStream_t st) {
       if (nch == 4 && abl == 1) return launch_hwide4<BN, W, 4, 1>(op, st);
       if (nch == 4 && abl == 2) return launch_hwide4<BN, W, 4, 2>(op, st);
       if (nch == 4 && abl == 3) return launch_hwide4<BN, W, 4, 3>(op, st);
+      if (nch == 4 && abl == 4) return launch_hwide4<BN, W, 4, 4>(op, st);
+      if (nch == 4 && abl == 7) return launch_hwide4<BN, W, 4, 7>(op, st);
+      if (nch == 4 && abl == 8) return launch_hwide4<BN, W, 4, 8>(op, st);
+      if (nch == 4 && abl == 12) return launch_hwide4<BN, W, 4, 12>(op, st);
       if (nch == 4) return launch_hwide4<BN, W, 4>(op, st);
     }
   }
