@@ -1040,10 +1040,151 @@ __device__ __forceinline__ void static_steps(F&& f, std::integer_sequence<int, S
 // (< 8 pixels x 1024 channels x 2 B), so a 16 KiB zero block
 __device__ __attribute__((aligned(256))) uint4 g_halo_zero[1024];
 
+// Direct-store epilogue of conv_hwide4_kernel<DS = true> (no LDS parking, no
+// block barriers).  The main loop ran the MFMAs with the operands swapped
+// (weights first), so a lane's accumulator holds 4 consecutive CHANNELS of one
+// pixel, and the B tile's rows were DMA'd in the order hw4_perm32 below, so
+// tiles 2p / 2p + 1 of a lane hold channels 32p + 8fg + 0..3 / + 4..7 of pixel
+// fr: 8 consecutive channels -> one 16-byte store per (fragment, pair), the
+// scale / bias / residual / ReLU / out2 / pool arithmetic in registers.  The
+// LDS epilogue parked 256 KiB of fp32 per block in 4 barrier-separated passes
+// (~20% of the bottleneck conv, profiles/r3_hwide4_bneck_ablations_v2.txt).
+__device__ __forceinline__ int hw4_perm32(int r) {
+  // LDS row r of a 32-row group = (b' r4 | i3 r3 r2 | i1 r1 r0) holds channel i3*8 + b'*4 + i1
+  return (r & ~31) | (((r >> 2) & 3) << 3) | (((r >> 4) & 1) << 2) | (r & 3);
+}
+
+template <int BN, int WM, int WN, int WAVES_M, int W>
+__device__ __forceinline__ void hw4_direct_epilogue(const ConvOp& op, f32x4_w (&acc)[WM][WN], int m0, int n0,
+                                                    int wm, int wn, int lane, const f16x8_w (&rv0)[WM],
+                                                    unsigned char* smem) {
+  constexpr int CW = W / WAVES_M, FPR = CW / 16, NP = WN / 2;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int img = m0 / (op.Ho * W);
+  const int cb = n0 + wn * WN * 16 + fg * 8;  // channel of pair p: cb + 32p
+  const int mb = m0 + CW * wm + fr;          // pixel of fragment a: mb + (a / FPR) * W + (a % FPR) * 16
+  const half_t* rpf = (const half_t*)(op.res1 ? op.res1 : op.res2);
+  const int rcs = op.res1 ? op.res1_cs : op.res2_cs;
+  // residual rows: pair 0's were loaded by the kernel during its last K steps
+  // (hw4_res_load), pair p + 1's load while pair p is finished (each
+  // fragment's pair-p accumulators die as its pair-p + 1 residual arrives)
+  f16x8_w rv[NP][WM];
+  auto rload = [&](int p, int a) {
+    return *(const f16x8_w*)(rpf + (size_t)(mb + (a / FPR) * W + (a % FPR) * 16) * rcs + cb + 32 * p);
+  };
+#pragma unroll
+  for (int a = 0; a < WM; ++a) rv[0][a] = rv0[a];
+  float psum[NP][8];
+#pragma unroll
+  for (int p = 0; p < NP; ++p)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) psum[p][e] = 0.f;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int c = cb + 32 * p;
+    float sc[8], bi[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { sc[e] = 1.f; bi[e] = 0.f; }
+    if (op.scale) {
+      const f32x4_w s0 = *(const f32x4_w*)(op.scale + c), s1 = *(const f32x4_w*)(op.scale + c + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { sc[e] = s0[e]; sc[e + 4] = s1[e]; }
+    }
+    if (op.bias) {
+      const f32x4_w b0 = *(const f32x4_w*)(op.bias + c), b1 = *(const f32x4_w*)(op.bias + c + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { bi[e] = b0[e]; bi[e + 4] = b1[e]; }
+    }
+    if (op.img_bias) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bi[e] += op.img_bias[img * op.N + c + e];
+    }
+#pragma unroll
+    for (int a = 0; a < WM; ++a) {
+      const size_t m = (size_t)(mb + (a / FPR) * W + (a % FPR) * 16);
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = acc[a][2 * p][e] * sc[e] + bi[e];
+        v[e + 4] = acc[a][2 * p + 1][e] * sc[e + 4] + bi[e + 4];
+      }
+      if (rpf && p + 1 < NP) rv[p + 1][a] = rload(p + 1, a);
+      if (op.res1) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += (float)rv[p][a][e];
+      }
+      if (op.relu) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      if (op.res2) {
+        const f16x8_w r = op.res1 ? *(const f16x8_w*)((const half_t*)op.res2 + m * op.res2_cs + c) : rv[p][a];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += (float)r[e];
+      }
+      f16x8_w o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (half_t)v[e];
+      *(f16x8_w*)((half_t*)op.out + m * op.out_cs + op.out_coff + c) = o;
+      if (op.out2) {
+        const f32x4_w s0 = *(const f32x4_w*)(op.pre2_scale + c), s1 = *(const f32x4_w*)(op.pre2_scale + c + 4);
+        const f32x4_w h0 = *(const f32x4_w*)(op.pre2_shift + c), h1 = *(const f32x4_w*)(op.pre2_shift + c + 4);
+        f16x8_w q;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          q[e] = (half_t)fmaxf(__builtin_fmaf((float)o[e], s0[e], h0[e]), 0.f);
+          q[e + 4] = (half_t)fmaxf(__builtin_fmaf((float)o[e + 4], s1[e], h1[e]), 0.f);
+        }
+        *(f16x8_w*)((half_t*)op.out2 + m * op.out2_cs + c) = q;
+      }
+      if (op.pool) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) psum[p][e] += (float)o[e];
+      }
+    }
+  }
+  if (op.pool) {
+    // per-lane partial sums -> LDS [16 fr][WAVES_M][BN] (the main loop is done
+    // with LDS: the kernel waited for its DMAs and a barrier precedes this),
+    // then one thread per channel adds its 16 * WAVES_M partials in a fixed
+    // order and issues ONE fixed-point atomic: 256 coalesced atomics per block
+    float* Ps = (float*)smem;
+    const int cl = cb - n0;
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) Ps[(fr * WAVES_M + wm) * BN + cl + 32 * p + e] = psum[p][e];
+    __syncthreads();
+    const int tid = threadIdx.x;
+    if (tid < BN) {
+      float t = 0.f;
+      for (int g = 0; g < 16 * WAVES_M; ++g) t += Ps[g * BN + tid];
+      pool_add(op.pool, (size_t)img * op.N + n0 + tid, t);
+    }
+  }
+}
+
+// pair-0 residual rows of a lane (see hw4_direct_epilogue), issued by the
+// kernel after the DMAs of its second-to-last K step: the loads fly under the
+// last 1.5 steps of MFMAs, and no counted vmcnt wait of the loop follows them
+template <int WM, int WN, int WAVES_M, int W>
+__device__ __forceinline__ void hw4_res_load(const ConvOp& op, f16x8_w (&rv0)[WM], int m0, int n0, int wm, int wn,
+                                             int lane) {
+  constexpr int CW = W / WAVES_M, FPR = CW / 16;
+  const half_t* rpf = (const half_t*)(op.res1 ? op.res1 : op.res2);
+  if (!rpf) return;
+  const int rcs = op.res1 ? op.res1_cs : op.res2_cs;
+  const int cb = n0 + wn * WN * 16 + (lane >> 4) * 8;
+  const int mb = m0 + CW * wm + (lane & 15);
+#pragma unroll
+  for (int a = 0; a < WM; ++a) rv0[a] = *(const f16x8_w*)(rpf + (size_t)(mb + (a / FPR) * W + (a % FPR) * 16) * rcs + cb);
+}
+
 // ABL (timing ablations only, UPR_HW4_ABL; results are garbage): bit 0 drops
 // the main loop's DMA (region rows + B stages), bit 1 its LDS fragment reads,
-// bit 2 the epilogue, bit 3 the MFMAs
-template <int BN, int W, int NCH, int ABL = 0>
+// bit 2 the epilogue, bit 3 the MFMAs.  DS: operand-swapped MFMAs + the
+// direct-store epilogue above (hw4_ds_ok decides per op)
+template <int BN, int W, int NCH, int ABL = 0, bool DS = false>
 __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
   using HC = Halo3Cfg<BN, W>;
   constexpr int WM = HC::WM, WN = HC::WN, BM = HC::BM, NBS = HC::NBS;
@@ -1119,14 +1260,29 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
                               (unsigned)((q8 * op.Kpad + ((qc ^ ((4 + sw_lane) & 7)) * 8)) * 2)};
   const unsigned char* bbase =
       (const unsigned char*)((const half_t*)op.W + (size_t)(n0 + wave * (BN / 8)) * op.Kpad + sg.kbase);
+  // DS: LDS row R of the B tile is filled from weight row hw4_perm32(R); the
+  // lane offsets are taken from the row's 32-row group base (unsigned)
+  const int g32 = (wave * (BN / 8)) & ~31;
+  const unsigned char* bbase_ds =
+      (const unsigned char*)((const half_t*)op.W + (size_t)(n0 + g32) * op.Kpad + sg.kbase);
+  unsigned voff_ds[HC::BJ];
+#pragma unroll
+  for (int j = 0; j < HC::BJ; ++j) {
+    const int R = wave * (BN / 8) + j * 8 + q8;
+    voff_ds[j] = (unsigned)(((hw4_perm32(R) - g32) * op.Kpad + ((qc ^ ((4 * j + sw_lane) & 7)) * 8)) * 2);
+  }
   // B of step (c, t) into stage stg; steps past the end re-read the last
   // step's rows into a stage nobody reads again (uniform DMA count)
   auto issue_b = [&](int stg, int c, int t) {
     unsigned char* Bs = smem + HC::RING + stg * HC::B_BYTES;
     const int kb = t * Cin + c * WBK;
 #pragma unroll
-    for (int j = 0; j < HC::BJ; ++j)
-      glds16(bbase + ((size_t)j * 8 * op.Kpad + kb) * 2 + voff_b[j & 1], Bs + (wave * (BN / 8) + j * 8) * 128);
+    for (int j = 0; j < HC::BJ; ++j) {
+      if constexpr (DS)
+        glds16(bbase_ds + (size_t)kb * 2 + voff_ds[j], Bs + (wave * (BN / 8) + j * 8) * 128);
+      else
+        glds16(bbase + ((size_t)j * 8 * op.Kpad + kb) * 2 + voff_b[j & 1], Bs + (wave * (BN / 8) + j * 8) * 128);
+    }
   };
 
   f32x4_w acc[WM][WN];
@@ -1178,13 +1334,18 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
 #pragma unroll
     for (int a = 0; a < WM; ++a) {
 #pragma unroll
-      for (int b = 0; b < WN; ++b)
-        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a], bf[b], acc[a][b], 0, 0, 0);
+      for (int b = 0; b < WN; ++b) {
+        if constexpr (DS)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[b], af[a], acc[a][b], 0, 0, 0);
+        else
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a], bf[b], acc[a][b], 0, 0, 0);
+      }
     }
   };
   // hipcc's own MFMA / fragment-read schedule: the sched_group_barrier
   // interleave of hwide3 made the straight-line steps spill (118 VGPRs)
   f16x8_w a0[WM], b0[WN], a1[WM], b1[WN];
+  f16x8_w rv0[WM];  // DS: pair-0 residual rows (hw4_res_load)
   region_row(0, 0);
   region_row(0, 1);
   region_row(0, 2);
@@ -1227,6 +1388,7 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
             issue_b(S % NBS, bc, bt);
             issue_rows(nc, nt);
           }
+          if constexpr (DS && S == TOTAL - 2) hw4_res_load<WM, WN, HC::WAVES_M, W>(op, rv0, m0, n0, wm, wn, lane);
           if constexpr (!(ABL & 2)) rd(std::integral_constant<int, n>{}, std::integral_constant<int, 0>{}, a0, b0);
           mm(S_, a1, b1);
         } else {
@@ -1236,6 +1398,25 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
         }
       },
       std::make_integer_sequence<int, TOTAL>{});
+  if constexpr (DS) {
+    // the last steps' (unread) DMAs land before the block ends; with a
+    // residual, the compiler's own wait for the residual loads (issued after
+    // them, in order) already covers them
+    if (!op.res1 && !op.res2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (op.pool) {
+      // the pool partials reuse LDS: every wave's DMAs landed, every wave's reads done
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    if constexpr ((ABL & 4) != 0) {
+      if (acc[0][0][0] == 12345.f) hw4_direct_epilogue<BN, WM, WN, HC::WAVES_M, W>(op, acc, m0, n0, wm, wn, lane, rv0, smem);
+    } else {
+      hw4_direct_epilogue<BN, WM, WN, HC::WAVES_M, W>(op, acc, m0, n0, wm, wn, lane, rv0, smem);
+    }
+    if constexpr ((ABL & 4) != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return;
+  }
+  // the last steps' (unread) DMAs land before the epilogue reuses LDS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // every wave is done with the ring and stages before the epilogue reuses LDS
 
@@ -1246,19 +1427,40 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
   }
 }
 
-template <int BN, int W, int NCH, int ABL = 0>
-static int launch_hwide4(const ConvOp& op, hipStream_t st) {
+template <int BN, int W, int NCH, int ABL = 0, bool DS = false>
+static int launch_hwide4_k(const ConvOp& op, hipStream_t st) {
   using HC = Halo3Cfg<BN, W>;
   static bool attr_set = false;
   if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute((const void*)conv_hwide4_kernel<BN, W, NCH, ABL>,
+    const hipError_t e = hipFuncSetAttribute((const void*)conv_hwide4_kernel<BN, W, NCH, ABL, DS>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, HC::LDS);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
   const int grid = (op.B * op.Ho * W / HC::BM) * (op.N / BN);
-  hipLaunchKernelGGL((conv_hwide4_kernel<BN, W, NCH, ABL>), dim3(grid), dim3(512), HC::LDS, st, op);
+  hipLaunchKernelGGL((conv_hwide4_kernel<BN, W, NCH, ABL, DS>), dim3(grid), dim3(512), HC::LDS, st, op);
   return (int)hipGetLastError();
+}
+
+// the direct-store epilogue takes the fp16 NHWC outputs with 16-byte aligned
+// channel runs (every inference op of the graph); the autocast fp32 outputs
+// (out32 / res32 / mask16) keep the LDS epilogue.  UPR_HW4_DS=0: always LDS (A/B)
+static bool hw4_ds_ok(const ConvOp& op) {
+  static const int en = env_int("UPR_HW4_DS", 1);
+  if (!en || op.out32 || op.store != kStoreNHWC) return false;
+  if ((uintptr_t)op.out % 16 || op.out_cs % 8 || op.out_coff % 8) return false;
+  if (op.res1 && ((uintptr_t)op.res1 % 16 || op.res1_cs % 8)) return false;
+  if (op.res2 && ((uintptr_t)op.res2 % 16 || op.res2_cs % 8)) return false;
+  if (op.out2 && op.out2_cs % 8) return false;
+  if (((uintptr_t)op.scale | (uintptr_t)op.bias | (uintptr_t)op.pre2_scale | (uintptr_t)op.pre2_shift) % 16) return false;
+  return true;
+}
+
+template <int BN, int W, int NCH, int ABL = 0>
+static int launch_hwide4(const ConvOp& op, hipStream_t st) {
+  // the timing ablations (ABL != 0) exist for the direct-store form only
+  if (ABL != 0 || hw4_ds_ok(op)) return launch_hwide4_k<BN, W, NCH, ABL, true>(op, st);
+  return launch_hwide4_k<BN, W, NCH, 0, false>(op, st);
 }
 
 // UPR_HW4=0 keeps the runtime-cursor hwide3 kernel (A/B timing)
@@ -1279,6 +1481,13 @@ static int launch_hwide34(const ConvOp& op, hipStream_t st) {
       if (nch == 4 && abl == 8) return launch_hwide4<BN, W, 4, 8>(op, st);
       if (nch == 4 && abl == 12) return launch_hwide4<BN, W, 4, 12>(op, st);
       if (nch == 4) return launch_hwide4<BN, W, 4>(op, st);
+    } else {
+      // dec3 (W 128, 2 chunks) on the direct-store form only (its LDS-epilogue
+      // straight line spilled 40 VGPRs): dec3.conv.0 shape 0.196 -> 0.153 ms,
+      // conv.3 (+ residual) 0.223 -> 0.186 (same-box A/B, profiles/r3_hw4_ds_ab.txt);
+      // UPR_HW4_128=0 keeps them on hwide3
+      static const int v128 = env_int("UPR_HW4_128", 1);
+      if (v128 && nch == 2 && hw4_ds_ok(op)) return launch_hwide4_k<BN, W, 2, 0, true>(op, st);
     }
   }
   return launch_hwide3<BN, W>(op, st);

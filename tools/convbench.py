@@ -26,7 +26,9 @@ SHAPES = {
     "dec2": (32, 256, 256, 64, 64, 3, 1, 1, 1, True),
     "dec2p": (32, 256, 256, 64, 64, 3, 1, 1, 1, False),  # dec2.conv.0-like (ReLU, no residual)
     "dec3": (32, 128, 128, 128, 128, 3, 1, 1, 1, True),
+    "dec3p": (32, 128, 128, 128, 128, 3, 1, 1, 1, False),  # dec3.conv.0-like (ReLU, no residual)
     "bneck": (32, 64, 64, 256, 256, 3, 1, 1, 1, False),
+    "bneckr": (32, 64, 64, 256, 256, 3, 1, 1, 1, True),   # bottleneck conv2 (+ residual)
     "enc1s2": (32, 512, 512, 32, 64, 3, 2, 1, 1, False),
     "d2": (32, 512, 512, 32, 32, 3, 1, 2, 2, False),
     "aspp6": (32, 64, 64, 256, 256, 3, 1, 6, 6, False),
