@@ -1183,8 +1183,15 @@ __device__ __forceinline__ void hw4_res_load(const ConvOp& op, f16x8_w (&rv0)[WM
 // ABL (timing ablations only, UPR_HW4_ABL; results are garbage): bit 0 drops
 // the main loop's DMA (region rows + B stages), bit 1 its LDS fragment reads,
 // bit 2 the epilogue, bit 3 the MFMAs.  DS: operand-swapped MFMAs + the
-// direct-store epilogue above (hw4_ds_ok decides per op)
-template <int BN, int W, int NCH, int ABL = 0, bool DS = false>
+// direct-store epilogue above (hw4_ds_ok decides per op).
+// DL: dilated 3x3 (the ASPP branches, dilation = padding = d, any d < W): the
+// three tap rows of a chunk read three disjoint 4-row bands, so the K loop is
+// (tap row, chunk, tap column) and each (tap row, chunk) REGION of 4 rows is
+// DMA'd once into one half of the 8-row ring (region k -> half k & 1, issued
+// after the barrier that ends region k - 1's reads, three steps ahead of its
+// first reader) and read by its 3 taps at per-lane column offsets +-d (lanes
+// whose column falls outside the image row read through the void LDS base)
+template <int BN, int W, int NCH, int ABL = 0, bool DS = false, bool DL = false>
 __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
   using HC = Halo3Cfg<BN, W>;
   constexpr int WM = HC::WM, WN = HC::WN, BM = HC::BM, NBS = HC::NBS;
@@ -1250,6 +1257,26 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
       else if (t == 6) region_row(c + 1, 3);
     }
   };
+  // DL: region k = (tap row k / NCH, chunk k % NCH), 4 rows into ring half k & 1;
+  // regions past the last re-read the last one into the free half (uniform DMA count)
+  constexpr int NREG = 3 * NCH;
+  const int dil = sg.dil;
+  auto region_dl = [&](int k) {  // k compile-time at every call site
+    const int kk = k < NREG ? k : NREG - 1;
+    const int ty = kk / NCH, cc = kk % NCH;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int iy = oy0 + (ty - 1) * dil + r;
+      const bool in = (unsigned)iy < (unsigned)H;
+      unsigned char* dst = smem + ((k & 1) * 4 + r) * HC::ROW + wave * 1024;
+#pragma unroll
+      for (int pc = 0; pc < HC::RP; ++pc) {
+        const unsigned char* ub = in ? abase + (size_t)iy * row_bytes + (size_t)pc * 64 * cs * 2 + cc * WBK * 2
+                                     : (const unsigned char*)g_halo_zero;
+        glds16(ub + voff_a, dst + pc * 8192);
+      }
+    }
+  };
 
   const int q8 = lane >> 3;
   const int qc = lane & 7;
@@ -1273,9 +1300,9 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
   }
   // B of step (c, t) into stage stg; steps past the end re-read the last
   // step's rows into a stage nobody reads again (uniform DMA count)
-  auto issue_b = [&](int stg, int c, int t) {
+  auto issue_b = [&](int stg, int c, int t) {  // DL: c = region, t = tap column
     unsigned char* Bs = smem + HC::RING + stg * HC::B_BYTES;
-    const int kb = t * Cin + c * WBK;
+    const int kb = DL ? ((c / NCH) * 3 + t) * Cin + (c % NCH) * WBK : t * Cin + c * WBK;
 #pragma unroll
     for (int j = 0; j < HC::BJ; ++j) {
       if constexpr (DS)
@@ -1309,12 +1336,36 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
   }
   aofs_e[0] = (wm == 0 && fr == 0) ? kLdsVoid : aofs[0];
   aofs_e[1] = (wm == HC::WAVES_M - 1 && fr == 15) ? kLdsVoid : aofs[2];
+  // DL: per (tap column, fragment of the row) lane offsets, void outside the row
+  int aofs_d[DL ? 3 : 1][DL ? FPR : 1];
+  if constexpr (DL) {
+#pragma unroll
+    for (int tx = 0; tx < 3; ++tx)
+#pragma unroll
+      for (int f = 0; f < FPR; ++f) {
+        const int p = CW * wm + f * 16 + fr + (tx - 1) * dil;
+        aofs_d[tx][f] = (unsigned)p < (unsigned)W ? p * 128 + ((fg ^ halo_swz(p)) * 16) : kLdsVoid;
+      }
+  }
   bofs = HC::RING + (wn * WN * 16 + fr) * 128 + ((fg ^ rsw) * 16);
 
   // fragments of step S, half KK
   auto rd = [&](auto S_, auto KK_, f16x8_w (&af)[WM], f16x8_w (&bf)[WN]) {
     constexpr int S = decltype(S_)::value, KK = decltype(KK_)::value;
     constexpr int c = S / 9, t = S % 9, ty = t / 3, tx = t % 3, stg = S % NBS;
+    if constexpr (DL) {
+      constexpr int h = (S / 3) & 1, dtx = S % 3;
+      const int bo = KK ? (bofs ^ 64) : bofs;
+#pragma unroll
+      for (int b = 0; b < WN; ++b)
+        bf[b] = *(const f16x8_w*)(smem + bo + stg * HC::B_BYTES + b * 16 * 128);
+#pragma unroll
+      for (int a = 0; a < WM; ++a) {
+        const int ao = KK ? (aofs_d[dtx][a % FPR] ^ 64) : aofs_d[dtx][a % FPR];
+        af[a] = *(const f16x8_w*)(smem + ao + (h * 4 + a / FPR) * HC::ROW);
+      }
+      return;
+    }
     const int bo = KK ? (bofs ^ 64) : bofs, ao = KK ? (aofs[tx] ^ 64) : aofs[tx];
     int aoe = ao;
     if constexpr (tx == 0) aoe = KK ? (aofs_e[0] ^ 64) : aofs_e[0];
@@ -1346,10 +1397,15 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
   // interleave of hwide3 made the straight-line steps spill (118 VGPRs)
   f16x8_w a0[WM], b0[WN], a1[WM], b1[WN];
   f16x8_w rv0[WM];  // DS: pair-0 residual rows (hw4_res_load)
-  region_row(0, 0);
-  region_row(0, 1);
-  region_row(0, 2);
-  region_row(0, 3);
+  static_assert(!DL || (DS && NBS == 3), "dilated form: direct-store epilogue, three B stages");
+  if constexpr (DL) {
+    region_dl(0);
+  } else {
+    region_row(0, 0);
+    region_row(0, 1);
+    region_row(0, 2);
+    region_row(0, 3);
+  }
   issue_b(0, 0, 0);
   if constexpr (NBS == 3) {
     issue_b(1, 0, 1);
@@ -1358,8 +1414,13 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __builtin_amdgcn_s_barrier();
-  issue_b(NBS - 1, (NBS - 1) / 9, (NBS - 1) % 9);  // B(NBS - 1)
-  issue_rows(0, 0);
+  if constexpr (DL) {
+    issue_b(2, 0, 2);  // B(2)
+    region_dl(1);
+  } else {
+    issue_b(NBS - 1, (NBS - 1) / 9, (NBS - 1) % 9);  // B(NBS - 1)
+    issue_rows(0, 0);
+  }
   rd(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, a0, b0);
   if constexpr ((ABL & 2) != 0) rd(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{}, a1, b1);
   static_steps(
@@ -1370,8 +1431,8 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
           constexpr int n = S + 1, nc = n / 9, nt = n % 9;
           // B DMA of step S + NBS (clamped past the end) into the stage step S read
           constexpr int bstep = S + NBS;
-          constexpr int bc = bstep / 9 < NCH ? bstep / 9 : NCH - 1;
-          constexpr int bt = bstep / 9 < NCH ? bstep % 9 : 8;
+          constexpr int bc = DL ? (bstep < TOTAL ? bstep / 3 : NREG - 1) : (bstep / 9 < NCH ? bstep / 9 : NCH - 1);
+          constexpr int bt = DL ? (bstep < TOTAL ? bstep % 3 : 2) : (bstep / 9 < NCH ? bstep % 9 : 8);
           if constexpr (!(ABL & 2)) rd(S_, std::integral_constant<int, 1>{}, a1, b1);
           mm(S_, a0, b0);
           // RAW: B(S + 1) and the region rows step S + 1 reads have landed: in
@@ -1379,14 +1440,26 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
           // steps ahead of their first reader) and, with three stages, its
           // B(S + 2).  WAR: own fragment reads of step S retired.
           constexpr int VB = NBS == 3 ? HC::BJ : 0;
-          if constexpr (rows_at(c, t))
+          // DL: at S = 3k + 2 region k + 1 (issued after B(S + 1) at S - 3) and
+          // B(S + 1) must have landed; B(S + 2) may fly.  Otherwise B(S + 1)
+          // must have landed; B(S + 2) and the region issued at 3k - 1 may fly.
+          if constexpr (DL) {
+            if constexpr (S % 3 == 2)
+              asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(HC::BJ) : "memory");
+            else
+              asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(HC::BJ + 4 * HC::RP) : "memory");
+          } else if constexpr (rows_at(c, t))
             asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(VB + HC::RP) : "memory");
           else
             asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(VB) : "memory");
           __builtin_amdgcn_s_barrier();
           if constexpr (!(ABL & 1)) {
             issue_b(S % NBS, bc, bt);
-            issue_rows(nc, nt);
+            if constexpr (DL) {
+              if constexpr (S % 3 == 2) region_dl(S / 3 + 2);
+            } else {
+              issue_rows(nc, nt);
+            }
           }
           if constexpr (DS && S == TOTAL - 2) hw4_res_load<WM, WN, HC::WAVES_M, W>(op, rv0, m0, n0, wm, wn, lane);
           if constexpr (!(ABL & 2)) rd(std::integral_constant<int, n>{}, std::integral_constant<int, 0>{}, a0, b0);
@@ -1427,18 +1500,18 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
   }
 }
 
-template <int BN, int W, int NCH, int ABL = 0, bool DS = false>
+template <int BN, int W, int NCH, int ABL = 0, bool DS = false, bool DL = false>
 static int launch_hwide4_k(const ConvOp& op, hipStream_t st) {
   using HC = Halo3Cfg<BN, W>;
   static bool attr_set = false;
   if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute((const void*)conv_hwide4_kernel<BN, W, NCH, ABL, DS>,
+    const hipError_t e = hipFuncSetAttribute((const void*)conv_hwide4_kernel<BN, W, NCH, ABL, DS, DL>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, HC::LDS);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
   const int grid = (op.B * op.Ho * W / HC::BM) * (op.N / BN);
-  hipLaunchKernelGGL((conv_hwide4_kernel<BN, W, NCH, ABL, DS>), dim3(grid), dim3(512), HC::LDS, st, op);
+  hipLaunchKernelGGL((conv_hwide4_kernel<BN, W, NCH, ABL, DS, DL>), dim3(grid), dim3(512), HC::LDS, st, op);
   return (int)hipGetLastError();
 }
 
@@ -1500,6 +1573,15 @@ static int halo_route(const ConvOp& op, hipStream_t st) {
   static const int mode = env_int("UPR_WIDE_HALO", 2);
   if (!mode || op.nseg != 1 || op.store != kStoreNHWC) return kErrUnsupported;
   const ConvSeg& s = op.seg[0];
+  {
+    // dilated 3x3 over 256 channels at W 64 (the ASPP branches, d 6 / 12 / 18):
+    // the region form of hwide4.  UPR_HW4_DIL=0 keeps them on the gathered kernel
+    static const int dl = env_int("UPR_HW4_DIL", 1);
+    if (dl && s.kh == 3 && s.kw == 3 && s.stride == 1 && s.dil > 1 && s.pad == s.dil && s.dil < 64 &&
+        s.pre == kPreNone && s.kbase == 0 && s.C == 256 && s.Hin == op.Ho && s.Win == op.Wo && op.Wo == 64 &&
+        op.N % 256 == 0 && (op.Ho * op.Wo) % WBM == 0 && hw4_ds_ok(op))
+      return launch_hwide4_k<256, 64, 4, 0, true, true>(op, st);
+  }
   if (s.kh != 3 || s.kw != 3 || s.stride != 1 || s.pad != 1 || s.dil != 1 || s.pre != kPreNone) return kErrUnsupported;
   if (s.Hin != op.Ho || s.Win != op.Wo || s.C % WBK || (op.Ho * op.Wo) % WBM) return kErrUnsupported;
   if (op.Wo == 64 && op.N % 256 == 0) return mode == 1 ? launch_hwide<256, 64>(op, st) : launch_hwide34<256, 64>(op, st);

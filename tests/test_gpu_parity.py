@@ -85,6 +85,10 @@ CONV_CASES = [
     (1, 32, 64, 128, 128, 3, 1, 1, 1, False, True),
     (2, 16, 128, 128, 128, 3, 1, 1, 1, True, False),
     (1, 8, 64, 64, 256, 3, 1, 1, 1, False, False),
+    # dilated region form of hwide4 (ASPP branches: 3x3, dilation = padding, 256 -> 256 at W 64)
+    (2, 64, 64, 256, 256, 3, 1, 6, 6, True, False),
+    (1, 64, 64, 256, 256, 3, 1, 18, 18, False, True),
+    (1, 32, 64, 256, 512, 3, 1, 12, 12, True, False),
 ]
 
 

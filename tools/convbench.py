@@ -32,6 +32,7 @@ SHAPES = {
     "enc1s2": (32, 512, 512, 32, 64, 3, 2, 1, 1, False),
     "d2": (32, 512, 512, 32, 32, 3, 1, 2, 2, False),
     "aspp6": (32, 64, 64, 256, 256, 3, 1, 6, 6, False),
+    "aspp12": (32, 64, 64, 256, 256, 3, 1, 12, 12, False),
     "aspp18": (32, 64, 64, 256, 256, 3, 1, 18, 18, False),
     "fuse": (32, 64, 64, 1280, 256, 1, 1, 0, 1, False),
     "enc3s2": (32, 128, 128, 128, 256, 3, 2, 1, 1, False),
