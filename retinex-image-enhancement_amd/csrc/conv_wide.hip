@@ -348,11 +348,164 @@ __device__ __forceinline__ void wide_epilogue(const ConvOp& op, f32x4_w (&acc)[W
   }
 }
 
+// Direct-store epilogue of conv_hwide4_kernel<DS = true> (no LDS parking, no
+// block barriers).  The main loop ran the MFMAs with the operands swapped
+// (weights first), so a lane's accumulator holds 4 consecutive CHANNELS of one
+// pixel, and the B tile's rows were DMA'd in the order hw4_perm32 below, so
+// tiles 2p / 2p + 1 of a lane hold channels 32p + 8fg + 0..3 / + 4..7 of pixel
+// fr: 8 consecutive channels -> one 16-byte store per (fragment, pair), the
+// scale / bias / residual / ReLU / out2 / pool arithmetic in registers.  The
+// LDS epilogue parked 256 KiB of fp32 per block in 4 barrier-separated passes
+// (~20% of the bottleneck conv, profiles/r3_hwide4_bneck_ablations_v2.txt).
+__device__ __forceinline__ int hw4_perm32(int r) {
+  // LDS row r of a 32-row group = (b' r4 | i3 r3 r2 | i1 r1 r0) holds channel i3*8 + b'*4 + i1
+  return (r & ~31) | (((r >> 2) & 3) << 3) | (((r >> 4) & 1) << 2) | (r & 3);
+}
+
+// Shared by conv_hwide4_kernel<DS> and conv_wide_kernel<DS>: PIX(a) = the
+// pixel (GEMM row) of the lane's fragment a, valid while < M; IMG >= 0: every
+// pixel of the block is in image IMG (required for op.pool), else the image is
+// divided out per fragment (only for the per-image bias).  PRE: the caller
+// preloaded pair 0's residual rows into rv0 (hw4_res_load).
+template <int BN, int WM, int WN, int WAVES_M, bool PRE, typename PixF>
+__device__ __forceinline__ void direct_epilogue(const ConvOp& op, f32x4_w (&acc)[WM][WN], int n0, int wm, int wn,
+                                                int lane, const f16x8_w (&rv0)[WM], unsigned char* smem, PixF pix,
+                                                int M, int HW, int IMG) {
+  constexpr int NP = WN / 2;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int cb = n0 + wn * WN * 16 + fg * 8;  // channel of pair p: cb + 32p
+  const half_t* rpf = (const half_t*)(op.res1 ? op.res1 : op.res2);
+  const int rcs = op.res1 ? op.res1_cs : op.res2_cs;
+  // residual rows: pair 0's up front (or preloaded), pair p + 1's while pair p
+  // is finished (each fragment's pair-p accumulators die as its pair-p + 1
+  // residual arrives)
+  f16x8_w rv[NP][WM];
+  auto rload = [&](int p, int a) {
+    const int m = pix(a);
+    return m < M ? *(const f16x8_w*)(rpf + (size_t)m * rcs + cb + 32 * p) : f16x8_w{};
+  };
+  if constexpr (PRE) {
+#pragma unroll
+    for (int a = 0; a < WM; ++a) rv[0][a] = rv0[a];
+  } else if (rpf) {
+#pragma unroll
+    for (int a = 0; a < WM; ++a) rv[0][a] = rload(0, a);
+  }
+  float psum[NP][8];
+#pragma unroll
+  for (int p = 0; p < NP; ++p)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) psum[p][e] = 0.f;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int c = cb + 32 * p;
+    float sc[8], bi[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { sc[e] = 1.f; bi[e] = 0.f; }
+    if (op.scale) {
+      const f32x4_w s0 = *(const f32x4_w*)(op.scale + c), s1 = *(const f32x4_w*)(op.scale + c + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { sc[e] = s0[e]; sc[e + 4] = s1[e]; }
+    }
+    if (op.bias) {
+      const f32x4_w b0 = *(const f32x4_w*)(op.bias + c), b1 = *(const f32x4_w*)(op.bias + c + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { bi[e] = b0[e]; bi[e + 4] = b1[e]; }
+    }
+    if (op.img_bias && IMG >= 0) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bi[e] += op.img_bias[IMG * op.N + c + e];
+    }
+#pragma unroll
+    for (int a = 0; a < WM; ++a) {
+      const int mi = pix(a);
+      const size_t m = (size_t)mi;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = acc[a][2 * p][e] * sc[e] + bi[e];
+        v[e + 4] = acc[a][2 * p + 1][e] * sc[e + 4] + bi[e + 4];
+      }
+      if (rpf && p + 1 < NP) rv[p + 1][a] = rload(p + 1, a);
+      if (mi >= M) continue;
+      if (op.img_bias && IMG < 0) {
+        const int im = mi / HW;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += op.img_bias[im * op.N + c + e];
+      }
+      if (op.res1) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += (float)rv[p][a][e];
+      }
+      if (op.relu) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      if (op.res2) {
+        const f16x8_w r = op.res1 ? *(const f16x8_w*)((const half_t*)op.res2 + m * op.res2_cs + c) : rv[p][a];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += (float)r[e];
+      }
+      f16x8_w o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (half_t)v[e];
+      *(f16x8_w*)((half_t*)op.out + m * op.out_cs + op.out_coff + c) = o;
+      if (op.out2) {
+        const f32x4_w s0 = *(const f32x4_w*)(op.pre2_scale + c), s1 = *(const f32x4_w*)(op.pre2_scale + c + 4);
+        const f32x4_w h0 = *(const f32x4_w*)(op.pre2_shift + c), h1 = *(const f32x4_w*)(op.pre2_shift + c + 4);
+        f16x8_w q;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          q[e] = (half_t)fmaxf(__builtin_fmaf((float)o[e], s0[e], h0[e]), 0.f);
+          q[e + 4] = (half_t)fmaxf(__builtin_fmaf((float)o[e + 4], s1[e], h1[e]), 0.f);
+        }
+        *(f16x8_w*)((half_t*)op.out2 + m * op.out2_cs + c) = q;
+      }
+      if (op.pool) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) psum[p][e] += (float)o[e];
+      }
+    }
+  }
+  if (op.pool && IMG >= 0) {
+    // per-lane partial sums -> LDS [16 fr][WAVES_M][BN] (the main loop is done
+    // with LDS: the kernel waited for its DMAs and a barrier precedes this),
+    // then one thread per channel adds its 16 * WAVES_M partials in a fixed
+    // order and issues ONE fixed-point atomic: 256 coalesced atomics per block
+    float* Ps = (float*)smem;
+    const int cl = cb - n0;
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) Ps[(fr * WAVES_M + wm) * BN + cl + 32 * p + e] = psum[p][e];
+    __syncthreads();
+    const int tid = threadIdx.x;
+    if (tid < BN) {
+      float t = 0.f;
+      for (int g = 0; g < 16 * WAVES_M; ++g) t += Ps[g * BN + tid];
+      pool_add(op.pool, (size_t)IMG * op.N + n0 + tid, t);
+    }
+  }
+}
+
+template <int BN, int WM, int WN, int WAVES_M, int W>
+__device__ __forceinline__ void hw4_direct_epilogue(const ConvOp& op, f32x4_w (&acc)[WM][WN], int m0, int n0,
+                                                    int wm, int wn, int lane, const f16x8_w (&rv0)[WM],
+                                                    unsigned char* smem) {
+  constexpr int CW = W / WAVES_M, FPR = CW / 16;
+  const int mb = m0 + CW * wm + (lane & 15);  // pixel of fragment a: mb + (a / FPR) * W + (a % FPR) * 16
+  direct_epilogue<BN, WM, WN, WAVES_M, true>(
+      op, acc, n0, wm, wn, lane, rv0, smem, [&](int a) { return mb + (a / FPR) * W + (a % FPR) * 16; }, 1 << 30,
+      op.Ho * W, m0 / (op.Ho * W));
+}
+
 // MINW: minimum waves per SIMD (HIP's second launch-bounds argument); 4 = two
 // 512-thread blocks per CU
 // (MINW 4 also selects ONE LDS stage: load -> compute per step, the other
 // block on the CU overlapping)
-template <int BN, bool PIPE, int MINW = 2, int SCHED = 0>
+// DS: operand-swapped MFMAs, B rows DMA'd in hw4_perm32 order and the
+// direct-store epilogue (wide_ds_ok decides per op)
+template <int BN, bool PIPE, int MINW = 2, int SCHED = 0, bool DS = false>
 __global__ __launch_bounds__(512, MINW) void conv_wide_kernel(ConvOp op) {
   constexpr bool ONE = MINW >= 4;
   using C = WideCfg<BN>;
@@ -414,7 +567,7 @@ __global__ __launch_bounds__(512, MINW) void conv_wide_kernel(ConvOp op) {
     for (int j = 0; j < C::BJ; ++j) {
       const int n = wave * (BN / 8) + j * 8 + q8;
       const int ch = qc ^ ((4 * j + sw_lane) & 7);
-      glds16(Wt + (size_t)(n0 + n) * op.Kpad + kb + ch * 8, Bs + (wave * (BN / 8) + j * 8) * 128);
+      glds16(Wt + (size_t)(n0 + (DS ? hw4_perm32(n) : n)) * op.Kpad + kb + ch * 8, Bs + (wave * (BN / 8) + j * 8) * 128);
     }
     cur.advance();
   };
@@ -449,8 +602,12 @@ __global__ __launch_bounds__(512, MINW) void conv_wide_kernel(ConvOp op) {
         for (int a = 0; a < C::WM; ++a) {
           const f16x8_w af = *(const f16x8_w*)(As + (wm * C::WM * 16 + a * 16 + fr) * 64 + pc);
   #pragma unroll
-          for (int b = 0; b < C::WN; ++b)
-            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf[b], acc[a][b], 0, 0, 0);
+          for (int b = 0; b < C::WN; ++b) {
+            if constexpr (DS)
+              acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[b], af, acc[a][b], 0, 0, 0);
+            else
+              acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf[b], acc[a][b], 0, 0, 0);
+          }
         }
       }
       if (ONE && step + 1 < total_steps) {
@@ -480,8 +637,12 @@ __global__ __launch_bounds__(512, MINW) void conv_wide_kernel(ConvOp op) {
 #pragma unroll
       for (int a = 0; a < C::WM; ++a)
 #pragma unroll
-        for (int b = 0; b < C::WN; ++b)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a], bf[b], acc[a][b], 0, 0, 0);
+        for (int b = 0; b < C::WN; ++b) {
+          if constexpr (DS)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[b], af[a], acc[a][b], 0, 0, 0);
+          else
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a], bf[b], acc[a][b], 0, 0, 0);
+        }
     };
     // (the host routes total_steps < 2 to the plain loop)
     // ds_read / MFMA interleave of one half-step: one A fragment (and, for the
@@ -530,10 +691,18 @@ __global__ __launch_bounds__(512, MINW) void conv_wide_kernel(ConvOp op) {
     mm(a0, b0);
     mm(a1, b1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // every wave is done with both stages before the epilogue reuses LDS
+    if constexpr (!DS) __syncthreads();  // every wave is done with both stages before the epilogue reuses LDS
   }
 
-  wide_epilogue<BN, C::WM, C::WN, C::WAVES_M, WBM, !ONE>(op, acc, smem, m0, n0, M, HW);
+  if constexpr (DS) {
+    // (no pool in this form: the LDS is not reused, no barrier)
+    f16x8_w rv0[C::WM];
+    const int mb = m0 + wm * C::WM * 16 + (lane & 15);
+    direct_epilogue<BN, C::WM, C::WN, C::WAVES_M, false>(
+        op, acc, n0, wm, wn, lane, rv0, smem, [&](int a) { return mb + a * 16; }, M, HW, -1);
+  } else {
+    wide_epilogue<BN, C::WM, C::WN, C::WAVES_M, WBM, !ONE>(op, acc, smem, m0, n0, M, HW);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1040,130 +1209,6 @@ __device__ __forceinline__ void static_steps(F&& f, std::integer_sequence<int, S
 // (< 8 pixels x 1024 channels x 2 B), so a 16 KiB zero block
 __device__ __attribute__((aligned(256))) uint4 g_halo_zero[1024];
 
-// Direct-store epilogue of conv_hwide4_kernel<DS = true> (no LDS parking, no
-// block barriers).  The main loop ran the MFMAs with the operands swapped
-// (weights first), so a lane's accumulator holds 4 consecutive CHANNELS of one
-// pixel, and the B tile's rows were DMA'd in the order hw4_perm32 below, so
-// tiles 2p / 2p + 1 of a lane hold channels 32p + 8fg + 0..3 / + 4..7 of pixel
-// fr: 8 consecutive channels -> one 16-byte store per (fragment, pair), the
-// scale / bias / residual / ReLU / out2 / pool arithmetic in registers.  The
-// LDS epilogue parked 256 KiB of fp32 per block in 4 barrier-separated passes
-// (~20% of the bottleneck conv, profiles/r3_hwide4_bneck_ablations_v2.txt).
-__device__ __forceinline__ int hw4_perm32(int r) {
-  // LDS row r of a 32-row group = (b' r4 | i3 r3 r2 | i1 r1 r0) holds channel i3*8 + b'*4 + i1
-  return (r & ~31) | (((r >> 2) & 3) << 3) | (((r >> 4) & 1) << 2) | (r & 3);
-}
-
-template <int BN, int WM, int WN, int WAVES_M, int W>
-__device__ __forceinline__ void hw4_direct_epilogue(const ConvOp& op, f32x4_w (&acc)[WM][WN], int m0, int n0,
-                                                    int wm, int wn, int lane, const f16x8_w (&rv0)[WM],
-                                                    unsigned char* smem) {
-  constexpr int CW = W / WAVES_M, FPR = CW / 16, NP = WN / 2;
-  const int fr = lane & 15, fg = lane >> 4;
-  const int img = m0 / (op.Ho * W);
-  const int cb = n0 + wn * WN * 16 + fg * 8;  // channel of pair p: cb + 32p
-  const int mb = m0 + CW * wm + fr;          // pixel of fragment a: mb + (a / FPR) * W + (a % FPR) * 16
-  const half_t* rpf = (const half_t*)(op.res1 ? op.res1 : op.res2);
-  const int rcs = op.res1 ? op.res1_cs : op.res2_cs;
-  // residual rows: pair 0's were loaded by the kernel during its last K steps
-  // (hw4_res_load), pair p + 1's load while pair p is finished (each
-  // fragment's pair-p accumulators die as its pair-p + 1 residual arrives)
-  f16x8_w rv[NP][WM];
-  auto rload = [&](int p, int a) {
-    return *(const f16x8_w*)(rpf + (size_t)(mb + (a / FPR) * W + (a % FPR) * 16) * rcs + cb + 32 * p);
-  };
-#pragma unroll
-  for (int a = 0; a < WM; ++a) rv[0][a] = rv0[a];
-  float psum[NP][8];
-#pragma unroll
-  for (int p = 0; p < NP; ++p)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) psum[p][e] = 0.f;
-#pragma unroll
-  for (int p = 0; p < NP; ++p) {
-    const int c = cb + 32 * p;
-    float sc[8], bi[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) { sc[e] = 1.f; bi[e] = 0.f; }
-    if (op.scale) {
-      const f32x4_w s0 = *(const f32x4_w*)(op.scale + c), s1 = *(const f32x4_w*)(op.scale + c + 4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) { sc[e] = s0[e]; sc[e + 4] = s1[e]; }
-    }
-    if (op.bias) {
-      const f32x4_w b0 = *(const f32x4_w*)(op.bias + c), b1 = *(const f32x4_w*)(op.bias + c + 4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) { bi[e] = b0[e]; bi[e + 4] = b1[e]; }
-    }
-    if (op.img_bias) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) bi[e] += op.img_bias[img * op.N + c + e];
-    }
-#pragma unroll
-    for (int a = 0; a < WM; ++a) {
-      const size_t m = (size_t)(mb + (a / FPR) * W + (a % FPR) * 16);
-      float v[8];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] = acc[a][2 * p][e] * sc[e] + bi[e];
-        v[e + 4] = acc[a][2 * p + 1][e] * sc[e + 4] + bi[e + 4];
-      }
-      if (rpf && p + 1 < NP) rv[p + 1][a] = rload(p + 1, a);
-      if (op.res1) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += (float)rv[p][a][e];
-      }
-      if (op.relu) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-      }
-      if (op.res2) {
-        const f16x8_w r = op.res1 ? *(const f16x8_w*)((const half_t*)op.res2 + m * op.res2_cs + c) : rv[p][a];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += (float)r[e];
-      }
-      f16x8_w o;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = (half_t)v[e];
-      *(f16x8_w*)((half_t*)op.out + m * op.out_cs + op.out_coff + c) = o;
-      if (op.out2) {
-        const f32x4_w s0 = *(const f32x4_w*)(op.pre2_scale + c), s1 = *(const f32x4_w*)(op.pre2_scale + c + 4);
-        const f32x4_w h0 = *(const f32x4_w*)(op.pre2_shift + c), h1 = *(const f32x4_w*)(op.pre2_shift + c + 4);
-        f16x8_w q;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          q[e] = (half_t)fmaxf(__builtin_fmaf((float)o[e], s0[e], h0[e]), 0.f);
-          q[e + 4] = (half_t)fmaxf(__builtin_fmaf((float)o[e + 4], s1[e], h1[e]), 0.f);
-        }
-        *(f16x8_w*)((half_t*)op.out2 + m * op.out2_cs + c) = q;
-      }
-      if (op.pool) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) psum[p][e] += (float)o[e];
-      }
-    }
-  }
-  if (op.pool) {
-    // per-lane partial sums -> LDS [16 fr][WAVES_M][BN] (the main loop is done
-    // with LDS: the kernel waited for its DMAs and a barrier precedes this),
-    // then one thread per channel adds its 16 * WAVES_M partials in a fixed
-    // order and issues ONE fixed-point atomic: 256 coalesced atomics per block
-    float* Ps = (float*)smem;
-    const int cl = cb - n0;
-#pragma unroll
-    for (int p = 0; p < NP; ++p)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) Ps[(fr * WAVES_M + wm) * BN + cl + 32 * p + e] = psum[p][e];
-    __syncthreads();
-    const int tid = threadIdx.x;
-    if (tid < BN) {
-      float t = 0.f;
-      for (int g = 0; g < 16 * WAVES_M; ++g) t += Ps[g * BN + tid];
-      pool_add(op.pool, (size_t)img * op.N + n0 + tid, t);
-    }
-  }
-}
-
 // pair-0 residual rows of a lane (see hw4_direct_epilogue), issued by the
 // kernel after the DMAs of its second-to-last K step: the loads fly under the
 // last 1.5 steps of MFMAs, and no counted vmcnt wait of the loop follows them
@@ -1592,20 +1637,31 @@ static int halo_route(const ConvOp& op, hipStream_t st) {
 }
 
 
-template <int BN, bool PIPE, int SCHED>
-static int launch_wide_bn_s(const ConvOp& op, hipStream_t st) {
+// the gathered kernel's direct-store form takes what hwide4's does minus the
+// per-image pool (its tiles may straddle images); UPR_WIDE_DS=0: LDS epilogue (A/B)
+static bool wide_ds_ok(const ConvOp& op) {
+  static const int en = env_int("UPR_WIDE_DS", 1);
+  return en && !op.pool && hw4_ds_ok(op);
+}
+
+template <int BN, bool PIPE, int SCHED, bool DS>
+static int launch_wide_bn_k(const ConvOp& op, hipStream_t st) {
   using C = WideCfg<BN>;
   static bool attr_set = false;
   if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute((const void*)conv_wide_kernel<BN, PIPE, 2, SCHED>,
+    const hipError_t e = hipFuncSetAttribute((const void*)conv_wide_kernel<BN, PIPE, 2, SCHED, DS>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
   const int M = op.B * op.Ho * op.Wo;
   const int grid = ((M + WBM - 1) / WBM) * (op.N / BN);
-  hipLaunchKernelGGL((conv_wide_kernel<BN, PIPE, 2, SCHED>), dim3(grid), dim3(512), C::LDS, st, op);
+  hipLaunchKernelGGL((conv_wide_kernel<BN, PIPE, 2, SCHED, DS>), dim3(grid), dim3(512), C::LDS, st, op);
   return (int)hipGetLastError();
+}
+template <int BN, bool PIPE, int SCHED>
+static int launch_wide_bn_s(const ConvOp& op, hipStream_t st) {
+  return wide_ds_ok(op) ? launch_wide_bn_k<BN, PIPE, SCHED, true>(op, st) : launch_wide_bn_k<BN, PIPE, SCHED, false>(op, st);
 }
 
 // UPR_WIDE_SCHED: 2 = one fragment read per two MFMAs (default), 0 = grouped interleave (A/B timing)
@@ -1675,7 +1731,10 @@ static int launch_wide_onestep128(const ConvOp& op, hipStream_t st) {
   constexpr int LDS1 = C::STAGE > EPI ? C::STAGE : EPI;
   const int M = op.B * op.Ho * op.Wo;
   const int grid = ((M + WBM - 1) / WBM) * (op.N / 128);
-  hipLaunchKernelGGL((conv_wide_kernel<128, false, 4>), dim3(grid), dim3(512), LDS1, st, op);
+  if (wide_ds_ok(op))
+    hipLaunchKernelGGL((conv_wide_kernel<128, false, 4, 0, true>), dim3(grid), dim3(512), LDS1, st, op);
+  else
+    hipLaunchKernelGGL((conv_wide_kernel<128, false, 4>), dim3(grid), dim3(512), LDS1, st, op);
   return (int)hipGetLastError();
 }
 
