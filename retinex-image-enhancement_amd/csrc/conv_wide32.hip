@@ -249,9 +249,95 @@ __device__ __forceinline__ void q32_epilogue(const ConvOp& op, f32x4_q (&acc)[Q3
   }
 }
 
+// Direct-store epilogue (conv_wide32_kernel<DS = true>): the main loop ran the
+// MFMAs with the operands swapped (weights first), so a lane's accumulator
+// tile b holds 4 consecutive fp32 CHANNELS (16 bytes) of pixel fr: bias /
+// per-image bias / residuals / ReLU in registers and one 16-byte store per
+// (fragment, tile) -- no LDS parking passes or block barriers.  NHWC stores;
+// the per-image pool needs every pixel of the block in one image (host check).
+template <int BM, int BN>
+__device__ __forceinline__ void q32_direct_epilogue(const ConvOp& op,
+                                                    f32x4_q (&acc)[Q32Cfg<BM, BN>::WM][Q32Cfg<BM, BN>::WN],
+                                                    unsigned char* smem, int m0, int n0, int M, int HW) {
+  using C = Q32Cfg<BM, BN>;
+  constexpr int WM = C::WM, WN = C::WN;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave % C::WAVES_M;
+  const int wn = wave / C::WAVES_M;
+  const int fr = lane & 15;
+  const int fg = lane >> 4;
+  const int cb = n0 + wn * WN * 16 + fg * 4;  // channel of tile b: cb + 16b
+  const int mb = m0 + wm * WM * 16 + fr;      // pixel of fragment a: mb + 16a
+  const float* res1 = (const float*)op.res1;
+  const float* res2 = (const float*)op.res2;
+  float* out = (float*)op.out;
+  const float* rp = res1 ? res1 : res2;
+  const int rcs = res1 ? op.res1_cs : op.res2_cs;
+  f32x4_q rv[WM][WN];
+  if (rp) {
+#pragma unroll
+    for (int a = 0; a < WM; ++a)
+#pragma unroll
+      for (int b = 0; b < WN; ++b)
+        rv[a][b] = mb + 16 * a < M ? *(const f32x4_q*)(rp + (size_t)(mb + 16 * a) * rcs + cb + 16 * b) : f32x4_q{};
+  }
+  const int img0 = m0 / HW;
+  float psum[WN][4];
+#pragma unroll
+  for (int b = 0; b < WN; ++b)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) psum[b][e] = 0.f;
+#pragma unroll
+  for (int b = 0; b < WN; ++b) {
+    const int c = cb + 16 * b;
+    const f32x4_q bi = op.bias ? *(const f32x4_q*)(op.bias + c) : f32x4_q{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int a = 0; a < WM; ++a) {
+      const int m = mb + 16 * a;
+      if (m >= M) continue;
+      f32x4_q v = acc[a][b] + bi;
+      if (op.img_bias) {
+        const int im = m / HW;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += op.img_bias[im * op.N + c + e];
+      }
+      if (res1) v += rv[a][b];
+      if (op.relu) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      if (res2) v += res1 ? *(const f32x4_q*)(res2 + (size_t)m * op.res2_cs + c) : rv[a][b];
+      *(f32x4_q*)(out + (size_t)m * op.out_cs + op.out_coff + c) = v;
+      if (op.pool) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) psum[b][e] += v[e];
+      }
+    }
+  }
+  if (op.pool) {
+    // wave partials -> LDS [16 fr][WAVES_M][BN], then one thread per channel
+    // adds them in a fixed order and issues one fixed-point atomic
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave is done with the stages
+    float* Ps = (float*)smem;
+#pragma unroll
+    for (int b = 0; b < WN; ++b)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Ps[(fr * C::WAVES_M + wm) * BN + (cb - n0) + 16 * b + e] = psum[b][e];
+    __syncthreads();
+    if (tid < BN) {
+      float t = 0.f;
+      for (int g = 0; g < 16 * C::WAVES_M; ++g) t += Ps[g * BN + tid];
+      pool_add(op.pool, (size_t)img0 * op.N + n0 + tid, t);
+    }
+  }
+}
+
 // OCC = co-resident blocks per CU the register budget must allow (1: 256
 // VGPRs; 2: 128 VGPRs, one block's prologue / epilogue overlaps the other's MFMAs)
-template <int BM, int BN, bool PIPE, int OCC>
+template <int BM, int BN, bool PIPE, int OCC, bool DS = false>
 __global__ __launch_bounds__(512, 2 * OCC) void conv_wide32_kernel(ConvOp op) {
   using C = Q32Cfg<BM, BN>;
   constexpr int WM = C::WM;
@@ -347,8 +433,12 @@ __global__ __launch_bounds__(512, 2 * OCC) void conv_wide32_kernel(ConvOp op) {
 #pragma unroll
       for (int a = 0; a < WM; ++a)
 #pragma unroll
-        for (int b = 0; b < WN; ++b)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[a][e], bf[b][e], acc[a][b], 0, 0, 0);
+        for (int b = 0; b < WN; ++b) {
+          if constexpr (DS)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(bf[b][e], af[a][e], acc[a][b], 0, 0, 0);
+          else
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[a][e], bf[b][e], acc[a][b], 0, 0, 0);
+        }
   };
   // one fragment read of the next half beside each group of MFMAs of this one
   auto interleave = [&]() {
@@ -398,19 +488,27 @@ __global__ __launch_bounds__(512, 2 * OCC) void conv_wide32_kernel(ConvOp op) {
     mm(a1, b1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-  q32_epilogue<BM, BN>(op, acc, smem, m0, n0, M, HW);
+  if constexpr (DS)
+    q32_direct_epilogue<BM, BN>(op, acc, smem, m0, n0, M, HW);
+  else
+    q32_epilogue<BM, BN>(op, acc, smem, m0, n0, M, HW);
 }
 
-template <int BM, int BN, int OCC>
-static int launch_w32(const ConvOp& op, int steps, hipStream_t st) {
+static int w32_env(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+template <int BM, int BN, int OCC, bool DS>
+static int launch_w32_k(const ConvOp& op, int steps, hipStream_t st) {
   using C = Q32Cfg<BM, BN>;
   static_assert(C::LDS * OCC <= 160 * 1024, "LDS for OCC blocks per CU");
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)conv_wide32_kernel<BM, BN, true, OCC>,
+    hipError_t e = hipFuncSetAttribute((const void*)conv_wide32_kernel<BM, BN, true, OCC, DS>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void*)conv_wide32_kernel<BM, BN, false, OCC>,
+      e = hipFuncSetAttribute((const void*)conv_wide32_kernel<BM, BN, false, OCC, DS>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
@@ -418,15 +516,23 @@ static int launch_w32(const ConvOp& op, int steps, hipStream_t st) {
   const int M = op.B * op.Ho * op.Wo;
   const int grid = ((M + BM - 1) / BM) * (op.N / BN);
   if (steps >= 2)
-    hipLaunchKernelGGL((conv_wide32_kernel<BM, BN, true, OCC>), dim3(grid), dim3(512), C::LDS, st, op);
+    hipLaunchKernelGGL((conv_wide32_kernel<BM, BN, true, OCC, DS>), dim3(grid), dim3(512), C::LDS, st, op);
   else
-    hipLaunchKernelGGL((conv_wide32_kernel<BM, BN, false, OCC>), dim3(grid), dim3(512), C::LDS, st, op);
+    hipLaunchKernelGGL((conv_wide32_kernel<BM, BN, false, OCC, DS>), dim3(grid), dim3(512), C::LDS, st, op);
   return (int)hipGetLastError();
 }
 
-static int w32_env(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
+// direct-store epilogue: NHWC outputs (the ConvTranspose pixel shuffle keeps
+// the LDS epilogue), pools only when no tile straddles two images, tiles >= 128
+// channels wide.  Same-box A/B (profiles/r3_w32_ds_ab.txt): neutral on the fp32
+// step (the fp32 MFMAs hide the epilogue: 27.65 -> 27.63 ms), bneck / fuse /
+// enc3 s2 -1%, the 64-wide dec2 tile +1.3% (kept on the LDS epilogue).
+// UPR_WIDE32_DS=0 keeps the LDS epilogue everywhere
+template <int BM, int BN, int OCC>
+static int launch_w32(const ConvOp& op, int steps, hipStream_t st) {
+  static const int en = w32_env("UPR_WIDE32_DS", 1);
+  const bool ds = en && BN >= 128 && op.store == kStoreNHWC && (!op.pool || (op.Ho * op.Wo) % BM == 0);
+  return ds ? launch_w32_k<BM, BN, OCC, true>(op, steps, st) : launch_w32_k<BM, BN, OCC, false>(op, steps, st);
 }
 
 // fp32 only; kErrUnsupported for shapes this kernel does not take.
