@@ -727,14 +727,18 @@ __global__ __launch_bounds__(512, MINW) void conv_wide_kernel(ConvOp op) {
 // * A region pixel is a 128-byte LDS row; its logical 16-byte chunk q sits at
 //   q ^ T[p & 15].  The tap shift starts a fragment's 16 pixels at p = 16k +
 //   tx (tx in {-1, 0, 1}); T (exhaustive search over the ds_read_b128 lane
-//   groups {0-3,12-15,20-27}, ...) keeps all three shifts conflict-free, where
-//   the aligned-row swizzle (p >> 1) & 7 would be 2-way at tx = +-1.
+//   groups {0-3,12-15,20-27}, ...) keeps every shift conflict-free, where
+//   the aligned-row swizzle (p >> 1) & 7 would be 2-way at tx = +-1.  The
+//   first table (0,0,1,2,2,0,4,4,5,5,6,2,2,6,6,7) covered shifts -1 / 0 / +1
+//   only; the dilated hwide4 reads at +-6 / 12 / 18 conflicted (PMC
+//   SQ_LDS_BANK_CONFLICT 5.5-6.3M cycles per ASPP launch).  T[p] = 2((p >> 1) & 3)
+//   is conflict-free at all 16 start offsets (tools/halo_swz_search.py).
 // * No padding columns: the one lane of an edge fragment whose tap leaves
 //   the image row is zeroed after the read (top / bottom halo rows outside
 //   the image are DMA'd from the zero line).
 // ---------------------------------------------------------------------------
 static int env_int(const char* name, int dflt);
-constexpr unsigned long long kHaloSwz = 0x7662265544022100ull;  // T[p] = 0,0,1,2,2,0,4,4,5,5,6,2,2,6,6,7
+constexpr unsigned long long kHaloSwz = 0x6644220066442200ull;  // T[p] = 0,0,2,2,4,4,6,6,0,0,2,2,4,4,6,6
 __device__ __forceinline__ int halo_swz(int p) { return (int)(kHaloSwz >> ((p & 15) * 4)) & 7; }
 
 template <int BN, int W>
@@ -1388,8 +1392,12 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
     for (int tx = 0; tx < 3; ++tx)
 #pragma unroll
       for (int f = 0; f < FPR; ++f) {
+        // a void lane keeps the bank bits of an in-row pixel of the same
+        // parity and residue: void lanes on one bank serialised the edge
+        // fragments' reads (SQ_LDS_BANK_CONFLICT 5.5M cycles per launch at d 6-18)
         const int p = CW * wm + f * 16 + fr + (tx - 1) * dil;
-        aofs_d[tx][f] = (unsigned)p < (unsigned)W ? p * 128 + ((fg ^ halo_swz(p)) * 16) : kLdsVoid;
+        aofs_d[tx][f] = (unsigned)p < (unsigned)W ? p * 128 + ((fg ^ halo_swz(p)) * 16)
+                                                  : kLdsVoid + (p & 15) * 128 + ((fg ^ halo_swz(p & 15)) * 16);
       }
   }
   bofs = HC::RING + (wn * WN * 16 + fr) * 128 + ((fg ^ rsw) * 16);
