@@ -449,7 +449,29 @@ __device__ __forceinline__ void direct_epilogue(const ConvOp& op, f32x4_w (&acc)
       f16x8_w o;
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = (half_t)v[e];
-      *(f16x8_w*)((half_t*)op.out + m * op.out_cs + op.out_coff + c) = o;
+      if (op.out32) {
+        // the training step's autocast convs (ConvOp::out32): the fp16-rounded
+        // result in fp32 (+ res32), zeroed where mask16 <= 0, and its fp16 copy
+        typedef _Float16 h4d __attribute__((ext_vector_type(4)));
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          f32x4_w t;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) t[e] = (float)o[hh * 4 + e];
+          if (op.res32) t += *(const f32x4_w*)(op.res32 + m * op.res32_cs + c + hh * 4);
+          if (op.mask16) {
+            const h4d mk = *(const h4d*)((const half_t*)op.mask16 + m * op.mask16_cs + c + hh * 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) t[e] = (float)mk[e] > 0.f ? t[e] : 0.f;
+          }
+          if (!op.skip32) *(f32x4_w*)(op.out32 + m * op.out32_cs + op.out32_coff + c + hh * 4) = t;
+          if (op.out32_h16)
+            *(h4d*)((half_t*)op.out32_h16 + m * op.out32_h16_cs + c + hh * 4) =
+                h4d{(half_t)t[0], (half_t)t[1], (half_t)t[2], (half_t)t[3]};
+        }
+      } else {
+        *(f16x8_w*)((half_t*)op.out + m * op.out_cs + op.out_coff + c) = o;
+      }
       if (op.out2) {
         const f32x4_w s0 = *(const f32x4_w*)(op.pre2_scale + c), s1 = *(const f32x4_w*)(op.pre2_scale + c + 4);
         const f32x4_w h0 = *(const f32x4_w*)(op.pre2_shift + c), h1 = *(const f32x4_w*)(op.pre2_shift + c + 4);
@@ -1568,13 +1590,22 @@ static int launch_hwide4_k(const ConvOp& op, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-// the direct-store epilogue takes the fp16 NHWC outputs with 16-byte aligned
-// channel runs (every inference op of the graph); the autocast fp32 outputs
-// (out32 / res32 / mask16) keep the LDS epilogue.  UPR_HW4_DS=0: always LDS (A/B)
+// the direct-store epilogue takes NHWC outputs with aligned channel runs:
+// every inference op of the graph and the training step's autocast fp32
+// outputs (out32 / res32 / mask16 / out32_h16; UPR_DS_OUT32=0 keeps those on
+// the LDS epilogue).  UPR_HW4_DS=0: always LDS (A/B)
 static bool hw4_ds_ok(const ConvOp& op) {
   static const int en = env_int("UPR_HW4_DS", 1);
-  if (!en || op.out32 || op.store != kStoreNHWC) return false;
-  if ((uintptr_t)op.out % 16 || op.out_cs % 8 || op.out_coff % 8) return false;
+  static const int en32 = env_int("UPR_DS_OUT32", 1);  // the autocast fp32-output form (A/B)
+  if (!en || op.store != kStoreNHWC) return false;
+  if (op.out32) {
+    if (!en32 || (uintptr_t)op.out32 % 16 || op.out32_cs % 8 || op.out32_coff % 8) return false;
+    if (op.res32 && ((uintptr_t)op.res32 % 16 || op.res32_cs % 8)) return false;
+    if (op.mask16 && ((uintptr_t)op.mask16 % 8 || op.mask16_cs % 4)) return false;
+    if (op.out32_h16 && ((uintptr_t)op.out32_h16 % 8 || op.out32_h16_cs % 4)) return false;
+  } else if ((uintptr_t)op.out % 16 || op.out_cs % 8 || op.out_coff % 8) {
+    return false;
+  }
   if (op.res1 && ((uintptr_t)op.res1 % 16 || op.res1_cs % 8)) return false;
   if (op.res2 && ((uintptr_t)op.res2 % 16 || op.res2_cs % 8)) return false;
   if (op.out2 && op.out2_cs % 8) return false;
