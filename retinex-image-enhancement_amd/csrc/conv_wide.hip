@@ -968,21 +968,25 @@ static int launch_hwide(const ConvOp& op, hipStream_t st) {
 //   fragments right before their MFMAs, not at the read (a select on freshly
 //   read registers stalls the wave on the LDS read).
 // ---------------------------------------------------------------------------
-template <int BN, int W>
+// TR_ = output rows per tile: 4 (the 8-row ring over several chunks), or 2
+// for one 64-channel chunk at W 256 (hwide4 only: its 4 region rows are the
+// whole "ring", DMA'd in the prologue)
+template <int BN, int W, int TR_ = 4>
 struct Halo3Cfg {
-  static constexpr int TR = 4;               // output rows per tile
-  static constexpr int BM = TR * W;          // 256 (W 64) / 512 (W 128) pixels
-  static constexpr int WAVES_M = BM / 128;   // each wave: 128 pixels x 64 channels
-  static constexpr int WAVES_N = 8 / WAVES_M;
-  static constexpr int WM = 8, WN = BN / WAVES_N / 16;
+  static constexpr int TR = TR_;             // output rows per tile
+  static constexpr int BM = TR * W;          // 256 (W 64) / 512 (W 128, W 256 x 2 rows) pixels
+  static constexpr int WAVES_N = BN / 64;    // each wave: BM / WAVES_M pixels x 64 channels
+  static constexpr int WAVES_M = 8 / WAVES_N;
+  static constexpr int WM = BM / WAVES_M / 16, WN = BN / WAVES_N / 16;
   static constexpr int ROW = W * 128;        // one region row of one 64-channel chunk
   static constexpr int RP = W / 64;          // DMA pieces per wave per region row
-  static constexpr int RING = 8 * ROW;       // 8-row ring
+  static constexpr int RR = TR == 4 ? 8 : TR + 2;  // ring rows
+  static constexpr int RING = RR * ROW;
   static constexpr int B_BYTES = BN * WBK * 2;
   static constexpr int BJ = BN / 64;         // B DMA instructions per wave per step
   static constexpr int NBS = RING + 3 * B_BYTES <= 163840 ? 3 : 2;  // B stages
   static constexpr int LDS = RING + NBS * B_BYTES;
-  static_assert(WN == 4 && WAVES_M * WAVES_N == 8, "wave tile 128 x 64");
+  static_assert(WN == 4 && WAVES_M * WAVES_N == 8, "wave tile (BM / WAVES_M) x 64");
   static_assert(LDS <= 163840, "LDS");
 };
 
@@ -1262,9 +1266,10 @@ __device__ __forceinline__ void hw4_res_load(const ConvOp& op, f16x8_w (&rv0)[WM
 // after the barrier that ends region k - 1's reads, three steps ahead of its
 // first reader) and read by its 3 taps at per-lane column offsets +-d (lanes
 // whose column falls outside the image row read through the void LDS base)
-template <int BN, int W, int NCH, int ABL = 0, bool DS = false, bool DL = false>
+template <int BN, int W, int NCH, int ABL = 0, bool DS = false, bool DL = false, int TR = 4>
 __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
-  using HC = Halo3Cfg<BN, W>;
+  using HC = Halo3Cfg<BN, W, TR>;
+  static_assert(TR == 4 || (NCH == 1 && !DL && DS), "2-row tiles: one chunk, direct store");
   constexpr int WM = HC::WM, WN = HC::WN, BM = HC::BM, NBS = HC::NBS;
   constexpr int TOTAL = NCH * 9;
   constexpr int CW = W / HC::WAVES_M;  // columns per wave
@@ -1316,10 +1321,12 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
   // region rows issued right before the reads of step (c, t): this chunk's
   // rows 4 / 5 at t 0 / 1, the next chunk's rows 0, 2, 1, 3 at t 2, 3, 4, 6
   constexpr auto rows_at = [](int c, int t) -> int {
+    if (TR != 4) return 0;  // 2-row tiles: all 4 region rows in the prologue
     if (t < 2) return 1;
     return (t <= 4 || t == 6) && c + 1 < NCH ? 1 : 0;
   };
   auto issue_rows = [&](int c, int t) {
+    if (TR != 4) return;
     if (t < 2) region_row(c, 4 + t);
     else if (c + 1 < NCH) {
       if (t == 2) region_row(c + 1, 0);
@@ -1366,8 +1373,9 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
   unsigned voff_ds[HC::BJ];
 #pragma unroll
   for (int j = 0; j < HC::BJ; ++j) {
+    // LDS row R's chunk swizzle (R >> 1) & 7 (for BN 64 it depends on the wave's parity)
     const int R = wave * (BN / 8) + j * 8 + q8;
-    voff_ds[j] = (unsigned)(((hw4_perm32(R) - g32) * op.Kpad + ((qc ^ ((4 * j + sw_lane) & 7)) * 8)) * 2);
+    voff_ds[j] = (unsigned)(((hw4_perm32(R) - g32) * op.Kpad + ((qc ^ ((R >> 1) & 7)) * 8)) * 2);
   }
   // B of step (c, t) into stage stg; steps past the end re-read the last
   // step's rows into a stage nobody reads again (uniform DMA count)
@@ -1575,18 +1583,18 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
   }
 }
 
-template <int BN, int W, int NCH, int ABL = 0, bool DS = false, bool DL = false>
+template <int BN, int W, int NCH, int ABL = 0, bool DS = false, bool DL = false, int TR = 4>
 static int launch_hwide4_k(const ConvOp& op, hipStream_t st) {
-  using HC = Halo3Cfg<BN, W>;
+  using HC = Halo3Cfg<BN, W, TR>;
   static bool attr_set = false;
   if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute((const void*)conv_hwide4_kernel<BN, W, NCH, ABL, DS, DL>,
+    const hipError_t e = hipFuncSetAttribute((const void*)conv_hwide4_kernel<BN, W, NCH, ABL, DS, DL, TR>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, HC::LDS);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
   const int grid = (op.B * op.Ho * W / HC::BM) * (op.N / BN);
-  hipLaunchKernelGGL((conv_hwide4_kernel<BN, W, NCH, ABL, DS, DL>), dim3(grid), dim3(512), HC::LDS, st, op);
+  hipLaunchKernelGGL((conv_hwide4_kernel<BN, W, NCH, ABL, DS, DL, TR>), dim3(grid), dim3(512), HC::LDS, st, op);
   return (int)hipGetLastError();
 }
 
@@ -1668,6 +1676,17 @@ static int halo_route(const ConvOp& op, hipStream_t st) {
   }
   if (s.kh != 3 || s.kw != 3 || s.stride != 1 || s.pad != 1 || s.dil != 1 || s.pre != kPreNone) return kErrUnsupported;
   if (s.Hin != op.Ho || s.Win != op.Wo || s.C % WBK || (op.Ho * op.Wo) % WBM) return kErrUnsupported;
+  {
+    // 64 -> 64 at W 256 (dec2 UpBlock convs, 256^2 x 64): hwide4 with 2-row
+    // tiles over the one 64-channel chunk (4 region rows of 32 KiB, 9 taps).
+    // Opt-in (UPR_HW4_64=1): correct, but 9% SLOWER than the row ring on the
+    // same box (dec2p 0.234 -> 0.255 ms, profiles/r3_hw4_64_ab.txt): at 152 KiB
+    // of LDS one block per CU exposes every tile's 128 KiB region fill
+    static const int v64 = env_int("UPR_HW4_64", 0);
+    if (v64 && op.Wo == 256 && op.N == 64 && s.C == 64 && s.kbase == 0 && op.Ho % 2 == 0 && hw4_ds_ok(op))
+      return launch_hwide4_k<64, 256, 1, 0, true, false, 2>(op, st);
+  }
+  if (op.N % 128) return kErrUnsupported;
   if (op.Wo == 64 && op.N % 256 == 0) return mode == 1 ? launch_hwide<256, 64>(op, st) : launch_hwide34<256, 64>(op, st);
   if (op.Wo == 64) return launch_hwide<128, 64>(op, st);
   if (op.Wo == 128 && mode == 1) return launch_hwide<128, 128>(op, st);
@@ -1793,7 +1812,7 @@ int launch_conv_wide(const ConvOp& op, hipStream_t st) {
   if (op.out2 && ((uintptr_t)op.out2 % 16 || op.store != kStoreNHWC)) return kErrUnsupported;
   if (op.out32 && ((uintptr_t)op.out32 % 16 || op.out32_cs % 4 || op.out32_coff % 4)) return kErrUnsupported;
   if (op.res32 && ((uintptr_t)op.res32 % 16 || op.res32_cs % 4)) return kErrUnsupported;
-  if (op.store == kStoreHeadIllu || op.N % 128) return kErrUnsupported;
+  if (op.store == kStoreHeadIllu || op.N % 64) return kErrUnsupported;
   if (op.Kpad % 8 || ((uintptr_t)op.W % 16)) return kErrUnsupported;
   for (int s = 0; s < op.nseg; ++s) {
     const ConvSeg& sg = op.seg[s];
@@ -1804,6 +1823,7 @@ int launch_conv_wide(const ConvOp& op, hipStream_t st) {
     const int rc = halo_route(op, st);
     if (rc != kErrUnsupported) return rc;
   }
+  if (op.N % 128) return kErrUnsupported;  // (64-wide: only the halo route above)
   if (op.N % 256 == 0) return launch_wide_any<256>(op, st);
   // 128-channel stride-1 3x3 convs (dec3) used to stay on the halo kernel;
   // on the single-stage two-blocks-per-CU variant they are faster (dec3.conv.0
