@@ -263,9 +263,10 @@ __global__ __launch_bounds__(256) void retinex_tail_kernel(const T* __restrict__
                                                            T* __restrict__ enh, T* __restrict__ refl,
                                                            int B, int H, int W, int h2, int w2, int h3, int w3,
                                                            int refl_in) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= B * H * W) return;
-  const int ox = idx % W, oy = (idx / W) % H, b = idx / (W * H);
+  // 2-D grid (64 x 4 pixels per block, z = image): no per-pixel div / mod
+  const int ox = blockIdx.x * 64 + (threadIdx.x & 63), oy = blockIdx.y * 4 + (threadIdx.x >> 6), b = blockIdx.z;
+  if (ox >= W || oy >= H) return;
+  const size_t idx = ((size_t)b * H + oy) * W + ox;
   int ay0, ay1, ax0, ax1, by0, by1, bx0, bx1;
   float aly, alx, bly, blx;
   src_idx(oy, h2, (float)h2 / (float)H, ay0, ay1, aly);
@@ -504,13 +505,14 @@ int launch_fam_sa(const float* mm, const float* p, const float* w, float bias, f
 int launch_tail(const void* x, const float* illu_f32, const void* illu_t, const float* q1, const float* q2,
                 const float* q3, const float* cst, void* enh, void* refl, int B, int H, int W, int h2, int w2, int h3,
                 int w3, int dtype, hipStream_t st, int refl_in) {
-  const int n = B * H * W;
+  if (B <= 0 || H <= 0 || W <= 0) return kErrShape;
+  const dim3 grid(cdiv(W, 64), cdiv(H, 4), B);
   if (dtype == kF16)
-    hipLaunchKernelGGL((retinex_tail_kernel<half_t>), dim3(grid1d(n)), dim3(256), 0, st, (const half_t*)x, illu_f32,
+    hipLaunchKernelGGL((retinex_tail_kernel<half_t>), grid, dim3(256), 0, st, (const half_t*)x, illu_f32,
                        (const half_t*)illu_t, q1, q2, q3, cst, (half_t*)enh, (half_t*)refl, B, H, W, h2, w2, h3, w3,
                        refl_in);
   else
-    hipLaunchKernelGGL((retinex_tail_kernel<float>), dim3(grid1d(n)), dim3(256), 0, st, (const float*)x, illu_f32,
+    hipLaunchKernelGGL((retinex_tail_kernel<float>), grid, dim3(256), 0, st, (const float*)x, illu_f32,
                        (const float*)illu_t, q1, q2, q3, cst, (float*)enh, (float*)refl, B, H, W, h2, w2, h3, w3,
                        refl_in);
   return (int)hipGetLastError();
