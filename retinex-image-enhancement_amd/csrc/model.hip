@@ -22,6 +22,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -304,6 +305,28 @@ struct UprModel {
   std::vector<double> st_ms, st_flops, st_bytes;
   std::vector<int> st_calls;
   std::vector<double> cur_flops, cur_bytes;  // geometry of the latest forward, per op
+  // multi-scale branch ops [side_begin, side_end) (scale pyramid, scale2/3 first
+  // convs, the three EnhancedFAM blocks) depend only on the input and on op 0's
+  // scale1 output, and the IENet ops [1, side_begin) never read theirs: they run
+  // on a side stream forked after op 0 and joined before the tail (-1: no fork)
+  int side_begin = -1, side_end = -1;
+  struct Side {
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+    unsigned long long last_use = 0;
+    ~Side() {
+      if (s) (void)hipStreamSynchronize(s);
+      if (join) (void)hipEventDestroy(join);
+      if (fork) (void)hipEventDestroy(fork);
+      if (s) (void)hipStreamDestroy(s);
+    }
+  };
+  // per (device, caller stream), least recently used evicted beyond kMaxSides
+  // (a forward holds its entry's reference until it has enqueued everything)
+  static constexpr size_t kMaxSides = 16;
+  std::map<std::pair<int, hipStream_t>, std::shared_ptr<Side>> sides;
+  unsigned long long side_clock = 0;
+  std::mutex sides_mu;
 };
 
 namespace upr {
@@ -770,6 +793,7 @@ static int build_model(UprModel* m, ParamSet& P) {
     // pyramid inputs of scale2/scale3 and their first convs
     Op op;
     op.kind = OP_PREP; op.name = "scale_pyramid";
+    if (!head_only) m->side_begin = (int)m->ops.size();
     m->ops.push_back(op);
     for (int k = 1; k <= 2; ++k) {
       const std::string p = "scale" + std::to_string(k + 1) + ".1";
@@ -789,6 +813,7 @@ static int build_model(UprModel* m, ParamSet& P) {
     Op t;
     t.kind = OP_TAIL; t.name = "retinex_tail";
     t.cst = blob.add_f32(cst);
+    if (m->side_begin >= 0) m->side_end = (int)m->ops.size();
     m->ops.push_back(t);
   }
   if (!bd.ok) return kErrMissingParam;
@@ -801,6 +826,50 @@ static int build_model(UprModel* m, ParamSet& P) {
 // ---------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------
+// The multi-scale side stream of (current device, caller stream), created on
+// first use: non-blocking, joined through events every forward.  nullptr keeps
+// the whole forward on the caller's stream: UPR_MS_STREAMS=0 (A/B timing).
+// UPR_MS_PRIO: the side stream's priority (-1 high, 0 normal, 1 low).
+using Side = UprModel::Side;
+static std::shared_ptr<Side> side_of(UprModel* m, hipStream_t st) {
+  static const int en = [] {
+    const char* e = getenv("UPR_MS_STREAMS");
+    return (e && atoi(e) == 0) ? 0 : 1;
+  }();
+  static const int prio = [] {
+    const char* e = getenv("UPR_MS_PRIO");
+    return e ? atoi(e) : 0;
+  }();
+  if (!en) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(m->sides_mu);
+  auto it = m->sides.find({dev, st});
+  if (it != m->sides.end()) {
+    it->second->last_use = ++m->side_clock;
+    return it->second;
+  }
+  auto sd = std::make_shared<Side>();
+  int least = 0, greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = greatest = 0;
+  const int p = prio < 0 ? greatest : prio > 0 ? least : 0;
+  if (hipStreamCreateWithPriority(&sd->s, hipStreamNonBlocking, p) != hipSuccess ||
+      hipEventCreateWithFlags(&sd->fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&sd->join, hipEventDisableTiming) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;  // ~Side releases what was created
+  }
+  if (m->sides.size() >= UprModel::kMaxSides) {
+    auto old = m->sides.begin();
+    for (auto i = m->sides.begin(); i != m->sides.end(); ++i)
+      if (i->second->last_use < old->second->last_use) old = i;
+    m->sides.erase(old);
+  }
+  sd->last_use = ++m->side_clock;
+  m->sides[{dev, st}] = sd;
+  return sd;
+}
+
 static int run_forward(UprModel* m, const void* x, int B, int H, int W, void* enh, void* refl, void* illu,
                        uint8_t* ws, hipStream_t st) {
   size_t offs[B_COUNT] = {0};
@@ -835,7 +904,8 @@ static int run_forward(UprModel* m, const void* x, int B, int H, int W, void* en
     m->cur_bytes.assign(nops, 0.0);
   }
   const double elt = dt == kF16 ? 2.0 : 4.0;
-  for (size_t oi = 0; oi < nops; ++oi) {
+  // launch op oi on stream st (the caller's stream or the multi-scale side stream)
+  auto run_op = [&](size_t oi, hipStream_t st) -> int {
     const Op& o = m->ops[oi];
     int rc = kOk;
     if (m->prof) UPR_CHECK_HIP(hipEventRecord(evs[2 * oi], st));
@@ -958,7 +1028,30 @@ static int run_forward(UprModel* m, const void* x, int B, int H, int W, void* en
         break;
     }
     if (m->prof) UPR_CHECK_HIP(hipEventRecord(evs[2 * oi + 1], st));
+    return rc;
+  };
+  // profiled forwards stay on one stream (per-op events time one kernel each)
+  const std::shared_ptr<Side> sd =
+      (!m->prof && m->side_begin > 0 && m->side_end > m->side_begin) ? side_of(m, st) : nullptr;
+  if (!sd) {
+    for (size_t oi = 0; oi < nops; ++oi) {
+      const int rc = run_op(oi, st);
+      if (rc != kOk) return rc;
+    }
+  } else {
+    // op 0 -> fork -> side: the multi-scale ops, main: the IENet -> join -> tail
+    int rc = run_op(0, st);
     if (rc != kOk) return rc;
+    UPR_CHECK_HIP(hipEventRecord(sd->fork, st));
+    UPR_CHECK_HIP(hipStreamWaitEvent(sd->s, sd->fork, 0));
+    for (int oi = m->side_begin; oi < m->side_end; ++oi)
+      if ((rc = run_op(oi, sd->s)) != kOk) return rc;
+    UPR_CHECK_HIP(hipEventRecord(sd->join, sd->s));
+    for (int oi = 1; oi < m->side_begin; ++oi)
+      if ((rc = run_op(oi, st)) != kOk) return rc;
+    UPR_CHECK_HIP(hipStreamWaitEvent(st, sd->join, 0));
+    for (size_t oi = m->side_end; oi < nops; ++oi)
+      if ((rc = run_op(oi, st)) != kOk) return rc;
   }
   if (m->prof) {
     m->ev_pending.push_back(evs);
@@ -1084,6 +1177,7 @@ void upr_model_destroy(UprModel* model) {
   if (!model) return;
   upr_model_profile(model, 0);
   for (auto e : model->ev_free) (void)hipEventDestroy(e);
+  model->sides.clear();  // ~Side: synchronise, destroy
   if (model->dev_blob) (void)hipFree(model->dev_blob);
   delete model;
 }
