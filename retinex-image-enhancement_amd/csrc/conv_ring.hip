@@ -1135,6 +1135,12 @@ __global__ __launch_bounds__(256) void conv_ring32_kernel(RingArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// CU budget of the persistent ring grids launched by this host thread (0: all
+// CUs): the executor caps the multi-scale side stream's ring convs so that they
+// stream beside the IENet's kernels instead of claiming every CU (ring_set_cu_cap)
+static thread_local int t_ring_cu_cap = 0;
+void ring_set_cu_cap(int cus) { t_ring_cu_cap = cus; }
+
 static int ring_cus() {
   static int cus = 0;
   if (!cus) {
@@ -1143,6 +1149,7 @@ static int ring_cus() {
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
       cus = 256;
   }
+  if (t_ring_cu_cap > 0 && t_ring_cu_cap < cus) return std::max(8, t_ring_cu_cap / 8 * 8);
   return cus;
 }
 

@@ -830,6 +830,16 @@ static int build_model(UprModel* m, ParamSet& P) {
 // first use: non-blocking, joined through events every forward.  nullptr keeps
 // the whole forward on the caller's stream: UPR_MS_STREAMS=0 (A/B timing).
 // UPR_MS_PRIO: the side stream's priority (-1 high, 0 normal, 1 low).
+void ring_set_cu_cap(int cus);  // conv_ring.hip
+// UPR_SIDE_CUS: CU budget of the side stream's persistent ring convs (0: all)
+static int side_cu_cap() {
+  static const int v = [] {
+    const char* e = getenv("UPR_SIDE_CUS");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 using Side = UprModel::Side;
 static std::shared_ptr<Side> side_of(UprModel* m, hipStream_t st) {
   static const int en = [] {
@@ -1044,8 +1054,11 @@ static int run_forward(UprModel* m, const void* x, int B, int H, int W, void* en
     if (rc != kOk) return rc;
     UPR_CHECK_HIP(hipEventRecord(sd->fork, st));
     UPR_CHECK_HIP(hipStreamWaitEvent(sd->s, sd->fork, 0));
+    ring_set_cu_cap(side_cu_cap());
     for (int oi = m->side_begin; oi < m->side_end; ++oi)
-      if ((rc = run_op(oi, sd->s)) != kOk) return rc;
+      if ((rc = run_op(oi, sd->s)) != kOk) break;
+    ring_set_cu_cap(0);
+    if (rc != kOk) return rc;
     UPR_CHECK_HIP(hipEventRecord(sd->join, sd->s));
     for (int oi = 1; oi < m->side_begin; ++oi)
       if ((rc = run_op(oi, st)) != kOk) return rc;
