@@ -840,6 +840,21 @@ static int side_cu_cap() {
   return v;
 }
 
+// UPR_MS_FORK: fork the side stream before the first IENet op whose name
+// contains this string (e.g. "enc3": the multi-scale ops then overlap the
+// MFMA-bound 64^2-128^2 middle of the IENet instead of its HBM-bound 512^2
+// start); unset / not found: right after op 0
+static int fork_op(const UprModel* m) {
+  static const std::string key = [] {
+    const char* e = getenv("UPR_MS_FORK");
+    return std::string(e ? e : "");
+  }();
+  if (!key.empty())
+    for (int i = 1; i < m->side_begin; ++i)
+      if (m->ops[i].name.find(key) != std::string::npos) return i;
+  return 1;
+}
+
 using Side = UprModel::Side;
 static std::shared_ptr<Side> side_of(UprModel* m, hipStream_t st) {
   static const int en = [] {
@@ -1049,9 +1064,13 @@ static int run_forward(UprModel* m, const void* x, int B, int H, int W, void* en
       if (rc != kOk) return rc;
     }
   } else {
-    // op 0 -> fork -> side: the multi-scale ops, main: the IENet -> join -> tail
-    int rc = run_op(0, st);
-    if (rc != kOk) return rc;
+    // IENet ops [0, fork) -> fork -> side: the multi-scale ops, main: the rest
+    // of the IENet -> join -> tail.  The fork point (fork_op) defaults to right
+    // after op 0 (the side ops need only its scale1 output)
+    const int fk = fork_op(m);
+    int rc = kOk;
+    for (int oi = 0; oi < fk; ++oi)
+      if ((rc = run_op(oi, st)) != kOk) return rc;
     UPR_CHECK_HIP(hipEventRecord(sd->fork, st));
     UPR_CHECK_HIP(hipStreamWaitEvent(sd->s, sd->fork, 0));
     ring_set_cu_cap(side_cu_cap());
@@ -1060,7 +1079,7 @@ static int run_forward(UprModel* m, const void* x, int B, int H, int W, void* en
     ring_set_cu_cap(0);
     if (rc != kOk) return rc;
     UPR_CHECK_HIP(hipEventRecord(sd->join, sd->s));
-    for (int oi = 1; oi < m->side_begin; ++oi)
+    for (int oi = fk; oi < m->side_begin; ++oi)
       if ((rc = run_op(oi, st)) != kOk) return rc;
     UPR_CHECK_HIP(hipStreamWaitEvent(st, sd->join, 0));
     for (size_t oi = m->side_end; oi < nops; ++oi)
