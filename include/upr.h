@@ -74,9 +74,10 @@ size_t upr_model_workspace(const UprModel* model, int B, int H, int W);
  * (multi_scale_enhance(x, reflectance, illu), :415-443) `refl` is an INPUT
  * [B,3,H,W], only `enh` is written and `illu` may be NULL (the reference
  * method does not read it).
- * The full model forks its multi-scale ops onto an internal side stream after
- * the first conv and joins it before the Retinex tail: completion of `stream`
- * implies completion of the whole forward (env UPR_MS_STREAMS=0: one stream). */
+ * An fp16 full model forks its multi-scale ops onto an internal side stream
+ * after the first conv and joins it before the Retinex tail: completion of
+ * `stream` implies completion of the whole forward (env UPR_MS_STREAMS=0: one
+ * stream for every model, =1: fp32 models fork too). */
 int upr_model_forward(UprModel* model, const void* x, int B, int H, int W, void* enh, void* refl, void* illu,
                       void* workspace, size_t workspace_bytes, void* stream);
 

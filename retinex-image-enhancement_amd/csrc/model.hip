@@ -828,7 +828,8 @@ static int build_model(UprModel* m, ParamSet& P) {
 // ---------------------------------------------------------------------------
 // The multi-scale side stream of (current device, caller stream), created on
 // first use: non-blocking, joined through events every forward.  nullptr keeps
-// the whole forward on the caller's stream: UPR_MS_STREAMS=0 (A/B timing).
+// the whole forward on the caller's stream: UPR_MS_STREAMS=0 (A/B timing;
+// =1 forks fp32 models too, unset forks fp16 models only).
 // UPR_MS_PRIO: the side stream's priority (-1 high, 0 normal, 1 low).
 void ring_set_cu_cap(int cus);  // conv_ring.hip
 // UPR_SIDE_CUS: CU budget of the side stream's persistent ring convs (0: all)
@@ -859,13 +860,16 @@ using Side = UprModel::Side;
 static std::shared_ptr<Side> side_of(UprModel* m, hipStream_t st) {
   static const int en = [] {
     const char* e = getenv("UPR_MS_STREAMS");
-    return (e && atoi(e) == 0) ? 0 : 1;
+    return e ? (atoi(e) != 0 ? 1 : 0) : -1;
   }();
   static const int prio = [] {
     const char* e = getenv("UPR_MS_PRIO");
     return e ? atoi(e) : 0;
   }();
-  if (!en) return nullptr;
+  // default: fp16 models only.  fp32 gains ~1% (every fp32 conv is MFMA-bound,
+  // profiles/r3_ms_streams_ab.txt) and a single stream keeps each kernel's
+  // duration separable in a trace (the headline's rocprofv3 evidence)
+  if (en == 0 || (en < 0 && m->dtype != kF16)) return nullptr;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
   std::lock_guard<std::mutex> lk(m->sides_mu);

@@ -396,7 +396,10 @@ def test_multiscale_side_stream_matches_serial(dtype):
     profiled forward (upr_model_profile) keeps every op on the caller's stream.
     Both orders give bit-identical outputs, on the default stream and on a
     non-default caller stream, for repeated forwards of different batches
-    (a missing fork / join edge would read a half-written buffer)."""
+    (a missing fork / join edge would read a half-written buffer).  fp16
+    models fork by default; fp32 ones only under UPR_MS_STREAMS=1
+    (tools/gpu/env_ab.sh runs this file under its B env), else this is the
+    serial order twice."""
     m = make_model(True, True).to(DEV)
     if dtype == torch.float16:
         m = m.half()
