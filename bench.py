@@ -422,6 +422,17 @@ def forward_leg(args, world, rank, dev, precision, variant, B, S, traffic, cpu_s
                        "all": "(+ timed final collect: RCCL all_gather_into_tensor of fp16 enhanced to every rank)",
                        "rank0": "(+ timed final collect: RCCL gather of fp16 enhanced to rank 0)"}[args.collect]},
     }
+    ms_env = os.environ.get("UPR_MS_STREAMS")  # csrc/model.hip side_of: atoi(), unset = fp16 only
+    if ms_env is None:
+        two = precision == "fp16"
+    else:
+        try:
+            two = int(ms_env.strip() or "0") != 0
+        except ValueError:
+            two = False
+    out["executor"] = ("two streams: the multi-scale ops on a side stream forked after the first conv, joined "
+                       "before the Retinex tail (DESIGN §3)" if two else "one stream") + \
+        ("; roofline per-launch events from the serialised profiled step" if stats else "")
     if stats:
         rf = conv_roofline(stats, precision, B, traffic)
         rf["ref_equiv_tflops"] = REF_GFLOP_PER_IMG[variant] * (S / 512) ** 2 * total / world / elapsed / 1e3
