@@ -1081,11 +1081,14 @@ static int run_forward(UprModel* m, const void* x, int B, int H, int W, void* en
     for (int oi = m->side_begin; oi < m->side_end; ++oi)
       if ((rc = run_op(oi, sd->s)) != kOk) break;
     ring_set_cu_cap(0);
-    if (rc != kOk) return rc;
+    // joined on every path once forked: after an error return too, completion
+    // of the caller's stream still covers whatever the side stream enqueued
     UPR_CHECK_HIP(hipEventRecord(sd->join, sd->s));
-    for (int oi = fk; oi < m->side_begin; ++oi)
-      if ((rc = run_op(oi, st)) != kOk) return rc;
+    if (rc == kOk)
+      for (int oi = fk; oi < m->side_begin; ++oi)
+        if ((rc = run_op(oi, st)) != kOk) break;
     UPR_CHECK_HIP(hipStreamWaitEvent(st, sd->join, 0));
+    if (rc != kOk) return rc;
     for (size_t oi = m->side_end; oi < nops; ++oi)
       if ((rc = run_op(oi, st)) != kOk) return rc;
   }
