@@ -30,7 +30,7 @@ Extra objects on the JSON line:
                 child passes run before this process touches the GPU (N=1 only:
                 the numbers are per rank, and the passes need the whole GPU);
                 --ceilings adds the fractions against measured MFMA / HBM rates
-  parity        image 0 of rank 0's last timed batch vs the CPU oracle, at any world size
+  parity        images 0 and B-1 of rank 0's last timed batch vs the CPU oracle, at any world size
   cpu_baseline  the CPU oracle (oracle/net.py, torch-CPU fp32) on the host cores this process may use,
                 rank 0 of an N=1 run only: 1 warm-up image, then the median of 3 timed repetitions of the sample
 """
@@ -167,19 +167,21 @@ def cpu_train_baseline(sd, size):
 
 
 def parity_vs_cpu(sd, pre, aspp, x, outs, precision):
-    """Per-pixel max |d| of image 0 of the last timed step's outputs against the
-    CPU oracle (oracle/net.py, fp32) on the same input (the fp16 run's input is
-    the fp16-rounded image, widened to fp32 for the oracle)."""
+    """Per-pixel max |d| of images 0 and B-1 of the last timed step's outputs
+    (the first and last image of the shard, as the GPU tests check) against
+    the CPU oracle (oracle/net.py, fp32) on the same inputs (the fp16 run's
+    input is the fp16-rounded image, widened to fp32 for the oracle)."""
     from oracle import net as onet  # checker only
+    idx = [0] if x.shape[0] == 1 else [0, x.shape[0] - 1]
     with torch.no_grad():
-        ref = onet.forward(sd, x[:1].float().cpu(), pre, aspp)
+        ref = onet.forward(sd, x[idx].float().cpu(), pre, aspp)
     names = ("enhanced", "reflectance", "illumination")
-    d = {n: (o[:1].float().cpu() - r).abs().max().item() for n, o, r in zip(names, outs, ref)}
+    d = {n: (o[idx].float().cpu() - r).abs().max().item() for n, o, r in zip(names, outs, ref)}
     if precision == "fp16":  # reflectance x/(I+1e-6) is unbounded: relative to max(1, max|R|) as in the tests
         d["reflectance"] /= max(1.0, ref[1].abs().max().item())
     tol = 1e-3  # fp32: north_star; fp16: tests/test_gpu_bn_parity.py FP16_TOL
-    return {"max_abs_diff": d, "tol": tol, "pass": all(v <= tol for v in d.values()),
-            "sample": "image 0 of rank 0's last timed batch vs oracle/net.py fp32 on host cores"}
+    return {"max_abs_diff": d, "tol": tol, "pass": all(v <= tol for v in d.values()), "images": idx,
+            "sample": f"images {idx} of rank 0's last timed batch vs oracle/net.py fp32 on host cores"}
 
 
 # ----------------------------------------------------------------------------
@@ -328,11 +330,24 @@ def collect_fn(mode, world):
 # ----------------------------------------------------------------------------
 # forward leg (configs[1] / [2] / [3])
 # ----------------------------------------------------------------------------
-def _cfg_index(precision, variant, size):
-    """BASELINE.json configs[] entry a forward run corresponds to."""
-    if size == 1024 and variant == "preact_aspp":
-        return 3  # bs=256 1024^2 over 8 GPUs = 32 per GPU
-    return 1 if precision == "fp32" and variant == "plain" else 2
+def cfg_label(precision, variant, size, batch):
+    """The BASELINE.json configs[] entry a forward run IS, or "off-config".
+
+    configs[1]: bs=32 512^2 random-init forward, fp32 (the plain model, the
+                reference's default UP_Retinex flags in bench terms);
+    configs[2]: bs=32 512^2 fp16 with ASPP + preact;
+    configs[3]: bs=256 1024^2 over 8 GPUs, i.e. 32 images of 1024^2 per GPU,
+                preact + ASPP (the UP_Retinex() default of enhance_batch_images),
+                fp32 or fp16 (BASELINE.json names no precision).
+    Anything else (fp16 plain, fp32 preact+ASPP at 512^2, other batch sizes)
+    is a number on a config BASELINE.json does not define."""
+    if batch == 32 and size == 512 and precision == "fp32" and variant == "plain":
+        return "configs[1]"
+    if batch == 32 and size == 512 and precision == "fp16" and variant == "preact_aspp":
+        return "configs[2]"
+    if batch == 32 and size == 1024 and variant == "preact_aspp":
+        return "configs[3]"
+    return "off-config"
 
 
 def conv_roofline(stats, precision, B, traffic):
@@ -414,7 +429,7 @@ def forward_leg(args, world, rank, dev, precision, variant, B, S, traffic, cpu_s
         "scaling": "weak", "vs_baseline": None,
         "dtype": "f32" if precision == "fp32" else "f16 (fp32 accumulate)",
         "data": "synthetic torch.rand inputs, random-init weights (torch.manual_seed(0))",
-        "config": {"workload": f"configs[{_cfg_index(precision, variant, S)}]: bs={B}/GPU {S}x{S} "
+        "config": {"workload": f"{cfg_label(precision, variant, S, B)}: bs={B}/GPU {S}x{S} "
                                f"{variant} forward, {precision}",
                    "global_batch": world * B, "image_size": S, "variant": variant,
                    "parallelism": f"batch-shard x{world} " + {
@@ -614,15 +629,17 @@ def dry_run(args):
         ranks = [(rank, os.getpid())]
     if rank == 0:
         stand_in = {"value": None, "note": "dry run: no GPU work"}
+        wl = "configs[4]" if args.train else cfg_label(args.precision, args.variant, args.size, args.batch)
         out = {"metric": "dry run (no GPU work)", "value": world * args.steps / elapsed, "unit": "steps/s",
                "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": 1000.0 * elapsed / args.steps, "ranks": ranks, "data": "none",
-               "config": {"parallelism": f"batch-shard x{world} collect={args.collect}"},
+               "config": {"workload": wl, "parallelism": f"batch-shard x{world} collect={args.collect}"},
                "roofline": dict(stand_in, traffic=None), "parity": dict(stand_in, max_abs_diff=None)}
         if world == 1:
             out["cpu_baseline"] = dict(stand_in, cpu=cpu_info())
-        if not args.no_nested:
-            out["fp16_preact_aspp"] = {"value": None, "roofline": None, "parity": dict(stand_in)}
+        if not args.no_nested and not args.train and not (args.precision == "fp16" and args.variant == "preact_aspp"):
+            out["fp16_preact_aspp"] = {"value": None, "roofline": None, "parity": dict(stand_in),
+                                       "config": {"workload": cfg_label("fp16", "preact_aspp", args.size, args.batch)}}
             if world == 1:
                 out["train_amp"] = {"value": None, "roofline": None}
         print(json.dumps(out))
@@ -659,9 +676,8 @@ def main():
     out = forward_leg(args, world, rank, dev, args.precision, args.variant, B, S, traffic,
                       (B, "the full timed batch"))
     if nested:
-        n16 = min(B, 8)
         out["fp16_preact_aspp"] = forward_leg(args, world, rank, dev, "fp16", "preact_aspp", B, S, traffic16,
-                                              (n16, f"a bounded {n16}-image sample of the timed batch's shape"))
+                                              (B, "the full timed batch"))
         if world == 1:
             out["train_amp"] = train_leg(args, world, rank, dev, 8, S, True, 5, 2, "plain")
     if rank == 0:

@@ -15,7 +15,12 @@
  *   - return 0 on success, a hipError_t value (> 0) passed through, or a
  *     negative UPR_ERR_* code; upr_status_string() describes either.
  * Thread safety: distinct models / streams may be used concurrently; one model
- * handle must not be used on two streams at once.
+ * handle must not be used on two streams at once.  A forward of an fp16 model
+ * forks its multi-scale head onto a side stream of the library's own, keyed
+ * by (device, caller stream); the pseudo-handles that name a different real
+ * stream per thread (NULL and hipStreamPerThread) never fork: such forwards
+ * run on the one stream, so two threads passing the same pseudo-handle never
+ * share a side stream.
  */
 #ifndef UPR_H_
 #define UPR_H_
@@ -59,7 +64,9 @@ typedef struct {
  * UPR_MODEL_IENET_ONLY): packs an eval-mode state_dict (BatchNorm folded,
  * linear 1x1 chains composed, weights laid out [N][K] in `dtype`) into device
  * memory owned by the handle.  Keys follow the reference state_dict
- * (ResidualIENet keys carry the "ie_net." prefix). */
+ * (ResidualIENet keys carry the "ie_net." prefix).  `flags`: 0 or ONE of
+ * UPR_MODEL_IENET_ONLY / UPR_MODEL_HEAD_ONLY; unknown bits or both flags
+ * return UPR_ERR_ARG before any device call. */
 int upr_model_create(const UprTensorDesc* params, int n_params, int use_preact, int use_aspp, int dtype,
                      int flags, UprModel** out);
 

@@ -870,6 +870,11 @@ static std::shared_ptr<Side> side_of(UprModel* m, hipStream_t st) {
   // profiles/r3_ms_streams_ab.txt) and a single stream keeps each kernel's
   // duration separable in a trace (the headline's rocprofv3 evidence)
   if (en == 0 || (en < 0 && m->dtype != kF16)) return nullptr;
+  // a pseudo-handle names a different real stream per calling thread
+  // (hipStreamPerThread, and the null stream under per-thread default
+  // streams): a Side keyed by it would be shared by threads whose fork / join
+  // events then interleave.  Those forwards stay on the one stream (upr.h)
+  if (st == nullptr || st == hipStreamPerThread) return nullptr;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
   std::lock_guard<std::mutex> lk(m->sides_mu);
@@ -1131,6 +1136,10 @@ int upr_model_create(const UprTensorDesc* params, int n_params, int use_preact, 
                      UprModel** out) {
   if (!out || (n_params > 0 && !params) || (dtype != UPR_F32 && dtype != UPR_F16)) return UPR_ERR_ARG;
   *out = nullptr;
+  // one of the two partial graphs at most, and no unknown bits (IENET_ONLY |
+  // HEAD_ONLY would build neither the IENet nor the head and write nothing)
+  constexpr int kKnownFlags = UPR_MODEL_IENET_ONLY | UPR_MODEL_HEAD_ONLY;
+  if ((flags & ~kKnownFlags) || (flags & kKnownFlags) == kKnownFlags) return UPR_ERR_ARG;
   ParamSet P;
   for (int i = 0; i < n_params; ++i) {
     const UprTensorDesc& d = params[i];

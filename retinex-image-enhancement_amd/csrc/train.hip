@@ -119,12 +119,14 @@ void* scratch(int slot, size_t bytes, hipStream_t st) {
   struct Entry {
     int dev;
     hipStream_t st;
+    unsigned long long last_use;
     void* p[kSlotCount];
     size_t n[kSlotCount];
   };
   static std::mutex mu;
-  static Entry tab[64];
+  static Entry tab[kScratchStreams];
   static int used = 0;
+  static unsigned long long clock = 0;
   if (slot < 0 || slot >= kSlotCount) return nullptr;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
@@ -133,12 +135,28 @@ void* scratch(int slot, size_t bytes, hipStream_t st) {
   for (int i = 0; i < used; ++i)
     if (tab[i].dev == dev && tab[i].st == st) e = &tab[i];
   if (!e) {
-    if (used == 64) return nullptr;
-    e = &tab[used++];
+    if (used < kScratchStreams) {
+      e = &tab[used++];
+    } else {
+      // full: evict the least recently used (device, stream).  Its stream may
+      // have been destroyed since, so its kernels are waited for by a device
+      // synchronise of ITS device (rare: only once more than kScratchStreams
+      // streams have called in), then its buffers are freed and reused
+      e = &tab[0];
+      for (int i = 1; i < used; ++i)
+        if (tab[i].last_use < e->last_use) e = &tab[i];
+      if (e->dev != dev && hipSetDevice(e->dev) != hipSuccess) return nullptr;
+      const hipError_t se = hipDeviceSynchronize();
+      for (int s = 0; s < kSlotCount; ++s)
+        if (e->p[s]) (void)hipFree(e->p[s]);
+      if (e->dev != dev) (void)hipSetDevice(dev);
+      if (se != hipSuccess) return nullptr;
+    }
     memset(e, 0, sizeof(*e));
     e->dev = dev;
     e->st = st;
   }
+  e->last_use = ++clock;
   if (bytes == 0) bytes = 16;
   if (e->n[slot] < bytes) {
     if (e->p[slot]) {

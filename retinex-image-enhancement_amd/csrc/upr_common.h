@@ -154,6 +154,9 @@ inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 // call on this stack (13 of 36 ms per training step went to them) and
 // stalled the launch queue.  Growth (warm-up only) synchronises the stream
 // before freeing the smaller buffer.  Returns nullptr when out of memory.
+// At most kScratchStreams (device, stream) pairs hold buffers; a new pair
+// past that evicts the least recently used one (device synchronise + free).
+constexpr int kScratchStreams = 64;
 enum ScratchSlot { kSlotSlab = 0, kSlotCast, kSlotTmp, kSlotCode, kSlotRows, kSlotPart, kSlotCount };
 void* scratch(int slot, size_t bytes, hipStream_t st);
 

@@ -227,11 +227,13 @@ class MultiScaleUP_Retinex(_HipGraphMixin, nn.Module):
         alone on the HIP kernels (UPR_MODEL_HEAD_ONLY handle).  The head has no
         BatchNorm or Dropout, so train and eval mode compute the same values;
         like the eval-mode forward, the result records no autograd history
-        (training gradients flow through forward())."""
+        (training gradients flow through forward()).  Inputs that require
+        grad are refused in either mode (with grad enabled) rather than
+        silently getting no gradient."""
         from upr.runtime import _require_device
         _require_device(x)
         _require_device(reflectance, "reflectance")
-        if torch.is_grad_enabled() and (reflectance.requires_grad or x.requires_grad) and self.training:
+        if torch.is_grad_enabled() and (reflectance.requires_grad or x.requires_grad):
             raise NotImplementedError("multi_scale_enhance: gradients through the head alone are not provided; "
                                       "train through forward() (the full graph's backward covers the head)")
         key = ("head", x.device, x.dtype)

@@ -55,15 +55,21 @@ def gather_to_rank0(local, total, group=None, dst=0):
     rank 0 if only rank 0 writes"): one gather, so the fabric carries each
     shard once instead of to every rank as the all-gather does.  Returns the
     [total, ...] tensor on `dst`, None elsewhere.  Shards are padded to the
-    largest size (dist.gather needs equal shapes); padding is dropped."""
+    largest size (dist.gather needs equal shapes); padding is dropped.
+
+    `dst` and the shard order are GROUP ranks (shard r is group rank r's);
+    dist.gather takes a global rank, so `dst` is translated for it."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    if not 0 <= dst < world:
+        raise ValueError(f"dst {dst} is not a rank of the group (size {world})")
+    dst_global = dst if group is None else dist.get_global_rank(group, dst)
     per = -(-total // world)
     pad = per - local.shape[0]
     buf = local if pad == 0 else torch.cat([local, local.new_zeros((pad,) + tuple(local.shape[1:]))])
     buf = buf.contiguous()
     parts = [torch.empty_like(buf) for _ in range(world)] if rank == dst else None
-    dist.gather(buf, parts, dst=dst, group=group)
+    dist.gather(buf, parts, dst=dst_global, group=group)
     if rank != dst:
         return None
     keep = []

@@ -55,6 +55,41 @@ def test_gloo_gather_world2():
         assert sorted(res) == [(0, True), (1, True)]
 
 
+def _subgroup_worker(rank, world, port, total, q):
+    """World 3; the subgroup is global ranks {1, 2}: its group rank 0 is global
+    rank 1, so gather_to_rank0(dst=0) must land on global rank 1."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sub = dist.new_group([1, 2])  # every rank takes part in new_group
+    ok = True
+    if rank in (1, 2):
+        full = torch.arange(total * 4, dtype=torch.float32).reshape(total, 4)
+        gr = dist.get_rank(sub)
+        a, b = shard_bounds(total, 2, gr)
+        g0 = gather_to_rank0(full[a:b] * 1.0, total, group=sub, dst=0)
+        ok = bool(torch.equal(g0, full)) if rank == 1 else g0 is None
+        g1 = gather_to_rank0(full[a:b] * 1.0, total, group=sub, dst=1)
+        ok = ok and (bool(torch.equal(g1, full)) if rank == 2 else g1 is None)
+        got = gather_shards(full[a:b] * 1.0, total, group=sub)
+        ok = ok and bool(torch.equal(got, full))
+    q.put((rank, ok))
+    dist.destroy_process_group()
+
+
+def test_gloo_gather_subgroup_world3():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_subgroup_worker, args=(r, 3, port, 5, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert sorted(res) == [(0, True), (1, True), (2, True)]
+
+
 def _grad_worker(rank, world, port, q):
     from types import SimpleNamespace
     from upr.dist import allreduce_grads
@@ -135,3 +170,28 @@ def test_bench_n1_line_carries_cpu_and_train_keys():
         assert k in out, k
     ci = out["cpu_baseline"]["cpu"]
     assert ci["threads"] >= 1 and "cpu_model" in ci and ci["os_cpu_count"] >= ci["threads"]
+
+
+def test_bench_config_labels():
+    """bench.py names only the configs BASELINE.json defines; every other
+    combination is labelled off-config (the dry-run line carries the label)."""
+    import importlib.util
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(repo, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    assert b.cfg_label("fp32", "plain", 512, 32) == "configs[1]"
+    assert b.cfg_label("fp16", "preact_aspp", 512, 32) == "configs[2]"
+    assert b.cfg_label("fp16", "preact_aspp", 1024, 32) == "configs[3]"
+    assert b.cfg_label("fp32", "preact_aspp", 1024, 32) == "configs[3]"
+    for args in (("fp16", "plain", 512, 32), ("fp32", "preact_aspp", 512, 32), ("fp32", "plain", 512, 8),
+                 ("fp16", "preact_aspp", 512, 16), ("fp32", "plain", 1024, 32), ("fp16", "preact_aspp", 256, 32)):
+        assert b.cfg_label(*args) == "off-config", args
+    out = _bench_json(["--dry-run", "--steps", "1", "--warmup", "0"])
+    assert out["config"]["workload"] == "configs[1]"
+    assert out["fp16_preact_aspp"]["config"]["workload"] == "configs[2]"
+    out = _bench_json(["--dry-run", "--steps", "1", "--warmup", "0", "--precision", "fp16"])
+    assert out["config"]["workload"] == "off-config"
+    out = _bench_json(["--dry-run", "--steps", "1", "--warmup", "0", "--precision", "fp16", "--variant",
+                       "preact_aspp", "--size", "1024"])
+    assert out["config"]["workload"] == "configs[3]" and "fp16_preact_aspp" not in out

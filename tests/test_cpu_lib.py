@@ -59,6 +59,11 @@ def test_null_args_rejected_without_device():
         == L.UPR_ERR_ARG
     out = ctypes.c_void_p()
     assert lib.upr_model_create(None, 0, 0, 0, 7, 0, ctypes.byref(out)) == L.UPR_ERR_ARG
+    # flags: at most one of IENET_ONLY (1) / HEAD_ONLY (2), no unknown bits -- refused
+    # before the (empty) state_dict is even looked at, so before any device call
+    for bad in (3, 4, 8, 1 << 20, -1):
+        assert lib.upr_model_create(None, 0, 0, 0, 0, bad, ctypes.byref(out)) == L.UPR_ERR_ARG, bad
+        assert not out.value
     # training entries (include/upr_train.h) validate before touching the device
     assert lib.upr_t_conv_mfma(None, 1, 8, 8, 32, 32, 0, None, None, 32, 3, 3, 1, 1, 1, None, 0, 0, None, 32, 0, 0,
                                None) == L.UPR_ERR_ARG

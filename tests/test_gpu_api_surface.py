@@ -74,6 +74,14 @@ def test_multi_scale_enhance_matches_forward_and_oracle(pre, aspp):
     err = (e3.cpu() - ref).abs().max().item()
     print(f"multi_scale_enhance pre={pre} aspp={aspp}: max|d| {err:.2e}")
     assert err <= 1e-4
+    # an input that requires grad is refused in eval mode as in training mode
+    # (no silently detached result); without grad inputs the eval result has no history
+    rg = r.to(DEV).requires_grad_(True)
+    for train in (False, True):
+        with pytest.raises(NotImplementedError, match="gradients"):
+            model.train(train).multi_scale_enhance(x.to(DEV), rg, None)
+    e4 = model.eval().multi_scale_enhance(x.to(DEV), r.to(DEV), None)
+    assert not e4.requires_grad and torch.equal(e4, e3)
     # float16 model
     m16 = model.half()
     with torch.no_grad():

@@ -182,6 +182,50 @@ def test_maxpool_bwd_matches_torch(B, C, H, W, k, s, p, nchw):
     assert (out[m] - ref[m]).abs().max().item() <= 1e-6 * max(1.0, ref[m].abs().max().item())  # summation order
 
 
+def test_scratch_more_streams_than_table():
+    """The per-(device, stream) scratch table (upr_common.h scratch(), 64
+    entries) evicts its least recently used stream: a training call that needs
+    scratch keeps working on the 65th..80th distinct stream (it returned
+    hipErrorOutOfMemory once 64 streams had been seen), and every result is
+    still right -- including on streams created after earlier ones were
+    destroyed."""
+    import ctypes
+    import torch.nn.functional as F
+    from upr import _lib as L
+    torch.manual_seed(6)
+    B, C, H, W = 1, 4, 16, 16
+    x = torch.randn(B, C, H, W)
+    xr = x.clone().requires_grad_(True)
+    y = F.max_pool2d(xr, 2, 2, 0)
+    gy = torch.randn(y.shape)
+    y.backward(gy)
+    ref = xr.grad
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    gyd = gy.permute(0, 2, 3, 1).contiguous().to(DEV)
+    vx = L.UprView(xd.data_ptr(), H * W * C, W * C, C, 1)
+    vg = L.UprView(gyd.data_ptr(), 8 * 8 * C, 8 * C, C, 1)
+    lib = L.lib()
+    # raw HIP streams (torch.cuda.Stream() hands out a pool of 32 handles)
+    hip = ctypes.CDLL("libamdhip64.so")
+    live = []
+    for i in range(80):
+        s = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+        live.append(s)
+        dxd = torch.zeros(B, H, W, C, device=DEV)
+        vd = L.UprView(dxd.data_ptr(), H * W * C, W * C, C, 1)
+        torch.cuda.synchronize()
+        rc = lib.upr_t_maxpool_bwd(ctypes.byref(vx), ctypes.byref(vg), B, H, W, C, 2, 2, 0, 8, 8,
+                                   ctypes.byref(vd), s)
+        assert rc == 0, (i, rc)
+        assert hip.hipStreamSynchronize(s) == 0
+        assert torch.equal(dxd.permute(0, 3, 1, 2).cpu(), ref), i
+        if i % 3 == 0:  # destroyed while its scratch entry lives on
+            assert hip.hipStreamDestroy(live.pop()) == 0
+    for s in live:
+        assert hip.hipStreamDestroy(s) == 0
+
+
 @pytest.mark.parametrize("B,C,H,W,k,s,p,acc", [
     (2, 32, 40, 56, 3, 1, 1, 1),   # EnhancedFAM branch2 (fast 3x3/1/1 path, dx accumulated)
     (2, 64, 34, 50, 2, 2, 0, 0),   # VGG pool (fast 2x2/2 path, dx written)
