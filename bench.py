@@ -8,6 +8,9 @@ makes configs[2] the headline instead.  A default run (no --no-nested) adds
 two nested objects to the same JSON line, each with its own roofline, parity
 and CPU baseline:
   fp16_preact_aspp  configs[2]: bs 32 512^2 fp16 preact+ASPP forward
+  enhance           the enhancers main.py --mode enhance runs after the model (CLAHE-in-Lab,
+                    multi-scale factor + clamp) over a resident bs 32 512^2 batch (`--enhance`
+                    makes it the headline)
   train_amp         configs[4]: bs 8 512^2 AMP training step (rank 0 of an N=1
                     run only; `--train` makes it the headline)
 
@@ -80,6 +83,9 @@ def parse(argv=None):
                     help="time the final collect too: fp16 enhanced images to every rank (all) or to rank 0")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: gloo ranks run a small CPU step through the same launch / barrier / report path")
+    ap.add_argument("--enhance", action="store_true",
+                    help="the enhancer stage as the headline: CLAHE-in-Lab + multi-scale factor/clamp over a resident "
+                         "bs=32 512x512 batch (adaptive_params.py:121-169, multi_scale.py:62-100)")
     ap.add_argument("--amp", action="store_true",
                     help="with --train: the reference's AMP branch (autocast fp16 convs + GradScaler)")
     return ap.parse_args(argv)
@@ -193,7 +199,7 @@ CONV_KERNELS = ("conv_halo_kernel", "conv_igemm_kernel", "conv_wide_kernel", "co
                 "conv_hwide_kernel", "conv_hwide3_kernel", "conv_hwide4_kernel", "conv_t2_kernel", "conv_t2_f32_kernel")
 
 
-def pmc_traffic(precision, variant, batch, size):
+def pmc_traffic(precision, variant, batch, size, extra=(), kernels=CONV_KERNELS):
     """HBM bytes of the conv kernels per forward from rocprofv3 PMC counters.
 
     Two child passes of this script (one forward of warm-up + one timed) under
@@ -211,7 +217,7 @@ def pmc_traffic(precision, variant, batch, size):
     out = {}
     base = [sys.executable, os.path.abspath(__file__), "--steps", "1", "--warmup", "1", "--cpu-seconds", "0",
             "--no-profile", "--no-traffic", "--no-nested", "--batch", str(batch), "--size", str(size),
-            "--precision", precision, "--variant", variant]
+            "--precision", precision, "--variant", variant] + list(extra)
     env = dict(os.environ, TMPDIR="/tmp")
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix="upr_pmc_", dir="/tmp")
@@ -229,7 +235,7 @@ def pmc_traffic(precision, variant, batch, size):
             tot, n = 0.0, 0
             with open(path) as f:
                 for r in csv.DictReader(f):
-                    if r["Counter_Name"] == ctr and any(k in r["Kernel_Name"] for k in CONV_KERNELS):
+                    if r["Counter_Name"] == ctr and any(k in r["Kernel_Name"] for k in kernels):
                         tot += float(r["Counter_Value"])
                         n += 1
             out[ctr] = (tot, n)
@@ -607,6 +613,119 @@ def train_leg(args, world, rank, dev, B, S, amp, steps, warmup, variant):
 
 
 # ----------------------------------------------------------------------------
+# enhancer leg (what main.py --mode enhance runs after the model: SURVEY §8a a11-a16)
+# ----------------------------------------------------------------------------
+# the CLAHE-in-Lab pipeline's kernels (one upr_clahe_enhance call) and the multi-scale ones
+CLAHE_KERNELS = ("clahe_hist_kernel", "clahe_lut_kernel", "clahe_apply_kernel")
+MS_KERNELS = ("ms_sums_kernel", "ms_factor_kernel", "scale_clamp_kernel")
+
+
+def cpu_enhance_baseline(n, size):
+    """oracle/enhancers.py (numpy restatement of OpenCV's 8-bit Lab + CLAHE,
+    torch-CPU multi-scale features) on n images, single-threaded: 1 warm-up
+    image, then the median of CPU_REPS timed passes over the sample."""
+    from oracle import enhancers as oenh  # checker / baseline only
+    ci = cpu_info()
+    torch.set_num_threads(1)
+    g = torch.Generator().manual_seed(97)
+    x = torch.rand(n, 3, size, size, generator=g)
+    enh = torch.rand(n, 3, size, size, generator=g) * 0.8
+
+    def run(k):
+        oenh.clahe_enhancement(enh[:k])
+        fac = oenh.multiscale_factor(x[:k])
+        torch.stack([torch.clamp(enh[b] * fac[b], 0, 1) for b in range(k)])
+    run(1)
+    med, times = _median_reps(lambda: run(n))
+    torch.set_num_threads(ci["threads"])
+    return {"value": n / med, "unit": "images/s", "cores": 1, "kind": "port", "cpu": ci, "rep_seconds": times,
+            "sample": f"{n}x3x{size}x{size}: oracle/enhancers.py clahe_enhancement (numpy OpenCV restatement) + "
+                      f"multiscale_factor + clamp, one thread; 1-image warm-up, median of {CPU_REPS}"}
+
+
+def enhance_leg(args, world, rank, dev, B, S, traffic, cpu_n):
+    """One step = the enhancers over a resident batch of B SxS images: the
+    CLAHE-in-Lab pipeline of apply_clahe_enhancement on the enhanced images
+    (upr_clahe_enhance: quantise + Lab + tile histograms -> LUTs -> blend +
+    Lab->RGB) and the multi-scale factor + clamp of apply_multi_scale_enhancement
+    (upr_multiscale).  Each stage is timed with HIP events on the stream the
+    library launches on (torch's current stream) in every timed step."""
+    from upr import runtime
+    g = torch.Generator(device=dev).manual_seed(3 + rank)
+    x = torch.rand(B, 3, S, S, device=dev, generator=g)
+    enh = torch.rand(B, 3, S, S, device=dev, generator=g) * 0.8  # stand-in for the model's enhanced images
+    ev = []
+
+    def step():
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        e[0].record()
+        o1 = runtime.clahe_enhance(enh)
+        e[1].record()
+        o2, _, _ = runtime.multiscale(x, enh)
+        e[2].record()
+        ev.append(e)
+        return o1, o2
+
+    for _ in range(max(args.warmup, 1)):
+        step()
+    sync(world, dev)
+    ev.clear()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        last = step()
+    sync(world, dev)
+    elapsed = max_over_ranks(world, dev, time.perf_counter() - t0)
+    clahe_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / len(ev)
+    ms_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / len(ev)
+    HW = S * S
+    clahe_bytes = B * (HW * 24 + 8 * 8 * 256)   # fp32 RGB in + out, the tile LUTs
+    ms_bytes = B * HW * (12 * 3 + 24)           # 12 B/px per scale (SURVEY §8d) + the clamp pass
+    clahe_gbs = clahe_bytes / (clahe_ms * 1e-3) / 1e9
+    out = {
+        "metric": f"enhancer images/sec at {S}x{S} bs={B} per GPU (CLAHE-in-Lab + multi-scale factor/clamp)",
+        "value": world * B * args.steps / elapsed, "unit": "images/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8 (8-bit Lab / histograms) over f32 images",
+        "data": "synthetic torch.rand images (stand-in for the model's enhanced output)",
+        "config": {"workload": f"enhancers of main.py --mode enhance on a resident bs={B}/GPU {S}x{S} fp32 batch "
+                               f"(adaptive_params.py:121-169, multi_scale.py:62-100)",
+                   "global_batch": world * B, "image_size": S, "parallelism": f"batch-shard x{world}"},
+        "roofline": {
+            "bound": "hbm", "achieved": clahe_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": clahe_gbs / PEAK_HBM_GBS,
+            "traffic": traffic["bytes_per_forward"] if traffic else None,
+            "traffic_unit": "HBM bytes per upr_clahe_enhance call (all its kernel launches; rocprofv3 FETCH_SIZE*2 + "
+                            "WRITE_SIZE, N=1 only)",
+            "kernel": "upr_clahe_enhance: clahe_hist (+ clahe_lut when tiles are split into row bands) + clahe_apply "
+                      "(one call, HIP events around it)",
+            "alg_bytes": clahe_bytes, "alg_bytes_note": "24 B/px (fp32 RGB read once, written once) + 8x8x256 B LUTs "
+                                                        "per image; the u8 L/A/B planes between the kernels are not "
+                                                        "algorithmic",
+            "avg_call_ms": clahe_ms,
+            "multiscale": {"avg_call_ms": ms_ms, "alg_bytes": ms_bytes,
+                           "achieved_GBs": ms_bytes / (ms_ms * 1e-3) / 1e9,
+                           "frac": ms_bytes / (ms_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
+                           "kernel": "upr_multiscale: 3 ms_sums (one per scale) + factor + scale_clamp",
+                           "alg_bytes_note": "12 B/px per scale (SURVEY §8d) + 24 B/px clamp (read enh, write out)"},
+        },
+    }
+    if rank == 0:
+        # parity: images 0 and B-1 of the last step vs the restatement (bit-exact bytes expected)
+        from oracle import enhancers as oenh  # checker only
+        idx = [0, B - 1] if B > 1 else [0]
+        ref = oenh.clahe_enhancement(enh[idx].cpu())
+        d = (last[0][idx].cpu() - ref).abs().max().item()
+        out["parity"] = {"max_abs_diff": {"clahe": d}, "tol": 0.0, "pass": d == 0.0, "images": idx,
+                         "sample": f"CLAHE output of images {idx} of rank 0's last step vs oracle/enhancers.py "
+                                   f"(numpy OpenCV restatement; bit-exact)"}
+        if world == 1 and args.cpu_seconds > 0 and cpu_n:
+            out["cpu_baseline"] = cpu_enhance_baseline(cpu_n, S)
+    del x, enh, last
+    torch.cuda.empty_cache()
+    return out
+
+
+# ----------------------------------------------------------------------------
 # dry run: the same launch / rank / report path with a CPU stand-in step
 # ----------------------------------------------------------------------------
 def dry_run(args):
@@ -640,6 +759,7 @@ def dry_run(args):
         if not args.no_nested and not args.train and not (args.precision == "fp16" and args.variant == "preact_aspp"):
             out["fp16_preact_aspp"] = {"value": None, "roofline": None, "parity": dict(stand_in),
                                        "config": {"workload": cfg_label("fp16", "preact_aspp", args.size, args.batch)}}
+            out["enhance"] = {"value": None, "roofline": None, "parity": dict(stand_in)}
             if world == 1:
                 out["train_amp"] = {"value": None, "roofline": None}
         print(json.dumps(out))
@@ -655,6 +775,17 @@ def main():
     if args.dry_run:
         return dry_run(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.enhance:
+        trE = None
+        if world == 1 and not args.no_traffic and not any(k.startswith("ROCPROF") for k in os.environ):
+            trE = pmc_traffic("fp32", "plain", args.batch, args.size, ["--enhance"], CLAHE_KERNELS)
+        world, rank, dev = dist_setup(args)
+        out = enhance_leg(args, world, rank, dev, args.batch, args.size, trE, 4)
+        if rank == 0:
+            print(json.dumps(out))
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
     if args.train:
         world, rank, dev = dist_setup(args)
         out = train_leg(args, world, rank, dev, args.batch if args.batch != 32 else 8, args.size, args.amp,
@@ -665,12 +796,13 @@ def main():
             torch.distributed.destroy_process_group()
         return
     nested = not args.no_nested and not (args.precision == "fp16" and args.variant == "preact_aspp")
-    traffic = traffic16 = None
+    traffic = traffic16 = trafficE = None
     if world == 1 and not args.no_traffic and not any(k.startswith("ROCPROF") for k in os.environ):
         # child processes, before this process initialises the GPU
         traffic = pmc_traffic(args.precision, args.variant, args.batch, args.size)
         if nested:
             traffic16 = pmc_traffic("fp16", "preact_aspp", args.batch, args.size)
+            trafficE = pmc_traffic("fp32", "plain", args.batch, args.size, ["--enhance"], CLAHE_KERNELS)
     world, rank, dev = dist_setup(args)
     B, S = args.batch, args.size
     out = forward_leg(args, world, rank, dev, args.precision, args.variant, B, S, traffic,
@@ -678,6 +810,7 @@ def main():
     if nested:
         out["fp16_preact_aspp"] = forward_leg(args, world, rank, dev, "fp16", "preact_aspp", B, S, traffic16,
                                               (B, "the full timed batch"))
+        out["enhance"] = enhance_leg(args, world, rank, dev, B, S, trafficE, 4)
         if world == 1:
             out["train_amp"] = train_leg(args, world, rank, dev, 8, S, True, 5, 2, "plain")
     if rank == 0:

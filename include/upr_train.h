@@ -351,6 +351,12 @@ typedef struct UprLossParams {
   float freq_high;        /* FrequencyLoss weight_high [1] (:442) */
   float freq_low;         /* weight_low [0.5] */
   int dynamic_smooth;     /* TotalLoss use_dynamic_smooth_weight [1] (:617) */
+  int illu_channels;      /* channels of illu / g_illu: 1 (the model's [B,1,H,W]) or 3 (the
+                             reference self-test's [B,3,H,W], loss.py:806-844); 0 = 1.
+                             Smoothness: mean over the C planes (:148, :171-172); decoupling:
+                             C = 1 the expanded uncentred cross-covariance (:308-312) and
+                             the mse of channel-mean means (:326-329), C = 3 the centred 3x3
+                             covariance (:302-304) and the per-channel mean mse (:323-324) */
 } UprLossParams;
 /* Loss workspace bytes for a B x 3 x H x W batch (H, W multiples of 16). */
 size_t upr_t_loss_workspace(int B, int H, int W);

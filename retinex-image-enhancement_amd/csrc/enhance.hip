@@ -1,11 +1,11 @@
 // Enhancer kernels (gfx950): integer/histogram work, HBM/latency-bound.
 //
-//  quant_lab      float -> u8 cast exactly as numpy's astype(uint8) on x*255
-//                 (trunc, wrap mod 256; NaN/|v|>=2^31 -> 0), then 8-bit sRGB ->
-//                 Lab (enhancers/adaptive_params.py:142,145)
-//  clahe_lut      per-tile 256-bin LDS histogram, clip + redistribute, CDF -> LUT
+//  clahe_hist     float -> u8 cast exactly as numpy's astype(uint8) on x*255
+//                 (trunc, wrap mod 256; NaN/|v|>=2^31 -> 0), 8-bit sRGB -> Lab
+//                 (enhancers/adaptive_params.py:142,145), per-wave tile histograms
+//  clahe_lut      clip + redistribute, CDF -> LUT
 //                 (cv2.createCLAHE(2.0,(8,8)).apply, adaptive_params.py:149-152)
-//  clahe_lab2rgb  bilinear LUT blend of L, Lab -> sRGB 8-bit, /255 back to float
+//  clahe_apply    bilinear LUT blend of L, Lab -> sRGB 8-bit, /255 back to float
 //                 (adaptive_params.py:155-167)
 //  gray_hist      8-bit BGR2GRAY histogram (calculate_brightness_features :45-66)
 //  ms_sums        multi-scale feature sums (enhancers/multi_scale.py:17-60, :87-94)
@@ -96,23 +96,6 @@ __device__ __forceinline__ void lab2rgb_u8(const DevLab* T, int L, int A, int Bb
   R = T->invgamma_b[r]; G = T->invgamma_b[g]; B = T->invgamma_b[b];
 }
 
-// ---------------------------------------------------------------------------
-template <typename T>
-__global__ __launch_bounds__(256) void quant_lab_kernel(const T* __restrict__ img, const DevLab* __restrict__ tab,
-                                                        uint8_t* __restrict__ L, uint8_t* __restrict__ A,
-                                                        uint8_t* __restrict__ Bc, int B, int HW) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= B * HW) return;
-  const int b = idx / HW, p = idx - b * HW;
-  const T* base = img + (size_t)b * 3 * HW + p;
-  const int r = quant_u8(ldf(base, 0)), g = quant_u8(ldf(base, HW)), bl = quant_u8(ldf(base, 2 * HW));
-  int l, a, bb;
-  rgb2lab_u8(tab, r, g, bl, l, a, bb);
-  L[idx] = (uint8_t)l;
-  A[idx] = (uint8_t)a;
-  Bc[idx] = (uint8_t)bb;
-}
-
 // quantise only: NCHW float -> NCHW u8
 template <typename T>
 __global__ __launch_bounds__(256) void quant_kernel(const T* __restrict__ x, uint8_t* __restrict__ out, size_t n) {
@@ -121,113 +104,340 @@ __global__ __launch_bounds__(256) void quant_kernel(const T* __restrict__ x, uin
 }
 
 // ---------------------------------------------------------------------------
-// CLAHE LUT: one 256-thread block per (image, tile).  Tiles cover the image
-// extended by BORDER_REFLECT_101 to a multiple of the tile grid
-// (CLAHE_Impl::apply + CLAHE_CalcLut_Body, OpenCV imgproc/src/clahe.cpp).
+// CLAHE (cv2.createCLAHE(clip, (tilesX, tilesY)).apply; OpenCV
+// imgproc/src/clahe.cpp CLAHE_CalcLut_Body / CLAHE_Interpolation_Body), on the
+// L plane of the 8-bit Lab image (adaptive_params.py:142-161) or on a u8 plane.
+// The tiles cover the image extended by BORDER_REFLECT_101 to a multiple of
+// the tile grid (at most tiles - 1 extra rows / columns: one reflection).
+//
+//   clahe_hist   one block per (image, tile, row band s of S): quantise + 8-bit
+//                Lab of the band's pixels (SRC 0) or the u8 plane (SRC 1); the L
+//                / A / B planes are written (SRC 0); every wave counts into its
+//                own 256-bin LDS histogram, the 4 copies are summed per bin ->
+//                the band's partial histogram (S > 1) or, S == 1, the tile's
+//                LUT in the same block
+//   clahe_lut    (S > 1) the S partials of a tile summed per bin -> LUT
+//   clahe_apply  one block per (image, band of R3 <= tileH rows): the LUT rows
+//                the band reads (<= 3 tile rows) and the Lab tables staged in
+//                LDS, bilinear LUT blend, Lab -> sRGB 8-bit, /255 (DST 0) or
+//                the u8 plane (DST 1)
+// Threads walk their (row, column group) items with constant increments: no
+// per-pixel division, no reflect loop; V = 4 pixels per item when the rows
+// are whole groups of 4 and the tiles too (vector loads / stores).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ int reflect101(int i, int n) {
-  if (n == 1) return 0;
-  while (i < 0 || i >= n) i = i < 0 ? -i : 2 * (n - 1) - i;
-  return i;
+struct ClaheArgs {
+  int H, W, tilesX, tilesY, tileW, tileH;
+  int S, R;      // hist: row bands per tile, rows per band (tileH = S * R)
+  int R3;        // apply: rows per block (<= tileH)
+  int clip;      // clip limit in counts (0: none)
+  float lutScale;
+};
+
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
 }
 
-__global__ __launch_bounds__(256) void clahe_lut_kernel(const uint8_t* __restrict__ L, uint8_t* __restrict__ lut,
-                                                        int H, int W, int tilesX, int tilesY, int tileW, int tileH,
-                                                        int clipLimit, float lutScale) {
-  const int tile = blockIdx.x;
-  const int b = blockIdx.y;
-  const int tx = tile % tilesX, ty = tile / tilesX;
-  __shared__ int hist[256];
-  __shared__ int red[256];
-  const int t = threadIdx.x;
-  hist[t] = 0;
-  __syncthreads();
-  const uint8_t* img = L + (size_t)b * H * W;
-  const int n = tileW * tileH;
-  for (int i = t; i < n; i += 256) {
-    const int yy = reflect101(ty * tileH + i / tileW, H);
-    const int xx = reflect101(tx * tileW + i % tileW, W);
-    atomicAdd(&hist[img[(size_t)yy * W + xx]], 1);
-  }
-  __syncthreads();
-  int h = hist[t];
-  if (clipLimit > 0) {
-    const int ex = h > clipLimit ? h - clipLimit : 0;
-    h = h > clipLimit ? clipLimit : h;
-    red[t] = ex;
+// clip + redistribute + inclusive CDF -> LUT byte of bin t (256 threads, one bin each)
+__device__ __forceinline__ uint8_t clahe_lut_bin(int h, int t, int clip, float lutScale, int* red) {
+  const int lane = t & 63, w = t >> 6;
+  if (clip > 0) {
+    const int ex = wave_sum_i(h > clip ? h - clip : 0);
+    h = h > clip ? clip : h;
+    if (lane == 0) red[w] = ex;
     __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-      if (t < s) red[t] += red[t + s];
-      __syncthreads();
-    }
-    const int clipped = red[0];
+    const int clipped = red[0] + red[1] + red[2] + red[3];
     const int redistBatch = clipped / 256;
     const int residual = clipped - redistBatch * 256;
     h += redistBatch;
     if (residual != 0) {
+      // bins 0, step, 2 step, ... take one each until residual runs out
       const int step = max(256 / residual, 1);
-      // bins 0, step, 2*step, ... take one each until residual runs out
       if (t % step == 0 && t / step < residual) h += 1;
     }
     __syncthreads();
   }
-  // inclusive prefix sum (Hillis-Steele over 256 bins)
-  red[t] = h;
-  __syncthreads();
-  for (int off = 1; off < 256; off <<= 1) {
-    const int v = t >= off ? red[t - off] : 0;
-    __syncthreads();
-    red[t] += v;
-    __syncthreads();
+  // inclusive scan: within the wave, then the preceding waves' totals
+  int c = h;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(c, o, 64);
+    if (lane >= o) c += u;
   }
-  const float v = __fmul_rn((float)red[t], lutScale);
-  const int r = __float2int_rn(v);  // saturate_cast<uchar>(float): cvRound then clamp
-  lut[((size_t)b * tilesX * tilesY + tile) * 256 + t] = (uint8_t)(r < 0 ? 0 : (r > 255 ? 255 : r));
+  if (lane == 63) red[4 + w] = c;
+  __syncthreads();
+  for (int k = 0; k < w; ++k) c += red[4 + k];
+  const int r = __float2int_rn(__fmul_rn((float)c, lutScale));  // saturate_cast<uchar>(float)
+  return (uint8_t)(r < 0 ? 0 : (r > 255 ? 255 : r));
 }
 
-// CLAHE_Interpolation_Body + Lab -> sRGB 8-bit + /255
 template <typename T>
-__global__ __launch_bounds__(256) void clahe_lab2rgb_kernel(const uint8_t* __restrict__ L, const uint8_t* __restrict__ A,
-                                                            const uint8_t* __restrict__ Bc,
-                                                            const uint8_t* __restrict__ lut,
-                                                            const DevLab* __restrict__ tab, T* __restrict__ out,
-                                                            int B, int H, int W, int tilesX, int tilesY, int tileW,
-                                                            int tileH) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= B * H * W) return;
-  const int HW = H * W;
-  const int b = idx / HW, p = idx - b * HW;
-  const int y = p / W, x = p - y * W;
-  const float inv_tw = __fdiv_rn(1.0f, (float)tileW);
-  const float inv_th = __fdiv_rn(1.0f, (float)tileH);
-  const float txf = __fsub_rn(__fmul_rn((float)x, inv_tw), 0.5f);
-  int tx1 = (int)floorf(txf);
-  int tx2 = tx1 + 1;
-  const float xa = __fsub_rn(txf, (float)tx1), xa1 = __fsub_rn(1.0f, xa);
-  tx1 = max(tx1, 0);
-  tx2 = min(tx2, tilesX - 1);
-  const float tyf = __fsub_rn(__fmul_rn((float)y, inv_th), 0.5f);
-  int ty1 = (int)floorf(tyf);
-  int ty2 = ty1 + 1;
-  const float ya = __fsub_rn(tyf, (float)ty1), ya1 = __fsub_rn(1.0f, ya);
-  ty1 = max(ty1, 0);
-  ty2 = min(ty2, tilesY - 1);
-  const uint8_t* lb = lut + (size_t)b * tilesX * tilesY * 256;
-  const int v = L[idx];
-  const float l11 = lb[(ty1 * tilesX + tx1) * 256 + v], l12 = lb[(ty1 * tilesX + tx2) * 256 + v];
-  const float l21 = lb[(ty2 * tilesX + tx1) * 256 + v], l22 = lb[(ty2 * tilesX + tx2) * 256 + v];
-  // res = (l11*xa1 + l12*xa)*ya1 + (l21*xa1 + l22*xa)*ya, no contraction
-  const float top = __fadd_rn(__fmul_rn(l11, xa1), __fmul_rn(l12, xa));
-  const float bot = __fadd_rn(__fmul_rn(l21, xa1), __fmul_rn(l22, xa));
-  const float res = __fadd_rn(__fmul_rn(top, ya1), __fmul_rn(bot, ya));
-  int lc = __float2int_rn(res);
-  lc = lc < 0 ? 0 : (lc > 255 ? 255 : lc);
-  int R, G, Bo;
-  lab2rgb_u8(tab, lc, A[idx], Bc[idx], R, G, Bo);
-  T* o = out + (size_t)b * 3 * HW + p;
-  stf(o, 0, __fdiv_rn((float)R, 255.f));
-  stf(o, HW, __fdiv_rn((float)G, 255.f));
-  stf(o, 2 * (size_t)HW, __fdiv_rn((float)Bo, 255.f));
+struct Vec4 {};
+template <>
+struct Vec4<float> {
+  static __device__ __forceinline__ void load(const float* p, float (&v)[4]) {
+    const float4 q = *(const float4*)p;
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  }
+  static __device__ __forceinline__ void store(float* p, const float (&v)[4]) {
+    *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+  }
+};
+template <>
+struct Vec4<half_t> {
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+  static __device__ __forceinline__ void load(const half_t* p, float (&v)[4]) {
+    const h4 q = *(const h4*)p;
+    v[0] = (float)q[0]; v[1] = (float)q[1]; v[2] = (float)q[2]; v[3] = (float)q[3];
+  }
+  static __device__ __forceinline__ void store(half_t* p, const float (&v)[4]) {
+    h4 q;
+    q[0] = (half_t)v[0]; q[1] = (half_t)v[1]; q[2] = (half_t)v[2]; q[3] = (half_t)v[3];
+    *(h4*)p = q;
+  }
+};
+
+// RGB2Lab_b on LDS copies of the gamma / cube-root tables
+__device__ __forceinline__ void rgb2lab_lds(const uint16_t* gam, const uint16_t* cbrt, const int* c, int R8, int G8,
+                                            int B8, int& L, int& A, int& Bb) {
+  const int R = gam[R8], G = gam[G8], B = gam[B8];
+  const int fX = cbrt[descale(R * c[0] + G * c[1] + B * c[2], 12)];
+  const int fY = cbrt[descale(R * c[3] + G * c[4] + B * c[5], 12)];
+  const int fZ = cbrt[descale(R * c[6] + G * c[7] + B * c[8], 12)];
+  const int Lscale = (116 * 255 + 50) / 100;
+  const int Lshift = -((16 * 255 * (1 << 15) + 50) / 100);
+  L = sat_u8(descale(Lscale * fY + Lshift, 15));
+  A = sat_u8(descale(500 * (fX - fY) + 128 * (1 << 15), 15));
+  Bb = sat_u8(descale(200 * (fY - fZ) + 128 * (1 << 15), 15));
+}
+
+// Lab2RGBinteger on LDS copies of the Y / inverse-gamma tables
+__device__ __forceinline__ void lab2rgb_lds(const uint16_t* yf, const uint16_t* ig, const int* c, int L, int A, int Bb,
+                                            int& R, int& G, int& B) {
+  const int BASE = 1 << 14;
+  const int y = yf[L * 2], ify = yf[L * 2 + 1];
+  const int adiv = ((5 * A * 53687 + (1 << 7)) >> 13) - 128 * BASE / 500;
+  const int bdiv = ((Bb * 41943 + (1 << 4)) >> 9) - 128 * BASE / 200 + 1;
+  const int x = ab_to_xz(ify + adiv);
+  const int z = ab_to_xz(ify - bdiv);
+  int r = descale(c[0] * x + c[1] * y + c[2] * z, 14);
+  int g = descale(c[3] * x + c[4] * y + c[5] * z, 14);
+  int b = descale(c[6] * x + c[7] * y + c[8] * z, 14);
+  r = max(0, min(4095, r)); g = max(0, min(4095, g)); b = max(0, min(4095, b));
+  R = ig[r]; G = ig[g]; B = ig[b];
+}
+
+// SRC 0: T RGB planes [B,3,H,W] -> L / A / B planes; SRC 1: u8 plane [B,H,W] (src = L)
+template <int SRC, typename T, int V>
+__global__ __launch_bounds__(256) void clahe_hist_kernel(const void* __restrict__ src, uint8_t* __restrict__ Lp,
+                                                         uint8_t* __restrict__ Ap, uint8_t* __restrict__ Bp,
+                                                         int* __restrict__ part, uint8_t* __restrict__ lut,
+                                                         const DevLab* __restrict__ tab, ClaheArgs g) {
+  __shared__ int hist[4][256];
+  __shared__ uint16_t gam[SRC == 0 ? 256 : 1];
+  __shared__ uint16_t cbrt[SRC == 0 ? 3072 : 1];
+  __shared__ int red[8];
+  const int t = threadIdx.x, wave = t >> 6;
+  const int b = blockIdx.y;
+  const int s = blockIdx.x % g.S, tile = blockIdx.x / g.S;  // block-uniform
+  const int tx = tile % g.tilesX, ty = tile / g.tilesX;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) hist[k][t] = 0;
+  int c[9];
+  if constexpr (SRC == 0) {
+    for (int i = t; i < 256; i += 256) gam[i] = tab->gamma_b[i];
+    for (int i = t; i < 3072; i += 256) cbrt[i] = tab->cbrt_b[i];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) c[k] = tab->rgb2xyz[k];
+  }
+  __syncthreads();
+  const int H = g.H, W = g.W;
+  const size_t HW = (size_t)H * W;
+  const int y0 = ty * g.tileH + s * g.R, x0 = tx * g.tileW;
+  const int TWV = g.tileW / V;
+  // item cursor (row, column group), advanced by 256 items per iteration
+  int row = t / TWV, col = t - (t / TWV) * TWV;
+  const int inc_r = 256 / TWV, inc_c = 256 - inc_r * TWV;
+  int* hw = hist[wave];
+  for (; row < g.R; row += inc_r) {
+    const int y = y0 + row;
+    const int yr = y < H ? y : 2 * H - 2 - y;  // BORDER_REFLECT_101 (one reflection)
+    const int x = x0 + col * V;
+    if constexpr (V == 4) {
+      // whole groups inside the image (no column padding on this path)
+      const size_t o = (size_t)b * (SRC == 0 ? 3 : 1) * HW + (size_t)yr * W + x;
+      int Lv[4];
+      if constexpr (SRC == 0) {
+        const T* img = (const T*)src;
+        float r[4], gg[4], bl[4];
+        Vec4<T>::load(img + o, r);
+        Vec4<T>::load(img + o + HW, gg);
+        Vec4<T>::load(img + o + 2 * HW, bl);
+        int Av[4], Bv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) rgb2lab_lds(gam, cbrt, c, quant_u8(r[k]), quant_u8(gg[k]), quant_u8(bl[k]), Lv[k],
+                                                 Av[k], Bv[k]);
+        if (y < H) {
+          const size_t q = (size_t)b * HW + (size_t)y * W + x;
+          *(uchar4*)(Lp + q) = make_uchar4(Lv[0], Lv[1], Lv[2], Lv[3]);
+          *(uchar4*)(Ap + q) = make_uchar4(Av[0], Av[1], Av[2], Av[3]);
+          *(uchar4*)(Bp + q) = make_uchar4(Bv[0], Bv[1], Bv[2], Bv[3]);
+        }
+      } else {
+        const uchar4 q = *(const uchar4*)((const uint8_t*)src + o);
+        Lv[0] = q.x; Lv[1] = q.y; Lv[2] = q.z; Lv[3] = q.w;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) atomicAdd(&hw[Lv[k]], 1);
+    } else {
+      const int xr = x < W ? x : 2 * W - 2 - x;
+      const size_t o = (size_t)b * (SRC == 0 ? 3 : 1) * HW + (size_t)yr * W + xr;
+      int Lv;
+      if constexpr (SRC == 0) {
+        const T* img = (const T*)src;
+        int Av, Bv;
+        rgb2lab_lds(gam, cbrt, c, quant_u8(ldf(img, o)), quant_u8(ldf(img, o + HW)), quant_u8(ldf(img, o + 2 * HW)),
+                    Lv, Av, Bv);
+        if (y < H && x < W) {
+          const size_t q = (size_t)b * HW + (size_t)y * W + x;
+          Lp[q] = (uint8_t)Lv; Ap[q] = (uint8_t)Av; Bp[q] = (uint8_t)Bv;
+        }
+      } else {
+        Lv = ((const uint8_t*)src)[o];
+      }
+      atomicAdd(&hw[Lv], 1);
+    }
+    col += inc_c;
+    if (col >= TWV) { col -= TWV; ++row; }
+  }
+  __syncthreads();
+  const int h = hist[0][t] + hist[1][t] + hist[2][t] + hist[3][t];
+  const size_t tb = (size_t)b * g.tilesX * g.tilesY + tile;
+  if (g.S > 1) {
+    part[(tb * g.S + s) * 256 + t] = h;
+    return;
+  }
+  lut[tb * 256 + t] = clahe_lut_bin(h, t, g.clip, g.lutScale, red);
+}
+
+// S > 1: one block per (image, tile)
+__global__ __launch_bounds__(256) void clahe_lut_kernel(const int* __restrict__ part, uint8_t* __restrict__ lut,
+                                                        ClaheArgs g) {
+  __shared__ int red[8];
+  const int t = threadIdx.x;
+  const size_t tb = (size_t)blockIdx.y * g.tilesX * g.tilesY + blockIdx.x;
+  int h = 0;
+  for (int s = 0; s < g.S; ++s) h += part[(tb * g.S + s) * 256 + t];
+  lut[tb * 256 + t] = clahe_lut_bin(h, t, g.clip, g.lutScale, red);
+}
+
+// DST 0: L / A / B planes -> T RGB planes (/255); DST 1: u8 plane (Lp) -> u8 plane (out)
+template <int DST, typename T, int V>
+__global__ __launch_bounds__(256) void clahe_apply_kernel(const uint8_t* __restrict__ Lp, const uint8_t* __restrict__ Ap,
+                                                          const uint8_t* __restrict__ Bp, const uint8_t* __restrict__ lut,
+                                                          const DevLab* __restrict__ tab, void* __restrict__ out,
+                                                          ClaheArgs g) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+  uint16_t* yf = (uint16_t*)sm;            // 512
+  uint16_t* ig = yf + 512;                 // 4096
+  uint8_t* lrows = (uint8_t*)(ig + 4096);  // <= 3 tile rows of LUTs
+  const int t = threadIdx.x;
+  const int b = blockIdx.y;
+  const int H = g.H, W = g.W;
+  const size_t HW = (size_t)H * W;
+  const int y0 = blockIdx.x * g.R3;
+  const int nrows = min(g.R3, H - y0);
+  const float inv_tw = __fdiv_rn(1.0f, (float)g.tileW);
+  const float inv_th = __fdiv_rn(1.0f, (float)g.tileH);
+  // tile rows the band reads: ty1 of its first row .. ty2 of its last row
+  const int ty_lo = max((int)floorf(__fsub_rn(__fmul_rn((float)y0, inv_th), 0.5f)), 0);
+  const int ty_hi = min((int)floorf(__fsub_rn(__fmul_rn((float)(y0 + nrows - 1), inv_th), 0.5f)) + 1, g.tilesY - 1);
+  const int lbytes = (ty_hi - ty_lo + 1) * g.tilesX * 256;
+  const uint8_t* lsrc = lut + ((size_t)b * g.tilesY + ty_lo) * g.tilesX * 256;
+  for (int i = t * 16; i < lbytes; i += 256 * 16) *(uint4*)(lrows + i) = *(const uint4*)(lsrc + i);
+  int c[9];
+  if constexpr (DST == 0) {
+    for (int i = t; i < 512; i += 256) yf[i] = tab->yf_b[i];
+    for (int i = t; i < 4096; i += 256) ig[i] = tab->invgamma_b[i];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) c[k] = tab->xyz2rgb[k];
+  }
+  __syncthreads();
+  const int WV = W / V;
+  int row = t / WV, col = t - (t / WV) * WV;
+  const int inc_r = 256 / WV, inc_c = 256 - inc_r * WV;
+  for (; row < nrows; row += inc_r) {
+    const int y = y0 + row;
+    const float tyf = __fsub_rn(__fmul_rn((float)y, inv_th), 0.5f);
+    int ty1 = (int)floorf(tyf);
+    int ty2 = ty1 + 1;
+    const float ya = __fsub_rn(tyf, (float)ty1), ya1 = __fsub_rn(1.0f, ya);
+    ty1 = max(ty1, 0) - ty_lo;
+    ty2 = min(ty2, g.tilesY - 1) - ty_lo;
+    const uint8_t* r1 = lrows + ty1 * g.tilesX * 256;
+    const uint8_t* r2 = lrows + ty2 * g.tilesX * 256;
+    const size_t q = (size_t)b * HW + (size_t)y * W + col * V;
+    int Lv[V], Av[V], Bv[V];
+    if constexpr (V == 4) {
+      const uchar4 l4 = *(const uchar4*)(Lp + q);
+      Lv[0] = l4.x; Lv[1] = l4.y; Lv[2] = l4.z; Lv[3] = l4.w;
+      if constexpr (DST == 0) {
+        const uchar4 a4 = *(const uchar4*)(Ap + q), b4 = *(const uchar4*)(Bp + q);
+        Av[0] = a4.x; Av[1] = a4.y; Av[2] = a4.z; Av[3] = a4.w;
+        Bv[0] = b4.x; Bv[1] = b4.y; Bv[2] = b4.z; Bv[3] = b4.w;
+      }
+    } else {
+      Lv[0] = Lp[q];
+      if constexpr (DST == 0) { Av[0] = Ap[q]; Bv[0] = Bp[q]; }
+    }
+    int lc[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const int x = col * V + k;
+      const float txf = __fsub_rn(__fmul_rn((float)x, inv_tw), 0.5f);
+      int tx1 = (int)floorf(txf);
+      int tx2 = tx1 + 1;
+      const float xa = __fsub_rn(txf, (float)tx1), xa1 = __fsub_rn(1.0f, xa);
+      tx1 = max(tx1, 0);
+      tx2 = min(tx2, g.tilesX - 1);
+      const int v = Lv[k];
+      const float l11 = r1[tx1 * 256 + v], l12 = r1[tx2 * 256 + v];
+      const float l21 = r2[tx1 * 256 + v], l22 = r2[tx2 * 256 + v];
+      // res = (l11*xa1 + l12*xa)*ya1 + (l21*xa1 + l22*xa)*ya, no contraction
+      const float top = __fadd_rn(__fmul_rn(l11, xa1), __fmul_rn(l12, xa));
+      const float bot = __fadd_rn(__fmul_rn(l21, xa1), __fmul_rn(l22, xa));
+      const int r = __float2int_rn(__fadd_rn(__fmul_rn(top, ya1), __fmul_rn(bot, ya)));
+      lc[k] = r < 0 ? 0 : (r > 255 ? 255 : r);
+    }
+    if constexpr (DST == 1) {
+      uint8_t* o = (uint8_t*)out + q;
+      if constexpr (V == 4) *(uchar4*)o = make_uchar4(lc[0], lc[1], lc[2], lc[3]);
+      else o[0] = (uint8_t)lc[0];
+    } else {
+      float R[V], G[V], Bo[V];
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        int r8, g8, b8;
+        lab2rgb_lds(yf, ig, c, lc[k], Av[k], Bv[k], r8, g8, b8);
+        R[k] = __fdiv_rn((float)r8, 255.f);
+        G[k] = __fdiv_rn((float)g8, 255.f);
+        Bo[k] = __fdiv_rn((float)b8, 255.f);
+      }
+      T* o = (T*)out + (size_t)b * 3 * HW + (size_t)y * W + col * V;
+      if constexpr (V == 4) {
+        Vec4<T>::store(o, R);
+        Vec4<T>::store(o + HW, G);
+        Vec4<T>::store(o + 2 * HW, Bo);
+      } else {
+        stf(o, 0, R[0]);
+        stf(o, HW, G[0]);
+        stf(o, 2 * HW, Bo[0]);
+      }
+    }
+    col += inc_c;
+    if (col >= WV) { col -= WV; ++row; }
+  }
 }
 
 // Lab <-> RGB standalone kernels (u8 HWC RGB <-> u8 HWC Lab), for API/tests
@@ -244,40 +454,6 @@ __global__ void lab2rgb_kernel(const uint8_t* __restrict__ lab, uint8_t* __restr
   int r, g, b;
   lab2rgb_u8(tab, lab[3 * i], lab[3 * i + 1], lab[3 * i + 2], r, g, b);
   rgb[3 * i] = r; rgb[3 * i + 1] = g; rgb[3 * i + 2] = b;
-}
-
-// CLAHE interpolation alone (u8 -> u8), for API/tests
-__global__ void clahe_apply_kernel(const uint8_t* __restrict__ L, const uint8_t* __restrict__ lut,
-                                   uint8_t* __restrict__ out, int B, int H, int W, int tilesX, int tilesY,
-                                   int tileW, int tileH) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= B * H * W) return;
-  const int HW = H * W;
-  const int b = idx / HW, p = idx - b * HW;
-  const int y = p / W, x = p - y * W;
-  const float inv_tw = __fdiv_rn(1.0f, (float)tileW);
-  const float inv_th = __fdiv_rn(1.0f, (float)tileH);
-  const float txf = __fsub_rn(__fmul_rn((float)x, inv_tw), 0.5f);
-  int tx1 = (int)floorf(txf);
-  int tx2 = tx1 + 1;
-  const float xa = __fsub_rn(txf, (float)tx1), xa1 = __fsub_rn(1.0f, xa);
-  tx1 = max(tx1, 0);
-  tx2 = min(tx2, tilesX - 1);
-  const float tyf = __fsub_rn(__fmul_rn((float)y, inv_th), 0.5f);
-  int ty1 = (int)floorf(tyf);
-  int ty2 = ty1 + 1;
-  const float ya = __fsub_rn(tyf, (float)ty1), ya1 = __fsub_rn(1.0f, ya);
-  ty1 = max(ty1, 0);
-  ty2 = min(ty2, tilesY - 1);
-  const uint8_t* lb = lut + (size_t)b * tilesX * tilesY * 256;
-  const int v = L[idx];
-  const float l11 = lb[(ty1 * tilesX + tx1) * 256 + v], l12 = lb[(ty1 * tilesX + tx2) * 256 + v];
-  const float l21 = lb[(ty2 * tilesX + tx1) * 256 + v], l22 = lb[(ty2 * tilesX + tx2) * 256 + v];
-  const float top = __fadd_rn(__fmul_rn(l11, xa1), __fmul_rn(l12, xa));
-  const float bot = __fadd_rn(__fmul_rn(l21, xa1), __fmul_rn(l22, xa));
-  const float res = __fadd_rn(__fmul_rn(top, ya1), __fmul_rn(bot, ya));
-  int lc = __float2int_rn(res);
-  out[idx] = (uint8_t)(lc < 0 ? 0 : (lc > 255 ? 255 : lc));
 }
 
 // ---------------------------------------------------------------------------
@@ -320,46 +496,81 @@ __device__ __forceinline__ float sample_s(const T* img, int H, int W, int hs, in
   return (1.f - ly) * ((1.f - lx) * v00 + lx * v01) + ly * ((1.f - lx) * v10 + lx * v11);
 }
 
+// One block per (image, 16 x 64 tile of the scaled image): the tile's
+// bilinear samples plus a 1-sample halo are computed ONCE into LDS (each is
+// read by up to 5 feature terms: value, +-x and +-y neighbours of the
+// gradient), then every pixel's 7 features are summed from LDS.  Block sums
+// go to the per-(image, scale) accumulator as 64-bit fixed point (2^-24):
+// integer atomics, so the total does not depend on block order.
+constexpr int MS_TH = 16, MS_TW = 64;
+constexpr double kMsFix = 16777216.0;  // 2^24
+
 template <typename T>
-__global__ __launch_bounds__(256) void ms_sums_kernel(const T* __restrict__ x, double* __restrict__ sums, int H, int W,
-                                                      int hs, int ws, int scale_idx) {
+__global__ __launch_bounds__(256) void ms_sums_kernel(const T* __restrict__ x, unsigned long long* __restrict__ acc,
+                                                      int H, int W, int hs, int ws, int scale_idx, int tiles_x) {
+  __shared__ float smp[3][MS_TH + 2][MS_TW + 2];
+  __shared__ double red[4];
+  const int t = threadIdx.x;
   const int b = blockIdx.y;
+  const int ty0 = (blockIdx.x / tiles_x) * MS_TH, tx0 = (blockIdx.x % tiles_x) * MS_TW;  // block-uniform
   const T* img = x + (size_t)b * 3 * H * W;
   const float sy = (float)H / (float)hs, sx = (float)W / (float)ws;
-  double acc = 0.0;
-  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < hs * ws; p += gridDim.x * blockDim.x) {
-    const int y = p / ws, xx = p - y * ws;
-    float c3[3];
-    float fsum = 0.f;
-    for (int c = 0; c < 3; ++c) {
-      const T* ch = img + (size_t)c * H * W;
-      const float v = sample_s(ch, H, W, hs, ws, sy, sx, y, xx);
-      c3[c] = v;
-      float gx, gy;
-      if (ws < 2) gx = 0.f;
-      else if (xx == 0) gx = sample_s(ch, H, W, hs, ws, sy, sx, y, 1) - v;
-      else if (xx == ws - 1) gx = v - sample_s(ch, H, W, hs, ws, sy, sx, y, ws - 2);
-      else gx = (sample_s(ch, H, W, hs, ws, sy, sx, y, xx + 1) - sample_s(ch, H, W, hs, ws, sy, sx, y, xx - 1)) / 2.f;
-      if (hs < 2) gy = 0.f;
-      else if (y == 0) gy = sample_s(ch, H, W, hs, ws, sy, sx, 1, xx) - v;
-      else if (y == hs - 1) gy = v - sample_s(ch, H, W, hs, ws, sy, sx, hs - 2, xx);
-      else gy = (sample_s(ch, H, W, hs, ws, sy, sx, y + 1, xx) - sample_s(ch, H, W, hs, ws, sy, sx, y - 1, xx)) / 2.f;
-      fsum += v + sqrtf(gx * gx + gy * gy);
+  constexpr int RW = MS_TW + 2, NS = (MS_TH + 2) * RW;
+  int r = t / RW, c = t - (t / RW) * RW;
+  constexpr int inc_r = 256 / RW, inc_c = 256 - inc_r * RW;
+  for (; r < MS_TH + 2; r += inc_r) {
+    const int ys = ty0 - 1 + r, xs = tx0 - 1 + c;
+    if ((unsigned)ys < (unsigned)hs && (unsigned)xs < (unsigned)ws) {
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) smp[ch][r][c] = sample_s(img + (size_t)ch * H * W, H, W, hs, ws, sy, sx, ys, xs);
     }
-    fsum += 0.299f * c3[0] + 0.587f * c3[1] + 0.114f * c3[2];
-    acc += (double)fsum;
+    c += inc_c;
+    if (c >= RW) { c -= RW; ++r; }
   }
-  // block reduce
-  __shared__ double red[256];
-  red[threadIdx.x] = acc;
+  (void)NS;
   __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-    __syncthreads();
+  // thread: row t / 16, pixels 4 (t % 16) .. + 3 of the tile
+  const int lr = t >> 4, lc0 = (t & 15) * 4;
+  const int y = ty0 + lr;
+  double a = 0.0;
+  if (y < hs) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int xx = tx0 + lc0 + k;
+      if (xx >= ws) break;
+      const int R = lr + 1, C = lc0 + k + 1;
+      float c3[3];
+      float fsum = 0.f;
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {
+        const float v = smp[ch][R][C];
+        c3[ch] = v;
+        float gx, gy;
+        if (ws < 2) gx = 0.f;
+        else if (xx == 0) gx = smp[ch][R][C + 1] - v;
+        else if (xx == ws - 1) gx = v - smp[ch][R][C - 1];
+        else gx = (smp[ch][R][C + 1] - smp[ch][R][C - 1]) / 2.f;
+        if (hs < 2) gy = 0.f;
+        else if (y == 0) gy = smp[ch][R + 1][C] - v;
+        else if (y == hs - 1) gy = v - smp[ch][R - 1][C];
+        else gy = (smp[ch][R + 1][C] - smp[ch][R - 1][C]) / 2.f;
+        fsum += v + sqrtf(gx * gx + gy * gy);
+      }
+      fsum += 0.299f * c3[0] + 0.587f * c3[1] + 0.114f * c3[2];
+      a += (double)fsum;
+    }
   }
-  if (threadIdx.x == 0) atomicAdd(&sums[b * 3 + scale_idx], red[0]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+  if ((t & 63) == 0) red[t >> 6] = a;
+  __syncthreads();
+  if (t == 0) {
+    const double blk = red[0] + red[1] + red[2] + red[3];
+    atomicAdd(&acc[b * 3 + scale_idx], (unsigned long long)(long long)llrint(blk * kMsFix));
+  }
 }
 
+// fixed-point accumulators -> fp64 sums (in place) and the factor
 // factor[b] = 1 + sum_i w_i * mean_i * 0.1, mean_i = float32(sums[b][i] / (7*h_i*w_i))
 // (torch.mean returns a float32 tensor; .item() widens it; Python accumulates in
 // double, multi_scale.py:310-314)
@@ -371,23 +582,35 @@ __device__ __forceinline__ double ms_factor(const double* sums, int b, double n0
   return f;
 }
 
-__global__ void ms_factor_kernel(const double* __restrict__ sums, double* __restrict__ factor, int B, double n0,
-                                 double n1, double n2) {
+__global__ void ms_factor_kernel(double* __restrict__ sums, double* __restrict__ factor, int B, double n0, double n1,
+                                 double n2) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b < B) factor[b] = ms_factor(sums, b, n0, n1, n2);
+  if (b >= B) return;
+  for (int i = 0; i < 3; ++i) {
+    const long long q = (long long)((const unsigned long long*)sums)[b * 3 + i];
+    sums[b * 3 + i] = (double)q / kMsFix;
+  }
+  if (factor) factor[b] = ms_factor(sums, b, n0, n1, n2);
 }
 
-// clamp(enh * float(factor), 0, 1)   (multi_scale.py:317-318)
-template <typename T>
+// clamp(enh * float(factor), 0, 1)   (multi_scale.py:317-318); grid (chunks, B)
+template <typename T, int V>
 __global__ __launch_bounds__(256) void scale_clamp_kernel(const T* __restrict__ enh, T* __restrict__ out,
-                                                          const double* __restrict__ sums, double n0, double n1,
-                                                          double n2, int CHW, int B) {
-  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (size_t)B * CHW) return;
-  const int b = (int)(idx / CHW);
-  const float f = (float)ms_factor(sums, b, n0, n1, n2);
-  const float v = __fmul_rn(ldf(enh, idx), f);
-  stf(out, idx, fminf(fmaxf(v, 0.f), 1.f));
+                                                          const double* __restrict__ factor, int CHW) {
+  const int b = blockIdx.y;
+  const float f = (float)factor[b];
+  const size_t base = (size_t)b * CHW;
+  for (int i = (blockIdx.x * 256 + threadIdx.x) * V; i < CHW; i += gridDim.x * 256 * V) {
+    if constexpr (V == 4) {
+      float v[4];
+      Vec4<T>::load(enh + base + i, v);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = fminf(fmaxf(__fmul_rn(v[k], f), 0.f), 1.f);
+      Vec4<T>::store(out + base + i, v);
+    } else {
+      stf(out, base + i, fminf(fmaxf(__fmul_rn(ldf(enh, base + i), f), 0.f), 1.f));
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -395,13 +618,10 @@ __global__ __launch_bounds__(256) void scale_clamp_kernel(const T* __restrict__ 
 // ---------------------------------------------------------------------------
 static inline int g1(size_t n) { return (int)((n + 255) / 256); }
 
-struct ClaheGeom {
-  int tilesX, tilesY, tileW, tileH, clip;
-  float lutScale;
-};
-static ClaheGeom clahe_geom(int H, int W, float clipLimit, int tilesX, int tilesY) {
-  ClaheGeom g;
-  g.tilesX = tilesX; g.tilesY = tilesY;
+// tile geometry of OpenCV's CLAHE_Impl::apply + the band split of the launches
+static ClaheArgs clahe_args(int B, int H, int W, float clipLimit, int tilesX, int tilesY, bool split) {
+  ClaheArgs g;
+  g.H = H; g.W = W; g.tilesX = tilesX; g.tilesY = tilesY;
   const int Hp = (H % tilesY) ? H + tilesY - (H % tilesY) : H;
   const int Wp = (W % tilesX) ? W + tilesX - (W % tilesX) : W;
   g.tileW = Wp / tilesX; g.tileH = Hp / tilesY;
@@ -412,49 +632,90 @@ static ClaheGeom clahe_geom(int H, int W, float clipLimit, int tilesX, int tiles
     g.clip = (int)(clipLimit * area / 256);
     if (g.clip < 1) g.clip = 1;
   }
+  // histogram blocks: (image, tile, band).  With few images, split each tile
+  // into S row bands (S | tileH) so the launch still fills the chip, keeping
+  // >= ~2048 pixels per block; S = 1 computes the LUT in the same block
+  g.S = 1;
+  if (split) {
+    const long long tiles = (long long)B * tilesX * tilesY;
+    for (int S = 2; S <= g.tileH; ++S) {
+      if (g.tileH % S) continue;
+      if (tiles * (g.S) >= 1024 || (long long)(g.tileH / S) * g.tileW < 2048) break;
+      g.S = S;
+    }
+  }
+  g.R = g.tileH / g.S;
+  // apply blocks: R3 rows (<= tileH: the band reads <= 3 tile rows of LUTs),
+  // ~1024 blocks per launch
+  long long r3 = ((long long)B * H + 1023) / 1024;
+  r3 = r3 < 1 ? 1 : (r3 > 32 ? 32 : r3);
+  g.R3 = (int)(r3 > g.tileH ? g.tileH : r3);
   return g;
+}
+
+static size_t clahe_apply_lds(const ClaheArgs& g) { return (512 + 4096) * 2 + (size_t)3 * g.tilesX * 256; }
+
+// the three launches; src: T RGB planes (SRC 0) or a u8 plane (SRC 1, then L = src)
+template <int SRC, typename T>
+static int clahe_launch(const void* src, void* out, uint8_t* L, uint8_t* A, uint8_t* Bc, uint8_t* lut, int* part,
+                        const DevLab* tab, int B, const ClaheArgs& g, hipStream_t st) {
+  if (g.tilesX > 64 || g.tilesY > 64) return kErrUnsupported;  // LDS of the apply kernel's LUT rows
+  // 4-pixel items: whole groups of 4 per tile row (no column padding) and per image row
+  const bool v4h = g.tileW % 4 == 0 && g.tileW * g.tilesX == g.W;
+  const bool v4a = g.W % 4 == 0;
+  const dim3 gh(g.tilesX * g.tilesY * g.S, B);
+  if (v4h)
+    hipLaunchKernelGGL((clahe_hist_kernel<SRC, T, 4>), gh, dim3(256), 0, st, src, L, A, Bc, part, lut, tab, g);
+  else
+    hipLaunchKernelGGL((clahe_hist_kernel<SRC, T, 1>), gh, dim3(256), 0, st, src, L, A, Bc, part, lut, tab, g);
+  UPR_CHECK_HIP(hipGetLastError());
+  if (g.S > 1) {
+    hipLaunchKernelGGL(clahe_lut_kernel, dim3(g.tilesX * g.tilesY, B), dim3(256), 0, st, (const int*)part, lut, g);
+    UPR_CHECK_HIP(hipGetLastError());
+  }
+  const dim3 ga((g.H + g.R3 - 1) / g.R3, B);
+  const size_t lds = clahe_apply_lds(g);
+  const uint8_t* Lsrc = SRC == 0 ? L : (const uint8_t*)src;
+  constexpr int DST = SRC;
+  if (v4a)
+    hipLaunchKernelGGL((clahe_apply_kernel<DST, T, 4>), ga, dim3(256), lds, st, Lsrc, A, Bc, lut, tab, out, g);
+  else
+    hipLaunchKernelGGL((clahe_apply_kernel<DST, T, 1>), ga, dim3(256), lds, st, Lsrc, A, Bc, lut, tab, out, g);
+  return (int)hipGetLastError();
+}
+
+static size_t clahe_part_bytes(const ClaheArgs& g, int B) {
+  return g.S > 1 ? (size_t)B * g.tilesX * g.tilesY * g.S * 256 * sizeof(int) : 0;
+}
+
+// workspace: L, A, B planes | LUTs | partial histograms (S > 1)
+size_t clahe_pipeline_ws(int B, int H, int W, int tilesX, int tilesY) {
+  const ClaheArgs g = clahe_args(B, H, W, 2.0f, tilesX, tilesY, true);
+  const size_t planes = ((size_t)B * H * W * 3 + 15) & ~(size_t)15;
+  const size_t luts = ((size_t)B * tilesX * tilesY * 256 + 15) & ~(size_t)15;
+  return planes + luts + clahe_part_bytes(g, B);
 }
 
 int launch_clahe_pipeline(const void* enh, void* out, uint8_t* ws, int B, int H, int W, float clip, int tilesX,
                           int tilesY, int dtype, hipStream_t st) {
   const DevLab* tab = dev_lab_tables(st);
   if (!tab) return kErrUnsupported;
+  const ClaheArgs g = clahe_args(B, H, W, clip, tilesX, tilesY, true);
   const size_t HW = (size_t)H * W;
   uint8_t* L = ws;
   uint8_t* A = L + B * HW;
   uint8_t* Bc = A + B * HW;
-  uint8_t* lut = Bc + B * HW;
-  const ClaheGeom g = clahe_geom(H, W, clip, tilesX, tilesY);
-  const int n = (int)(B * HW);
-  if (dtype == kF16)
-    hipLaunchKernelGGL((quant_lab_kernel<half_t>), dim3(g1(n)), dim3(256), 0, st, (const half_t*)enh, tab, L, A, Bc, B,
-                       (int)HW);
-  else
-    hipLaunchKernelGGL((quant_lab_kernel<float>), dim3(g1(n)), dim3(256), 0, st, (const float*)enh, tab, L, A, Bc, B,
-                       (int)HW);
-  hipLaunchKernelGGL(clahe_lut_kernel, dim3(tilesX * tilesY, B), dim3(256), 0, st, L, lut, H, W, tilesX, tilesY,
-                     g.tileW, g.tileH, g.clip, g.lutScale);
-  if (dtype == kF16)
-    hipLaunchKernelGGL((clahe_lab2rgb_kernel<half_t>), dim3(g1(n)), dim3(256), 0, st, L, A, Bc, lut, tab,
-                       (half_t*)out, B, H, W, tilesX, tilesY, g.tileW, g.tileH);
-  else
-    hipLaunchKernelGGL((clahe_lab2rgb_kernel<float>), dim3(g1(n)), dim3(256), 0, st, L, A, Bc, lut, tab,
-                       (float*)out, B, H, W, tilesX, tilesY, g.tileW, g.tileH);
-  return (int)hipGetLastError();
+  uint8_t* lut = ws + (((size_t)B * HW * 3 + 15) & ~(size_t)15);
+  int* part = (int*)(lut + (((size_t)B * tilesX * tilesY * 256 + 15) & ~(size_t)15));
+  if (dtype == kF16) return clahe_launch<0, half_t>(enh, out, L, A, Bc, lut, part, tab, B, g, st);
+  return clahe_launch<0, float>(enh, out, L, A, Bc, lut, part, tab, B, g, st);
 }
 
-size_t clahe_pipeline_ws(int B, int H, int W, int tilesX, int tilesY) {
-  return (size_t)B * H * W * 3 + (size_t)B * tilesX * tilesY * 256;
-}
-
+// u8 plane -> u8 plane (upr_clahe_u8: the caller's workspace holds the LUTs only, so S = 1)
 int launch_clahe_u8(const uint8_t* src, uint8_t* dst, uint8_t* lut, int B, int H, int W, float clip, int tilesX,
                     int tilesY, hipStream_t st) {
-  const ClaheGeom g = clahe_geom(H, W, clip, tilesX, tilesY);
-  hipLaunchKernelGGL(clahe_lut_kernel, dim3(tilesX * tilesY, B), dim3(256), 0, st, src, lut, H, W, tilesX, tilesY,
-                     g.tileW, g.tileH, g.clip, g.lutScale);
-  hipLaunchKernelGGL(clahe_apply_kernel, dim3(g1((size_t)B * H * W)), dim3(256), 0, st, src, lut, dst, B, H, W,
-                     tilesX, tilesY, g.tileW, g.tileH);
-  return (int)hipGetLastError();
+  const ClaheArgs g = clahe_args(B, H, W, clip, tilesX, tilesY, false);
+  return clahe_launch<1, float>(src, dst, nullptr, nullptr, nullptr, lut, nullptr, nullptr, B, g, st);
 }
 
 int launch_rgb2lab(const uint8_t* rgb, uint8_t* lab, size_t npix, hipStream_t st) {
@@ -497,26 +758,43 @@ int launch_multiscale(const void* x, const void* enh, void* out, double* sums, d
   const int wsz[3] = {W, (int)(W * 0.5), (int)(W * 0.25)};
   for (int s = 0; s < 3; ++s) {
     if (hs[s] < 1 || wsz[s] < 1) return kErrShape;
-    const int gx = min(g1((size_t)hs[s] * wsz[s]), 512);
+    const int tx = (wsz[s] + MS_TW - 1) / MS_TW, ty = (hs[s] + MS_TH - 1) / MS_TH;
+    unsigned long long* acc = (unsigned long long*)sums;
     if (dtype == kF16)
-      hipLaunchKernelGGL((ms_sums_kernel<half_t>), dim3(gx, B), dim3(256), 0, st, (const half_t*)x, sums, H, W, hs[s],
-                         wsz[s], s);
+      hipLaunchKernelGGL((ms_sums_kernel<half_t>), dim3(tx * ty, B), dim3(256), 0, st, (const half_t*)x, acc, H, W,
+                         hs[s], wsz[s], s, tx);
     else
-      hipLaunchKernelGGL((ms_sums_kernel<float>), dim3(gx, B), dim3(256), 0, st, (const float*)x, sums, H, W, hs[s],
-                         wsz[s], s);
+      hipLaunchKernelGGL((ms_sums_kernel<float>), dim3(tx * ty, B), dim3(256), 0, st, (const float*)x, acc, H, W,
+                         hs[s], wsz[s], s, tx);
   }
   const double n0 = 7.0 * hs[0] * wsz[0], n1 = 7.0 * hs[1] * wsz[1], n2 = 7.0 * hs[2] * wsz[2];
-  if (factor)
-    hipLaunchKernelGGL(ms_factor_kernel, dim3((B + 63) / 64), dim3(64), 0, st, (const double*)sums, factor, B, n0, n1,
-                       n2);
+  // the clamp needs the factor: use the caller's buffer, else a per-device scratch one
+  double* fac = factor;
+  if (!fac && enh && out) {
+    fac = (double*)scratch(kSlotTmp, sizeof(double) * B, st);
+    if (!fac) return (int)hipErrorOutOfMemory;
+  }
+  hipLaunchKernelGGL(ms_factor_kernel, dim3((B + 63) / 64), dim3(64), 0, st, sums, fac, B, n0, n1, n2);
   if (enh && out) {
-    const size_t n = (size_t)B * 3 * H * W;
-    if (dtype == kF16)
-      hipLaunchKernelGGL((scale_clamp_kernel<half_t>), dim3(g1(n)), dim3(256), 0, st, (const half_t*)enh,
-                         (half_t*)out, sums, n0, n1, n2, 3 * H * W, B);
-    else
-      hipLaunchKernelGGL((scale_clamp_kernel<float>), dim3(g1(n)), dim3(256), 0, st, (const float*)enh, (float*)out,
-                         sums, n0, n1, n2, 3 * H * W, B);
+    const int CHW = 3 * H * W;
+    const bool v4 = CHW % 4 == 0 && ((uintptr_t)enh | (uintptr_t)out) % (dtype == kF16 ? 8 : 16) == 0;
+    const int per = v4 ? 1024 : 256;
+    const int gx = min((CHW + per - 1) / per, 1024);
+    if (dtype == kF16) {
+      if (v4)
+        hipLaunchKernelGGL((scale_clamp_kernel<half_t, 4>), dim3(gx, B), dim3(256), 0, st, (const half_t*)enh,
+                           (half_t*)out, (const double*)fac, CHW);
+      else
+        hipLaunchKernelGGL((scale_clamp_kernel<half_t, 1>), dim3(gx, B), dim3(256), 0, st, (const half_t*)enh,
+                           (half_t*)out, (const double*)fac, CHW);
+    } else {
+      if (v4)
+        hipLaunchKernelGGL((scale_clamp_kernel<float, 4>), dim3(gx, B), dim3(256), 0, st, (const float*)enh,
+                           (float*)out, (const double*)fac, CHW);
+      else
+        hipLaunchKernelGGL((scale_clamp_kernel<float, 1>), dim3(gx, B), dim3(256), 0, st, (const float*)enh,
+                           (float*)out, (const double*)fac, CHW);
+    }
   }
   return (int)hipGetLastError();
 }

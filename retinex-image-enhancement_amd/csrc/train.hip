@@ -1783,11 +1783,12 @@ enum {
   LA_SM_H = 5, LA_SM_V = 6,
   LA_TV_H = 7, LA_TV_V = 8,
   LA_GLOW = 9,
-  LA_FIXED = 16,   // then per image: [sum illu, sum r_j (3), sum illu*r_j (3)]
+  LA_FIXED = 16,   // then per image LA_IMG: [sum illu_c (3), sum r_j (3), sum illu_c*r_j (3x3)]
+  LA_IMG = 16,     // (one illumination channel: c = 0 only)
 };
 
 struct LossWS {
-  double* acc;     // LA_FIXED + 7B
+  double* acc;     // LA_FIXED + LA_IMG * B
   double* patch;   // B * (H/ps) * (W/ps) sums of gray(enh) (ps = exposure patch size)
   double* rowsum;  // B*H   sum_{x<W-1} edge
   double* colsum;  // B*W   sum_{y<H-1} edge
@@ -1801,10 +1802,13 @@ struct LossWS {
   int dynamic;     // TotalLoss use_dynamic_smooth_weight
 };
 
+// finalised scalars: 64 + per image LS_IMG
+static size_t loss_scal_bytes(int B) { return align_up(sizeof(float) * (64 + 16 * B), 256); }
+
 static LossWS loss_ws(void* ws, int B, int H, int W, int ps) {
   LossWS l;
   char* p = (char*)ws;
-  l.acc = (double*)p; p += align_up(sizeof(double) * (LA_FIXED + 7 * B), 256);
+  l.acc = (double*)p; p += align_up(sizeof(double) * (LA_FIXED + LA_IMG * B), 256);
   l.patch = (double*)p; p += align_up(sizeof(double) * B * (H / ps) * (W / ps), 256);
   l.rowsum = (double*)p; p += align_up(sizeof(double) * B * H, 256);
   l.colsum = (double*)p; p += align_up(sizeof(double) * B * W, 256);
@@ -1813,13 +1817,16 @@ static LossWS loss_ws(void* ws, int B, int H, int W, int ps) {
   return l;
 }
 static size_t loss_ws_bytes(int B, int H, int W, int ps) {
-  return align_up(sizeof(double) * (LA_FIXED + 7 * B), 256) + align_up(sizeof(double) * B * (H / ps) * (W / ps), 256) +
-         align_up(sizeof(double) * B * H, 256) + align_up(sizeof(double) * B * W, 256) +
-         align_up(sizeof(double) * 2 * B, 256) + align_up(sizeof(float) * (64 + 8 * B), 256);
+  return align_up(sizeof(double) * (LA_FIXED + LA_IMG * B), 256) +
+         align_up(sizeof(double) * B * (H / ps) * (W / ps), 256) + align_up(sizeof(double) * B * H, 256) +
+         align_up(sizeof(double) * B * W, 256) + align_up(sizeof(double) * 2 * B, 256) + loss_scal_bytes(B);
 }
 
 // scalar slots
-enum { LS_T = 0, LS_NPATCH = 1, LS_WS = 2, LS_MU = 3 /*3*/, LS_NH = 6, LS_NV = 7, LS_DEC = 8 /* per image 5 */ };
+// per image LS_IMG: covariance [c][j] (9; one illumination channel: [j] = row 0),
+// mean differences (3 at +9; one channel: +9 = mean I - mean of the R means),
+// illumination means (3 at +12)
+enum { LS_T = 0, LS_NPATCH = 1, LS_WS = 2, LS_MU = 3 /*3*/, LS_NH = 6, LS_NV = 7, LS_DEC = 8, LS_IMG = 16 };
 
 __device__ __forceinline__ float gray_at(const float* img, size_t base, int HW, int p) {
   return (img[base + p] + img[base + HW + p] + img[base + 2 * HW + p]) / 3.f;
@@ -1864,18 +1871,20 @@ __device__ __forceinline__ void block_sum_atomic(double (&v)[NV], double* dst[NV
   __syncthreads();
 }
 
-// pass 1: grid (chunks, B)
+// pass 1: grid (chunks, B); CI = illumination channels (1 or 3)
+template <int CI>
 __global__ __launch_bounds__(256) void loss_pass1_kernel(const float* __restrict__ low, const float* __restrict__ enh,
                                                          const float* __restrict__ illu,
                                                          const float* __restrict__ refl, int H, int W, LossWS ws) {
+  constexpr int NV = 10 + CI + 3 + 3 * CI;  // fixed sums, then sum I_c, sum R_j, sum I_c R_j
   const int b = blockIdx.y;
   const int HW = H * W;
   const size_t base = (size_t)b * 3 * HW;
   const int per = (HW + gridDim.x - 1) / gridDim.x;
   const int p0 = blockIdx.x * per, p1 = min(HW, p0 + per);
-  double v[17];
+  double v[NV];
 #pragma unroll
-  for (int k = 0; k < 17; ++k) v[k] = 0.0;
+  for (int k = 0; k < NV; ++k) v[k] = 0.0;
   const int ps = ws.ps, PH = H / ps, PW = W / ps;
   for (int q = p0 + threadIdx.x; q < p1; q += 256) {
     const int y = q / W, x = q - y * W;
@@ -1897,12 +1906,18 @@ __global__ __launch_bounds__(256) void loss_pass1_kernel(const float* __restrict
         v[8] += fabsf(dl);
       }
     }
-    const float il = illu[(size_t)b * HW + q];
-    v[10] += il;
-    for (int c = 0; c < 3; ++c) {
-      const float r = refl[base + c * HW + q];
-      v[11 + c] += r;
-      v[14 + c] += (double)il * r;
+    float il[CI];
+#pragma unroll
+    for (int c = 0; c < CI; ++c) {
+      il[c] = illu[((size_t)b * CI + c) * HW + q];
+      v[10 + c] += il[c];
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const float r = refl[base + j * HW + q];
+      v[10 + CI + j] += r;
+#pragma unroll
+      for (int c = 0; c < CI; ++c) v[13 + CI + c * 3 + j] += (double)il[c] * r;
     }
     // exposure patches, edge row / column sums (per-pixel atomics on small arrays)
     const float ge = (le[0] + le[1] + le[2]) / 3.f;
@@ -1912,14 +1927,18 @@ __global__ __launch_bounds__(256) void loss_pass1_kernel(const float* __restrict
     if (x < W - 1) atomicAdd(ws.rowsum + (size_t)b * H + y, (double)ed);
     if (y < H - 1) atomicAdd(ws.colsum + (size_t)b * W + x, (double)ed);
   }
-  double* dst[17];
+  double* dst[NV];
   for (int k = 0; k < 10; ++k) dst[k] = ws.acc + k;
-  for (int k = 10; k < 17; ++k) dst[k] = nullptr;
-  for (int k = 0; k < 7; ++k) dst[10 + k] = ws.acc + LA_FIXED + b * 7 + k;
-  block_sum_atomic<17>(v, dst);
+  double* img = ws.acc + LA_FIXED + b * LA_IMG;
+  for (int c = 0; c < CI; ++c) dst[10 + c] = img + c;
+  for (int j = 0; j < 3; ++j) dst[10 + CI + j] = img + 3 + j;
+  for (int k = 0; k < 3 * CI; ++k) dst[13 + CI + k] = img + 6 + k;
+  block_sum_atomic<NV>(v, dst);
 }
 
-// pass 2: edge-aware smoothness sums (needs the row / column edge means)
+// pass 2: edge-aware smoothness sums (needs the row / column edge means),
+// summed over the CI illumination planes (the finaliser divides by CI)
+template <int CI>
 __global__ __launch_bounds__(256) void loss_pass2_kernel(const float* __restrict__ low, const float* __restrict__ illu,
                                                          int H, int W, LossWS ws) {
   const int b = blockIdx.y;
@@ -1930,20 +1949,22 @@ __global__ __launch_bounds__(256) void loss_pass2_kernel(const float* __restrict
   double v[2] = {0.0, 0.0};
   for (int q = p0 + threadIdx.x; q < p1; q += 256) {
     const int y = q / W, x = q - y * W;
-    const float il = illu[(size_t)b * HW + q];
+    const float* ip = illu + (size_t)b * CI * HW + q;
     if (x < W - 1) {
       float s = 0.f;
       for (int c = 0; c < 3; ++c) s += fabsf(low[base + c * HW + q] - low[base + c * HW + q + 1]);
       const float wh = expf(-ws.lam_s * (s / 3.f));
       const float ef = 1.f + ws.alpha * (float)(ws.rowsum[(size_t)b * H + y] / (W - 1));
-      v[0] += wh * ef * fabsf(il - illu[(size_t)b * HW + q + 1]);
+#pragma unroll
+      for (int c = 0; c < CI; ++c) v[0] += wh * ef * fabsf(ip[c * HW] - ip[c * HW + 1]);
     }
     if (y < H - 1) {
       float s = 0.f;
       for (int c = 0; c < 3; ++c) s += fabsf(low[base + c * HW + q] - low[base + c * HW + q + W]);
       const float wv = expf(-ws.lam_s * (s / 3.f));
       const float ef = 1.f + ws.alpha * (float)(ws.colsum[(size_t)b * W + x] / (H - 1));
-      v[1] += wv * ef * fabsf(il - illu[(size_t)b * HW + q + W]);
+#pragma unroll
+      for (int c = 0; c < CI; ++c) v[1] += wv * ef * fabsf(ip[c * HW] - ip[c * HW + W]);
     }
   }
   double* dst[2] = {ws.acc + LA_SM_H, ws.acc + LA_SM_V};
@@ -2039,7 +2060,7 @@ __global__ void texture_final_kernel(const double* __restrict__ acc, int B, int 
 
 // finalise: one block
 __global__ void loss_final_kernel(int B, int H, int W, LossWS ws, float* __restrict__ terms, int texture,
-                                  float w_smooth) {
+                                  float w_smooth, int CI) {
   __shared__ double ex[256];
   const int HW = H * W;
   const double N = (double)B * HW;
@@ -2061,7 +2082,8 @@ __global__ void loss_final_kernel(int B, int H, int W, LossWS ws, float* __restr
   const double mu0 = ws.acc[0] / N, mu1 = ws.acc[1] / N, mu2 = ws.acc[2] / N;
   const double col = (mu0 - mu1) * (mu0 - mu1) + (mu0 - mu2) * (mu0 - mu2) + (mu1 - mu2) * (mu1 - mu2);
   const double spa = ws.acc[LA_SPA_H] / nh + ws.acc[LA_SPA_V] / nv;
-  const double smo = ws.acc[LA_SM_H] / nh1 + ws.acc[LA_SM_V] / nv1;
+  // smoothness: torch.mean over B x CI x H x (W-1) (loss.py:171-172)
+  const double smo = (ws.acc[LA_SM_H] / nh1 + ws.acc[LA_SM_V] / nv1) / CI;
   double tc = ws.acc[LA_TV_H] / nh + ws.acc[LA_TV_V] / nv;
   if (texture == 1) {
     tc = 0.0;
@@ -2075,18 +2097,38 @@ __global__ void loss_final_kernel(int B, int H, int W, LossWS ws, float* __restr
   }
   double frob = 0.0, md = 0.0;
   for (int b = 0; b < B; ++b) {
-    const double* a = ws.acc + LA_FIXED + b * 7;
-    const double im = a[0] / HW;
-    double rmm = 0.0;
-    for (int j = 0; j < 3; ++j) {
-      const double cov = (a[4 + j] - a[1 + j] * a[0] / HW) / (HW - 1);
-      frob += 3.0 * cov * cov;
-      ws.scal[LS_DEC + b * 5 + j] = (float)cov;
-      rmm += a[1 + j] / HW / 3.0;
+    const double* a = ws.acc + LA_FIXED + b * LA_IMG;  // [sI_c (3), sR_j (3), sIR_cj (9)]
+    float* sc = ws.scal + LS_DEC + b * LS_IMG;
+    if (CI == 1) {
+      // loss.py:308-312: illumination expanded to 3 rows, NOT centred; each
+      // row of the 3x3 covariance is the same cov_j -> Frobenius^2 = 3 sum_j cov_j^2;
+      // mean term: mse of the channel means' means (:326-329)
+      const double im = a[0] / HW;
+      double rmm = 0.0;
+      for (int j = 0; j < 3; ++j) {
+        const double cov = (a[6 + j] - a[3 + j] * a[0] / HW) / (HW - 1);
+        frob += 3.0 * cov * cov;
+        sc[j] = (float)cov;
+        rmm += a[3 + j] / HW / 3.0;
+      }
+      md += (im - rmm) * (im - rmm) / B;
+      sc[9] = (float)(im - rmm);
+      sc[12] = (float)im;
+    } else {
+      // loss.py:302-304: both centred, cov[c][j] over the 3x3 channel pairs;
+      // mean term: F.mse_loss of the [B,3,1] means (:323-324)
+      for (int c = 0; c < 3; ++c) {
+        for (int j = 0; j < 3; ++j) {
+          const double cov = (a[6 + c * 3 + j] - a[c] * a[3 + j] / HW) / (HW - 1);
+          frob += cov * cov;
+          sc[c * 3 + j] = (float)cov;
+        }
+        const double d = a[c] / HW - a[3 + c] / HW;
+        md += d * d / (3.0 * B);
+        sc[9 + c] = (float)d;
+        sc[12 + c] = (float)(a[c] / HW);
+      }
     }
-    md += (im - rmm) * (im - rmm) / B;
-    ws.scal[LS_DEC + b * 5 + 3] = (float)(im - rmm);
-    ws.scal[LS_DEC + b * 5 + 4] = (float)im;
   }
   const double dec = frob + (double)ws.lam_d * md;
   terms[0] = (float)(ex[0] / NP);
@@ -2104,6 +2146,7 @@ __global__ void loss_final_kernel(int B, int H, int W, LossWS ws, float* __restr
 }
 
 // gradient pass: one thread per pixel, overwrites g_enh / g_illu / g_refl
+template <int CI>
 __global__ __launch_bounds__(256) void loss_grad_kernel(const float* __restrict__ low, const float* __restrict__ enh,
                                                         const float* __restrict__ illu,
                                                         const float* __restrict__ refl, int B, int H, int W,
@@ -2145,10 +2188,7 @@ __global__ __launch_bounds__(256) void loss_grad_kernel(const float* __restrict_
       if (y > 0) g -= w_spa * 2.f * ((enh[k - W] - e0) - (low[k - W] - l0)) / nv;
       g_enh[k] = g;
     }
-    // smoothness on illumination (weight wsm)
-    const size_t ii = (size_t)b * HW + q;
-    const float il = illu[ii];
-    float gi = 0.f;
+    // smoothness on each illumination plane (weight wsm; mean over CI planes)
     auto sgn = [](float v) { return v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f); };
     auto wgt = [&](int qa, int qb) {
       float s = 0.f;
@@ -2156,26 +2196,56 @@ __global__ __launch_bounds__(256) void loss_grad_kernel(const float* __restrict_
       return expf(-ws.lam_s * (s / 3.f));
     };
     const float efh = 1.f + ws.alpha * (float)(ws.rowsum[(size_t)b * H + y] / (W - 1));
-    if (x < W - 1) gi += wgt(q, q + 1) * efh * sgn(il - illu[ii + 1]) / nh1;
-    if (x > 0) gi -= wgt(q - 1, q) * efh * sgn(illu[ii - 1] - il) / nh1;
     const float efv = 1.f + ws.alpha * (float)(ws.colsum[(size_t)b * W + x] / (H - 1));
-    if (y < H - 1) gi += wgt(q, q + W) * efv * sgn(il - illu[ii + W]) / nv1;
-    if (y > 0) gi -= wgt(q - W, q) * efv * sgn(illu[ii - W] - il) / nv1;
-    gi *= wsm;
-    // decoupling: 3*sum_j cov_j^2 + lam_d*(imean - rmean)^2 / B
-    const float* sc = ws.scal + LS_DEC + b * 5;
-    const float md = sc[3], imean = sc[4];
+    const float wr = x < W - 1 ? wgt(q, q + 1) * efh : 0.f, wl = x > 0 ? wgt(q - 1, q) * efh : 0.f;
+    const float wd = y < H - 1 ? wgt(q, q + W) * efv : 0.f, wu = y > 0 ? wgt(q - W, q) * efv : 0.f;
+    const float* sc = ws.scal + LS_DEC + b * LS_IMG;
+    const double* a = ws.acc + LA_FIXED + b * LA_IMG;
     const float inv = 1.f / (float)(HW - 1);
-    const double* a = ws.acc + LA_FIXED + b * 7;
-    float gd = 0.f;
+    float il[CI], r[3], rm[3];
+#pragma unroll
+    for (int c = 0; c < CI; ++c) il[c] = illu[((size_t)b * CI + c) * HW + q];
+#pragma unroll
     for (int j = 0; j < 3; ++j) {
-      const float rmj = (float)(a[1 + j] / HW);
-      const float r = refl[base + j * HW + q];
-      gd += 6.f * sc[j] * (r - rmj) * inv;
-      g_refl[base + j * HW + q] = w_dec * (6.f * sc[j] * (il - imean) * inv - ws.lam_d * 2.f * md / (B * 3.f * HW));
+      r[j] = refl[base + j * HW + q];
+      rm[j] = (float)(a[3 + j] / HW);
     }
-    gd += ws.lam_d * 2.f * md / ((float)B * HW);
-    g_illu[ii] = gi + w_dec * gd;
+#pragma unroll
+    for (int c = 0; c < CI; ++c) {
+      const size_t ii = ((size_t)b * CI + c) * HW + q;
+      float gi = 0.f;
+      if (x < W - 1) gi += wr * sgn(il[c] - illu[ii + 1]) / nh1;
+      if (x > 0) gi -= wl * sgn(illu[ii - 1] - il[c]) / nh1;
+      if (y < H - 1) gi += wd * sgn(il[c] - illu[ii + W]) / nv1;
+      if (y > 0) gi -= wu * sgn(illu[ii - W] - il[c]) / nv1;
+      gi *= wsm / CI;
+      float gd = 0.f;
+      if (CI == 1) {
+        // 3 * sum_j cov_j^2 (uncentred I) + lam_d (imean - mean_j rmean_j)^2 / B
+#pragma unroll
+        for (int j = 0; j < 3; ++j) gd += 6.f * sc[j] * (r[j] - rm[j]) * inv;
+        gd += ws.lam_d * 2.f * sc[9] / ((float)B * HW);
+      } else {
+        // sum_cj cov_cj^2 (centred) + lam_d sum_c (imean_c - rmean_c)^2 / (3B)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) gd += 2.f * sc[c * 3 + j] * (r[j] - rm[j]) * inv;
+        gd += ws.lam_d * 2.f * sc[9 + c] / (3.f * B * HW);
+      }
+      g_illu[ii] = gi + w_dec * gd;
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      float g;
+      if (CI == 1) {
+        g = 6.f * sc[j] * (il[0] - sc[12]) * inv - ws.lam_d * 2.f * sc[9] / (B * 3.f * HW);
+      } else {
+        g = 0.f;
+#pragma unroll
+        for (int c = 0; c < CI; ++c) g += 2.f * sc[c * 3 + j] * (il[c] - sc[12 + c]) * inv;
+        g -= ws.lam_d * 2.f * sc[9 + j] / (3.f * B * HW);
+      }
+      g_refl[base + j * HW + q] = w_dec * g;
+    }
   }
 }
 
@@ -3483,7 +3553,7 @@ int upr_t_retinex_bwd(const float* x, const float* illu, const float* e, const f
   LAUNCH_CHECK();
 }
 
-static const UprLossParams kLossDefaults = {16, 0.6f, 10.f, 1.f, 0.1f, 1.f, 0.5f, 1};
+static const UprLossParams kLossDefaults = {16, 0.6f, 10.f, 1.f, 0.1f, 1.f, 0.5f, 1, 1};
 
 size_t upr_t_loss_workspace(int B, int H, int W) { return upr_t_loss_workspace_p(B, H, W, 16); }
 
@@ -3508,8 +3578,10 @@ int upr_t_loss_pixel_p(const float* low, const float* enh, const float* illu, co
   if (texture != 0 && texture != 1) return UPR_ERR_ARG;
   if (prm->patch <= 0 || H < prm->patch || W < prm->patch || H < 2 || W < 2) return UPR_ERR_SHAPE;
   if (grads && (!g_enh || !g_illu || !g_refl)) return UPR_ERR_ARG;
+  const int CI = prm->illu_channels == 0 ? 1 : prm->illu_channels;
+  if (CI != 1 && CI != 3) return UPR_ERR_UNSUPPORTED;
   hipStream_t st = ST(stream);
-  const size_t zero_bytes = loss_ws_bytes(B, H, W, prm->patch) - align_up(sizeof(float) * (64 + 8 * B), 256);
+  const size_t zero_bytes = loss_ws_bytes(B, H, W, prm->patch) - loss_scal_bytes(B);
   UPR_CHECK_HIP(hipMemsetAsync(ws, 0, zero_bytes, st));
   LossWS l = loss_ws(ws, B, H, W, prm->patch);
   l.ps = prm->patch;
@@ -3520,9 +3592,15 @@ int upr_t_loss_pixel_p(const float* low, const float* enh, const float* illu, co
   l.dynamic = prm->dynamic_smooth ? 1 : 0;
   int chunks = (H * W) / 4096;
   chunks = chunks < 1 ? 1 : (chunks > 128 ? 128 : chunks);
-  hipLaunchKernelGGL(loss_pass1_kernel, dim3(chunks, B), dim3(256), 0, st, low, enh, illu, refl, H, W, l);
-  UPR_CHECK_HIP(hipGetLastError());
-  hipLaunchKernelGGL(loss_pass2_kernel, dim3(chunks, B), dim3(256), 0, st, low, illu, H, W, l);
+  if (CI == 1) {
+    hipLaunchKernelGGL(loss_pass1_kernel<1>, dim3(chunks, B), dim3(256), 0, st, low, enh, illu, refl, H, W, l);
+    UPR_CHECK_HIP(hipGetLastError());
+    hipLaunchKernelGGL(loss_pass2_kernel<1>, dim3(chunks, B), dim3(256), 0, st, low, illu, H, W, l);
+  } else {
+    hipLaunchKernelGGL(loss_pass1_kernel<3>, dim3(chunks, B), dim3(256), 0, st, low, enh, illu, refl, H, W, l);
+    UPR_CHECK_HIP(hipGetLastError());
+    hipLaunchKernelGGL(loss_pass2_kernel<3>, dim3(chunks, B), dim3(256), 0, st, low, illu, H, W, l);
+  }
   UPR_CHECK_HIP(hipGetLastError());
   if (texture == 1 && l.dynamic) {
     for (int mode = 0; mode < 2; ++mode) {
@@ -3530,11 +3608,15 @@ int upr_t_loss_pixel_p(const float* low, const float* enh, const float* illu, co
       UPR_CHECK_HIP(hipGetLastError());
     }
   }
-  hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(256), 0, st, B, H, W, l, terms, texture, w_smooth);
+  hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(256), 0, st, B, H, W, l, terms, texture, w_smooth, CI);
   UPR_CHECK_HIP(hipGetLastError());
   if (grads) {
-    hipLaunchKernelGGL(loss_grad_kernel, dim3(grid_for((long long)B * H * W)), dim3(256), 0, st, low, enh, illu, refl,
-                       B, H, W, l, g_enh, g_illu, g_refl, w_exp, w_col, w_spa, w_dec);
+    if (CI == 1)
+      hipLaunchKernelGGL(loss_grad_kernel<1>, dim3(grid_for((long long)B * H * W)), dim3(256), 0, st, low, enh, illu,
+                         refl, B, H, W, l, g_enh, g_illu, g_refl, w_exp, w_col, w_spa, w_dec);
+    else
+      hipLaunchKernelGGL(loss_grad_kernel<3>, dim3(grid_for((long long)B * H * W)), dim3(256), 0, st, low, enh, illu,
+                         refl, B, H, W, l, g_enh, g_illu, g_refl, w_exp, w_col, w_spa, w_dec);
   }
   LAUNCH_CHECK();
 }

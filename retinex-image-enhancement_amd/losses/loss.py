@@ -118,8 +118,10 @@ class EdgeAwareSmoothnessLoss(_Term):
         self._setup(smooth_lambda=float(lambda_val), smooth_alpha=float(alpha))
 
     def forward(self, illu_map, img_low):
-        if illu_map.dim() != 4 or illu_map.shape[1] != 1:
-            raise NotImplementedError("device smoothness loss: illumination [B,1,H,W] (the model's)")
+        # illu_map [B,1,H,W] (the model's) or [B,3,H,W] (the reference self-test's, loss.py:806-819):
+        # the mean runs over every illumination plane (:171-172)
+        if illu_map.dim() != 4 or illu_map.shape[1] not in (1, 3):
+            raise NotImplementedError("device smoothness loss: illumination [B,1,H,W] or [B,3,H,W]")
         return self._eval(img_low, img_low, illu_map, img_low)
 
 
@@ -151,8 +153,11 @@ class SpatialConsistencyLoss(_Term):
 
 
 class IlluminationReflectanceDecouplingLoss(_Term):
-    """L_decouple (reference :258-334), the model's case C_illu = 1, C_refl = 3:
-    ||cov||_F^2 + lambda x mse(mean I, mean R)."""
+    """L_decouple (reference :258-334): ||cov||_F^2 + lambda x mse(means), for the
+    model's C_illu = 1 (the expanded, uncentred illumination against the
+    centred reflectance, :308-312; channel-mean means, :326-329) and for
+    C_illu = C_refl = 3 (the centred 3x3 covariance, :302-304; per-channel
+    means, :323-324).  Other channel counts (:313-317) are refused."""
 
     _term = "decouple"
 
@@ -162,8 +167,9 @@ class IlluminationReflectanceDecouplingLoss(_Term):
         self._setup(decouple_lambda=float(lambda_val))
 
     def forward(self, illu_map, reflectance):
-        if illu_map.shape[1] != 1 or reflectance.shape[1] != 3:
-            raise NotImplementedError("device decoupling loss: illumination [B,1,H,W], reflectance [B,3,H,W]")
+        if illu_map.shape[1] not in (1, 3) or reflectance.shape[1] != 3:
+            raise NotImplementedError("device decoupling loss: illumination [B,1,H,W] or [B,3,H,W], "
+                                      "reflectance [B,3,H,W]")
         return self._eval(reflectance.detach(), reflectance, illu_map, reflectance)  # img_low: placeholder
 
 

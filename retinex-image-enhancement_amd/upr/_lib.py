@@ -96,7 +96,8 @@ class UprLossParams(ctypes.Structure):
     """include/upr_train.h UprLossParams: the loss modules' constructor arguments."""
     _fields_ = [("patch", ctypes.c_int), ("base_exposure", ctypes.c_float), ("smooth_lambda", ctypes.c_float),
                 ("smooth_alpha", ctypes.c_float), ("decouple_lambda", ctypes.c_float), ("freq_high", ctypes.c_float),
-                ("freq_low", ctypes.c_float), ("dynamic_smooth", ctypes.c_int)]
+                ("freq_low", ctypes.c_float), ("dynamic_smooth", ctypes.c_int),
+                ("illu_channels", ctypes.c_int)]
 
 
 class UprPackJob(ctypes.Structure):

@@ -167,22 +167,26 @@ class TotalLossEngine:
         self.vgg = VGGPerceptual(vgg_features) if vgg_features is not None else None
         self.features = vgg_features
 
-    def _cparams(self):
+    def _cparams(self, illu_channels=1):
         p = self.params
         return L.UprLossParams(int(p["patch"]), float(p["base_exposure"]), float(p["smooth_lambda"]),
                                float(p["smooth_alpha"]), float(p["decouple_lambda"]), float(p["freq_high"]),
-                               float(p["freq_low"]), int(bool(p["dynamic_smooth"])))
+                               float(p["freq_low"]), int(bool(p["dynamic_smooth"])), int(illu_channels))
 
     def __call__(self, low, enh, illu, refl, grads=True):
-        """All NCHW fp32 device tensors.  Returns (terms [9] device tensor in
+        """All NCHW fp32 device tensors; illu [B,1,H,W] (the model's) or
+        [B,3,H,W] (loss.py:806-844).  Returns (terms [9] device tensor in
         upr_t_loss_total order, (g_enh, g_illu, g_refl) or None)."""
         lib, st = L.lib(), _stream()
         B, C, H, W = enh.shape
         dev = enh.device
+        if illu.dim() != 4 or illu.shape[1] not in (1, 3) or illu.shape[0] != B or tuple(illu.shape[2:]) != (H, W):
+            raise NotImplementedError(f"loss: illumination [B,1,H,W] or [B,3,H,W] matching the images, got "
+                                      f"{tuple(illu.shape)}")
         w = self.w
         terms = torch.empty(9, dtype=torch.float32, device=dev)
         zero(terms)
-        prm = self._cparams()
+        prm = self._cparams(illu.shape[1])
         nws = lib.upr_t_loss_workspace_p(B, H, W, prm.patch)
         if nws == 0:
             raise ValueError(f"loss: a {H}x{W} image is smaller than the exposure patch ({prm.patch})")

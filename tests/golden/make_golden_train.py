@@ -7,6 +7,9 @@ models/model.py) and records, on seeded inputs:
   G6 g6_losses.npz      every loss term of losses/loss.py + TotalLoss on
                         B=2 64x64 random maps, plus calculate_texture_complexity
                         ('tv' and 'edge_density')
+  G6c3 g6_losses_c3.npz the reference self-test's shapes (loss.py:806-844):
+                        3-channel illumination, smoothness / decoupling /
+                        TotalLoss values and gradients
   G7 g7_train_step.npz  one train_one_epoch step body (trainers/train.py:63-103,
                         no AMP) of the plain model (seed 0) on x = rand(2,3,64,64)
                         (generator seed 2): loss dict, per-parameter gradient
@@ -111,6 +114,42 @@ def g6():
     np.savez_compressed(os.path.join(OUT, "g6_losses.npz"), **rec)
 
 
+def g6c3():
+    """The reference self-test's shapes (losses/loss.py:806-844): B=2, 64x64,
+    a 3-CHANNEL illumination [B,3,H,W] -> the C_illu == C_refl branches of the
+    smoothness (:148, :171-172) and decoupling (:302-304, :323-324) terms and
+    TotalLoss, with the gradients w.r.t. (enh, illu, refl)."""
+    gen = torch.Generator().manual_seed(16)
+    low = 0.4 * torch.rand(2, 3, 64, 64, generator=gen)
+    enh = torch.rand(2, 3, 64, 64, generator=gen)
+    illu = torch.rand(2, 3, 64, 64, generator=gen)
+    refl = torch.rand(2, 3, 64, 64, generator=gen)
+    rec = {"low": low.numpy(), "enh": enh.numpy(), "illu": illu.numpy(), "refl": refl.numpy()}
+    with torch.no_grad():
+        rec["smoothness"] = ref_loss.EdgeAwareSmoothnessLoss()(illu, low).numpy()
+        rec["decouple"] = ref_loss.IlluminationReflectanceDecouplingLoss()(illu, refl).numpy()
+    crit = ref_loss.TotalLoss(use_freq_loss=True, adaptive_weights=False, texture_method="tv")
+    e = enh.clone().requires_grad_(True)
+    i = illu.clone().requires_grad_(True)
+    r = refl.clone().requires_grad_(True)
+    t, d = crit(low, e, i, r)
+    t.backward()
+    rec["total"] = t.detach().numpy()
+    for k, v in d.items():
+        rec["dict_" + k] = np.float64(v)
+    rec.update(grad_enh=e.grad.numpy(), grad_illu=i.grad.numpy(), grad_refl=r.grad.numpy())
+    # the single terms' gradients w.r.t. the illumination (and reflectance)
+    i2 = illu.clone().requires_grad_(True)
+    ref_loss.EdgeAwareSmoothnessLoss()(i2, low).backward()
+    rec["grad_illu_smooth"] = i2.grad.numpy()
+    i3 = illu.clone().requires_grad_(True)
+    r3 = refl.clone().requires_grad_(True)
+    ref_loss.IlluminationReflectanceDecouplingLoss()(i3, r3).backward()
+    rec["grad_illu_decouple"] = i3.grad.numpy()
+    rec["grad_refl_decouple"] = r3.grad.numpy()
+    np.savez_compressed(os.path.join(OUT, "g6_losses_c3.npz"), **rec)
+
+
 def g7():
     torch.manual_seed(0)
     model = ref_model.UP_Retinex(use_preact=False, use_aspp=False)
@@ -151,6 +190,11 @@ def g7():
 
 if __name__ == "__main__":
     torch.set_num_threads(8)
-    g6()
-    g7()
-    print("wrote g6_losses.npz g7_train_step.npz")
+    only = sys.argv[1:]
+    if not only or "g6" in only:
+        g6()
+    if not only or "g6c3" in only:
+        g6c3()
+    if not only or "g7" in only:
+        g7()
+    print("wrote", " ".join(only) if only else "g6_losses.npz g6_losses_c3.npz g7_train_step.npz")

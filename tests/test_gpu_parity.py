@@ -271,6 +271,42 @@ def test_clahe_enhance_pipeline():
     assert torch.equal(out, ref), f"max|d| {maxdiff(out, ref)}"
 
 
+@pytest.mark.parametrize("B,H,W,dt", [
+    (1, 512, 512, torch.float32),   # one image: each tile split into 2 row bands (partial histograms + LUT pass)
+    (1, 1024, 768, torch.float16),  # 8 bands per tile, fp16 in / out
+    (3, 100, 75, torch.float32),    # reflect-padded rows and columns: the 1-pixel item path
+    (2, 256, 252, torch.float32),   # W % 8 != 0 (column padding), W % 4 == 0: 4-pixel apply, 1-pixel histogram
+    (1, 31, 45, torch.float16),
+])
+def test_clahe_enhance_shapes(B, H, W, dt):
+    """upr_clahe_enhance bit-exact to the OpenCV restatement (oracle/cv_u8.py)
+    on every launch form: row-band split histograms (few images), the
+    reflect-padded 1-pixel path, fp16 input and output."""
+    from upr import runtime
+    g = torch.Generator().manual_seed(H * 7 + W)
+    x = (torch.rand(B, 3, H, W, generator=g) * 0.7).to(dt)
+    out = runtime.clahe_enhance(x.to(DEV)).cpu()
+    ref = oenh.clahe_enhancement(x.float())
+    assert out.dtype == dt
+    assert torch.equal(out, ref.to(dt)), f"max|d| {maxdiff(out.float(), ref)}"
+
+
+def test_clahe_enhance_full_batch_bs32_512():
+    """The bench's enhance workload (bs 32, 512^2, fp32, one histogram block
+    per tile with the LUT in the same block): images 0 and 31 bit-exact to
+    the restatement, and the batch is per-image independent (image 31 alone
+    gives the same bytes)."""
+    from upr import runtime
+    x = torch.rand(32, 3, 512, 512, generator=torch.Generator().manual_seed(12)) * 0.8
+    xd = x.to(DEV)
+    out = runtime.clahe_enhance(xd)
+    for b in (0, 31):
+        ref = oenh.clahe_enhancement(x[b:b + 1])
+        assert torch.equal(out[b:b + 1].cpu(), ref), (b, maxdiff(out[b:b + 1].cpu(), ref))
+    alone = runtime.clahe_enhance(xd[31:32].contiguous())
+    assert torch.equal(alone, out[31:32])
+
+
 def test_gray_hist():
     from upr import runtime
     x = torch.rand(3, 3, 50, 70, generator=torch.Generator().manual_seed(11))

@@ -584,6 +584,42 @@ def test_loss_terms_and_grads(golden):
         _close(t.grad, torch.from_numpy(g[name]), 1e-4, name)
 
 
+def test_loss_three_channel_illumination(golden):
+    """The reference self-test (losses/loss.py:806-844): B=2, 64x64 and a
+    3-channel illumination map [B,3,H,W] through EdgeAwareSmoothnessLoss,
+    IlluminationReflectanceDecouplingLoss and TotalLoss on the device, vs the
+    reference's own values and gradients (G6c3) and the oracle."""
+    from losses.loss import EdgeAwareSmoothnessLoss, IlluminationReflectanceDecouplingLoss, TotalLoss
+    g = golden("g6_losses_c3.npz")
+    low, enh, illu, refl = (torch.from_numpy(g[k]).to(DEV) for k in ("low", "enh", "illu", "refl"))
+    assert illu.shape[1] == 3
+    i = illu.clone().requires_grad_(True)
+    s = EdgeAwareSmoothnessLoss().to(DEV)(i, low)
+    np.testing.assert_allclose(float(s), float(g["smoothness"]), rtol=1e-4)
+    s.backward()
+    torch.cuda.synchronize()
+    _close(i.grad, torch.from_numpy(g["grad_illu_smooth"]), 1e-4, "smooth grad_illu")
+    i = illu.clone().requires_grad_(True)
+    r = refl.clone().requires_grad_(True)
+    dl = IlluminationReflectanceDecouplingLoss().to(DEV)(i, r)
+    np.testing.assert_allclose(float(dl), float(g["decouple"]), rtol=1e-4)
+    dl.backward()
+    torch.cuda.synchronize()
+    _close(i.grad, torch.from_numpy(g["grad_illu_decouple"]), 1e-4, "decouple grad_illu")
+    _close(r.grad, torch.from_numpy(g["grad_refl_decouple"]), 1e-4, "decouple grad_refl")
+    crit = TotalLoss(use_freq_loss=True).to(DEV)
+    e, i, r = (t.clone().requires_grad_(True) for t in (enh, illu, refl))
+    total, d = crit(low, e, i, r)
+    for k in ("exposure", "smoothness", "color", "spatial", "decouple", "perceptual", "frequency", "total"):
+        np.testing.assert_allclose(d[k], float(g["dict_" + k]), rtol=1e-4, atol=1e-8, err_msg=k)
+    total.backward()
+    torch.cuda.synchronize()
+    for name, t in (("grad_enh", e), ("grad_illu", i), ("grad_refl", r)):
+        _close(t.grad, torch.from_numpy(g[name]), 1e-4, name)
+    with pytest.raises(NotImplementedError):
+        crit(low, enh, illu[:, :2].contiguous(), refl)
+
+
 @pytest.mark.parametrize("texture,w_smooth", [("edge_density", 1.0), ("edge_density", 2.0), ("tv", 0.5)])
 def test_loss_texture_methods_vs_oracle(golden, texture, w_smooth):
     """TotalLoss(texture_method, weight_smooth) on the G6 inputs: the dynamic
