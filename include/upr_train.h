@@ -89,7 +89,12 @@ int upr_t_conv_mfma(const float* x, int B, int H, int W, int Cin, int x_cs, int 
  * that bit y16 is scratch.  y16_cs: y16's channel stride (0 = compact: N, or
  * N / 4 for store 1), e.g. a channel slice of a concat's fp16 copy.
  * store | 4 (with | 2): y need not be written (every reader takes y16); the
- * fp32 store is skipped where the kernel allows it. */
+ * fp32 store is skipped where the kernel allows it.
+ * store | 8: the input gradient of a 1x1 stride-2 conv (model.py:119-122
+ * shortcut) without the zero-upsampled operand: x is dy at H x W, y (and res,
+ * which must be given: y accumulates) is the 2H x 2W gradient, and pixel
+ * (b, i, j) of the 1x1 stride-1 product is added at (b, 2i, 2j) only (the
+ * other pixels of y are untouched); kh = kw = 1, pad 0, no relu, store 0. */
 int upr_t_conv_mfma16(const float* x, int B, int H, int W, int Cin, int x_cs, int x_coff, const void* wp16,
                       const float* bias, int N, int kh, int kw, int stride, int pad, int dil, const float* res,
                       int res_cs, int relu, float* y, int y_cs, int y_coff, int store, void* x16, int x16_ready,

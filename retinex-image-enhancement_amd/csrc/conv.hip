@@ -358,15 +358,8 @@ static int launch_cfg(const ConvOp& op, hipStream_t stream) {
 }
 
 // fp16 with every segment a multiple of 64 channels: 64-deep K steps (half the
-// barriers and LDS round trips per MFMA; UPR_IGEMM_BK=32 forces the 32-deep
-// variant for A/B timing)
+// barriers and LDS round trips per MFMA)
 static bool k64_ok(const ConvOp& op) {
-  static int force32 = -1;
-  if (force32 < 0) {
-    const char* e = getenv("UPR_IGEMM_BK");
-    force32 = (e && strcmp(e, "32") == 0) ? 1 : 0;
-  }
-  if (force32) return false;
   for (int s = 0; s < op.nseg; ++s)
     if (op.seg[s].C % 64) return false;
   return true;
@@ -393,69 +386,55 @@ static int launch_t(const ConvOp& op, hipStream_t stream) {
 
 int launch_conv_halo(const ConvOp& op, int dtype, hipStream_t st);
 int launch_conv_wide(const ConvOp& op, hipStream_t st);
-int launch_conv_stream(const ConvOp& op, hipStream_t st);
 int launch_conv_ring(const ConvOp& op, hipStream_t st);
 int launch_conv_ring32(const ConvOp& op, hipStream_t st);
 int launch_conv_wide32(const ConvOp& op, hipStream_t st);
 int launch_conv_t2(const ConvOp& op, int dtype, hipStream_t st);
-
-// UPR_CONV_IMPL=generic forces the implicit-GEMM kernel everywhere (A/B tests);
-// default: halo-tiled kernel where the shape allows, implicit GEMM otherwise.
-static int conv_impl_mode() {
-  static int mode = -1;
-  if (mode < 0) {
-    const char* e = getenv("UPR_CONV_IMPL");
-    mode = (e && strcmp(e, "generic") == 0) ? 1 : 0;
-  }
-  return mode;
-}
+int launch_conv_pw(const ConvOp& op, hipStream_t st);
 
 int launch_preact_f16(const void* x, const float* sc, const float* sh, void* o, size_t npix, int C, hipStream_t st);
 
 int launch_conv_out32(const ConvOp& op, hipStream_t stream) {
   if (!op.out32 || op.out || op.out2 || op.pool || op.store == kStoreHeadIllu) return kErrArg;
   if (op.nseg < 1 || op.nseg > 4 || op.B <= 0 || op.Ho <= 0 || op.Wo <= 0) return kErrArg;
-  if (conv_impl_mode() != 0) return kErrUnsupported;
-  int rc = launch_conv_wide(op, stream);
+  // narrow 1x1 GEMMs stream (conv_pw.hip); the stride-2 scatter form exists only there
+  int rc = launch_conv_pw(op, stream);
+  if (rc != kErrUnsupported || op.out_s2) return rc;
+  rc = launch_conv_wide(op, stream);
   if (rc != kErrUnsupported) return rc;
   rc = launch_conv_ring(op, stream);
   if (rc != kErrUnsupported) return rc;
-  static const int halo32 = getenv("UPR_HALO_OUT32") ? atoi(getenv("UPR_HALO_OUT32")) : 1;
-  return halo32 ? launch_conv_halo(op, kF16, stream) : kErrUnsupported;
+  return launch_conv_halo(op, kF16, stream);
 }
 
 int launch_conv(const ConvOp& op, int dtype, hipStream_t stream) {
   if (op.nseg < 1 || op.nseg > 4 || op.B <= 0 || op.Ho <= 0 || op.Wo <= 0) return kErrArg;
-  if (op.out32) return kErrArg;  // launch_conv_out32
+  if (op.out32 || op.out_s2) return kErrArg;  // launch_conv_out32
   if (op.out2) {
     // fused second output: only the wide-tile and row-ring epilogues write it;
     // any other kernel runs the plain op and the PreAct pass separately
     if (dtype != kF16 || op.store != kStoreNHWC || op.out_coff || op.out_cs != op.N || op.out2_cs != op.N ||
         !op.pre2_scale || !op.pre2_shift)
       return kErrArg;
-    if (conv_impl_mode() == 0) {
-      int rc = launch_conv_wide(op, stream);
-      if (rc != kErrUnsupported) return rc;
-      rc = launch_conv_ring(op, stream);
-      if (rc != kErrUnsupported) return rc;
-    }
+    int rc = launch_conv_wide(op, stream);
+    if (rc != kErrUnsupported) return rc;
+    rc = launch_conv_ring(op, stream);
+    if (rc != kErrUnsupported) return rc;
     ConvOp c = op;
     c.out2 = nullptr;
-    const int rc = launch_conv(c, dtype, stream);
+    rc = launch_conv(c, dtype, stream);
     if (rc != kOk) return rc;
     return launch_preact_f16(op.out, op.pre2_scale, op.pre2_shift, op.out2, (size_t)op.B * op.Ho * op.Wo, op.N, stream);
   }
   for (int s = 0; s < op.nseg; ++s)
     if (op.seg[s].C % 32 || op.seg[s].src == nullptr) return kErrShape;
-  if (conv_impl_mode() == 0) {
+  {
     if (dtype == kF16) {
       int rc = launch_conv_t2(op, dtype, stream);
       if (rc != kErrUnsupported) return rc;
       rc = launch_conv_wide(op, stream);
       if (rc != kErrUnsupported) return rc;
       rc = launch_conv_ring(op, stream);
-      if (rc != kErrUnsupported) return rc;
-      rc = launch_conv_stream(op, stream);
       if (rc != kErrUnsupported) return rc;
     } else {
       // 32 -> 64 3x3 without a residual (EnhancedFAM branch34_conv1): the fp32

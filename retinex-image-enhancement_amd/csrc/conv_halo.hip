@@ -757,9 +757,6 @@ static int launch_halo_cfg(const ConvOp& op, const HaloSteps& hs, hipStream_t st
   int grid = 256 * per_cu;
   if (grid > ntiles) grid = ntiles;
   grid -= grid % (op.N / NB);  // a whole number of N slices per grid stride (resident weights)
-  if (getenv("UPR_HALO_DEBUG"))
-    fprintf(stderr, "[halo]   lds %d B (%s weights), %d blocks/CU, grid %d, tiles %d\n", lds,
-            res ? "resident" : "per-step", per_cu, grid, ntiles);
   HaloArgs args;
   args.op = op;
   args.hs = hs;
@@ -768,14 +765,7 @@ static int launch_halo_cfg(const ConvOp& op, const HaloSteps& hs, hipStream_t st
   args.tiles_y = tiles_y;
   args.ntiles = ntiles;
   args.region_bytes = region;
-  static int sched = -1;
-  if (sched < 0) {
-    const char* e = getenv("UPR_HALO_SCHED");
-    int f = 0, n = 0;
-    if (e) sscanf(e, "%d,%d", &f, &n);
-    sched = (f & 255) | (n << 8);
-  }
-  args.sched = sched;
+  args.sched = 0;
   hipLaunchKernelGGL((conv_halo_kernel<T, NB, TH, OCC, PROG>), dim3(grid), dim3(256), lds, st, args);
   return (int)hipGetLastError();
 }
@@ -866,11 +856,6 @@ static void halo_choice(int dtype, int prog, int store, int N, int& th, int& occ
     if (prog == kProgFam) { th = 8; occ = 1; }
   }
   if (prog == kProgS2) { th = 4; occ = 1; }
-  const char* e = getenv("UPR_HALO");
-  if (e && prog != kProgS2) {
-    int a = 0, b = 0;
-    if (sscanf(e, "%d,%d", &a, &b) == 2 && (a == 4 || a == 8) && b >= 1 && b <= 3) { th = a; occ = b; }
-  }
 }
 
 // Returns kErrUnsupported when the op is not a halo-kernel shape (caller falls back).
@@ -925,9 +910,6 @@ int launch_conv_halo(const ConvOp& op, int dtype, hipStream_t st) {
   const int prog = nph == 1 ? prog1(kinds[0]) : (nph == 2 ? prog2(kinds[0], kinds[1]) : prog3(kinds[0], kinds[1], kinds[2]));
   int th, occ;
   halo_choice(dtype, prog, op.store, op.N, th, occ);
-  if (getenv("UPR_HALO_DEBUG"))
-    fprintf(stderr, "[halo] prog %d (%d phases, %d steps) N=%d %dx%d th=%d occ=%d\n", prog, nph, hs.n, op.N, op.Ho,
-            op.Wo, th, occ);
   if (dtype == kF16) {
     if (op.N == 32) return launch_halo_nb<half_t, 32>(op, hs, prog, th, occ, st);
     if (op.N % 64 == 0) return launch_halo_nb<half_t, 64>(op, hs, prog, th, occ, st);

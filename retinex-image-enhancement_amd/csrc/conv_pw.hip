@@ -1,0 +1,184 @@
+// Streaming 1x1 convolution (fp16 operands, fp32 accumulate) for the narrow
+// GEMMs of the training step: K = Cin and N = Cout both in {32, 64, 96, 128}
+// at 256^2 / 512^2 -- the multi-scale head's fusion 96 -> 32 and the
+// EnhancedFAM fusion 128 -> 32 (models/model.py:49, :413-414) and their input
+// gradients 32 -> 96 / 32 -> 128, and the projecting shortcut's stride-2 input
+// gradient (model.py:119-122).  A 64-deep tile GEMM spends these in prologue /
+// epilogue (one or two K steps); here, as in conv_t2:
+//   * a wave keeps the whole filter (N/16 x K/32 fragments) and the bias in
+//     registers for the block's lifetime and walks 16-pixel groups;
+//   * the pixels are the B operand, read straight from HBM into registers
+//     (lane = pixel fr, channels 8 fg .. 8 fg + 7 of each 32-channel slice:
+//     16-byte loads) one group ahead of the MFMAs;
+//   * the MFMA operands are swapped (weights first), so a lane holds 4
+//     consecutive output channels of one pixel: the epilogue stores 16 bytes
+//     (fp32) / 8 bytes (fp16) per lane with no LDS staging.
+// Epilogues: the fp16 `out` (bias, ReLU) and the training step's fp32 family
+// (ConvOp::out32 / res32 / mask16 / out32_h16 / skip32: the fp16-rounded
+// result widened to fp32, plus the accumulated gradient, ReLU-masked).
+// out_s2: the 1x1 stride-2 input gradient -- input pixel (b, i, j) is written
+// to output pixel (b, 2i, 2j) of a 2H x 2W map; the other pixels are left as
+// they are (the caller accumulates into a gradient that already holds the
+// rest), so the zero-upsampled operand of the generic path is never built.
+// HBM-bound: (K * 2 + N * (4 + 2 [+ 4 residual])) bytes per pixel.
+#include <algorithm>
+
+#include "upr_common.h"
+
+namespace upr {
+
+typedef _Float16 pwh8 __attribute__((ext_vector_type(8)));
+typedef _Float16 pwh4 __attribute__((ext_vector_type(4)));
+typedef float pwf4 __attribute__((ext_vector_type(4)));
+
+template <int KC, int NC, bool OUT32, bool S2>
+__global__ __launch_bounds__(256, 2) void conv_pw_kernel(ConvOp op, int ngroups) {
+  constexpr int KS = KC / 32, NT = NC / 16;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int fr = lane & 15, fg = lane >> 4;
+  const ConvSeg& sg = op.seg[0];
+  const half_t* src = (const half_t*)sg.src + sg.coff;
+  const int cs = sg.cs;
+  const int Win = sg.Win, HWin = sg.Hin * sg.Win;
+
+  // filter fragment (nt, ks): lane (fr, fg) = W[nt*16 + fr][ks*32 + 8 fg .. +7]
+  pwh8 wf[NT][KS];
+  pwf4 bias[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      wf[nt][ks] = *(const pwh8*)((const half_t*)op.W + (size_t)(nt * 16 + fr) * op.Kpad + ks * 32 + fg * 8);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias[nt][r] = op.bias ? op.bias[nt * 16 + fg * 4 + r] : 0.f;
+  }
+  const int stride = gridDim.x * 4;
+  int g = blockIdx.x * 4 + wave;
+  auto load = [&](int gg, pwh8 (&x)[KS]) {
+    if (gg < ngroups) {
+      const half_t* p = src + ((size_t)gg * 16 + fr) * cs + fg * 8;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) x[ks] = *(const pwh8*)(p + ks * 32);
+    }
+  };
+  pwh8 x0[KS], x1[KS];
+  load(g, x0);
+  for (; g < ngroups; g += stride) {
+    load(g + stride, x1);
+    pwf4 acc[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[nt] = pwf4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[nt][ks], x0[ks], acc[nt], 0, 0, 0);
+    // output pixel of this lane
+    size_t m = (size_t)g * 16 + fr;
+    if constexpr (S2) {
+      // groups are whole 16-pixel runs of one input row (Win % 16 == 0)
+      const int q0 = g * 16;
+      const int b = q0 / HWin, rem = q0 - b * HWin, i = rem / Win, j = rem - i * Win + fr;
+      m = ((size_t)(b * 2 * sg.Hin + 2 * i) * (2 * Win)) + 2 * j;
+    }
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int n = nt * 16 + fg * 4;
+      pwh4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = acc[nt][r] + bias[nt][r];
+        if (op.relu) v = fmaxf(v, 0.f);
+        o[r] = (half_t)v;
+      }
+      if constexpr (OUT32) {
+        pwf4 t;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) t[r] = (float)o[r];
+        if (op.res32) t += *(const pwf4*)(op.res32 + m * op.res32_cs + n);
+        if (op.mask16) {
+          const pwh4 mk = *(const pwh4*)((const half_t*)op.mask16 + m * op.mask16_cs + n);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) t[r] = (float)mk[r] > 0.f ? t[r] : 0.f;
+        }
+        if (!op.skip32) *(pwf4*)(op.out32 + m * op.out32_cs + op.out32_coff + n) = t;
+        if (op.out32_h16)
+          *(pwh4*)((half_t*)op.out32_h16 + m * op.out32_h16_cs + n) =
+              pwh4{(half_t)t[0], (half_t)t[1], (half_t)t[2], (half_t)t[3]};
+      } else {
+        *(pwh4*)((half_t*)op.out + m * op.out_cs + op.out_coff + n) = o;
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) x0[ks] = x1[ks];
+  }
+}
+
+template <int KC, int NC, bool OUT32, bool S2>
+static int launch_pw(const ConvOp& op, hipStream_t st) {
+  static int occ = 0;
+  if (!occ) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)conv_pw_kernel<KC, NC, OUT32, S2>, 256, 0) !=
+            hipSuccess ||
+        occ < 1)
+      occ = 1;
+  }
+  int cus = 256;
+  {
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  }
+  const long long npix = (long long)op.B * op.seg[0].Hin * op.seg[0].Win;
+  const int ngroups = (int)(npix / 16);
+  int grid = std::min(cus * occ, (ngroups + 3) / 4);
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL((conv_pw_kernel<KC, NC, OUT32, S2>), dim3(grid), dim3(256), 0, st, op, ngroups);
+  return (int)hipGetLastError();
+}
+
+template <int KC, bool OUT32, bool S2>
+static int pw_n(const ConvOp& op, hipStream_t st) {
+  switch (op.N) {
+    case 32: return launch_pw<KC, 32, OUT32, S2>(op, st);
+    case 64: return launch_pw<KC, 64, OUT32, S2>(op, st);
+    case 96: return launch_pw<KC, 96, OUT32, S2>(op, st);
+    case 128: return launch_pw<KC, 128, OUT32, S2>(op, st);
+    default: return kErrUnsupported;
+  }
+}
+
+template <bool OUT32, bool S2>
+static int pw_k(const ConvOp& op, hipStream_t st) {
+  switch (op.seg[0].C) {
+    case 32: return pw_n<32, OUT32, S2>(op, st);
+    case 64: return pw_n<64, OUT32, S2>(op, st);
+    case 96: return pw_n<96, OUT32, S2>(op, st);
+    case 128: return pw_n<128, OUT32, S2>(op, st);
+    default: return kErrUnsupported;
+  }
+}
+
+// fp16 1x1 stride-1 convs of the shapes above; kErrUnsupported otherwise
+// (an out_s2 op must be taken here: no other kernel implements it)
+int launch_conv_pw(const ConvOp& op, hipStream_t st) {
+  if (op.nseg != 1 || op.store != kStoreNHWC) return kErrUnsupported;
+  const ConvSeg& s = op.seg[0];
+  if (s.kh != 1 || s.kw != 1 || s.stride != 1 || s.pad != 0 || s.pre != kPreNone || s.kbase != 0) return kErrUnsupported;
+  if (s.Hin != op.Ho || s.Win != op.Wo) return kErrUnsupported;
+  if (s.C > 128 || s.C % 32 || op.N > 128 || op.N % 32) return kErrUnsupported;
+  if (op.res1 || op.res2 || op.pool || op.img_bias || op.scale || op.out2) return kErrUnsupported;
+  if (s.cs % 8 || s.coff % 8 || (uintptr_t)s.src % 16 || op.Kpad % 8 || (uintptr_t)op.W % 16) return kErrUnsupported;
+  if (((long long)op.B * s.Hin * s.Win) % 16) return kErrUnsupported;
+  if (op.out_s2 && (s.Win % 16 || !op.out32)) return kErrUnsupported;
+  if (op.out32) {
+    if ((uintptr_t)op.out32 % 16 || op.out32_cs % 4 || op.out32_coff % 4) return kErrUnsupported;
+    if (op.res32 && ((uintptr_t)op.res32 % 16 || op.res32_cs % 4)) return kErrUnsupported;
+    if (op.mask16 && ((uintptr_t)op.mask16 % 8 || op.mask16_cs % 4)) return kErrUnsupported;
+    if (op.out32_h16 && ((uintptr_t)op.out32_h16 % 8 || op.out32_h16_cs % 4)) return kErrUnsupported;
+    return op.out_s2 ? pw_k<true, true>(op, st) : pw_k<true, false>(op, st);
+  }
+  if ((uintptr_t)op.out % 8 || op.out_cs % 4 || op.out_coff % 4) return kErrUnsupported;
+  return pw_k<false, false>(op, st);
+}
+
+}  // namespace upr

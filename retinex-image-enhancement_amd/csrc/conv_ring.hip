@@ -1135,12 +1135,6 @@ __global__ __launch_bounds__(256) void conv_ring32_kernel(RingArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// CU budget of the persistent ring grids launched by this host thread (0: all
-// CUs): the executor caps the multi-scale side stream's ring convs so that they
-// stream beside the IENet's kernels instead of claiming every CU (ring_set_cu_cap)
-static thread_local int t_ring_cu_cap = 0;
-void ring_set_cu_cap(int cus) { t_ring_cu_cap = cus; }
-
 static int ring_cus() {
   static int cus = 0;
   if (!cus) {
@@ -1149,7 +1143,6 @@ static int ring_cus() {
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
       cus = 256;
   }
-  if (t_ring_cu_cap > 0 && t_ring_cu_cap < cus) return std::max(8, t_ring_cu_cap / 8 * 8);
   return cus;
 }
 
@@ -1217,16 +1210,6 @@ static int launch_ring32_cfg(const ConvOp& op, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-// UPR_CONV_RING=0 disables this path (A/B timing against conv_stream / conv_halo)
-static bool ring_enabled() {
-  static int en = -1;
-  if (en < 0) {
-    const char* e = getenv("UPR_CONV_RING");
-    en = (e && strcmp(e, "0") == 0) ? 0 : 1;
-  }
-  return en == 1;
-}
-
 static bool ring_fam_program(const ConvOp& op) {
   if (op.nseg != 4 || op.N != 32 || op.store != kStoreNHWC || op.res1 || op.res2 || op.img_bias || op.scale) return false;
   if (op.Kpad != 640 || op.out_cs % 4 || op.out_coff % 4) return false;
@@ -1253,27 +1236,8 @@ static int ring_relu(const ConvOp& op, hipStream_t st) {
   return op.relu ? launch_ring_cfg<MODE, C, NB, FL | kRingRelu>(op, st) : launch_ring_cfg<MODE, C, NB, FL>(op, st);
 }
 
-// UPR_RING_WIDE=0 keeps the 32 -> 32 convs (and the head) on 32-pixel strips (A/B timing)
-static bool ring_wide() {
-  static const int v = [] {
-    const char* e = getenv("UPR_RING_WIDE");
-    return (e && atoi(e) == 0) ? 0 : 1;
-  }();
-  return v == 1;
-}
-
-// UPR_RING_OCC3=0 keeps the plain 32 -> 32 conv at two blocks per CU (A/B timing)
-static bool ring_occ3() {
-  static const int v = [] {
-    const char* e = getenv("UPR_RING_OCC3");
-    return (e && atoi(e) == 0) ? 0 : 1;
-  }();
-  return v == 1;
-}
-
 // fp16 only; kErrUnsupported for every op this kernel does not take
 int launch_conv_ring(const ConvOp& op, hipStream_t st) {
-  if (!ring_enabled()) return kErrUnsupported;
   if (op.Ho < 4 || op.Wo < 16) return kErrUnsupported;
   if (op.out2 && op.nseg != 2) return kErrUnsupported;  // fused PreAct output: enc1.conv2 program only
   if (op.out32) {
@@ -1290,7 +1254,7 @@ int launch_conv_ring(const ConvOp& op, hipStream_t st) {
     }
     if (s.stride != 1 || s.Hin != op.Ho || s.Win != op.Wo) return kErrUnsupported;
     if (s.C == 32 && op.N == 32)
-      return op.Wo >= 48 && ring_wide() ? ring_relu<kRingConv, 32, 32, kRingWide | kRingOut32>(op, st)
+      return op.Wo >= 48 ? ring_relu<kRingConv, 32, 32, kRingWide | kRingOut32>(op, st)
                                         : ring_relu<kRingConv, 32, 32, kRingOut32>(op, st);
     if (s.C == 32 && op.N == 64) return ring_relu<kRingConv, 32, 64, kRingOut32>(op, st);
     if (s.C == 64 && op.N == 64) return ring_relu<kRingConv, 64, 64, kRingOut32>(op, st);
@@ -1303,7 +1267,7 @@ int launch_conv_ring(const ConvOp& op, hipStream_t st) {
   if (op.store == kStoreHeadIllu) {
     if (op.nseg != 1 || s.stride != 1 || s.Hin != op.Ho || s.Win != op.Wo) return kErrUnsupported;
     if (op.N != 32 || s.C != 32 || op.res2 || op.illu_f16 || op.Wo % 8) return kErrUnsupported;
-    return ring_wide() ? launch_ring_cfg<kRingHead, 32, 32, kRingWide>(op, st) : launch_ring_cfg<kRingHead, 32, 32, 0>(op, st);
+    return launch_ring_cfg<kRingHead, 32, 32, kRingWide>(op, st);
   }
   if (op.store != kStoreNHWC || op.out_cs % 4 || op.out_coff % 4) return kErrUnsupported;
   if (op.res2 && op.res2_cs % 4) return kErrUnsupported;
@@ -1331,8 +1295,8 @@ int launch_conv_ring(const ConvOp& op, hipStream_t st) {
     // 64-pixel strips for the plain conv only: with the residual landing zone
     // (4 KB per wave) they measured slower (dec1.conv.3 0.301 -> 0.308 ms)
     if (res) return ring_relu<kRingConv, 32, 32, kRingRes>(op, st);
-    if (ring_wide() && op.Wo >= 48) return ring_relu<kRingConv, 32, 32, kRingWide>(op, st);
-    return ring_occ3() ? ring_relu<kRingConv, 32, 32, kRingOcc3>(op, st) : ring_relu<kRingConv, 32, 32, 0>(op, st);
+    if (op.Wo >= 48) return ring_relu<kRingConv, 32, 32, kRingWide>(op, st);
+    return ring_relu<kRingConv, 32, 32, kRingOcc3>(op, st);
   }
   // (64-pixel strips do not fit here: a 32 -> 64 filter in registers spills, the
   // 64 -> 64 ring + LDS filter needs 209 KB)
@@ -1350,7 +1314,6 @@ static int ring32_relu(const ConvOp& op, hipStream_t st) {
 // EnhancedFAM fusion's 3x3 parts (N 32: dilation 1 or 2, a pre-ReLU residual,
 // per-image pool sums); kErrUnsupported otherwise
 int launch_conv_ring32(const ConvOp& op, hipStream_t st) {
-  if (!ring_enabled()) return kErrUnsupported;
   if (op.Ho < 4 || op.Wo < 16) return kErrUnsupported;
   const ConvSeg& s = op.seg[0];
   if (op.nseg == 3) {

@@ -272,13 +272,8 @@ static int launch_t2(const ConvOp& op, hipStream_t st) {
 }
 
 // ConvT 2x2 ops these kernels take; kErrUnsupported otherwise.
-// UPR_CONVT_STREAM=0 leaves them on the tile kernels (A/B timing).
 int launch_conv_t2(const ConvOp& op, int dtype, hipStream_t st) {
-  static const int en = [] {
-    const char* e = getenv("UPR_CONVT_STREAM");
-    return (e && atoi(e) == 0) ? 0 : 1;
-  }();
-  if (!en || op.store != kStoreConvT2x2 || op.nseg != 1) return kErrUnsupported;
+  if (op.store != kStoreConvT2x2 || op.nseg != 1) return kErrUnsupported;
   if (op.res1 || op.res2 || op.pool || op.img_bias || op.scale || op.out2 || op.out32) return kErrUnsupported;
   const ConvSeg& s = op.seg[0];
   if (s.kh != 1 || s.kw != 1 || s.stride != 1 || s.pad != 0 || s.pre != kPreNone || s.kbase != 0) return kErrUnsupported;

@@ -77,6 +77,23 @@ __device__ __forceinline__ void glds16(const void* g, unsigned char* lds) {
   __builtin_amdgcn_global_load_lds(g, (lds_void_ptr)lds, 16, 0, 0);
 }
 
+// the same DMA as a buffer load: a wave-uniform base read into SGPRs
+// (readfirstlane) as a raw buffer descriptor + a per-lane 32-bit byte offset,
+// so no DMA needs a 64-bit per-lane address.  (With 64-bit VGPR addresses --
+// and even with global saddr + voffset, which hipcc widened back to 64-bit
+// offsets -- it precomputed every step's addresses of the unrolled hwide4
+// loop, spilled them, and each reload came with a vmcnt(0) wait that drained
+// the DMA pipeline.)  The range check is disabled (all-ones record count):
+// every offset is in bounds by construction.
+__device__ __forceinline__ void glds16_s(const void* ubase, unsigned voff, unsigned char* lds) {
+  const uint64_t b = (uint64_t)ubase;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  void* sb = (void*)(((uint64_t)hi << 32) | lo);
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(sb, 0, (int)0xffffffff, 0x00020000);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_ptr)lds, 16, voff, 0, 0, 0);
+}
+
 
 // (segment, tap, channel) cursor of the K loop with the current segment's
 // geometry held in registers: the per-step DMA issue needs no kernarg loads
@@ -759,7 +776,6 @@ __global__ __launch_bounds__(512, MINW) void conv_wide_kernel(ConvOp op) {
 //   the image row is zeroed after the read (top / bottom halo rows outside
 //   the image are DMA'd from the zero line).
 // ---------------------------------------------------------------------------
-static int env_int(const char* name, int dflt);
 constexpr unsigned long long kHaloSwz = 0x6644220066442200ull;  // T[p] = 0,0,2,2,4,4,6,6,0,0,2,2,4,4,6,6
 __device__ __forceinline__ int halo_swz(int p) { return (int)(kHaloSwz >> ((p & 15) * 4)) & 7; }
 
@@ -1201,15 +1217,12 @@ static int launch_hwide3_s(const ConvOp& op, hipStream_t st) {
   hipLaunchKernelGGL((conv_hwide3_kernel<BN, W, SCHED>), dim3(grid), dim3(512), HC::LDS, st, op);
   return (int)hipGetLastError();
 }
-// UPR_HW3_SCHED: 2 = one fragment read per two MFMAs, VALU between (default; measured
-// bneck 0.177 -> 0.172 ms, dec3 0.219 -> 0.214 on random operands), 0 = grouped
-// MFMA / fragment-read interleave, 1 = hipcc's own schedule (A/B timing)
+// schedule 2: one fragment read per two MFMAs, VALU between (measured bneck
+// 0.177 -> 0.172 ms, dec3 0.219 -> 0.214 against the grouped interleave and
+// hipcc's own schedule)
 template <int BN, int W>
 static int launch_hwide3(const ConvOp& op, hipStream_t st) {
-  static const int v = getenv("UPR_HW3_SCHED") ? atoi(getenv("UPR_HW3_SCHED")) : 2;
-  if (v == 1) return launch_hwide3_s<BN, W, 1>(op, st);
-  if (v == 2) return launch_hwide3_s<BN, W, 2>(op, st);
-  return launch_hwide3_s<BN, W, 0>(op, st);
+  return launch_hwide3_s<BN, W, 2>(op, st);
 }
 
 // ---------------------------------------------------------------------------
@@ -1234,6 +1247,10 @@ template <typename F, int... S>
 __device__ __forceinline__ void static_steps(F&& f, std::integer_sequence<int, S...>) {
   (f(std::integral_constant<int, S>{}), ...);
 }
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_steps(f, std::make_integer_sequence<int, N>{});
+}
 
 // zero source of the out-of-image halo rows: a lane reads at its lane offset
 // (< 8 pixels x 1024 channels x 2 B), so a 16 KiB zero block
@@ -1255,7 +1272,8 @@ __device__ __forceinline__ void hw4_res_load(const ConvOp& op, f16x8_w (&rv0)[WM
   for (int a = 0; a < WM; ++a) rv0[a] = *(const f16x8_w*)(rpf + (size_t)(mb + (a / FPR) * W + (a % FPR) * 16) * rcs + cb);
 }
 
-// ABL (timing ablations only, UPR_HW4_ABL; results are garbage): bit 0 drops
+// ABL (timing ablations only, compiled on request -- the dispatcher instantiates
+// ABL = 0; results are garbage; profiles/r3_hwide4_bneck_ablations*): bit 0 drops
 // the main loop's DMA (region rows + B stages), bit 1 its LDS fragment reads,
 // bit 2 the epilogue, bit 3 the MFMAs.  DS: operand-swapped MFMAs + the
 // direct-store epilogue above (hw4_ds_ok decides per op).
@@ -1315,7 +1333,7 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
     for (int k = 0; k < HC::RP; ++k) {
       const unsigned char* ub = in ? abase + (size_t)iy * row_bytes + (size_t)k * 64 * cs * 2 + cc * WBK * 2
                                    : (const unsigned char*)g_halo_zero;
-      glds16(ub + voff_a, dst + k * 8192);
+      glds16_s(ub, voff_a, dst + k * 8192);
     }
   };
   // region rows issued right before the reads of step (c, t): this chunk's
@@ -1351,7 +1369,7 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
       for (int pc = 0; pc < HC::RP; ++pc) {
         const unsigned char* ub = in ? abase + (size_t)iy * row_bytes + (size_t)pc * 64 * cs * 2 + cc * WBK * 2
                                      : (const unsigned char*)g_halo_zero;
-        glds16(ub + voff_a, dst + pc * 8192);
+        glds16_s(ub, voff_a, dst + pc * 8192);
       }
     }
   };
@@ -1385,9 +1403,9 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
 #pragma unroll
     for (int j = 0; j < HC::BJ; ++j) {
       if constexpr (DS)
-        glds16(bbase_ds + (size_t)kb * 2 + voff_ds[j], Bs + (wave * (BN / 8) + j * 8) * 128);
+        glds16_s(bbase_ds + (size_t)kb * 2, voff_ds[j], Bs + (wave * (BN / 8) + j * 8) * 128);
       else
-        glds16(bbase + ((size_t)j * 8 * op.Kpad + kb) * 2 + voff_b[j & 1], Bs + (wave * (BN / 8) + j * 8) * 128);
+        glds16_s(bbase + ((size_t)j * 8 * op.Kpad + kb) * 2, voff_b[j & 1], Bs + (wave * (BN / 8) + j * 8) * 128);
     }
   };
 
@@ -1432,54 +1450,62 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
   }
   bofs = HC::RING + (wn * WN * 16 + fr) * 128 + ((fg ^ rsw) * 16);
 
-  // fragments of step S, half KK
-  auto rd = [&](auto S_, auto KK_, f16x8_w (&af)[WM], f16x8_w (&bf)[WN]) {
+  // fragments of step S, half KK: B (all WN) and A row fragment a
+  auto rd_b = [&](auto S_, auto KK_, f16x8_w (&bf)[WN]) {
     constexpr int S = decltype(S_)::value, KK = decltype(KK_)::value;
-    constexpr int c = S / 9, t = S % 9, ty = t / 3, tx = t % 3, stg = S % NBS;
+    constexpr int stg = S % NBS;
+    const int bo = KK ? (bofs ^ 64) : bofs;
+#pragma unroll
+    for (int b = 0; b < WN; ++b) bf[b] = *(const f16x8_w*)(smem + bo + stg * HC::B_BYTES + b * 16 * 128);
+  };
+  auto rd_a = [&](auto S_, auto KK_, auto A_) -> f16x8_w {
+    constexpr int S = decltype(S_)::value, KK = decltype(KK_)::value, a = decltype(A_)::value;
+    constexpr int c = S / 9, t = S % 9, ty = t / 3, tx = t % 3;
     if constexpr (DL) {
       constexpr int h = (S / 3) & 1, dtx = S % 3;
-      const int bo = KK ? (bofs ^ 64) : bofs;
-#pragma unroll
-      for (int b = 0; b < WN; ++b)
-        bf[b] = *(const f16x8_w*)(smem + bo + stg * HC::B_BYTES + b * 16 * 128);
-#pragma unroll
-      for (int a = 0; a < WM; ++a) {
-        const int ao = KK ? (aofs_d[dtx][a % FPR] ^ 64) : aofs_d[dtx][a % FPR];
-        af[a] = *(const f16x8_w*)(smem + ao + (h * 4 + a / FPR) * HC::ROW);
-      }
-      return;
-    }
-    const int bo = KK ? (bofs ^ 64) : bofs, ao = KK ? (aofs[tx] ^ 64) : aofs[tx];
-    int aoe = ao;
-    if constexpr (tx == 0) aoe = KK ? (aofs_e[0] ^ 64) : aofs_e[0];
-    if constexpr (tx == 2) aoe = KK ? (aofs_e[1] ^ 64) : aofs_e[1];
-#pragma unroll
-    for (int b = 0; b < WN; ++b)
-      bf[b] = *(const f16x8_w*)(smem + bo + stg * HC::B_BYTES + b * 16 * 128);
-#pragma unroll
-    for (int a = 0; a < WM; ++a) {
-      const int rr = (6 * c + ty + a / FPR) & 7;  // compile-time
-      const bool edge = (tx == 0 && a % FPR == 0) || (tx == 2 && a % FPR == FPR - 1);
-      af[a] = *(const f16x8_w*)(smem + (edge ? aoe : ao) + rr * HC::ROW + (a % FPR) * 16 * 128);
+      const int ao = KK ? (aofs_d[dtx][a % FPR] ^ 64) : aofs_d[dtx][a % FPR];
+      return *(const f16x8_w*)(smem + ao + (h * 4 + a / FPR) * HC::ROW);
+    } else {
+      constexpr bool edge = (tx == 0 && a % FPR == 0) || (tx == 2 && a % FPR == FPR - 1);
+      constexpr int rr = (6 * c + ty + a / FPR) & 7;
+      constexpr int off = rr * HC::ROW + (a % FPR) * 16 * 128;
+      int ao;
+      if constexpr (edge && tx == 0) ao = KK ? (aofs_e[0] ^ 64) : aofs_e[0];
+      else if constexpr (edge) ao = KK ? (aofs_e[1] ^ 64) : aofs_e[1];
+      else ao = KK ? (aofs[tx] ^ 64) : aofs[tx];
+      // ds_read's immediate offset is 16 bits: a ring row at >= 64 KiB (W 128)
+      // needs a base of its own.  Formed here, per step, by an add the
+      // compiler may not hoist -- hoisted, one base per (row, tap column,
+      // half) stayed live across the unrolled loop and spilled.
+      if constexpr (off >= 65536) asm volatile("v_add_u32_e32 %0, %1, %0" : "+v"(ao) : "n"(off & ~0xffff));
+      return *(const f16x8_w*)(smem + ao + (off & 0xffff));
     }
   };
-  auto mm = [&](auto S_, f16x8_w (&af)[WM], const f16x8_w (&bf)[WN]) {
+  // one A row fragment against all WN B fragments
+  auto mm_row = [&](int a, const f16x8_w& af, const f16x8_w (&bf)[WN]) {
     if constexpr ((ABL & 8) != 0) return;
 #pragma unroll
-    for (int a = 0; a < WM; ++a) {
-#pragma unroll
-      for (int b = 0; b < WN; ++b) {
-        if constexpr (DS)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[b], af[a], acc[a][b], 0, 0, 0);
-        else
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a], bf[b], acc[a][b], 0, 0, 0);
-      }
+    for (int b = 0; b < WN; ++b) {
+      if constexpr (DS)
+        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[b], af, acc[a][b], 0, 0, 0);
+      else
+        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf[b], acc[a][b], 0, 0, 0);
     }
   };
-  // hipcc's own MFMA / fragment-read schedule: the sched_group_barrier
-  // interleave of hwide3 made the straight-line steps spill (118 VGPRs)
-  f16x8_w a0[WM], b0[WN], a1[WM], b1[WN];
+  // A fragments roll: each row fragment is replaced by the next half's as
+  // soon as its MFMAs are issued, so one A set (WM) and two B sets (2 WN) are
+  // live instead of two of each -- 32 VGPRs less, the difference between
+  // spilling (each reload drained the DMA queue with a vmcnt(0)) and not
+  f16x8_w af[WM], b0[WN], b1[WN];
   f16x8_w rv0[WM];  // DS: pair-0 residual rows (hw4_res_load)
+  // half KK of step S (af, bf) issued; af rolls to (S2, KK2)
+  auto mm_roll = [&](auto S2_, auto KK2_, const f16x8_w (&bf)[WN], bool roll) {
+    static_for<WM>([&](auto A_) {
+      constexpr int a = decltype(A_)::value;
+      mm_row(a, af[a], bf);
+      if (roll) af[a] = rd_a(S2_, KK2_, A_);
+    });
+  };
   static_assert(!DL || (DS && NBS == 3), "dilated form: direct-store epilogue, three B stages");
   if constexpr (DL) {
     region_dl(0);
@@ -1504,11 +1530,14 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
     issue_b(NBS - 1, (NBS - 1) / 9, (NBS - 1) % 9);  // B(NBS - 1)
     issue_rows(0, 0);
   }
-  rd(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, a0, b0);
-  if constexpr ((ABL & 2) != 0) rd(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{}, a1, b1);
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  rd_b(I0{}, I0{}, b0);
+  static_for<WM>([&](auto A_) { af[decltype(A_)::value] = rd_a(I0{}, I0{}, A_); });
   static_steps(
       [&](auto S_) {
         constexpr int S = decltype(S_)::value;
+        rd_b(S_, I1{}, b1);
         if constexpr (S + 1 < TOTAL) {
           constexpr int c = S / 9, t = S % 9;
           constexpr int n = S + 1, nc = n / 9, nt = n % 9;
@@ -1516,8 +1545,7 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
           constexpr int bstep = S + NBS;
           constexpr int bc = DL ? (bstep < TOTAL ? bstep / 3 : NREG - 1) : (bstep / 9 < NCH ? bstep / 9 : NCH - 1);
           constexpr int bt = DL ? (bstep < TOTAL ? bstep % 3 : 2) : (bstep / 9 < NCH ? bstep % 9 : 8);
-          if constexpr (!(ABL & 2)) rd(S_, std::integral_constant<int, 1>{}, a1, b1);
-          mm(S_, a0, b0);
+          mm_roll(S_, I1{}, b0, true);
           // RAW: B(S + 1) and the region rows step S + 1 reads have landed: in
           // flight may stay the previous iteration's region rows (issued two
           // steps ahead of their first reader) and, with three stages, its
@@ -1545,12 +1573,11 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
             }
           }
           if constexpr (DS && S == TOTAL - 2) hw4_res_load<WM, WN, HC::WAVES_M, W>(op, rv0, m0, n0, wm, wn, lane);
-          if constexpr (!(ABL & 2)) rd(std::integral_constant<int, n>{}, std::integral_constant<int, 0>{}, a0, b0);
-          mm(S_, a1, b1);
+          rd_b(std::integral_constant<int, n>{}, I0{}, b0);
+          mm_roll(std::integral_constant<int, n>{}, I0{}, b1, true);
         } else {
-          if constexpr (!(ABL & 2)) rd(S_, std::integral_constant<int, 1>{}, a1, b1);
-          mm(S_, a0, b0);
-          mm(S_, a1, b1);
+          mm_roll(S_, I1{}, b0, true);
+          mm_roll(S_, I1{}, b1, false);
         }
       },
       std::make_integer_sequence<int, TOTAL>{});
@@ -1600,14 +1627,11 @@ static int launch_hwide4_k(const ConvOp& op, hipStream_t st) {
 
 // the direct-store epilogue takes NHWC outputs with aligned channel runs:
 // every inference op of the graph and the training step's autocast fp32
-// outputs (out32 / res32 / mask16 / out32_h16; UPR_DS_OUT32=0 keeps those on
-// the LDS epilogue).  UPR_HW4_DS=0: always LDS (A/B)
+// outputs (out32 / res32 / mask16 / out32_h16)
 static bool hw4_ds_ok(const ConvOp& op) {
-  static const int en = env_int("UPR_HW4_DS", 1);
-  static const int en32 = env_int("UPR_DS_OUT32", 1);  // the autocast fp32-output form (A/B)
-  if (!en || op.store != kStoreNHWC) return false;
+  if (op.store != kStoreNHWC) return false;
   if (op.out32) {
-    if (!en32 || (uintptr_t)op.out32 % 16 || op.out32_cs % 8 || op.out32_coff % 8) return false;
+    if ((uintptr_t)op.out32 % 16 || op.out32_cs % 8 || op.out32_coff % 8) return false;
     if (op.res32 && ((uintptr_t)op.res32 % 16 || op.res32_cs % 8)) return false;
     if (op.mask16 && ((uintptr_t)op.mask16 % 8 || op.mask16_cs % 4)) return false;
     if (op.out32_h16 && ((uintptr_t)op.out32_h16 % 8 || op.out32_h16_cs % 4)) return false;
@@ -1621,86 +1645,61 @@ static bool hw4_ds_ok(const ConvOp& op) {
   return true;
 }
 
-template <int BN, int W, int NCH, int ABL = 0>
+template <int BN, int W, int NCH>
 static int launch_hwide4(const ConvOp& op, hipStream_t st) {
-  // the timing ablations (ABL != 0) exist for the direct-store form only
-  if (ABL != 0 || hw4_ds_ok(op)) return launch_hwide4_k<BN, W, NCH, ABL, true>(op, st);
+  if (hw4_ds_ok(op)) return launch_hwide4_k<BN, W, NCH, 0, true>(op, st);
   return launch_hwide4_k<BN, W, NCH, 0, false>(op, st);
 }
 
-// UPR_HW4=0 keeps the runtime-cursor hwide3 kernel (A/B timing)
+// the compile-time-schedule hwide4 for the graph's shapes (bottleneck: W 64,
+// Cin 256; dec3: W 128, Cin 128), the runtime-cursor hwide3 otherwise
 template <int BN, int W>
 static int launch_hwide34(const ConvOp& op, hipStream_t st) {
-  static const int v = env_int("UPR_HW4", 1);
   const int nch = op.seg[0].C / WBK;
-  if (v && op.seg[0].kbase == 0) {
-    // the graph's shapes: bottleneck (W 64, Cin 256), dec3 (W 128, Cin 128)
-    // (W 128 / 2 chunks still spills 40 VGPRs as a straight line: dec3 stays on hwide3)
+  if (op.seg[0].kbase == 0) {
     if constexpr (W == 64) {
-      static const int abl = env_int("UPR_HW4_ABL", 0);  // timing ablations (garbage results)
-      if (nch == 4 && abl == 1) return launch_hwide4<BN, W, 4, 1>(op, st);
-      if (nch == 4 && abl == 2) return launch_hwide4<BN, W, 4, 2>(op, st);
-      if (nch == 4 && abl == 3) return launch_hwide4<BN, W, 4, 3>(op, st);
-      if (nch == 4 && abl == 4) return launch_hwide4<BN, W, 4, 4>(op, st);
-      if (nch == 4 && abl == 7) return launch_hwide4<BN, W, 4, 7>(op, st);
-      if (nch == 4 && abl == 8) return launch_hwide4<BN, W, 4, 8>(op, st);
-      if (nch == 4 && abl == 12) return launch_hwide4<BN, W, 4, 12>(op, st);
       if (nch == 4) return launch_hwide4<BN, W, 4>(op, st);
     } else {
       // dec3 (W 128, 2 chunks) on the direct-store form only (its LDS-epilogue
       // straight line spilled 40 VGPRs): dec3.conv.0 shape 0.196 -> 0.153 ms,
-      // conv.3 (+ residual) 0.223 -> 0.186 (same-box A/B, profiles/r3_hw4_ds_ab.txt);
-      // UPR_HW4_128=0 keeps them on hwide3
-      static const int v128 = env_int("UPR_HW4_128", 1);
-      if (v128 && nch == 2 && hw4_ds_ok(op)) return launch_hwide4_k<BN, W, 2, 0, true>(op, st);
+      // conv.3 (+ residual) 0.223 -> 0.186 (same-box A/B, profiles/r3_hw4_ds_ab.txt)
+      if (nch == 2 && hw4_ds_ok(op)) return launch_hwide4_k<BN, W, 2, 0, true>(op, st);
+      // 256-channel inputs at W 128 (the training step's VGG-19 conv3_x and
+      // their input gradients, losses/loss.py:198-211)
+      if (nch == 4 && hw4_ds_ok(op)) return launch_hwide4_k<BN, W, 4, 0, true>(op, st);
     }
   }
   return launch_hwide3<BN, W>(op, st);
 }
 
-// UPR_WIDE_HALO=0 routes these convs to the gathered-A kernel, =1 to the
-// two-stage halo kernel (A/B timing); default: the ring / three-stage form
-// for W 64 x N 256, two-stage halo for W 64 x N 128, gathered for W 128
+// halo-tiled convs: the ring / three-stage form (hwide4 / hwide3) for W 64 x
+// N 256 and W 128 x N 128, the two-stage halo kernel for W 64 x N 128
+// (measured against the gathered-A kernel: profiles/r2_halo*, r3_hw4_*)
 static int halo_route(const ConvOp& op, hipStream_t st) {
-  static const int mode = env_int("UPR_WIDE_HALO", 2);
-  if (!mode || op.nseg != 1 || op.store != kStoreNHWC) return kErrUnsupported;
+  if (op.nseg != 1 || op.store != kStoreNHWC) return kErrUnsupported;
   const ConvSeg& s = op.seg[0];
-  {
-    // dilated 3x3 over 256 channels at W 64 (the ASPP branches, d 6 / 12 / 18):
-    // the region form of hwide4.  UPR_HW4_DIL=0 keeps them on the gathered kernel
-    static const int dl = env_int("UPR_HW4_DIL", 1);
-    if (dl && s.kh == 3 && s.kw == 3 && s.stride == 1 && s.dil > 1 && s.pad == s.dil && s.dil < 64 &&
-        s.pre == kPreNone && s.kbase == 0 && s.C == 256 && s.Hin == op.Ho && s.Win == op.Wo && op.Wo == 64 &&
-        op.N % 256 == 0 && (op.Ho * op.Wo) % WBM == 0 && hw4_ds_ok(op))
-      return launch_hwide4_k<256, 64, 4, 0, true, true>(op, st);
-  }
+  // dilated 3x3 over 256 channels at W 64 (the ASPP branches, d = 6 / 12 / 18):
+  // the region form of hwide4 (gathered kernel: 0.168 / 0.153 / 0.143 ms vs
+  // 0.158 / 0.145 / 0.136, profiles/r3_hw4_dil_ab.txt)
+  if (s.kh == 3 && s.kw == 3 && s.stride == 1 && s.dil > 1 && s.pad == s.dil && s.dil < 64 && s.pre == kPreNone &&
+      s.kbase == 0 && s.C == 256 && s.Hin == op.Ho && s.Win == op.Wo && op.Wo == 64 && op.N % 256 == 0 &&
+      (op.Ho * op.Wo) % WBM == 0 && hw4_ds_ok(op))
+    return launch_hwide4_k<256, 64, 4, 0, true, true>(op, st);
   if (s.kh != 3 || s.kw != 3 || s.stride != 1 || s.pad != 1 || s.dil != 1 || s.pre != kPreNone) return kErrUnsupported;
   if (s.Hin != op.Ho || s.Win != op.Wo || s.C % WBK || (op.Ho * op.Wo) % WBM) return kErrUnsupported;
-  {
-    // 64 -> 64 at W 256 (dec2 UpBlock convs, 256^2 x 64): hwide4 with 2-row
-    // tiles over the one 64-channel chunk (4 region rows of 32 KiB, 9 taps).
-    // Opt-in (UPR_HW4_64=1): correct, but 9% SLOWER than the row ring on the
-    // same box (dec2p 0.234 -> 0.255 ms, profiles/r3_hw4_64_ab.txt): at 152 KiB
-    // of LDS one block per CU exposes every tile's 128 KiB region fill
-    static const int v64 = env_int("UPR_HW4_64", 0);
-    if (v64 && op.Wo == 256 && op.N == 64 && s.C == 64 && s.kbase == 0 && op.Ho % 2 == 0 && hw4_ds_ok(op))
-      return launch_hwide4_k<64, 256, 1, 0, true, false, 2>(op, st);
-  }
+  // (64 -> 64 at W 256, the dec2 UpBlock convs, as hwide4 2-row tiles measured
+  // 9% slower than the row ring: dec2p 0.234 -> 0.255 ms, profiles/r3_hw4_64_ab.txt)
   if (op.N % 128) return kErrUnsupported;
-  if (op.Wo == 64 && op.N % 256 == 0) return mode == 1 ? launch_hwide<256, 64>(op, st) : launch_hwide34<256, 64>(op, st);
+  if (op.Wo == 64 && op.N % 256 == 0) return launch_hwide34<256, 64>(op, st);
   if (op.Wo == 64) return launch_hwide<128, 64>(op, st);
-  if (op.Wo == 128 && mode == 1) return launch_hwide<128, 128>(op, st);
-  if (op.Wo == 128 && mode == 2 && (op.Ho * op.Wo) % 512 == 0) return launch_hwide34<128, 128>(op, st);
+  if (op.Wo == 128 && (op.Ho * op.Wo) % 512 == 0) return launch_hwide34<128, 128>(op, st);
   return kErrUnsupported;
 }
 
 
 // the gathered kernel's direct-store form takes what hwide4's does minus the
-// per-image pool (its tiles may straddle images); UPR_WIDE_DS=0: LDS epilogue (A/B)
-static bool wide_ds_ok(const ConvOp& op) {
-  static const int en = env_int("UPR_WIDE_DS", 1);
-  return en && !op.pool && hw4_ds_ok(op);
-}
+// per-image pool (its tiles may straddle images)
+static bool wide_ds_ok(const ConvOp& op) { return !op.pool && hw4_ds_ok(op); }
 
 template <int BN, bool PIPE, int SCHED, bool DS>
 static int launch_wide_bn_k(const ConvOp& op, hipStream_t st) {
@@ -1722,22 +1721,10 @@ static int launch_wide_bn_s(const ConvOp& op, hipStream_t st) {
   return wide_ds_ok(op) ? launch_wide_bn_k<BN, PIPE, SCHED, true>(op, st) : launch_wide_bn_k<BN, PIPE, SCHED, false>(op, st);
 }
 
-// UPR_WIDE_SCHED: 2 = one fragment read per two MFMAs (default), 0 = grouped interleave (A/B timing)
+// schedule 2: one fragment read per two MFMAs (beat the grouped interleave)
 template <int BN, bool PIPE>
 static int launch_wide_bn(const ConvOp& op, hipStream_t st) {
-  static const int v = getenv("UPR_WIDE_SCHED") ? atoi(getenv("UPR_WIDE_SCHED")) : 2;
-  return v == 2 ? launch_wide_bn_s<BN, PIPE, 2>(op, st) : launch_wide_bn_s<BN, PIPE, 0>(op, st);
-}
-
-// UPR_WIDE_KIND=0 selects the plain main loop (A/B timing); default: the
-// half-step pipeline across the barrier
-static int wide_kind() {
-  static int k = -1;
-  if (k < 0) {
-    const char* e = getenv("UPR_WIDE_KIND");
-    k = (e && atoi(e) == 0) ? 0 : 1;
-  }
-  return k;
+  return launch_wide_bn_s<BN, PIPE, 2>(op, st);
 }
 
 static int launch_wide_onestep128(const ConvOp& op, hipStream_t st);
@@ -1748,20 +1735,9 @@ static int launch_wide_onestep128(const ConvOp& op, hipStream_t st);
 // 0.255 -> 0.204, dec1.up 0.369 -> 0.258 -- and, as 128-wide halves, on the
 // 2-step 256-wide dec2.up 0.178 -> 0.157; the 4-step 256-wide ASPP conv1x1
 // 0.070 -> 0.053 ms; the 16-step ASPP fusion breaks even, so it stays whole).
-// UPR_WIDE_ONESTEP = max K steps for 128-wide GEMMs (0 = never; A/B timing),
-// UPR_WIDE_SPLIT256 = max K steps for splitting 256-wide GEMMs.
-static int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-static int onestep_max() {
-  static const int v = env_int("UPR_WIDE_ONESTEP", 1 << 30);
-  return v;
-}
-static int split256_max() {
-  static const int v = env_int("UPR_WIDE_SPLIT256", 4);
-  return v;
-}
+// 128-wide GEMMs always take it; 256-wide ones of <= kSplit256 K steps (and
+// stride-2 ones) run as two 128-wide halves on it.
+constexpr int kSplit256 = 4;
 
 template <int BN>
 static int launch_wide_any(const ConvOp& op, hipStream_t st) {
@@ -1771,11 +1747,9 @@ static int launch_wide_any(const ConvOp& op, hipStream_t st) {
   // where the 16-step 1x1 ASPP fusion loses (0.127 -> 0.156)
   bool s2 = false;
   for (int s = 0; s < op.nseg; ++s) s2 = s2 || op.seg[s].stride == 2;
-  static const int s2_split = env_int("UPR_WIDE_SPLIT256_S2", 1);
-  if (steps <= (BN == 128 ? onestep_max() : split256_max()) || (BN == 256 && s2 && s2_split))
-    return launch_wide_onestep128(op, st);
+  if (BN == 128 || steps <= kSplit256 || s2) return launch_wide_onestep128(op, st);
   if (steps < 2) return launch_wide_bn<BN, false>(op, st);
-  return wide_kind() == 0 ? launch_wide_bn<BN, false>(op, st) : launch_wide_bn<BN, true>(op, st);
+  return launch_wide_bn<BN, true>(op, st);
 }
 
 // One-step GEMMs (K = 64: the dec1 ConvTranspose) are latency-bound at one
@@ -1796,19 +1770,8 @@ static int launch_wide_onestep128(const ConvOp& op, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-// UPR_CONV_WIDE=0 disables this path (A/B timing against conv_halo / conv_igemm)
-static bool wide_enabled() {
-  static int en = -1;
-  if (en < 0) {
-    const char* e = getenv("UPR_CONV_WIDE");
-    en = (e && strcmp(e, "0") == 0) ? 0 : 1;
-  }
-  return en == 1;
-}
-
 // fp16 only; returns kErrUnsupported for shapes this kernel does not take
 int launch_conv_wide(const ConvOp& op, hipStream_t st) {
-  if (!wide_enabled()) return kErrUnsupported;
   if (op.out2 && ((uintptr_t)op.out2 % 16 || op.store != kStoreNHWC)) return kErrUnsupported;
   if (op.out32 && ((uintptr_t)op.out32 % 16 || op.out32_cs % 4 || op.out32_coff % 4)) return kErrUnsupported;
   if (op.res32 && ((uintptr_t)op.res32 % 16 || op.res32_cs % 4)) return kErrUnsupported;
@@ -1825,15 +1788,8 @@ int launch_conv_wide(const ConvOp& op, hipStream_t st) {
   }
   if (op.N % 128) return kErrUnsupported;  // (64-wide: only the halo route above)
   if (op.N % 256 == 0) return launch_wide_any<256>(op, st);
-  // 128-channel stride-1 3x3 convs (dec3) used to stay on the halo kernel;
-  // on the single-stage two-blocks-per-CU variant they are faster (dec3.conv.0
-  // 0.264 -> 0.191 ms, conv.3 0.276 -> 0.217).  UPR_WIDE128_S1=0 restores the
-  // halo routing (A/B timing).
-  bool all_s1_3x3 = true;
-  for (int s = 0; s < op.nseg; ++s)
-    if (!(op.seg[s].kh == 3 && op.seg[s].stride == 1)) all_s1_3x3 = false;
-  static const int s1_wide = env_int("UPR_WIDE128_S1", 1);
-  if (all_s1_3x3 && op.Wo >= 24 && op.Ho >= 8 && !s1_wide) return kErrUnsupported;
+  // (128-channel stride-1 3x3 convs: faster here than on the old halo kernel,
+  // dec3.conv.0 0.264 -> 0.191 ms, conv.3 0.276 -> 0.217)
   return launch_wide_any<128>(op, st);
 }
 

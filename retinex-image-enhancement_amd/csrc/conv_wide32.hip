@@ -494,11 +494,6 @@ __global__ __launch_bounds__(512, 2 * OCC) void conv_wide32_kernel(ConvOp op) {
     q32_epilogue<BM, BN>(op, acc, smem, m0, n0, M, HW);
 }
 
-static int w32_env(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-
 template <int BM, int BN, int OCC, bool DS>
 static int launch_w32_k(const ConvOp& op, int steps, hipStream_t st) {
   using C = Q32Cfg<BM, BN>;
@@ -527,25 +522,16 @@ static int launch_w32_k(const ConvOp& op, int steps, hipStream_t st) {
 // channels wide.  Same-box A/B (profiles/r3_w32_ds_ab.txt): neutral on the fp32
 // step (the fp32 MFMAs hide the epilogue: 27.65 -> 27.63 ms), bneck / fuse /
 // enc3 s2 -1%, the 64-wide dec2 tile +1.3% (kept on the LDS epilogue).
-// UPR_WIDE32_DS=0 keeps the LDS epilogue everywhere
 template <int BM, int BN, int OCC>
 static int launch_w32(const ConvOp& op, int steps, hipStream_t st) {
-  static const int en = w32_env("UPR_WIDE32_DS", 1);
-  const bool ds = en && BN >= 128 && op.store == kStoreNHWC && (!op.pool || (op.Ho * op.Wo) % BM == 0);
+  const bool ds = BN >= 128 && op.store == kStoreNHWC && (!op.pool || (op.Ho * op.Wo) % BM == 0);
   return ds ? launch_w32_k<BM, BN, OCC, true>(op, steps, st) : launch_w32_k<BM, BN, OCC, false>(op, steps, st);
 }
 
-// fp32 only; kErrUnsupported for shapes this kernel does not take.
-// UPR_WIDE32=0 disables it (A/B timing against conv_halo / conv_igemm);
-// UPR_WIDE32=<cfg> forces a tile (1: 256x128 one block per CU, 2: 128x128 two,
-// 3: 512x64 one, 4: 256x64 two, 5: 256x64 one, 6: 128x64 two, 7: 128x64 three,
-// 8: 64x128 three, 9: 64x128 two) where the shape allows it.
+// fp32 only; kErrUnsupported for shapes this kernel does not take (N % 64:
+// the row ring / halo kernels).
 int launch_conv_wide32(const ConvOp& op, hipStream_t st) {
-  static const int mode = w32_env("UPR_WIDE32", -1);
-  if (mode == 0) return kErrUnsupported;
-  if (op.store == kStoreHeadIllu || op.N % 32) return kErrUnsupported;
-  static const int n32 = w32_env("UPR_WIDE32_N32", 0);
-  if (op.N % 64 && !n32) return kErrUnsupported;
+  if (op.store == kStoreHeadIllu || op.N % 64) return kErrUnsupported;
   if (op.store == kStoreConvT2x2 && (op.N / 4) % 8) return kErrUnsupported;
   if (op.Kpad % 4 || ((uintptr_t)op.W % 16) || op.scale) return kErrUnsupported;
   if (op.out_cs % 4 || op.out_coff % 4 || ((uintptr_t)op.out % 16)) return kErrUnsupported;
@@ -560,23 +546,6 @@ int launch_conv_wide32(const ConvOp& op, hipStream_t st) {
     steps += sg.kh * sg.kw * (sg.C / Q_BK);
   }
   const bool n128 = op.N % 128 == 0;
-  if (op.N % 64) {  // 32-wide (UPR_WIDE32_N32=1: 1 = 256 x 32 one block per CU, 2 = 256 x 32 two, 3 = 512 x 32 one)
-    if (n32 == 2) return launch_w32<256, 32, 2>(op, steps, st);
-    if (n32 == 3) return launch_w32<512, 32, 1>(op, steps, st);
-    return launch_w32<256, 32, 1>(op, steps, st);
-  }
-  switch (mode) {
-    case 1: if (n128) return launch_w32<256, 128, 1>(op, steps, st); break;
-    case 2: if (n128) return launch_w32<128, 128, 2>(op, steps, st); break;
-    case 3: return launch_w32<512, 64, 1>(op, steps, st);
-    case 4: return launch_w32<256, 64, 2>(op, steps, st);
-    case 5: return launch_w32<256, 64, 1>(op, steps, st);
-    case 6: return launch_w32<128, 64, 2>(op, steps, st);
-    case 7: return launch_w32<128, 64, 3>(op, steps, st);
-    case 8: if (n128) return launch_w32<64, 128, 3>(op, steps, st); break;
-    case 9: if (n128) return launch_w32<64, 128, 2>(op, steps, st); break;
-    default: break;
-  }
   // Tile per width, from per-shape sweeps on MI355X (tools/r2_w32sweep.sh, bs
   // 32, fp32): 128 x 128 at two blocks per CU beats 256 x 128 at one on every
   // 128/256/512-wide GEMM of the graph (enc3 s2 121.7 -> 128.3 TF/s, ASPP d18

@@ -395,15 +395,8 @@ static bool preact_materialised(const UprModel* m) { return m->use_preact && m->
 // the fp32 row ring with their filters in registers (the fused K = 640 filter
 // does not fit registers, and one ring with both halos and x does not fit
 // LDS); the x / maxpool3(x) 1x1 slices ride with the h3 part (second ring).
-// Same sum in a different association (fp32 rounding only).  UPR_FAM32_SPLIT=0
-// keeps the single launch (A/B timing).
-static bool fam32_split(const UprModel* m) {
-  static const int v = [] {
-    const char* e = getenv("UPR_FAM32_SPLIT");
-    return (e && atoi(e) == 0) ? 0 : 1;
-  }();
-  return v == 1 && m->dtype != kF16 && !(m->flags & UPR_MODEL_IENET_ONLY);
-}
+// Same sum in a different association (fp32 rounding only).
+static bool fam32_split(const UprModel* m) { return m->dtype != kF16 && !(m->flags & UPR_MODEL_IENET_ONLY); }
 
 static size_t ws_layout(const UprModel* m, int B, int H, int W, size_t* offs) {
   size_t off = 0;
@@ -830,41 +823,16 @@ static int build_model(UprModel* m, ParamSet& P) {
 // first use: non-blocking, joined through events every forward.  nullptr keeps
 // the whole forward on the caller's stream: UPR_MS_STREAMS=0 (A/B timing;
 // =1 forks fp32 models too, unset forks fp16 models only).
-// UPR_MS_PRIO: the side stream's priority (-1 high, 0 normal, 1 low).
-void ring_set_cu_cap(int cus);  // conv_ring.hip
-// UPR_SIDE_CUS: CU budget of the side stream's persistent ring convs (0: all)
-static int side_cu_cap() {
-  static const int v = [] {
-    const char* e = getenv("UPR_SIDE_CUS");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
-// UPR_MS_FORK: fork the side stream before the first IENet op whose name
-// contains this string (e.g. "enc3": the multi-scale ops then overlap the
-// MFMA-bound 64^2-128^2 middle of the IENet instead of its HBM-bound 512^2
-// start); unset / not found: right after op 0
-static int fork_op(const UprModel* m) {
-  static const std::string key = [] {
-    const char* e = getenv("UPR_MS_FORK");
-    return std::string(e ? e : "");
-  }();
-  if (!key.empty())
-    for (int i = 1; i < m->side_begin; ++i)
-      if (m->ops[i].name.find(key) != std::string::npos) return i;
-  return 1;
-}
+// The side stream forks right after op 0 (the side ops need only its scale1
+// output); a later fork (before enc3 / the bottleneck) and a capped CU budget
+// for the side stream's ring convs measured no better (profiles/r3_ms_fork_ab.txt,
+// r3_side_cus_ab.txt), as did a low-priority side stream (r3_ms_streams_ab.txt).
 
 using Side = UprModel::Side;
 static std::shared_ptr<Side> side_of(UprModel* m, hipStream_t st) {
   static const int en = [] {
     const char* e = getenv("UPR_MS_STREAMS");
     return e ? (atoi(e) != 0 ? 1 : 0) : -1;
-  }();
-  static const int prio = [] {
-    const char* e = getenv("UPR_MS_PRIO");
-    return e ? atoi(e) : 0;
   }();
   // default: fp16 models only.  fp32 gains ~1% (every fp32 conv is MFMA-bound,
   // profiles/r3_ms_streams_ab.txt) and a single stream keeps each kernel's
@@ -884,10 +852,7 @@ static std::shared_ptr<Side> side_of(UprModel* m, hipStream_t st) {
     return it->second;
   }
   auto sd = std::make_shared<Side>();
-  int least = 0, greatest = 0;
-  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = greatest = 0;
-  const int p = prio < 0 ? greatest : prio > 0 ? least : 0;
-  if (hipStreamCreateWithPriority(&sd->s, hipStreamNonBlocking, p) != hipSuccess ||
+  if (hipStreamCreateWithFlags(&sd->s, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&sd->fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&sd->join, hipEventDisableTiming) != hipSuccess) {
     (void)hipGetLastError();
@@ -1074,18 +1039,16 @@ static int run_forward(UprModel* m, const void* x, int B, int H, int W, void* en
     }
   } else {
     // IENet ops [0, fork) -> fork -> side: the multi-scale ops, main: the rest
-    // of the IENet -> join -> tail.  The fork point (fork_op) defaults to right
+    // of the IENet -> join -> tail.  The fork point is right
     // after op 0 (the side ops need only its scale1 output)
-    const int fk = fork_op(m);
+    const int fk = 1;
     int rc = kOk;
     for (int oi = 0; oi < fk; ++oi)
       if ((rc = run_op(oi, st)) != kOk) return rc;
     UPR_CHECK_HIP(hipEventRecord(sd->fork, st));
     UPR_CHECK_HIP(hipStreamWaitEvent(sd->s, sd->fork, 0));
-    ring_set_cu_cap(side_cu_cap());
     for (int oi = m->side_begin; oi < m->side_end; ++oi)
       if ((rc = run_op(oi, sd->s)) != kOk) break;
-    ring_set_cu_cap(0);
     // joined on every path once forked: after an error return too, completion
     // of the caller's stream still covers whatever the side stream enqueued
     UPR_CHECK_HIP(hipEventRecord(sd->join, sd->s));

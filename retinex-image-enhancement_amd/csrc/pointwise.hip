@@ -439,18 +439,14 @@ int launch_conv3(const void* x, const float* w, const float* bias, void* out0, v
                  int dtype, hipStream_t st, void* out2, const float* ps, const float* ph) {
   const int n = B * h * wd;
   if (n <= 0) return kErrShape;
-  if (dtype == kF16 && getenv("UPR_CONV3_DIRECT") == nullptr) {
+  if (dtype == kF16) {
     const int tx = cdiv(wd, 32), ty = cdiv(h, 8);
     // persistent grid: one wave of resident blocks (108 / 80 VGPRs -> 4 / 6 blocks per CU)
     const int grid = std::min(B * tx * ty, 256 * (out1 ? 4 : 6));
     // non-temporal output stores (measured 0.355 -> 0.313 ms at bs 32 512^2; the
-    // three 1 GB outputs do not fit the caches anyway); UPR_CONV3_NT=0 for A/B
-    static const int nt = getenv("UPR_CONV3_NT") ? atoi(getenv("UPR_CONV3_NT")) : 1;
-    if (out1 && nt)
+    // three 1 GB outputs do not fit the caches anyway)
+    if (out1)
       hipLaunchKernelGGL((conv3_mfma_kernel<2, true>), dim3(grid), dim3(256), 0, st, (const half_t*)x, w, bias,
-                         (half_t*)out0, (half_t*)out1, (half_t*)out2, ps, ph, h, wd, tx, ty, B);
-    else if (out1)
-      hipLaunchKernelGGL((conv3_mfma_kernel<2, false>), dim3(grid), dim3(256), 0, st, (const half_t*)x, w, bias,
                          (half_t*)out0, (half_t*)out1, (half_t*)out2, ps, ph, h, wd, tx, ty, B);
     else
       hipLaunchKernelGGL((conv3_mfma_kernel<1, false>), dim3(grid), dim3(256), 0, st, (const half_t*)x, w, bias,

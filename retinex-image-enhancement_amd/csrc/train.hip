@@ -89,30 +89,13 @@ int small_conv_dgrad_c3_16(const void* dy16, int B, int H, int W, const float* w
                            int accumulate, hipStream_t st);
 int small_conv_wgrad(const UprView* xv, const UprView* dyv, int B, int H, int W, int Cin, int Ho, int Wo, int Cout,
                      int kh, int kw, int stride, int pad, int dil, float* dw, float* dbias, hipStream_t st);
-// train_wgrad.hip: split-K GEMM weight gradient (UPR_WGRAD_GEMM=0: round-1 kernel)
+// train_wgrad.hip: split-K GEMM weight gradient (the conv_wgrad_kernel below takes the shapes it does not)
 int wgrad_gemm(const float* x, int B, int H, int W, int Cin, int x_cs, int x_coff, const float* dy, int Ho, int Wo,
                int Cout, int dy_cs, int dy_coff, int kh, int kw, int stride, int pad, int dil, float* dwp,
                hipStream_t st, int torch_ci = 0);
 int wgrad16_gemm(const void* x16, int B, int H, int W, int Cin, const float* dy, int Ho, int Wo, int Cout, int dy_cs,
                  int dy_coff, int kh, int kw, int stride, int pad, int dil, float* dwp, hipStream_t st,
                  int torch_ci = 0, const void* dy16 = nullptr);
-static bool wgrad_gemm_on() {
-  static int on = -1;
-  if (on < 0) {
-    const char* e = getenv("UPR_WGRAD_GEMM");
-    on = (e && atoi(e) == 0) ? 0 : 1;
-  }
-  return on == 1;
-}
-// UPR_TRAIN_SMALL=0 keeps the round-1 per-element kernels (A/B timing)
-static bool small_kernels_on() {
-  static int on = -1;
-  if (on < 0) {
-    const char* e = getenv("UPR_TRAIN_SMALL");
-    on = (e && atoi(e) == 0) ? 0 : 1;
-  }
-  return on == 1;
-}
 
 // scratch(): see upr_common.h
 void* scratch(int slot, size_t bytes, hipStream_t st) {
@@ -694,11 +677,7 @@ __global__ __launch_bounds__(256) void chan_reduce4_kernel(const float* __restri
 }
 
 static bool reduce4_ok(int C, int cs, int coff, const void* p) {
-  static const bool off = [] {  // UPR_REDUCE4=0: the scalar form (A/B timing)
-    const char* e = getenv("UPR_REDUCE4");
-    return e && e[0] == '0';
-  }();
-  return !off && C % 4 == 0 && C <= 1024 && cs % 4 == 0 && coff % 4 == 0 && ((uintptr_t)p & 15) == 0;
+  return C % 4 == 0 && C <= 1024 && cs % 4 == 0 && coff % 4 == 0 && ((uintptr_t)p & 15) == 0;
 }
 
 // Two-stage per-channel reductions (the float4 path): kRedSlots blocks of 1024
@@ -1211,31 +1190,6 @@ __global__ void maxpool_kernel(V x, int B, int H, int W, int C, int k, int s, in
   }
 }
 
-__global__ void maxpool_bwd_kernel(V x, V dy, int B, int H, int W, int C, int k, int s, int p, int Ho, int Wo, V dx) {
-  const long long n = (long long)B * Ho * Wo * C;
-  GSTRIDE(i, n) {
-    const int c = (int)(i % C);
-    long long r = i / C;
-    const int ox = (int)(r % Wo); r /= Wo;
-    const int oy = (int)(r % Ho);
-    const int b = (int)(r / Ho);
-    float m = -INFINITY;
-    int by = -1, bx = -1;
-    for (int ky = 0; ky < k; ++ky) {
-      const int iy = oy * s - p + ky;
-      if (iy < 0 || iy >= H) continue;
-      for (int kx = 0; kx < k; ++kx) {
-        const int ix = ox * s - p + kx;
-        if (ix < 0 || ix >= W) continue;
-        const float v = x.d[x.at(b, iy, ix, c)];
-        if (v > m || isnan(v) || by < 0) { m = v; by = iy; bx = ix; }
-        if (isnan(v)) break;
-      }
-    }
-    if (by >= 0) atomicAdd(dx.d + dx.at(b, by, bx, c), dy.d[dy.at(b, oy, ox, c)]);
-  }
-}
-
 __device__ __forceinline__ void bilin_src(int o, int in, float scale, int& i0, int& i1, float& l) {
   float sr = ((float)o + 0.5f) * scale - 0.5f;
   if (sr < 0.f) sr = 0.f;
@@ -1261,26 +1215,6 @@ __global__ void bilinear_kernel(V x, int B, int H, int W, int C, V y, int Ho, in
                     ly * ((1.f - lx) * x.d[x.at(b, y1, x0, c)] + lx * x.d[x.at(b, y1, x1, c)]);
     float* o = y.d + y.at(b, oy, ox, c);
     *o = accum ? *o + v : v;
-  }
-}
-
-__global__ void bilinear_bwd_kernel(V dy, int B, int H, int W, int C, int Ho, int Wo, float sh, float sw, V dx) {
-  const long long n = (long long)B * Ho * Wo * C;
-  GSTRIDE(i, n) {
-    const int c = (int)(i % C);
-    long long r = i / C;
-    const int ox = (int)(r % Wo); r /= Wo;
-    const int oy = (int)(r % Ho);
-    const int b = (int)(r / Ho);
-    int y0, y1, x0, x1;
-    float ly, lx;
-    bilin_src(oy, H, sh, y0, y1, ly);
-    bilin_src(ox, W, sw, x0, x1, lx);
-    const float g = dy.d[dy.at(b, oy, ox, c)];
-    atomicAdd(dx.d + dx.at(b, y0, x0, c), g * (1.f - ly) * (1.f - lx));
-    atomicAdd(dx.d + dx.at(b, y0, x1, c), g * (1.f - ly) * lx);
-    atomicAdd(dx.d + dx.at(b, y1, x0, c), g * ly * (1.f - lx));
-    atomicAdd(dx.d + dx.at(b, y1, x1, c), g * ly * lx);
   }
 }
 
@@ -2384,7 +2318,7 @@ int upr_t_conv_direct(const UprView* x, int B, int H, int W, int Cin, const floa
     return UPR_ERR_ARG;
   if (Ho != (H + 2 * pad - dil * (kh - 1) - 1) / stride + 1 || Wo != (W + 2 * pad - dil * (kw - 1) - 1) / stride + 1)
     return UPR_ERR_SHAPE;
-  if (small_kernels_on()) {
+  {
     const int rc = small_conv_fwd(x, B, H, W, Cin, w, bias, Cout, kh, kw, stride, pad, dil, y, Ho, Wo, relu,
                                   accumulate, ST(stream));
     if (rc != kErrUnsupported) return rc;
@@ -2414,7 +2348,6 @@ int upr_t_conv_direct16(const UprView* x, int B, int H, int W, int Cin, const fl
     return UPR_ERR_ARG;
   if (Ho != (H + 2 * pad - dil * (kh - 1) - 1) / stride + 1 || Wo != (W + 2 * pad - dil * (kw - 1) - 1) / stride + 1)
     return UPR_ERR_SHAPE;
-  if (!small_kernels_on()) return UPR_ERR_UNSUPPORTED;
   if (skip32 && accumulate) return UPR_ERR_ARG;
   const int rc = small_conv_fwd(x, B, H, W, Cin, w, bias, Cout, kh, kw, stride, pad, dil, y, Ho, Wo, relu, accumulate,
                                 ST(stream), y16, skip32);
@@ -2425,7 +2358,7 @@ int upr_t_conv_direct_dgrad(const UprView* dy, int Ho, int Wo, const float* w, i
                             int kh, int kw, int stride, int pad, int dil, const UprView* dx, int accumulate,
                             void* stream) {
   if (!dy || !dx || !dy->data || !dx->data || !w || B <= 0 || stride <= 0 || dil <= 0) return UPR_ERR_ARG;
-  if (small_kernels_on()) {
+  {
     const int rc = small_conv_dgrad(dy, Ho, Wo, w, B, H, W, Cin, Cout, kh, kw, stride, pad, dil, dx, accumulate,
                                     ST(stream));
     if (rc != kErrUnsupported) return rc;
@@ -2440,7 +2373,7 @@ int upr_t_conv_direct_wgrad(const UprView* x, const UprView* dy, int B, int H, i
                             int Cout, int kh, int kw, int stride, int pad, int dil, float* dw, float* dbias,
                             void* stream) {
   if (!x || !dy || !dw || B <= 0) return UPR_ERR_ARG;
-  if (small_kernels_on()) {
+  {
     const int rc = small_conv_wgrad(x, dy, B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pad, dil, dw, dbias, ST(stream));
     if (rc != kErrUnsupported) return rc;
   }
@@ -2535,14 +2468,6 @@ int upr_t_cast_f16(const float* x, void* y, size_t n, void* stream) {
 }
 
 // UPR_T_OUT32=0: fp16 conv output + separate fp32 cast pass (A/B timing)
-static bool out32_on() {
-  static int on = -1;
-  if (on < 0) {
-    const char* e = getenv("UPR_T_OUT32");
-    on = (e && atoi(e) == 0) ? 0 : 1;
-  }
-  return on == 1;
-}
 
 int upr_t_conv_mfma16(const float* x, int B, int H, int W, int Cin, int x_cs, int x_coff, const void* wp16,
                       const float* bias, int N, int kh, int kw, int stride, int pad, int dil, const float* res,
@@ -2552,7 +2477,10 @@ int upr_t_conv_mfma16(const float* x, int B, int H, int W, int Cin, int x_cs, in
   if (!x16_ready && !x) return UPR_ERR_ARG;
   const bool want16 = (store & 2) != 0;  // y16 must end up holding (half)y
   const bool only16 = want16 && (store & 4) != 0;  // y itself not needed (written only on the fallback path)
+  // the 1x1 stride-2 conv's input gradient (y = 2H x 2W, accumulated into at the even pixels)
+  const bool s2 = (store & 8) != 0;
   store &= 1;
+  if (s2 && (kh != 1 || kw != 1 || stride != 1 || pad != 0 || dil != 1 || store != 0 || !res || relu)) return UPR_ERR_ARG;
   const int ycs16 = y16_cs > 0 ? y16_cs : (store == 1 ? N / 4 : N);  // y16's channel stride
   if (ycs16 % 8 || ((uintptr_t)y16 & 15)) return UPR_ERR_ARG;
   if (kh <= 0 || kw <= 0 || stride <= 0 || dil <= 0 || pad < 0) return UPR_ERR_ARG;
@@ -2579,18 +2507,20 @@ int upr_t_conv_mfma16(const float* x, int B, int H, int W, int Cin, int x_cs, in
   c.B = B; c.Ho = Ho; c.Wo = Wo; c.N = N; c.Kpad = kh * kw * Cin;
   c.W = wp16; c.bias = bias; c.relu = relu;
   c.store = store == 1 ? kStoreConvT2x2 : kStoreNHWC;
-  if (out32_on()) {
+  {
     // the fp32 output (+ fp32 residual / accumulated gradient) straight from the conv epilogue
     ConvOp c32 = c;
     c32.out32 = y; c32.out32_cs = y_cs; c32.out32_coff = y_coff;
     c32.res32 = res; c32.res32_cs = res_cs;
     if (want16) { c32.out32_h16 = y16; c32.out32_h16_cs = ycs16; }
     c32.skip32 = only16 ? 1 : 0;
+    c32.out_s2 = s2 ? 1 : 0;
     const int rc = launch_conv_out32(c32, st);
     if (rc != kErrUnsupported) {
       if (rc != 0) return rc;
       LAUNCH_CHECK();
     }
+    if (s2) return UPR_ERR_UNSUPPORTED;  // no other kernel scatters at stride 2
   }
   c.out = y16; c.out_cs = ycs16; c.out_coff = 0;
   const int rc = launch_conv(c, kF16, st);
@@ -2610,7 +2540,6 @@ int upr_t_conv_mfma16_relu_bwd(const void* x16, int B, int H, int W, int Cin, co
   if (((uintptr_t)x16 | (uintptr_t)y16 | (uintptr_t)mask16) % 16 || y16_cs % 8 || mask16_cs % 8 || y_cs % 4 ||
       y_coff % 4 || (uintptr_t)y % 16)
     return UPR_ERR_UNSUPPORTED;
-  if (!out32_on()) return UPR_ERR_UNSUPPORTED;
   const int Ho = H + 2 * pad - dil * (kh - 1), Wo = W + 2 * pad - dil * (kw - 1);
   if (Ho <= 0 || Wo <= 0) return UPR_ERR_SHAPE;
   ConvOp c;
@@ -2635,7 +2564,7 @@ int upr_t_conv_wgrad(const float* x, int B, int H, int W, int Cin, int x_cs, int
                      int Wo, int Cout, int dy_cs, int dy_coff, int kh, int kw, int stride, int pad, int dil,
                      float* dwp, void* stream) {
   if (!x || !dy || !dwp || B <= 0 || Cin % 32 || Cout % 32 || Cin <= 0 || Cout <= 0) return UPR_ERR_ARG;
-  if (wgrad_gemm_on()) {
+  {
     const int rc = wgrad_gemm(x, B, H, W, Cin, x_cs, x_coff, dy, Ho, Wo, Cout, dy_cs, dy_coff, kh, kw, stride, pad, dil,
                               dwp, ST(stream));
     if (rc != kErrUnsupported) return rc;
@@ -2686,7 +2615,7 @@ int upr_t_conv_wgrad_into(const float* x, const void* x16, int B, int H, int W, 
     if (rc != kErrUnsupported) return rc;
   }
   if (!x) return UPR_ERR_ARG;
-  if (wgrad_gemm_on()) {
+  {
     const int rc = wgrad_gemm(x, B, H, W, Cin, x_cs, x_coff, dy, Ho, Wo, Cout, dy_cs, dy_coff, kh, kw, stride, pad, dil,
                               dw, st, Cin);
     if (rc != kErrUnsupported) return rc;
@@ -3227,11 +3156,6 @@ int upr_t_maxpool_bwd(const UprView* x, const UprView* dy, int B, int H, int W, 
   if (!x || !dy || !dx || k <= 0 || s <= 0 || k * k > 255) return UPR_ERR_ARG;
   hipStream_t st = ST(stream);
   const long long n = (long long)B * Ho * Wo * C;
-  if (getenv("UPR_MAXPOOL_BWD_SCATTER")) {
-    hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, st, mkv(x), mkv(dy), B, H, W, C, k, s, p,
-                       Ho, Wo, mkv(dx));
-    LAUNCH_CHECK();
-  }
   void* code = nullptr;
   code = scratch(kSlotCode, (size_t)n, st);
   if (!code) return (int)hipErrorOutOfMemory;
@@ -3368,10 +3292,7 @@ int upr_t_bilinear_bwd(const UprView* dy, int B, int H, int W, int C, int Ho, in
                        void* stream) {
   if (!dy || !dx) return UPR_ERR_ARG;
   const long long n = (long long)B * Ho * Wo * C;
-  if (getenv("UPR_BILINEAR_BWD_SCATTER")) {  // the atomic scatter form (A/B timing)
-    hipLaunchKernelGGL(bilinear_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), mkv(dy), B, H, W, C, Ho, Wo,
-                       (float)H / Ho, (float)W / Wo, mkv(dx));
-  } else if (n > 0 && vec4_view_ok(dy, B, Ho, Wo, C) && vec4_view_ok(dx, B, H, W, C) &&
+  if (n > 0 && vec4_view_ok(dy, B, Ho, Wo, C) && vec4_view_ok(dx, B, H, W, C) &&
              (long long)B * Ho * W * C < (1LL << 31)) {
     hipStream_t st = ST(stream);
     const int nr = B * Ho * W * C / 4, ns = B * H * W * C / 4;

@@ -572,9 +572,159 @@ int small_conv_dgrad(const UprView* dyv, int Ho, int Wo, const float* w, int B, 
   return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// weight gradient of the 7x7 2 -> 1 spatial-attention conv (stride 1, pad 3;
+// EnhancedFAM, models/model.py:53,92-95): dW[ci][ky][kx] = sum_p dy[p] *
+// x[p + (ky, kx) - 3][ci], db = sum_p dy[p] -- 99 dot products over the
+// pixels, 12 bytes per pixel.  The generic MFMA form above spent its time in
+// per-pixel index math and per-lane gathers (0.58 ms at bs 8 512^2).  Here a
+// block owns an 8 x 64 pixel tile: dy and the (8 + 6) x (64 + 6) x 2 input
+// window (zero outside the image) are staged in LDS once, then two threads
+// per entry each sum 4 rows of the tile from LDS; one partial row per block
+// (part[block][99]), summed in block order by small_wgrad_fin_kernel.
+// ---------------------------------------------------------------------------
+constexpr int SA_TR = 8, SA_TC = 64, SA_K = 7, SA_P = 3;
+
+__global__ __launch_bounds__(256) void sa_wgrad_kernel(SV x, SV dy, int B, int H, int W, int tiles_x, int tiles_y,
+                                                       float* __restrict__ part) {
+  constexpr int LR = SA_TR + SA_K - 1, LC = SA_TC + SA_K - 1;
+  __shared__ float xs[2][LR][LC + 1];
+  __shared__ float ds[SA_TR][SA_TC];
+  __shared__ float red[99];
+  const int t = threadIdx.x;
+  const int tile = blockIdx.x;
+  const int tx = tile % tiles_x, rest = tile / tiles_x, ty = rest % tiles_y, b = rest / tiles_y;
+  const int y0 = ty * SA_TR, x0 = tx * SA_TC;
+  for (int i = t; i < LR * LC; i += 256) {
+    const int r = i / LC, c = i - r * LC;  // LDS fill only (once per element)
+    const int iy = y0 + r - SA_P, ix = x0 + c - SA_P;
+    const bool in = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+    xs[0][r][c] = in ? x.d[x.at(b, iy, ix, 0)] : 0.f;
+    xs[1][r][c] = in ? x.d[x.at(b, iy, ix, 1)] : 0.f;
+  }
+  for (int i = t; i < SA_TR * SA_TC; i += 256) {
+    const int r = i / SA_TC, c = i - r * SA_TC;
+    const int oy = y0 + r, ox = x0 + c;
+    ds[r][c] = (oy < H && ox < W) ? dy.d[dy.at(b, oy, ox, 0)] : 0.f;
+  }
+  if (t < 99) red[t] = 0.f;
+  __syncthreads();
+  // entry e = ci * 49 + ky * 7 + kx (PyTorch's weight order), e = 98: the bias;
+  // threads e and e + 99 take rows 0-3 / 4-7
+  float a = 0.f;
+  int e = -1;
+  if (t < 198) {
+    e = t % 99;
+    const int r0 = (t / 99) * (SA_TR / 2);
+    if (e < 98) {
+      const int ci = e / 49, tap = e - ci * 49, ky = tap / 7, kx = tap - ky * 7;
+      for (int r = r0; r < r0 + SA_TR / 2; ++r) {
+#pragma unroll 8
+        for (int c = 0; c < SA_TC; ++c) a = fmaf(ds[r][c], xs[ci][r + ky][c + kx], a);
+      }
+    } else {
+      for (int r = r0; r < r0 + SA_TR / 2; ++r)
+#pragma unroll 8
+        for (int c = 0; c < SA_TC; ++c) a += ds[r][c];
+    }
+  }
+  // the two halves in a fixed order: rows 0-3 first, then rows 4-7
+  if (t < 99) red[t] = a;
+  __syncthreads();
+  if (t >= 99 && t < 198) red[e] += a;
+  __syncthreads();
+  if (t < 99) part[(size_t)blockIdx.x * 99 + t] = red[t];
+}
+
+// weight gradient of a 1x1 stride-1 conv with Cin * Cout <= 128 (the output
+// layer 32 -> 3 and the residual head's 32 -> 1, model.py:326,402):
+// dW[co][ci] = sum_p dy[p][co] * x[p][ci] (+ db[co] = sum_p dy[p][co]).  One
+// thread per pixel keeps all Cin * Cout (+ Cout) partials in registers; a
+// block owns 4 image rows, reduces per entry over its waves (shuffles, then 4
+// wave partials in order) into part[block][co * (Cin + 1) + k].
+template <int CIN, int COUT>
+__global__ __launch_bounds__(256) void pw_wgrad_kernel(SV x, SV dy, int B, int H, int W, int rows_per_block,
+                                                       float* __restrict__ part) {
+  constexpr int NE = COUT * (CIN + 1);
+  __shared__ float wred[4][NE];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  float acc[COUT][CIN + 1];
+#pragma unroll
+  for (int co = 0; co < COUT; ++co)
+#pragma unroll
+    for (int k = 0; k <= CIN; ++k) acc[co][k] = 0.f;
+  const int row0 = blockIdx.x * rows_per_block;
+  const int nrow = B * H;
+  for (int rr = 0; rr < rows_per_block; ++rr) {
+    const int row = row0 + rr;
+    if (row >= nrow) break;
+    const int b = row / H, y = row - b * H;  // once per row
+    for (int px = t; px < W; px += 256) {
+      const float* xp = x.d + x.at(b, y, px, 0);
+      float xv[CIN];
+#pragma unroll
+      for (int c = 0; c < CIN; c += 4) {
+        const f32x4_t2 q = *(const f32x4_t2*)(xp + c);
+        xv[c] = q[0]; xv[c + 1] = q[1]; xv[c + 2] = q[2]; xv[c + 3] = q[3];
+      }
+#pragma unroll
+      for (int co = 0; co < COUT; ++co) {
+        const float g = dy.d[dy.at(b, y, px, co)];
+#pragma unroll
+        for (int c = 0; c < CIN; ++c) acc[co][c] = fmaf(g, xv[c], acc[co][c]);
+        acc[co][CIN] += g;
+      }
+    }
+  }
+#pragma unroll
+  for (int co = 0; co < COUT; ++co)
+#pragma unroll
+    for (int k = 0; k <= CIN; ++k) {
+      float v = acc[co][k];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      if (lane == 0) wred[wave][co * (CIN + 1) + k] = v;
+    }
+  __syncthreads();
+  for (int i = t; i < NE; i += 256)
+    part[(size_t)blockIdx.x * NE + i] = ((wred[0][i] + wred[1][i]) + wred[2][i]) + wred[3][i];
+}
+
 int small_conv_wgrad(const UprView* xv, const UprView* dyv, int B, int H, int W, int Cin, int Ho, int Wo, int Cout,
                      int kh, int kw, int stride, int pad, int dil, float* dw, float* dbias, hipStream_t st) {
   if (Cout > 32) return kErrUnsupported;
+  {
+    const SV x = mksv(xv), dy = mksv(dyv);
+    // the 7x7 spatial-attention conv: LDS-tiled dot products
+    if (Cin == 2 && Cout == 1 && kh == SA_K && kw == SA_K && stride == 1 && dil == 1 && pad == SA_P && dbias &&
+        Ho == H && Wo == W) {
+      const int tx = (W + SA_TC - 1) / SA_TC, ty = (H + SA_TR - 1) / SA_TR;
+      const int grid = B * tx * ty;
+      float* part = (float*)scratch(kSlotPart, sizeof(float) * (size_t)grid * 99, st);
+      if (!part) return (int)hipErrorOutOfMemory;
+      hipLaunchKernelGGL(sa_wgrad_kernel, dim3(grid), dim3(256), 0, st, x, dy, B, H, W, tx, ty, part);
+      hipLaunchKernelGGL(small_wgrad_fin_kernel, dim3(99), dim3(256), 0, st, (const float*)part, grid, 1, 98, dw,
+                         dbias);
+      return (int)hipGetLastError();
+    }
+    // 1x1 heads: one thread per pixel, all partials in registers
+    if (kh == 1 && kw == 1 && stride == 1 && pad == 0 && Ho == H && Wo == W && xv->sc == 1 && Cin % 4 == 0 &&
+        x.sw % 4 == 0 && x.sh % 4 == 0 && x.sb % 4 == 0 && ((uintptr_t)x.d & 15) == 0 &&
+        ((Cin == 32 && (Cout == 1 || Cout == 3)))) {
+      const int rows_per_block = 4;
+      const int grid = (B * H + rows_per_block - 1) / rows_per_block;
+      const int ne = Cout * (Cin + 1);
+      float* part = (float*)scratch(kSlotPart, sizeof(float) * (size_t)grid * ne, st);
+      if (!part) return (int)hipErrorOutOfMemory;
+      if (Cout == 1)
+        hipLaunchKernelGGL((pw_wgrad_kernel<32, 1>), dim3(grid), dim3(256), 0, st, x, dy, B, H, W, rows_per_block, part);
+      else
+        hipLaunchKernelGGL((pw_wgrad_kernel<32, 3>), dim3(grid), dim3(256), 0, st, x, dy, B, H, W, rows_per_block, part);
+      hipLaunchKernelGGL(small_wgrad_fin_kernel, dim3(ne), dim3(256), 0, st, (const float*)part, grid, Cout, Cin, dw,
+                         dbias);
+      return (int)hipGetLastError();
+    }
+  }
   const int KC = Cin * kh * kw + (dbias ? 1 : 0);
   const int nt = (KC + 31) / 32;
   if (nt > 4) return kErrUnsupported;

@@ -108,6 +108,10 @@ struct ConvOp {
   // into, fused (mask16 = that activation's fp16 copy); skip32: out32 is not
   // written, only out32_h16 (a gradient whose one reader takes the fp16 copy)
   const void* mask16; int mask16_cs; int skip32;
+  // with out32, a 1x1 stride-1 op over an H x W input (launch_conv_pw only):
+  // input pixel (b, i, j) lands at output pixel (b, 2i, 2j) of a 2H x 2W map,
+  // the others are not written (the 1x1 stride-2 conv's input gradient)
+  int out_s2;
 };
 
 // fp16 convs with an fp32 output (ConvOp::out32): the wide-tile and row-ring

@@ -414,6 +414,26 @@ class Conv:
                                        self.Cout, self.kh, self.kw, self.s, self.p, self.d,
                                        ctypes.byref(out.view()), Ho, Wo, int(relu), 0, st), "conv_direct")
 
+    def _dgrad_s2_1x1(self, gy, src16, B, Ho, Wo, gx):
+        """Input gradient of a 1x1 stride-2 conv (the projecting shortcut,
+        model.py:119-122) accumulated into gx: dx(2i, 2j) += W^T dy(i, j) on the
+        streaming 1x1 kernel (upr_t_conv_mfma16 store | 8), with no zero-upsampled
+        operand.  False when the shape is not one that kernel takes."""
+        if gy.stale32 and src16 is None:
+            return False
+        lib = L.lib()
+        x16 = src16 if src16 is not None else _h16(B * Ho * Wo * self.Cout, gy.t.device)
+        y16 = _h16(16, gy.t.device)  # not written (store has no | 2)
+        rc = lib.upr_t_conv_mfma16(None if src16 is not None else _fp(gy.t, 0), B, Ho, Wo, self.Cout,
+                                   gy.cs, gy.coff, _p(self.wt16), None, self.Cin, 1, 1, 1, 0, 1, gx.ptr(), gx.cs, 0,
+                                   _fp(gx.t), gx.cs, gx.coff, 8, _p(x16), int(src16 is not None), _p(y16), 0,
+                                   _stream())
+        if rc == L.UPR_ERR_UNSUPPORTED:
+            return False
+        _chk(rc, "conv_dgrad_s2_1x1")
+        gx.t16, gx.t16_grad = None, False  # gx changed: any fp16 copy of it is stale
+        return True
+
     def bwd(self, x, gy, gx=None, x_view=None, mask=None, gx_only16=False):
         """gy: Act gradient of this conv's output (pre-activation).
         Accumulates the weight / bias gradients; gx (Act, nullable) receives
@@ -488,6 +508,9 @@ class Conv:
                 # autocast: the fp16 operand comes from gy's producer (gy.t16) or, for
                 # stride 2, straight from an fp16 zero-upsample (no fp32 pass + cast)
                 src16 = gy.t16 if self.amp and gy.t16_grad and gy.coff == 0 and gy.cs == gy.C == self.Cout else None
+                if self.s == 2 and self.amp and acc and (self.kh, self.kw, self.p, self.d) == (1, 1, 0, 1) and \
+                        H == 2 * Ho and W == 2 * Wo and self._dgrad_s2_1x1(gy, src16, B, Ho, Wo, gx):
+                    return
                 if self.s != 1:
                     assert self.s == 2 and H == 2 * Ho and W == 2 * Wo, "stride-2 dgrad needs even sizes"
                     if self.amp and self.Cout % 8 == 0:
@@ -878,7 +901,6 @@ class ResBlockT:
         if self.proj:
             g_cs = Act.new(g.B, g.H, g.W, self.sconv.Cout, g.t.device)
             self.sbn.bwd(g, g_cs, only16=self.sconv.takes16_grad())
-            self.sconv.bwd(self.x, g_cs, gx)
         else:
             add_into(gx, g)
         g_a1 = Act.new(self.a1.B, self.a1.H, self.a1.W, self.a1.C, g.t.device)
@@ -886,6 +908,11 @@ class ResBlockT:
         g_c1 = Act.new(g_a1.B, g_a1.H, g_a1.W, g_a1.C, g.t.device)
         self.bn1.bwd(g_a1, g_c1, relu=True, only16=self.conv1.takes16_grad())
         self.conv1.bwd(self.x, g_c1, gx)
+        if self.proj:
+            # after conv1's: the shortcut's input gradient accumulates (the 1x1
+            # stride-2 one then adds at the even pixels only, _dgrad_s2_1x1);
+            # fp32 addition commutes, so the sum is the same bits either order
+            self.sconv.bwd(self.x, g_cs, gx)
 
 
 class PreActResBlockT:

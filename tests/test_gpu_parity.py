@@ -89,7 +89,7 @@ CONV_CASES = [
     (2, 64, 64, 256, 256, 3, 1, 6, 6, True, False),
     (1, 64, 64, 256, 256, 3, 1, 18, 18, False, True),
     (1, 32, 64, 256, 512, 3, 1, 12, 12, True, False),
-    # 64 -> 64 at W 256 (dec2 shape class: the row ring; hwide4 2-row tiles under UPR_HW4_64=1)
+    # 64 -> 64 at W 256 (dec2 shape class: the row ring)
     (1, 8, 256, 64, 64, 3, 1, 1, 1, True, False),
     (2, 6, 256, 64, 64, 3, 1, 1, 1, False, True),
 ]

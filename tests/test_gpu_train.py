@@ -401,6 +401,86 @@ def test_conv_mfma16_relu_bwd_vs_fp64(cin, cout, H, W, skip32):
         assert torch.equal(y.half().float(), g16)
 
 
+@pytest.mark.parametrize("cin,cout,bias,relu,resid", [
+    (96, 32, True, False, False),   # multi-scale head fusion forward (model.py:413)
+    (128, 32, True, True, False),   # EnhancedFAM fusion + ReLU (model.py:49, :86)
+    (32, 96, False, False, True),   # the fusion's input gradient, accumulated
+    (32, 128, False, False, False),
+    (64, 64, True, False, True),
+])
+def test_conv_mfma16_1x1_streaming(cin, cout, bias, relu, resid):
+    """upr_t_conv_mfma16 on 1x1 convs with K, N <= 128 (the streaming 1x1
+    kernel, conv_pw.hip): fp16 operands, fp32 output = (half)(x W^T + b) (+ the
+    accumulated fp32 gradient), the fp16 copy == (half) of it; vs fp64 on the
+    fp16-rounded operands."""
+    from upr import _lib as L
+    gen = torch.Generator().manual_seed(cin * 7 + cout)
+    B, H, W = 2, 48, 64
+    x = torch.randn(B, H, W, cin, generator=gen)
+    w = torch.randn(cout, cin, generator=gen) * 0.1
+    b = torch.randn(cout, generator=gen) if bias else None
+    r = torch.randn(B, H, W, cout, generator=gen) if resid else None
+    ref = x.half().double() @ w.half().double().t()
+    if bias:
+        ref = ref + b.double()
+    if relu:
+        ref = ref.clamp_min(0)
+    ref = ref.float().half().float()
+    if resid:
+        ref = ref + r
+    lib, st = L.lib(), torch.cuda.current_stream().cuda_stream
+    xd, wd16 = x.to(DEV), w.half().to(DEV).contiguous()
+    x16 = torch.empty(B * H * W * cin, dtype=torch.float16, device=DEV)
+    y = r.to(DEV) if resid else torch.full((B, H, W, cout), 5.0, device=DEV)
+    y16 = torch.empty(B * H * W * cout, dtype=torch.float16, device=DEV)
+    bd = b.to(DEV) if bias else None
+    rc = lib.upr_t_conv_mfma16(xd.data_ptr(), B, H, W, cin, cin, 0, wd16.data_ptr(), bd.data_ptr() if bias else None,
+                               cout, 1, 1, 1, 0, 1, y.data_ptr() if resid else None, cout if resid else 0, int(relu),
+                               y.data_ptr(), cout, 0, 0 if resid else 2, x16.data_ptr(), 0, y16.data_ptr(), 0, st)
+    assert rc == 0, rc
+    torch.cuda.synchronize()
+    _close(y, ref, 1e-3, "1x1 fp32 out")
+    if not resid:
+        assert torch.equal(y.half().float().view(-1), y16.float())
+
+
+@pytest.mark.parametrize("cin,cout", [(32, 64), (64, 128)])
+def test_dgrad_1x1_stride2_scatter(cin, cout):
+    """The projecting shortcut's input gradient (1x1 stride 2, model.py:119-122)
+    without the zero-upsampled operand (upr_t_conv_mfma16 store | 8): dx at the
+    even pixels += W^T dy, the odd pixels untouched; vs torch's conv2d_input on
+    the fp16-rounded operands."""
+    from upr import _lib as L
+    gen = torch.Generator().manual_seed(cin + 3 * cout)
+    B, Ho, Wo = 2, 32, 48
+    w = torch.randn(cout, cin, 1, 1, generator=gen) * 0.1
+    dy = torch.randn(B, cout, Ho, Wo, generator=gen)
+    base = torch.randn(B, 2 * Ho, 2 * Wo, cin, generator=gen)
+    g = torch.nn.grad.conv2d_input((B, cin, 2 * Ho, 2 * Wo), w.half().double(), dy.half().double(), stride=2)
+    ref = base + g.float().half().float().permute(0, 2, 3, 1)
+    lib, st = L.lib(), torch.cuda.current_stream().cuda_stream
+    wd = w.to(DEV)
+    wt = torch.empty(w.numel(), device=DEV)
+    assert lib.upr_t_pack_weight(wd.data_ptr(), wt.data_ptr(), cout, cin, 1, 1, 1, st) == 0
+    wt16 = wt.half()
+    dyd = dy.permute(0, 2, 3, 1).contiguous().to(DEV)
+    x16 = torch.empty(B * Ho * Wo * cout, dtype=torch.float16, device=DEV)
+    y16 = torch.empty(16, dtype=torch.float16, device=DEV)
+    gx = base.to(DEV)
+    rc = lib.upr_t_conv_mfma16(dyd.data_ptr(), B, Ho, Wo, cout, cout, 0, wt16.data_ptr(), None, cin, 1, 1, 1, 0, 1,
+                               gx.data_ptr(), cin, 0, gx.data_ptr(), cin, 0, 8, x16.data_ptr(), 0, y16.data_ptr(), 0,
+                               st)
+    assert rc == 0, rc
+    torch.cuda.synchronize()
+    _close(gx, ref, 1e-3, "1x1 s2 dgrad")
+    odd = torch.ones(2 * Ho, 2 * Wo, dtype=torch.bool)
+    odd[::2, ::2] = False
+    assert torch.equal(gx.cpu()[:, odd], base[:, odd])
+    # the flag is refused on anything but a 1x1 accumulate
+    assert lib.upr_t_conv_mfma16(dyd.data_ptr(), B, Ho, Wo, cout, cout, 0, wt16.data_ptr(), None, cin, 1, 1, 1, 0, 1,
+                                 None, 0, 0, gx.data_ptr(), cin, 0, 8, x16.data_ptr(), 0, y16.data_ptr(), 0, st) != 0
+
+
 def test_fp16_copy_producers():
     """The autocast operand copies written by their producers (no cast pass):
     upr_t_conv_direct16 (3 -> 32 / 64 3x3 + ReLU), upr_t_maxpool_code(y16),
