@@ -158,6 +158,125 @@ static int pw_k(const ConvOp& op, hipStream_t st) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Input gradient of a 3x3 stride-2 pad-1 conv (enc1.conv1, 32 -> 64 at 512^2:
+// models/model.py:100-178) without the zero-upsampled operand.  As a stride-1
+// conv over the zero-upsampled dy z (z(2i', 2j') = dy(i', j')) with the
+// flipped filter wf, dx(r, c) = sum_{t'} z(r - 1 + t'y, c - 1 + t'x) wf(t');
+// only the taps that land on even z positions contribute, so the four output
+// phases (r, c) = (2i + py, 2j + px) are small convs over dy itself:
+//   (0,0): wf(1,1) dy(i,j)
+//   (0,1): wf(1,0) dy(i,j) + wf(1,2) dy(i,j+1)
+//   (1,0): wf(0,1) dy(i,j) + wf(2,1) dy(i+1,j)
+//   (1,1): wf(0,0) dy(i,j) + wf(0,2) dy(i,j+1) + wf(2,0) dy(i+1,j) + wf(2,2) dy(i+1,j+1)
+// -- the 9 taps once each, no MFMA on zeros, no upsampled tensor in HBM.  A
+// wave keeps the whole flipped filter (9 taps x N/16 x K/32 fragments) in
+// registers and walks 16-pixel groups of dy rows, loading the four shifted
+// pixel runs (zero past the image) and writing all four phases with the
+// out32 epilogue family of conv_pw_kernel.
+// ---------------------------------------------------------------------------
+template <int KC, int NC>
+__global__ __launch_bounds__(256) void conv_s2dg_kernel(ConvOp op, int ngroups) {
+  constexpr int KS = KC / 32, NT = NC / 16;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int fr = lane & 15, fg = lane >> 4;
+  const ConvSeg& sg = op.seg[0];
+  const half_t* src = (const half_t*)sg.src;
+  const int Hin = sg.Hin, Win = sg.Win, HWin = Hin * Win;
+
+  // flipped tap (ty, tx) fragment (nt, ks): lane (fr, fg) = W[nt*16 + fr][(ty*3 + tx)*KC + ks*32 + 8 fg .. +7]
+  pwh8 wf[9][NT][KS];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        wf[t][nt][ks] = *(const pwh8*)((const half_t*)op.W + (size_t)(nt * 16 + fr) * op.Kpad + t * KC + ks * 32 + fg * 8);
+  const int stride = gridDim.x * 4;
+  for (int g = blockIdx.x * 4 + wave; g < ngroups; g += stride) {
+    const int q0 = g * 16;
+    const int b = q0 / HWin, rem = q0 - b * HWin, i = rem / Win, j = rem - i * Win + fr;
+    pwh8 x[4][KS];  // (di, dj) = (0,0), (0,1), (1,0), (1,1)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int ii = i + (s >> 1), jj = j + (s & 1);
+      const bool in = ii < Hin && jj < Win;
+      const half_t* p = src + ((size_t)(b * Hin + ii) * Win + jj) * sg.cs + fg * 8;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) x[s][ks] = in ? *(const pwh8*)(p + ks * 32) : pwh8{};
+    }
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) {
+      const int py = ph >> 1, px = ph & 1;
+      pwf4 acc[NT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[nt] = pwf4{0.f, 0.f, 0.f, 0.f};
+      // taps of the phase: (di, flipped ty) = py ? {(0, 0), (1, 2)} : {(0, 1)}; the same in x
+#pragma unroll
+      for (int a = 0; a < 1 + py; ++a) {
+        const int di = a, ty = py ? 2 * a : 1;
+#pragma unroll
+        for (int c = 0; c < 1 + px; ++c) {
+          const int dj = c, tx = px ? 2 * c : 1;
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+              acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ty * 3 + tx][nt][ks], x[di * 2 + dj][ks], acc[nt], 0, 0, 0);
+        }
+      }
+      const size_t m = (size_t)(b * 2 * Hin + 2 * i + py) * (2 * Win) + 2 * j + px;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int n = nt * 16 + fg * 4;
+        pwf4 t;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) t[r] = (float)(half_t)acc[nt][r];
+        if (op.res32) t += *(const pwf4*)(op.res32 + m * op.res32_cs + n);
+        if (op.mask16) {
+          const pwh4 mk = *(const pwh4*)((const half_t*)op.mask16 + m * op.mask16_cs + n);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) t[r] = (float)mk[r] > 0.f ? t[r] : 0.f;
+        }
+        if (!op.skip32) *(pwf4*)(op.out32 + m * op.out32_cs + op.out32_coff + n) = t;
+        if (op.out32_h16)
+          *(pwh4*)((half_t*)op.out32_h16 + m * op.out32_h16_cs + n) =
+              pwh4{(half_t)t[0], (half_t)t[1], (half_t)t[2], (half_t)t[3]};
+      }
+    }
+  }
+}
+
+// the 3x3 stride-2 input gradient above (op: dy as a 1-segment 3x3 op over
+// Hin x Win with the flipped filter, out32 family at 2 Hin x 2 Win); 64 -> 32
+// channels only (the filter must fit the registers)
+int launch_conv_s2dg(const ConvOp& op, hipStream_t st) {
+  const ConvSeg& s = op.seg[0];
+  if (op.nseg != 1 || op.store != kStoreNHWC || !op.out32 || op.bias || op.relu || op.res1 || op.res2 || op.pool ||
+      op.img_bias || op.scale || op.out2)
+    return kErrUnsupported;
+  if (s.kh != 3 || s.kw != 3 || s.C != 64 || op.N != 32 || s.kbase != 0 || s.pre != kPreNone) return kErrUnsupported;
+  if (s.cs % 8 || (uintptr_t)s.src % 16 || op.Kpad % 8 || (uintptr_t)op.W % 16 || s.Win % 16) return kErrUnsupported;
+  if ((uintptr_t)op.out32 % 16 || op.out32_cs % 4 || op.out32_coff % 4) return kErrUnsupported;
+  if (op.res32 && ((uintptr_t)op.res32 % 16 || op.res32_cs % 4)) return kErrUnsupported;
+  if (op.mask16 && ((uintptr_t)op.mask16 % 8 || op.mask16_cs % 4)) return kErrUnsupported;
+  if (op.out32_h16 && ((uintptr_t)op.out32_h16 % 8 || op.out32_h16_cs % 4)) return kErrUnsupported;
+  const long long npix = (long long)op.B * s.Hin * s.Win;
+  if (npix >= (1ll << 31) / 4) return kErrUnsupported;
+  const int ngroups = (int)(npix / 16);
+  int cus = 256;
+  {
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  }
+  int grid = std::min(cus * 2, (ngroups + 3) / 4);
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL((conv_s2dg_kernel<64, 32>), dim3(grid), dim3(256), 0, st, op, ngroups);
+  return (int)hipGetLastError();
+}
+
 // fp16 1x1 stride-1 convs of the shapes above; kErrUnsupported otherwise
 // (an out_s2 op must be taken here: no other kernel implements it)
 int launch_conv_pw(const ConvOp& op, hipStream_t st) {

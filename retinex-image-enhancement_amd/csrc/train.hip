@@ -2479,8 +2479,12 @@ int upr_t_conv_mfma16(const float* x, int B, int H, int W, int Cin, int x_cs, in
   const bool only16 = want16 && (store & 4) != 0;  // y itself not needed (written only on the fallback path)
   // the 1x1 stride-2 conv's input gradient (y = 2H x 2W, accumulated into at the even pixels)
   const bool s2 = (store & 8) != 0;
+  // the 3x3 stride-2 pad-1 conv's input gradient from dy itself (x16 = dy over H x W, wp16 the
+  // flipped filter, y = 2H x 2W); UPR_ERR_UNSUPPORTED when the kernel does not take the shape
+  const bool s2dg = (store & 16) != 0;
   store &= 1;
   if (s2 && (kh != 1 || kw != 1 || stride != 1 || pad != 0 || dil != 1 || store != 0 || !res || relu)) return UPR_ERR_ARG;
+  if (s2dg && (s2 || kh != 3 || kw != 3 || stride != 1 || dil != 1 || store != 0 || relu || bias)) return UPR_ERR_ARG;
   const int ycs16 = y16_cs > 0 ? y16_cs : (store == 1 ? N / 4 : N);  // y16's channel stride
   if (ycs16 % 8 || ((uintptr_t)y16 & 15)) return UPR_ERR_ARG;
   if (kh <= 0 || kw <= 0 || stride <= 0 || dil <= 0 || pad < 0) return UPR_ERR_ARG;
@@ -2507,6 +2511,17 @@ int upr_t_conv_mfma16(const float* x, int B, int H, int W, int Cin, int x_cs, in
   c.B = B; c.Ho = Ho; c.Wo = Wo; c.N = N; c.Kpad = kh * kw * Cin;
   c.W = wp16; c.bias = bias; c.relu = relu;
   c.store = store == 1 ? kStoreConvT2x2 : kStoreNHWC;
+  if (s2dg) {
+    c.Ho = 2 * H; c.Wo = 2 * W;
+    c.out32 = y; c.out32_cs = y_cs; c.out32_coff = y_coff;
+    c.res32 = res; c.res32_cs = res_cs;
+    if (want16) { c.out32_h16 = y16; c.out32_h16_cs = ycs16; }
+    c.skip32 = only16 ? 1 : 0;
+    const int rc = launch_conv_s2dg(c, st);
+    if (rc == kErrUnsupported) return UPR_ERR_UNSUPPORTED;
+    if (rc != 0) return rc;
+    LAUNCH_CHECK();
+  }
   {
     // the fp32 output (+ fp32 residual / accumulated gradient) straight from the conv epilogue
     ConvOp c32 = c;

@@ -195,6 +195,64 @@ __global__ __launch_bounds__(256) void small_fwd_kernel(SV x, int B, int H, int 
 }
 
 // ---------------------------------------------------------------------------
+// forward, 1x1 heads of <= 4 outputs over 16 / 32 / 64 channel-contiguous
+// inputs (32 -> 3 / 32 -> 1 at 512^2: models/model.py:335, 440).  The
+// one-pixel-per-thread kernel above has each lane walk its own 128-byte pixel
+// (0.25 ms, 1 TB/s); here a wave reads 64 pixels as consecutive 16-byte
+// chunks (lane = (pixel, channel quad), LPP = Cin / 4 lanes per pixel), each
+// lane forms the quad's partial dot products and the LPP lanes of a pixel sum
+// them with xor shuffles.
+// ---------------------------------------------------------------------------
+template <int COUT, int LPP>
+__global__ __launch_bounds__(256) void head1x1_kernel(SV x, int P, int Ho, int Wo, const float* __restrict__ w,
+                                                      const float* __restrict__ bias, SV y, int relu, int accum) {
+  const int lane = threadIdx.x & 63;
+  const long long gw = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int q = lane % LPP;
+  constexpr int CIN = LPP * 4;
+  float wv[4][COUT];
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int c = 0; c < COUT; ++c) wv[e][c] = w[c * CIN + q * 4 + e];
+#pragma unroll
+  for (int j = 0; j < LPP; ++j) {
+    const long long pix = gw * 64 + (j * 64 + lane) / LPP;
+    const bool in = pix < P;
+    int b = 0, oy = 0, ox = 0;
+    f32x4_t2 v = f32x4_t2{0.f, 0.f, 0.f, 0.f};
+    if (in) {
+      ox = (int)(pix % Wo);
+      const long long r = pix / Wo;
+      oy = (int)(r % Ho);
+      b = (int)(r / Ho);
+      v = *(const f32x4_t2*)(x.d + x.at(b, oy, ox, q * 4));
+    }
+    float part[COUT];
+#pragma unroll
+    for (int c = 0; c < COUT; ++c) {
+      part[c] = v[0] * wv[0][c];
+#pragma unroll
+      for (int e = 1; e < 4; ++e) part[c] = fmaf(v[e], wv[e][c], part[c]);
+    }
+#pragma unroll
+    for (int off = LPP / 2; off >= 1; off >>= 1)
+#pragma unroll
+      for (int c = 0; c < COUT; ++c) part[c] += __shfl_xor(part[c], off);
+    if (in && q == 0) {
+      float* yp = y.d + y.at(b, oy, ox, 0);
+#pragma unroll
+      for (int c = 0; c < COUT; ++c) {
+        float o = part[c] + (bias ? bias[c] : 0.f);
+        if (accum) o += yp[c * y.sc];
+        if (relu) o = fmaxf(o, 0.f);
+        yp[c * y.sc] = o;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // input gradient, stride 1: dx[b,iy,ix,ci] (+)= sum_{ky,kx,co} dy[b,iy+p-ky*d,ix+p-kx*d,co] w[co][ci][ky][kx]
 // ---------------------------------------------------------------------------
 template <int CIN, int COUTT>
@@ -506,6 +564,23 @@ int small_conv_fwd(const UprView* xv, int B, int H, int W, int Cin, const float*
     if (lds > 48 * 1024) return kErrUnsupported;
     const SV x = mksv(xv), y = mksv(yv);
     const int xvec = x.sc == 1 && x.sw % 4 == 0 && x.sh % 4 == 0 && x.sb % 4 == 0 && (uintptr_t)x.d % 16 == 0;
+    if (xvec && kh == 1 && kw == 1 && stride == 1 && pad == 0 && (Cin == 16 || Cin == 32 || Cin == 64)) {
+      const int P = B * Ho * Wo;
+      const int hgrid = (P + 255) / 256;
+#define UPR_HEAD(C, L) \
+  hipLaunchKernelGGL((head1x1_kernel<C, L>), dim3(hgrid), dim3(256), 0, st, x, P, Ho, Wo, w, bias, y, relu, accumulate)
+#define UPR_HEAD_C(L)            \
+  switch (Cout) {                \
+    case 1: UPR_HEAD(1, L); break; \
+    case 2: UPR_HEAD(2, L); break; \
+    case 3: UPR_HEAD(3, L); break; \
+    default: UPR_HEAD(4, L); break; \
+  }
+      if (Cin == 16) { UPR_HEAD_C(4) } else if (Cin == 32) { UPR_HEAD_C(8) } else { UPR_HEAD_C(16) }
+#undef UPR_HEAD_C
+#undef UPR_HEAD
+      return (int)hipGetLastError();
+    }
     const int grid = (B * Ho * Wo + 255) / 256;
 #define UPR_SMALL_FWD(C)                                                                                         \
   hipLaunchKernelGGL(small_fwd_kernel<C>, dim3(grid), dim3(256), lds, st, x, B, H, W, Cin, w, bias, kh, kw, stride, \

@@ -499,6 +499,331 @@ static int wgrad16_nr(const Wg16Args& a, float* dwp, hipStream_t st, int torch_c
   return launch_wgrad16<BM, 1>(a, dwp, st, torch_ci);
 }
 
+// ---------------------------------------------------------------------------
+// Halo-tile AMP weight gradient for stride-1 3x3 convs (pad = dilation) over
+// 32 / 64 channels -- the 512^2 decoder / FAM / head convs of the training
+// step (models/model.py:49, 98-102, 413-425).  wgrad16_kernel above stages
+// im2col(x): every input pixel crosses LDS nine times, 36 KiB per 64-pixel
+// step, and with one step of prefetch the step time was the DMA round trip
+// (0.25 ms per 32 -> 32 conv at bs 8, 150 TF/s).  Here a block walks TR = 4 *
+// RPW output rows of one 64-pixel column segment per step and stages
+//   * the input rows those rows' taps touch, 64 + 2d pixels each (halo
+//     included, zero outside the image) -- NTAP 9: TR + 2d rows, every tap
+//     read from them by a shifted LDS address; NTAP 3 (one kernel row ky per
+//     block, for 64-channel shapes whose nine-tap tile would not fit the
+//     registers -- measured no faster than the im2col kernel, not routed): TR
+//     rows; NTAP 1: the 1x1 convs (no halo);
+//   * dy of the TR rows (fp32 -> fp16 through registers, or the fp16 copy),
+// double-buffered with one barrier per step.  The MFMA tiles are those of
+// wgrad16_kernel (dy rows x input columns, both read pixel-contiguous with
+// ds_read_b64_tr_b16, rows XOR-swizzled by w16_swz -- conflict-free for any
+// uniform pixel shift of all lanes, so the tap shifts keep it).  Each wave
+// owns RPW output rows of the step and the whole (co, k) tile of the block's
+// taps; the four waves' tiles are summed through LDS at the end and the sum
+// goes to the split's slab as in wgrad16_kernel (splits = (image, row block,
+// segment); the tap groups of one split fill disjoint k ranges of its slab
+// row), reduced in order.  Same-box timings, bs 8 (tools/wgrad_bench.py):
+// 32 -> 32 at 512^2 0.192 -> 0.105 ms with dy's fp16 copy (0.203 -> 0.165 from
+// fp32 dy), dilation 2 0.198 -> 0.135, 1x1 96 -> 32 0.234 -> 0.144.
+// ---------------------------------------------------------------------------
+struct Wg16hArgs {
+  const half_t* x16;  // [B][H][W][CIN] fp16
+  int B, H, W;        // = Ho, Wo
+  const float* dy;
+  const half_t* dy16;  // nullable compact [pixel][COUT] fp16 copy
+  int dy_cs, dy_coff;
+  int steps_per_col;   // H / TR
+  int spb;             // steps per block
+  int nrb, segs, ntg;  // row blocks per image column, 64-pixel segments per row, tap groups
+  int ldn;             // taps * CIN
+  float* slab;
+};
+
+// D: dilation (= pad) of the 3x3 forms, 0 for the 1x1 form.  Input rows are
+// CINP channels wide in LDS (CIN rounded up to a power of two, so the XOR
+// swizzle of w16_swz stays inside the row; the pad chunks are never read).
+template <int CIN, int COUT, int NTAP, int RPW, int D>
+struct Wg16hCfg {
+  static constexpr int TR = 4 * RPW;
+  static constexpr int CINP = CIN == 96 ? 128 : CIN;
+  static constexpr int CINB = CINP * 2, COUTB = COUT * 2;
+  static constexpr int MT = COUT / 16, KTC = CIN / 16, NKT = NTAP * KTC;
+  static constexpr int AQ = TR * 64 * COUT / 4 / 256;  // dy quads per thread per step
+  static constexpr int PXR = 64 + 2 * D;                // pixels per staged input row
+  static constexpr int IR = NTAP == 9 ? TR + 2 * D : TR;
+  static constexpr int IN_BYTES = IR * PXR * CINB;
+  static constexpr int STAGE = IN_BYTES + TR * 64 * COUTB;
+  static constexpr int LDS = 2 * STAGE;
+  static constexpr int TAPS = NTAP == 1 ? 1 : 9;
+  // cross-wave reduction of the tile: 2 waves x MT x NKT x 1 KiB per stage, in NPASS k-slices
+  static constexpr int RED = 2 * MT * NKT * 1024;
+  static constexpr int NPASS = RED <= STAGE ? 1 : RED <= 2 * STAGE && NKT % 2 == 0 ? 2 : 3;
+  static_assert(NKT % NPASS == 0 && RED / NPASS <= STAGE, "reduction passes");
+};
+
+template <int CIN, int COUT, int NTAP, int RPW, int D, bool A16>
+__global__ __launch_bounds__(256) void wgrad16h_kernel(Wg16hArgs a) {
+  using C = Wg16hCfg<CIN, COUT, NTAP, RPW, D>;
+  constexpr int TR = C::TR, CINP = C::CINP, CINB = C::CINB, COUTB = C::COUTB, MT = C::MT, KTC = C::KTC,
+                NKT = C::NKT, AQ = C::AQ, PXR = C::PXR, IR = C::IR, IN_BYTES = C::IN_BYTES, STAGE = C::STAGE;
+  // the two stages are separate LDS objects: hipcc then knows that the DMA into one
+  // and the fragment reads of the other do not alias, and does not drain the DMA
+  // (vmcnt(0)) before every read (it did with one carved buffer)
+  __shared__ __attribute__((aligned(16))) unsigned char stg0[STAGE];
+  __shared__ __attribute__((aligned(16))) unsigned char stg1[STAGE];
+  auto stage = [&](auto STG_) -> unsigned char* {
+    if constexpr (decltype(STG_)::value == 0) return stg0;
+    else return stg1;
+  };
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int bid = blockIdx.x;
+  const int tg = bid % a.ntg;
+  const int split = bid / a.ntg;
+  const int seg = split % a.segs;
+  const int rest = split / a.segs;
+  const int rb = rest % a.nrb, b = rest / a.nrb;
+  const int s0 = rb * a.spb, s1 = min(a.steps_per_col, s0 + a.spb);
+  const int ox0 = seg * 64;
+  // input row 0 of a stage: NTAP 9 -> oy0 - D (every kernel row); NTAP 3 -> oy0 + (tg - 1) D;
+  // NTAP 1 (1x1) -> oy0
+  const int iy_off = NTAP == 9 ? -D : NTAP == 3 ? (tg - 1) * D : 0;
+  const half_t* zero16 = (const half_t*)g_wg_zero;
+
+  // input rows of step s -> stage STG: 16-byte slot q of the stage (LDS-linear per
+  // wave-instruction) = pixel row R = q / (CINP/8), slot q % (CINP/8), which holds
+  // data chunk slot ^ (w16_swz(R) / 2) (pad chunks >= CIN/8: not loaded)
+  constexpr int NQ_IN = IR * PXR * (CINP / 8);
+  auto issue_in = [&](int s, auto STG_) {
+    const int iy0 = s * TR + iy_off;
+#pragma unroll 4
+    for (int q0 = 0; q0 < NQ_IN; q0 += 256) {
+      const int q = q0 + tid;
+      const int R = q / (CINP / 8), sl = q - R * (CINP / 8);
+      const int c16 = sl ^ (w16_swz<CINP / 4>(R) >> 1);
+      if (q < NQ_IN && (CINP == CIN || c16 < CIN / 8)) {
+        const int r = R / PXR, px = R - r * PXR;
+        const int iy = iy0 + r, ix = ox0 - D + px;
+        const half_t* src = zero16;
+        if ((unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
+          src = a.x16 + ((size_t)(b * a.H + iy) * a.W + ix) * CIN + c16 * 8;
+        wg_glds16(src, stage(STG_) + (q0 + wave * 64) * 16);
+      }
+    }
+  };
+  // dy of step s -> registers (quad i of this thread: q = i * 256 + tid -> pixel q / (COUT/4), quad q % (COUT/4))
+  // A16: dy's fp16 copy is read (a compile-time choice: a runtime one put each load in
+  // its own branch, and hipcc waited for every load at the join)
+  f32x4_w2 areg[A16 ? 1 : AQ];
+  f16x4_w2 hreg[A16 ? AQ : 1];
+  auto load_dy = [&](int s) {
+    const size_t pix0 = (size_t)(b * a.H + s * TR) * a.W + ox0;
+#pragma unroll
+    for (int i = 0; i < AQ; ++i) {
+      const int q = i * 256 + tid;
+      const int R = q / (COUT / 4), cq = q - R * (COUT / 4);
+      const size_t pix = pix0 + (size_t)(R >> 6) * a.W + (R & 63);
+      if constexpr (A16)
+        hreg[i] = *(const f16x4_w2*)(a.dy16 + pix * COUT + cq * 4);
+      else
+        areg[i] = *(const f32x4_w2*)(a.dy + pix * a.dy_cs + a.dy_coff + cq * 4);
+    }
+  };
+  auto store_dy = [&](auto STG_) {
+    unsigned char* As = stage(STG_) + IN_BYTES;
+#pragma unroll
+    for (int i = 0; i < AQ; ++i) {
+      const int q = i * 256 + tid;
+      const int R = q / (COUT / 4), cq = q - R * (COUT / 4);
+      f16x4_w2 h;
+      if constexpr (A16) {
+        h = hreg[i];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) h[e] = (half_t)areg[i][e];
+      }
+      *(f16x4_w2*)(As + R * COUTB + ((cq ^ w16_swz<COUT / 4>(R)) * 8)) = h;
+    }
+  };
+
+  f32x4_w2 acc[MT][NKT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int k = 0; k < NKT; ++k) acc[m][k] = f32x4_w2{0.f, 0.f, 0.f, 0.f};
+  const int fg = lane >> 4, l16 = lane & 15, tq = l16 >> 2, tp = l16 & 3;
+
+  auto compute = [&](auto STG_) {
+    // the lane's pixel term, opaque per step: hoisted, the ~150 tap / row /
+    // swizzle addresses of a step stayed live across the loop and spilled
+    int fgq = fg * 8 + tq;
+    asm volatile("" : "+v"(fgq));
+    const unsigned char* Bs = stage(STG_);
+    const unsigned char* As = Bs + IN_BYTES;
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr) {
+      const int lr = wave * RPW + rr;  // local output row
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int p = ks * 32 + fgq;  // this lane's pixel of the lo read (hi: + 4)
+        f16x8_w2 af[MT];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          const int r0 = lr * 64 + p, r1 = r0 + 4;
+          const f16x4_w2 lo = w16_tr(As + r0 * COUTB + (((m * 4 + tp) ^ w16_swz<COUT / 4>(r0)) * 8));
+          const f16x4_w2 hi = w16_tr(As + r1 * COUTB + (((m * 4 + tp) ^ w16_swz<COUT / 4>(r1)) * 8));
+          af[m] = f16x8_w2{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+#pragma unroll
+        for (int t = 0; t < NTAP; ++t) {
+          const int ky = NTAP == 9 ? t / 3 : 0, kx = NTAP == 1 ? 0 : t % 3;
+          const int r0 = (lr + ky * D) * PXR + p + kx * D, r1 = r0 + 4;
+#pragma unroll
+          for (int c = 0; c < KTC; ++c) {
+            const f16x4_w2 lo = w16_tr(Bs + r0 * CINB + (((c * 4 + tp) ^ w16_swz<CINP / 4>(r0)) * 8));
+            const f16x4_w2 hi = w16_tr(Bs + r1 * CINB + (((c * 4 + tp) ^ w16_swz<CINP / 4>(r1)) * 8));
+            const f16x8_w2 bf = f16x8_w2{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+            for (int m = 0; m < MT; ++m)
+              acc[m][t * KTC + c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[m], bf, acc[m][t * KTC + c], 0, 0, 0);
+          }
+        }
+      }
+    }
+  };
+
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  // step s from stage CUR; the next step's rows / dy go to the other stage (last read by
+  // step s - 1, before the barrier that ended it).  Stages are compile-time in the
+  // unrolled pair, so hipcc sees that the DMA and the fragment reads touch disjoint LDS.
+  auto step = [&](int s, auto CUR_) {
+    constexpr int CUR = decltype(CUR_)::value;
+    using NXT = std::integral_constant<int, CUR ^ 1>;
+    const bool more = s + 1 < s1;  // uniform
+    if (more) {
+      issue_in(s + 1, NXT{});
+      load_dy(s + 1);
+    }
+    compute(CUR_);
+    if (more) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      store_dy(NXT{});
+    }
+    __syncthreads();
+  };
+  if (s0 < s1) {
+    issue_in(s0, S0{});
+    load_dy(s0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    store_dy(S0{});
+    __syncthreads();
+  }
+  for (int s = s0; s < s1; s += 2) {
+    step(s, S0{});
+    if (s + 1 < s1) step(s + 1, S1{});
+  }
+  // every wave holds a partial of the whole (co, k) tile (its own output rows):
+  // the four are summed through LDS (the stages are free after the loop's last
+  // barrier), NPASS k-slices at a time, and the sum goes to the split's slab --
+  // D[row = fg*4 + i][col = l16] of tile (m, k-tile) -- one 16-byte LDS chunk
+  // per (wave, m, k-tile, lane), stored by consecutive threads as consecutive columns
+  constexpr int NPASS = C::NPASS, NKP = NKT / NPASS;
+  constexpr int WSTRIDE = MT * NKP * 64;  // f32x4 chunks per wave per pass
+  // waves 0, 1 park in stage 0, waves 2, 3 in stage 1
+  f32x4_w2* red0 = (f32x4_w2*)stg0;
+  f32x4_w2* red1 = (f32x4_w2*)stg1;
+  float* sl = a.slab + (size_t)split * COUT * a.ldn + (size_t)tg * NTAP * CIN;
+#pragma unroll
+  for (int ps = 0; ps < NPASS; ++ps) {
+    if (ps) __syncthreads();  // the previous pass's sums are read
+    f32x4_w2* mine = (wave < 2 ? red0 : red1) + (wave & 1) * WSTRIDE;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int k = 0; k < NKP; ++k) mine[(m * NKP + k) * 64 + lane] = acc[m][ps * NKP + k];
+    __syncthreads();
+    for (int c = tid; c < WSTRIDE; c += 256) {
+      const f32x4_w2 v = red0[c] + red0[WSTRIDE + c] + red1[c] + red1[WSTRIDE + c];
+      const int ln = c & 63, mk = c >> 6, m = mk / NKP, k = ps * NKP + mk % NKP;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sl[(size_t)(m * 16 + (ln >> 4) * 4 + i) * a.ldn + k * 16 + (ln & 15)] = v[i];
+    }
+  }
+}
+
+template <int CIN, int COUT, int NTAP, int RPW, int D>
+static int launch_wgrad16h(Wg16hArgs a, float* dwp, hipStream_t st, int torch_ci) {
+  using C = Wg16hCfg<CIN, COUT, NTAP, RPW, D>;
+  static_assert(C::LDS <= 160 * 1024, "LDS");
+  if (a.H % C::TR) return kErrUnsupported;
+  a.ntg = C::TAPS / NTAP;
+  a.segs = a.W / 64;
+  a.steps_per_col = a.H / C::TR;
+  a.ldn = C::TAPS * CIN;
+  // ~512 blocks (one per CU at a time, two rounds), >= 2 steps each
+  const long long cols = (long long)a.B * a.segs * a.ntg;
+  int nrb = (int)((512 + cols - 1) / cols);
+  const int max_nrb = (a.steps_per_col + 1) / 2;
+  if (nrb > max_nrb) nrb = max_nrb;
+  if (nrb < 1) nrb = 1;
+  a.spb = (a.steps_per_col + nrb - 1) / nrb;
+  a.nrb = (a.steps_per_col + a.spb - 1) / a.spb;
+  const int splits = a.B * a.nrb * a.segs;
+  const int groups = splits > WG_GROUP ? (splits + WG_GROUP - 1) / WG_GROUP : 0;
+  const size_t slab_elems = (size_t)COUT * a.ldn;
+  void* buf = scratch(kSlotSlab, (size_t)(splits + groups) * slab_elems * sizeof(float), st);
+  if (!buf) return (int)hipErrorOutOfMemory;
+  a.slab = (float*)buf;
+  if (a.dy16)
+    hipLaunchKernelGGL((wgrad16h_kernel<CIN, COUT, NTAP, RPW, D, true>), dim3(splits * a.ntg), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((wgrad16h_kernel<CIN, COUT, NTAP, RPW, D, false>), dim3(splits * a.ntg), dim3(256), 0, st, a);
+  const int KT = C::TAPS * CIN;
+  const int n4 = COUT * KT / 4;
+  const int g1 = (n4 + 255) / 256 < 1024 ? (n4 + 255) / 256 : 1024;
+  const float* part = a.slab;
+  int nparts = splits;
+  if (groups) {
+    float* out = a.slab + (size_t)splits * slab_elems;
+    hipLaunchKernelGGL(wgrad_group_kernel, dim3(g1, groups), dim3(256), 0, st, (const float*)a.slab, splits, COUT, KT,
+                       a.ldn, out);
+    part = out;
+    nparts = groups;
+  }
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(g1), dim3(256), 0, st, part, nparts, COUT, KT, a.ldn, dwp, torch_ci);
+  return (int)hipGetLastError();
+}
+
+// 32 -> 32 only: the one-kernel-row forms of 64 -> 32 / 32 -> 64 / 64 -> 64 measured
+// even / slower than the im2col kernel (bs 8: 0.333 vs 0.337, 0.370 vs 0.235, 0.476
+// vs 0.132 ms -- the 64-channel tiles spill), so those shapes stay there
+template <int D>
+static int wgrad16h_d(const Wg16hArgs& a, int Cin, int Cout, float* dwp, hipStream_t st, int torch_ci) {
+  if (Cin == 32 && Cout == 32) return launch_wgrad16h<32, 32, 9, D == 1 ? 2 : 1, D>(a, dwp, st, torch_ci);
+  return kErrUnsupported;
+}
+
+// the halo form's shapes (k 3: pad = dil <= 2; k 1: stride 1, no padding); kErrUnsupported otherwise
+static int wgrad16h(const void* x16, int B, int H, int W, int Cin, const float* dy, int Cout, int dy_cs, int dy_coff,
+                    int k, int dil, float* dwp, hipStream_t st, int torch_ci, const void* dy16) {
+  if (W % 64) return kErrUnsupported;
+  Wg16hArgs a;
+  memset(&a, 0, sizeof(a));
+  a.x16 = (const half_t*)x16; a.B = B; a.H = H; a.W = W;
+  a.dy = dy; a.dy16 = (const half_t*)dy16; a.dy_cs = dy_cs; a.dy_coff = dy_coff;
+  if (k == 1) {
+    // the multi-scale head fusion 96 -> 32 and the EnhancedFAM fusion 128 -> 32 (model.py:49, 413-414)
+    if (Cin == 96 && Cout == 32) return launch_wgrad16h<96, 32, 1, 1, 0>(a, dwp, st, torch_ci);
+    if (Cin == 128 && Cout == 32) return launch_wgrad16h<128, 32, 1, 1, 0>(a, dwp, st, torch_ci);
+    return kErrUnsupported;
+  }
+  if (k != 3) return kErrUnsupported;
+  if (dil == 1) return wgrad16h_d<1>(a, Cin, Cout, dwp, st, torch_ci);
+  if (dil == 2) return wgrad16h_d<2>(a, Cin, Cout, dwp, st, torch_ci);
+  return kErrUnsupported;
+}
+
 // AMP entry (upr_t_conv_wgrad16): x16 = the compact fp16 copy of x ([B][H][W][Cin]);
 // kErrUnsupported when the shape does not fit (the caller falls back to fp32)
 int wgrad16_gemm(const void* x16, int B, int H, int W, int Cin, const float* dy, int Ho, int Wo, int Cout, int dy_cs,
@@ -518,6 +843,11 @@ int wgrad16_gemm(const void* x16, int B, int H, int W, int Cin, const float* dy,
   a.KT = kh * kw * Cin;
   a.nruns = a.KT / 32;
   a.units = (int)(P / W16_KP);
+  if (((kh == 3 && kw == 3 && pad == dil) || (kh == 1 && kw == 1 && pad == 0)) && stride == 1 && Ho == H &&
+      Wo == W) {
+    const int rc = wgrad16h(x16, B, H, W, Cin, dy, Cout, dy_cs, dy_coff, kh, dil, dwp, st, torch_ci, a.dy16);
+    if (rc != kErrUnsupported) return rc;
+  }
   if (Cout % 128 == 0) return wgrad16_nr<128>(a, dwp, st, torch_ci);
   if (Cout % 64 == 0) return wgrad16_nr<64>(a, dwp, st, torch_ci);
   return wgrad16_nr<32>(a, dwp, st, torch_ci);

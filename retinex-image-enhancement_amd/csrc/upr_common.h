@@ -117,6 +117,9 @@ struct ConvOp {
 // fp16 convs with an fp32 output (ConvOp::out32): the wide-tile and row-ring
 // kernels; kErrUnsupported when neither takes the op
 int launch_conv_out32(const ConvOp& op, hipStream_t stream);
+// the input gradient of a 3x3 stride-2 pad-1 conv straight from dy (conv_pw.hip;
+// op = the stride-1 dgrad op over dy with the flipped filter, output 2H x 2W)
+int launch_conv_s2dg(const ConvOp& op, hipStream_t stream);
 
 int launch_conv(const ConvOp& op, int dtype, hipStream_t stream);
 

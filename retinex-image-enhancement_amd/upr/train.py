@@ -434,6 +434,30 @@ class Conv:
         gx.t16, gx.t16_grad = None, False  # gx changed: any fp16 copy of it is stale
         return True
 
+    def _dgrad_s2_3x3(self, gy, src16, B, Ho, Wo, gx, acc, o16):
+        """Input gradient of a 3x3 stride-2 pad-1 conv (enc1.conv1, model.py:100-178)
+        straight from dy: the four output phases as small convs over dy (upr_t_conv_mfma16
+        store | 16), no zero-upsampled operand.  False when the kernel does not take
+        the shape (the caller then zero-upsamples)."""
+        if gy.stale32 and src16 is None:
+            return False
+        lib, dev = L.lib(), gy.t.device
+        ready = src16 is not None
+        x16 = src16 if ready else _h16(B * Ho * Wo * self.Cout, dev)
+        keep = bool(o16) and not acc
+        y16 = _h16(B * 4 * Ho * Wo * self.Cin, dev)
+        rc = lib.upr_t_conv_mfma16(None if ready else _fp(gy.t, 0), B, Ho, Wo, self.Cout, gy.cs, gy.coff,
+                                   _p(self.wt16), None, self.Cin, 3, 3, 1, 1, 1, gx.ptr() if acc else None,
+                                   gx.cs if acc else 0, 0, _fp(gx.t), gx.cs, gx.coff, 16 | (6 if keep else 0),
+                                   _p(x16), int(ready), _p(y16), 0, _stream())
+        if rc == L.UPR_ERR_UNSUPPORTED:
+            return False
+        _chk(rc, "conv_dgrad_s2_3x3")
+        gx.t16 = y16 if keep else None
+        gx.stale32 = keep
+        gx.t16_grad = keep
+        return True
+
     def bwd(self, x, gy, gx=None, x_view=None, mask=None, gx_only16=False):
         """gy: Act gradient of this conv's output (pre-activation).
         Accumulates the weight / bias gradients; gx (Act, nullable) receives
@@ -510,6 +534,11 @@ class Conv:
                 src16 = gy.t16 if self.amp and gy.t16_grad and gy.coff == 0 and gy.cs == gy.C == self.Cout else None
                 if self.s == 2 and self.amp and acc and (self.kh, self.kw, self.p, self.d) == (1, 1, 0, 1) and \
                         H == 2 * Ho and W == 2 * Wo and self._dgrad_s2_1x1(gy, src16, B, Ho, Wo, gx):
+                    return
+                if self.s == 2 and self.amp and (self.kh, self.kw, self.p, self.d) == (3, 3, 1, 1) and \
+                        H == 2 * Ho and W == 2 * Wo and \
+                        self._dgrad_s2_3x3(gy, src16, B, Ho, Wo, gx, acc,
+                                           bool(gx_only16) and gx.coff == 0 and gx.cs == gx.C == self.Cin):
                     return
                 if self.s != 1:
                     assert self.s == 2 and H == 2 * Ho and W == 2 * Wo, "stride-2 dgrad needs even sizes"

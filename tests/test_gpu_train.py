@@ -44,7 +44,8 @@ def _act(t_nhwc):
     (32, 32, 3, 1, 2, 2, True),     # FAM branch4_conv2 (dilation 2)
     (256, 256, 3, 1, 6, 6, False),  # ASPP d6
     (3, 32, 3, 1, 1, 1, True),      # input layer (direct)
-    (32, 3, 1, 1, 0, 1, True),      # output layer (direct)
+    (32, 3, 1, 1, 0, 1, True),      # output layer (direct; coalesced 1x1 head kernel)
+    (64, 1, 1, 1, 0, 1, True),      # 1x1 head, 64 channels -> 1
     (2, 1, 7, 1, 3, 1, True),       # spatial attention (direct)
 ])
 def test_conv_layer(cin, cout, k, s, p, d, bias):
@@ -85,6 +86,11 @@ def test_conv_layer(cin, cout, k, s, p, d, bias):
     (2, 32, 64, 128, 128, 1, 2, 0, 1),   # projecting shortcut 1x1 s2: BM 64, 1 run
     (1, 32, 32, 64, 64, 3, 1, 2, 2),     # FAM branch4_conv2 (dilation 2)
     (2, 64, 64, 64, 64, 3, 1, 1, 1),     # BM 64, 9 runs x 2 tiles
+    (2, 64, 32, 32, 128, 3, 1, 1, 1),    # halo form 64 -> 32 (one kernel row per block)
+    (1, 32, 64, 16, 64, 3, 1, 3, 3),     # halo form 32 -> 64, dilation 3
+    (1, 32, 32, 20, 64, 3, 1, 1, 1),     # H % 8 != 0: the im2col form
+    (2, 96, 32, 16, 64, 1, 1, 0, 1),     # 1x1 streaming form: multi-scale head fusion 96 -> 32
+    (1, 128, 32, 8, 128, 1, 1, 0, 1),    # 1x1 streaming form: FAM fusion 128 -> 32
     (1, 32, 32, 24, 24, 3, 1, 1, 1),     # Wo % 64 != 0: the fp32 path
 ])
 def test_conv_wgrad16_vs_fp64(B, cin, cout, H, W, k, s, p, d):
@@ -479,6 +485,44 @@ def test_dgrad_1x1_stride2_scatter(cin, cout):
     # the flag is refused on anything but a 1x1 accumulate
     assert lib.upr_t_conv_mfma16(dyd.data_ptr(), B, Ho, Wo, cout, cout, 0, wt16.data_ptr(), None, cin, 1, 1, 1, 0, 1,
                                  None, 0, 0, gx.data_ptr(), cin, 0, 8, x16.data_ptr(), 0, y16.data_ptr(), 0, st) != 0
+
+
+@pytest.mark.parametrize("acc,keep16", [(False, False), (True, False), (False, True)])
+def test_dgrad_3x3_stride2_phases(acc, keep16):
+    """enc1.conv1's input gradient (3x3 stride 2 pad 1, 32 -> 64, model.py:100-178)
+    from dy itself (upr_t_conv_mfma16 store | 16: the four output phases as small
+    convs, no zero-upsampled operand) vs torch's conv2d_input on the fp16-rounded
+    operands: overwrite, accumulate into an existing gradient, and the fp16-only
+    form (store | 2 | 4: y16 = (half) dx, dx itself not written)."""
+    from upr import _lib as L
+    gen = torch.Generator().manual_seed(11 + int(acc) + 2 * int(keep16))
+    cin, cout, B, Ho, Wo = 32, 64, 2, 16, 48
+    w = torch.randn(cout, cin, 3, 3, generator=gen) * 0.1
+    dy = torch.randn(B, cout, Ho, Wo, generator=gen)
+    base = torch.randn(B, 2 * Ho, 2 * Wo, cin, generator=gen)
+    g = torch.nn.grad.conv2d_input((B, cin, 2 * Ho, 2 * Wo), w.half().double(), dy.half().double(), stride=2,
+                                   padding=1)
+    g = g.float().half().float().permute(0, 2, 3, 1)
+    ref = base + g if acc else g
+    lib, st = L.lib(), torch.cuda.current_stream().cuda_stream
+    wt = torch.empty(w.numel(), device=DEV)
+    assert lib.upr_t_pack_weight(w.to(DEV).data_ptr(), wt.data_ptr(), cout, cin, 3, 3, 1, st) == 0
+    wt16 = wt.half()
+    dyd = dy.permute(0, 2, 3, 1).contiguous().to(DEV)
+    x16 = torch.empty(B * Ho * Wo * cout, dtype=torch.float16, device=DEV)
+    y16 = torch.zeros(B * 4 * Ho * Wo * cin, dtype=torch.float16, device=DEV)
+    gx = base.to(DEV) if acc else torch.full((B, 2 * Ho, 2 * Wo, cin), 7.0, device=DEV)
+    store = 16 | (6 if keep16 else 0)
+    rc = lib.upr_t_conv_mfma16(dyd.data_ptr(), B, Ho, Wo, cout, cout, 0, wt16.data_ptr(), None, cin, 3, 3, 1, 1, 1,
+                               gx.data_ptr() if acc else None, cin if acc else 0, 0, gx.data_ptr(), cin, 0, store,
+                               x16.data_ptr(), 0, y16.data_ptr(), 0, st)
+    assert rc == 0, rc
+    torch.cuda.synchronize()
+    if keep16:
+        _close(y16.float().view(B, 2 * Ho, 2 * Wo, cin), ref, 2e-3, "3x3 s2 dgrad (fp16 copy)")
+        assert bool((gx == 7.0).all()), "only16: the fp32 output must not be written"
+    else:
+        _close(gx, ref, 1e-3, "3x3 s2 dgrad")
 
 
 def test_fp16_copy_producers():
