@@ -1284,12 +1284,22 @@ __device__ __forceinline__ void hw4_res_load(const ConvOp& op, f16x8_w (&rv0)[WM
 // after the barrier that ends region k - 1's reads, three steps ahead of its
 // first reader) and read by its 3 taps at per-lane column offsets +-d (lanes
 // whose column falls outside the image row read through the void LDS base)
-template <int BN, int W, int NCH, int ABL = 0, bool DS = false, bool DL = false, int TR = 4>
+// NSC = 1: a second K segment after the 3x3 chunks, the projecting shortcut
+// of ResBlock / PreActResBlock (1x1 stride 2 over 64 channels of a 2H x 2W
+// source, kbase 9 * Cin: models/model.py:119-122, 159-162): one more K step
+// whose 4 region rows are the source rows 2(oy0 + r), every other pixel,
+// DMA'd into the ring slots the last chunk frees (the schedule of a next
+// chunk's rows 0-3) and read without a tap shift
+template <int BN, int W, int NCH, int ABL = 0, bool DS = false, bool DL = false, int TR = 4, int NSC = 0>
 __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
   using HC = Halo3Cfg<BN, W, TR>;
   static_assert(TR == 4 || (NCH == 1 && !DL && DS), "2-row tiles: one chunk, direct store");
+  static_assert(NSC == 0 || (NSC == 1 && !DL && TR == 4 && DS), "shortcut segment: 4-row tiles, direct store");
   constexpr int WM = HC::WM, WN = HC::WN, BM = HC::BM, NBS = HC::NBS;
-  constexpr int TOTAL = NCH * 9;
+  constexpr int TOTAL = NCH * 9 + NSC;
+  // (chunk, tap) of K step S; the shortcut step is chunk NCH with the centre column (tap 1: row 0, column 1)
+  constexpr auto step_c = [](int S) -> int { return S < NCH * 9 ? S / 9 : NCH + (S - NCH * 9); };
+  constexpr auto step_t = [](int S) -> int { return S < NCH * 9 ? S % 9 : 1; };
   constexpr int CW = W / HC::WAVES_M;  // columns per wave
   constexpr int FPR = CW / 16;         // fragments per tile row per wave
   static_assert(CW % 16 == 0 && WM == HC::TR * FPR, "column blocks of whole 16-pixel fragments");
@@ -1325,7 +1335,21 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
   const unsigned char* abase =
       (const unsigned char*)((const half_t*)sg.src + sg.coff + ((size_t)img * HW + (size_t)wave * 8) * cs);
   const size_t row_bytes = (size_t)W * cs * 2;
+  // shortcut region row r: source row 2 (oy0 + r), source pixels 2p
+  const ConvSeg& sc = op.seg[NSC ? 1 : 0];
+  const unsigned voff_sc = (unsigned)(((lane >> 3) * 2 * sc.cs + (((lane & 7) ^ halo_swz(rpx)) * 8)) * 2);
+  const unsigned char* scbase =
+      (const unsigned char*)((const half_t*)sc.src + sc.coff +
+                             ((size_t)img * sc.Hin * sc.Win + (size_t)wave * 8 * 2) * sc.cs);
   auto region_row = [&](int cc, int r) {  // cc, r compile-time at every call site
+    if (NSC && cc >= NCH) {
+      unsigned char* dst = smem + ((6 * cc + r) & 7) * HC::ROW + wave * 1024;
+      const size_t srow = (size_t)2 * (oy0 + r) * sc.Win * sc.cs * 2;
+#pragma unroll
+      for (int k = 0; k < HC::RP; ++k)
+        glds16_s(scbase + srow + (size_t)k * 128 * sc.cs * 2, voff_sc, dst + k * 8192);
+      return;
+    }
     const int iy = oy0 - 1 + r;
     const bool in = (unsigned)iy < (unsigned)H;
     unsigned char* dst = smem + ((6 * cc + r) & 7) * HC::ROW + wave * 1024;
@@ -1340,13 +1364,14 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
   // rows 4 / 5 at t 0 / 1, the next chunk's rows 0, 2, 1, 3 at t 2, 3, 4, 6
   constexpr auto rows_at = [](int c, int t) -> int {
     if (TR != 4) return 0;  // 2-row tiles: all 4 region rows in the prologue
-    if (t < 2) return 1;
-    return (t <= 4 || t == 6) && c + 1 < NCH ? 1 : 0;
+    if (t < 2) return c < NCH ? 1 : 0;  // (the shortcut region has no rows 4 / 5)
+    return (t <= 4 || t == 6) && c + 1 < NCH + NSC ? 1 : 0;
   };
   auto issue_rows = [&](int c, int t) {
     if (TR != 4) return;
-    if (t < 2) region_row(c, 4 + t);
-    else if (c + 1 < NCH) {
+    if (t < 2) {
+      if (c < NCH) region_row(c, 4 + t);
+    } else if (c + 1 < NCH + NSC) {
       if (t == 2) region_row(c + 1, 0);
       else if (t == 3) region_row(c + 1, 2);
       else if (t == 4) region_row(c + 1, 1);
@@ -1399,7 +1424,7 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
   // step's rows into a stage nobody reads again (uniform DMA count)
   auto issue_b = [&](int stg, int c, int t) {  // DL: c = region, t = tap column
     unsigned char* Bs = smem + HC::RING + stg * HC::B_BYTES;
-    const int kb = DL ? ((c / NCH) * 3 + t) * Cin + (c % NCH) * WBK : t * Cin + c * WBK;
+    const int kb = DL ? ((c / NCH) * 3 + t) * Cin + (c % NCH) * WBK : c < NCH ? t * Cin + c * WBK : 9 * Cin + (c - NCH) * WBK;
 #pragma unroll
     for (int j = 0; j < HC::BJ; ++j) {
       if constexpr (DS)
@@ -1460,7 +1485,7 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
   };
   auto rd_a = [&](auto S_, auto KK_, auto A_) -> f16x8_w {
     constexpr int S = decltype(S_)::value, KK = decltype(KK_)::value, a = decltype(A_)::value;
-    constexpr int c = S / 9, t = S % 9, ty = t / 3, tx = t % 3;
+    constexpr int c = step_c(S), t = step_t(S), ty = t / 3, tx = t % 3;
     if constexpr (DL) {
       constexpr int h = (S / 3) & 1, dtx = S % 3;
       const int ao = KK ? (aofs_d[dtx][a % FPR] ^ 64) : aofs_d[dtx][a % FPR];
@@ -1539,12 +1564,12 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
         constexpr int S = decltype(S_)::value;
         rd_b(S_, I1{}, b1);
         if constexpr (S + 1 < TOTAL) {
-          constexpr int c = S / 9, t = S % 9;
-          constexpr int n = S + 1, nc = n / 9, nt = n % 9;
+          constexpr int c = step_c(S), t = step_t(S);
+          constexpr int n = S + 1, nc = step_c(n), nt = step_t(n);
           // B DMA of step S + NBS (clamped past the end) into the stage step S read
-          constexpr int bstep = S + NBS;
-          constexpr int bc = DL ? (bstep < TOTAL ? bstep / 3 : NREG - 1) : (bstep / 9 < NCH ? bstep / 9 : NCH - 1);
-          constexpr int bt = DL ? (bstep < TOTAL ? bstep % 3 : 2) : (bstep / 9 < NCH ? bstep % 9 : 8);
+          constexpr int bstep = S + NBS < TOTAL ? S + NBS : TOTAL - 1;
+          constexpr int bc = DL ? (S + NBS < TOTAL ? bstep / 3 : NREG - 1) : step_c(bstep);
+          constexpr int bt = DL ? (S + NBS < TOTAL ? bstep % 3 : 2) : step_t(bstep);
           mm_roll(S_, I1{}, b0, true);
           // RAW: B(S + 1) and the region rows step S + 1 reads have landed: in
           // flight may stay the previous iteration's region rows (issued two
@@ -1610,18 +1635,18 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
   }
 }
 
-template <int BN, int W, int NCH, int ABL = 0, bool DS = false, bool DL = false, int TR = 4>
+template <int BN, int W, int NCH, int ABL = 0, bool DS = false, bool DL = false, int TR = 4, int NSC = 0>
 static int launch_hwide4_k(const ConvOp& op, hipStream_t st) {
   using HC = Halo3Cfg<BN, W, TR>;
   static bool attr_set = false;
   if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute((const void*)conv_hwide4_kernel<BN, W, NCH, ABL, DS, DL, TR>,
+    const hipError_t e = hipFuncSetAttribute((const void*)conv_hwide4_kernel<BN, W, NCH, ABL, DS, DL, TR, NSC>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, HC::LDS);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
   const int grid = (op.B * op.Ho * W / HC::BM) * (op.N / BN);
-  hipLaunchKernelGGL((conv_hwide4_kernel<BN, W, NCH, ABL, DS, DL, TR>), dim3(grid), dim3(512), HC::LDS, st, op);
+  hipLaunchKernelGGL((conv_hwide4_kernel<BN, W, NCH, ABL, DS, DL, TR, NSC>), dim3(grid), dim3(512), HC::LDS, st, op);
   return (int)hipGetLastError();
 }
 
@@ -1675,7 +1700,24 @@ static int launch_hwide34(const ConvOp& op, hipStream_t st) {
 // halo-tiled convs: the ring / three-stage form (hwide4 / hwide3) for W 64 x
 // N 256 and W 128 x N 128, the two-stage halo kernel for W 64 x N 128
 // (measured against the gathered-A kernel: profiles/r2_halo*, r3_hw4_*)
+// the 3x3 segment + projecting-shortcut program hwide4 takes (NSC = 1): enc2.conv2
+// (128 -> 128 at W 128, shortcut over the block's 64-channel input)
+static bool hw4_sc_ok(const ConvOp& op) {
+  if (op.nseg != 2 || op.store != kStoreNHWC) return false;
+  const ConvSeg& s = op.seg[0];
+  const ConvSeg& q = op.seg[1];
+  if (s.kh != 3 || s.kw != 3 || s.stride != 1 || s.pad != 1 || s.dil != 1 || s.pre != kPreNone || s.kbase != 0)
+    return false;
+  if (s.C != 128 || s.Hin != op.Ho || s.Win != op.Wo || op.Wo != 128 || op.N != 128 || (op.Ho * op.Wo) % 512) return false;
+  if (q.kh != 1 || q.kw != 1 || q.stride != 2 || q.pad != 0 || q.pre != kPreNone || q.C != 64 || q.kbase != 9 * s.C)
+    return false;
+  if (q.Hin != 2 * op.Ho || q.Win != 2 * op.Wo || q.cs % 8 || q.coff % 8 || (uintptr_t)q.src % 16) return false;
+  if (op.Kpad != 9 * s.C + 64 || s.cs % 8 || s.coff % 8 || (uintptr_t)s.src % 16) return false;
+  return hw4_ds_ok(op);
+}
+
 static int halo_route(const ConvOp& op, hipStream_t st) {
+  if (hw4_sc_ok(op)) return launch_hwide4_k<128, 128, 2, 0, true, false, 4, 1>(op, st);
   if (op.nseg != 1 || op.store != kStoreNHWC) return kErrUnsupported;
   const ConvSeg& s = op.seg[0];
   // dilated 3x3 over 256 channels at W 64 (the ASPP branches, d = 6 / 12 / 18):

@@ -342,6 +342,7 @@ FULL_CASES = [
     # B, size, pre, aspp, dtype
     (32, 512, False, False, torch.float32),   # configs[1]
     (32, 512, True, True, torch.float16),     # configs[2]
+    (4, 512, False, False, torch.float16),    # plain fp16 (ResBlock enc2.conv2 + shortcut on hwide4)
     (32, 1024, True, True, torch.float32),    # configs[3] per-GPU shard
     (32, 1024, True, True, torch.float16),
 ]
