@@ -195,8 +195,8 @@ def parity_vs_cpu(sd, pre, aspp, x, outs, precision):
 # ----------------------------------------------------------------------------
 # every kernel launch_conv dispatches to (the bench's conv family = the executor's GEMM ops)
 CONV_KERNELS = ("conv_halo_kernel", "conv_igemm_kernel", "conv_wide_kernel", "conv_wide32_kernel",
-                "conv_stream_kernel", "conv_stream_fam_kernel", "conv_ring_kernel", "conv_ring32_kernel",
-                "conv_hwide_kernel", "conv_hwide3_kernel", "conv_hwide4_kernel", "conv_t2_kernel", "conv_t2_f32_kernel")
+                "conv_ring_kernel", "conv_ring32_kernel", "conv_hwide_kernel", "conv_hwide3_kernel",
+                "conv_hwide4_kernel", "conv_t2_kernel", "conv_t2_f32_kernel")
 
 
 def pmc_traffic(precision, variant, batch, size, extra=(), kernels=CONV_KERNELS):
