@@ -327,11 +327,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, RingCfg<MODE, C, NB, FL
   issue(0);
   issue(1);
 
-  float bv[NT][4];
+  f32x4_r bias4[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) bv[nt][i] = op.bias ? op.bias[nt * 16 + fg * 4 + i] : 0.f;
+    for (int i = 0; i < 4; ++i) bias4[nt][i] = op.bias ? op.bias[nt * 16 + fg * 4 + i] : 0.f;
   float hw2[NT][4];
   if constexpr (HEAD) {
 #pragma unroll
@@ -441,10 +441,14 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, RingCfg<MODE, C, NB, FL
 
     // ---- MFMAs: D[n][px] = bias[n] + sum_k W[n][k] * X[px][k] -----------------
     f32x4_r acc[NT][GPW];
+    // plain programs: the bias is the C operand of each tile's first MFMA (no
+    // per-step copies into the accumulators); FAM / DMA-only steps start from it here
+    if (FAM || s < 0) {
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
+      for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-      for (int g = 0; g < GPW; ++g) acc[nt][g] = f32x4_r{bv[nt][0], bv[nt][1], bv[nt][2], bv[nt][3]};
+        for (int g = 0; g < GPW; ++g) acc[nt][g] = bias4[nt];
+    }
     // LDS pipeline per "chunk" (one ring row's fragments): [reads of chunk c+1]
     // [MFMAs of chunk c] [lgkmcnt(0)].  The wait is a real s_waitcnt
     // (__builtin_amdgcn_s_waitcnt, which hipcc's counter pass sees) placed
@@ -499,7 +503,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, RingCfg<MODE, C, NB, FL
                 f16x8_r wf;
                 if constexpr (K::WREG) wf = wr[(r * 3 + sc) * K::KS + ks][nt];
                 else wf = w[sc][nt];
-                acc[nt][g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf, x[sc * GPW + g], acc[nt][g], 0, 0, 0);
+                acc[nt][g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf, x[sc * GPW + g],
+                                                                    c == 0 && sc == 0 ? bias4[nt] : acc[nt][g], 0, 0, 0);
               }
         };
         ld(0, bx[0], bw[0]);
@@ -665,7 +670,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, RingCfg<MODE, C, NB, FL
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             v[i] = acc[nt][g][i];
-            if constexpr (K::RELU) v[i] = fmaxf(v[i], 0.f);
+            if constexpr (K::RELU && RES) v[i] = fmaxf(v[i], 0.f);
           }
           if constexpr (RES) {
             const int k = nt * 2 + (fg >> 1);  // logical 16-byte chunk of this lane's 4 channels
@@ -677,6 +682,17 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, RingCfg<MODE, C, NB, FL
           f16x4_r o;
 #pragma unroll
           for (int i = 0; i < 4; ++i) o[i] = (half_t)v[i];
+          if constexpr (K::RELU && !RES) {
+            // relu after the RNE rounding (the same values: rounding is monotone and
+            // keeps the sign) as a signed 16-bit max per pair: every negative half,
+            // -0 included, becomes +0 -- 2 instructions per 4 channels instead of 8
+            // (inline asm: written as vector code, hipcc split the packed conversions
+            // into per-element ones + permutes to feed an element-wise max)
+            uint2 w = __builtin_bit_cast(uint2, o);
+            asm("v_pk_max_i16 %0, %1, 0" : "=v"(w.x) : "v"(w.x));
+            asm("v_pk_max_i16 %0, %1, 0" : "=v"(w.y) : "v"(w.y));
+            o = __builtin_bit_cast(f16x4_r, w);
+          }
           if constexpr (FAM) {
 #pragma unroll
             for (int i = 0; i < 4; ++i)
