@@ -94,7 +94,15 @@ int upr_t_conv_mfma(const float* x, int B, int H, int W, int Cin, int x_cs, int 
  * shortcut) without the zero-upsampled operand: x is dy at H x W, y (and res,
  * which must be given: y accumulates) is the 2H x 2W gradient, and pixel
  * (b, i, j) of the 1x1 stride-1 product is added at (b, 2i, 2j) only (the
- * other pixels of y are untouched); kh = kw = 1, pad 0, no relu, store 0. */
+ * other pixels of y are untouched); kh = kw = 1, pad 0, no relu, store 0.
+ * store | 16: the input gradient of a 3x3 stride-2 pad-1 conv from dy itself
+ * (x = dy at H x W, wp16 the flipped filter, y = 2H x 2W; the four output
+ * phases as small convs over dy, no zero-upsampled operand): kh = kw = 3,
+ * stride 1, no bias / relu; UPR_ERR_UNSUPPORTED when the kernel does not take
+ * the shape (64 -> 32 channels, W % 16).
+ * store | 32 (with x16_ready): x16 is in x's layout, element (pixel p, channel
+ * c) at x16[p * x_cs + c] (the pointer already at the channel offset): a
+ * channel slice of a concat's fp16 copy is read in place. */
 int upr_t_conv_mfma16(const float* x, int B, int H, int W, int Cin, int x_cs, int x_coff, const void* wp16,
                       const float* bias, int N, int kh, int kw, int stride, int pad, int dil, const float* res,
                       int res_cs, int relu, float* y, int y_cs, int y_coff, int store, void* x16, int x16_ready,
@@ -130,8 +138,10 @@ int upr_t_conv_mfma16_relu_bwd(const void* x16, int B, int H, int W, int Cin, co
  * += (no packed buffer, zero fill or unpack pass).  x16 non-NULL: the AMP
  * arithmetic of upr_t_conv_wgrad16 (x may then be NULL when the fp16 path
  * takes the shape); else the fp32 upr_t_conv_wgrad.  dy16 (nullable, AMP
- * only): dy's compact [pixel][Cout] fp16 copy = (half)dy, read instead of dy
- * (the same operand values, half the bytes).  dw needs no alignment. */
+ * only): dy's fp16 copy = (half)dy in dy's own layout (element (pixel p,
+ * channel c) at dy16[p * dy_cs + dy_coff + c]: a channel slice of a concat's
+ * gradient reads the concat's copy), read instead of dy (the same operand
+ * values, half the bytes).  dw needs no alignment. */
 int upr_t_conv_wgrad_into(const float* x, const void* x16, int B, int H, int W, int Cin, int x_cs, int x_coff,
                           const float* dy, const void* dy16, int Ho, int Wo, int Cout, int dy_cs, int dy_coff, int kh,
                           int kw, int stride, int pad, int dil, float* dw, void* stream);
@@ -226,6 +236,9 @@ int upr_t_bn_bwd_fused16(const float* g, const void* g16, int g_cs, int g_coff, 
  * out[c] (+)= sum over m (two-stage, ws = upr_t_reduce_acc_doubles(C)
  * doubles). */
 int upr_t_chan_sum16(const void* g16, int M, int C, float* out, int accumulate, double* ws, void* stream);
+/* upr_t_chan_sum16 over a channel slice of a wider fp16 copy: g16 points at the
+ * slice's first channel, cs is the copy's channel stride. */
+int upr_t_chan_sum16s(const void* g16, int M, int C, int cs, float* out, int accumulate, double* ws, void* stream);
 /* upr_t_zero_upsample16 from the gradient's compact fp16 copy dy16. */
 int upr_t_zero_upsample16h(const void* dy16, int B, int Ho, int Wo, int C, void* z16, void* stream);
 /* upr_t_zero_upsample with an fp16 result z16 [B,2Ho,2Wo,C] (dy rounded to

@@ -2482,7 +2482,10 @@ int upr_t_conv_mfma16(const float* x, int B, int H, int W, int Cin, int x_cs, in
   // the 3x3 stride-2 pad-1 conv's input gradient from dy itself (x16 = dy over H x W, wp16 the
   // flipped filter, y = 2H x 2W); UPR_ERR_UNSUPPORTED when the kernel does not take the shape
   const bool s2dg = (store & 16) != 0;
+  // the ready x16 keeps x's channel stride (a slice of a concat's fp16 copy)
+  const bool x16_strided = (store & 32) != 0;
   store &= 1;
+  if (x16_strided && (!x16_ready || x_cs % 8 || x_cs < Cin || (uintptr_t)x16 % 16)) return UPR_ERR_ARG;
   if (s2 && (kh != 1 || kw != 1 || stride != 1 || pad != 0 || dil != 1 || store != 0 || !res || relu)) return UPR_ERR_ARG;
   if (s2dg && (s2 || kh != 3 || kw != 3 || stride != 1 || dil != 1 || store != 0 || relu || bias)) return UPR_ERR_ARG;
   const int ycs16 = y16_cs > 0 ? y16_cs : (store == 1 ? N / 4 : N);  // y16's channel stride
@@ -2506,7 +2509,7 @@ int upr_t_conv_mfma16(const float* x, int B, int H, int W, int Cin, int x_cs, in
   memset(&c, 0, sizeof(c));
   c.nseg = 1;
   ConvSeg& s = c.seg[0];
-  s.src = x16; s.C = Cin; s.cs = Cin; s.coff = 0; s.Hin = H; s.Win = W;
+  s.src = x16; s.C = Cin; s.cs = x16_strided ? x_cs : Cin; s.coff = 0; s.Hin = H; s.Win = W;
   s.kh = kh; s.kw = kw; s.stride = stride; s.pad = pad; s.dil = dil; s.pre = kPreNone; s.kbase = 0;
   c.B = B; c.Ho = Ho; c.Wo = Wo; c.N = N; c.Kpad = kh * kw * Cin;
   c.W = wp16; c.bias = bias; c.relu = relu;
@@ -2891,6 +2894,13 @@ int upr_t_chan_sum16(const void* g16, int M, int C, float* out, int accumulate, 
   if (!g16 || !out || !ws || M <= 0 || C <= 0) return UPR_ERR_ARG;
   if (C % 4 || C > 1024 || (uintptr_t)g16 % 8) return UPR_ERR_UNSUPPORTED;
   return chan_reduce2((const half_t*)g16, C, 0, (const float*)nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr, M, C,
+                      2, ws, nullptr, out, accumulate, ST(stream));
+}
+
+int upr_t_chan_sum16s(const void* g16, int M, int C, int cs, float* out, int accumulate, double* ws, void* stream) {
+  if (!g16 || !out || !ws || M <= 0 || C <= 0 || cs < C) return UPR_ERR_ARG;
+  if (C % 4 || C > 1024 || cs % 4 || (uintptr_t)g16 % 8) return UPR_ERR_UNSUPPORTED;
+  return chan_reduce2((const half_t*)g16, cs, 0, (const float*)nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr, M, C,
                       2, ws, nullptr, out, accumulate, ST(stream));
 }
 

@@ -8,9 +8,8 @@
 //
 // Round 1 ran them as one thread per OUTPUT ELEMENT with 64-bit index math
 // (26 % of the bs-8 512^2 step).  Here:
-//   * forward (3 -> COUT 3x3): one thread per output PIXEL computes all COUT
-//     channels from its 27 inputs (weights broadcast from LDS), the tile's
-//     outputs are transposed through LDS and leave as 16-byte row stores;
+//   * forward (3 -> COUT 3x3): fp32 MFMA over 16-pixel groups, the filter in
+//     registers, 16-byte stores straight from the accumulators;
 //   * input gradient (stride 1): one thread per input pixel accumulates all
 //     CIN input-channel gradients over (tap, Cout), weights broadcast from LDS;
 //   * weight gradient (Cout <= 32): a GEMM over pixels on
@@ -20,6 +19,7 @@
 //     partial row per block, summed in block order by a second kernel.
 // All fp32 (exact-fp32 MFMA); only the summation order differs from a serial
 // loop.
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -48,84 +48,95 @@ static SV mksv(const UprView* u) {
 }
 
 // ---------------------------------------------------------------------------
-// forward: 3 -> COUT, 3x3, stride 1, dilation 1, padding p
+// forward: 3 -> COUT (32 / 64), 3x3, stride 1, dilation 1, on fp32 MFMA
+// (v_mfma_f32_16x16x4_f32: exact fp32 products, fp32 accumulation).  The
+// kernel above reads every weight from LDS once per output pixel (432
+// ds_read_b128 per thread for 64 channels: 0.26 ms, 1 TB/s, for VGG conv1_1 at
+// bs 8 512^2).  Here a wave walks 16-pixel groups: lane (pixel l & 15, k-group
+// l >> 4) gathers the 7 input values k = kg + 4s (k = ci*9 + ky*3 + kx, 27
+// padded to 28) straight from HBM, the filter lives in registers as the A
+// operand (COUT/16 tiles x 7 k-steps, one float per lane each), and the
+// accumulator of tile t holds channels 16t + 4(l >> 4) .. +3 of pixel l & 15:
+// 16-byte fp32 / 8-byte fp16 stores from registers.
 // ---------------------------------------------------------------------------
 template <int COUT>
-__global__ __launch_bounds__(256) void c3k3_fwd_kernel(SV x, int B, int H, int W, const float* __restrict__ w,
-                                                      const float* __restrict__ bias, int p, SV y, int Ho, int Wo,
-                                                      int relu, int accum, half_t* __restrict__ y16, int skip32) {
-  constexpr int TS = COUT + 4;  // LDS row stride (floats): 16-byte aligned rows, spread banks
-  extern __shared__ __attribute__((aligned(16))) float sm3[];
-  float* sw_ = sm3;                  // [27][COUT] weights, k-major (broadcast reads)
-  float* sb_ = sm3 + 27 * COUT;      // [COUT]
-  float* tile = sb_ + COUT;          // [256][TS]
-  const int tid = threadIdx.x;
-  for (int i = tid; i < 27 * COUT; i += 256) {
-    const int co = i / 27, k = i - co * 27;
-    sw_[k * COUT + co] = w[i];
-  }
-  for (int i = tid; i < COUT; i += 256) sb_[i] = bias ? bias[i] : 0.f;
-  __syncthreads();
-  const int P = B * Ho * Wo;
-  const int p0 = blockIdx.x * 256;
-  const int pix = p0 + tid;
-  if (pix < P) {
-    const int ox = pix % Wo;
-    const int r = pix / Wo;
-    const int oy = r % Ho, b = r / Ho;
-    float in[27];
+__global__ __launch_bounds__(256) void c3k3_mfma_kernel(SV x, int B, int H, int W, const float* __restrict__ w,
+                                                       const float* __restrict__ bias, int p, SV y, int Ho, int Wo,
+                                                       int relu, int accum, half_t* __restrict__ y16, int skip32) {
+  constexpr int NT = COUT / 16;
+  const int lane = threadIdx.x & 63;
+  const int fr = lane & 15, kg = lane >> 4;
+  float wa[NT][7];
 #pragma unroll
-    for (int ci = 0; ci < 3; ++ci)
+  for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int ky = 0; ky < 3; ++ky) {
-        const int iy = oy - p + ky;
+    for (int st = 0; st < 7; ++st) {
+      const int k = kg + 4 * st;
+      wa[t][st] = k < 27 ? w[(t * 16 + fr) * 27 + k] : 0.f;
+    }
+  f32x4_t2 bv[NT];
 #pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-          const int ix = ox - p + kx;
-          const bool ok = iy >= 0 && iy < H && ix >= 0 && ix < W;
-          in[(ci * 3 + ky) * 3 + kx] = ok ? x.d[x.at(b, iy, ix, ci)] : 0.f;
-        }
-      }
-    float acc[COUT];
+  for (int t = 0; t < NT; ++t)
 #pragma unroll
-    for (int co = 0; co < COUT; ++co) acc[co] = sb_[co];
-    // same accumulation order as the serial form: ci, ky, kx
-#pragma unroll
-    for (int k = 0; k < 27; ++k) {
-#pragma unroll
-      for (int co = 0; co < COUT; co += 4) {
-        const f32x4_t2 wv = *(const f32x4_t2*)(sw_ + k * COUT + co);
-        acc[co] = fmaf(in[k], wv[0], acc[co]);
-        acc[co + 1] = fmaf(in[k], wv[1], acc[co + 1]);
-        acc[co + 2] = fmaf(in[k], wv[2], acc[co + 2]);
-        acc[co + 3] = fmaf(in[k], wv[3], acc[co + 3]);
-      }
+    for (int i = 0; i < 4; ++i) bv[t][i] = bias ? bias[t * 16 + kg * 4 + i] : 0.f;
+  const long long P = (long long)B * Ho * Wo;
+  const long long ngroups = (P + 15) / 16;
+  const long long gstride = (long long)gridDim.x * 4;
+  // inputs of group g (the next group's are loaded before this group's MFMAs)
+  auto gather = [&](long long g, float (&xin)[7], int& b, int& oy, int& ox, bool& pok) {
+    const long long pix = g * 16 + fr;
+    pok = g < ngroups && pix < P;
+    b = 0; oy = 0; ox = 0;
+    if (pok) {
+      ox = (int)(pix % Wo);
+      const long long r = pix / Wo;
+      oy = (int)(r % Ho);
+      b = (int)(r / Ho);
     }
 #pragma unroll
-    for (int co = 0; co < COUT; co += 4)
-      *(f32x4_t2*)(tile + tid * TS + co) = f32x4_t2{acc[co], acc[co + 1], acc[co + 2], acc[co + 3]};
-  }
-  __syncthreads();
-  // copy-out: consecutive lanes store consecutive 16-byte chunks of a pixel's
-  // channel run (y.sc == 1, checked by the host)
-  constexpr int CQ = COUT / 4;
-  for (int it = tid; it < 256 * CQ; it += 256) {
-    const int lp = it / CQ, q = it - lp * CQ;
-    const int pp = p0 + lp;
-    if (pp >= P) break;
-    const int ox = pp % Wo;
-    const int r = pp / Wo;
-    const int oy = r % Ho, b = r / Ho;
-    f32x4_t2 v = *(const f32x4_t2*)(tile + lp * TS + q * 4);
-    f32x4_t2* dst = (f32x4_t2*)(y.d + y.at(b, oy, ox, q * 4));
-    if (accum) v += *dst;
-    if (relu) {
-      v[0] = fmaxf(v[0], 0.f); v[1] = fmaxf(v[1], 0.f); v[2] = fmaxf(v[2], 0.f); v[3] = fmaxf(v[3], 0.f);
+    for (int st = 0; st < 7; ++st) {
+      const int k = kg + 4 * st;
+      const int ci = k / 9, ky = (k % 9) / 3, kx = k % 3;
+      const int iy = oy - p + ky, ix = ox - p + kx;
+      xin[st] = (pok && k < 27 && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) ? x.d[x.at(b, iy, ix, ci)]
+                                                                                           : 0.f;
     }
-    if (!skip32) *dst = v;
-    if (y16) {  // the autocast consumer's fp16 operand, [pixel][COUT] compact
-      typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-      *(h4*)(y16 + (size_t)pp * COUT + q * 4) = h4{(half_t)v[0], (half_t)v[1], (half_t)v[2], (half_t)v[3]};
+  };
+  long long g = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  float xn[7];
+  int nb, noy, nox;
+  bool npok;
+  gather(g, xn, nb, noy, nox, npok);
+  for (; g < ngroups; g += gstride) {
+    float xin[7];
+#pragma unroll
+    for (int st = 0; st < 7; ++st) xin[st] = xn[st];
+    const int b = nb, oy = noy, ox = nox;
+    const bool pok = npok;
+    const long long pix = g * 16 + fr;
+    gather(g + gstride, xn, nb, noy, nox, npok);
+    f32x4_t2 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      acc[t] = bv[t];
+#pragma unroll
+      for (int st = 0; st < 7; ++st) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[t][st], xin[st], acc[t], 0, 0, 0);
+    }
+    if (!pok) continue;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int co = t * 16 + kg * 4;
+      f32x4_t2 v = acc[t];
+      f32x4_t2* dst = (f32x4_t2*)(y.d + y.at(b, oy, ox, co));
+      if (accum) v += *dst;
+      if (relu) {
+        v[0] = fmaxf(v[0], 0.f); v[1] = fmaxf(v[1], 0.f); v[2] = fmaxf(v[2], 0.f); v[3] = fmaxf(v[3], 0.f);
+      }
+      if (!skip32) *dst = v;
+      if (y16) {
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        *(h4*)(y16 + (size_t)pix * COUT + co) = h4{(half_t)v[0], (half_t)v[1], (half_t)v[2], (half_t)v[3]};
+      }
     }
   }
 }
@@ -480,18 +491,9 @@ __global__ __launch_bounds__(256) void dgrad_c3_mfma_kernel(const half_t* __rest
   constexpr int TR = 4, TC = 64, LR = TR + 2, LC = TC + 2;
   __shared__ __attribute__((aligned(16))) half_t tile[LR * LC * COUT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fg = lane >> 4;
-  const int tx = blockIdx.x, ty = blockIdx.y, b = blockIdx.z;
-  const int iy0 = ty * TR, ix0 = tx * TC;
-  // dy rows iy0-1 .. iy0+4, columns ix0-1 .. ix0+64 -> LDS
-  for (int q = tid; q < LR * LC * CH; q += 256) {
-    const int ch = q % CH, rc = q / CH, col = rc % LC, r = rc / LC;
-    const int gy = iy0 - 1 + r, gx = ix0 - 1 + col;
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if ((unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
-      v = *(const uint4*)(dy + (((size_t)b * H + gy) * W + gx) * COUT + ch * 8);
-    *(uint4*)(tile + (r * LC + col) * COUT + ((ch ^ (col & (CH - 1))) * 8)) = v;
-  }
-  // A = weights: lane (fr = ci, fg) holds w[co = kc*32 + fg*8 + e][ci][tap], tap = 8 - (dr*3 + dc)
+  // A = weights: lane (fr = ci, fg) holds w[co = kc*32 + fg*8 + e][ci][tap], tap = 8 - (dr*3 + dc);
+  // built once per (persistent) block -- per tile, these 144 scalar loads per lane were
+  // most of the kernel's time (0.24 ms for VGG conv1_1 at bs 8 512^2)
   h8 wa[KC][9];
 #pragma unroll
   for (int kc = 0; kc < KC; ++kc)
@@ -500,35 +502,51 @@ __global__ __launch_bounds__(256) void dgrad_c3_mfma_kernel(const half_t* __rest
 #pragma unroll
       for (int e = 0; e < 8; ++e)
         wa[kc][t][e] = fr < 3 ? (half_t)w[((kc * 32 + fg * 8 + e) * 3 + fr) * 9 + (8 - t)] : (half_t)0.f;
-  __syncthreads();
-  const int iy = iy0 + wave;
-  f4 acc[4];
-#pragma unroll
-  for (int g = 0; g < 4; ++g) acc[g] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int g = 0; g < 4; ++g)
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int dr = t / 3, dc = t % 3;
-      const int col = g * 16 + fr + dc;  // LDS column of this lane's pixel, shifted by the tap
-      const half_t* row = tile + ((wave + dr) * LC + col) * COUT;
-#pragma unroll
-      for (int kc = 0; kc < KC; ++kc) {
-        const h8 bv = *(const h8*)(row + (((kc * 4 + fg) ^ (col & (CH - 1))) * 8));
-        acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[kc][t], bv, acc[g], 0, 0, 0);
-      }
+  const int ntx = (W + TC - 1) / TC, nty = (H + TR - 1) / TR;
+  const int ntiles = ntx * nty * B;
+  for (int tile_id = blockIdx.x; tile_id < ntiles; tile_id += gridDim.x) {
+    const int tx = tile_id % ntx, ty = (tile_id / ntx) % nty, b = tile_id / (ntx * nty);
+    const int iy0 = ty * TR, ix0 = tx * TC;
+    __syncthreads();  // the previous tile's LDS reads are done
+    // dy rows iy0-1 .. iy0+4, columns ix0-1 .. ix0+64 -> LDS
+    for (int q = tid; q < LR * LC * CH; q += 256) {
+      const int ch = q % CH, rc = q / CH, col = rc % LC, r = rc / LC;
+      const int gy = iy0 - 1 + r, gx = ix0 - 1 + col;
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if ((unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
+        v = *(const uint4*)(dy + (((size_t)b * H + gy) * W + gx) * COUT + ch * 8);
+      *(uint4*)(tile + (r * LC + col) * COUT + ((ch ^ (col & (CH - 1))) * 8)) = v;
     }
-  if (iy >= H || fg != 0) return;
+    __syncthreads();
+    const int iy = iy0 + wave;
+    f4 acc[4];
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const int ix = ix0 + g * 16 + fr;
-    if (ix >= W) continue;
-    float* o = dx.d + dx.at(b, iy, ix, 0);
+    for (int g = 0; g < 4; ++g) acc[g] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      float v = acc[g][c];
-      if (accum) v += o[c * dx.sc];
-      o[c * dx.sc] = v;
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int dr = t / 3, dc = t % 3;
+        const int col = g * 16 + fr + dc;  // LDS column of this lane's pixel, shifted by the tap
+        const half_t* row = tile + ((wave + dr) * LC + col) * COUT;
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) {
+          const h8 bv = *(const h8*)(row + (((kc * 4 + fg) ^ (col & (CH - 1))) * 8));
+          acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[kc][t], bv, acc[g], 0, 0, 0);
+        }
+      }
+    if (iy >= H || fg != 0) continue;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int ix = ix0 + g * 16 + fr;
+      if (ix >= W) continue;
+      float* o = dx.d + dx.at(b, iy, ix, 0);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        float v = acc[g][c];
+        if (accum) v += o[c * dx.sc];
+        o[c * dx.sc] = v;
+      }
     }
   }
 }
@@ -537,14 +555,17 @@ int small_conv_dgrad_c3_16(const void* dy16, int B, int H, int W, const float* w
                            int accumulate, hipStream_t st) {
   if ((Cout != 32 && Cout != 64) || ((uintptr_t)dy16 % 16)) return kErrUnsupported;
   if ((long long)B * H * W >= (1ll << 31)) return kErrUnsupported;
-  const dim3 grid((W + 63) / 64, (H + 3) / 4, B);
-  if (grid.y > 65535 || grid.z > 65535) return kErrUnsupported;
+  const long long ntiles = (long long)((W + 63) / 64) * ((H + 3) / 4) * B;
+  if (ntiles >= (1ll << 31)) return kErrUnsupported;
+  int cus = 256, dev = 0;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int grid = (int)std::min<long long>(ntiles, (long long)cus * 3);  // 3 blocks per CU (50 KB of LDS each)
   const SV dx = mksv(dxv);
   if (Cout == 64)
-    hipLaunchKernelGGL(dgrad_c3_mfma_kernel<64>, grid, dim3(256), 0, st, (const half_t*)dy16, B, H, W, w, dx,
+    hipLaunchKernelGGL(dgrad_c3_mfma_kernel<64>, dim3(grid), dim3(256), 0, st, (const half_t*)dy16, B, H, W, w, dx,
                        accumulate);
   else
-    hipLaunchKernelGGL(dgrad_c3_mfma_kernel<32>, grid, dim3(256), 0, st, (const half_t*)dy16, B, H, W, w, dx,
+    hipLaunchKernelGGL(dgrad_c3_mfma_kernel<32>, dim3(grid), dim3(256), 0, st, (const half_t*)dy16, B, H, W, w, dx,
                        accumulate);
   return (int)hipGetLastError();
 }
@@ -600,24 +621,20 @@ int small_conv_fwd(const UprView* xv, int B, int H, int W, int Cin, const float*
   if ((long long)B * Ho * Wo >= (1ll << 31)) return kErrUnsupported;
   const SV x = mksv(xv), y = mksv(yv);
   const int P = B * Ho * Wo;
-  const int grid = (P + 255) / 256;
-  static bool attr = false;
-  if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)c3k3_fwd_kernel<64>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-    if (e != hipSuccess) return (int)e;
-    attr = true;
+  {
+    // fp32 MFMA form (16-pixel groups, filter in registers); grid sized for ~8 waves per SIMD
+    int cus = 256, dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const long long groups = ((long long)P + 15) / 16;
+    const int mgrid = (int)std::min<long long>((groups + 3) / 4, (long long)cus * 8);
+    if (Cout == 32)
+      hipLaunchKernelGGL(c3k3_mfma_kernel<32>, dim3(mgrid), dim3(256), 0, st, x, B, H, W, w, bias, pad, y, Ho, Wo, relu,
+                         accumulate, (half_t*)y16, skip32);
+    else
+      hipLaunchKernelGGL(c3k3_mfma_kernel<64>, dim3(mgrid), dim3(256), 0, st, x, B, H, W, w, bias, pad, y, Ho, Wo, relu,
+                         accumulate, (half_t*)y16, skip32);
+    return (int)hipGetLastError();
   }
-  if (Cout == 32) {
-    const size_t lds = sizeof(float) * (27 * 32 + 32 + 256 * 36);
-    hipLaunchKernelGGL(c3k3_fwd_kernel<32>, dim3(grid), dim3(256), lds, st, x, B, H, W, w, bias, pad, y, Ho, Wo, relu,
-                       accumulate, (half_t*)y16, skip32);
-  } else {
-    const size_t lds = sizeof(float) * (27 * 64 + 64 + 256 * 68);
-    hipLaunchKernelGGL(c3k3_fwd_kernel<64>, dim3(grid), dim3(256), lds, st, x, B, H, W, w, bias, pad, y, Ho, Wo, relu,
-                       accumulate, (half_t*)y16, skip32);
-  }
-  return (int)hipGetLastError();
 }
 
 int small_conv_dgrad(const UprView* dyv, int Ho, int Wo, const float* w, int B, int H, int W, int Cin, int Cout,

@@ -258,7 +258,7 @@ struct Wg16Args {
   const half_t* x16;   // [B][H][W][Cin] fp16
   int B, H, W, Cin;
   const float* dy;
-  const half_t* dy16;  // nullable: dy's compact [pixel][Cout] fp16 copy (its producer's), read instead of dy
+  const half_t* dy16;  // nullable: dy's fp16 copy in dy's layout (dy_cs, dy_coff; its producer's), read instead of dy
   int Ho, Wo, Cout, dy_cs, dy_coff;
   int kh, kw, s, p, d;
   int KT, nruns;       // kh*kw*Cin, KT / 32
@@ -312,11 +312,11 @@ __global__ __launch_bounds__(256) void wgrad16_kernel(Wg16Args a) {
     const int oy = r / segs, ox0 = (r - oy * segs) * W16_KP;
     const size_t pix0 = (size_t)(b * a.Ho + oy) * a.Wo + ox0;
     if (a16) {  // the fp16 copy: half the bytes, the same RNE-rounded values
-      const half_t* base = a.dy16 + pix0 * a.Cout + co0 + qa * 4;
+      const half_t* base = a.dy16 + pix0 * a.dy_cs + a.dy_coff + co0 + qa * 4;
 #pragma unroll
       for (int i = 0; i < AC; ++i) {
         const int pr = tid / NQA + i * (256 / NQA);
-        hreg[i] = *(const f16x4_w2*)(base + (size_t)pr * a.Cout);
+        hreg[i] = *(const f16x4_w2*)(base + (size_t)pr * a.dy_cs);
       }
       return;
     }
@@ -530,7 +530,7 @@ struct Wg16hArgs {
   const half_t* x16;  // [B][H][W][CIN] fp16
   int B, H, W;        // = Ho, Wo
   const float* dy;
-  const half_t* dy16;  // nullable compact [pixel][COUT] fp16 copy
+  const half_t* dy16;  // nullable fp16 copy of dy in dy's layout (dy_cs, dy_coff)
   int dy_cs, dy_coff;
   int steps_per_col;   // H / TR
   int spb;             // steps per block
@@ -624,7 +624,7 @@ __global__ __launch_bounds__(256) void wgrad16h_kernel(Wg16hArgs a) {
       const int R = q / (COUT / 4), cq = q - R * (COUT / 4);
       const size_t pix = pix0 + (size_t)(R >> 6) * a.W + (R & 63);
       if constexpr (A16)
-        hreg[i] = *(const f16x4_w2*)(a.dy16 + pix * COUT + cq * 4);
+        hreg[i] = *(const f16x4_w2*)(a.dy16 + pix * a.dy_cs + a.dy_coff + cq * 4);
       else
         areg[i] = *(const f32x4_w2*)(a.dy + pix * a.dy_cs + a.dy_coff + cq * 4);
     }

@@ -152,6 +152,7 @@ SIGNATURES.update({
     "upr_t_bn_bwd_fused16": (_i, [_p, _p, _i, _i, _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _i, _i, _i, _i,
                                   _p, _i, _p]),
     "upr_t_chan_sum16": (_i, [_p, _i, _i, _p, _i, _p, _p]),
+    "upr_t_chan_sum16s": (_i, [_p, _i, _i, _i, _p, _i, _p, _p]),
     "upr_t_zero_upsample16h": (_i, [_p, _i, _i, _i, _i, _p, _p]),
     "upr_t_zero_upsample16": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _p]),
     "upr_t_relu_mask": (_i, [_p, _i, _i, _p, _i, _i, _i, _i, _p]),

@@ -133,6 +133,10 @@ class Act:
         self.t16 = None  # compact fp16 copy written by its producer (autocast conv input), or None
         self.t16_grad = False  # t16 of a gradient: written by the fused BN backward (BN.bwd), trusted by dgrad
         self.stale32 = False  # fp32 t left behind by relu_mask(only16): t16 is the gradient's only value
+        # t16 is a whole concat's fp16 copy its channel slices read in place (element (m, c) of
+        # a slice at t16[m * cs + coff + c]): set by the producer of a concat gradient whose
+        # slices are only read afterwards (EnhancedFAM's fusion input gradient)
+        self.t16_shared = False
 
     @staticmethod
     def new(B, H, W, C, dev, fresh=True):
@@ -143,7 +147,13 @@ class Act:
     def slice(self, coff, C):
         s = Act(self.t, C, self.coff + coff)
         s.fresh = self.fresh
+        if self.t16_shared and self.t16 is not None:
+            s.t16, s.t16_grad, s.t16_shared, s.stale32 = self.t16, self.t16_grad, True, self.stale32
         return s
+
+    def whole16(self):
+        """t16 is this Act's own compact copy (not a slice of a shared one)."""
+        return self.coff == 0 and self.cs == self.C
 
     @property
     def M(self):
@@ -166,6 +176,7 @@ class Act:
         self.fresh = False
         self.t16 = None
         self.t16_grad = False
+        self.t16_shared = False
         self.stale32 = False
         return acc
 
@@ -290,7 +301,7 @@ class Conv:
             _chk(lib.upr_t_cast_f16(_p(self.wt), _p(self.wt16), w.numel(), st), "cast_w")
 
     def _mfma16(self, x, B, H, W, C, cs, coff, w16, bias, N, kh, kw, s, p, d, res, relu, out, store=0, x16=None,
-                keep16=False, out16=None, only16=False):
+                keep16=False, out16=None, only16=False, x16_strided=False):
         """fp16 MFMA conv with fp32 in / out (upr_t_conv_mfma16); res: Act or None; x16: the
         input's compact fp16 copy when its producer already wrote it; out16 = (fp16 tensor, channel
         offset, channel stride): where the (half)out copy goes when `out` is a channel slice of a
@@ -301,6 +312,10 @@ class Conv:
         ready = x16 is not None
         if not ready:
             x16 = _h16(B * H * W * C, dev)
+        # x16_strided: x16 is the shared fp16 copy of the concat x is a slice of (channel stride cs)
+        x16p = ctypes.c_void_p(x16.data_ptr() + 2 * coff) if x16_strided else _p(x16)
+        if x16_strided:
+            store |= 32
         if out16 is not None:
             t16, c16, cs16 = out16
             y16p, y16cs = ctypes.c_void_p(t16.data_ptr() + 2 * c16), cs16
@@ -312,7 +327,7 @@ class Conv:
                                        int(relu), _fp(out.t), out.cs, out.coff,
                                        store | (2 if keep16 and res is None else 0) |
                                        (4 if only16 and keep16 and res is None and out16 is None else 0),
-                                       _p(x16), int(ready), y16p, y16cs, _stream()), "conv_mfma16")
+                                       x16p, int(ready), y16p, y16cs, _stream()), "conv_mfma16")
         if out16 is not None:
             out.t16 = None
             return x16
@@ -458,7 +473,7 @@ class Conv:
         gx.t16_grad = keep
         return True
 
-    def bwd(self, x, gy, gx=None, x_view=None, mask=None, gx_only16=False):
+    def bwd(self, x, gy, gx=None, x_view=None, mask=None, gx_only16=False, gx_keep16=False):
         """gy: Act gradient of this conv's output (pre-activation).
         Accumulates the weight / bias gradients; gx (Act, nullable) receives
         the input gradient (overwrite when fresh, else accumulate).
@@ -467,7 +482,8 @@ class Conv:
         fp16 copy, channel stride cs); gx.t16 then holds the masked gradient and
         gx.t is left stale when only16.  Returns True when the mask was applied.
         gx_only16: the input gradient's reader (a BatchNorm backward) takes its fp16
-        copy: under autocast gx gets gx.t16 and no fp32 store when fresh."""
+        copy: under autocast gx gets gx.t16 and no fp32 store when fresh.
+        gx_keep16: gx also gets its fp16 copy (fp32 kept), shared by gx's channel slices."""
         lib, st = L.lib(), _stream()
         if x_view is not None:
             xv, B, H, W = x_view
@@ -485,8 +501,10 @@ class Conv:
                     # autocast: fp16 operands, fp32 accumulation (trainers/train.py:72); added
                     # straight into weight.grad's layout
                     # gy's fp16 copy (the fused BN backward's dx16) is the AMP A operand as is
-                    dy16 = gy.t16 if self.amp and gy.t16_grad and gy.coff == 0 and gy.cs == gy.C == self.Cout \
-                        else None
+                    # (in gy's own layout: the C ABI indexes dy16 like dy, so a slice of a shared concat
+                    # copy passes the concat's base)
+                    dy16 = gy.t16 if self.amp and gy.t16_grad and (gy.whole16() and gy.C == self.Cout or
+                                                                   gy.t16_shared) else None
                     assert dy16 is not None or not gy.stale32, "fp16-only gradient without the fp16 weight gradient"
                     assert x16 is not None or not x.stale32, "fp16-only input without the fp16 weight gradient"
                     _chk(lib.upr_t_conv_wgrad_into(_fp(x.t), _p(x16) if self.amp else None, B, H, W, self.Cin, x.cs,
@@ -498,8 +516,13 @@ class Conv:
                         if gy.stale32:
                             ws = torch.empty((L.lib().upr_t_reduce_acc_doubles(self.Cout),), dtype=torch.float64,
                                              device=gy.t.device)
-                            _chk(lib.upr_t_chan_sum16(_p(gy.t16), gy.M, self.Cout, _p(self.bias.grad), 1, _p(ws), st),
-                                 "dbias16")
+                            if gy.whole16():
+                                _chk(lib.upr_t_chan_sum16(_p(gy.t16), gy.M, self.Cout, _p(self.bias.grad), 1, _p(ws),
+                                                          st), "dbias16")
+                            else:  # a slice of a shared concat copy
+                                _chk(lib.upr_t_chan_sum16s(ctypes.c_void_p(gy.t16.data_ptr() + 2 * gy.coff), gy.M,
+                                                           self.Cout, gy.cs, _p(self.bias.grad), 1, _p(ws), st),
+                                     "dbias16s")
                         else:
                             chan_sum(gy, self.Cout, self.bias.grad, st)
                 else:
@@ -532,6 +555,10 @@ class Conv:
                 # autocast: the fp16 operand comes from gy's producer (gy.t16) or, for
                 # stride 2, straight from an fp16 zero-upsample (no fp32 pass + cast)
                 src16 = gy.t16 if self.amp and gy.t16_grad and gy.coff == 0 and gy.cs == gy.C == self.Cout else None
+                # a channel slice of a shared concat copy (stride-1 convs read it in place)
+                strided16 = src16 is None and self.amp and self.s == 1 and gy.t16_grad and gy.t16_shared
+                if strided16:
+                    src16 = gy.t16
                 if self.s == 2 and self.amp and acc and (self.kh, self.kw, self.p, self.d) == (1, 1, 0, 1) and \
                         H == 2 * Ho and W == 2 * Wo and self._dgrad_s2_1x1(gy, src16, B, Ho, Wo, gx):
                     return
@@ -561,10 +588,14 @@ class Conv:
                 pad_t = self.d * (self.kh - 1) - self.p
                 assert src16 is not None or not gy.stale32, "fp16-only gradient without the fp16 input gradient"
                 if self.amp:
-                    o16 = bool(gx_only16) and not acc and gx.coff == 0 and gx.cs == gx.C == self.Cin
+                    whole_gx = not acc and gx.coff == 0 and gx.cs == gx.C == self.Cin
+                    o16 = bool(gx_only16) and whole_gx
+                    k16 = o16 or (bool(gx_keep16) and whole_gx)
                     self._mfma16(src, B, sH, sW, self.Cout, scs, scoff, self.wt16, None, self.Cin, self.kh, self.kw, 1,
-                                 pad_t, self.d, gx if acc else None, False, gx, x16=src16, keep16=o16, only16=o16)
+                                 pad_t, self.d, gx if acc else None, False, gx, x16=src16, keep16=k16, only16=o16,
+                                 x16_strided=strided16)
                     gx.t16_grad = gx.t16 is not None
+                    gx.t16_shared = bool(gx_keep16) and gx.t16 is not None
                 else:
                     _chk(lib.upr_t_conv_mfma(_fp(src), B, sH, sW, self.Cout, scs, scoff, _p(self.wt), None, self.Cin,
                                              self.kh, self.kw, 1, pad_t, self.d, gx.ptr() if acc else None,
@@ -1185,7 +1216,10 @@ class FAMT:
         self.ca1.bwd(self.pool, g_h1, g_pool)
         _chk(lib.upr_t_fam_pool_bwd(_fp(g_o.t), _fp(g_pool.t), _fp(self.o.t), B, HW, C, st), "pool_bwd")
         g_cat = Act.new(B, H, W, 4 * C, dev)
-        self.fu.bwd(self.cat, g_o, g_cat)
+        # the four branch convs read slices of its fp16 copy; no fp32 store when every one of
+        # them takes an fp16 gradient (their weight gradients on the fp16 GEMM: Wo % 64)
+        only16 = all(c.takes16_grad() for c in (self.b1, self.b2, self.b3b, self.b4b))
+        self.fu.bwd(self.cat, g_o, g_cat, gx_only16=only16, gx_keep16=True)
         self.b1.bwd(self.x, g_cat.slice(0, C), gx)
         g_mp = Act.new(B, H, W, self.x.C, dev)
         self.b2.bwd(self.mp, g_cat.slice(C, C), g_mp)
