@@ -11,6 +11,8 @@ Tolerances (fp32 everywhere; differences are summation order only):
     reduction-order noise), parameter deltas after Adam rel 1e-3, BatchNorm
     running stats <= 1e-4.
 """
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -523,6 +525,63 @@ def test_dgrad_3x3_stride2_phases(acc, keep16):
         assert bool((gx == 7.0).all()), "only16: the fp32 output must not be written"
     else:
         _close(gx, ref, 1e-3, "3x3 s2 dgrad")
+
+
+def test_shared_concat_fp16_slices():
+    """A channel slice of a concat gradient's shared fp16 copy, read in place
+    (EnhancedFAM's four branch convs): upr_t_conv_mfma16 store | 32 (x16 in x's
+    layout), upr_t_conv_wgrad_into's dy16 in dy's layout, upr_t_chan_sum16s --
+    each bit-identical to the same call on a compact copy of the slice."""
+    from upr import _lib as L
+    lib, st = L.lib(), torch.cuda.current_stream().cuda_stream
+    gen = torch.Generator().manual_seed(41)
+    B, H, W, C, N, k0 = 2, 16, 64, 32, 32, 64     # slice = channels 64..95 of a 128-channel concat
+    cat = torch.randn(B, H, W, 4 * C, generator=gen).to(DEV)
+    cat16 = cat.half()
+    sl16 = cat16[..., k0:k0 + C].contiguous()
+    w = (torch.randn(N, C, 3, 3, generator=gen) * 0.1).to(DEV)
+    wt = torch.empty(w.numel(), device=DEV)
+    assert lib.upr_t_pack_weight(w.data_ptr(), wt.data_ptr(), N, C, 3, 3, 0, st) == 0
+    wt16 = wt.half()
+    outs = []
+    for strided in (False, True):
+        y = torch.empty(B, H, W, N, device=DEV)
+        y16 = torch.empty(B * H * W * N, dtype=torch.float16, device=DEV)
+        if strided:
+            rc = lib.upr_t_conv_mfma16(None, B, H, W, C, 4 * C, k0, wt16.data_ptr(), None, N, 3, 3, 1, 1, 1, None, 0,
+                                       0, y.data_ptr(), N, 0, 32, ctypes.c_void_p(cat16.data_ptr() + 2 * k0), 1,
+                                       y16.data_ptr(), 0, st)
+        else:
+            rc = lib.upr_t_conv_mfma16(None, B, H, W, C, C, 0, wt16.data_ptr(), None, N, 3, 3, 1, 1, 1, None, 0, 0,
+                                       y.data_ptr(), N, 0, 0, sl16.data_ptr(), 1, y16.data_ptr(), 0, st)
+        assert rc == 0, rc
+        outs.append(y)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    # weight gradient: dy = the slice (fp32 strided + its fp16 copy in the same layout)
+    x16 = torch.randn(B, H, W, C, generator=gen).half().to(DEV)
+    dws = []
+    for strided in (False, True):
+        dw = torch.zeros(N, C, 3, 3, device=DEV)
+        if strided:
+            rc = lib.upr_t_conv_wgrad_into(None, x16.data_ptr(), B, H, W, C, C, 0, cat.data_ptr(), cat16.data_ptr(), H,
+                                           W, C, 4 * C, k0, 3, 3, 1, 1, 1, dw.data_ptr(), st)
+        else:
+            dyc = cat[..., k0:k0 + C].contiguous()
+            rc = lib.upr_t_conv_wgrad_into(None, x16.data_ptr(), B, H, W, C, C, 0, dyc.data_ptr(), sl16.data_ptr(), H,
+                                           W, C, C, 0, 3, 3, 1, 1, 1, dw.data_ptr(), st)
+        assert rc == 0, rc
+        dws.append(dw)
+    torch.cuda.synchronize()
+    assert torch.equal(dws[0], dws[1])
+    # channel sums of the slice's fp16 values
+    ws = torch.empty((lib.upr_t_reduce_acc_doubles(C),), dtype=torch.float64, device=DEV)
+    out = torch.zeros(C, device=DEV)
+    assert lib.upr_t_chan_sum16s(ctypes.c_void_p(cat16.data_ptr() + 2 * k0), B * H * W, C, 4 * C, out.data_ptr(), 0,
+                                 ws.data_ptr(), st) == 0
+    torch.cuda.synchronize()
+    ref = sl16.double().reshape(-1, C).sum(0).float().cpu()
+    assert torch.allclose(out.cpu(), ref, rtol=1e-5, atol=1e-4)
 
 
 def test_fp16_copy_producers():
