@@ -302,6 +302,13 @@ int upr_t_maxpool_code(const UprView* x, int B, int H, int W, int C, int k, int 
                        int Wo, unsigned char* code, void* y16, void* stream);
 int upr_t_maxpool_bwd_code(const unsigned char* code, const UprView* dy, int B, int H, int W, int C, int k, int s,
                            int p, int Ho, int Wo, const UprView* dx, int accumulate, void* stream);
+/* upr_t_maxpool_bwd_code (3x3/1/1, 2x2/2/0) writing the gathered gradient
+ * only as the compact fp16 g16 ([B][H][W][C]), masked by y16 > 0 when y16
+ * (the pool input = a ReLU's compact fp16 output) is given: the pool backward
+ * and the ReLU mask of a frozen fp16 dgrad's operand in one pass.
+ * UPR_ERR_UNSUPPORTED off the 4-channel path. */
+int upr_t_maxpool_bwd_code16(const unsigned char* code, const UprView* dy, int B, int H, int W, int C, int k, int s,
+                             int p, int Ho, int Wo, const void* y16, void* g16, void* stream);
 /* upr_t_maxpool_code reading the input's compact fp16 copy x16 ([B][H][W][C];
  * the autocast VGG activations exist in fp16 only): 3x3/1/1 and 2x2/2/0 with
  * C % 4 == 0, else UPR_ERR_UNSUPPORTED. */

@@ -983,15 +983,22 @@ __global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(const TG* __restrict
     // fixed channels per thread (see bn_apply4_kernel): the per-channel terms,
     // fp64 divides included, once per thread instead of per element
     const int c = (threadIdx.x % C4) * 4, rpb = 256 / C4;
+    // every per-channel load unconditional and issued together, the flags applied
+    // by selects, 1/M one uniform divide: the conditional-load form (a branch and
+    // a full memory wait per term, fp64 divides between) ran at ~2 TB/s on the
+    // training shapes, its per-thread prologue dominating a one-row thread
+    const float* bp = relu ? beta : gamma;  // beta may be NULL without the fold
+    const double invM = batch_stats ? 1.0 / M : 0.0;
     float mu[4], is[4], ga[4], be[4], sg[4], sgx[4], gis[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       mu[e] = mean[c + e];
       is[e] = invstd[c + e];
       ga[e] = gamma[c + e];
-      be[e] = relu ? beta[c + e] : 0.f;
-      sg[e] = batch_stats ? (float)(acc[c + e] / M) : 0.f;
-      sgx[e] = batch_stats ? (float)(acc[C + c + e] / M) : 0.f;
+      const float bv = bp[c + e];
+      be[e] = relu ? bv : 0.f;
+      sg[e] = (float)(acc[c + e] * invM);
+      sgx[e] = (float)(acc[C + c + e] * invM);
       gis[e] = ga[e] * is[e];
     }
     for (int m = blockIdx.x * rpb + threadIdx.x / C4; m < M; m += gridDim.x * rpb) {
@@ -3134,13 +3141,17 @@ __global__ __launch_bounds__(256) void maxpool4_kernel(const TI* __restrict__ x,
 }
 
 // dx[b][iy][ix][c..c+3] += dy of every window (ascending oy, then ox: the
-// generic gather's order) whose code points at (iy, ix)
-template <int K, int S, int P>
+// generic gather's order) whose code points at (iy, ix).  O16: the result
+// goes to the compact fp16 g16 instead (element 4 i), masked by the producing
+// ReLU's fp16 output y16 when given -- the frozen VGG's pool backward, whose
+// only reader is the masked fp16 dgrad operand (relu_mask16h fused away)
+template <int K, int S, int P, int O16 = 0>
 __global__ __launch_bounds__(256) void maxpool_gather4_kernel(const unsigned* __restrict__ code,
                                                               const float* __restrict__ dy, int dsb, int dsh, int dsw,
                                                               int H, int W, int CV, int Ho, int Wo, int n,
                                                               float* __restrict__ dx, int xsb, int xsh, int xsw,
-                                                              int accumulate) {
+                                                              int accumulate, const half_t* __restrict__ y16 = nullptr,
+                                                              half_t* __restrict__ g16 = nullptr) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   const int cv = i % CV, c = cv * 4;
@@ -3148,8 +3159,8 @@ __global__ __launch_bounds__(256) void maxpool_gather4_kernel(const unsigned* __
   const int ix = r % W;
   r /= W;
   const int iy = r % H, b = r / H;
-  float* dp = dx + b * xsb + iy * xsh + ix * xsw + c;
-  float4 acc = accumulate ? *(const float4*)dp : make_float4(0.f, 0.f, 0.f, 0.f);
+  float* dp = O16 ? nullptr : dx + b * xsb + iy * xsh + ix * xsw + c;
+  float4 acc = !O16 && accumulate ? *(const float4*)dp : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
   for (int t = 0; t < K; ++t) {
     const int ky = K - 1 - t, ny = iy + P - ky;  // oy * S
@@ -3170,6 +3181,18 @@ __global__ __launch_bounds__(256) void maxpool_gather4_kernel(const unsigned* __
       if ((hit & 0xff0000u) == 0) acc.z += g.z;
       if ((hit & 0xff000000u) == 0) acc.w += g.w;
     }
+  }
+  if (O16) {
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    if (y16) {
+      const h4 y = *(const h4*)(y16 + (size_t)i * 4);
+      if (!(y[0] > (half_t)0)) acc.x = 0.f;
+      if (!(y[1] > (half_t)0)) acc.y = 0.f;
+      if (!(y[2] > (half_t)0)) acc.z = 0.f;
+      if (!(y[3] > (half_t)0)) acc.w = 0.f;
+    }
+    *(h4*)(g16 + (size_t)i * 4) = h4{(half_t)acc.x, (half_t)acc.y, (half_t)acc.z, (half_t)acc.w};
+    return;
   }
   *(float4*)dp = acc;
 }
@@ -3282,7 +3305,8 @@ int upr_t_maxpool_bwd_code(const unsigned char* code, const UprView* dy, int B, 
     auto go = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3((nv + 255) / 256), dim3(256), 0, st, (const unsigned*)code,
                          (const float*)dy->data, (int)dy->sb, (int)dy->sh, (int)dy->sw, H, W, CV, Ho, Wo, nv,
-                         (float*)dx->data, (int)dx->sb, (int)dx->sh, (int)dx->sw, accumulate);
+                         (float*)dx->data, (int)dx->sb, (int)dx->sh, (int)dx->sw, accumulate, (const half_t*)nullptr,
+                         (half_t*)nullptr);
     };
     if (kind == 1) go(maxpool_gather4_kernel<3, 1, 1>);
     else go(maxpool_gather4_kernel<2, 2, 0>);
@@ -3294,6 +3318,26 @@ int upr_t_maxpool_bwd_code(const unsigned char* code, const UprView* dy, int B, 
   }
   hipLaunchKernelGGL(maxpool_bwd_gather_kernel<1>, dim3(grid_for(ni)), dim3(256), 0, st, code, mkv(dy), B, H, W, C,
                      k, s, p, Ho, Wo, mkv(dx));
+  LAUNCH_CHECK();
+}
+
+int upr_t_maxpool_bwd_code16(const unsigned char* code, const UprView* dy, int B, int H, int W, int C, int k, int s,
+                             int p, int Ho, int Wo, const void* y16, void* g16, void* stream) {
+  if (!code || !dy || !g16 || k <= 0 || s <= 0 || k * k > 255) return UPR_ERR_ARG;
+  const long long ni = (long long)B * H * W * C;
+  if (ni == 0) return UPR_OK;
+  const int kind = pool_fast_kind(k, s, p);
+  if (!kind || !vec4_view_ok(dy, B, Ho, Wo, C) || (uintptr_t)code % 4 || (uintptr_t)g16 % 8 || (uintptr_t)y16 % 8 ||
+      ni >= (1LL << 31))
+    return UPR_ERR_UNSUPPORTED;
+  const int nv = (int)(ni / 4), CV = C / 4;
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3((nv + 255) / 256), dim3(256), 0, ST(stream), (const unsigned*)code,
+                       (const float*)dy->data, (int)dy->sb, (int)dy->sh, (int)dy->sw, H, W, CV, Ho, Wo, nv,
+                       (float*)nullptr, 0, 0, 0, 0, (const half_t*)y16, (half_t*)g16);
+  };
+  if (kind == 1) go(maxpool_gather4_kernel<3, 1, 1, 1>);
+  else go(maxpool_gather4_kernel<2, 2, 0, 1>);
   LAUNCH_CHECK();
 }
 

@@ -140,44 +140,55 @@ __global__ __launch_bounds__(256) void wgrad_gemm_kernel(WgArgs a) {
   }
 }
 
-// out[g][co][k] = sum of slabs [g*G, min((g+1)*G, splits)) in order (grid.y = group)
-constexpr int WG_GROUP = 16;
-__global__ __launch_bounds__(256) void wgrad_group_kernel(const float* __restrict__ slab, int splits, int Cout, int KT,
-                                                          int ldn, float* __restrict__ out) {
+// dwp (+)= sum of all split slabs in ONE launch (replaces the group + reduce
+// pair): a block owns 16 quads of outputs, its 16 thread rows add slabs
+// j, j + 16, ... (4 independent sums, loads in flight), then the 16 row sums
+// are added in row order -- a fixed order, deterministic run to run.  Output
+// layouts: dwp[co][k] packed, or (torch_ci > 0) PyTorch's [Co][Ci][kh][kw] directly
+// (k = tap * Ci + ci; the 4 k of a quad share the tap; no unpack pass).
+__global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(const float* __restrict__ slab, int splits, int Cout,
+                                                                int KT, int ldn, float* __restrict__ dwp,
+                                                                int torch_ci) {
+  __shared__ f32x4_w2 red[16][16];
+  const int q = threadIdx.x & 15, j = threadIdx.x >> 4;
   const int n4 = Cout * KT / 4;
-  const int g = blockIdx.y;
-  const int s0 = g * WG_GROUP, s1 = min(splits, s0 + WG_GROUP);
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < n4; i += gridDim.x * 256) {
-    const int e = i * 4;
-    const int co = e / KT, k = e - co * KT;  // KT % 4 == 0: a quad never crosses rows
-    f32x4_w2 acc = *(const f32x4_w2*)(slab + ((size_t)s0 * Cout + co) * ldn + k);
-    for (int sp = s0 + 1; sp < s1; ++sp) acc += *(const f32x4_w2*)(slab + ((size_t)sp * Cout + co) * ldn + k);
-    *(f32x4_w2*)(out + ((size_t)g * Cout + co) * ldn + k) = acc;
+  const int i = blockIdx.x * 16 + q;
+  const int e = i * 4;
+  const int co = e / KT, k = e - co * KT;
+  f32x4_w2 s[4] = {};
+  if (i < n4) {
+    const float* p = slab + (size_t)co * ldn + k;
+    const size_t step = (size_t)Cout * ldn;
+    int sp = j;
+    for (; sp + 48 < splits; sp += 64) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s[u] += *(const f32x4_w2*)(p + (size_t)(sp + 16 * u) * step);
+    }
+    for (int u = 0; sp < splits; sp += 16, ++u) s[u & 3] += *(const f32x4_w2*)(p + (size_t)sp * step);
+  }
+  red[j][q] = (s[0] + s[1]) + (s[2] + s[3]);
+  __syncthreads();
+  if (j != 0 || i >= n4) return;
+  f32x4_w2 acc = red[0][q];
+#pragma unroll
+  for (int r = 1; r < 16; ++r) acc += red[r][q];
+  if (torch_ci) {
+    const int taps = KT / torch_ci, tap = k / torch_ci, ci = k - tap * torch_ci;
+    float* o = dwp + ((size_t)co * torch_ci + ci) * taps + tap;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) o[(size_t)jj * taps] += acc[jj];
+  } else {
+    f32x4_w2* o = (f32x4_w2*)(dwp + e);
+    *o = *o + acc;
   }
 }
 
-// dwp[co][k] += sum over n partial slabs (in order); torch_ci > 0: the
-// gradient goes straight into PyTorch's [Co][Ci][kh][kw] layout instead
-// (k = tap * Ci + ci; the 4 k of a quad share the tap), no packed buffer /
-// unpack pass
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int n, int Cout, int KT,
-                                                           int ldn, float* __restrict__ dwp, int torch_ci) {
+static int reduce_slabs(const float* slab, int splits, int Cout, int KT, int ldn, float* dwp, int torch_ci,
+                        hipStream_t st) {
   const int n4 = Cout * KT / 4;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < n4; i += gridDim.x * 256) {
-    const int e = i * 4;
-    const int co = e / KT, k = e - co * KT;
-    f32x4_w2 acc = *(const f32x4_w2*)(part + (size_t)co * ldn + k);
-    for (int sp = 1; sp < n; ++sp) acc += *(const f32x4_w2*)(part + ((size_t)sp * Cout + co) * ldn + k);
-    if (torch_ci) {
-      const int taps = KT / torch_ci, tap = k / torch_ci, ci = k - tap * torch_ci;
-      float* o = dwp + ((size_t)co * torch_ci + ci) * taps + tap;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) o[(size_t)j * taps] += acc[j];
-    } else {
-      f32x4_w2* o = (f32x4_w2*)(dwp + e);
-      *o = *o + acc;
-    }
-  }
+  hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3((n4 + 15) / 16), dim3(256), 0, st, slab, splits, Cout, KT, ldn,
+                     dwp, torch_ci);
+  return (int)hipGetLastError();
 }
 
 template <int BM, int BN>
@@ -204,26 +215,12 @@ static int launch_wgrad_gemm(WgArgs a, float* dwp, hipStream_t st, int torch_ci)
   splits = (a.P + pps - 1) / pps;
   a.splits = splits;
   a.pix_per_split = pps;
-  const int groups = splits > WG_GROUP ? (splits + WG_GROUP - 1) / WG_GROUP : 0;
   const size_t slab_elems = (size_t)a.Cout * a.ldn;
-  void* buf = scratch(kSlotSlab, (size_t)(splits + groups) * slab_elems * sizeof(float), st);
+  void* buf = scratch(kSlotSlab, (size_t)splits * slab_elems * sizeof(float), st);
   if (!buf) return (int)hipErrorOutOfMemory;
   a.slab = (float*)buf;
   hipLaunchKernelGGL((wgrad_gemm_kernel<BM, BN>), dim3(tiles * splits), dim3(256), LDS, st, a);
-  const int n4 = a.Cout * a.KT / 4;
-  const int g1 = (n4 + 255) / 256 < 1024 ? (n4 + 255) / 256 : 1024;
-  const float* part = a.slab;
-  int nparts = splits;
-  if (groups) {
-    float* out = a.slab + (size_t)splits * slab_elems;
-    hipLaunchKernelGGL(wgrad_group_kernel, dim3(g1, groups), dim3(256), 0, st, (const float*)a.slab, splits, a.Cout,
-                       a.KT, a.ldn, out);
-    part = out;
-    nparts = groups;
-  }
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(g1), dim3(256), 0, st, part, nparts, a.Cout, a.KT, a.ldn, dwp,
-                     torch_ci);
-  return (int)hipGetLastError();
+  return reduce_slabs(a.slab, splits, a.Cout, a.KT, a.ldn, dwp, torch_ci, st);
 }
 
 // ---------------------------------------------------------------------------
@@ -233,7 +230,7 @@ static int launch_wgrad_gemm(WgArgs a, float* dwp, hipStream_t st, int torch_ci)
 //
 // * K (the reduction) = output pixels in steps of 64 consecutive pixels of one
 //   output row (Wo % 64 == 0); split-K over those row segments into slabs,
-//   reduced in order by wgrad_group / wgrad_reduce (deterministic).
+//   reduced in a fixed order by wgrad_slab_reduce (deterministic).
 // * B = im2col(x16): x16 is the fp16 NHWC copy of the conv input the AMP
 //   forward already made (compact, Cin channels); per step, NR 32-channel runs
 //   (tap, ci32) of the 64 pixels go global -> LDS by LDS-DMA ([run][pixel][32]
@@ -467,26 +464,12 @@ static int launch_wgrad16(Wg16Args a, float* dwp, hipStream_t st, int torch_ci) 
   splits = (a.units + ups - 1) / ups;
   a.splits = splits;
   a.units_per_split = ups;
-  const int groups = splits > WG_GROUP ? (splits + WG_GROUP - 1) / WG_GROUP : 0;
   const size_t slab_elems = (size_t)a.Cout * a.ldn;
-  void* buf = scratch(kSlotSlab, (size_t)(splits + groups) * slab_elems * sizeof(float), st);
+  void* buf = scratch(kSlotSlab, (size_t)splits * slab_elems * sizeof(float), st);
   if (!buf) return (int)hipErrorOutOfMemory;
   a.slab = (float*)buf;
   hipLaunchKernelGGL((wgrad16_kernel<BM, NR>), dim3(tiles * splits), dim3(256), LDS, st, a);
-  const int n4 = a.Cout * a.KT / 4;
-  const int g1 = (n4 + 255) / 256 < 1024 ? (n4 + 255) / 256 : 1024;
-  const float* part = a.slab;
-  int nparts = splits;
-  if (groups) {
-    float* out = a.slab + (size_t)splits * slab_elems;
-    hipLaunchKernelGGL(wgrad_group_kernel, dim3(g1, groups), dim3(256), 0, st, (const float*)a.slab, splits, a.Cout,
-                       a.KT, a.ldn, out);
-    part = out;
-    nparts = groups;
-  }
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(g1), dim3(256), 0, st, part, nparts, a.Cout, a.KT, a.ldn, dwp,
-                     torch_ci);
-  return (int)hipGetLastError();
+  return reduce_slabs(a.slab, splits, a.Cout, a.KT, a.ldn, dwp, torch_ci, st);
 }
 
 template <int BM>
@@ -770,9 +753,8 @@ static int launch_wgrad16h(Wg16hArgs a, float* dwp, hipStream_t st, int torch_ci
   a.spb = (a.steps_per_col + nrb - 1) / nrb;
   a.nrb = (a.steps_per_col + a.spb - 1) / a.spb;
   const int splits = a.B * a.nrb * a.segs;
-  const int groups = splits > WG_GROUP ? (splits + WG_GROUP - 1) / WG_GROUP : 0;
   const size_t slab_elems = (size_t)COUT * a.ldn;
-  void* buf = scratch(kSlotSlab, (size_t)(splits + groups) * slab_elems * sizeof(float), st);
+  void* buf = scratch(kSlotSlab, (size_t)splits * slab_elems * sizeof(float), st);
   if (!buf) return (int)hipErrorOutOfMemory;
   a.slab = (float*)buf;
   if (a.dy16)
@@ -780,19 +762,7 @@ static int launch_wgrad16h(Wg16hArgs a, float* dwp, hipStream_t st, int torch_ci
   else
     hipLaunchKernelGGL((wgrad16h_kernel<CIN, COUT, NTAP, RPW, D, false>), dim3(splits * a.ntg), dim3(256), 0, st, a);
   const int KT = C::TAPS * CIN;
-  const int n4 = COUT * KT / 4;
-  const int g1 = (n4 + 255) / 256 < 1024 ? (n4 + 255) / 256 : 1024;
-  const float* part = a.slab;
-  int nparts = splits;
-  if (groups) {
-    float* out = a.slab + (size_t)splits * slab_elems;
-    hipLaunchKernelGGL(wgrad_group_kernel, dim3(g1, groups), dim3(256), 0, st, (const float*)a.slab, splits, COUT, KT,
-                       a.ldn, out);
-    part = out;
-    nparts = groups;
-  }
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(g1), dim3(256), 0, st, part, nparts, COUT, KT, a.ldn, dwp, torch_ci);
-  return (int)hipGetLastError();
+  return reduce_slabs(a.slab, splits, COUT, KT, a.ldn, dwp, torch_ci, st);
 }
 
 // 32 -> 32 only: the one-kernel-row forms of 64 -> 32 / 32 -> 64 / 64 -> 64 measured

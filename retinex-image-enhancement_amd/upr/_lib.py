@@ -169,6 +169,7 @@ SIGNATURES.update({
     "upr_t_bilinear16": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _p, _i, _p]),
     "upr_t_add16": (_i, [_p, _p, _p, c_size_t, _p, _p]),
     "upr_t_maxpool_bwd_code": (_i, [_p, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _p]),
+    "upr_t_maxpool_bwd_code16": (_i, [_p, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p]),
     "upr_t_bilinear": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _p]),
     "upr_t_bilinear_bwd": (_i, [_vp, _i, _i, _i, _i, _i, _i, _vp, _p]),
     "upr_t_pixel_sum": (_i, [_p, _i, _i, _i, _i, _i, _f, _p, _i, _p]),

@@ -21,8 +21,8 @@ import torch
 import torch.nn as nn
 
 from . import _lib as L
-from .train import (Act, Conv, _chk, _fp, _p, _stream, autocast_active, empty, maxpool_into, pack_convs, relu_mask,
-                    set_amp, zero)
+from .train import (Act, Conv, _chk, _fp, _h16, _p, _stream, autocast_active, empty, maxpool_into, pack_convs,
+                    relu_mask, set_amp, zero)
 
 WEIGHTS = dict(exposure=10.0, smoothness=1.0, color=0.5, spatial=1.0, decouple=0.1, perceptual=1.0,
                frequency=0.5)
@@ -116,10 +116,25 @@ class VGGPerceptual:
                                              ctypes.c_float(0), ctypes.c_uint64(0), st), "add")
                 level -= 1
                 gi = Act.new(inp.B, inp.H, inp.W, inp.C, inp.t.device, fresh=False)
-                _chk(lib.upr_t_maxpool_bwd_code(_p(i), ctypes.byref(g.view()), inp.B, inp.H, inp.W, inp.C, 2, 2, 0,
-                                                out.H, out.W, ctypes.byref(gi.view()), 0, st), "pool_bwd")
-                g = gi
-                premasked = False
+                g_src, g, premasked = g, gi, False
+                # the next conv's ReLU mask and fp16 operand fused into the gather when
+                # that frozen conv reads the masked gradient in fp16 only (relu_mask's only16)
+                nxt = entries[j + 1] if j + 1 < len(entries) else None
+                if nxt is not None and nxt[0] == "conv" and inp.t16 is not None and inp.coff == 0 \
+                        and inp.cs == inp.C:
+                    cn = self.convs[nxt[1]]
+                    if cn.frozen and ((cn.amp and cn.mfma) or cn.dgrad16_c3):
+                        g16 = _h16(gi.M * gi.C, gi.t.device)
+                        rc = lib.upr_t_maxpool_bwd_code16(_p(i), ctypes.byref(g_src.view()), inp.B, inp.H, inp.W,
+                                                          inp.C, 2, 2, 0, out.H, out.W, _p(inp.t16), _p(g16), st)
+                        if rc == 0:
+                            gi.t16, gi.t16_grad, gi.stale32 = g16, True, True
+                            premasked = True
+                        elif rc != L.UPR_ERR_UNSUPPORTED:
+                            _chk(rc, "pool_bwd16")
+                if not premasked:
+                    _chk(lib.upr_t_maxpool_bwd_code(_p(i), ctypes.byref(g_src.view()), inp.B, inp.H, inp.W, inp.C, 2,
+                                                    2, 0, out.H, out.W, ctypes.byref(gi.view()), 0, st), "pool_bwd")
             else:
                 c = self.convs[i]
                 if not premasked:

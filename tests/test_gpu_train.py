@@ -291,6 +291,45 @@ def test_maxpool_code_fwd_bwd_matches_torch(B, C, H, W, k, s, p, acc):
     assert (out[m] - ref[m]).abs().max().item() <= 1e-6 * max(1.0, ref[m].abs().max().item())
 
 
+@pytest.mark.parametrize("B,C,H,W,k,s,p", [(2, 64, 32, 24, 2, 2, 0), (1, 32, 20, 28, 3, 1, 1), (1, 8, 33, 17, 2, 2, 0)])
+def test_maxpool_bwd_code16_fuses_relu_mask(B, C, H, W, k, s, p):
+    """upr_t_maxpool_bwd_code16 (the VGG pool backward with the producing
+    ReLU's mask and the fp16 operand fused) equals upr_t_maxpool_bwd_code then
+    upr_t_relu_mask16h bit for bit; without y16 it is the plain gather in fp16."""
+    import ctypes
+    from upr import _lib as L
+    torch.manual_seed(9)
+    x = torch.relu(torch.randn(B, H, W, C, device=DEV)).half()  # a ReLU's fp16 output (zeros included)
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    y = torch.empty(B, Ho, Wo, C, device=DEV)
+    code = torch.empty(B * Ho * Wo * C, dtype=torch.uint8, device=DEV)
+    gy = torch.randn(B, Ho, Wo, C, device=DEV)
+    vy = L.UprView(y.data_ptr(), Ho * Wo * C, Wo * C, C, 1)
+    vg = L.UprView(gy.data_ptr(), Ho * Wo * C, Wo * C, C, 1)
+    st = torch.cuda.current_stream().cuda_stream
+    lib = L.lib()
+    cp = ctypes.c_void_p(code.data_ptr())
+    assert lib.upr_t_maxpool16_code(ctypes.c_void_p(x.data_ptr()), B, H, W, C, k, s, p, ctypes.byref(vy), Ho, Wo, cp,
+                                    None, st) == 0
+    dx = torch.empty(B, H, W, C, device=DEV)
+    vd = L.UprView(dx.data_ptr(), H * W * C, W * C, C, 1)
+    assert lib.upr_t_maxpool_bwd_code(cp, ctypes.byref(vg), B, H, W, C, k, s, p, Ho, Wo, ctypes.byref(vd), 0, st) == 0
+    plain16 = dx.half()
+    ref16 = torch.empty(B * H * W * C, dtype=torch.float16, device=DEV)
+    assert lib.upr_t_relu_mask16h(ctypes.c_void_p(dx.data_ptr()), C, 0, ctypes.c_void_p(x.data_ptr()), C, B * H * W,
+                                  C, ctypes.c_void_p(ref16.data_ptr()), 0, st) == 0
+    got = torch.full_like(ref16, 7.0)
+    assert lib.upr_t_maxpool_bwd_code16(cp, ctypes.byref(vg), B, H, W, C, k, s, p, Ho, Wo,
+                                        ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(got.data_ptr()), st) == 0
+    got2 = torch.full_like(ref16, 7.0)
+    assert lib.upr_t_maxpool_bwd_code16(cp, ctypes.byref(vg), B, H, W, C, k, s, p, Ho, Wo, None,
+                                        ctypes.c_void_p(got2.data_ptr()), st) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref16)
+    assert torch.equal(got2, plain16.reshape(-1))
+    assert (ref16 == 0).float().mean().item() > 0.3  # the mask did something
+
+
 @pytest.mark.parametrize("B,C,H,W,Ho,Wo,sliced", [
     (2, 32, 16, 12, 64, 48, True),   # scale3 -> full resolution (4x) into a channel slice of the concat (vec4 path)
     (2, 32, 24, 20, 48, 40, False),  # scale2 -> full resolution (2x)
