@@ -68,6 +68,13 @@ int upr_t_conv_direct_dgrad(const UprView* dy, int Ho, int Wo, const float* w, i
 int upr_t_conv_direct_wgrad(const UprView* x, const UprView* dy, int B, int H, int W, int Cin, int Ho, int Wo,
                             int Cout, int kh, int kw, int stride, int pad, int dil, float* dw, float* dbias,
                             void* stream);
+/* The same with dy masked by y > 0 on the fly (y: the producing ReLU's output,
+ * dy's shape) -- a ReLU backward whose masked gradient only this weight
+ * gradient reads (the first conv of a stem, its input the image).  Cout <= 32
+ * on the generic small-channel kernel, else UPR_ERR_UNSUPPORTED. */
+int upr_t_conv_direct_wgrad_relu(const UprView* x, const UprView* dy, const UprView* y, int B, int H, int W, int Cin,
+                                 int Ho, int Wo, int Cout, int kh, int kw, int stride, int pad, int dil, float* dw,
+                                 float* dbias, void* stream);
 
 /* MFMA implicit-GEMM conv (the inference kernels of conv.hip/conv_halo.hip) on
  * NHWC sources with channel stride/offset; Cin, Cout multiples of 32.
@@ -347,11 +354,20 @@ int upr_t_fam_sa_apply(const float* o2, const float* s_pre, int B, int HW, int C
 /* g_o2 = g*sa; g_spre = sum_c(g*o2) * sa*(1-sa). */
 int upr_t_fam_sa_bwd(const float* g, const float* o2, const float* sa, int B, int HW, int C, float* g_o2,
                      float* g_spre, void* stream);
+/* The same with g a channel slice: pixel p's C gradients at g[p * g_cs]
+ * (the fusion concat's first slice read in place, no split copy). */
+int upr_t_fam_sa_bwd_cs(const float* g, int g_cs, const float* o2, const float* sa, int B, int HW, int C,
+                        float* g_o2, float* g_spre, void* stream);
 /* g_o2 += g_m (mean/max routes); g_o = g_o2*ca; g_ca[b][c] += sum_p g_o2*o. */
 int upr_t_fam_ca_bwd(const float* g_o2, const float* g_m, const float* o, const float* o2, const float* ca, int B,
                      int HW, int C, float* g_o, float* g_ca, void* stream);
 /* g_o = (g_o + g_pool[b][c]/HW) * (o > 0). */
 int upr_t_fam_pool_bwd(float* g_o, const float* g_pool, const float* o, int B, int HW, int C, void* stream);
+/* The same also writing g16 = the result's compact fp16 copy ([B*HW][C]; the
+ * fusion conv's autocast gradient operand).  C % 4 == 0 with C / 4 dividing
+ * 256 and 16-byte aligned g_o / g_pool / o, else UPR_ERR_UNSUPPORTED. */
+int upr_t_fam_pool_bwd16(float* g_o, const float* g_pool, const float* o, int B, int HW, int C, void* g16,
+                         void* stream);
 
 /* ---- network tail (model.py:351-358, 405-413, 439-455) ------------------ */
 /* illu = sigmoid(mean_c x + r): x [B,3,H,W], r [B,H,W] (1 channel), illu [B,1,H,W]. */

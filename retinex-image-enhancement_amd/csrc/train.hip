@@ -88,7 +88,8 @@ int small_conv_dgrad(const UprView* dyv, int Ho, int Wo, const float* w, int B, 
 int small_conv_dgrad_c3_16(const void* dy16, int B, int H, int W, const float* w, int Cout, const UprView* dxv,
                            int accumulate, hipStream_t st);
 int small_conv_wgrad(const UprView* xv, const UprView* dyv, int B, int H, int W, int Cin, int Ho, int Wo, int Cout,
-                     int kh, int kw, int stride, int pad, int dil, float* dw, float* dbias, hipStream_t st);
+                     int kh, int kw, int stride, int pad, int dil, float* dw, float* dbias, hipStream_t st,
+                     const UprView* ymask = nullptr);
 // train_wgrad.hip: split-K GEMM weight gradient (the conv_wgrad_kernel below takes the shapes it does not)
 int wgrad_gemm(const float* x, int B, int H, int W, int Cin, int x_cs, int x_coff, const float* dy, int Ho, int Wo,
                int Cout, int dy_cs, int dy_coff, int kh, int kw, int stride, int pad, int dil, float* dwp,
@@ -1450,7 +1451,7 @@ __global__ void fam_sa_apply_kernel(const float* __restrict__ o2, const float* _
   }
 }
 
-__global__ void fam_sa_bwd_kernel(const float* __restrict__ g, const float* __restrict__ o2,
+__global__ void fam_sa_bwd_kernel(const float* __restrict__ g, int g_cs, const float* __restrict__ o2,
                                   const float* __restrict__ sa, int B, int HW, int C, float* __restrict__ g_o2,
                                   float* __restrict__ g_spre) {
   const long long n = (long long)B * HW;
@@ -1458,7 +1459,7 @@ __global__ void fam_sa_bwd_kernel(const float* __restrict__ g, const float* __re
     const float a = sa[i];
     float t = 0.f;
     for (int c = 0; c < C; ++c) {
-      const float gv = g[i * C + c];
+      const float gv = g[i * g_cs + c];
       t += gv * o2[i * C + c];
       g_o2[i * C + c] = gv * a;
     }
@@ -1511,7 +1512,7 @@ __global__ void fam_sa_apply32_kernel(const float* __restrict__ o2, const float*
   }
 }
 
-__global__ void fam_sa_bwd32_kernel(const float* __restrict__ g, const float* __restrict__ o2,
+__global__ void fam_sa_bwd32_kernel(const float* __restrict__ g, int g_cs, const float* __restrict__ o2,
                                     const float* __restrict__ sa, int B, int HW, float* __restrict__ g_o2,
                                     float* __restrict__ g_spre) {
   const long long n = (long long)B * HW * 8;
@@ -1519,7 +1520,7 @@ __global__ void fam_sa_bwd32_kernel(const float* __restrict__ g, const float* __
     const long long pix = i >> 3;
     const int q = (int)(i & 7);
     const float a = sa[pix];
-    const float4 gv = ((const float4*)(g + pix * 32))[q];
+    const float4 gv = ((const float4*)(g + pix * g_cs))[q];
     const float4 ov = ((const float4*)(o2 + pix * 32))[q];
     float t = (gv.x * ov.x + gv.y * ov.y) + (gv.z * ov.z + gv.w * ov.w);
     ((float4*)(g_o2 + pix * 32))[q] = make_float4(gv.x * a, gv.y * a, gv.z * a, gv.w * a);
@@ -1655,6 +1656,33 @@ __global__ void fam_pool_bwd_kernel(float* g_o, const float* __restrict__ g_pool
     const int b = (int)(i / ((long long)HW * C));
     const float v = g_o[i] + g_pool[(size_t)b * C + c] / (float)HW;
     g_o[i] = o[i] > 0.f ? v : 0.f;
+  }
+}
+
+// the same, 4 channels per thread (the channels of a thread fixed: C / 4
+// divides 256), 32-bit offsets (host-checked), and optionally the compact fp16
+// copy g16 of the result (the fusion conv's autocast gradient operand)
+__global__ __launch_bounds__(256) void fam_pool_bwd4_kernel(float* g_o, const float* __restrict__ g_pool,
+                                                            const float* __restrict__ o, int M, int HW, int C,
+                                                            half_t* __restrict__ g16) {
+  const int C4 = C / 4, c = (threadIdx.x % C4) * 4, rpb = 256 / C4;
+  const float inv = 1.f / (float)HW;
+  for (int m = blockIdx.x * rpb + threadIdx.x / C4; m < M; m += gridDim.x * rpb) {
+    const int b = m / HW;
+    const int off = m * C + c;
+    const float4 gv = *(const float4*)(g_o + off), ov = *(const float4*)(o + off);
+    const float4 pv = *(const float4*)(g_pool + b * C + c);
+    float4 r;
+    // g_pool / HW as the scalar kernel: a division per element
+    r.x = ov.x > 0.f ? gv.x + pv.x / (float)HW : 0.f;
+    r.y = ov.y > 0.f ? gv.y + pv.y / (float)HW : 0.f;
+    r.z = ov.z > 0.f ? gv.z + pv.z / (float)HW : 0.f;
+    r.w = ov.w > 0.f ? gv.w + pv.w / (float)HW : 0.f;
+    *(float4*)(g_o + off) = r;
+    if (g16) {
+      typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+      *(h4*)(g16 + off) = h4{(half_t)r.x, (half_t)r.y, (half_t)r.z, (half_t)r.w};
+    }
   }
 }
 
@@ -2438,6 +2466,15 @@ int upr_t_conv_direct_dgrad(const UprView* dy, int Ho, int Wo, const float* w, i
   hipLaunchKernelGGL(conv_direct_dgrad_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), mkv(dy), Ho, Wo, w, B, H,
                      W, Cin, Cout, kh, kw, stride, pad, dil, mkv(dx), accumulate);
   LAUNCH_CHECK();
+}
+
+int upr_t_conv_direct_wgrad_relu(const UprView* x, const UprView* dy, const UprView* y, int B, int H, int W, int Cin,
+                                 int Ho, int Wo, int Cout, int kh, int kw, int stride, int pad, int dil, float* dw,
+                                 float* dbias, void* stream) {
+  if (!x || !dy || !y || !dw || B <= 0) return UPR_ERR_ARG;
+  const int rc = small_conv_wgrad(x, dy, B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pad, dil, dw, dbias, ST(stream),
+                                  y);
+  return rc == kErrUnsupported ? UPR_ERR_UNSUPPORTED : rc;
 }
 
 int upr_t_conv_direct_wgrad(const UprView* x, const UprView* dy, int B, int H, int W, int Cin, int Ho, int Wo,
@@ -3540,17 +3577,22 @@ int upr_t_fam_sa_apply(const float* o2, const float* s_pre, int B, int HW, int C
   LAUNCH_CHECK();
 }
 
-int upr_t_fam_sa_bwd(const float* g, const float* o2, const float* sa, int B, int HW, int C, float* g_o2,
-                     float* g_spre, void* stream) {
-  if (!g || !o2 || !sa || !g_o2 || !g_spre) return UPR_ERR_ARG;
-  if (C == 32 && al16(g) && al16(o2) && al16(g_o2)) {
-    hipLaunchKernelGGL(fam_sa_bwd32_kernel, dim3(grid_for((long long)B * HW * 8)), dim3(256), 0, ST(stream), g, o2, sa,
-                       B, HW, g_o2, g_spre);
+int upr_t_fam_sa_bwd_cs(const float* g, int g_cs, const float* o2, const float* sa, int B, int HW, int C,
+                        float* g_o2, float* g_spre, void* stream) {
+  if (!g || !o2 || !sa || !g_o2 || !g_spre || g_cs < C) return UPR_ERR_ARG;
+  if (C == 32 && g_cs % 4 == 0 && al16(g) && al16(o2) && al16(g_o2)) {
+    hipLaunchKernelGGL(fam_sa_bwd32_kernel, dim3(grid_for((long long)B * HW * 8)), dim3(256), 0, ST(stream), g, g_cs,
+                       o2, sa, B, HW, g_o2, g_spre);
     LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(fam_sa_bwd_kernel, dim3(grid_for((long long)B * HW)), dim3(256), 0, ST(stream), g, o2, sa, B,
-                     HW, C, g_o2, g_spre);
+  hipLaunchKernelGGL(fam_sa_bwd_kernel, dim3(grid_for((long long)B * HW)), dim3(256), 0, ST(stream), g, g_cs, o2, sa,
+                     B, HW, C, g_o2, g_spre);
   LAUNCH_CHECK();
+}
+
+int upr_t_fam_sa_bwd(const float* g, const float* o2, const float* sa, int B, int HW, int C, float* g_o2,
+                     float* g_spre, void* stream) {
+  return upr_t_fam_sa_bwd_cs(g, C, o2, sa, B, HW, C, g_o2, g_spre, stream);
 }
 
 int upr_t_fam_ca_bwd(const float* g_o2, const float* g_m, const float* o, const float* o2, const float* ca, int B,
@@ -3576,11 +3618,24 @@ int upr_t_fam_ca_bwd(const float* g_o2, const float* g_m, const float* o, const 
   LAUNCH_CHECK();
 }
 
-int upr_t_fam_pool_bwd(float* g_o, const float* g_pool, const float* o, int B, int HW, int C, void* stream) {
-  if (!g_o || !g_pool || !o) return UPR_ERR_ARG;
+int upr_t_fam_pool_bwd16(float* g_o, const float* g_pool, const float* o, int B, int HW, int C, void* g16,
+                         void* stream) {
+  if (!g_o || !g_pool || !o || B <= 0 || HW <= 0 || C <= 0) return UPR_ERR_ARG;
   const long long n = (long long)B * HW * C;
+  if (C % 4 == 0 && 256 % (C / 4) == 0 && n < (1LL << 31) && al16(g_o) && al16(g_pool) && al16(o) &&
+      (uintptr_t)g16 % 8 == 0) {
+    const long long M = (long long)B * HW;
+    hipLaunchKernelGGL(fam_pool_bwd4_kernel, dim3(grid_for(M * (C / 4))), dim3(256), 0, ST(stream), g_o, g_pool, o,
+                       (int)M, HW, C, (half_t*)g16);
+    LAUNCH_CHECK();
+  }
+  if (g16) return UPR_ERR_UNSUPPORTED;
   hipLaunchKernelGGL(fam_pool_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), g_o, g_pool, o, B, HW, C);
   LAUNCH_CHECK();
+}
+
+int upr_t_fam_pool_bwd(float* g_o, const float* g_pool, const float* o, int B, int HW, int C, void* stream) {
+  return upr_t_fam_pool_bwd16(g_o, g_pool, o, B, HW, C, nullptr, stream);
 }
 
 int upr_t_head_fwd(const float* x, const float* r, float* illu, int B, int H, int W, void* stream) {

@@ -235,7 +235,7 @@ class TotalLoss(_EngineHolder):
         # weights of this step (loss.py:690-702): DWA from the history after epoch 1
         eng.w = self._compute_adaptive_weights() if self.adaptive_weights and epoch > 1 else dict(self._weights)
         total, terms = loss_forward(eng, img_low.contiguous(), img_enhanced, illu_map, reflectance)
-        d = E.terms_dict(terms)
+        d = E.terms_dict(terms, lazy=_DEFER_READBACK[0] and not self.adaptive_weights)
         if self.adaptive_weights:
             for k in _DWA_KEYS:
                 self.loss_history[k].append(d[k])
@@ -250,6 +250,21 @@ class TotalLoss(_EngineHolder):
 
 
 _DWA_KEYS = ("exposure", "smoothness", "color", "spatial", "decouple", "perceptual", "frequency")
+
+# set by trainers.train.train_step around its criterion call: the loss_dict's
+# host read-back is deferred until the step's backward and optimizer work is
+# queued (the step returns it materialised), instead of draining the device
+# between the forward and the backward as the reference's .item()s do
+_DEFER_READBACK = [False]
+
+
+class deferred_readback:
+    def __enter__(self):
+        self._prev = _DEFER_READBACK[0]
+        _DEFER_READBACK[0] = True
+
+    def __exit__(self, *exc):
+        _DEFER_READBACK[0] = self._prev
 
 
 def dwa_weights(history, defaults, temperature=2.0):

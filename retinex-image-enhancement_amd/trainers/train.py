@@ -19,6 +19,7 @@ import time
 
 import torch
 
+from losses.loss import deferred_readback
 from upr import amp as uamp
 from upr import optim as uoptim
 
@@ -48,7 +49,10 @@ def train_step(model, img_low, criterion, optimizer, max_norm=1.0, scaler=None, 
     backward and the unscale / clip."""
     optimizer.zero_grad()
     scaler = _as_upr_scaler(scaler) if use_amp else None
-    with torch.autocast("cuda", dtype=torch.float16, enabled=scaler is not None and amp_fp16):
+    # the loss_dict's floats are read back after the backward / optimizer work is
+    # queued (returned materialised), not between forward and backward
+    with torch.autocast("cuda", dtype=torch.float16, enabled=scaler is not None and amp_fp16), \
+            deferred_readback():
         img_enhanced, reflectance, illu_map = model(img_low)
         loss, loss_dict = criterion(img_low, img_enhanced, illu_map, reflectance)
     if scaler is not None:
@@ -65,7 +69,7 @@ def train_step(model, img_low, criterion, optimizer, max_norm=1.0, scaler=None, 
             grad_hook()
         clip_grad_norm_(model.parameters(), max_norm=max_norm)
         optimizer.step()
-    return loss, loss_dict
+    return loss, (dict(loss_dict.items()) if type(loss_dict) is not dict else loss_dict)
 
 
 def train_one_epoch(model, dataloader, criterion, optimizer, device, epoch, writer=None, scaler=None, use_amp=False):

@@ -120,6 +120,8 @@ SIGNATURES.update({
                                  _p]),
     "upr_t_conv_direct_dgrad": (_i, [_vp, _i, _i, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _p]),
     "upr_t_conv_direct_wgrad": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p]),
+    "upr_t_conv_direct_wgrad_relu": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p,
+                                          _p]),
     "upr_t_conv_mfma": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _p, _i, _i, _i, _i, _i, _i, _p, _i, _i, _p, _i, _i,
                              _i, _p]),
     "upr_t_conv_mfma16": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _p, _i, _i, _i, _i, _i, _i, _p, _i, _i, _p, _i, _i,
@@ -177,8 +179,10 @@ SIGNATURES.update({
     "upr_t_fam_ca_apply": (_i, [_p, _p, _i, _i, _i, _p, _p, _p]),
     "upr_t_fam_sa_apply": (_i, [_p, _p, _i, _i, _i, _p, _p, _p]),
     "upr_t_fam_sa_bwd": (_i, [_p, _p, _p, _i, _i, _i, _p, _p, _p]),
+    "upr_t_fam_sa_bwd_cs": (_i, [_p, _i, _p, _p, _i, _i, _i, _p, _p, _p]),
     "upr_t_fam_ca_bwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p]),
     "upr_t_fam_pool_bwd": (_i, [_p, _p, _p, _i, _i, _i, _p]),
+    "upr_t_fam_pool_bwd16": (_i, [_p, _p, _p, _i, _i, _i, _p, _p]),
     "upr_t_head_fwd": (_i, [_p, _p, _p, _i, _i, _i, _p]),
     "upr_t_retinex_fwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _p]),
     "upr_t_retinex_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p]),

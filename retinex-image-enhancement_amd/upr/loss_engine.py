@@ -266,10 +266,97 @@ class TotalLossEngine:
                                                                                   else 0.0), st), "total")
 
 
-def terms_dict(terms):
-    """One device->host copy of the 9 loss scalars -> the reference's loss_dict
-    (loss.py:741-751) + the dynamic smooth weight."""
-    v = terms.cpu().tolist()
-    d = {k: v[i] for i, k in enumerate(TERM_ORDER)}
-    d["smooth_weight"] = v[8]
-    return d
+class LossDict(dict):
+    """The reference's loss_dict (loss.py:741-751: python floats from .item())
+    plus the dynamic smooth weight, read back lazily: the 9 scalars go to a
+    pinned host buffer by an asynchronous copy queued behind the loss kernels,
+    and the first read of the dict waits for that copy alone.  The reference
+    syncs the host in the middle of every step here (its .item()s before the
+    backward); this leaves the device queue full until a caller actually reads
+    a value.  Every dict access path materialises first."""
+
+    __slots__ = ("_host", "_ev")
+
+    def __init__(self, terms):
+        super().__init__()
+        self._host = torch.empty(terms.shape, dtype=terms.dtype, pin_memory=True)
+        self._host.copy_(terms, non_blocking=True)
+        self._ev = torch.cuda.Event()
+        self._ev.record(torch.cuda.current_stream(terms.device))
+
+    def _m(self):
+        if self._ev is not None:
+            self._ev.synchronize()
+            v = self._host.tolist()
+            for i, k in enumerate(TERM_ORDER):
+                dict.__setitem__(self, k, v[i])
+            dict.__setitem__(self, "smooth_weight", v[8])
+            self._ev = self._host = None
+        return self
+
+    def __getitem__(self, k):
+        return dict.__getitem__(self._m(), k)
+
+    def __setitem__(self, k, v):
+        dict.__setitem__(self._m(), k, v)
+
+    def __delitem__(self, k):
+        dict.__delitem__(self._m(), k)
+
+    def __iter__(self):
+        return dict.__iter__(self._m())
+
+    def __len__(self):
+        return dict.__len__(self._m())
+
+    def __contains__(self, k):
+        return dict.__contains__(self._m(), k)
+
+    def __repr__(self):
+        return dict.__repr__(self._m())
+
+    def __eq__(self, o):
+        return dict.__eq__(self._m(), o)
+
+    def __ne__(self, o):
+        return dict.__ne__(self._m(), o)
+
+    __hash__ = None
+
+    def __reduce__(self):
+        return (dict, (dict(self.items()),))
+
+    def get(self, k, default=None):
+        return dict.get(self._m(), k, default)
+
+    def keys(self):
+        return dict.keys(self._m())
+
+    def values(self):
+        return dict.values(self._m())
+
+    def items(self):
+        return dict.items(self._m())
+
+    def copy(self):
+        return dict(self.items())
+
+    def pop(self, *a):
+        return dict.pop(self._m(), *a)
+
+    def popitem(self):
+        return dict.popitem(self._m())
+
+    def setdefault(self, *a):
+        return dict.setdefault(self._m(), *a)
+
+    def update(self, *a, **kw):
+        return dict.update(self._m(), *a, **kw)
+
+
+def terms_dict(terms, lazy=False):
+    """The 9 device loss scalars -> the reference's loss_dict.  lazy: a LossDict
+    still waiting for its copy (the training step reads it back after its
+    backward is queued); otherwise read back now, as the reference's .item()s."""
+    d = LossDict(terms)
+    return d if lazy else d._m()

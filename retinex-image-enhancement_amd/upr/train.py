@@ -473,6 +473,30 @@ class Conv:
         gx.t16_grad = keep
         return True
 
+    def bwd_relu_stem(self, x, gy, y, x_view=None):
+        """relu_mask(gy, y) then bwd(x, gy, None, x_view): the weight gradient of a
+        conv whose input needs no gradient (the image stems), the ReLU backward of
+        its output y fused into the small-channel weight-gradient kernel (gy is
+        left unmasked: this is its only reader)."""
+        if not self.frozen and not (self.mfma and x_view is None) and not gy.stale32 and not y.stale32:
+            lib, st = L.lib(), _stream()
+            if x_view is not None:
+                xv, B, H, W = x_view
+            else:
+                xv, B, H, W = x.view(), x.B, x.H, x.W
+            with _timed("direct", "wgrad", self.flops(B, gy.H, gy.W), (self.Cin, self.Cout, self.kh, self.s, H, W)):
+                rc = lib.upr_t_conv_direct_wgrad_relu(ctypes.byref(xv), ctypes.byref(gy.view()),
+                                                      ctypes.byref(y.view()), B, H, W, self.Cin, gy.H, gy.W,
+                                                      self.Cout, self.kh, self.kw, self.s, self.p, self.d,
+                                                      _p(self.m.weight.grad),
+                                                      _p(self.bias.grad) if self.bias is not None else None, st)
+            if rc == 0:
+                return
+            if rc != L.UPR_ERR_UNSUPPORTED:
+                _chk(rc, "conv_direct_wgrad_relu")
+        relu_mask(gy, y)
+        self.bwd(x, gy, None, x_view=x_view)
+
     def bwd(self, x, gy, gx=None, x_view=None, mask=None, gx_only16=False, gx_keep16=False):
         """gy: Act gradient of this conv's output (pre-activation).
         Accumulates the weight / bias gradients; gx (Act, nullable) receives
@@ -685,11 +709,14 @@ class ConvT:
         lib, st = L.lib(), _stream()
         F = self.flops(x)
         kind = "mfma16" if self.amp else "mfma32"
+        # gy's fp16 copy from its producer (UpBlockT: the following conv's input gradient,
+        # gx_keep16) is both GEMMs' fp16 operand as is -- no internal cast passes
+        gy16 = gy.t16 if self.amp and gy.t16 is not None and gy.t16_grad and gy.coff == 0 and gy.cs == gy.C else None
         with _timed(kind, "wgrad", F):
             zero(self.gp)
             # dwp[ci][(a,b,co)] = sum_p x[p][ci] * gy[2y+a][2x+b][co]: a k2 s2 "conv" of gy producing x
             if self.amp:
-                _chk(lib.upr_t_conv_wgrad16(gy.ptr(), None, gy.B, gy.H, gy.W, self.Cout, gy.cs, 0, x.ptr(), x.H, x.W,
+                _chk(lib.upr_t_conv_wgrad16(gy.ptr(), _p(gy16), gy.B, gy.H, gy.W, self.Cout, gy.cs, 0, x.ptr(), x.H, x.W,
                                             self.Cin, x.cs, 0, 2, 2, 2, 0, 1, _p(self.gp), st), "convT_wgrad16")
             else:
                 _chk(lib.upr_t_conv_wgrad(gy.ptr(), gy.B, gy.H, gy.W, self.Cout, gy.cs, 0, x.ptr(), x.H, x.W, self.Cin,
@@ -701,7 +728,7 @@ class ConvT:
             acc = gx.consume_fresh()
             if self.amp:
                 Conv._mfma16(self, gy.t, gy.B, gy.H, gy.W, self.Cout, gy.cs, gy.coff, self.wd16, None, self.Cin, 2, 2, 2,
-                             0, 1, gx if acc else None, False, gx)
+                             0, 1, gx if acc else None, False, gx, x16=gy16)
             else:
                 _chk(lib.upr_t_conv_mfma(gy.ptr(), gy.B, gy.H, gy.W, self.Cout, gy.cs, 0, _p(self.wd), None, self.Cin, 2,
                                          2, 2, 0, 1, gx.ptr() if acc else None, gx.cs if acc else 0, 0, _fp(gx.t),
@@ -770,7 +797,8 @@ class BN:
         self.x = x
         self.out_act = out
         self.batch_stats = bool(m.training)  # the backward follows the statistics this forward used
-        self.relu_only = bool(relu) and res is None  # y = relu(bn(x)): the backward may fold the mask in
+        # y = relu(bn(x)) (+ a residual added after the ReLU): the backward may fold the mask in
+        self.relu_only = bool(relu) and (res is None or bool(res_post))
         return out
 
     def bwd(self, g, gx, relu=False, only16=False):
@@ -1112,12 +1140,9 @@ class UpBlockT:
         self.u = self.up.fwd(x)
         c1 = self.c1.fwd(self.u, only16=True)
         self.a1 = self.b1.fwd(c1, relu=True, only16=self.c2.wgrad16_ok(c1.W))
-        self.a2 = self.b2.fwd(self.c2.fwd(self.a1, only16=True), relu=True)
-        if skip is None:
-            return self.a2
-        out = Act.new(self.a2.B, self.a2.H, self.a2.W, self.a2.C, x.t.device, fresh=False)
-        add_acts(self.a2, skip, out)
-        return out
+        # the skip add (model.py:346-348) in the BatchNorm apply's epilogue: relu(bn(c2)) + skip,
+        # the same fp32 operations as the separate add
+        return self.b2.fwd(self.c2.fwd(self.a1, only16=True), relu=True, res=skip, res_post=skip is not None)
 
     def bwd(self, g, gx, g_skip=None):
         dev = g.t.device
@@ -1130,7 +1155,7 @@ class UpBlockT:
         g_c1 = Act.new(g.B, g.H, g.W, g.C, dev)
         self.b1.bwd(g_a1, g_c1, relu=True, only16=self.c1.takes16_grad())
         g_u = Act.new(g.B, g.H, g.W, g.C, dev)
-        self.c1.bwd(self.u, g_c1, g_u)
+        self.c1.bwd(self.u, g_c1, g_u, gx_keep16=True)  # + the fp16 copy ConvT's backward reads
         self.up.bwd(self.x, g_u, gx)
 
 
@@ -1193,14 +1218,16 @@ class FAMT:
         return out
 
     def bwd(self, g, gx):
-        """g: contiguous Act [B,H,W,32]; gx receives the input gradient."""
+        """g: Act [B,H,W,32] (a channel slice of a wider tensor allowed); gx receives the input gradient."""
         dev = g.t.device
         lib, st = L.lib(), _stream()
         B, H, W, C = g.B, g.H, g.W, self.fu.Cout
         HW = H * W
         g_o2 = empty((B, H, W, C), dev)
         g_s = Act.new(B, H, W, 1, dev, fresh=False)
-        _chk(lib.upr_t_fam_sa_bwd(_fp(g.t), _p(self.o2), _p(self.sav), B, HW, C, _p(g_o2), _fp(g_s.t), st), "sa_bwd")
+        assert not g.stale32, "FAM backward reads the fp32 gradient"
+        _chk(lib.upr_t_fam_sa_bwd_cs(g.ptr(), g.cs, _p(self.o2), _p(self.sav), B, HW, C, _p(g_o2), _fp(g_s.t), st),
+             "sa_bwd")
         g_m = Act.new(B, H, W, 2, dev)
         self.sa.bwd(self.m, g_s, g_m)
         g_o = Act.new(B, H, W, C, dev, fresh=False)
@@ -1214,7 +1241,11 @@ class FAMT:
         relu_mask(g_h1, self.h1)
         g_pool = Act.new(B, 1, 1, C, dev)
         self.ca1.bwd(self.pool, g_h1, g_pool)
-        _chk(lib.upr_t_fam_pool_bwd(_fp(g_o.t), _fp(g_pool.t), _fp(self.o.t), B, HW, C, st), "pool_bwd")
+        # under autocast the fusion conv's gradient operand (its fp16 copy) comes out of the same pass
+        g16 = _h16(g_o.M * C, dev) if self.fu.amp and self.fu.mfma else None
+        _chk(lib.upr_t_fam_pool_bwd16(_fp(g_o.t), _fp(g_pool.t), _fp(self.o.t), B, HW, C, _p(g16), st), "pool_bwd")
+        if g16 is not None:
+            g_o.t16, g_o.t16_grad = g16, True
         g_cat = Act.new(B, H, W, 4 * C, dev)
         # the four branch convs read slices of its fp16 copy; no fp32 store when every one of
         # them takes an fp16 gradient (their weight gradients on the fp16 GEMM: Wo % 64)
@@ -1303,8 +1334,7 @@ class IENetT:
         self.enc[2].bwd(g_t, g_x3)
         self.enc[1].bwd(g_x3, g_x2)
         self.enc[0].bwd(g_x2, g_x1)
-        relu_mask(g_x1, self.x1)
-        self.inp.bwd(None, g_x1, None, x_view=self.xin)
+        self.inp.bwd_relu_stem(None, g_x1, self.x1, x_view=self.xin)
 
 
 class UPRetinexTrainGraph:
@@ -1410,19 +1440,17 @@ class UPRetinexTrainGraph:
         for (sc, sf, s_act, xin), i in zip(((self.s1c, self.s1f, self.s1, None),
                                             (self.s2c, self.s2f, self.s2, self.pyr[0]),
                                             (self.s3c, self.s3f, self.s3, self.pyr[1])), range(3)):
-            g_f = Act.new(s_act.B, s_act.H, s_act.W, 32, dev, fresh=False)
             if i == 0:
-                _chk(lib.upr_t_copy(ctypes.byref(g_fused.slice(0, 32).view()), ctypes.byref(g_f.view()), B, H, W, 32, 0,
-                                    st), "split")
+                g_f = g_fused.slice(0, 32)  # read in place by the FAM backward (no split copy)
             else:
+                g_f = Act.new(s_act.B, s_act.H, s_act.W, 32, dev, fresh=False)
                 zero(g_f.t)
                 _chk(lib.upr_t_bilinear_bwd(ctypes.byref(g_fused.slice(32 * i, 32).view()), B, g_f.H, g_f.W, 32, H, W,
                                             ctypes.byref(g_f.view()), st), "upsample_bwd")
             g_s = Act.new(s_act.B, s_act.H, s_act.W, 32, dev)
             sf.bwd(g_f, g_s)
-            relu_mask(g_s, s_act)
             if i == 0:
-                sc.bwd(None, g_s, None, x_view=(nchw_view(x), B, H, W))
+                sc.bwd_relu_stem(None, g_s, s_act, x_view=(nchw_view(x), B, H, W))
             else:
-                sc.bwd(xin, g_s, None)
+                sc.bwd_relu_stem(xin, g_s, s_act)
         self.ie.bwd(g_r)

@@ -81,6 +81,52 @@ def test_conv_layer(cin, cout, k, s, p, d, bias):
         _close(md.bias.grad, m.bias.grad, 1e-4, "dbias")
 
 
+@pytest.mark.parametrize("nchw", [True, False])
+def test_stem_relu_fused_into_wgrad(nchw):
+    """Conv.bwd_relu_stem (upr_t_conv_direct_wgrad_relu: the stem's ReLU
+    backward applied to dy inside the small-channel weight-gradient kernel)
+    equals relu_mask + the plain direct weight gradient bit for bit, and the
+    torch weight / bias gradient of relu(conv(x)) within 1e-4."""
+    from upr.train import Act, Conv, nchw_view, relu_mask
+    torch.manual_seed(5)
+    B, H, W = 2, 40, 56
+    m = torch.nn.Conv2d(3, 32, 3, padding=1)
+    x = torch.rand(B, 3, H, W)
+    w0 = m.weight.detach().clone()
+    gy = torch.randn(B, 32, H, W)
+    mr = torch.nn.Conv2d(3, 32, 3, padding=1)
+    mr.load_state_dict(m.state_dict())
+    torch.relu(mr(x)).backward(gy)
+    outs = []
+    for fused in (True, False):
+        md = torch.nn.Conv2d(3, 32, 3, padding=1).to(DEV)
+        md.load_state_dict(m.state_dict())
+        md.weight.grad = torch.zeros_like(md.weight)
+        md.bias.grad = torch.zeros_like(md.bias)
+        c = Conv(md)
+        c.pack()
+        xd = x.to(DEV).contiguous()
+        xa = Act(x.permute(0, 2, 3, 1).contiguous().to(DEV))
+        if nchw:
+            xv = (nchw_view(xd), B, H, W)
+            y = c.fwd(None, relu=True, x_view=xv, out=Act.new(B, H, W, 32, DEV, fresh=False))
+        else:
+            xv = None
+            y = c.fwd(xa, relu=True)
+        g = Act(gy.permute(0, 2, 3, 1).contiguous().to(DEV))
+        if fused:
+            c.bwd_relu_stem(None if nchw else xa, g, y, x_view=xv)
+        else:
+            relu_mask(g, y)
+            c.bwd(None if nchw else xa, g, None, x_view=xv)
+        torch.cuda.synchronize()
+        outs.append((md.weight.grad.clone(), md.bias.grad.clone()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    _close(outs[0][0], mr.weight.grad, 1e-4, "stem wgrad")
+    _close(outs[0][1], mr.bias.grad, 1e-4, "stem dbias")
+    assert torch.equal(m.weight.detach(), w0)
+
+
 @pytest.mark.parametrize("B,cin,cout,H,W,k,s,p,d", [
     (2, 32, 32, 64, 128, 3, 1, 1, 1),    # 32 -> 32 3x3 (dec1 / head / FAM class): BM 32, 9 runs per tile
     (1, 64, 128, 128, 128, 3, 2, 1, 1),  # encoder stride-2 conv: BM 128, 4 runs

@@ -64,6 +64,15 @@ def main():
         step()
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / steps
+    # enqueue time of one step from an idle device (host-bound when close to the wall)
+    for _ in range(4):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        step()
+        t1 = time.perf_counter()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        print(f"one step: host enqueue {(t1 - t0) * 1e3:.2f} ms, to device idle {(t2 - t0) * 1e3:.2f} ms")
     prox = _Timed(L.lib())
     L._lib = prox
     pr = cProfile.Profile()
