@@ -141,6 +141,12 @@ int upr_t_conv_wgrad16(const float* x, const void* x16, int B, int H, int W, int
 int upr_t_conv_mfma16_relu_bwd(const void* x16, int B, int H, int W, int Cin, const void* wp16, int N, int kh, int kw,
                                int pad, int dil, float* y, int y_cs, int y_coff, void* y16, int y16_cs,
                                const void* mask16, int mask16_cs, int skip32, void* stream);
+/* The same with x16 a channel slice of a wider fp16 tensor: pixel p's Cin
+ * values at x16[p * x16_cs] (x16 points at the slice's first channel; x16_cs
+ * % 8 == 0) -- a slice of a shared concat gradient copy read in place. */
+int upr_t_conv_mfma16_relu_bwd_cs(const void* x16, int x16_cs, int B, int H, int W, int Cin, const void* wp16, int N,
+                                  int kh, int kw, int pad, int dil, float* y, int y_cs, int y_coff, void* y16,
+                                  int y16_cs, const void* mask16, int mask16_cs, int skip32, void* stream);
 /* The weight gradient added straight into PyTorch's layout: dw[co][ci][ky][kx]
  * += (no packed buffer, zero fill or unpack pass).  x16 non-NULL: the AMP
  * arithmetic of upr_t_conv_wgrad16 (x may then be NULL when the fp16 path

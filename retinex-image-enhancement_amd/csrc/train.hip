@@ -2661,10 +2661,17 @@ int upr_t_conv_mfma16(const float* x, int B, int H, int W, int Cin, int x_cs, in
 int upr_t_conv_mfma16_relu_bwd(const void* x16, int B, int H, int W, int Cin, const void* wp16, int N, int kh, int kw,
                                int pad, int dil, float* y, int y_cs, int y_coff, void* y16, int y16_cs,
                                const void* mask16, int mask16_cs, int skip32, void* stream) {
+  return upr_t_conv_mfma16_relu_bwd_cs(x16, Cin, B, H, W, Cin, wp16, N, kh, kw, pad, dil, y, y_cs, y_coff, y16, y16_cs,
+                                       mask16, mask16_cs, skip32, stream);
+}
+
+int upr_t_conv_mfma16_relu_bwd_cs(const void* x16, int x16_cs, int B, int H, int W, int Cin, const void* wp16, int N,
+                                  int kh, int kw, int pad, int dil, float* y, int y_cs, int y_coff, void* y16,
+                                  int y16_cs, const void* mask16, int mask16_cs, int skip32, void* stream) {
   if (!x16 || !wp16 || !y || !y16 || !mask16 || B <= 0 || Cin % 32 || N % 32 || Cin <= 0 || N <= 0) return UPR_ERR_ARG;
-  if (kh <= 0 || kw <= 0 || dil <= 0 || pad < 0) return UPR_ERR_ARG;
+  if (kh <= 0 || kw <= 0 || dil <= 0 || pad < 0 || x16_cs < Cin) return UPR_ERR_ARG;
   if (((uintptr_t)x16 | (uintptr_t)y16 | (uintptr_t)mask16) % 16 || y16_cs % 8 || mask16_cs % 8 || y_cs % 4 ||
-      y_coff % 4 || (uintptr_t)y % 16)
+      y_coff % 4 || (uintptr_t)y % 16 || x16_cs % 8)
     return UPR_ERR_UNSUPPORTED;
   const int Ho = H + 2 * pad - dil * (kh - 1), Wo = W + 2 * pad - dil * (kw - 1);
   if (Ho <= 0 || Wo <= 0) return UPR_ERR_SHAPE;
@@ -2672,7 +2679,7 @@ int upr_t_conv_mfma16_relu_bwd(const void* x16, int B, int H, int W, int Cin, co
   memset(&c, 0, sizeof(c));
   c.nseg = 1;
   ConvSeg& sg = c.seg[0];
-  sg.src = x16; sg.C = Cin; sg.cs = Cin; sg.coff = 0; sg.Hin = H; sg.Win = W;
+  sg.src = x16; sg.C = Cin; sg.cs = x16_cs; sg.coff = 0; sg.Hin = H; sg.Win = W;
   sg.kh = kh; sg.kw = kw; sg.stride = 1; sg.pad = pad; sg.dil = dil; sg.pre = kPreNone; sg.kbase = 0;
   c.B = B; c.Ho = Ho; c.Wo = Wo; c.N = N; c.Kpad = kh * kw * Cin;
   c.W = wp16; c.bias = nullptr; c.relu = 0;

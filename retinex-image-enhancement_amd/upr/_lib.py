@@ -131,6 +131,8 @@ SIGNATURES.update({
     "upr_t_conv_wgrad16": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p]),
     "upr_t_conv_mfma16_relu_bwd": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p, _i, _i, _p, _i, _p, _i, _i,
                                         _p]),
+    "upr_t_conv_mfma16_relu_bwd_cs": (_i, [_p, _i, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p, _i, _i, _p, _i, _p,
+                                           _i, _i, _p]),
     "upr_t_conv_wgrad_into": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i,
                                    _p, _p]),
     "upr_t_pack_weight": (_i, [_p, _p, _i, _i, _i, _i, _i, _p]),

@@ -563,14 +563,18 @@ class Conv:
                 acc = gx.consume_fresh()
                 src, sH, sW, scs, scoff = gy.t, Ho, Wo, gy.cs, gy.coff
                 src16 = gy.t16 if self.amp and gy.t16_grad and gy.coff == 0 and gy.cs == gy.C == self.Cout else None
-                if mask is not None and self.amp and self.s == 1 and not acc and src16 is not None and \
+                # a channel slice of a shared concat copy: its pixels at gy.t16[p * gy.cs + gy.coff]
+                m16, m16cs = (src16, self.Cout) if src16 is not None else \
+                    ((ctypes.c_void_p(gy.t16.data_ptr() + 2 * gy.coff), gy.cs)
+                     if self.amp and gy.t16_grad and gy.t16_shared and gy.C == self.Cout else (None, 0))
+                if mask is not None and self.amp and self.s == 1 and not acc and m16 is not None and \
                         gx.coff == 0 and gx.cs == gx.C == self.Cin:
                     a16, mcs, only16 = mask
                     y16 = _h16(B * H * W * self.Cin, gx.t.device)
-                    rc = lib.upr_t_conv_mfma16_relu_bwd(_p(src16), B, Ho, Wo, self.Cout, _p(self.wt16), self.Cin,
-                                                        self.kh, self.kw, self.d * (self.kh - 1) - self.p, self.d,
-                                                        _fp(gx.t), gx.cs, 0, _p(y16), self.Cin, _p(a16), mcs,
-                                                        int(only16), st)
+                    rc = lib.upr_t_conv_mfma16_relu_bwd_cs(_p(m16) if m16 is src16 else m16, m16cs, B, Ho, Wo,
+                                                           self.Cout, _p(self.wt16), self.Cin, self.kh, self.kw,
+                                                           self.d * (self.kh - 1) - self.p, self.d, _fp(gx.t), gx.cs,
+                                                           0, _p(y16), self.Cin, _p(a16), mcs, int(only16), st)
                     if rc == 0:
                         gx.t16, gx.t16_grad, gx.stale32 = y16, True, bool(only16)
                         return True
@@ -1261,8 +1265,11 @@ class FAMT:
         for (ca_, cb_, t) in ((self.b3a, self.b3b, self.t3), (self.b4a, self.b4b, self.t4)):
             k = 2 if cb_ is self.b3b else 3
             g_t = Act.new(B, H, W, t.C, dev)
-            cb_.bwd(t, g_cat.slice(k * C, C), g_t)
-            relu_mask(g_t, t, want16=ca_.amp and ca_.mfma)
+            # the ReLU backward of t fused into this input gradient's epilogue (t's fp16 copy as
+            # the mask); fp32 g_t skipped when the consuming conv takes the fp16 gradient only
+            mask = (t.t16, t.C, ca_.takes16_grad()) if t.t16 is not None and t.whole16() else None
+            if not cb_.bwd(t, g_cat.slice(k * C, C), g_t, mask=mask):
+                relu_mask(g_t, t, want16=ca_.amp and ca_.mfma)
             ca_.bwd(self.x, g_t, gx)
 
 

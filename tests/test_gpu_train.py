@@ -643,6 +643,20 @@ def test_shared_concat_fp16_slices():
         outs.append(y)
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
+    # the ReLU-masked input-gradient form (upr_t_conv_mfma16_relu_bwd_cs) on the slice in place
+    mask16 = torch.randn(B, H, W, N, generator=gen).half().to(DEV)
+    mo = []
+    for strided in (False, True):
+        y = torch.empty(B, H, W, N, device=DEV)
+        y16 = torch.empty(B * H * W * N, dtype=torch.float16, device=DEV)
+        src, cs = (ctypes.c_void_p(cat16.data_ptr() + 2 * k0), 4 * C) if strided else (sl16.data_ptr(), C)
+        rc = lib.upr_t_conv_mfma16_relu_bwd_cs(src, cs, B, H, W, C, wt16.data_ptr(), N, 3, 3, 1, 1, y.data_ptr(), N,
+                                               0, y16.data_ptr(), N, mask16.data_ptr(), N, 0, st)
+        assert rc == 0, rc
+        mo.append((y, y16))
+    torch.cuda.synchronize()
+    assert torch.equal(mo[0][0], mo[1][0]) and torch.equal(mo[0][1], mo[1][1])
+    assert torch.equal(mo[0][0] == 0, (mask16 <= 0) | (outs[0] == 0))  # zero exactly where masked
     # weight gradient: dy = the slice (fp32 strided + its fp16 copy in the same layout)
     x16 = torch.randn(B, H, W, C, generator=gen).half().to(DEV)
     dws = []
