@@ -185,8 +185,9 @@ int upr_t_zero_upsample(const float* dy, int B, int Ho, int Wo, int C, int dy_cs
                         void* stream);
 
 /* ---- BatchNorm2d, training mode (nn.BatchNorm2d, model.py:106-162,196-229) -- */
-/* acc[2C] = (sum x, sum x^2) per channel of x[M][cs] (acc: upr_t_reduce_acc_doubles(C)
- * doubles; the atomic fallback for C % 4 / unaligned rows adds to a zeroed acc). */
+/* acc[2C] = (sum x, sum x^2) per channel of x[M][cs], overwritten (acc:
+ * upr_t_reduce_acc_doubles(C) doubles; the atomic fallback for C % 4 / unaligned
+ * rows clears acc itself first). */
 int upr_t_bn_stats(const float* x, int M, int C, int cs, int coff, double* acc, void* stream);
 /* batch mean / 1/sqrt(var_biased + eps); running stats updated with the
  * unbiased variance and momentum; *nbt += 1 (num_batches_tracked). */
@@ -330,7 +331,9 @@ int upr_t_maxpool16_code(const void* x16, int B, int H, int W, int C, int k, int
 /* upr_t_copy / upr_t_bilinear also writing the fp16 copy of the result at
  * dst16[pixel * dst16_cs + c] (dst16 points at the slice's first channel of
  * a [B][H][W][dst16_cs] fp16 concat): 4-channel views only, else
- * UPR_ERR_UNSUPPORTED (nothing launched). */
+ * UPR_ERR_UNSUPPORTED (nothing launched).  accumulate 2: the fp16 copy only
+ * (dst's fp32 untouched) -- for a concat whose every reader takes its fp16
+ * copy. */
 int upr_t_copy16(const UprView* src, const UprView* dst, int B, int H, int W, int C, int accumulate, void* dst16,
                  int dst16_cs, void* stream);
 int upr_t_bilinear16(const UprView* x, int B, int H, int W, int C, const UprView* y, int Ho, int Wo, int accumulate,

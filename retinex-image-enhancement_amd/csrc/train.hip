@@ -1295,11 +1295,11 @@ __global__ __launch_bounds__(256) void copy4_kernel(V4 s, V4 d, int H, int W, in
   dec4(i, CV, W, H, b, y, x, c);
   float4 v = *(const float4*)s.at(b, y, x, c);
   float4* o = (float4*)d.at(b, y, x, c);
-  if (accum) {
+  if (accum == 1) {
     const float4 u = *o;
     v = make_float4(u.x + v.x, u.y + v.y, u.z + v.z, u.w + v.w);
   }
-  *o = v;
+  if (accum != 2) *o = v;  // 2: the fp16 copy only
   if (d16) store16(d16, cs16, i / CV, c, v);
 }
 
@@ -1323,11 +1323,11 @@ __global__ __launch_bounds__(256) void bilinear4_kernel(V4 x, int H, int W, int 
   v.z = (1.f - ly) * ((1.f - lx) * a.z + lx * bq.z) + ly * ((1.f - lx) * cq.z + lx * d.z);
   v.w = (1.f - ly) * ((1.f - lx) * a.w + lx * bq.w) + ly * ((1.f - lx) * cq.w + lx * d.w);
   float4* o = (float4*)y.at(b, oy, ox, c);
-  if (accum) {
+  if (accum == 1) {
     const float4 u = *o;
     v = make_float4(u.x + v.x, u.y + v.y, u.z + v.z, u.w + v.w);
   }
-  *o = v;
+  if (accum != 2) *o = v;  // 2: the fp16 copy only
   if (y16) store16(y16, cs16, i / CV, c, v);
 }
 
@@ -2806,9 +2806,10 @@ int upr_t_bn_stats(const float* x, int M, int C, int cs, int coff, double* acc, 
   if (reduce4_ok(C, cs, coff, x))
     return chan_reduce2(x, cs, coff, (const float*)nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr, M, C, 0,
                         acc + 2 * C, acc, nullptr, 0, ST(stream));
-  else
-    hipLaunchKernelGGL(chan_reduce_kernel, dim3(reduce_grid(M)), dim3(256), 0, ST(stream), x, cs, coff, nullptr, 0, 0,
-                       nullptr, nullptr, M, C, 0, acc, nullptr);
+  // the atomic fallback adds into acc: cleared here, so every path overwrites
+  UPR_CHECK_HIP(hipMemsetAsync(acc, 0, sizeof(double) * 2 * C, ST(stream)));
+  hipLaunchKernelGGL(chan_reduce_kernel, dim3(reduce_grid(M)), dim3(256), 0, ST(stream), x, cs, coff, nullptr, 0, 0,
+                     nullptr, nullptr, M, C, 0, acc, nullptr);
   LAUNCH_CHECK();
 }
 
@@ -3492,7 +3493,7 @@ int upr_t_bilinear_bwd(const UprView* dy, int B, int H, int W, int C, int Ho, in
 
 int upr_t_copy16(const UprView* src, const UprView* dst, int B, int H, int W, int C, int accumulate, void* dst16,
                  int dst16_cs, void* stream) {
-  if (!src || !dst || !src->data || !dst->data || !dst16) return UPR_ERR_ARG;
+  if (!src || !dst || !src->data || !dst->data || !dst16 || accumulate < 0 || accumulate > 2) return UPR_ERR_ARG;
   const long long n = (long long)B * H * W * C;
   if (n == 0) return UPR_OK;
   if (!vec4_view_ok(src, B, H, W, C) || !vec4_view_ok(dst, B, H, W, C) || (uintptr_t)dst16 % 8 || dst16_cs % 4 ||
@@ -3506,7 +3507,7 @@ int upr_t_copy16(const UprView* src, const UprView* dst, int B, int H, int W, in
 
 int upr_t_bilinear16(const UprView* x, int B, int H, int W, int C, const UprView* y, int Ho, int Wo, int accumulate,
                      void* y16, int y16_cs, void* stream) {
-  if (!x || !y || !y16 || Ho <= 0 || Wo <= 0) return UPR_ERR_ARG;
+  if (!x || !y || !y16 || Ho <= 0 || Wo <= 0 || accumulate < 0 || accumulate > 2) return UPR_ERR_ARG;
   const long long n = (long long)B * Ho * Wo * C;
   if (n == 0) return UPR_OK;
   if (!vec4_view_ok(x, B, H, W, C) || !vec4_view_ok(y, B, Ho, Wo, C) || (uintptr_t)y16 % 8 || y16_cs % 4 ||

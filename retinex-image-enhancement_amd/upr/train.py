@@ -763,7 +763,6 @@ class BN:
         x16 = x.t16 if _AMP[0] and x.t16 is not None and x.coff == 0 and x.cs == x.C == self.C else None
         self.x16 = x16
         if m.training:
-            zero(self.acc[:2 * self.C])  # only the atomic fallback adds into acc
             rc = lib.upr_t_bn_stats16(_p(x16), x.M, self.C, _p(self.acc), st) if x16 is not None \
                 else L.UPR_ERR_UNSUPPORTED
             if rc == L.UPR_ERR_UNSUPPORTED:
@@ -1392,31 +1391,31 @@ class UPRetinexTrainGraph:
         self.s3 = self.s3c.fwd(pyr[1], relu=True)
         f3 = self.s3f.fwd(self.s3)
         fused = Act.new(B, H, W, 96, dev, fresh=False)
-        # under autocast the concat's fp16 copy (the fusion conv's operand) is written alongside
+        # under autocast the concat's fp16 copy (the fusion conv's operand) is written alongside;
+        # only that copy when the fusion conv's weight gradient also reads it (wm = 2)
         f16 = _h16(B * H * W * 96, dev) if _AMP[0] else None
         ok16 = f16 is not None
+        wm = 2 if ok16 and self.fusion.wgrad16_ok(W) else 0
         if ok16:
-            rc = lib.upr_t_copy16(ctypes.byref(f1.view()), ctypes.byref(fused.slice(0, 32).view()), B, H, W, 32, 0,
+            rc = lib.upr_t_copy16(ctypes.byref(f1.view()), ctypes.byref(fused.slice(0, 32).view()), B, H, W, 32, wm,
                                   _p(f16), 96, st)
-            ok16 = rc == 0
+            for i, f in enumerate((f2, f3)):
+                if rc != 0:
+                    break
+                rc = lib.upr_t_bilinear16(ctypes.byref(f.view()), B, f.H, f.W, 32,
+                                          ctypes.byref(fused.slice(32 * (i + 1), 32).view()), H, W, wm,
+                                          ctypes.c_void_p(f16.data_ptr() + 2 * 32 * (i + 1)), 96, st)
             if rc not in (0, L.UPR_ERR_UNSUPPORTED):
                 _chk(rc, "cat16")
-        if not ok16:
+            ok16 = rc == 0
+        if not ok16:  # every slice in fp32 (whatever the fp16 attempt left behind)
             _chk(lib.upr_t_copy(ctypes.byref(f1.view()), ctypes.byref(fused.slice(0, 32).view()), B, H, W, 32, 0, st),
                  "cat")
-        for i, f in enumerate((f2, f3)):
-            dst = fused.slice(32 * (i + 1), 32).view()
-            if ok16:
-                rc = lib.upr_t_bilinear16(ctypes.byref(f.view()), B, f.H, f.W, 32, ctypes.byref(dst), H, W, 0,
-                                          ctypes.c_void_p(f16.data_ptr() + 2 * 32 * (i + 1)), 96, st)
-                ok16 = rc == 0
-                if rc == 0:
-                    continue
-                if rc != L.UPR_ERR_UNSUPPORTED:
-                    _chk(rc, "upsample16")
-            _chk(lib.upr_t_bilinear(ctypes.byref(f.view()), B, f.H, f.W, 32, ctypes.byref(dst), H, W, 0, st),
-                 "upsample")
+            for i, f in enumerate((f2, f3)):
+                _chk(lib.upr_t_bilinear(ctypes.byref(f.view()), B, f.H, f.W, 32,
+                                        ctypes.byref(fused.slice(32 * (i + 1), 32).view()), H, W, 0, st), "upsample")
         fused.t16 = f16 if ok16 else None
+        fused.stale32 = bool(ok16 and wm == 2)
         self.fused = fused
         self.fz = self.fusion.fwd(fused)
         o = self.outc.fwd(self.fz)
