@@ -75,6 +75,13 @@ int upr_t_conv_direct_wgrad(const UprView* x, const UprView* dy, int B, int H, i
 int upr_t_conv_direct_wgrad_relu(const UprView* x, const UprView* dy, const UprView* y, int B, int H, int W, int Cin,
                                  int Ho, int Wo, int Cout, int kh, int kw, int stride, int pad, int dil, float* dw,
                                  float* dbias, void* stream);
+/* The image stems' case of it (Cin 3 -> Cout 32, 3x3, stride 1, pad 1,
+ * dilation 1, with bias): dy contiguous [B][H][W][32] fp32 (16-byte aligned),
+ * the mask from the ReLU output's compact fp16 copy y16 ([B][H][W][32]), x any
+ * view of the 3-channel input.  dw ([32][27], PyTorch's [co][ci][kh][kw]) and
+ * dbias += the sums.  UPR_ERR_UNSUPPORTED off those layouts. */
+int upr_t_conv_stem_wgrad_relu16(const UprView* x, const float* dy, const void* y16, int B, int H, int W, float* dw,
+                                 float* dbias, void* stream);
 
 /* MFMA implicit-GEMM conv (the inference kernels of conv.hip/conv_halo.hip) on
  * NHWC sources with channel stride/offset; Cin, Cout multiples of 32.

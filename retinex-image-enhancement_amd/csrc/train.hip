@@ -83,6 +83,8 @@ static inline int grid_for(long long n, int per = 256, int cap = 65536) {
 int small_conv_fwd(const UprView* xv, int B, int H, int W, int Cin, const float* w, const float* bias, int Cout,
                    int kh, int kw, int stride, int pad, int dil, const UprView* yv, int Ho, int Wo, int relu,
                    int accumulate, hipStream_t st, void* y16 = nullptr, int skip32 = 0);
+int small_stem_wgrad_relu16(const UprView* xv, const float* dy, const void* y16, int B, int H, int W, float* dw,
+                            float* dbias, hipStream_t st);
 int small_conv_dgrad(const UprView* dyv, int Ho, int Wo, const float* w, int B, int H, int W, int Cin, int Cout,
                      int kh, int kw, int stride, int pad, int dil, const UprView* dxv, int accumulate, hipStream_t st);
 int small_conv_dgrad_c3_16(const void* dy16, int B, int H, int W, const float* w, int Cout, const UprView* dxv,
@@ -1666,7 +1668,6 @@ __global__ __launch_bounds__(256) void fam_pool_bwd4_kernel(float* g_o, const fl
                                                             const float* __restrict__ o, int M, int HW, int C,
                                                             half_t* __restrict__ g16) {
   const int C4 = C / 4, c = (threadIdx.x % C4) * 4, rpb = 256 / C4;
-  const float inv = 1.f / (float)HW;
   for (int m = blockIdx.x * rpb + threadIdx.x / C4; m < M; m += gridDim.x * rpb) {
     const int b = m / HW;
     const int off = m * C + c;
@@ -2466,6 +2467,13 @@ int upr_t_conv_direct_dgrad(const UprView* dy, int Ho, int Wo, const float* w, i
   hipLaunchKernelGGL(conv_direct_dgrad_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), mkv(dy), Ho, Wo, w, B, H,
                      W, Cin, Cout, kh, kw, stride, pad, dil, mkv(dx), accumulate);
   LAUNCH_CHECK();
+}
+
+int upr_t_conv_stem_wgrad_relu16(const UprView* x, const float* dy, const void* y16, int B, int H, int W, float* dw,
+                                 float* dbias, void* stream) {
+  if (!x || !dy || !y16 || !dw || !dbias || B <= 0 || H <= 0 || W <= 0) return UPR_ERR_ARG;
+  const int rc = small_stem_wgrad_relu16(x, dy, y16, B, H, W, dw, dbias, ST(stream));
+  return rc == kErrUnsupported ? UPR_ERR_UNSUPPORTED : rc;
 }
 
 int upr_t_conv_direct_wgrad_relu(const UprView* x, const UprView* dy, const UprView* y, int B, int H, int W, int Cin,

@@ -806,6 +806,98 @@ __global__ __launch_bounds__(256) void pw_wgrad_kernel(SV x, SV dy, int B, int H
     part[(size_t)blockIdx.x * NE + i] = ((wred[0][i] + wred[1][i]) + wred[2][i]) + wred[3][i];
 }
 
+// ---------------------------------------------------------------------------
+// weight gradient of the 3 -> 32 3x3 / s1 / p1 image stems with the ReLU
+// backward of their output fused: dW[co][ci][tap] = sum_p (dy[p][co] masked by
+// y16[p][co] > 0) * x[ci][p + tap], db[co] = sum_p of the masked dy.  A block
+// stages a 4 x 64 pixel tile of the masked dy (coalesced 16-byte loads, the
+// mask applied on the way into LDS) and the 3 x 6 x 66 input patch, then each
+// wave runs v_mfma_f32_32x32x2f32 over its tile row (A = dy rows, B = the
+// im2col columns read from the patch at per-lane tap offsets).  Persistent over
+// tiles; per-block partials summed in block order by small_wgrad_fin_kernel.
+// The generic small_wgrad_mfma_kernel gathered every operand with 4-byte loads
+// (0.32 ms per stem at bs 8 512^2, the mask read included).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void stem_wgrad_relu_kernel(SV x, const float* __restrict__ dy,
+                                                              const half_t* __restrict__ y16, int B, int H, int W,
+                                                              float* __restrict__ part) {
+  constexpr int TR = 4, TC = 64, CO = 32, KC = 27;
+  __shared__ __attribute__((aligned(16))) float dyl[TR * TC][CO];  // 32 KB; the wave sums reuse it
+  __shared__ float xl[3][TR + 2][TC + 2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = lane & 31, kk = lane >> 5;
+  // this lane's im2col column n: input channel and tap offsets into the patch
+  const int ci = n < KC ? n / 9 : 0, tap = n < KC ? n % 9 : 0, ky = tap / 3, kx = tap % 3;
+  f32x16_t2 acc;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+  const int ntx = (W + TC - 1) / TC, nty = (H + TR - 1) / TR, ntiles = ntx * nty * B;
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int tx = t % ntx, ty = (t / ntx) % nty, b = t / (ntx * nty);
+    const int iy0 = ty * TR, ix0 = tx * TC;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < (TR * TC * CO / 4) / 256; ++j) {
+      const int q = tid + j * 256, px = q >> 3, c4 = (q & 7) * 4;
+      const int iy = iy0 + px / TC, ix = ix0 + px % TC;
+      f32x4_t2 v = f32x4_t2{0.f, 0.f, 0.f, 0.f};
+      if (iy < H && ix < W) {
+        const size_t pix = ((size_t)b * H + iy) * W + ix;
+        v = *(const f32x4_t2*)(dy + pix * CO + c4);
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        const h4 m = *(const h4*)(y16 + pix * CO + c4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (!(m[e] > (half_t)0)) v[e] = 0.f;
+      }
+      *(f32x4_t2*)&dyl[px][c4] = v;
+    }
+    for (int q = tid; q < 3 * (TR + 2) * (TC + 2); q += 256) {
+      const int c = q / ((TR + 2) * (TC + 2)), r = (q / (TC + 2)) % (TR + 2), col = q % (TC + 2);
+      const int iy = iy0 - 1 + r, ix = ix0 - 1 + col;
+      xl[c][r][col] = ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) ? x.d[x.at(b, iy, ix, c)] : 0.f;
+    }
+    __syncthreads();
+    // wave w: tile row w, 32 pixel pairs
+#pragma unroll 4
+    for (int j = 0; j < TC / 2; ++j) {
+      const int col = 2 * j + kk;
+      const float a = dyl[wave * TC + col][n];
+      const float bv = n < KC ? xl[ci][wave + ky][col + kx] : (n == KC ? 1.f : 0.f);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv, acc, 0, 0, 0);
+    }
+  }
+  __syncthreads();
+  float* red = &dyl[0][0];  // [4 waves][16][64]
+#pragma unroll
+  for (int e = 0; e < 16; ++e) red[(wave * 16 + e) * 64 + lane] = acc[e];
+  __syncthreads();
+  for (int idx = tid; idx < 16 * 64; idx += 256) {
+    const int e = idx >> 6, l = idx & 63;
+    const float v = ((red[(0 * 16 + e) * 64 + l] + red[(1 * 16 + e) * 64 + l]) + red[(2 * 16 + e) * 64 + l]) +
+                    red[(3 * 16 + e) * 64 + l];
+    // 32x32 accumulator map: column = l & 31, row = (e & 3) + 8 * (e >> 2) + 4 * (l >> 5)
+    const int co = (e & 3) + 8 * (e >> 2) + 4 * (l >> 5), k = l & 31;
+    if (k <= KC) part[(size_t)blockIdx.x * CO * (KC + 1) + co * (KC + 1) + k] = v;
+  }
+}
+
+int small_stem_wgrad_relu16(const UprView* xv, const float* dy, const void* y16, int B, int H, int W, float* dw,
+                            float* dbias, hipStream_t st) {
+  if (((uintptr_t)dy % 16) || ((uintptr_t)y16 % 8) || (long long)B * H * W >= (1ll << 31)) return kErrUnsupported;
+  const long long ntiles = (long long)((W + 63) / 64) * ((H + 3) / 4) * B;
+  int cus = 256, dev = 0;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int grid = (int)std::min<long long>(ntiles, (long long)cus * 4);
+  constexpr int NE = 32 * 28;
+  float* part = (float*)scratch(kSlotPart, sizeof(float) * (size_t)grid * NE, st);
+  if (!part) return (int)hipErrorOutOfMemory;
+  hipLaunchKernelGGL(stem_wgrad_relu_kernel, dim3(grid), dim3(256), 0, st, mksv(xv), dy, (const half_t*)y16, B, H, W,
+                     part);
+  hipLaunchKernelGGL(small_wgrad_fin_kernel, dim3(NE), dim3(256), 0, st, (const float*)part, grid, 32, 27, dw, dbias);
+  return (int)hipGetLastError();
+}
+
 int small_conv_wgrad(const UprView* xv, const UprView* dyv, int B, int H, int W, int Cin, int Ho, int Wo, int Cout,
                      int kh, int kw, int stride, int pad, int dil, float* dw, float* dbias, hipStream_t st,
                      const UprView* ymask) {

@@ -120,6 +120,7 @@ SIGNATURES.update({
                                  _p]),
     "upr_t_conv_direct_dgrad": (_i, [_vp, _i, _i, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _p]),
     "upr_t_conv_direct_wgrad": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p]),
+    "upr_t_conv_stem_wgrad_relu16": (_i, [_vp, _p, _p, _i, _i, _i, _p, _p, _p]),
     "upr_t_conv_direct_wgrad_relu": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p,
                                           _p]),
     "upr_t_conv_mfma": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _p, _i, _i, _i, _i, _i, _i, _p, _i, _i, _p, _i, _i,

@@ -484,6 +484,17 @@ class Conv:
                 xv, B, H, W = x_view
             else:
                 xv, B, H, W = x.view(), x.B, x.H, x.W
+            stem = (self.Cin, self.Cout, self.kh, self.kw, self.s, self.p, self.d) == (3, 32, 3, 3, 1, 1, 1) and \
+                self.bias is not None and gy.coff == 0 and gy.cs == 32 and y.t16 is not None and y.whole16() and \
+                (gy.H, gy.W) == (H, W)
+            if stem:  # the LDS-staged 3 -> 32 kernel, mask from y's fp16 copy
+                with _timed("direct", "wgrad", self.flops(B, H, W), (3, 32, 3, 1, H, W)):
+                    rc = lib.upr_t_conv_stem_wgrad_relu16(ctypes.byref(xv), gy.ptr(), _p(y.t16), B, H, W,
+                                                          _p(self.m.weight.grad), _p(self.bias.grad), st)
+                if rc == 0:
+                    return
+                if rc != L.UPR_ERR_UNSUPPORTED:
+                    _chk(rc, "conv_stem_wgrad_relu16")
             with _timed("direct", "wgrad", self.flops(B, gy.H, gy.W), (self.Cin, self.Cout, self.kh, self.s, H, W)):
                 rc = lib.upr_t_conv_direct_wgrad_relu(ctypes.byref(xv), ctypes.byref(gy.view()),
                                                       ctypes.byref(y.view()), B, H, W, self.Cin, gy.H, gy.W,

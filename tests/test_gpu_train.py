@@ -127,6 +127,35 @@ def test_stem_relu_fused_into_wgrad(nchw):
     assert torch.equal(m.weight.detach(), w0)
 
 
+@pytest.mark.parametrize("nchw,H,W", [(True, 40, 72), (False, 24, 64), (True, 13, 7)])
+def test_stem_wgrad_relu16_vs_torch(nchw, H, W):
+    """upr_t_conv_stem_wgrad_relu16 (the 3 -> 32 3x3 stem weight gradient, dy
+    masked by the ReLU output's fp16 copy > 0, LDS-staged tiles with ragged
+    edges) vs torch's conv2d_weight of the masked dy in fp64, 1e-4 of max."""
+    from upr import _lib as L
+    from upr.train import nchw_view
+    gen = torch.Generator().manual_seed(8)
+    B = 2
+    x = torch.rand(B, 3, H, W, generator=gen)
+    dy = torch.randn(B, H, W, 32, generator=gen)
+    y16 = torch.randn(B, H, W, 32, generator=gen).half()
+    gm = dy * (y16.float() > 0)
+    ref = torch.nn.grad.conv2d_weight(x.double(), (32, 3, 3, 3), gm.permute(0, 3, 1, 2).double(), padding=1).float()
+    refb = gm.double().sum(dim=(0, 1, 2)).float()
+    xd = x.to(DEV).contiguous()
+    xn = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    xv = nchw_view(xd) if nchw else L.UprView(xn.data_ptr(), H * W * 3, W * 3, 3, 1)
+    dyd, y16d = dy.to(DEV), y16.to(DEV)
+    dw = torch.full((32, 3, 3, 3), 0.5, device=DEV)
+    db = torch.full((32,), 0.25, device=DEV)
+    rc = L.lib().upr_t_conv_stem_wgrad_relu16(ctypes.byref(xv), dyd.data_ptr(), y16d.data_ptr(), B, H, W,
+                                              dw.data_ptr(), db.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, rc
+    torch.cuda.synchronize()
+    _close(dw - 0.5, ref, 1e-4, "stem wgrad")
+    _close(db - 0.25, refb, 1e-4, "stem dbias")
+
+
 @pytest.mark.parametrize("B,cin,cout,H,W,k,s,p,d", [
     (2, 32, 32, 64, 128, 3, 1, 1, 1),    # 32 -> 32 3x3 (dec1 / head / FAM class): BM 32, 9 runs per tile
     (1, 64, 128, 128, 128, 3, 2, 1, 1),  # encoder stride-2 conv: BM 128, 4 runs
