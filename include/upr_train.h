@@ -242,6 +242,10 @@ int upr_t_bn_bwd_fused(const float* g, int g_cs, int g_coff, const float* x, int
  * gradients) at half the bytes.  C % 4 == 0 (and <= 1024 for the reductions),
  * else UPR_ERR_UNSUPPORTED. */
 int upr_t_bn_stats16(const void* x16, int M, int C, double* acc, void* stream);
+/* upr_t_bn_stats16 then upr_t_bn_finalize, the slot sums and the finalise in
+ * one kernel (the same acc, mean / invstd and running statistics bits). */
+int upr_t_bn_stats16_fin(const void* x16, int M, int C, double* acc, float momentum, float eps, float* running_mean,
+                         float* running_var, int64_t* nbt, float* mean, float* invstd, void* stream);
 int upr_t_bn_apply16h(const void* x16, int M, int C, const float* mean, const float* invstd, const float* gamma,
                       const float* beta, const float* res, int res_cs, int res_coff, int res_post, int relu, float* y,
                       int y_cs, int y_coff, void* y16, int skip32, void* stream);

@@ -2927,6 +2927,70 @@ int upr_t_bn_stats16(const void* x16, int M, int C, double* acc, void* stream) {
                       0, acc + 2 * C, acc, nullptr, 0, ST(stream));
 }
 
+// chan_fin (mode 0) and bn_finalize in one launch: a block owns 32 channels,
+// lanes 0-31 their sums and 32-63 their sums of squares (the same slot order
+// and partial-sum tree as chan_fin: bit-identical acc), then lanes 0-31
+// finalise their channel as bn_finalize_kernel does
+__global__ __launch_bounds__(256) void chan_fin_bn_kernel(const double* __restrict__ part, int slots, int C,
+                                                          double* __restrict__ acc, int M, float momentum, float eps,
+                                                          float* __restrict__ rm, float* __restrict__ rv,
+                                                          long long* nbt, float* __restrict__ mean,
+                                                          float* __restrict__ invstd) {
+  __shared__ double red[4][64];
+  __shared__ double fin[64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 32 + (lane & 31);
+  const bool ok = c < C;
+  const int t = lane < 32 ? c : C + c;
+  double s4[4] = {0.0, 0.0, 0.0, 0.0};
+  if (ok) {
+    int k = w;
+    for (; k + 12 < slots; k += 16) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s4[u] += part[(size_t)(k + 4 * u) * 2 * C + t];
+    }
+    for (int u = 0; k < slots; k += 4, ++u) s4[u & 3] += part[(size_t)k * 2 * C + t];
+  }
+  red[w][lane] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+  __syncthreads();
+  if (w == 0) {
+    const double v = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    fin[lane] = v;
+    if (ok) acc[t] = v;
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
+  if (w != 0 || lane >= 32 || !ok) return;
+  const double mu = fin[lane] / M;
+  double var = fin[lane + 32] / M - mu * mu;
+  if (var < 0) var = 0;
+  mean[c] = (float)mu;
+  invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (rm) rm[c] = (1.f - momentum) * rm[c] + momentum * (float)mu;
+  if (rv) {
+    const double unb = M > 1 ? var * M / (M - 1) : var;
+    rv[c] = (1.f - momentum) * rv[c] + momentum * (float)unb;
+  }
+}
+
+int upr_t_bn_stats16_fin(const void* x16, int M, int C, double* acc, float momentum, float eps, float* running_mean,
+                         float* running_var, int64_t* nbt, float* mean, float* invstd, void* stream) {
+  if (!x16 || !acc || !mean || !invstd || M <= 0 || C <= 0) return UPR_ERR_ARG;
+  if (C % 4 || C > 1024 || (uintptr_t)x16 % 8) return UPR_ERR_UNSUPPORTED;
+  hipStream_t st = ST(stream);
+  const int R = kRedThreads / (C / 4);
+  int slots = M / (R * 16);
+  slots = slots < 1 ? 1 : (slots > kRedSlots ? kRedSlots : slots);
+  double* part = acc + 2 * C;
+  hipLaunchKernelGGL((chan_part_kernel<half_t, float>), dim3(slots), dim3(kRedThreads),
+                     (size_t)R * 2 * C * sizeof(double), st, (const half_t*)x16, C, 0, (const float*)nullptr, 0, 0,
+                     nullptr, nullptr, nullptr, nullptr, M, C, 0, part);
+  UPR_CHECK_HIP(hipGetLastError());
+  hipLaunchKernelGGL(chan_fin_bn_kernel, dim3((C + 31) / 32), dim3(256), 0, st, (const double*)part, slots, C, acc, M,
+                     momentum, eps, running_mean, running_var, (long long*)nbt, mean, invstd);
+  LAUNCH_CHECK();
+}
+
 int upr_t_bn_apply16h(const void* x16, int M, int C, const float* mean, const float* invstd, const float* gamma,
                       const float* beta, const float* res, int res_cs, int res_coff, int res_post, int relu, float* y,
                       int y_cs, int y_coff, void* y16, int skip32, void* stream) {

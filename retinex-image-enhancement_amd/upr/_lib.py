@@ -153,6 +153,7 @@ SIGNATURES.update({
     "upr_t_bn_bwd_fused": (_i, [_p, _i, _i, _p, _i, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _i, _i, _i, _i, _p,
                                 _p]),
     "upr_t_bn_stats16": (_i, [_p, _i, _i, _p, _p]),
+    "upr_t_bn_stats16_fin": (_i, [_p, _i, _i, _p, _f, _f, _p, _p, _p, _p, _p, _p]),
     "upr_t_bn_apply16h": (_i, [_p, _i, _i, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _i, _i, _p, _i, _p]),
     "upr_t_bn_bwd_fused16": (_i, [_p, _p, _i, _i, _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _i, _i, _i, _i,
                                   _p, _i, _p]),

@@ -784,15 +784,20 @@ class BN:
         x16 = x.t16 if _AMP[0] and x.t16 is not None and x.coff == 0 and x.cs == x.C == self.C else None
         self.x16 = x16
         if m.training:
-            rc = lib.upr_t_bn_stats16(_p(x16), x.M, self.C, _p(self.acc), st) if x16 is not None \
-                else L.UPR_ERR_UNSUPPORTED
+            # fp16 input: statistics and finalise in two launches (upr_t_bn_stats16_fin)
+            rc = lib.upr_t_bn_stats16_fin(_p(x16), x.M, self.C, _p(self.acc), ctypes.c_float(m.momentum),
+                                          ctypes.c_float(m.eps), _p(m.running_mean), _p(m.running_var),
+                                          _p(m.num_batches_tracked), _p(self.mean), _p(self.invstd), st) \
+                if x16 is not None else L.UPR_ERR_UNSUPPORTED
             if rc == L.UPR_ERR_UNSUPPORTED:
                 assert not x.stale32, "fp16-only BN input without an fp16 statistics path"
-                rc = lib.upr_t_bn_stats(x.ptr(), x.M, self.C, x.cs, 0, _p(self.acc), st)
-            _chk(rc, "bn_stats")
-            _chk(lib.upr_t_bn_finalize(_p(self.acc), x.M, self.C, ctypes.c_float(m.momentum), ctypes.c_float(m.eps),
-                                       _p(m.running_mean), _p(m.running_var), _p(m.num_batches_tracked),
-                                       _p(self.mean), _p(self.invstd), st), "bn_finalize")
+                _chk(lib.upr_t_bn_stats(x.ptr(), x.M, self.C, x.cs, 0, _p(self.acc), st), "bn_stats")
+                _chk(lib.upr_t_bn_finalize(_p(self.acc), x.M, self.C, ctypes.c_float(m.momentum),
+                                           ctypes.c_float(m.eps), _p(m.running_mean), _p(m.running_var),
+                                           _p(m.num_batches_tracked), _p(self.mean), _p(self.invstd), st),
+                     "bn_finalize")
+            else:
+                _chk(rc, "bn_stats16_fin")
         else:
             _chk(lib.upr_t_bn_eval_stats(_p(m.running_mean), _p(m.running_var), self.C, ctypes.c_float(m.eps),
                                          _p(self.mean), _p(self.invstd), st), "bn_eval_stats")

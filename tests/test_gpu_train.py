@@ -1491,3 +1491,34 @@ def test_train_grads_512_b2_fixed_bound(amp):
         assert l2 <= tol, f"{n}: rel-L2 {l2:.3e} > {tol:.3e}"
     if not amp:
         assert med <= 1e-3, med
+
+
+@pytest.mark.parametrize("M,C", [(8 * 64 * 64, 32), (2 * 40 * 24, 64), (8 * 32 * 32, 256), (100, 4)])
+def test_bn_stats16_fin_matches_two_step(M, C):
+    """upr_t_bn_stats16_fin (slot sums + finalise in one kernel) equals
+    upr_t_bn_stats16 followed by upr_t_bn_finalize bit for bit: acc, mean,
+    invstd, running mean / variance and num_batches_tracked."""
+    from upr import _lib as L
+    lib, st = L.lib(), torch.cuda.current_stream().cuda_stream
+    gen = torch.Generator().manual_seed(13)
+    x16 = (torch.randn(M, C, generator=gen) * 2 + 0.5).half().to(DEV)
+    nacc = lib.upr_t_reduce_acc_doubles(C)
+    outs = []
+    for fused in (False, True):
+        acc = torch.zeros(nacc, dtype=torch.float64, device=DEV)
+        rm = torch.linspace(-1, 1, C, device=DEV)
+        rv = torch.linspace(0.5, 2, C, device=DEV)
+        nbt = torch.tensor(7, dtype=torch.int64, device=DEV)
+        mean, inv = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+        args = (ctypes.c_float(0.1), ctypes.c_float(1e-5), rm.data_ptr(), rv.data_ptr(), nbt.data_ptr(),
+                mean.data_ptr(), inv.data_ptr())
+        if fused:
+            assert lib.upr_t_bn_stats16_fin(x16.data_ptr(), M, C, acc.data_ptr(), *args, st) == 0
+        else:
+            assert lib.upr_t_bn_stats16(x16.data_ptr(), M, C, acc.data_ptr(), st) == 0
+            assert lib.upr_t_bn_finalize(acc.data_ptr(), M, C, *args, st) == 0
+        torch.cuda.synchronize()
+        outs.append((acc[:2 * C].clone(), mean, inv, rm, rv, nbt))
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+    assert int(outs[1][5]) == 8
