@@ -86,6 +86,11 @@ def parse(argv=None):
     ap.add_argument("--enhance", action="store_true",
                     help="the enhancer stage as the headline: CLAHE-in-Lab + multi-scale factor/clamp over a resident "
                          "bs=32 512x512 batch (adaptive_params.py:121-169, multi_scale.py:62-100)")
+    ap.add_argument("--detail", default=os.path.join("gpurun_out", "bench_detail.json"),
+                    help="where rank 0 writes the full JSON record (per-pass tables, slowest calls, CPU details); "
+                         "stdout gets the compact line ('' = no file)")
+    ap.add_argument("--cpu-enhance-child", nargs=2, type=int, metavar=("N", "SIZE"), default=None,
+                    help=argparse.SUPPRESS)  # internal: the enhancer CPU baseline's child process
     ap.add_argument("--amp", action="store_true",
                     help="with --train: the reference's AMP branch (autocast fp16 convs + GradScaler)")
     return ap.parse_args(argv)
@@ -216,7 +221,7 @@ def pmc_traffic(precision, variant, batch, size, extra=(), kernels=CONV_KERNELS)
         return None
     out = {}
     base = [sys.executable, os.path.abspath(__file__), "--steps", "1", "--warmup", "1", "--cpu-seconds", "0",
-            "--no-profile", "--no-traffic", "--no-nested", "--batch", str(batch), "--size", str(size),
+            "--no-profile", "--no-traffic", "--no-nested", "--detail", "", "--batch", str(batch), "--size", str(size),
             "--precision", precision, "--variant", variant] + list(extra)
     env = dict(os.environ, TMPDIR="/tmp")
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
@@ -443,16 +448,14 @@ def forward_leg(args, world, rank, dev, precision, variant, B, S, traffic, cpu_s
                        "all": "(+ timed final collect: RCCL all_gather_into_tensor of fp16 enhanced to every rank)",
                        "rank0": "(+ timed final collect: RCCL gather of fp16 enhanced to rank 0)"}[args.collect]},
     }
-    ms_env = os.environ.get("UPR_MS_STREAMS")  # csrc/model.hip side_of: atoi(), unset = fp16 only
-    if ms_env is None:
-        two = precision == "fp16"
-    else:
-        try:
-            two = int(ms_env.strip() or "0") != 0
-        except ValueError:
-            two = False
+    # which executor ran the timed steps: the library counts the forwards that
+    # forked the multi-scale side stream (csrc/model.hip side_of); the profiled
+    # last step always stays on one stream
+    forked = handle.forks()
+    two = forked >= args.steps + max(args.warmup - 1, 0)
     out["executor"] = ("two streams: the multi-scale ops on a side stream forked after the first conv, joined "
                        "before the Retinex tail (DESIGN §3)" if two else "one stream") + \
+        f" ({forked} of {args.steps + args.warmup} forwards forked)" + \
         ("; roofline per-launch events from the serialised profiled step" if stats else "")
     if stats:
         rf = conv_roofline(stats, precision, B, traffic)
@@ -617,33 +620,58 @@ def train_leg(args, world, rank, dev, B, S, amp, steps, warmup, variant):
 # ----------------------------------------------------------------------------
 # the CLAHE-in-Lab pipeline's kernels (one upr_clahe_enhance call) and the multi-scale ones
 CLAHE_KERNELS = ("clahe_hist_kernel", "clahe_lut_kernel", "clahe_apply_kernel")
-MS_KERNELS = ("ms_sums_kernel", "ms_factor_kernel", "scale_clamp_kernel")
+MS_KERNELS = ("ms_sums3_kernel", "ms_sums_kernel", "ms_factor_kernel", "scale_clamp_kernel")
+
+
+_ENH_DATA = {}
+
+
+def _enh_one(b):
+    from oracle import enhancers as oenh  # checker / baseline only
+    x, enh = _ENH_DATA["x"], _ENH_DATA["enh"]
+    oenh.clahe_enhancement(enh[b:b + 1])
+    fac = oenh.multiscale_factor(x[b:b + 1])
+    torch.clamp(enh[b] * fac[0], 0, 1)
 
 
 def cpu_enhance_baseline(n, size):
     """oracle/enhancers.py (numpy restatement of OpenCV's 8-bit Lab + CLAHE,
-    torch-CPU multi-scale features) on n images, single-threaded: 1 warm-up
-    image, then the median of CPU_REPS timed passes over the sample."""
-    from oracle import enhancers as oenh  # checker / baseline only
+    torch-CPU multi-scale features) over all n images, one image per task on a
+    pool of worker PROCESSES, one per usable core (the restatement is
+    GIL-bound: threads do not scale).  Runs in a child of bench.py started
+    before the parent touches the GPU (cpu_enhance_child), so the fork is of a
+    process without a GPU context.  1 warm-up pass (one image per worker), then
+    the median of CPU_REPS timed passes over the n images."""
+    import multiprocessing as mp
+    from concurrent.futures import ProcessPoolExecutor
     ci = cpu_info()
+    workers = max(1, min(ci["threads"], n))
     torch.set_num_threads(1)
     g = torch.Generator().manual_seed(97)
-    x = torch.rand(n, 3, size, size, generator=g)
-    enh = torch.rand(n, 3, size, size, generator=g) * 0.8
-
-    def run(k):
-        oenh.clahe_enhancement(enh[:k])
-        fac = oenh.multiscale_factor(x[:k])
-        torch.stack([torch.clamp(enh[b] * fac[b], 0, 1) for b in range(k)])
-    run(1)
-    med, times = _median_reps(lambda: run(n))
-    torch.set_num_threads(ci["threads"])
-    return {"value": n / med, "unit": "images/s", "cores": 1, "kind": "port", "cpu": ci, "rep_seconds": times,
+    _ENH_DATA["x"] = torch.rand(n, 3, size, size, generator=g)
+    _ENH_DATA["enh"] = torch.rand(n, 3, size, size, generator=g) * 0.8
+    with ProcessPoolExecutor(workers, mp_context=mp.get_context("fork")) as ex:
+        list(ex.map(_enh_one, range(workers)))  # warm-up: imports + first touch in every worker
+        med, times = _median_reps(lambda: list(ex.map(_enh_one, range(n))))
+    return {"value": n / med, "unit": "images/s", "cores": workers, "kind": "port", "cpu": ci, "rep_seconds": times,
             "sample": f"{n}x3x{size}x{size}: oracle/enhancers.py clahe_enhancement (numpy OpenCV restatement) + "
-                      f"multiscale_factor + clamp, one thread; 1-image warm-up, median of {CPU_REPS}"}
+                      f"multiscale_factor + clamp, one image per task on {workers} worker processes; warm-up pass, "
+                      f"median of {CPU_REPS}"}
 
 
-def enhance_leg(args, world, rank, dev, B, S, traffic, cpu_n):
+def cpu_enhance_child(n, size):
+    """Run cpu_enhance_baseline in a child process (before this process
+    initialises the GPU); None on failure."""
+    import subprocess
+    try:
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-enhance-child", str(n), str(size)],
+                           capture_output=True, text=True, timeout=600, check=True)
+        return json.loads(r.stdout.strip().splitlines()[-1])
+    except Exception as e:  # reported, not fatal: the baseline is not the measurement
+        return {"value": None, "error": f"{type(e).__name__}: {e}"[:300]}
+
+
+def enhance_leg(args, world, rank, dev, B, S, traffic, cpu_res):
     """One step = the enhancers over a resident batch of B SxS images: the
     CLAHE-in-Lab pipeline of apply_clahe_enhancement on the enhanced images
     (upr_clahe_enhance: quantise + Lab + tile histograms -> LUTs -> blend +
@@ -679,7 +707,7 @@ def enhance_leg(args, world, rank, dev, B, S, traffic, cpu_n):
     ms_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / len(ev)
     HW = S * S
     clahe_bytes = B * (HW * 24 + 8 * 8 * 256)   # fp32 RGB in + out, the tile LUTs
-    ms_bytes = B * HW * (12 * 3 + 24)           # 12 B/px per scale + the clamp pass
+    ms_bytes = B * HW * (12 + 24)               # the image read once for all three scales + the clamp pass
     clahe_gbs = clahe_bytes / (clahe_ms * 1e-3) / 1e9
     out = {
         "metric": f"enhancer images/sec at {S}x{S} bs={B} per GPU (CLAHE-in-Lab + multi-scale factor/clamp)",
@@ -705,8 +733,10 @@ def enhance_leg(args, world, rank, dev, B, S, traffic, cpu_n):
             "multiscale": {"avg_call_ms": ms_ms, "alg_bytes": ms_bytes,
                            "achieved_GBs": ms_bytes / (ms_ms * 1e-3) / 1e9,
                            "frac": ms_bytes / (ms_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
-                           "kernel": "upr_multiscale: 3 ms_sums (one per scale) + factor + scale_clamp",
-                           "alg_bytes_note": "12 B/px per scale (SURVEY §8d) + 24 B/px clamp (read enh, write out)"},
+                           "kernel": "upr_multiscale: ms_sums3 (all three scales from one read; the block completing "
+                                     "an image writes its factor) + scale_clamp",
+                           "alg_bytes_note": "12 B/px: the fp32 image read once for the three scales' sums + 24 B/px "
+                                             "clamp (read enh, write out)"},
         },
     }
     if rank == 0:
@@ -718,8 +748,8 @@ def enhance_leg(args, world, rank, dev, B, S, traffic, cpu_n):
         out["parity"] = {"max_abs_diff": {"clahe": d}, "tol": 0.0, "pass": d == 0.0, "images": idx,
                          "sample": f"CLAHE output of images {idx} of rank 0's last step vs oracle/enhancers.py "
                                    f"(numpy OpenCV restatement; bit-exact)"}
-        if world == 1 and args.cpu_seconds > 0 and cpu_n:
-            out["cpu_baseline"] = cpu_enhance_baseline(cpu_n, S)
+        if world == 1 and cpu_res is not None:
+            out["cpu_baseline"] = cpu_res
     del x, enh, last
     torch.cuda.empty_cache()
     return out
@@ -768,21 +798,88 @@ def dry_run(args):
 
 
 # ----------------------------------------------------------------------------
+# the printed line: compact (the driver keeps only the tail of stdout); the
+# full objects (per-pass tables, slowest calls, CPU details) go to --detail
+# ----------------------------------------------------------------------------
+_ROOF_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_per_img_GB", "gemm_alg_GB_per_img",
+              "alg_bytes_per_launch", "alg_bytes", "avg_launch_us", "launches_per_step", "avg_call_ms",
+              "layer_roofline_frac", "step_ms", "conv_ms", "non_conv_ms", "whole_step_frac_fp16_peak")
+
+
+def _sig(v, n=5):
+    if isinstance(v, float):
+        return float(f"{v:.{n}g}")
+    if isinstance(v, dict):
+        return {k: _sig(x, n) for k, x in v.items()}
+    if isinstance(v, (list, tuple)):
+        return [_sig(x, n) for x in v]
+    return v
+
+
+def compact(out):
+    """The bench line as printed: every headline key of the contract, and per
+    object only the numbers a reader checks (value, roofline frac / achieved /
+    traffic, parity max and verdict, cpu_baseline value / cores / kind)."""
+    c = {k: v for k, v in out.items() if not isinstance(v, dict) or k == "config"}
+    if "roofline" in out and out["roofline"]:
+        r = out["roofline"]
+        cr = {k: r[k] for k in _ROOF_KEYS if k in r}
+        if r.get("mfma_bound_layers"):
+            cr["mfma_bound_layers"] = {k: r["mfma_bound_layers"].get(k) for k in ("launches", "achieved_TFLOPs", "frac")}
+        if r.get("multiscale"):
+            cr["multiscale"] = {k: r["multiscale"].get(k) for k in ("avg_call_ms", "achieved_GBs", "frac")}
+        if r.get("measured_ceilings"):
+            cr["frac_vs_measured_mfma"] = r["measured_ceilings"].get("frac_vs_measured_mfma")
+        if "non_conv_ms" in r and r.get("step_ms"):
+            cr["non_conv_share"] = r["non_conv_ms"] / r["step_ms"]
+        c["roofline"] = cr
+    if "parity" in out and out["parity"]:
+        p = out["parity"]
+        c["parity"] = {k: p[k] for k in ("max_abs_diff", "rel_diff", "tol", "pass", "images") if k in p}
+    if "cpu_baseline" in out and out["cpu_baseline"]:
+        b = out["cpu_baseline"]
+        c["cpu_baseline"] = {k: b[k] for k in ("value", "unit", "cores", "kind", "sample") if k in b}
+    for k in ("fp16_preact_aspp", "enhance", "train_amp"):
+        if k in out and out[k]:
+            c[k] = compact(out[k])
+    return _sig(c)
+
+
+def emit(out, args):
+    """rank 0: the full record to args.detail (when set), the compact line to stdout."""
+    if args.detail:
+        try:
+            os.makedirs(os.path.dirname(os.path.abspath(args.detail)), exist_ok=True)
+            with open(args.detail, "w") as f:
+                json.dump(out, f)
+            out = dict(out, detail=os.path.relpath(os.path.abspath(args.detail), REPO))
+        except OSError:
+            pass
+    print(json.dumps(compact(out)))
+
+
+# ----------------------------------------------------------------------------
 def main():
     args = parse()
+    if args.cpu_enhance_child:
+        n, size = args.cpu_enhance_child
+        print(json.dumps(cpu_enhance_baseline(n, size)))
+        return
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args))
     if args.dry_run:
         return dry_run(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.enhance:
-        trE = None
+        trE = cpuE = None
         if world == 1 and not args.no_traffic and not any(k.startswith("ROCPROF") for k in os.environ):
             trE = pmc_traffic("fp32", "plain", args.batch, args.size, ["--enhance"], CLAHE_KERNELS)
+        if world == 1 and args.cpu_seconds > 0:
+            cpuE = cpu_enhance_child(args.batch, args.size)
         world, rank, dev = dist_setup(args)
-        out = enhance_leg(args, world, rank, dev, args.batch, args.size, trE, 4)
+        out = enhance_leg(args, world, rank, dev, args.batch, args.size, trE, cpuE)
         if rank == 0:
-            print(json.dumps(out))
+            emit(out, args)
         if world > 1:
             torch.distributed.destroy_process_group()
         return
@@ -791,18 +888,20 @@ def main():
         out = train_leg(args, world, rank, dev, args.batch if args.batch != 32 else 8, args.size, args.amp,
                         args.steps, args.warmup, args.variant)
         if rank == 0:
-            print(json.dumps(out))
+            emit(out, args)
         if world > 1:
             torch.distributed.destroy_process_group()
         return
     nested = not args.no_nested and not (args.precision == "fp16" and args.variant == "preact_aspp")
-    traffic = traffic16 = trafficE = None
+    traffic = traffic16 = trafficE = cpuE = None
     if world == 1 and not args.no_traffic and not any(k.startswith("ROCPROF") for k in os.environ):
         # child processes, before this process initialises the GPU
         traffic = pmc_traffic(args.precision, args.variant, args.batch, args.size)
         if nested:
             traffic16 = pmc_traffic("fp16", "preact_aspp", args.batch, args.size)
             trafficE = pmc_traffic("fp32", "plain", args.batch, args.size, ["--enhance"], CLAHE_KERNELS)
+    if world == 1 and nested and args.cpu_seconds > 0:
+        cpuE = cpu_enhance_child(args.batch, args.size)  # a process pool: forked before any GPU context exists
     world, rank, dev = dist_setup(args)
     B, S = args.batch, args.size
     out = forward_leg(args, world, rank, dev, args.precision, args.variant, B, S, traffic,
@@ -810,11 +909,11 @@ def main():
     if nested:
         out["fp16_preact_aspp"] = forward_leg(args, world, rank, dev, "fp16", "preact_aspp", B, S, traffic16,
                                               (B, "the full timed batch"))
-        out["enhance"] = enhance_leg(args, world, rank, dev, B, S, trafficE, 4)
+        out["enhance"] = enhance_leg(args, world, rank, dev, B, S, trafficE, cpuE)
         if world == 1:
             out["train_amp"] = train_leg(args, world, rank, dev, 8, S, True, 5, 2, "plain")
     if rank == 0:
-        print(json.dumps(out))
+        emit(out, args)
     if world > 1:
         torch.distributed.destroy_process_group()
 

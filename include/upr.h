@@ -90,6 +90,11 @@ int upr_model_forward(UprModel* model, const void* x, int B, int H, int W, void*
 
 void upr_model_destroy(UprModel* model);
 
+/* Number of forwards of this handle so far that ran the two-stream schedule
+ * above (0 when every forward stayed on one stream; -1 for NULL).  No
+ * reference counterpart: lets a caller report which executor actually ran. */
+long long upr_model_forks(const UprModel* model);
+
 /* Per-op profiling of upr_model_forward (no reference counterpart: the
  * reference only brackets whole calls with time.time(), simple_enhance.py:165-179).
  * enable != 0 records a hipEvent pair around every op of every later forward

@@ -390,7 +390,6 @@ int launch_conv_ring(const ConvOp& op, hipStream_t st);
 int launch_conv_ring32(const ConvOp& op, hipStream_t st);
 int launch_conv_wide32(const ConvOp& op, hipStream_t st);
 int launch_conv_t2(const ConvOp& op, int dtype, hipStream_t st);
-int launch_conv_pw(const ConvOp& op, hipStream_t st);
 
 int launch_preact_f16(const void* x, const float* sc, const float* sh, void* o, size_t npix, int C, hipStream_t st);
 

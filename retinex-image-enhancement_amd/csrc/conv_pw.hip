@@ -252,7 +252,7 @@ __global__ __launch_bounds__(256) void conv_s2dg_kernel(ConvOp op, int ngroups) 
 // the 3x3 stride-2 input gradient above (op: dy as a 1-segment 3x3 op over
 // Hin x Win with the flipped filter, out32 family at 2 Hin x 2 Win); 64 -> 32
 // channels only (the filter must fit the registers)
-int launch_conv_s2dg(const ConvOp& op, hipStream_t st) {
+int launch_conv_s2dg(const ConvOp& op, hipStream_t st, bool probe) {
   const ConvSeg& s = op.seg[0];
   if (op.nseg != 1 || op.store != kStoreNHWC || !op.out32 || op.bias || op.relu || op.res1 || op.res2 || op.pool ||
       op.img_bias || op.scale || op.out2)
@@ -265,6 +265,7 @@ int launch_conv_s2dg(const ConvOp& op, hipStream_t st) {
   if (op.out32_h16 && ((uintptr_t)op.out32_h16 % 8 || op.out32_h16_cs % 4)) return kErrUnsupported;
   const long long npix = (long long)op.B * s.Hin * s.Win;
   if (npix >= (1ll << 31) / 4) return kErrUnsupported;
+  if (probe) return kOk;
   const int ngroups = (int)(npix / 16);
   int cus = 256;
   {
@@ -279,7 +280,7 @@ int launch_conv_s2dg(const ConvOp& op, hipStream_t st) {
 
 // fp16 1x1 stride-1 convs of the shapes above; kErrUnsupported otherwise
 // (an out_s2 op must be taken here: no other kernel implements it)
-int launch_conv_pw(const ConvOp& op, hipStream_t st) {
+int launch_conv_pw(const ConvOp& op, hipStream_t st, bool probe) {
   if (op.nseg != 1 || op.store != kStoreNHWC) return kErrUnsupported;
   const ConvSeg& s = op.seg[0];
   if (s.kh != 1 || s.kw != 1 || s.stride != 1 || s.pad != 0 || s.pre != kPreNone || s.kbase != 0) return kErrUnsupported;
@@ -294,9 +295,11 @@ int launch_conv_pw(const ConvOp& op, hipStream_t st) {
     if (op.res32 && ((uintptr_t)op.res32 % 16 || op.res32_cs % 4)) return kErrUnsupported;
     if (op.mask16 && ((uintptr_t)op.mask16 % 8 || op.mask16_cs % 4)) return kErrUnsupported;
     if (op.out32_h16 && ((uintptr_t)op.out32_h16 % 8 || op.out32_h16_cs % 4)) return kErrUnsupported;
+    if (probe) return kOk;
     return op.out_s2 ? pw_k<true, true>(op, st) : pw_k<true, false>(op, st);
   }
   if ((uintptr_t)op.out % 8 || op.out_cs % 4 || op.out_coff % 4) return kErrUnsupported;
+  if (probe) return kOk;
   return pw_k<false, false>(op, st);
 }
 

@@ -570,6 +570,159 @@ __global__ __launch_bounds__(256) void ms_sums_kernel(const T* __restrict__ x, u
   }
 }
 
+// One pass for all three scales (H % 4 == 0, W % 4 == 0: the 0.5 / 0.25
+// bilinear samples are then 2x2 blends of full-resolution pixels, taps at
+// rows / columns 2y, 2y + 1 and 4y + 1, 4y + 2, weights exactly 0.5).  A block
+// owns a 32 x 64 full-resolution tile = a 16 x 32 half and an 8 x 16 quarter
+// tile; it stages the full-resolution region with a 4-pixel halo in LDS
+// (every pixel of the image is read from HBM once, halos from L2), forms the
+// half / quarter samples (+ their 1-sample halos) from LDS with sample_s's
+// arithmetic, and sums the 7 features of all three tiles.  The three block
+// sums go to the image's fixed-point accumulators; the block that completes
+// an image (per-image arrival counter) writes its fp64 sums and factor and
+// resets the accumulators to zero for the next call -- no factor launch, no
+// per-call memset (the scratch is zeroed once when allocated).
+constexpr int M3_TH = 32, M3_TW = 64, M3_HALO = 4;
+constexpr int M3_RH = M3_TH + 2 * M3_HALO, M3_RW = M3_TW + 2 * M3_HALO;
+constexpr int M3_H1 = M3_TH / 2 + 2, M3_W1 = M3_TW / 2 + 2, M3_H2 = M3_TH / 4 + 2, M3_W2 = M3_TW / 4 + 2;
+
+__device__ __forceinline__ float blend_half(float v00, float v01, float v10, float v11) {
+  const float ly = 0.5f, lx = 0.5f;  // sample_s with fy - y0 = fx - x0 = 0.5
+  return (1.f - ly) * ((1.f - lx) * v00 + lx * v01) + ly * ((1.f - lx) * v10 + lx * v11);
+}
+
+// the 7 features of pixel (R, C) of an LDS image P (3 planes of PH x PW)
+// whose pixel (R, C) is image pixel (y, x) of an hs x ws scale (torch.gradient:
+// central differences, one-sided at the borders)
+template <int PH, int PW>
+__device__ __forceinline__ float ms_feat(const float (&P)[3][PH][PW], int R, int C, int y, int x, int hs, int ws) {
+  float c3[3];
+  float fsum = 0.f;
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) {
+    const float v = P[ch][R][C];
+    c3[ch] = v;
+    float gx, gy;
+    if (ws < 2) gx = 0.f;
+    else if (x == 0) gx = P[ch][R][C + 1] - v;
+    else if (x == ws - 1) gx = v - P[ch][R][C - 1];
+    else gx = (P[ch][R][C + 1] - P[ch][R][C - 1]) / 2.f;
+    if (hs < 2) gy = 0.f;
+    else if (y == 0) gy = P[ch][R + 1][C] - v;
+    else if (y == hs - 1) gy = v - P[ch][R - 1][C];
+    else gy = (P[ch][R + 1][C] - P[ch][R - 1][C]) / 2.f;
+    fsum += v + sqrtf(gx * gx + gy * gy);
+  }
+  fsum += 0.299f * c3[0] + 0.587f * c3[1] + 0.114f * c3[2];
+  return fsum;
+}
+
+__device__ __forceinline__ double ms_factor(const double* sums, int b, double n0, double n1, double n2);
+
+template <typename T>
+__global__ __launch_bounds__(256) void ms_sums3_kernel(const T* __restrict__ x, unsigned long long* __restrict__ acc,
+                                                       unsigned* __restrict__ cnt, double* __restrict__ sums,
+                                                       double* __restrict__ factor, int H, int W, int tiles_x,
+                                                       unsigned nblk_img, double n0, double n1, double n2) {
+  __shared__ float full[3][M3_RH][M3_RW];
+  __shared__ float s1[3][M3_H1][M3_W1];
+  __shared__ float s2[3][M3_H2][M3_W2];
+  __shared__ double red[4][3];
+  __shared__ int is_last;
+  const int t = threadIdx.x;
+  const int b = blockIdx.y;
+  const int ty0 = (blockIdx.x / tiles_x) * M3_TH, tx0 = (blockIdx.x % tiles_x) * M3_TW;
+  const size_t HW = (size_t)H * W;
+  const T* img = x + (size_t)b * 3 * HW;
+  // full-resolution region: rows ty0 - 4 .., columns tx0 - 4 .. in 4-pixel quads
+  constexpr int QPR = M3_RW / 4, QPC = M3_RH * QPR;
+  for (int i = t; i < 3 * QPC; i += 256) {
+    const int ch = i / QPC, rq = i - ch * QPC, r = rq / QPR, q = rq - r * QPR;
+    const int ys = ty0 - M3_HALO + r, xs = tx0 - M3_HALO + 4 * q;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if ((unsigned)ys < (unsigned)H && (unsigned)xs < (unsigned)W) Vec4<T>::load(img + ch * HW + (size_t)ys * W + xs, v);
+    *(float4*)&full[ch][r][4 * q] = make_float4(v[0], v[1], v[2], v[3]);
+  }
+  __syncthreads();
+  const int h1 = H / 2, w1 = W / 2, h2 = H / 4, w2 = W / 4;
+  // half / quarter samples with their 1-sample halos (LDS rows of sample r:
+  // 2r + 2, 2r + 3 / 4r + 1, 4r + 2 of the region, by the halo of 4)
+  for (int i = t; i < M3_H1 * M3_W1 + M3_H2 * M3_W2; i += 256) {
+    if (i < M3_H1 * M3_W1) {
+      const int r = i / M3_W1, c = i - r * M3_W1;
+      const int ys = ty0 / 2 - 1 + r, xs = tx0 / 2 - 1 + c;
+      if ((unsigned)ys < (unsigned)h1 && (unsigned)xs < (unsigned)w1) {
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch)
+          s1[ch][r][c] = blend_half(full[ch][2 * r + 2][2 * c + 2], full[ch][2 * r + 2][2 * c + 3],
+                                    full[ch][2 * r + 3][2 * c + 2], full[ch][2 * r + 3][2 * c + 3]);
+      }
+    } else {
+      const int j = i - M3_H1 * M3_W1;
+      const int r = j / M3_W2, c = j - r * M3_W2;
+      const int ys = ty0 / 4 - 1 + r, xs = tx0 / 4 - 1 + c;
+      if ((unsigned)ys < (unsigned)h2 && (unsigned)xs < (unsigned)w2) {
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch)
+          s2[ch][r][c] = blend_half(full[ch][4 * r + 1][4 * c + 1], full[ch][4 * r + 1][4 * c + 2],
+                                    full[ch][4 * r + 2][4 * c + 1], full[ch][4 * r + 2][4 * c + 2]);
+      }
+    }
+  }
+  __syncthreads();
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+  {
+    const int c = t & 63;
+#pragma unroll
+    for (int k = 0; k < M3_TH / 4; ++k) {
+      const int r = (t >> 6) + 4 * k;
+      const int y = ty0 + r, xx = tx0 + c;
+      if (y < H && xx < W) a0 += (double)ms_feat(full, r + M3_HALO, c + M3_HALO, y, xx, H, W);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int i = t + 256 * k, r = i >> 5, c = i & 31;
+    const int y = ty0 / 2 + r, xx = tx0 / 2 + c;
+    if (y < h1 && xx < w1) a1 += (double)ms_feat(s1, r + 1, c + 1, y, xx, h1, w1);
+  }
+  if (t < 128) {
+    const int r = t >> 4, c = t & 15;
+    const int y = ty0 / 4 + r, xx = tx0 / 4 + c;
+    if (y < h2 && xx < w2) a2 += (double)ms_feat(s2, r + 1, c + 1, y, xx, h2, w2);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a0 += __shfl_xor(a0, o, 64);
+    a1 += __shfl_xor(a1, o, 64);
+    a2 += __shfl_xor(a2, o, 64);
+  }
+  if ((t & 63) == 0) { red[t >> 6][0] = a0; red[t >> 6][1] = a1; red[t >> 6][2] = a2; }
+  __syncthreads();
+  if (t < 3) {
+    const double blk = red[0][t] + red[1][t] + red[2][t] + red[3][t];
+    atomicAdd(&acc[b * 3 + t], (unsigned long long)(long long)llrint(blk * kMsFix));
+  }
+  __syncthreads();
+  if (t == 0) {
+    __threadfence();  // this block's adds are performed before its arrival is
+    is_last = atomicAdd(&cnt[b], 1u) == nblk_img - 1;
+  }
+  __syncthreads();
+  if (is_last && t == 0) {
+    __threadfence();
+    double sm[3];
+    for (int i = 0; i < 3; ++i) {
+      // read and reset in one atomic (the accumulators stay zero between calls)
+      const unsigned long long q = atomicExch(&acc[b * 3 + i], 0ull);
+      sm[i] = (double)(long long)q / kMsFix;
+      sums[b * 3 + i] = sm[i];
+    }
+    atomicExch(&cnt[b], 0u);
+    if (factor) factor[b] = ms_factor(sums, b, n0, n1, n2);
+  }
+}
+
 // fixed-point accumulators -> fp64 sums (in place) and the factor
 // factor[b] = 1 + sum_i w_i * mean_i * 0.1, mean_i = float32(sums[b][i] / (7*h_i*w_i))
 // (torch.mean returns a float32 tensor; .item() widens it; Python accumulates in
@@ -753,20 +906,10 @@ int launch_gray_hist(const void* img, int* hist, int B, int H, int W, int dtype,
 
 int launch_multiscale(const void* x, const void* enh, void* out, double* sums, double* factor, int B, int H, int W,
                       int dtype, hipStream_t st) {
-  UPR_CHECK_HIP(hipMemsetAsync(sums, 0, sizeof(double) * 3 * B, st));
   const int hs[3] = {H, (int)(H * 0.5), (int)(H * 0.25)};
   const int wsz[3] = {W, (int)(W * 0.5), (int)(W * 0.25)};
-  for (int s = 0; s < 3; ++s) {
+  for (int s = 0; s < 3; ++s)
     if (hs[s] < 1 || wsz[s] < 1) return kErrShape;
-    const int tx = (wsz[s] + MS_TW - 1) / MS_TW, ty = (hs[s] + MS_TH - 1) / MS_TH;
-    unsigned long long* acc = (unsigned long long*)sums;
-    if (dtype == kF16)
-      hipLaunchKernelGGL((ms_sums_kernel<half_t>), dim3(tx * ty, B), dim3(256), 0, st, (const half_t*)x, acc, H, W,
-                         hs[s], wsz[s], s, tx);
-    else
-      hipLaunchKernelGGL((ms_sums_kernel<float>), dim3(tx * ty, B), dim3(256), 0, st, (const float*)x, acc, H, W,
-                         hs[s], wsz[s], s, tx);
-  }
   const double n0 = 7.0 * hs[0] * wsz[0], n1 = 7.0 * hs[1] * wsz[1], n2 = 7.0 * hs[2] * wsz[2];
   // the clamp needs the factor: use the caller's buffer, else a per-device scratch one
   double* fac = factor;
@@ -774,7 +917,38 @@ int launch_multiscale(const void* x, const void* enh, void* out, double* sums, d
     fac = (double*)scratch(kSlotTmp, sizeof(double) * B, st);
     if (!fac) return (int)hipErrorOutOfMemory;
   }
-  hipLaunchKernelGGL(ms_factor_kernel, dim3((B + 63) / 64), dim3(64), 0, st, sums, fac, B, n0, n1, n2);
+  if (H % 4 == 0 && W % 4 == 0 && (uintptr_t)x % (dtype == kF16 ? 8 : 16) == 0) {
+    // single pass (ms_sums3_kernel): accumulators + arrival counters in a
+    // scratch slot that the kernel leaves zeroed
+    bool fresh = false;
+    const size_t accb = ((size_t)B * 3 * sizeof(unsigned long long) + 255) & ~(size_t)255;
+    uint8_t* sc = (uint8_t*)scratch(kSlotMs, accb + (size_t)B * sizeof(unsigned), st, &fresh);
+    if (!sc) return (int)hipErrorOutOfMemory;
+    if (fresh) UPR_CHECK_HIP(hipMemsetAsync(sc, 0, accb + (size_t)B * sizeof(unsigned), st));
+    const int tx = (W + M3_TW - 1) / M3_TW, ty = (H + M3_TH - 1) / M3_TH;
+    unsigned long long* acc = (unsigned long long*)sc;
+    unsigned* cnt = (unsigned*)(sc + accb);
+    if (dtype == kF16)
+      hipLaunchKernelGGL((ms_sums3_kernel<half_t>), dim3(tx * ty, B), dim3(256), 0, st, (const half_t*)x, acc, cnt,
+                         sums, fac, H, W, tx, (unsigned)(tx * ty), n0, n1, n2);
+    else
+      hipLaunchKernelGGL((ms_sums3_kernel<float>), dim3(tx * ty, B), dim3(256), 0, st, (const float*)x, acc, cnt,
+                         sums, fac, H, W, tx, (unsigned)(tx * ty), n0, n1, n2);
+    UPR_CHECK_HIP(hipGetLastError());
+  } else {
+    UPR_CHECK_HIP(hipMemsetAsync(sums, 0, sizeof(double) * 3 * B, st));
+    for (int s = 0; s < 3; ++s) {
+      const int tx = (wsz[s] + MS_TW - 1) / MS_TW, ty = (hs[s] + MS_TH - 1) / MS_TH;
+      unsigned long long* acc = (unsigned long long*)sums;
+      if (dtype == kF16)
+        hipLaunchKernelGGL((ms_sums_kernel<half_t>), dim3(tx * ty, B), dim3(256), 0, st, (const half_t*)x, acc, H, W,
+                           hs[s], wsz[s], s, tx);
+      else
+        hipLaunchKernelGGL((ms_sums_kernel<float>), dim3(tx * ty, B), dim3(256), 0, st, (const float*)x, acc, H, W,
+                           hs[s], wsz[s], s, tx);
+    }
+    hipLaunchKernelGGL(ms_factor_kernel, dim3((B + 63) / 64), dim3(64), 0, st, sums, fac, B, n0, n1, n2);
+  }
   if (enh && out) {
     const int CHW = 3 * H * W;
     const bool v4 = CHW % 4 == 0 && ((uintptr_t)enh | (uintptr_t)out) % (dtype == kF16 ? 8 : 16) == 0;

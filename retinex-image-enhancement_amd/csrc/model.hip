@@ -17,6 +17,7 @@
 //  * Spatial attention is a per-pixel scalar and commutes with that projection.
 //  * ASPP's global branch is a per-(image, channel) bias of the ASPP fusion GEMM.
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -327,6 +328,7 @@ struct UprModel {
   std::map<std::pair<int, hipStream_t>, std::shared_ptr<Side>> sides;
   unsigned long long side_clock = 0;
   std::mutex sides_mu;
+  std::atomic<long long> forks{0};  // forwards that ran the two-stream schedule (upr_model_forks)
 };
 
 namespace upr {
@@ -838,11 +840,12 @@ static std::shared_ptr<Side> side_of(UprModel* m, hipStream_t st) {
   // profiles/r3_ms_streams_ab.txt) and a single stream keeps each kernel's
   // duration separable in a trace (the headline's rocprofv3 evidence)
   if (en == 0 || (en < 0 && m->dtype != kF16)) return nullptr;
-  // a pseudo-handle names a different real stream per calling thread
-  // (hipStreamPerThread, and the null stream under per-thread default
-  // streams): a Side keyed by it would be shared by threads whose fork / join
-  // events then interleave.  Those forwards stay on the one stream (upr.h)
-  if (st == nullptr || st == hipStreamPerThread) return nullptr;
+  // hipStreamPerThread names a different real stream per calling thread: a
+  // Side keyed by it would be shared by threads whose fork / join events then
+  // interleave, so those forwards stay on the one stream (upr.h).  The null
+  // stream is ONE real stream here (libupr is built without per-thread default
+  // streams), and torch's default stream passes it: it forks like any other.
+  if (st == hipStreamPerThread) return nullptr;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
   std::lock_guard<std::mutex> lk(m->sides_mu);
@@ -1043,6 +1046,7 @@ static int run_forward(UprModel* m, const void* x, int B, int H, int W, void* en
     // after op 0 (the side ops need only its scale1 output)
     const int fk = 1;
     int rc = kOk;
+    m->forks.fetch_add(1, std::memory_order_relaxed);
     for (int oi = 0; oi < fk; ++oi)
       if ((rc = run_op(oi, st)) != kOk) return rc;
     UPR_CHECK_HIP(hipEventRecord(sd->fork, st));
@@ -1183,6 +1187,8 @@ int upr_model_profile_read(UprModel* model, UprOpStat* out, int max_ops, int* n_
   }
   return UPR_OK;
 }
+
+long long upr_model_forks(const UprModel* model) { return model ? model->forks.load() : -1; }
 
 void upr_model_destroy(UprModel* model) {
   if (!model) return;

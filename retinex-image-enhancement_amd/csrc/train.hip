@@ -101,18 +101,17 @@ int wgrad16_gemm(const void* x16, int B, int H, int W, int Cin, const float* dy,
                  int torch_ci = 0, const void* dy16 = nullptr);
 
 // scratch(): see upr_common.h
-void* scratch(int slot, size_t bytes, hipStream_t st) {
+void* scratch(int slot, size_t bytes, hipStream_t st, bool* fresh) {
   struct Entry {
     int dev;
     hipStream_t st;
-    unsigned long long last_use;
     void* p[kSlotCount];
     size_t n[kSlotCount];
   };
   static std::mutex mu;
   static Entry tab[kScratchStreams];
   static int used = 0;
-  static unsigned long long clock = 0;
+  if (fresh) *fresh = false;
   if (slot < 0 || slot >= kSlotCount) return nullptr;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
@@ -121,28 +120,16 @@ void* scratch(int slot, size_t bytes, hipStream_t st) {
   for (int i = 0; i < used; ++i)
     if (tab[i].dev == dev && tab[i].st == st) e = &tab[i];
   if (!e) {
-    if (used < kScratchStreams) {
-      e = &tab[used++];
-    } else {
-      // full: evict the least recently used (device, stream).  Its stream may
-      // have been destroyed since, so its kernels are waited for by a device
-      // synchronise of ITS device (rare: only once more than kScratchStreams
-      // streams have called in), then its buffers are freed and reused
-      e = &tab[0];
-      for (int i = 1; i < used; ++i)
-        if (tab[i].last_use < e->last_use) e = &tab[i];
-      if (e->dev != dev && hipSetDevice(e->dev) != hipSuccess) return nullptr;
-      const hipError_t se = hipDeviceSynchronize();
-      for (int s = 0; s < kSlotCount; ++s)
-        if (e->p[s]) (void)hipFree(e->p[s]);
-      if (e->dev != dev) (void)hipSetDevice(dev);
-      if (se != hipSuccess) return nullptr;
-    }
+    // full: an error, not an eviction.  Another thread may hold a pointer of
+    // any entry whose kernel it has not launched yet, so no entry can be freed
+    // safely here (a device synchronise does not cover a launch still to come,
+    // and it fails while any stream of the device is being captured)
+    if (used >= kScratchStreams) return nullptr;
+    e = &tab[used++];
     memset(e, 0, sizeof(*e));
     e->dev = dev;
     e->st = st;
   }
-  e->last_use = ++clock;
   if (bytes == 0) bytes = 16;
   if (e->n[slot] < bytes) {
     if (e->p[slot]) {
@@ -158,6 +145,7 @@ void* scratch(int slot, size_t bytes, hipStream_t st) {
       return nullptr;
     }
     e->n[slot] = grow;
+    if (fresh) *fresh = true;
   }
   return e->p[slot];
 }
@@ -2615,12 +2603,6 @@ int upr_t_conv_mfma16(const float* x, int B, int H, int W, int Cin, int x_cs, in
   if (Ho <= 0 || Wo <= 0) return UPR_ERR_SHAPE;
   hipStream_t st = ST(stream);
   const long long Mi = (long long)B * H * W;
-  if (!x16_ready) {
-    if ((uintptr_t)x % 16 || x_cs % 8 || x_coff % 8) return UPR_ERR_ARG;
-    hipLaunchKernelGGL(cast_act_f16_kernel, dim3(grid_for(Mi * (Cin / 8))), dim3(256), 0, st, x, Mi, Cin, x_cs, x_coff,
-                       (half_t*)x16);
-    UPR_CHECK_HIP(hipGetLastError());
-  }
   ConvOp c;
   memset(&c, 0, sizeof(c));
   c.nseg = 1;
@@ -2630,25 +2612,37 @@ int upr_t_conv_mfma16(const float* x, int B, int H, int W, int Cin, int x_cs, in
   c.B = B; c.Ho = Ho; c.Wo = Wo; c.N = N; c.Kpad = kh * kw * Cin;
   c.W = wp16; c.bias = bias; c.relu = relu;
   c.store = store == 1 ? kStoreConvT2x2 : kStoreNHWC;
+  // the fp32 output (+ fp32 residual / accumulated gradient) straight from the conv epilogue
+  ConvOp c32 = c;
+  c32.out32 = y; c32.out32_cs = y_cs; c32.out32_coff = y_coff;
+  c32.res32 = res; c32.res32_cs = res_cs;
+  if (want16) { c32.out32_h16 = y16; c32.out32_h16_cs = ycs16; }
+  c32.skip32 = only16 ? 1 : 0;
+  c32.out_s2 = s2 ? 1 : 0;
+  ConvOp cdg = c;
   if (s2dg) {
-    c.Ho = 2 * H; c.Wo = 2 * W;
-    c.out32 = y; c.out32_cs = y_cs; c.out32_coff = y_coff;
-    c.res32 = res; c.res32_cs = res_cs;
-    if (want16) { c.out32_h16 = y16; c.out32_h16_cs = ycs16; }
-    c.skip32 = only16 ? 1 : 0;
-    const int rc = launch_conv_s2dg(c, st);
+    cdg.Ho = 2 * H; cdg.Wo = 2 * W;
+    cdg.out32 = y; cdg.out32_cs = y_cs; cdg.out32_coff = y_coff;
+    cdg.res32 = res; cdg.res32_cs = res_cs;
+    if (want16) { cdg.out32_h16 = y16; cdg.out32_h16_cs = ycs16; }
+    cdg.skip32 = only16 ? 1 : 0;
+  }
+  // the forms only one kernel implements decline BEFORE the operand cast is queued
+  if (s2dg && launch_conv_s2dg(cdg, st, true) == kErrUnsupported) return UPR_ERR_UNSUPPORTED;
+  if (s2 && launch_conv_pw(c32, st, true) == kErrUnsupported) return UPR_ERR_UNSUPPORTED;
+  if (!x16_ready) {
+    if ((uintptr_t)x % 16 || x_cs % 8 || x_coff % 8) return UPR_ERR_ARG;
+    hipLaunchKernelGGL(cast_act_f16_kernel, dim3(grid_for(Mi * (Cin / 8))), dim3(256), 0, st, x, Mi, Cin, x_cs, x_coff,
+                       (half_t*)x16);
+    UPR_CHECK_HIP(hipGetLastError());
+  }
+  if (s2dg) {
+    const int rc = launch_conv_s2dg(cdg, st);
     if (rc == kErrUnsupported) return UPR_ERR_UNSUPPORTED;
     if (rc != 0) return rc;
     LAUNCH_CHECK();
   }
   {
-    // the fp32 output (+ fp32 residual / accumulated gradient) straight from the conv epilogue
-    ConvOp c32 = c;
-    c32.out32 = y; c32.out32_cs = y_cs; c32.out32_coff = y_coff;
-    c32.res32 = res; c32.res32_cs = res_cs;
-    if (want16) { c32.out32_h16 = y16; c32.out32_h16_cs = ycs16; }
-    c32.skip32 = only16 ? 1 : 0;
-    c32.out_s2 = s2 ? 1 : 0;
     const int rc = launch_conv_out32(c32, st);
     if (rc != kErrUnsupported) {
       if (rc != 0) return rc;

@@ -119,7 +119,9 @@ struct ConvOp {
 int launch_conv_out32(const ConvOp& op, hipStream_t stream);
 // the input gradient of a 3x3 stride-2 pad-1 conv straight from dy (conv_pw.hip;
 // op = the stride-1 dgrad op over dy with the flipped filter, output 2H x 2W)
-int launch_conv_s2dg(const ConvOp& op, hipStream_t stream);
+int launch_conv_s2dg(const ConvOp& op, hipStream_t stream, bool probe = false);
+// fp16 1x1 streaming convs (conv_pw.hip); probe: only answer kOk / kErrUnsupported
+int launch_conv_pw(const ConvOp& op, hipStream_t stream, bool probe = false);
 
 int launch_conv(const ConvOp& op, int dtype, hipStream_t stream);
 
@@ -162,9 +164,11 @@ inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 // stalled the launch queue.  Growth (warm-up only) synchronises the stream
 // before freeing the smaller buffer.  Returns nullptr when out of memory.
 // At most kScratchStreams (device, stream) pairs hold buffers; a new pair
-// past that evicts the least recently used one (device synchronise + free).
+// past that gets nullptr (the caller's entry point returns an error): an
+// entry is never freed while the process runs, so no thread's pointer dangles.
 constexpr int kScratchStreams = 64;
-enum ScratchSlot { kSlotSlab = 0, kSlotCast, kSlotTmp, kSlotCode, kSlotRows, kSlotPart, kSlotCount };
-void* scratch(int slot, size_t bytes, hipStream_t st);
+enum ScratchSlot { kSlotSlab = 0, kSlotCast, kSlotTmp, kSlotCode, kSlotRows, kSlotPart, kSlotMs, kSlotCount };
+// fresh (optional): set true when the returned buffer was (re)allocated by this call
+void* scratch(int slot, size_t bytes, hipStream_t st, bool* fresh = nullptr);
 
 }  // namespace upr

@@ -19,6 +19,8 @@ Differences, all forced by the environment and recorded in DESIGN.md:
     history; texture_method 'tv' and 'edge_density' both run on the device;
     use_dynamic_smooth_weight=False uses weight_smooth as is.
 """
+import threading
+
 import torch
 import torch.nn as nn
 
@@ -226,16 +228,25 @@ class TotalLoss(_EngineHolder):
             self.loss_history = {k: [] for k in _DWA_KEYS}
 
     def forward(self, img_low, img_enhanced, illu_map, reflectance=None, epoch=0):
-        if reflectance is None:
-            raise NotImplementedError("the device TotalLoss needs the reflectance (the model always returns it)")
+        no_refl = reflectance is None
         for t, n in ((img_low, "img_low"), (img_enhanced, "img_enhanced"), (illu_map, "illu_map"),
                      (reflectance, "reflectance")):
-            _require(t, n)
+            if t is not None:
+                _require(t, n)
+        if no_refl:
+            # loss.py:678-682: no reflectance -> the decoupling term is 0.  The
+            # kernels still take a [B,3,H,W] operand: the enhanced image stands
+            # in (weight 0: no contribution to the total or any gradient), and
+            # the term is reported as exactly 0
+            reflectance = img_enhanced.detach()
         eng = self._engine(img_enhanced.device)
         # weights of this step (loss.py:690-702): DWA from the history after epoch 1
         eng.w = self._compute_adaptive_weights() if self.adaptive_weights and epoch > 1 else dict(self._weights)
+        if no_refl:
+            eng.w["decouple"] = 0.0
+        eng.zero_decouple = no_refl
         total, terms = loss_forward(eng, img_low.contiguous(), img_enhanced, illu_map, reflectance)
-        d = E.terms_dict(terms, lazy=_DEFER_READBACK[0] and not self.adaptive_weights)
+        d = E.terms_dict(terms, lazy=_defer_readback() and not self.adaptive_weights)
         if self.adaptive_weights:
             for k in _DWA_KEYS:
                 self.loss_history[k].append(d[k])
@@ -254,17 +265,22 @@ _DWA_KEYS = ("exposure", "smoothness", "color", "spatial", "decouple", "perceptu
 # set by trainers.train.train_step around its criterion call: the loss_dict's
 # host read-back is deferred until the step's backward and optimizer work is
 # queued (the step returns it materialised), instead of draining the device
-# between the forward and the backward as the reference's .item()s do
-_DEFER_READBACK = [False]
+# between the forward and the backward as the reference's .item()s do.
+# Per thread: another thread's criterion call never sees this one's switch.
+_DEFER_READBACK = threading.local()
+
+
+def _defer_readback():
+    return getattr(_DEFER_READBACK, "on", False)
 
 
 class deferred_readback:
     def __enter__(self):
-        self._prev = _DEFER_READBACK[0]
-        _DEFER_READBACK[0] = True
+        self._prev = _defer_readback()
+        _DEFER_READBACK.on = True
 
     def __exit__(self, *exc):
-        _DEFER_READBACK[0] = self._prev
+        _DEFER_READBACK.on = self._prev
 
 
 def dwa_weights(history, defaults, temperature=2.0):

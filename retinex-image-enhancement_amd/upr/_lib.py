@@ -54,6 +54,7 @@ SIGNATURES = {
     "upr_model_forward": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_size_t, c_void_p]),
     "upr_model_destroy": (None, [c_void_p]),
+    "upr_model_forks": (ctypes.c_longlong, [c_void_p]),
     "upr_model_profile": (c_int, [c_void_p, c_int]),
     "upr_model_profile_read": (c_int, [c_void_p, ctypes.POINTER(UprOpStat), c_int, ctypes.POINTER(c_int)]),
     "upr_status_string": (ctypes.c_char_p, [c_int]),

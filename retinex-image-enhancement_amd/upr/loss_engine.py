@@ -174,6 +174,7 @@ class TotalLossEngine:
         if weights:
             self.w.update(weights)
         self.w_smooth = self.w["smoothness"]
+        self.zero_decouple = False  # set per call by TotalLoss.forward(reflectance=None)
         self.texture_method = texture_method
         self.use_freq = use_freq_loss
         self.params = dict(PARAMS)
@@ -214,6 +215,8 @@ class TotalLossEngine:
                                     ctypes.c_float(w["color"]), ctypes.c_float(w["spatial"]),
                                     ctypes.c_float(w["decouple"]), ctypes.c_float(self.w_smooth),
                                     TEXTURE[self.texture_method], ctypes.byref(prm), st), "loss_pixel")
+        if self.zero_decouple:  # TotalLoss without a reflectance: that term is 0 (loss.py:678-682)
+            zero(terms[TERM_ORDER.index("decouple"):TERM_ORDER.index("decouple") + 1])
         acc = torch.empty(4, dtype=torch.float64, device=dev)
         zero(acc)
         if self.vgg is not None and w["perceptual"] != 0.0:

@@ -118,6 +118,10 @@ class ModelHandle:
         """Record a HIP event pair around every op of later forwards."""
         L.check(self._lib.upr_model_profile(self._h, int(bool(enable))), "upr_model_profile")
 
+    def forks(self):
+        """Forwards so far that ran the two-stream (multi-scale side stream) schedule."""
+        return int(self._lib.upr_model_forks(self._h))
+
     def profile_read(self):
         """Per-op stats (launch order): list of dicts name/kind/calls/ms/flops/bytes."""
         n = ctypes.c_int(0)

@@ -470,7 +470,7 @@ class Conv:
         ready = src16 is not None
         x16 = src16 if ready else _h16(B * Ho * Wo * self.Cout, dev)
         keep = bool(o16) and not acc
-        y16 = _h16(B * 4 * Ho * Wo * self.Cin, dev)
+        y16 = _h16(B * 4 * Ho * Wo * self.Cin if keep else 16, dev)  # written only with keep
         rc = lib.upr_t_conv_mfma16(None if ready else _fp(gy.t, 0), B, Ho, Wo, self.Cout, gy.cs, gy.coff,
                                    _p(self.wt16), None, self.Cin, 3, 3, 1, 1, 1, gx.ptr() if acc else None,
                                    gx.cs if acc else 0, 0, _fp(gx.t), gx.cs, gx.coff, 16 | (6 if keep else 0),
@@ -828,12 +828,14 @@ class BN:
         self.batch_stats = bool(m.training)  # the backward follows the statistics this forward used
         # y = relu(bn(x)) (+ a residual added after the ReLU): the backward may fold the mask in
         self.relu_only = bool(relu) and (res is None or bool(res_post))
+        self.has_res = res is not None
         return out
 
     def bwd(self, g, gx, relu=False, only16=False):
         """g: Act gradient of the BN output; relu=True: g is the gradient of
-        relu(bn(x)) (this forward's relu=True, no residual), the ReLU mask is
-        folded into the BN backward (recomputed from x, no separate pass).
+        relu(bn(x)) (+ a residual added after the ReLU, res_post: this
+        forward's relu=True), the ReLU mask is folded into the BN backward
+        (recomputed from x, no separate pass; the residual does not enter it).
         Under autocast the input gradient also gets its compact fp16 copy
         (gx.t16) for the input-gradient conv that consumes it; only16 (the
         consumer's Conv.takes16_grad()): the fp32 gx is not written at all."""
@@ -870,6 +872,10 @@ class BN:
                 gx.t16, gx.t16_grad = dx16, dx16 is not None
                 return
         if relu:
+            # the mask comes from the stored output here: with a post-ReLU
+            # residual that output is relu(bn(x)) + skip, not the ReLU's own
+            # output, and the mask would be wrong wherever skip > 0 >= bn(x)
+            assert not self.has_res, "unfused ReLU backward of relu(bn(x)) + skip: mask needs the pre-residual value"
             relu_mask(g, self.out_act)
         zero(self.acc[:2 * self.C])
         _chk(lib.upr_t_bn_bwd_reduce(_fp(g.t), g.cs, g.coff, x.ptr(), x.cs, 0, _p(self.mean), _p(self.invstd), x.M,

@@ -10,6 +10,9 @@ models/model.py) and records, on seeded inputs:
   G6c3 g6_losses_c3.npz the reference self-test's shapes (loss.py:806-844):
                         3-channel illumination, smoothness / decoupling /
                         TotalLoss values and gradients
+  G6nr g6_losses_norefl.npz  TotalLoss(low, enh, illu) with reflectance=None
+                        (loss.py:678-682: the decoupling term is 0) on G6's
+                        inputs: value, loss dict, gradients w.r.t. enh / illu
   G7 g7_train_step.npz  one train_one_epoch step body (trainers/train.py:63-103,
                         no AMP) of the plain model (seed 0) on x = rand(2,3,64,64)
                         (generator seed 2): loss dict, per-parameter gradient
@@ -150,6 +153,26 @@ def g6c3():
     np.savez_compressed(os.path.join(OUT, "g6_losses_c3.npz"), **rec)
 
 
+def g6nr():
+    """TotalLoss without a reflectance (losses/loss.py:678-682): decouple = 0,
+    on the G6 inputs (seed 6), with the gradients w.r.t. enh and illu."""
+    gen = torch.Generator().manual_seed(6)
+    low = 0.4 * torch.rand(2, 3, 64, 64, generator=gen)
+    enh = torch.rand(2, 3, 64, 64, generator=gen)
+    illu = 0.2 + 0.6 * torch.rand(2, 1, 64, 64, generator=gen)
+    rec = {"low": low.numpy(), "enh": enh.numpy(), "illu": illu.numpy()}
+    crit = ref_loss.TotalLoss(use_freq_loss=True, adaptive_weights=False, texture_method="tv")
+    e = enh.clone().requires_grad_(True)
+    i = illu.clone().requires_grad_(True)
+    t, d = crit(low, e, i)
+    t.backward()
+    rec["total"] = t.detach().numpy()
+    for k, v in d.items():
+        rec["dict_" + k] = np.float64(v)
+    rec.update(grad_enh=e.grad.numpy(), grad_illu=i.grad.numpy())
+    np.savez_compressed(os.path.join(OUT, "g6_losses_norefl.npz"), **rec)
+
+
 def g7():
     torch.manual_seed(0)
     model = ref_model.UP_Retinex(use_preact=False, use_aspp=False)
@@ -195,6 +218,9 @@ if __name__ == "__main__":
         g6()
     if not only or "g6c3" in only:
         g6c3()
+    if not only or "g6nr" in only:
+        g6nr()
     if not only or "g7" in only:
         g7()
-    print("wrote", " ".join(only) if only else "g6_losses.npz g6_losses_c3.npz g7_train_step.npz")
+    print("wrote", " ".join(only) if only else
+          "g6_losses.npz g6_losses_c3.npz g6_losses_norefl.npz g7_train_step.npz")

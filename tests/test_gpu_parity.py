@@ -333,6 +333,36 @@ def test_multiscale_kernel(golden):
         assert maxdiff(out[b], ref) <= 1e-6
 
 
+@pytest.mark.parametrize("B,H,W,dtype", [
+    (2, 100, 136, torch.float32),   # single pass (H, W % 4 == 0), partial 32 x 64 tiles
+    (1, 8, 8, torch.float32),       # smallest: 2 x 2 quarter scale inside one tile
+    (3, 66, 50, torch.float32),     # H % 4 != 0: the three-launch path
+    (2, 96, 128, torch.float16),    # fp16 input, single pass
+    (32, 512, 512, torch.float32),  # the bench's enhance leg (images 0 and 31 checked)
+])
+def test_multiscale_single_pass(B, H, W, dtype):
+    """upr_multiscale's one-pass kernel (ms_sums3_kernel: all three scales from
+    one read, the completing block writes the sums / factor and re-zeroes the
+    accumulators) vs the oracle's per-image factor (multi_scale.py:62-100),
+    called three times in a row (a stale accumulator or arrival counter would
+    change the second and third result)."""
+    from upr import runtime
+    x = torch.rand(B, 3, H, W, generator=torch.Generator().manual_seed(21)).to(dtype)
+    enh = torch.rand(B, 3, H, W, generator=torch.Generator().manual_seed(22)).to(dtype)
+    xd, ed = x.to(DEV), enh.to(DEV)
+    runs = [runtime.multiscale(xd, ed) for _ in range(3)]
+    torch.cuda.synchronize()
+    idx = [0, B - 1] if B > 1 else [0]
+    fac = oenh.multiscale_factor(x[idx].float())
+    out0, f0, s0 = runs[0]
+    for out, f, sm in runs[1:]:
+        assert torch.equal(f, f0) and torch.equal(sm, s0) and torch.equal(out, out0)
+    for j, b in enumerate(idx):
+        assert abs(f0[b].item() - fac[j]) < 1e-6, (b, f0[b].item(), fac[j])
+        ref = torch.clamp(enh[b].float() * fac[j], 0, 1)
+        assert maxdiff(out0[b].float(), ref) <= (1e-6 if dtype == torch.float32 else 1e-3)
+
+
 # ---------------------------------------------------------------------------
 # full-size configs (BASELINE.json configs[1..3]): the whole batch runs on the
 # GPU, the oracle checks the first and the last image of the batch (direct
@@ -448,7 +478,14 @@ def test_multiscale_side_stream_matches_serial(dtype):
         handle.profile(True)
         serial = [[t.clone() for t in m(x)] for x in xs]
         handle.profile(False)
+        n0 = handle.forks()
         forked = [[t.clone() for t in m(x)] for x in xs]
+        # fp16 models fork on torch's default (null) stream too (unless
+        # UPR_MS_STREAMS=0), not only on an explicit caller stream
+        import os
+        env = os.environ.get("UPR_MS_STREAMS")
+        want = (dtype == torch.float16) if env is None else (int(env) != 0)
+        assert handle.forks() - n0 == (len(xs) if want else 0)
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):

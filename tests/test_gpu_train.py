@@ -267,11 +267,10 @@ def test_maxpool_bwd_matches_torch(B, C, H, W, k, s, p, nchw):
 
 def test_scratch_more_streams_than_table():
     """The per-(device, stream) scratch table (upr_common.h scratch(), 64
-    entries) evicts its least recently used stream: a training call that needs
-    scratch keeps working on the 65th..80th distinct stream (it returned
-    hipErrorOutOfMemory once 64 streams had been seen), and every result is
-    still right -- including on streams created after earlier ones were
-    destroyed."""
+    entries) never frees an entry while the process runs (another thread may
+    hold its pointer for a kernel it has not launched yet): once it is full a
+    call on a NEW stream returns an error instead of evicting, every call
+    before that is right, and a stream already in the table keeps working."""
     import ctypes
     import torch.nn.functional as F
     from upr import _lib as L
@@ -290,21 +289,29 @@ def test_scratch_more_streams_than_table():
     lib = L.lib()
     # raw HIP streams (torch.cuda.Stream() hands out a pool of 32 handles)
     hip = ctypes.CDLL("libamdhip64.so")
-    live = []
-    for i in range(80):
-        s = ctypes.c_void_p()
-        assert hip.hipStreamCreate(ctypes.byref(s)) == 0
-        live.append(s)
+
+    def run(s):
         dxd = torch.zeros(B, H, W, C, device=DEV)
         vd = L.UprView(dxd.data_ptr(), H * W * C, W * C, C, 1)
         torch.cuda.synchronize()
         rc = lib.upr_t_maxpool_bwd(ctypes.byref(vx), ctypes.byref(vg), B, H, W, C, 2, 2, 0, 8, 8,
                                    ctypes.byref(vd), s)
-        assert rc == 0, (i, rc)
-        assert hip.hipStreamSynchronize(s) == 0
-        assert torch.equal(dxd.permute(0, 3, 1, 2).cpu(), ref), i
-        if i % 3 == 0:  # destroyed while its scratch entry lives on
-            assert hip.hipStreamDestroy(live.pop()) == 0
+        if rc == 0:
+            assert hip.hipStreamSynchronize(s) == 0
+            assert torch.equal(dxd.permute(0, 3, 1, 2).cpu(), ref)
+        return rc
+
+    live, failed = [], None
+    for i in range(80):  # the table holds at most 64: some call below must fail
+        s = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+        live.append(s)
+        rc = run(s)
+        if rc != 0:
+            failed = i
+            break
+    assert failed is not None and failed <= 64, failed
+    assert run(live[0]) == 0  # registered before the table filled
     for s in live:
         assert hip.hipStreamDestroy(s) == 0
 
@@ -929,6 +936,32 @@ def test_loss_three_channel_illumination(golden):
         _close(t.grad, torch.from_numpy(g[name]), 1e-4, name)
     with pytest.raises(NotImplementedError):
         crit(low, enh, illu[:, :2].contiguous(), refl)
+
+
+def test_loss_without_reflectance(golden):
+    """TotalLoss(low, enh, illu) with reflectance=None (losses/loss.py:678-682:
+    the decoupling term is 0) on the device vs the reference's own value, loss
+    dict and gradients w.r.t. enh / illu (G6nr, make_golden_train.py)."""
+    from losses.loss import TotalLoss
+    g = golden("g6_losses_norefl.npz")
+    low, enh, illu = (torch.from_numpy(g[k]).to(DEV) for k in ("low", "enh", "illu"))
+    crit = TotalLoss(use_freq_loss=True).to(DEV)
+    e = enh.clone().requires_grad_(True)
+    i = illu.clone().requires_grad_(True)
+    total, d = crit(low, e, i)
+    assert d["decouple"] == 0.0
+    for k in ("exposure", "smoothness", "color", "spatial", "perceptual", "frequency", "total"):
+        np.testing.assert_allclose(d[k], float(g["dict_" + k]), rtol=1e-4, atol=1e-8, err_msg=k)
+    total.backward()
+    torch.cuda.synchronize()
+    for name, t in (("grad_enh", e), ("grad_illu", i)):
+        _close(t.grad, torch.from_numpy(g[name]), 1e-4, name)
+    # the same criterion object with a reflectance again: the decoupling term is back
+    g6 = golden("g6_losses.npz")
+    low, enh, illu, refl = (torch.from_numpy(g6[k]).to(DEV) for k in ("low", "enh", "illu", "refl"))
+    _, d = crit(low, enh, illu, refl)
+    np.testing.assert_allclose(d["decouple"], float(g6["dict_decouple"]), rtol=1e-4)
+    np.testing.assert_allclose(d["total"], float(g6["dict_total"]), rtol=1e-4)
 
 
 @pytest.mark.parametrize("texture,w_smooth", [("edge_density", 1.0), ("edge_density", 2.0), ("tv", 0.5)])
