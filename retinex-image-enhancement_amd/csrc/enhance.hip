@@ -635,13 +635,24 @@ __global__ __launch_bounds__(256) void ms_sums3_kernel(const T* __restrict__ x, 
   const size_t HW = (size_t)H * W;
   const T* img = x + (size_t)b * 3 * HW;
   // full-resolution region: rows ty0 - 4 .., columns tx0 - 4 .. in 4-pixel quads
-  constexpr int QPR = M3_RW / 4, QPC = M3_RH * QPR;
-  for (int i = t; i < 3 * QPC; i += 256) {
+  // every quad's load is issued before the first LDS store (NLD loads in
+  // flight per thread: one HBM round trip per block, not one per quad)
+  constexpr int QPR = M3_RW / 4, QPC = M3_RH * QPR, NLD = (3 * QPC + 255) / 256;
+  float v[NLD][4];
+#pragma unroll
+  for (int k = 0; k < NLD; ++k) {
+    const int i = t + 256 * k;
     const int ch = i / QPC, rq = i - ch * QPC, r = rq / QPR, q = rq - r * QPR;
     const int ys = ty0 - M3_HALO + r, xs = tx0 - M3_HALO + 4 * q;
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
-    if ((unsigned)ys < (unsigned)H && (unsigned)xs < (unsigned)W) Vec4<T>::load(img + ch * HW + (size_t)ys * W + xs, v);
-    *(float4*)&full[ch][r][4 * q] = make_float4(v[0], v[1], v[2], v[3]);
+    v[k][0] = v[k][1] = v[k][2] = v[k][3] = 0.f;
+    if (i < 3 * QPC && (unsigned)ys < (unsigned)H && (unsigned)xs < (unsigned)W)
+      Vec4<T>::load(img + ch * HW + (size_t)ys * W + xs, v[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < NLD; ++k) {
+    const int i = t + 256 * k;
+    const int ch = i / QPC, rq = i - ch * QPC, r = rq / QPR, q = rq - r * QPR;
+    if (i < 3 * QPC) *(float4*)&full[ch][r][4 * q] = make_float4(v[k][0], v[k][1], v[k][2], v[k][3]);
   }
   __syncthreads();
   const int h1 = H / 2, w1 = W / 2, h2 = H / 4, w2 = W / 4;
@@ -699,18 +710,20 @@ __global__ __launch_bounds__(256) void ms_sums3_kernel(const T* __restrict__ x, 
   }
   if ((t & 63) == 0) { red[t >> 6][0] = a0; red[t >> 6][1] = a1; red[t >> 6][2] = a2; }
   __syncthreads();
-  if (t < 3) {
-    const double blk = red[0][t] + red[1][t] + red[2][t] + red[3][t];
-    atomicAdd(&acc[b * 3 + t], (unsigned long long)(long long)llrint(blk * kMsFix));
-  }
-  __syncthreads();
-  if (t == 0) {
-    __threadfence();  // this block's adds are performed before its arrival is
-    is_last = atomicAdd(&cnt[b], 1u) == nblk_img - 1;
+  if (t < 64) {
+    // wave 0: the block's three fixed-point adds, then (once they are
+    // performed: agent-scope integer atomics execute at the memory side, and
+    // vmcnt(0) waits for their acknowledgement) its arrival.  No release
+    // fence: __threadfence's L2 write-back cost ~30 us per CU slot here
+    if (t < 3) {
+      const double blk = red[0][t] + red[1][t] + red[2][t] + red[3][t];
+      atomicAdd(&acc[b * 3 + t], (unsigned long long)(long long)llrint(blk * kMsFix));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (t == 0) is_last = atomicAdd(&cnt[b], 1u) == nblk_img - 1;
   }
   __syncthreads();
   if (is_last && t == 0) {
-    __threadfence();
     double sm[3];
     for (int i = 0; i < 3; ++i) {
       // read and reset in one atomic (the accumulators stay zero between calls)
