@@ -86,7 +86,10 @@ enum RingMode : int { kRingConv = 0, kRingHead = 1, kRingFam = 2, kRingS2 = 3 };
 // res2 (after it); kRingPool = per-image channel sums of the output into ConvOp::pool
 enum RingFlags : int {
   kRingRes = 1, kRingRelu = 2, kRingSc = 4, kRingOcc3 = 8, kRingWide = 16, kRingOut2 = 32, kRingOut32 = 64,
-  kRingDil2 = 128, kRingResPre = 256, kRingPool = 512, kRingXPool = 1024
+  kRingDil2 = 128, kRingResPre = 256, kRingPool = 512, kRingXPool = 1024,
+  // timing ablations only (results garbage; UPR_RING_ABL, tools/convbench.py):
+  // no ring DMA after the first two steps / no MFMAs / no output stores
+  kRingAblDma = 4096, kRingAblMma = 8192, kRingAblSt = 16384
 };
 // kRingXPool (fp32 ring): two more K slices after the 3x3 segment, a 1x1 over
 // x and a 1x1 over maxpool3x3(x) (EnhancedFAM branch1 / branch2 composed with
@@ -149,13 +152,30 @@ struct RingLanes {
   }
 };
 
+// Output-channel order of the fp16 ring's MFMA rows: fragment nt, row r holds
+// channel 32 (nt >> 1) + 8 (r >> 2) + 4 (nt & 1) + (r & 3), so a lane's
+// accumulators of fragments 2p and 2p + 1 are 8 CONSECUTIVE channels (32p +
+// 8 fg .. + 7) and the epilogue stores 16 bytes per lane (8-byte stores of 4
+// channels moved the 32/64-channel outputs at ~3 TB/s: every store
+// instruction wrote half-lines of 16 pixels).  The filter rows and every
+// per-channel parameter are read in this order.
+__device__ __forceinline__ int ring_ch(int nt, int r) { return 32 * (nt >> 1) + 8 * (r >> 2) + 4 * (nt & 1) + (r & 3); }
+// PAIR = false (the FAM fusion and the fp32-output programs: their registers
+// are full, and the fp32 stores are 16 bytes either way) keeps the plain order
+template <bool PAIR>
+__device__ __forceinline__ int ring_chm(int nt, int r) {
+  if constexpr (PAIR) return ring_ch(nt, r);
+  else return nt * 16 + r;
+}
+
 // filter [nslices x 32 k][NB] -> LDS [slice][n][64 B], chunk ^ ((n >> 2) & 1) * 2
-template <int NB, int THREADS>
+// (LDS row n holds filter row ring_ch(n >> 4, n & 15))
+template <int NB, int THREADS, bool PAIR = true>
 __device__ __forceinline__ void ring_load_filter(unsigned char* Wl, const half_t* Wg, int kpad, int nslices, int tid) {
   for (int i = tid; i < nslices * NB * 4; i += THREADS) {
     const int pc = i & 3, n = (i >> 2) % NB, sl = (i >> 2) / NB;
     const int c = pc ^ (((n >> 2) & 1) << 1);
-    *(uint4*)(Wl + (size_t)i * 16) = *(const uint4*)(Wg + (size_t)n * kpad + sl * 32 + c * 8);
+    *(uint4*)(Wl + (size_t)i * 16) = *(const uint4*)(Wg + (size_t)ring_chm<PAIR>(n >> 4, n & 15) * kpad + sl * 32 + c * 8);
   }
 }
 
@@ -218,7 +238,12 @@ struct RingCfg {
   static constexpr bool OUT2 = (FL & kRingOut2) != 0;
   static constexpr bool OUT32 = (FL & kRingOut32) != 0;
   static_assert(!OUT32 || (!RES && !SC && !OUT2 && MODE != kRingHead && MODE != kRingFam), "fp32 output: plain convs");
-  static constexpr int S = HEAD ? GPW : GPW * NT * (OUT2 ? 2 : 1);  // stores per wave per step
+  // stores per wave per step: one 16-byte store per fragment pair (ring_ch),
+  // two with OUT2; OUT32 issues one or two more (its fp32 halves / fp16 copy,
+  // runtime flags): counted at the minimum, so the waits below stay safe
+  static constexpr bool PAIR = !FAM && !OUT32;
+  static_assert(!PAIR || NT % 2 == 0, "fragment pairs");
+  static constexpr int S = HEAD ? GPW : PAIR ? GPW * (NT / 2) * (OUT2 ? 2 : 1) : GPW * NT * (OUT2 ? 2 : 1);
   // vmcnt waits, waves 0-3 (ring DMA) / waves 4-7 (none): DMA(kk) has landed
   // at step 0 / step 1 / steps >= 2 / after a FAM pool flush (its atomics)
   static constexpr int W0 = G, W1 = E + G + S, WK = 2 * S + E + G, WF = WK + (FAM ? 4 * NT : 0);
@@ -265,15 +290,15 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, RingCfg<MODE, C, NB, FL
     for (int sl = 0; sl < K::NSL; ++sl)
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt)
-        wr[sl][nt] = *(const f16x8_r*)((const half_t*)op.W + (size_t)(nt * 16 + fr) * op.Kpad + sl * 32 + fg * 8);
+        wr[sl][nt] = *(const f16x8_r*)((const half_t*)op.W + (size_t)ring_chm<K::PAIR>(nt, fr) * op.Kpad + sl * 32 + fg * 8);
   } else {
-    ring_load_filter<NB, K::THREADS>(Wl, (const half_t*)op.W, op.Kpad, K::NSL, tid);
+    ring_load_filter<NB, K::THREADS, K::PAIR>(Wl, (const half_t*)op.W, op.Kpad, K::NSL, tid);
   }
   f16x8_r wsc[SC ? NT : 1];  // shortcut segment (k rows NSL*32 ..)
   if constexpr (SC) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
-      wsc[nt] = *(const f16x8_r*)((const half_t*)op.W + (size_t)(nt * 16 + fr) * op.Kpad + K::NSL * 32 + fg * 8);
+      wsc[nt] = *(const f16x8_r*)((const half_t*)op.W + (size_t)ring_chm<K::PAIR>(nt, fr) * op.Kpad + K::NSL * 32 + fg * 8);
   }
   const half_t* srcA = (const half_t*)sa.src + sa.coff;
   const half_t* srcB = FAM ? (const half_t*)op.seg[2].src + op.seg[2].coff : nullptr;
@@ -312,7 +337,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, RingCfg<MODE, C, NB, FL
   auto issue = [&](int k) {
     const bool live = dc.j < nu;
     const int grp = (k + 1) & 3;
-    if (!dma_wave) {
+    if ((FL & kRingAblDma) && k >= 2) {
+    } else if (!dma_wave) {
     } else if constexpr (S2) {
       la.issue(srcA, csA, dc.b, Hin, Win, 2 * (dc.y0 + 4 * dc.s), 2 * dc.x0 - 1, live, zero, ringA, grp, wave);
     } else {
@@ -331,13 +357,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, RingCfg<MODE, C, NB, FL
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) bias4[nt][i] = op.bias ? op.bias[nt * 16 + fg * 4 + i] : 0.f;
+    for (int i = 0; i < 4; ++i) bias4[nt][i] = op.bias ? op.bias[K::PAIR ? ring_ch(nt, fg * 4 + i) : nt * 16 + fg * 4 + i] : 0.f;
   float hw2[NT][4];
   if constexpr (HEAD) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) hw2[nt][i] = op.head_w[nt * 16 + fg * 4 + i];
+      for (int i = 0; i < 4; ++i) hw2[nt][i] = op.head_w[ring_chm<K::PAIR>(nt, fg * 4 + i)];
   }
   float p2s[K::OUT2 ? NT : 1][4], p2h[K::OUT2 ? NT : 1][4];
   if constexpr (K::OUT2) {
@@ -345,8 +371,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, RingCfg<MODE, C, NB, FL
     for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        p2s[nt][i] = op.pre2_scale[nt * 16 + fg * 4 + i];
-        p2h[nt][i] = op.pre2_shift[nt * 16 + fg * 4 + i];
+        p2s[nt][i] = op.pre2_scale[ring_chm<K::PAIR>(nt, fg * 4 + i)];
+        p2h[nt][i] = op.pre2_shift[ring_chm<K::PAIR>(nt, fg * 4 + i)];
       }
   }
   const int abase = fg * RA::PLANE + fr * 16;  // chunk plane fg, pixel fr of a ring row
@@ -356,7 +382,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, RingCfg<MODE, C, NB, FL
   static_assert(K::THREADS <= 512 && NT <= 4, "sink: 128 bytes per thread");
   int oloff[GPW];
 #pragma unroll
-  for (int g = 0; g < GPW; ++g) oloff[g] = ((g0 + g) * 16 + fr) * ocs + fg * 4;
+  for (int g = 0; g < GPW; ++g) oloff[g] = ((g0 + g) * 16 + fr) * ocs + fg * (K::PAIR ? 8 : 4);
   const size_t HWs = (size_t)H * W;
   const ConvSeg& ss = op.seg[SC ? 1 : 0];
   const half_t* scsrc = (const half_t*)ss.src + ss.coff;
@@ -503,8 +529,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, RingCfg<MODE, C, NB, FL
                 f16x8_r wf;
                 if constexpr (K::WREG) wf = wr[(r * 3 + sc) * K::KS + ks][nt];
                 else wf = w[sc][nt];
-                acc[nt][g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf, x[sc * GPW + g],
-                                                                    c == 0 && sc == 0 ? bias4[nt] : acc[nt][g], 0, 0, 0);
+                if constexpr ((FL & kRingAblMma) != 0) {
+                  if (c == 0 && sc == 0) acc[nt][g] = bias4[nt] + (f32x4_r)__builtin_bit_cast(f32x4_r, x[sc * GPW + g]);
+                } else {
+                  acc[nt][g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf, x[sc * GPW + g],
+                                                                      c == 0 && sc == 0 ? bias4[nt] : acc[nt][g], 0, 0, 0);
+                }
               }
         };
         ld(0, bx[0], bw[0]);
@@ -664,6 +694,84 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, RingCfg<MODE, C, NB, FL
         // one pointer per pixel group (the sink for invalid outputs), channel tiles at immediates
         half_t* dg = ovalid[g] ? (half_t*)op.out + prow * ocs + op.out_coff + oloff[g]
                                : (half_t*)(g_ring_sink + tid * 16);
+        if constexpr (K::PAIR) {
+#pragma unroll
+        for (int p = 0; p < NT / 2; ++p) {
+          // fragments 2p, 2p + 1: channels 32p + 8fg .. + 7 of pixel fr (ring_ch)
+          float v[8];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            v[i] = acc[2 * p][g][i];
+            v[4 + i] = acc[2 * p + 1][g][i];
+          }
+          if constexpr (K::RELU && RES) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = fmaxf(v[i], 0.f);
+          }
+          if constexpr (RES) {
+            const int k = 4 * p + fg;  // logical 16-byte chunk of this lane's 8 channels
+            const f16x8_r rr = *(const f16x8_r*)(epi + (g * 16 + fr) * NB * 2 + ((k ^ ring_res_swz<NB / 8>(fr)) * 16));
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] += (float)rr[i];
+          }
+          f16x8_r o;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[i] = (half_t)v[i];
+          if constexpr (K::RELU && !RES) {
+            // relu after the RNE rounding (the same values: rounding is monotone and
+            // keeps the sign) as a signed 16-bit max per pair: every negative half,
+            // -0 included, becomes +0 -- 4 instructions per 8 channels instead of 16
+            // (inline asm: written as vector code, hipcc split the packed conversions
+            // into per-element ones + permutes to feed an element-wise max)
+            uint4 w = __builtin_bit_cast(uint4, o);
+            asm("v_pk_max_i16 %0, %1, 0" : "=v"(w.x) : "v"(w.x));
+            asm("v_pk_max_i16 %0, %1, 0" : "=v"(w.y) : "v"(w.y));
+            asm("v_pk_max_i16 %0, %1, 0" : "=v"(w.z) : "v"(w.z));
+            asm("v_pk_max_i16 %0, %1, 0" : "=v"(w.w) : "v"(w.w));
+            o = __builtin_bit_cast(f16x8_r, w);
+          }
+          if constexpr (K::OUT32) {
+            if (op.mask16 && ovalid[g]) {
+              const half_t* mk = (const half_t*)op.mask16 + prow * op.mask16_cs +
+                                 (size_t)((g0 + g) * 16 + fr) * op.mask16_cs + fg * 8 + p * 32;
+              const f16x8_r mv = *(const f16x8_r*)mk;
+#pragma unroll
+              for (int i = 0; i < 8; ++i) o[i] = (float)mv[i] > 0.f ? o[i] : (half_t)0.f;
+            }
+            f32x4_r o32a, o32b;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              o32a[i] = (float)o[i];
+              o32b[i] = (float)o[4 + i];
+            }
+            float* d32 = ovalid[g] ? op.out32 + prow * op.out32_cs + op.out32_coff +
+                                         (size_t)((g0 + g) * 16 + fr) * op.out32_cs + fg * 8
+                                   : g_ring_sink32 + tid * 64;
+            if (!op.skip32) {
+              *(f32x4_r*)(d32 + p * 32) = o32a;
+              *(f32x4_r*)(d32 + p * 32 + 4) = o32b;
+            }
+            if (op.out32_h16) {  // compact fp16 copy: o itself (no res32 on the ring)
+              half_t* d16 = ovalid[g] ? (half_t*)op.out32_h16 + prow * op.out32_h16_cs +
+                                            (size_t)((g0 + g) * 16 + fr) * op.out32_h16_cs + fg * 8
+                                      : (half_t*)(g_ring_sink + tid * 16);
+              *(uint4*)(d16 + p * 32) = __builtin_bit_cast(uint4, o);
+            }
+          } else {
+            *(uint4*)(dg + p * 32) = __builtin_bit_cast(uint4, o);
+          }
+          if constexpr (K::OUT2) {
+            f16x8_r q;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              q[i] = (half_t)fmaxf(__builtin_fmaf((float)o[i], p2s[2 * p][i], p2h[2 * p][i]), 0.f);
+              q[4 + i] = (half_t)fmaxf(__builtin_fmaf((float)o[4 + i], p2s[2 * p + 1][i], p2h[2 * p + 1][i]), 0.f);
+            }
+            half_t* d2 = ovalid[g] ? (half_t*)op.out2 + prow * ocs + oloff[g] : (half_t*)(g_ring_sink + tid * 16);
+            *(uint4*)(d2 + p * 32) = __builtin_bit_cast(uint4, q);
+          }
+        }
+        } else {
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
           float v[4];
@@ -683,11 +791,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, RingCfg<MODE, C, NB, FL
 #pragma unroll
           for (int i = 0; i < 4; ++i) o[i] = (half_t)v[i];
           if constexpr (K::RELU && !RES) {
-            // relu after the RNE rounding (the same values: rounding is monotone and
-            // keeps the sign) as a signed 16-bit max per pair: every negative half,
-            // -0 included, becomes +0 -- 2 instructions per 4 channels instead of 8
-            // (inline asm: written as vector code, hipcc split the packed conversions
-            // into per-element ones + permutes to feed an element-wise max)
+            // relu after the RNE rounding, as a signed 16-bit max per pair (see above)
             uint2 w = __builtin_bit_cast(uint2, o);
             asm("v_pk_max_i16 %0, %1, 0" : "=v"(w.x) : "v"(w.x));
             asm("v_pk_max_i16 %0, %1, 0" : "=v"(w.y) : "v"(w.y));
@@ -730,6 +834,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, RingCfg<MODE, C, NB, FL
             half_t* d2 = ovalid[g] ? (half_t*)op.out2 + prow * ocs + oloff[g] : (half_t*)(g_ring_sink + tid * 16);
             *(uint2*)(d2 + nt * 16) = __builtin_bit_cast(uint2, q);
           }
+        }
         }
       }
     }
@@ -1249,6 +1354,12 @@ static bool ring_seg_ok(const ConvSeg& s) {
 
 template <int MODE, int C, int NB, int FL>
 static int ring_relu(const ConvOp& op, hipStream_t st) {
+  // timing ablations of the plain 32/64-channel programs (UPR_RING_ABL = 1 no DMA, 2 no MFMA)
+  static const int abl = [] { const char* e = getenv("UPR_RING_ABL"); return e ? atoi(e) : 0; }();
+  if constexpr (MODE == kRingConv && (FL & ~(kRingWide | kRingOcc3)) == 0) {
+    if (abl == 1 && op.relu) return launch_ring_cfg<MODE, C, NB, FL | kRingRelu | kRingAblDma>(op, st);
+    if (abl == 2 && op.relu) return launch_ring_cfg<MODE, C, NB, FL | kRingRelu | kRingAblMma>(op, st);
+  }
   return op.relu ? launch_ring_cfg<MODE, C, NB, FL | kRingRelu>(op, st) : launch_ring_cfg<MODE, C, NB, FL>(op, st);
 }
 

@@ -987,7 +987,8 @@ static int launch_hwide(const ConvOp& op, hipStream_t st) {
 // TR_ = output rows per tile: 4 (the 8-row ring over several chunks), or 2
 // for one 64-channel chunk at W 256 (hwide4 only: its 4 region rows are the
 // whole "ring", DMA'd in the prologue)
-template <int BN, int W, int TR_ = 4>
+// RR_: ring rows when not the default (the pointwise form: 12 = three chunks' 4 rows)
+template <int BN, int W, int TR_ = 4, int RR_ = 0>
 struct Halo3Cfg {
   static constexpr int TR = TR_;             // output rows per tile
   static constexpr int BM = TR * W;          // 256 (W 64) / 512 (W 128, W 256 x 2 rows) pixels
@@ -996,7 +997,7 @@ struct Halo3Cfg {
   static constexpr int WM = BM / WAVES_M / 16, WN = BN / WAVES_N / 16;
   static constexpr int ROW = W * 128;        // one region row of one 64-channel chunk
   static constexpr int RP = W / 64;          // DMA pieces per wave per region row
-  static constexpr int RR = TR == 4 ? 8 : TR + 2;  // ring rows
+  static constexpr int RR = RR_ ? RR_ : TR == 4 ? 8 : TR + 2;  // ring rows
   static constexpr int RING = RR * ROW;
   static constexpr int B_BYTES = BN * WBK * 2;
   static constexpr int BJ = BN / 64;         // B DMA instructions per wave per step
@@ -1290,16 +1291,38 @@ __device__ __forceinline__ void hw4_res_load(const ConvOp& op, f16x8_w (&rv0)[WM
 // whose 4 region rows are the source rows 2(oy0 + r), every other pixel,
 // DMA'd into the ring slots the last chunk frees (the schedule of a next
 // chunk's rows 0-3) and read without a tap shift
-template <int BN, int W, int NCH, int ABL = 0, bool DS = false, bool DL = false, int TR = 4, int NSC = 0>
+// PW: pointwise (1x1 stride 1) over NCH chunks, one K step per chunk (the
+// ASPP fusion, K 1024, and conv1x1, K 256: models/model.py:231-251).  A
+// chunk's region is its 4 tile rows (no halo), read by one step only, so the
+// ring holds three chunks (12 rows, 96 KB) and two B stages fill the rest:
+// chunk S + 3's rows go out after barrier S into the rows chunk S freed (two
+// steps of lookahead for the HBM stream), B(S + 2) into B(S)'s stage (one
+// step for the L2-resident filter)
+// S2: 3x3 stride 2 pad 1 over a 2H x 2W source (enc2.conv1 / enc3.conv1,
+// models/model.py:100-178) in the dilated form's region order (tap row,
+// chunk, tap column): region k = (tap row ty, chunk c) is the TR source rows
+// 2 (oy0 + r) + ty - 1, each DMA'd de-interleaved into an even-column and an
+// odd-column plane of W pixels (a per-lane 2-pixel source stride), so the
+// three taps read unit-stride fragments: tx 1 the even plane at column j, tx 0
+// / 2 the odd plane at j - 1 / j (j - 1 < 0 through the void base).  Region k
+// fills ring half k & 1 (2 x TR x ROW: 64 KB at W 64 x 4 rows, W 128 x 2
+// rows); BN 128 leaves two 16 KB B stages.  Region k + 2 is issued after
+// region k's last tap (three steps of lookahead), B(S + 2) after barrier S.
+template <int BN, int W, int NCH, int ABL = 0, bool DS = false, bool DL = false, int TR = 4, int NSC = 0,
+          bool PW = false, bool S2 = false>
 __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
-  using HC = Halo3Cfg<BN, W, TR>;
+  using HC = Halo3Cfg<BN, W, TR, PW ? 12 : S2 ? 4 * TR : 0>;
   static_assert(TR == 4 || (NCH == 1 && !DL && DS), "2-row tiles: one chunk, direct store");
   static_assert(NSC == 0 || (NSC == 1 && !DL && TR == 4 && DS), "shortcut segment: 4-row tiles, direct store");
+  static_assert(!PW || (!DL && NSC == 0 && TR == 4 && DS && HC::NBS == 2 && NCH >= 3), "pointwise form");
+  static_assert(!S2 || (!DL && !PW && NSC == 0 && DS && HC::NBS == 2), "stride-2 form");
   constexpr int WM = HC::WM, WN = HC::WN, BM = HC::BM, NBS = HC::NBS;
-  constexpr int TOTAL = NCH * 9 + NSC;
-  // (chunk, tap) of K step S; the shortcut step is chunk NCH with the centre column (tap 1: row 0, column 1)
-  constexpr auto step_c = [](int S) -> int { return S < NCH * 9 ? S / 9 : NCH + (S - NCH * 9); };
-  constexpr auto step_t = [](int S) -> int { return S < NCH * 9 ? S % 9 : 1; };
+  constexpr int KT = PW ? 1 : 9;  // K steps (taps) per chunk
+  constexpr int TOTAL = NCH * KT + NSC;
+  // (chunk, tap) of K step S; the shortcut step is chunk NCH with the centre column (tap 1: row 0, column 1);
+  // a pointwise step reads its chunk's rows 0-3 at the centre column (tap 4 with the ring rows below)
+  constexpr auto step_c = [](int S) -> int { return S < NCH * KT ? S / KT : NCH + (S - NCH * KT); };
+  constexpr auto step_t = [](int S) -> int { return PW ? 4 : S < NCH * 9 ? S % 9 : 1; };
   constexpr int CW = W / HC::WAVES_M;  // columns per wave
   constexpr int FPR = CW / 16;         // fragments per tile row per wave
   static_assert(CW % 16 == 0 && WM == HC::TR * FPR, "column blocks of whole 16-pixel fragments");
@@ -1342,6 +1365,14 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
       (const unsigned char*)((const half_t*)sc.src + sc.coff +
                              ((size_t)img * sc.Hin * sc.Win + (size_t)wave * 8 * 2) * sc.cs);
   auto region_row = [&](int cc, int r) {  // cc, r compile-time at every call site
+    if constexpr (PW) {  // tile row r of chunk cc -> ring row (4 cc + r) % 12 (always inside the image)
+      unsigned char* dst = smem + ((4 * cc + r) % HC::RR) * HC::ROW + wave * 1024;
+#pragma unroll
+      for (int k = 0; k < HC::RP; ++k)
+        glds16_s(abase + (size_t)(oy0 + r) * row_bytes + (size_t)k * 64 * cs * 2 + cc * WBK * 2, voff_a,
+                 dst + k * 8192);
+      return;
+    }
     if (NSC && cc >= NCH) {
       unsigned char* dst = smem + ((6 * cc + r) & 7) * HC::ROW + wave * 1024;
       const size_t srow = (size_t)2 * (oy0 + r) * sc.Win * sc.cs * 2;
@@ -1399,6 +1430,32 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
     }
   };
 
+  // S2 region k (regions past the last are not issued; the waits count them)
+  const unsigned char* s2base =
+      (const unsigned char*)((const half_t*)sg.src + sg.coff + ((size_t)img * sg.Hin * sg.Win + (size_t)wave * 16) * cs);
+  const size_t s2row_bytes = (size_t)sg.Win * cs * 2;
+  const unsigned voff_s2 = (unsigned)(((lane >> 3) * 2 * cs + (((lane & 7) ^ halo_swz(rpx)) * 8)) * 2);
+  auto region_s2 = [&](int k) {  // k compile-time at every call site
+    const int ty = k / NCH, cc = k % NCH;
+#pragma unroll
+    for (int r = 0; r < TR; ++r) {
+      const int iy = 2 * (oy0 + r) + ty - 1;
+      const bool in = (unsigned)iy < (unsigned)sg.Hin;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        unsigned char* dst = smem + ((k & 1) * 2 * TR + q * TR + r) * HC::ROW + wave * 1024;
+#pragma unroll
+        for (int pc = 0; pc < HC::RP; ++pc) {
+          const unsigned char* ub = in ? s2base + (size_t)iy * s2row_bytes + (size_t)pc * 128 * cs * 2 + cc * WBK * 2 +
+                                             q * cs * 2
+                                       : (const unsigned char*)g_halo_zero;
+          glds16_s(ub, voff_s2, dst + pc * 8192);
+        }
+      }
+    }
+  };
+  constexpr int S2DMA = 2 * TR * HC::RP;  // DMAs per wave per S2 region
+
   const int q8 = lane >> 3;
   const int qc = lane & 7;
   const int sw_lane = lane >> 4;
@@ -1424,7 +1481,9 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
   // step's rows into a stage nobody reads again (uniform DMA count)
   auto issue_b = [&](int stg, int c, int t) {  // DL: c = region, t = tap column
     unsigned char* Bs = smem + HC::RING + stg * HC::B_BYTES;
-    const int kb = DL ? ((c / NCH) * 3 + t) * Cin + (c % NCH) * WBK : c < NCH ? t * Cin + c * WBK : 9 * Cin + (c - NCH) * WBK;
+    const int kb = PW   ? c * WBK
+                   : (DL || S2) ? ((c / NCH) * 3 + t) * Cin + (c % NCH) * WBK
+                   : c < NCH ? t * Cin + c * WBK : 9 * Cin + (c - NCH) * WBK;
 #pragma unroll
     for (int j = 0; j < HC::BJ; ++j) {
       if constexpr (DS)
@@ -1473,6 +1532,20 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
                                                   : kLdsVoid + (p & 15) * 128 + ((fg ^ halo_swz(p & 15)) * 16);
       }
   }
+  // S2: per (tap column, fragment) lane offsets into the region's planes
+  int aofs_s[S2 ? 3 : 1][S2 ? FPR : 1];
+  if constexpr (S2) {
+#pragma unroll
+    for (int tx = 0; tx < 3; ++tx)
+#pragma unroll
+      for (int f = 0; f < FPR; ++f) {
+        const int j = CW * wm + f * 16 + fr;
+        const int p = tx == 0 ? j - 1 : j;
+        const int plane = tx == 1 ? 0 : 1;
+        aofs_s[tx][f] = p >= 0 ? plane * TR * HC::ROW + p * 128 + ((fg ^ halo_swz(p)) * 16)
+                               : kLdsVoid + (p & 15) * 128 + ((fg ^ halo_swz(p & 15)) * 16);
+      }
+  }
   bofs = HC::RING + (wn * WN * 16 + fr) * 128 + ((fg ^ rsw) * 16);
 
   // fragments of step S, half KK: B (all WN) and A row fragment a
@@ -1490,9 +1563,15 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
       constexpr int h = (S / 3) & 1, dtx = S % 3;
       const int ao = KK ? (aofs_d[dtx][a % FPR] ^ 64) : aofs_d[dtx][a % FPR];
       return *(const f16x8_w*)(smem + ao + (h * 4 + a / FPR) * HC::ROW);
+    } else if constexpr (S2) {
+      constexpr int h = (S / 3) & 1, dtx = S % 3;
+      constexpr int off = (h * 2 * TR + a / FPR) * HC::ROW;
+      int ao = KK ? (aofs_s[dtx][a % FPR] ^ 64) : aofs_s[dtx][a % FPR];
+      if constexpr (off >= 65536) asm volatile("v_add_u32_e32 %0, %1, %0" : "+v"(ao) : "n"(off & ~0xffff));
+      return *(const f16x8_w*)(smem + ao + (off & 0xffff));
     } else {
       constexpr bool edge = (tx == 0 && a % FPR == 0) || (tx == 2 && a % FPR == FPR - 1);
-      constexpr int rr = (6 * c + ty + a / FPR) & 7;
+      constexpr int rr = PW ? (4 * c + a / FPR) % HC::RR : (6 * c + ty + a / FPR) & 7;
       constexpr int off = rr * HC::ROW + (a % FPR) * 16 * 128;
       int ao;
       if constexpr (edge && tx == 0) ao = KK ? (aofs_e[0] ^ 64) : aofs_e[0];
@@ -1532,28 +1611,49 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
     });
   };
   static_assert(!DL || (DS && NBS == 3), "dilated form: direct-store epilogue, three B stages");
-  if constexpr (DL) {
+  if constexpr (S2) {
+    region_s2(0);
+    issue_b(0, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    issue_b(1, 0, 1);
+    if constexpr (3 * NCH > 1) region_s2(1);
+  } else if constexpr (PW) {
+    // chunk 0 + B(0) landed, chunk 1 may fly; then B(1) and chunk 2
+#pragma unroll
+    for (int r = 0; r < 4; ++r) region_row(0, r);
+    issue_b(0, 0, 4);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) region_row(1, r);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * HC::RP) : "memory");
+    __builtin_amdgcn_s_barrier();
+    issue_b(1, 1, 4);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) region_row(2, r);
+  } else if constexpr (DL) {
     region_dl(0);
-  } else {
+  } else if constexpr (!S2) {
     region_row(0, 0);
     region_row(0, 1);
     region_row(0, 2);
     region_row(0, 3);
   }
-  issue_b(0, 0, 0);
-  if constexpr (NBS == 3) {
-    issue_b(1, 0, 1);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(HC::BJ) : "memory");  // rows 0-3 and B(0) landed
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __builtin_amdgcn_s_barrier();
-  if constexpr (DL) {
-    issue_b(2, 0, 2);  // B(2)
-    region_dl(1);
-  } else {
-    issue_b(NBS - 1, (NBS - 1) / 9, (NBS - 1) % 9);  // B(NBS - 1)
-    issue_rows(0, 0);
+  if constexpr (!PW && !S2) {
+    issue_b(0, 0, 0);
+    if constexpr (NBS == 3) {
+      issue_b(1, 0, 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(HC::BJ) : "memory");  // rows 0-3 and B(0) landed
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if constexpr (DL) {
+      issue_b(2, 0, 2);  // B(2)
+      region_dl(1);
+    } else {
+      issue_b(NBS - 1, (NBS - 1) / 9, (NBS - 1) % 9);  // B(NBS - 1)
+      issue_rows(0, 0);
+    }
   }
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
@@ -1568,8 +1668,8 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
           constexpr int n = S + 1, nc = step_c(n), nt = step_t(n);
           // B DMA of step S + NBS (clamped past the end) into the stage step S read
           constexpr int bstep = S + NBS < TOTAL ? S + NBS : TOTAL - 1;
-          constexpr int bc = DL ? (S + NBS < TOTAL ? bstep / 3 : NREG - 1) : step_c(bstep);
-          constexpr int bt = DL ? (S + NBS < TOTAL ? bstep % 3 : 2) : step_t(bstep);
+          constexpr int bc = (DL || S2) ? (S + NBS < TOTAL ? bstep / 3 : NREG - 1) : step_c(bstep);
+          constexpr int bt = (DL || S2) ? (S + NBS < TOTAL ? bstep % 3 : 2) : step_t(bstep);
           mm_roll(S_, I1{}, b0, true);
           // RAW: B(S + 1) and the region rows step S + 1 reads have landed: in
           // flight may stay the previous iteration's region rows (issued two
@@ -1579,7 +1679,17 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
           // DL: at S = 3k + 2 region k + 1 (issued after B(S + 1) at S - 3) and
           // B(S + 1) must have landed; B(S + 2) may fly.  Otherwise B(S + 1)
           // must have landed; B(S + 2) and the region issued at 3k - 1 may fly.
-          if constexpr (DL) {
+          // PW: B(S + 1) (issued at barrier S - 1, before chunk S + 2) and chunk S +
+          // 1 (barrier S - 2) must have landed; chunk S + 2 may fly when it exists
+          if constexpr (PW) {
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(S + 2 < NCH ? 4 * HC::RP : 0) : "memory");
+          } else if constexpr (S2) {
+            // B(S + 1) (issued at barrier S - 1) must have landed, and so must the
+            // region step S + 1 reads (issued 3+ steps earlier); in flight may stay
+            // region S / 3 + 1 when it was issued after B(S + 1) (S % 3 == 0)
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(S % 3 == 0 && S / 3 + 1 < NREG ? S2DMA : 0)
+                         : "memory");
+          } else if constexpr (DL) {
             if constexpr (S % 3 == 2)
               asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(HC::BJ) : "memory");
             else
@@ -1591,7 +1701,14 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
           __builtin_amdgcn_s_barrier();
           if constexpr (!(ABL & 1)) {
             issue_b(S % NBS, bc, bt);
-            if constexpr (DL) {
+            if constexpr (S2) {
+              if constexpr (S % 3 == 2 && S / 3 + 2 < NREG) region_s2(S / 3 + 2);
+            } else if constexpr (PW) {
+              if constexpr (S + 3 < NCH) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) region_row(S + 3, r);
+              }
+            } else if constexpr (DL) {
               if constexpr (S % 3 == 2) region_dl(S / 3 + 2);
             } else {
               issue_rows(nc, nt);
@@ -1635,18 +1752,20 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
   }
 }
 
-template <int BN, int W, int NCH, int ABL = 0, bool DS = false, bool DL = false, int TR = 4, int NSC = 0>
+template <int BN, int W, int NCH, int ABL = 0, bool DS = false, bool DL = false, int TR = 4, int NSC = 0,
+          bool PW = false, bool S2 = false>
 static int launch_hwide4_k(const ConvOp& op, hipStream_t st) {
-  using HC = Halo3Cfg<BN, W, TR>;
+  using HC = Halo3Cfg<BN, W, TR, PW ? 12 : S2 ? 4 * TR : 0>;
   static bool attr_set = false;
   if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute((const void*)conv_hwide4_kernel<BN, W, NCH, ABL, DS, DL, TR, NSC>,
+    const hipError_t e = hipFuncSetAttribute((const void*)conv_hwide4_kernel<BN, W, NCH, ABL, DS, DL, TR, NSC, PW, S2>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, HC::LDS);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
   const int grid = (op.B * op.Ho * W / HC::BM) * (op.N / BN);
-  hipLaunchKernelGGL((conv_hwide4_kernel<BN, W, NCH, ABL, DS, DL, TR, NSC>), dim3(grid), dim3(512), HC::LDS, st, op);
+  hipLaunchKernelGGL((conv_hwide4_kernel<BN, W, NCH, ABL, DS, DL, TR, NSC, PW, S2>), dim3(grid), dim3(512), HC::LDS,
+                     st, op);
   return (int)hipGetLastError();
 }
 
@@ -1716,10 +1835,50 @@ static bool hw4_sc_ok(const ConvOp& op) {
   return hw4_ds_ok(op);
 }
 
+// 1x1 stride-1 GEMMs over whole 64-pixel rows, K 256 / 1024 / 1280 -> N 256k (the ASPP
+// conv1x1 and fusion, models/model.py:231-251): the pointwise hwide4 form
+static int hw4_pw_route(const ConvOp& op, hipStream_t st) {
+  const ConvSeg& s = op.seg[0];
+  if (s.kh != 1 || s.kw != 1 || s.stride != 1 || s.pad != 0 || s.dil != 1 || s.pre != kPreNone || s.kbase != 0)
+    return kErrUnsupported;
+  if (s.Hin != op.Ho || s.Win != op.Wo || op.Wo != 64 || op.N % 256 || (op.Ho * op.Wo) % 256 || op.Kpad != s.C)
+    return kErrUnsupported;
+  if (s.cs % 8 || s.coff % 8 || (uintptr_t)s.src % 16 || !hw4_ds_ok(op)) return kErrUnsupported;
+  static const bool off = [] { const char* e = getenv("UPR_HW4_PW"); return e && atoi(e) == 0; }();
+  if (off) return kErrUnsupported;  // A/B against the gathered kernel (tools/convbench.py)
+  if (s.C == 256) return launch_hwide4_k<256, 64, 4, 0, true, false, 4, 0, true>(op, st);
+  if (s.C == 1024) return launch_hwide4_k<256, 64, 16, 0, true, false, 4, 0, true>(op, st);
+  if (s.C == 1280) return launch_hwide4_k<256, 64, 20, 0, true, false, 4, 0, true>(op, st);  // (+ global branch)
+  return kErrUnsupported;
+}
+
+// 3x3 stride-2 convs over 64-channel chunks, N 128k: W 64 x 4-row tiles
+// (enc3.conv1: 128 -> 256 at 128^2 -> 64^2) and W 128 x 2-row tiles (enc2.conv1:
+// 64 -> 128 at 256^2 -> 128^2) on the stride-2 hwide4 form
+static int hw4_s2_route(const ConvOp& op, hipStream_t st) {
+  const ConvSeg& s = op.seg[0];
+  if (s.kh != 3 || s.kw != 3 || s.stride != 2 || s.pad != 1 || s.dil != 1 || s.pre != kPreNone || s.kbase != 0)
+    return kErrUnsupported;
+  if (s.Hin != 2 * op.Ho || s.Win != 2 * op.Wo || op.N % 128 || op.Kpad != 9 * s.C || !hw4_ds_ok(op))
+    return kErrUnsupported;
+  static const bool off = [] { const char* e = getenv("UPR_HW4_S2"); return e && atoi(e) == 0; }();
+  if (off) return kErrUnsupported;  // A/B against the gathered kernel (tools/convbench.py)
+  if (op.Wo == 64 && op.Ho % 4 == 0) {
+    if (s.C == 64) return launch_hwide4_k<128, 64, 1, 0, true, false, 4, 0, false, true>(op, st);
+    if (s.C == 128) return launch_hwide4_k<128, 64, 2, 0, true, false, 4, 0, false, true>(op, st);
+    if (s.C == 256) return launch_hwide4_k<128, 64, 4, 0, true, false, 4, 0, false, true>(op, st);
+  }
+  if (op.Wo == 128 && op.Ho % 2 == 0 && s.C == 64)
+    return launch_hwide4_k<128, 128, 1, 0, true, false, 2, 0, false, true>(op, st);
+  return kErrUnsupported;
+}
+
 static int halo_route(const ConvOp& op, hipStream_t st) {
   if (hw4_sc_ok(op)) return launch_hwide4_k<128, 128, 2, 0, true, false, 4, 1>(op, st);
   if (op.nseg != 1 || op.store != kStoreNHWC) return kErrUnsupported;
   const ConvSeg& s = op.seg[0];
+  if (s.kh == 1 && s.kw == 1) return hw4_pw_route(op, st);
+  if (s.stride == 2) return hw4_s2_route(op, st);
   // dilated 3x3 over 256 channels at W 64 (the ASPP branches, d = 6 / 12 / 18):
   // the region form of hwide4 (gathered kernel: 0.168 / 0.153 / 0.143 ms vs
   // 0.158 / 0.145 / 0.136, profiles/r3_hw4_dil_ab.txt)

@@ -585,6 +585,9 @@ __global__ __launch_bounds__(256) void ms_sums_kernel(const T* __restrict__ x, u
 constexpr int M3_TH = 32, M3_TW = 64, M3_HALO = 4;
 constexpr int M3_RH = M3_TH + 2 * M3_HALO, M3_RW = M3_TW + 2 * M3_HALO;
 constexpr int M3_H1 = M3_TH / 2 + 2, M3_W1 = M3_TW / 2 + 2, M3_H2 = M3_TH / 4 + 2, M3_W2 = M3_TW / 4 + 2;
+// half / quarter sample planes: interior columns from 4 (16-byte aligned
+// quads), the 1-sample halo at columns 3 and 4 + width
+constexpr int M3_P1 = M3_TW / 2 + 8, M3_P2 = M3_TW / 4 + 8;
 
 __device__ __forceinline__ float blend_half(float v00, float v01, float v10, float v11) {
   const float ly = 0.5f, lx = 0.5f;  // sample_s with fy - y0 = fx - x0 = 0.5
@@ -617,6 +620,42 @@ __device__ __forceinline__ float ms_feat(const float (&P)[3][PH][PW], int R, int
   return fsum;
 }
 
+// the features of the 4 pixels (R, C .. C + 3) (C 16-byte aligned), summed in
+// fp64 as ms_feat's per-pixel floats: interior quads read 16-byte rows (center,
+// above, below) and the two side neighbours -- 5 LDS reads per channel for 4
+// pixels instead of 5 per pixel; quads at an image border take ms_feat
+template <int PH, int PW>
+__device__ __forceinline__ double ms_feat4(const float (&P)[3][PH][PW], int R, int C, int y, int x, int hs, int ws) {
+  if (x < 1 || x + 4 > ws - 1 || y < 1 || y > hs - 2) {
+    double a = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (x + k < ws) a += (double)ms_feat(P, R, C + k, y, x + k, hs, ws);
+    return a;
+  }
+  float fs[4] = {0.f, 0.f, 0.f, 0.f}, c3[3][4];
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) {
+    const float4 ce = *(const float4*)&P[ch][R][C];
+    const float4 up = *(const float4*)&P[ch][R - 1][C];
+    const float4 dn = *(const float4*)&P[ch][R + 1][C];
+    const float l = P[ch][R][C - 1], r = P[ch][R][C + 4];
+    const float v[6] = {l, ce.x, ce.y, ce.z, ce.w, r};
+    const float u[4] = {up.x, up.y, up.z, up.w}, d[4] = {dn.x, dn.y, dn.z, dn.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float gx = (v[k + 2] - v[k]) / 2.f;
+      const float gy = (d[k] - u[k]) / 2.f;
+      fs[k] += v[k + 1] + sqrtf(gx * gx + gy * gy);
+      c3[ch][k] = v[k + 1];
+    }
+  }
+  double a = 0.0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) a += (double)(fs[k] + (0.299f * c3[0][k] + 0.587f * c3[1][k] + 0.114f * c3[2][k]));
+  return a;
+}
+
 __device__ __forceinline__ double ms_factor(const double* sums, int b, double n0, double n1, double n2);
 
 template <typename T>
@@ -625,13 +664,19 @@ __global__ __launch_bounds__(256) void ms_sums3_kernel(const T* __restrict__ x, 
                                                        double* __restrict__ factor, int H, int W, int tiles_x,
                                                        unsigned nblk_img, double n0, double n1, double n2) {
   __shared__ float full[3][M3_RH][M3_RW];
-  __shared__ float s1[3][M3_H1][M3_W1];
-  __shared__ float s2[3][M3_H2][M3_W2];
+  __shared__ __attribute__((aligned(16))) float s1[3][M3_H1][M3_P1];
+  __shared__ __attribute__((aligned(16))) float s2[3][M3_H2][M3_P2];
   __shared__ double red[4][3];
   __shared__ int is_last;
   const int t = threadIdx.x;
-  const int b = blockIdx.y;
-  const int ty0 = (blockIdx.x / tiles_x) * M3_TH, tx0 = (blockIdx.x % tiles_x) * M3_TW;
+  // tiles in XCD-contiguous order (blocks i, i + 8, ... share an XCD: they take
+  // neighbouring tiles, whose 4-pixel halo lines then come from that XCD's L2;
+  // dealt round-robin, every tile's halos were fetched from HBM twice)
+  const int nb = gridDim.x * gridDim.y, bid = blockIdx.y * gridDim.x + blockIdx.x;
+  const int q8 = nb >> 3, r8 = nb & 7, xcd = bid & 7, k8 = bid >> 3;
+  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + k8;
+  const int b = tile / gridDim.x, tin = tile - b * gridDim.x;
+  const int ty0 = (tin / tiles_x) * M3_TH, tx0 = (tin % tiles_x) * M3_TW;
   const size_t HW = (size_t)H * W;
   const T* img = x + (size_t)b * 3 * HW;
   // full-resolution region: rows ty0 - 4 .., columns tx0 - 4 .. in 4-pixel quads
@@ -657,7 +702,8 @@ __global__ __launch_bounds__(256) void ms_sums3_kernel(const T* __restrict__ x, 
   __syncthreads();
   const int h1 = H / 2, w1 = W / 2, h2 = H / 4, w2 = W / 4;
   // half / quarter samples with their 1-sample halos (LDS rows of sample r:
-  // 2r + 2, 2r + 3 / 4r + 1, 4r + 2 of the region, by the halo of 4)
+  // 2r + 2, 2r + 3 / 4r + 1, 4r + 2 of the region, by the halo of 4); sample
+  // column c at plane column c + 3
   for (int i = t; i < M3_H1 * M3_W1 + M3_H2 * M3_W2; i += 256) {
     if (i < M3_H1 * M3_W1) {
       const int r = i / M3_W1, c = i - r * M3_W1;
@@ -665,8 +711,8 @@ __global__ __launch_bounds__(256) void ms_sums3_kernel(const T* __restrict__ x, 
       if ((unsigned)ys < (unsigned)h1 && (unsigned)xs < (unsigned)w1) {
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch)
-          s1[ch][r][c] = blend_half(full[ch][2 * r + 2][2 * c + 2], full[ch][2 * r + 2][2 * c + 3],
-                                    full[ch][2 * r + 3][2 * c + 2], full[ch][2 * r + 3][2 * c + 3]);
+          s1[ch][r][c + 3] = blend_half(full[ch][2 * r + 2][2 * c + 2], full[ch][2 * r + 2][2 * c + 3],
+                                        full[ch][2 * r + 3][2 * c + 2], full[ch][2 * r + 3][2 * c + 3]);
       }
     } else {
       const int j = i - M3_H1 * M3_W1;
@@ -675,32 +721,28 @@ __global__ __launch_bounds__(256) void ms_sums3_kernel(const T* __restrict__ x, 
       if ((unsigned)ys < (unsigned)h2 && (unsigned)xs < (unsigned)w2) {
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch)
-          s2[ch][r][c] = blend_half(full[ch][4 * r + 1][4 * c + 1], full[ch][4 * r + 1][4 * c + 2],
-                                    full[ch][4 * r + 2][4 * c + 1], full[ch][4 * r + 2][4 * c + 2]);
+          s2[ch][r][c + 3] = blend_half(full[ch][4 * r + 1][4 * c + 1], full[ch][4 * r + 1][4 * c + 2],
+                                        full[ch][4 * r + 2][4 * c + 1], full[ch][4 * r + 2][4 * c + 2]);
       }
     }
   }
   __syncthreads();
+  // quads: 512 of the full tile (2 per thread), 128 half (threads 0-127), 32 quarter (128-159)
   double a0 = 0.0, a1 = 0.0, a2 = 0.0;
-  {
-    const int c = t & 63;
-#pragma unroll
-    for (int k = 0; k < M3_TH / 4; ++k) {
-      const int r = (t >> 6) + 4 * k;
-      const int y = ty0 + r, xx = tx0 + c;
-      if (y < H && xx < W) a0 += (double)ms_feat(full, r + M3_HALO, c + M3_HALO, y, xx, H, W);
-    }
-  }
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
-    const int i = t + 256 * k, r = i >> 5, c = i & 31;
-    const int y = ty0 / 2 + r, xx = tx0 / 2 + c;
-    if (y < h1 && xx < w1) a1 += (double)ms_feat(s1, r + 1, c + 1, y, xx, h1, w1);
+    const int i = t + 256 * k, r = i >> 4, q = i & 15;
+    const int y = ty0 + r, xx = tx0 + 4 * q;
+    if (y < H && xx < W) a0 += ms_feat4(full, r + M3_HALO, 4 * q + M3_HALO, y, xx, H, W);
   }
   if (t < 128) {
-    const int r = t >> 4, c = t & 15;
-    const int y = ty0 / 4 + r, xx = tx0 / 4 + c;
-    if (y < h2 && xx < w2) a2 += (double)ms_feat(s2, r + 1, c + 1, y, xx, h2, w2);
+    const int r = t >> 3, q = t & 7;
+    const int y = ty0 / 2 + r, xx = tx0 / 2 + 4 * q;
+    if (y < h1 && xx < w1) a1 += ms_feat4(s1, r + 1, 4 * q + 4, y, xx, h1, w1);
+  } else if (t < 160) {
+    const int r = (t - 128) >> 2, q = (t - 128) & 3;
+    const int y = ty0 / 4 + r, xx = tx0 / 4 + 4 * q;
+    if (y < h2 && xx < w2) a2 += ms_feat4(s2, r + 1, 4 * q + 4, y, xx, h2, w2);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {

@@ -89,6 +89,16 @@ CONV_CASES = [
     (2, 64, 64, 256, 256, 3, 1, 6, 6, True, False),
     (1, 64, 64, 256, 256, 3, 1, 18, 18, False, True),
     (1, 32, 64, 256, 512, 3, 1, 12, 12, True, False),
+    # pointwise hwide4 (1x1 over whole 64-pixel rows: ASPP conv1x1 K 256, fusion K 1024 / 1280)
+    (2, 64, 64, 1024, 256, 1, 1, 0, 1, True, False),
+    (1, 16, 64, 256, 512, 1, 1, 0, 1, False, True),
+    (3, 12, 64, 1280, 256, 1, 1, 0, 1, False, False),
+    # stride-2 hwide4 (de-interleaved region planes, BN 128): W 64 x 4-row tiles over 1 / 2 / 4
+    # chunks (enc3.conv1 class), W 128 x 2-row tiles over one chunk (enc2.conv1 class)
+    (2, 128, 128, 128, 256, 3, 2, 1, 1, True, False),
+    (1, 16, 128, 256, 128, 3, 2, 1, 1, True, False),
+    (2, 8, 128, 64, 256, 3, 2, 1, 1, False, False),
+    (1, 64, 256, 64, 128, 3, 2, 1, 1, False, True),
     # 64 -> 64 at W 256 (dec2 shape class: the row ring)
     (1, 8, 256, 64, 64, 3, 1, 1, 1, True, False),
     (2, 6, 256, 64, 64, 3, 1, 1, 1, False, True),

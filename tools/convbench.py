@@ -35,6 +35,8 @@ SHAPES = {
     "aspp12": (32, 64, 64, 256, 256, 3, 1, 12, 12, False),
     "aspp18": (32, 64, 64, 256, 256, 3, 1, 18, 18, False),
     "fuse": (32, 64, 64, 1280, 256, 1, 1, 0, 1, False),
+    "fuse1k": (32, 64, 64, 1024, 256, 1, 1, 0, 1, False),  # ASPP fusion as executed (global branch = bias)
+    "a1x1": (32, 64, 64, 256, 256, 1, 1, 0, 1, False),     # ASPP conv1x1
     "enc3s2": (32, 128, 128, 128, 256, 3, 2, 1, 1, False),
     "enc2s2": (32, 256, 256, 64, 128, 3, 2, 1, 1, False),
     "enc1c2": (32, 256, 256, 64, 64, 3, 1, 1, 1, True),   # enc1.conv2 (without the shortcut segment)
