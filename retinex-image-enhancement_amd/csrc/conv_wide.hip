@@ -1364,12 +1364,18 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
   const unsigned char* scbase =
       (const unsigned char*)((const half_t*)sc.src + sc.coff +
                              ((size_t)img * sc.Hin * sc.Win + (size_t)wave * 8 * 2) * sc.cs);
+  // PW: the K chunk of step cc is (cc + rot) % NCH (op.krot): tiles in flight
+  // together start at different chunks, so their row DMAs (a pixel's 2 KB of
+  // 1024 channels read 128 B per step) do not all land on the same HBM
+  // channels at once
+  const int rot = PW && op.krot ? __builtin_amdgcn_readfirstlane(mtile % NCH) : 0;
+  auto kchunk = [&](int cc) { const int k = cc + rot; return k >= NCH ? k - NCH : k; };
   auto region_row = [&](int cc, int r) {  // cc, r compile-time at every call site
     if constexpr (PW) {  // tile row r of chunk cc -> ring row (4 cc + r) % 12 (always inside the image)
       unsigned char* dst = smem + ((4 * cc + r) % HC::RR) * HC::ROW + wave * 1024;
 #pragma unroll
       for (int k = 0; k < HC::RP; ++k)
-        glds16_s(abase + (size_t)(oy0 + r) * row_bytes + (size_t)k * 64 * cs * 2 + cc * WBK * 2, voff_a,
+        glds16_s(abase + (size_t)(oy0 + r) * row_bytes + (size_t)k * 64 * cs * 2 + kchunk(cc) * WBK * 2, voff_a,
                  dst + k * 8192);
       return;
     }
@@ -1481,7 +1487,7 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
   // step's rows into a stage nobody reads again (uniform DMA count)
   auto issue_b = [&](int stg, int c, int t) {  // DL: c = region, t = tap column
     unsigned char* Bs = smem + HC::RING + stg * HC::B_BYTES;
-    const int kb = PW   ? c * WBK
+    const int kb = PW   ? kchunk(c) * WBK
                    : (DL || S2) ? ((c / NCH) * 3 + t) * Cin + (c % NCH) * WBK
                    : c < NCH ? t * Cin + c * WBK : 9 * Cin + (c - NCH) * WBK;
 #pragma unroll
@@ -1844,11 +1850,14 @@ static int hw4_pw_route(const ConvOp& op, hipStream_t st) {
   if (s.Hin != op.Ho || s.Win != op.Wo || op.Wo != 64 || op.N % 256 || (op.Ho * op.Wo) % 256 || op.Kpad != s.C)
     return kErrUnsupported;
   if (s.cs % 8 || s.coff % 8 || (uintptr_t)s.src % 16 || !hw4_ds_ok(op)) return kErrUnsupported;
-  static const bool off = [] { const char* e = getenv("UPR_HW4_PW"); return e && atoi(e) == 0; }();
-  if (off) return kErrUnsupported;  // A/B against the gathered kernel (tools/convbench.py)
-  if (s.C == 256) return launch_hwide4_k<256, 64, 4, 0, true, false, 4, 0, true>(op, st);
-  if (s.C == 1024) return launch_hwide4_k<256, 64, 16, 0, true, false, 4, 0, true>(op, st);
-  if (s.C == 1280) return launch_hwide4_k<256, 64, 20, 0, true, false, 4, 0, true>(op, st);  // (+ global branch)
+  // UPR_HW4_PW: 0 = the gathered kernel instead, 2 = no chunk rotation (A/B, tools/convbench.py)
+  static const int mode = [] { const char* e = getenv("UPR_HW4_PW"); return e ? atoi(e) : 1; }();
+  if (mode == 0) return kErrUnsupported;
+  ConvOp o = op;
+  o.krot = mode != 2;
+  if (s.C == 256) return launch_hwide4_k<256, 64, 4, 0, true, false, 4, 0, true>(o, st);
+  if (s.C == 1024) return launch_hwide4_k<256, 64, 16, 0, true, false, 4, 0, true>(o, st);
+  if (s.C == 1280) return launch_hwide4_k<256, 64, 20, 0, true, false, 4, 0, true>(o, st);  // (+ global branch)
   return kErrUnsupported;
 }
 

@@ -112,6 +112,9 @@ struct ConvOp {
   // input pixel (b, i, j) lands at output pixel (b, 2i, 2j) of a 2H x 2W map,
   // the others are not written (the 1x1 stride-2 conv's input gradient)
   int out_s2;
+  // hwide4 pointwise form (set by its dispatcher, 0 elsewhere): each tile walks
+  // its K chunks starting at chunk mtile % NCH instead of 0
+  int krot;
 };
 
 // fp16 convs with an fp32 output (ConvOp::out32): the wide-tile and row-ring

@@ -84,7 +84,11 @@ CONV_CASES = [
     (1, 64, 64, 256, 512, 3, 1, 1, 1, False, True),
     (1, 32, 64, 128, 128, 3, 1, 1, 1, False, True),
     (2, 16, 128, 128, 128, 3, 1, 1, 1, True, False),
+    # runtime-cursor hwide3 (the fallback for W 64 / 128 shapes hwide4 has no program for:
+    # 1 or 3 chunks at W 64 x N 256, 3 chunks at W 128)
     (1, 8, 64, 64, 256, 3, 1, 1, 1, False, False),
+    (1, 8, 128, 192, 128, 3, 1, 1, 1, True, False),
+    (2, 4, 64, 192, 256, 3, 1, 1, 1, False, True),
     # dilated region form of hwide4 (ASPP branches: 3x3, dilation = padding, 256 -> 256 at W 64)
     (2, 64, 64, 256, 256, 3, 1, 6, 6, True, False),
     (1, 64, 64, 256, 256, 3, 1, 18, 18, False, True),

@@ -53,13 +53,17 @@ def main():
     ap.add_argument("--dtype", choices=["fp32", "fp16"], default="fp16")
     ap.add_argument("--shapes", default=",".join(SHAPES))
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--bufs", type=int, default=1,
+                    help="cycle over this many input copies (> 1: inputs larger than the 256 MB MALL "
+                         "come from HBM, as inside the model)")
     args = ap.parse_args()
     dt = torch.float16 if args.dtype == "fp16" else torch.float32
     dev = torch.device("cuda", 0)
     for name in args.shapes.split(","):
         B, H, W, Ci, Co, k, s, p, d, res = SHAPES[name]
         g = torch.Generator(device=dev).manual_seed(0)
-        x = torch.randn(B, H, W, Ci, device=dev, generator=g).to(dt)
+        xs = [torch.randn(B, H, W, Ci, device=dev, generator=g).to(dt) for _ in range(args.bufs)]
+        x = xs[0]
         w = (torch.randn(Co, k * k * Ci, device=dev, generator=g) / (k * k * Ci) ** 0.5).to(dt)
         b = torch.randn(Co, device=dev, generator=g)
         Ho = (H + 2 * p - d * (k - 1) - 1) // s + 1
@@ -71,8 +75,8 @@ def main():
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        for _ in range(args.iters):
-            runtime.conv2d_nhwc(x, w, b, k, k, s, p, d, residual=r, relu=relu)
+        for i in range(args.iters):
+            runtime.conv2d_nhwc(xs[i % args.bufs], w, b, k, k, s, p, d, residual=r, relu=relu)
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / args.iters
