@@ -513,6 +513,19 @@ def train_parity(sd, x, d0, amp):
                       f"vs oracle/train.py forward + TotalLoss (fp32 torch-CPU, train-mode BatchNorm)"}
 
 
+def call_bound(kind, what, fl, ms, sh, B):
+    """The roofline bound of one timed training conv call (see bound_note)."""
+    if not sh or ms <= 0:
+        return {}
+    ci, co, k, s, H, W = sh
+    ho, wo = H // s, W // s
+    xb, yb = 2.0 * B * H * W * ci, 2.0 * B * ho * wo * co
+    nbytes = xb + yb + 2.0 * ci * co * k * k
+    peak = PEAK_TFLOPS["fp16"] if kind == "mfma16" else PEAK_TFLOPS["fp32"]
+    bound = max(fl / 1e9 / peak, nbytes / 1e6 / PEAK_HBM_GBS)  # ms
+    return {"bound_ms": round(bound, 4), "x_bound": round(ms / bound, 2)}
+
+
 def train_roofline(recs, step_ms, B, S):
     """Convs of the profiled step against the peak of the arithmetic they ran
     in (fp16 MFMA under autocast, fp32 MFMA otherwise); the rest of the step
@@ -545,9 +558,14 @@ def train_roofline(recs, step_ms, B, S):
             "kernel": f"{main} conv calls of one profiled step (forward, input gradient, weight gradient; each call "
                       f"timed with HIP events around its library call(s), algorithmic flops)",
             "by_arithmetic": by, "by_pass": by_what,
-            "slowest_calls": [{"kind": k, "pass": w, "shape": ("%d->%d k%d s%d %dx%d" % sh) if sh else None,
-                               "ms": round(ms, 4), "TFLOPs": round(fl / 1e9 / ms, 1) if ms > 0 else None}
+            "slowest_calls": [dict({"kind": k, "pass": w, "shape": ("%d->%d k%d s%d %dx%d" % sh) if sh else None,
+                                    "ms": round(ms, 4), "TFLOPs": round(fl / 1e9 / ms, 1) if ms > 0 else None},
+                                   **call_bound(k, w, fl, ms, sh, B))
                               for k, w, fl, ms, sh in sorted(recs, key=lambda r: -r[3])[:16]],
+            "bound_note": "bound_ms per call = max(algorithmic flops / the arithmetic's peak, the minimal operand "
+                          "bytes / 8 TB/s) with fp16 tensors in and out (fwd: x + y, dgrad: dy + dx, wgrad: x + dy; "
+                          "the step also writes fp32 copies where its fp32 BatchNorm / loss read them); x_bound = "
+                          "ms / bound_ms",
             "step_ms": step_ms, "conv_ms": conv_ms,
             "non_conv_ms": step_ms - conv_ms,
             "non_conv_note": "BatchNorm stats/apply, ReLU masks, fp32<->fp16 casts, pooling, losses, FFTs, "
@@ -832,6 +850,9 @@ def compact(out):
             cr["frac_vs_measured_mfma"] = r["measured_ceilings"].get("frac_vs_measured_mfma")
         if "non_conv_ms" in r and r.get("step_ms"):
             cr["non_conv_share"] = r["non_conv_ms"] / r["step_ms"]
+        xb = [c_["x_bound"] for c_ in r.get("slowest_calls") or [] if "x_bound" in c_]
+        if xb:
+            cr["slowest_calls_max_x_bound"] = max(xb)
         c["roofline"] = cr
     if "parity" in out and out["parity"]:
         p = out["parity"]
