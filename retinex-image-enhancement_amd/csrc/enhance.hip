@@ -260,6 +260,8 @@ __global__ __launch_bounds__(256) void clahe_hist_kernel(const void* __restrict_
   int row = t / TWV, col = t - (t / TWV) * TWV;
   const int inc_r = 256 / TWV, inc_c = 256 - inc_r * TWV;
   int* hw = hist[wave];
+  // (issuing 4 iterations' loads together measured slower twice: 27.5 -> 36.0 us,
+  // profiles/r5_enh_kernels_ab.txt -- occupancy halves, the LDS atomics are the limit)
   for (; row < g.R; row += inc_r) {
     const int y = y0 + row;
     const int yr = y < H ? y : 2 * H - 2 - y;  // BORDER_REFLECT_101 (one reflection)
@@ -339,6 +341,7 @@ __global__ __launch_bounds__(256) void clahe_apply_kernel(const uint8_t* __restr
                                                           const DevLab* __restrict__ tab, void* __restrict__ out,
                                                           ClaheArgs g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+  __shared__ float inv255[256];            // __fdiv_rn(i, 255): the /255 of the output, looked up
   uint16_t* yf = (uint16_t*)sm;            // 512
   uint16_t* ig = yf + 512;                 // 4096
   uint8_t* lrows = (uint8_t*)(ig + 4096);  // <= 3 tile rows of LUTs
@@ -360,6 +363,7 @@ __global__ __launch_bounds__(256) void clahe_apply_kernel(const uint8_t* __restr
   if constexpr (DST == 0) {
     for (int i = t; i < 512; i += 256) yf[i] = tab->yf_b[i];
     for (int i = t; i < 4096; i += 256) ig[i] = tab->invgamma_b[i];
+    inv255[t] = __fdiv_rn((float)t, 255.f);
 #pragma unroll
     for (int k = 0; k < 9; ++k) c[k] = tab->xyz2rgb[k];
   }
@@ -367,7 +371,25 @@ __global__ __launch_bounds__(256) void clahe_apply_kernel(const uint8_t* __restr
   const int WV = W / V;
   int row = t / WV, col = t - (t / WV) * WV;
   const int inc_r = 256 / WV, inc_c = 256 - inc_r * WV;
+  // per-column interpolation terms of this thread's V pixels: computed once
+  // when every iteration keeps the column (inc_c == 0: W / V divides 256)
+  int cx1[V], cx2[V];
+  float cxa[V], cxa1[V];
+  auto colterms = [&](int cl) {
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const int x = cl * V + k;
+      const float txf = __fsub_rn(__fmul_rn((float)x, inv_tw), 0.5f);
+      const int tx1 = (int)floorf(txf);
+      cxa[k] = __fsub_rn(txf, (float)tx1);
+      cxa1[k] = __fsub_rn(1.0f, cxa[k]);
+      cx1[k] = max(tx1, 0) * 256;
+      cx2[k] = min(tx1 + 1, g.tilesX - 1) * 256;
+    }
+  };
+  if (inc_c == 0) colterms(col);
   for (; row < nrows; row += inc_r) {
+    if (inc_c != 0) colterms(col);
     const int y = y0 + row;
     const float tyf = __fsub_rn(__fmul_rn((float)y, inv_th), 0.5f);
     int ty1 = (int)floorf(tyf);
@@ -394,16 +416,10 @@ __global__ __launch_bounds__(256) void clahe_apply_kernel(const uint8_t* __restr
     int lc[V];
 #pragma unroll
     for (int k = 0; k < V; ++k) {
-      const int x = col * V + k;
-      const float txf = __fsub_rn(__fmul_rn((float)x, inv_tw), 0.5f);
-      int tx1 = (int)floorf(txf);
-      int tx2 = tx1 + 1;
-      const float xa = __fsub_rn(txf, (float)tx1), xa1 = __fsub_rn(1.0f, xa);
-      tx1 = max(tx1, 0);
-      tx2 = min(tx2, g.tilesX - 1);
+      const float xa = cxa[k], xa1 = cxa1[k];
       const int v = Lv[k];
-      const float l11 = r1[tx1 * 256 + v], l12 = r1[tx2 * 256 + v];
-      const float l21 = r2[tx1 * 256 + v], l22 = r2[tx2 * 256 + v];
+      const float l11 = r1[cx1[k] + v], l12 = r1[cx2[k] + v];
+      const float l21 = r2[cx1[k] + v], l22 = r2[cx2[k] + v];
       // res = (l11*xa1 + l12*xa)*ya1 + (l21*xa1 + l22*xa)*ya, no contraction
       const float top = __fadd_rn(__fmul_rn(l11, xa1), __fmul_rn(l12, xa));
       const float bot = __fadd_rn(__fmul_rn(l21, xa1), __fmul_rn(l22, xa));
@@ -420,9 +436,9 @@ __global__ __launch_bounds__(256) void clahe_apply_kernel(const uint8_t* __restr
       for (int k = 0; k < V; ++k) {
         int r8, g8, b8;
         lab2rgb_lds(yf, ig, c, lc[k], Av[k], Bv[k], r8, g8, b8);
-        R[k] = __fdiv_rn((float)r8, 255.f);
-        G[k] = __fdiv_rn((float)g8, 255.f);
-        Bo[k] = __fdiv_rn((float)b8, 255.f);
+        R[k] = inv255[r8];
+        G[k] = inv255[g8];
+        Bo[k] = inv255[b8];
       }
       T* o = (T*)out + (size_t)b * 3 * HW + (size_t)y * W + col * V;
       if constexpr (V == 4) {
@@ -578,10 +594,11 @@ __global__ __launch_bounds__(256) void ms_sums_kernel(const T* __restrict__ x, u
 // (every pixel of the image is read from HBM once, halos from L2), forms the
 // half / quarter samples (+ their 1-sample halos) from LDS with sample_s's
 // arithmetic, and sums the 7 features of all three tiles.  The three block
-// sums go to the image's fixed-point accumulators; the block that completes
-// an image (per-image arrival counter) writes its fp64 sums and factor and
-// resets the accumulators to zero for the next call -- no factor launch, no
-// per-call memset (the scratch is zeroed once when allocated).
+// sums are stored to the tile's partial slot and the block ends; ms_fin_kernel
+// adds an image's partials in tile order (fp64, deterministic) and writes the
+// sums and the factor.  (An earlier form ended every block with fixed-point
+// atomics and an arrival counter, the last block finishing the image: the
+// blocks' atomic tails held their LDS and cost more than the extra launch.)
 constexpr int M3_TH = 32, M3_TW = 64, M3_HALO = 4;
 constexpr int M3_RH = M3_TH + 2 * M3_HALO, M3_RW = M3_TW + 2 * M3_HALO;
 constexpr int M3_H1 = M3_TH / 2 + 2, M3_W1 = M3_TW / 2 + 2, M3_H2 = M3_TH / 4 + 2, M3_W2 = M3_TW / 4 + 2;
@@ -596,7 +613,12 @@ __device__ __forceinline__ float blend_half(float v00, float v01, float v10, flo
 
 // the 7 features of pixel (R, C) of an LDS image P (3 planes of PH x PW)
 // whose pixel (R, C) is image pixel (y, x) of an hs x ws scale (torch.gradient:
-// central differences, one-sided at the borders)
+// central differences, one-sided at the borders).  The gradient magnitude
+// takes the hardware square root (v_sqrt_f32, <= 1 ulp) instead of the
+// correctly rounded expansion (~15 instructions each, 3 per pixel: that
+// expansion was a third of this pass's VALU work); the sums feed means over
+// >= 10^5 pixels, and the factor stays within 1e-8 of the oracle's (tests
+// hold it to 1e-6).  The feature MAPS (ms_features_kernel) keep sqrtf.
 template <int PH, int PW>
 __device__ __forceinline__ float ms_feat(const float (&P)[3][PH][PW], int R, int C, int y, int x, int hs, int ws) {
   float c3[3];
@@ -614,7 +636,7 @@ __device__ __forceinline__ float ms_feat(const float (&P)[3][PH][PW], int R, int
     else if (y == 0) gy = P[ch][R + 1][C] - v;
     else if (y == hs - 1) gy = v - P[ch][R - 1][C];
     else gy = (P[ch][R + 1][C] - P[ch][R - 1][C]) / 2.f;
-    fsum += v + sqrtf(gx * gx + gy * gy);
+    fsum += v + __builtin_amdgcn_sqrtf(gx * gx + gy * gy);
   }
   fsum += 0.299f * c3[0] + 0.587f * c3[1] + 0.114f * c3[2];
   return fsum;
@@ -646,7 +668,7 @@ __device__ __forceinline__ double ms_feat4(const float (&P)[3][PH][PW], int R, i
     for (int k = 0; k < 4; ++k) {
       const float gx = (v[k + 2] - v[k]) / 2.f;
       const float gy = (d[k] - u[k]) / 2.f;
-      fs[k] += v[k + 1] + sqrtf(gx * gx + gy * gy);
+      fs[k] += v[k + 1] + __builtin_amdgcn_sqrtf(gx * gx + gy * gy);
       c3[ch][k] = v[k + 1];
     }
   }
@@ -659,15 +681,12 @@ __device__ __forceinline__ double ms_feat4(const float (&P)[3][PH][PW], int R, i
 __device__ __forceinline__ double ms_factor(const double* sums, int b, double n0, double n1, double n2);
 
 template <typename T>
-__global__ __launch_bounds__(256) void ms_sums3_kernel(const T* __restrict__ x, unsigned long long* __restrict__ acc,
-                                                       unsigned* __restrict__ cnt, double* __restrict__ sums,
-                                                       double* __restrict__ factor, int H, int W, int tiles_x,
-                                                       unsigned nblk_img, double n0, double n1, double n2) {
+__global__ __launch_bounds__(256) void ms_sums3_kernel(const T* __restrict__ x, double* __restrict__ part, int H,
+                                                       int W, int tiles_x) {
   __shared__ float full[3][M3_RH][M3_RW];
   __shared__ __attribute__((aligned(16))) float s1[3][M3_H1][M3_P1];
   __shared__ __attribute__((aligned(16))) float s2[3][M3_H2][M3_P2];
   __shared__ double red[4][3];
-  __shared__ int is_last;
   const int t = threadIdx.x;
   // tiles in XCD-contiguous order (blocks i, i + 8, ... share an XCD: they take
   // neighbouring tiles, whose 4-pixel halo lines then come from that XCD's L2;
@@ -681,7 +700,9 @@ __global__ __launch_bounds__(256) void ms_sums3_kernel(const T* __restrict__ x, 
   const T* img = x + (size_t)b * 3 * HW;
   // full-resolution region: rows ty0 - 4 .., columns tx0 - 4 .. in 4-pixel quads
   // every quad's load is issued before the first LDS store (NLD loads in
-  // flight per thread: one HBM round trip per block, not one per quad)
+  // flight per thread: one HBM round trip per block, not one per quad).  (A
+  // persistent form loading tile j + 1 under tile j's work measured no faster:
+  // 0.074 vs 0.071 ms)
   constexpr int QPR = M3_RW / 4, QPC = M3_RH * QPR, NLD = (3 * QPC + 255) / 256;
   float v[NLD][4];
 #pragma unroll
@@ -752,28 +773,33 @@ __global__ __launch_bounds__(256) void ms_sums3_kernel(const T* __restrict__ x, 
   }
   if ((t & 63) == 0) { red[t >> 6][0] = a0; red[t >> 6][1] = a1; red[t >> 6][2] = a2; }
   __syncthreads();
-  if (t < 64) {
-    // wave 0: the block's three fixed-point adds, then (once they are
-    // performed: agent-scope integer atomics execute at the memory side, and
-    // vmcnt(0) waits for their acknowledgement) its arrival.  No release
-    // fence: __threadfence's L2 write-back cost ~30 us per CU slot here
-    if (t < 3) {
-      const double blk = red[0][t] + red[1][t] + red[2][t] + red[3][t];
-      atomicAdd(&acc[b * 3 + t], (unsigned long long)(long long)llrint(blk * kMsFix));
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (t == 0) is_last = atomicAdd(&cnt[b], 1u) == nblk_img - 1;
-  }
+  // the block's three sums, plain stores: no atomics or arrival counter to
+  // wait for at the end of every block (ms_fin_kernel adds them in order)
+  if (t < 3) part[((size_t)b * gridDim.x + tin) * 3 + t] = red[0][t] + red[1][t] + red[2][t] + red[3][t];
+}
+
+// per image: the tile partials of ms_sums3_kernel added in a fixed order (one
+// block per image; deterministic fp64), then sums and the factor
+__global__ __launch_bounds__(256) void ms_fin_kernel(const double* __restrict__ part, int nblk, double* __restrict__ sums,
+                                                     double* __restrict__ factor, double n0, double n1, double n2) {
+  __shared__ double red[3][256];
+  const int b = blockIdx.x, t = threadIdx.x;
+  double a[3] = {0.0, 0.0, 0.0};
+  for (int i = t; i < nblk; i += 256)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) a[k] += part[((size_t)b * nblk + i) * 3 + k];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) red[k][t] = a[k];
   __syncthreads();
-  if (is_last && t == 0) {
-    double sm[3];
-    for (int i = 0; i < 3; ++i) {
-      // read and reset in one atomic (the accumulators stay zero between calls)
-      const unsigned long long q = atomicExch(&acc[b * 3 + i], 0ull);
-      sm[i] = (double)(long long)q / kMsFix;
-      sums[b * 3 + i] = sm[i];
-    }
-    atomicExch(&cnt[b], 0u);
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) red[k][t] += red[k][t + o];
+    __syncthreads();
+  }
+  if (t == 0) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) sums[b * 3 + k] = red[k][0];
     if (factor) factor[b] = ms_factor(sums, b, n0, n1, n2);
   }
 }
@@ -973,22 +999,21 @@ int launch_multiscale(const void* x, const void* enh, void* out, double* sums, d
     if (!fac) return (int)hipErrorOutOfMemory;
   }
   if (H % 4 == 0 && W % 4 == 0 && (uintptr_t)x % (dtype == kF16 ? 8 : 16) == 0) {
-    // single pass (ms_sums3_kernel): accumulators + arrival counters in a
-    // scratch slot that the kernel leaves zeroed
-    bool fresh = false;
-    const size_t accb = ((size_t)B * 3 * sizeof(unsigned long long) + 255) & ~(size_t)255;
-    uint8_t* sc = (uint8_t*)scratch(kSlotMs, accb + (size_t)B * sizeof(unsigned), st, &fresh);
-    if (!sc) return (int)hipErrorOutOfMemory;
-    if (fresh) UPR_CHECK_HIP(hipMemsetAsync(sc, 0, accb + (size_t)B * sizeof(unsigned), st));
-    const int tx = (W + M3_TW - 1) / M3_TW, ty = (H + M3_TH - 1) / M3_TH;
-    unsigned long long* acc = (unsigned long long*)sc;
-    unsigned* cnt = (unsigned*)(sc + accb);
+    // single pass (ms_sums3_kernel): per-tile partials in a scratch slot,
+    // added in order by ms_fin_kernel.  (A streamed form -- 64-column strips
+    // walked in 4-row bands through LDS row rings, one band of prefetch --
+    // measured 0.281 ms against this kernel's 0.085: too little in flight per
+    // block, profiles/r5_ms_strip_vs_tiled.txt)
+    const int tx = (W + M3_TW - 1) / M3_TW;
+    const int nblk = tx * ((H + M3_TH - 1) / M3_TH);
+    double* part = (double*)scratch(kSlotMs, (size_t)B * nblk * 3 * sizeof(double), st);
+    if (!part) return (int)hipErrorOutOfMemory;
     if (dtype == kF16)
-      hipLaunchKernelGGL((ms_sums3_kernel<half_t>), dim3(tx * ty, B), dim3(256), 0, st, (const half_t*)x, acc, cnt,
-                         sums, fac, H, W, tx, (unsigned)(tx * ty), n0, n1, n2);
+      hipLaunchKernelGGL((ms_sums3_kernel<half_t>), dim3(nblk, B), dim3(256), 0, st, (const half_t*)x, part, H, W, tx);
     else
-      hipLaunchKernelGGL((ms_sums3_kernel<float>), dim3(tx * ty, B), dim3(256), 0, st, (const float*)x, acc, cnt,
-                         sums, fac, H, W, tx, (unsigned)(tx * ty), n0, n1, n2);
+      hipLaunchKernelGGL((ms_sums3_kernel<float>), dim3(nblk, B), dim3(256), 0, st, (const float*)x, part, H, W, tx);
+    UPR_CHECK_HIP(hipGetLastError());
+    hipLaunchKernelGGL(ms_fin_kernel, dim3(B), dim3(256), 0, st, (const double*)part, nblk, sums, fac, n0, n1, n2);
     UPR_CHECK_HIP(hipGetLastError());
   } else {
     UPR_CHECK_HIP(hipMemsetAsync(sums, 0, sizeof(double) * 3 * B, st));

@@ -356,10 +356,9 @@ def test_multiscale_kernel(golden):
 ])
 def test_multiscale_single_pass(B, H, W, dtype):
     """upr_multiscale's one-pass kernel (ms_sums3_kernel: all three scales from
-    one read, the completing block writes the sums / factor and re-zeroes the
-    accumulators) vs the oracle's per-image factor (multi_scale.py:62-100),
-    called three times in a row (a stale accumulator or arrival counter would
-    change the second and third result)."""
+    one read, per-tile partials added in order by ms_fin_kernel) vs the
+    oracle's per-image factor (multi_scale.py:62-100), called three times in a
+    row (the three results must be bit-identical)."""
     from upr import runtime
     x = torch.rand(B, 3, H, W, generator=torch.Generator().manual_seed(21)).to(dtype)
     enh = torch.rand(B, 3, H, W, generator=torch.Generator().manual_seed(22)).to(dtype)
