@@ -527,13 +527,13 @@ __device__ __forceinline__ void direct_epilogue(const ConvOp& op, f32x4_w (&acc)
   }
 }
 
-template <int BN, int WM, int WN, int WAVES_M, int W>
+template <int BN, int WM, int WN, int WAVES_M, int W, bool PRE = true>
 __device__ __forceinline__ void hw4_direct_epilogue(const ConvOp& op, f32x4_w (&acc)[WM][WN], int m0, int n0,
                                                     int wm, int wn, int lane, const f16x8_w (&rv0)[WM],
                                                     unsigned char* smem) {
   constexpr int CW = W / WAVES_M, FPR = CW / 16;
   const int mb = m0 + CW * wm + (lane & 15);  // pixel of fragment a: mb + (a / FPR) * W + (a % FPR) * 16
-  direct_epilogue<BN, WM, WN, WAVES_M, true>(
+  direct_epilogue<BN, WM, WN, WAVES_M, PRE>(
       op, acc, n0, wm, wn, lane, rv0, smem, [&](int a) { return mb + (a / FPR) * W + (a % FPR) * 16; }, 1 << 30,
       op.Ho * W, m0 / (op.Ho * W));
 }
@@ -1308,8 +1308,10 @@ __device__ __forceinline__ void hw4_res_load(const ConvOp& op, f16x8_w (&rv0)[WM
 // fills ring half k & 1 (2 x TR x ROW: 64 KB at W 64 x 4 rows, W 128 x 2
 // rows); BN 128 leaves two 16 KB B stages.  Region k + 2 is issued after
 // region k's last tap (three steps of lookahead), B(S + 2) after barrier S.
+// NR: the op has no residual (res1 = res2 = null): no residual prefetch
+// registers (rv0) -- 32 VGPRs the bottleneck conv1 / ASPP programs spilled for
 template <int BN, int W, int NCH, int ABL = 0, bool DS = false, bool DL = false, int TR = 4, int NSC = 0,
-          bool PW = false, bool S2 = false>
+          bool PW = false, bool S2 = false, bool NR = false>
 __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
   using HC = Halo3Cfg<BN, W, TR, PW ? 12 : S2 ? 4 * TR : 0>;
   static_assert(TR == 4 || (NCH == 1 && !DL && DS), "2-row tiles: one chunk, direct store");
@@ -1720,7 +1722,8 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
               issue_rows(nc, nt);
             }
           }
-          if constexpr (DS && S == TOTAL - 2) hw4_res_load<WM, WN, HC::WAVES_M, W>(op, rv0, m0, n0, wm, wn, lane);
+          if constexpr (DS && !NR && S == TOTAL - 2)
+            hw4_res_load<WM, WN, HC::WAVES_M, W>(op, rv0, m0, n0, wm, wn, lane);
           rd_b(std::integral_constant<int, n>{}, I0{}, b0);
           mm_roll(std::integral_constant<int, n>{}, I0{}, b1, true);
         } else {
@@ -1740,9 +1743,10 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
       __syncthreads();
     }
     if constexpr ((ABL & 4) != 0) {
-      if (acc[0][0][0] == 12345.f) hw4_direct_epilogue<BN, WM, WN, HC::WAVES_M, W>(op, acc, m0, n0, wm, wn, lane, rv0, smem);
+      if (acc[0][0][0] == 12345.f)
+        hw4_direct_epilogue<BN, WM, WN, HC::WAVES_M, W, !NR>(op, acc, m0, n0, wm, wn, lane, rv0, smem);
     } else {
-      hw4_direct_epilogue<BN, WM, WN, HC::WAVES_M, W>(op, acc, m0, n0, wm, wn, lane, rv0, smem);
+      hw4_direct_epilogue<BN, WM, WN, HC::WAVES_M, W, !NR>(op, acc, m0, n0, wm, wn, lane, rv0, smem);
     }
     if constexpr ((ABL & 4) != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     return;
@@ -1759,19 +1763,20 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
 }
 
 template <int BN, int W, int NCH, int ABL = 0, bool DS = false, bool DL = false, int TR = 4, int NSC = 0,
-          bool PW = false, bool S2 = false>
+          bool PW = false, bool S2 = false, bool NR = false>
 static int launch_hwide4_k(const ConvOp& op, hipStream_t st) {
   using HC = Halo3Cfg<BN, W, TR, PW ? 12 : S2 ? 4 * TR : 0>;
   static bool attr_set = false;
   if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute((const void*)conv_hwide4_kernel<BN, W, NCH, ABL, DS, DL, TR, NSC, PW, S2>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, HC::LDS);
+    const hipError_t e =
+        hipFuncSetAttribute((const void*)conv_hwide4_kernel<BN, W, NCH, ABL, DS, DL, TR, NSC, PW, S2, NR>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, HC::LDS);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
   const int grid = (op.B * op.Ho * W / HC::BM) * (op.N / BN);
-  hipLaunchKernelGGL((conv_hwide4_kernel<BN, W, NCH, ABL, DS, DL, TR, NSC, PW, S2>), dim3(grid), dim3(512), HC::LDS,
-                     st, op);
+  hipLaunchKernelGGL((conv_hwide4_kernel<BN, W, NCH, ABL, DS, DL, TR, NSC, PW, S2, NR>), dim3(grid), dim3(512),
+                     HC::LDS, st, op);
   return (int)hipGetLastError();
 }
 
@@ -1797,7 +1802,10 @@ static bool hw4_ds_ok(const ConvOp& op) {
 
 template <int BN, int W, int NCH>
 static int launch_hwide4(const ConvOp& op, hipStream_t st) {
-  if (hw4_ds_ok(op)) return launch_hwide4_k<BN, W, NCH, 0, true>(op, st);
+  if (hw4_ds_ok(op)) {
+    if (!op.res1 && !op.res2) return launch_hwide4_k<BN, W, NCH, 0, true, false, 4, 0, false, false, true>(op, st);
+    return launch_hwide4_k<BN, W, NCH, 0, true>(op, st);
+  }
   return launch_hwide4_k<BN, W, NCH, 0, false>(op, st);
 }
 
@@ -1893,8 +1901,10 @@ static int halo_route(const ConvOp& op, hipStream_t st) {
   // 0.158 / 0.145 / 0.136, profiles/r3_hw4_dil_ab.txt)
   if (s.kh == 3 && s.kw == 3 && s.stride == 1 && s.dil > 1 && s.pad == s.dil && s.dil < 64 && s.pre == kPreNone &&
       s.kbase == 0 && s.C == 256 && s.Hin == op.Ho && s.Win == op.Wo && op.Wo == 64 && op.N % 256 == 0 &&
-      (op.Ho * op.Wo) % WBM == 0 && hw4_ds_ok(op))
+      (op.Ho * op.Wo) % WBM == 0 && hw4_ds_ok(op)) {
+    if (!op.res1 && !op.res2) return launch_hwide4_k<256, 64, 4, 0, true, true, 4, 0, false, false, true>(op, st);
     return launch_hwide4_k<256, 64, 4, 0, true, true>(op, st);
+  }
   if (s.kh != 3 || s.kw != 3 || s.stride != 1 || s.pad != 1 || s.dil != 1 || s.pre != kPreNone) return kErrUnsupported;
   if (s.Hin != op.Ho || s.Win != op.Wo || s.C % WBK || (op.Ho * op.Wo) % WBM) return kErrUnsupported;
   // (64 -> 64 at W 256, the dec2 UpBlock convs, as hwide4 2-row tiles measured
