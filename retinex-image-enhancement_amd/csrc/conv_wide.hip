@@ -1315,7 +1315,7 @@ template <int BN, int W, int NCH, int ABL = 0, bool DS = false, bool DL = false,
 __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
   using HC = Halo3Cfg<BN, W, TR, PW ? 12 : S2 ? 4 * TR : 0>;
   static_assert(TR == 4 || (NCH == 1 && !DL && DS), "2-row tiles: one chunk, direct store");
-  static_assert(NSC == 0 || (NSC == 1 && !DL && TR == 4 && DS), "shortcut segment: 4-row tiles, direct store");
+  static_assert(NSC == 0 || (NSC <= 2 && !DL && TR == 4 && DS), "shortcut segment: 4-row tiles, direct store");
   static_assert(!PW || (!DL && NSC == 0 && TR == 4 && DS && HC::NBS == 2 && NCH >= 3), "pointwise form");
   static_assert(!S2 || (!DL && !PW && NSC == 0 && DS && HC::NBS == 2), "stride-2 form");
   constexpr int WM = HC::WM, WN = HC::WN, BM = HC::BM, NBS = HC::NBS;
@@ -1372,6 +1372,13 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
   // channels at once
   const int rot = PW && op.krot ? __builtin_amdgcn_readfirstlane(mtile % NCH) : 0;
   auto kchunk = [&](int cc) { const int k = cc + rot; return k >= NCH ? k - NCH : k; };
+  // ring row of region row r of chunk cc: (6 cc + r) & 7; with two shortcut
+  // chunks the second takes the last 3x3 chunk's rows 2-5 (free once its
+  // last tap is read; the first shortcut chunk holds the two spare rows and
+  // that chunk's rows 0 / 1)
+  constexpr auto ring_slot = [](int cc, int r) -> int {
+    return NSC == 2 && cc == NCH + 1 ? (6 * (NCH - 1) + 2 + r) & 7 : (6 * cc + r) & 7;
+  };
   auto region_row = [&](int cc, int r) {  // cc, r compile-time at every call site
     if constexpr (PW) {  // tile row r of chunk cc -> ring row (4 cc + r) % 12 (always inside the image)
       unsigned char* dst = smem + ((4 * cc + r) % HC::RR) * HC::ROW + wave * 1024;
@@ -1382,8 +1389,8 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
       return;
     }
     if (NSC && cc >= NCH) {
-      unsigned char* dst = smem + ((6 * cc + r) & 7) * HC::ROW + wave * 1024;
-      const size_t srow = (size_t)2 * (oy0 + r) * sc.Win * sc.cs * 2;
+      unsigned char* dst = smem + ring_slot(cc, r) * HC::ROW + wave * 1024;
+      const size_t srow = (size_t)2 * (oy0 + r) * sc.Win * sc.cs * 2 + (size_t)(cc - NCH) * WBK * 2;
 #pragma unroll
       for (int k = 0; k < HC::RP; ++k)
         glds16_s(scbase + srow + (size_t)k * 128 * sc.cs * 2, voff_sc, dst + k * 8192);
@@ -1410,6 +1417,12 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
     if (TR != 4) return;
     if (t < 2) {
       if (c < NCH) region_row(c, 4 + t);
+      // second shortcut chunk: all 4 rows right before the first shortcut step
+      // reads (one step of lookahead; the wait of that step drains them)
+      if (NSC == 2 && c == NCH) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) region_row(NCH + 1, r);
+      }
     } else if (c + 1 < NCH + NSC) {
       if (t == 2) region_row(c + 1, 0);
       else if (t == 3) region_row(c + 1, 2);
@@ -1579,7 +1592,7 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
       return *(const f16x8_w*)(smem + ao + (off & 0xffff));
     } else {
       constexpr bool edge = (tx == 0 && a % FPR == 0) || (tx == 2 && a % FPR == FPR - 1);
-      constexpr int rr = PW ? (4 * c + a / FPR) % HC::RR : (6 * c + ty + a / FPR) & 7;
+      constexpr int rr = PW ? (4 * c + a / FPR) % HC::RR : ring_slot(c, ty + a / FPR);
       constexpr int off = rr * HC::ROW + (a % FPR) * 16 * 128;
       int ao;
       if constexpr (edge && tx == 0) ao = KK ? (aofs_e[0] ^ 64) : aofs_e[0];
@@ -1702,6 +1715,9 @@ __global__ __launch_bounds__(512, 2) void conv_hwide4_kernel(ConvOp op) {
               asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(HC::BJ) : "memory");
             else
               asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(HC::BJ + 4 * HC::RP) : "memory");
+          } else if constexpr (NSC == 2 && S == NCH * 9) {
+            // the second shortcut chunk's rows (issued last, at barrier S - 1) are read next
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
           } else if constexpr (rows_at(c, t))
             asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(VB + HC::RP) : "memory");
           else
@@ -1833,20 +1849,23 @@ static int launch_hwide34(const ConvOp& op, hipStream_t st) {
 // halo-tiled convs: the ring / three-stage form (hwide4 / hwide3) for W 64 x
 // N 256 and W 128 x N 128, the two-stage halo kernel for W 64 x N 128
 // (measured against the gathered-A kernel: profiles/r2_halo*, r3_hw4_*)
-// the 3x3 segment + projecting-shortcut program hwide4 takes (NSC = 1): enc2.conv2
-// (128 -> 128 at W 128, shortcut over the block's 64-channel input)
-static bool hw4_sc_ok(const ConvOp& op) {
-  if (op.nseg != 2 || op.store != kStoreNHWC) return false;
+// the 3x3 segment + projecting-shortcut programs hwide4 takes: enc2.conv2 (128
+// -> 128 at W 128, shortcut over the block's 64-channel input: NSC 1) and
+// enc3.conv2 (256 -> 256 at W 64, shortcut over 128 channels: NSC 2).
+// Returns the shortcut chunk count, 0 when neither fits
+static int hw4_sc_ok(const ConvOp& op) {
+  if (op.nseg != 2 || op.store != kStoreNHWC) return 0;
   const ConvSeg& s = op.seg[0];
   const ConvSeg& q = op.seg[1];
   if (s.kh != 3 || s.kw != 3 || s.stride != 1 || s.pad != 1 || s.dil != 1 || s.pre != kPreNone || s.kbase != 0)
-    return false;
-  if (s.C != 128 || s.Hin != op.Ho || s.Win != op.Wo || op.Wo != 128 || op.N != 128 || (op.Ho * op.Wo) % 512) return false;
-  if (q.kh != 1 || q.kw != 1 || q.stride != 2 || q.pad != 0 || q.pre != kPreNone || q.C != 64 || q.kbase != 9 * s.C)
-    return false;
-  if (q.Hin != 2 * op.Ho || q.Win != 2 * op.Wo || q.cs % 8 || q.coff % 8 || (uintptr_t)q.src % 16) return false;
-  if (op.Kpad != 9 * s.C + 64 || s.cs % 8 || s.coff % 8 || (uintptr_t)s.src % 16) return false;
-  return hw4_ds_ok(op);
+    return 0;
+  if (q.kh != 1 || q.kw != 1 || q.stride != 2 || q.pad != 0 || q.pre != kPreNone || q.kbase != 9 * s.C) return 0;
+  if (s.Hin != op.Ho || s.Win != op.Wo || q.Hin != 2 * op.Ho || q.Win != 2 * op.Wo) return 0;
+  if (q.cs % 8 || q.coff % 8 || (uintptr_t)q.src % 16 || s.cs % 8 || s.coff % 8 || (uintptr_t)s.src % 16) return 0;
+  if (op.Kpad != 9 * s.C + q.C || !hw4_ds_ok(op)) return 0;
+  if (s.C == 128 && op.Wo == 128 && op.N == 128 && (op.Ho * op.Wo) % 512 == 0 && q.C == 64) return 1;
+  if (s.C == 256 && op.Wo == 64 && op.N == 256 && op.Ho % 4 == 0 && q.C == 128) return 2;
+  return 0;
 }
 
 // 1x1 stride-1 GEMMs over whole 64-pixel rows, K 256 / 1024 / 1280 -> N 256k (the ASPP
@@ -1891,7 +1910,11 @@ static int hw4_s2_route(const ConvOp& op, hipStream_t st) {
 }
 
 static int halo_route(const ConvOp& op, hipStream_t st) {
-  if (hw4_sc_ok(op)) return launch_hwide4_k<128, 128, 2, 0, true, false, 4, 1>(op, st);
+  if (const int nsc = hw4_sc_ok(op)) {
+    if (nsc == 1) return launch_hwide4_k<128, 128, 2, 0, true, false, 4, 1>(op, st);
+    static const bool off = [] { const char* e = getenv("UPR_HW4_SC2"); return e && atoi(e) == 0; }();
+    if (!off) return launch_hwide4_k<256, 64, 4, 0, true, false, 4, 2>(op, st);  // (UPR_HW4_SC2=0: A/B)
+  }
   if (op.nseg != 1 || op.store != kStoreNHWC) return kErrUnsupported;
   const ConvSeg& s = op.seg[0];
   if (s.kh == 1 && s.kw == 1) return hw4_pw_route(op, st);
