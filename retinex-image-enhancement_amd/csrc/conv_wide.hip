@@ -2025,7 +2025,9 @@ int launch_conv_wide(const ConvOp& op, hipStream_t st) {
     if (sg.pre != kPreNone || sg.C % WBK || sg.cs % 8 || sg.coff % 8 || sg.kbase % 8) return kErrUnsupported;
     if ((uintptr_t)sg.src % 16) return kErrUnsupported;
   }
-  {
+  // UPR_HALO=0: skip the halo-tiled forms (A/B against the gathered kernel, tools/convbench.py)
+  static const bool halo_off = [] { const char* e = getenv("UPR_HALO"); return e && atoi(e) == 0; }();
+  if (!halo_off) {
     const int rc = halo_route(op, st);
     if (rc != kErrUnsupported) return rc;
   }

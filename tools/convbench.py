@@ -42,6 +42,10 @@ SHAPES = {
     "enc1c2": (32, 256, 256, 64, 64, 3, 1, 1, 1, True),   # enc1.conv2 (without the shortcut segment)
     "enc2c2": (32, 128, 128, 128, 128, 3, 1, 1, 1, True),
     "vgg3": (16, 128, 128, 256, 256, 3, 1, 1, 1, False),  # perceptual-loss VGG conv3_2/3_3 at 512^2
+    "vgg31": (16, 128, 128, 128, 256, 3, 1, 1, 1, False),  # VGG conv3_1
+    "vgg2": (16, 256, 256, 128, 128, 3, 1, 1, 1, False),   # VGG conv2_2
+    "vgg21": (16, 256, 256, 64, 128, 3, 1, 1, 1, False),   # VGG conv2_1
+    "vgg1": (16, 512, 512, 64, 64, 3, 1, 1, 1, False),     # VGG conv1_2
     "up1": (32, 256, 256, 64, 128, 1, 1, 0, 1, False),    # dec1.up GEMM shape (plain store)
     "up2": (32, 128, 128, 128, 256, 1, 1, 0, 1, False),   # dec2.up
     "up3": (32, 64, 64, 256, 512, 1, 1, 0, 1, False),     # dec3.up
