@@ -401,6 +401,13 @@ int upr_t_retinex_bwd(const float* x, const float* illu, const float* e, const f
                       const float* g_refl, const float* g_illu, float* g_o, float* g_r, int B, int H, int W,
                       void* stream);
 
+/* multi_scale_enhance's combine with a caller-given reflectance (model.py:439-443,
+ * the head alone): e = sigmoid(o) (o NHWC [B,H,W,3]), enh = refl*e + (1-refl)*e^2
+ * (refl / enh NCHW).  Backward from g_enh: g_o NHWC, g_refl NCHW (nullable). */
+int upr_t_enhance_fwd(const float* refl, const float* o, float* e, float* enh, int B, int H, int W, void* stream);
+int upr_t_enhance_bwd(const float* e, const float* refl, const float* g_enh, float* g_o, float* g_refl, int B, int H,
+                      int W, void* stream);
+
 /* ---- TotalLoss (losses/loss.py:586-753) -------------------------------- */
 /* The loss modules' constructor arguments (reference defaults in brackets). */
 typedef struct UprLossParams {

@@ -1732,6 +1732,39 @@ __global__ void retinex_bwd_kernel(const float* __restrict__ x, const float* __r
   }
 }
 
+// multi_scale_enhance's combine with a caller-given reflectance
+// (models/model.py:439-443): e = sigmoid(o), enh = refl*e + (1-refl)*e^2; the
+// backward writes dL/do (NHWC, through the sigmoid) and dL/drefl (NCHW)
+__global__ void enhance_fwd_kernel(const float* __restrict__ refl, const float* __restrict__ o, float* __restrict__ e,
+                                   float* __restrict__ enh, int B, int HW) {
+  const long long n = (long long)B * HW;
+  GSTRIDE(i, n) {
+    const int b = (int)(i / HW), p = (int)(i - (long long)b * HW);
+    for (int c = 0; c < 3; ++c) {
+      const size_t k = ((size_t)b * 3 + c) * HW + p;
+      const float ev = 1.f / (1.f + expf(-o[i * 3 + c]));
+      const float rv = refl[k];
+      e[i * 3 + c] = ev;
+      enh[k] = rv * ev + (1.f - rv) * (ev * ev);
+    }
+  }
+}
+
+__global__ void enhance_bwd_kernel(const float* __restrict__ e, const float* __restrict__ refl,
+                                   const float* __restrict__ g_enh, float* __restrict__ g_o,
+                                   float* __restrict__ g_refl, int B, int HW) {
+  const long long n = (long long)B * HW;
+  GSTRIDE(i, n) {
+    const int b = (int)(i / HW), p = (int)(i - (long long)b * HW);
+    for (int c = 0; c < 3; ++c) {
+      const size_t k = ((size_t)b * 3 + c) * HW + p;
+      const float ev = e[i * 3 + c], rv = refl[k], ge = g_enh[k];
+      g_o[i * 3 + c] = ge * (rv + 2.f * ev * (1.f - rv)) * ev * (1.f - ev);
+      if (g_refl) g_refl[k] = ge * (ev - ev * ev);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // TotalLoss pixel terms (loss.py): workspace of fp64 accumulators
 // ---------------------------------------------------------------------------
@@ -3733,6 +3766,21 @@ int upr_t_retinex_bwd(const float* x, const float* illu, const float* e, const f
   if (!x || !illu || !e || !refl || !g_enh || !g_o || !g_r) return UPR_ERR_ARG;
   hipLaunchKernelGGL(retinex_bwd_kernel, dim3(grid_for((long long)B * H * W)), dim3(256), 0, ST(stream), x, illu, e,
                      refl, g_enh, g_refl, g_illu, g_o, g_r, B, H * W);
+  LAUNCH_CHECK();
+}
+
+int upr_t_enhance_fwd(const float* refl, const float* o, float* e, float* enh, int B, int H, int W, void* stream) {
+  if (!refl || !o || !e || !enh) return UPR_ERR_ARG;
+  hipLaunchKernelGGL(enhance_fwd_kernel, dim3(grid_for((long long)B * H * W)), dim3(256), 0, ST(stream), refl, o, e,
+                     enh, B, H * W);
+  LAUNCH_CHECK();
+}
+
+int upr_t_enhance_bwd(const float* e, const float* refl, const float* g_enh, float* g_o, float* g_refl, int B, int H,
+                      int W, void* stream) {
+  if (!e || !refl || !g_enh || !g_o) return UPR_ERR_ARG;
+  hipLaunchKernelGGL(enhance_bwd_kernel, dim3(grid_for((long long)B * H * W)), dim3(256), 0, ST(stream), e, refl,
+                     g_enh, g_o, g_refl, B, H * W);
   LAUNCH_CHECK();
 }
 

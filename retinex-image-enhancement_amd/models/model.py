@@ -223,19 +223,24 @@ class MultiScaleUP_Retinex(_HipGraphMixin, nn.Module):
     def multi_scale_enhance(self, x, reflectance, illu):
         """Enhanced image from the 3-scale FAM head of x and the given
         reflectance: R*E + (1-R)*E^2 with E = sigmoid(output_layer(fusion(...)))
-        (reference :415-443; `illu` is not read there either).  Runs the head
-        alone on the HIP kernels (UPR_MODEL_HEAD_ONLY handle).  The head has no
-        BatchNorm or Dropout, so train and eval mode compute the same values;
-        like the eval-mode forward, the result records no autograd history
-        (training gradients flow through forward()).  Inputs that require
-        grad are refused in either mode (with grad enabled) rather than
-        silently getting no gradient."""
+        (reference :415-443; `illu` is not read there either).  The head has
+        no BatchNorm or Dropout, so train and eval mode compute the same values.
+        With grad enabled and a reflectance that requires grad (or the model in
+        training mode) the call is differentiable as the reference's is: the
+        head's training graph (upr.autograd._HeadStep, fp32) returns dL/d
+        reflectance and accumulates the head parameters' gradients.  Otherwise
+        it runs on the inference kernels (UPR_MODEL_HEAD_ONLY handle) and the
+        result records no history.  x gets no gradient (as in forward()): an
+        x that requires grad is refused rather than silently detached."""
         from upr.runtime import _require_device
         _require_device(x)
         _require_device(reflectance, "reflectance")
-        if torch.is_grad_enabled() and (reflectance.requires_grad or x.requires_grad):
-            raise NotImplementedError("multi_scale_enhance: gradients through the head alone are not provided; "
-                                      "train through forward() (the full graph's backward covers the head)")
+        if torch.is_grad_enabled() and x.requires_grad:
+            raise NotImplementedError("multi_scale_enhance: no gradient w.r.t. x (the HIP head differentiates "
+                                      "w.r.t. the reflectance and the parameters); pass x.detach()")
+        if torch.is_grad_enabled() and (reflectance.requires_grad or self.training):
+            from upr.autograd import head_train_forward
+            return head_train_forward(self, x, reflectance)
         key = ("head", x.device, x.dtype)
         sig = self._signature()
         cache = self.__dict__.setdefault("_upr_cache", {})

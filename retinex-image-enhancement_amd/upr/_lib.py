@@ -191,6 +191,8 @@ SIGNATURES.update({
     "upr_t_head_fwd": (_i, [_p, _p, _p, _i, _i, _i, _p]),
     "upr_t_retinex_fwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _p]),
     "upr_t_retinex_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p]),
+    "upr_t_enhance_fwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _p]),
+    "upr_t_enhance_bwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _p]),
     "upr_t_loss_workspace": (c_size_t, [_i, _i, _i]),
     "upr_t_loss_workspace_p": (c_size_t, [_i, _i, _i, _i]),
     "upr_t_loss_pixel_p": (_i, [_p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p, _i, _f, _f, _f, _f, _f, _i, _p, _p]),

@@ -2,11 +2,13 @@
 (trainers/train.py:91-103: `model(img_low)` -> `criterion(...)` ->
 `loss.backward()` -> clip -> `optimizer.step()`).
 
-Two autograd nodes, each a whole subgraph whose forward and backward are the
+Autograd nodes, each a whole subgraph whose forward and backward are the
 HIP engines of upr/train.py and upr/loss_engine.py:
   _ModelStep  MultiScaleUP_Retinex training forward; backward = the explicit
               network backward, accumulating every parameter's gradient into
               the flat gradient buffer (the .grad views);
+  _HeadStep   multi_scale_enhance alone (caller-given reflectance);
+  _IENetStep  ResidualIENet alone;
   _LossStep   TotalLoss forward; its gradients w.r.t. (enh, illu, refl) are
               produced with the forward and scaled on the device by the
               incoming gradient in backward (GradScaler / loss weights).
@@ -74,6 +76,54 @@ def model_train_forward(model, x):
     if x.dtype != torch.float32:
         raise TypeError("UP-Retinex HIP training computes in float32; pass a float32 batch")
     return _ModelStep.apply(x.contiguous(), st["anchor"], st["graph"])
+
+
+class _HeadStep(torch.autograd.Function):
+    """MultiScaleUP_Retinex.multi_scale_enhance (models/model.py:415-443) with a
+    caller-given reflectance: forward = the head layers of the training graph
+    (scale branches, FAM, fusion, output conv) and the combine; backward =
+    their explicit backward from dL/d(enhanced): parameter gradients accumulate
+    into the .grad views, dL/d(reflectance) is returned.  No gradient w.r.t.
+    x (as the full model's node)."""
+
+    @staticmethod
+    def forward(ctx, x, refl, anchor, graph):
+        enh = graph.enhance_forward(x, refl)
+        ctx.graph, ctx.want_refl = graph, refl.requires_grad
+        return enh
+
+    @staticmethod
+    def backward(ctx, g_enh):
+        graph = ctx.graph
+        flat = graph.flat
+        if flat.attach_grads():
+            zero(flat.grad)
+        with torch.cuda.device(graph.x.device):
+            g_refl = graph.enhance_backward(g_enh.contiguous().to(torch.float32), ctx.want_refl)
+        return None, g_refl, None, None
+
+
+def head_train_forward(model, x, refl):
+    """Differentiable multi_scale_enhance on the HIP engine (fp32; H, W
+    multiples of 16).  Every call gets its own head graph (saved activations)."""
+    from .train import UPRetinexTrainGraph
+    if x.dtype != torch.float32 or refl.dtype != torch.float32:
+        raise TypeError("UP-Retinex HIP training computes in float32; pass float32 x / reflectance")
+    B, C, H, W = x.shape
+    if C != 3 or tuple(refl.shape) != (B, 3, H, W) or H % 16 or W % 16:
+        raise ValueError(f"multi_scale_enhance (differentiable): x / reflectance [B,3,H,W] with H, W multiples "
+                         f"of 16, got {tuple(x.shape)} / {tuple(refl.shape)}")
+    ps = list(model.parameters())
+    flat = getattr(ps[0], "_upr_flat", None)
+    if flat is None or any(getattr(p, "_upr_flat", None) is not flat for p in ps) or flat.flat.device != x.device:
+        flat = FlatParams(model)
+    anchor = model.__dict__.get("_upr_anchor")
+    if anchor is None or anchor.device != x.device:
+        anchor = torch.empty(0, device=x.device, requires_grad=True)
+        model.__dict__["_upr_anchor"] = anchor
+    graph = UPRetinexTrainGraph(model, head_only=True)
+    graph.flat = flat
+    return _HeadStep.apply(x.contiguous(), refl.contiguous(), anchor, graph)
 
 
 class _IENetStep(torch.autograd.Function):

@@ -1380,14 +1380,17 @@ class UPRetinexTrainGraph:
     backward.  Built once per model; buffers are reallocated per step by the
     caching allocator (torch.empty), weights re-packed per step."""
 
-    def __init__(self, model):
+    def __init__(self, model, head_only=False):
+        """head_only: the multi-scale enhancement head alone (multi_scale_enhance
+        with a caller-given reflectance, model.py:415-443), no IENet."""
         self.model = model
-        self.ie = IENetT(model.ie_net)
+        self.ie = None if head_only else IENetT(model.ie_net)
         self.s1c, self.s1f = Conv(model.scale1[0]), FAMT(model.scale1[2])
         self.s2c, self.s2f = Conv(model.scale2[1]), FAMT(model.scale2[3])
         self.s3c, self.s3f = Conv(model.scale3[1]), FAMT(model.scale3[3])
         self.fusion, self.outc = Conv(model.fusion), Conv(model.output_layer)
-        self._convs = self.ie.convs() + [self.s1c, self.s2c, self.s3c, self.fusion, self.outc] + \
+        self._convs = (self.ie.convs() if self.ie is not None else []) + \
+            [self.s1c, self.s2c, self.s3c, self.fusion, self.outc] + \
             self.s1f.convs() + self.s2f.convs() + self.s3f.convs()
 
     def pack(self):
@@ -1403,6 +1406,47 @@ class UPRetinexTrainGraph:
         self.pack()
         illu = self.ie.fwd(x)
         self.illu = illu
+        o = self._head_fwd(x)
+        self.e = empty((B, H, W, 3), dev)
+        refl = empty((B, 3, H, W), dev)
+        enh = empty((B, 3, H, W), dev)
+        _chk(lib.upr_t_retinex_fwd(_p(x), _p(illu), _fp(o.t), _p(self.e), _p(refl), _p(enh), B, H, W, st),
+             "retinex")
+        self.refl, self.enh = refl, enh
+        return enh, refl, illu
+
+    def enhance_forward(self, x, refl):
+        """Head only: x, refl [B,3,H,W] fp32 NCHW (H, W multiples of 16) -> enh."""
+        lib, st = L.lib(), _stream()
+        B, _, H, W = x.shape
+        self.x = x
+        set_amp(autocast_active())
+        self.pack()
+        o = self._head_fwd(x)
+        self.e = empty((B, H, W, 3), x.device)
+        enh = empty((B, 3, H, W), x.device)
+        _chk(lib.upr_t_enhance_fwd(_p(refl), _fp(o.t), _p(self.e), _p(enh), B, H, W, st), "enhance")
+        self.refl, self.enh = refl, enh
+        return enh
+
+    def enhance_backward(self, g_enh, want_refl):
+        """Head only: parameter gradients into the .grad views; returns dL/drefl
+        (None unless want_refl)."""
+        lib, st = L.lib(), _stream()
+        B, _, H, W = self.x.shape
+        g_o = Act.new(B, H, W, 3, self.x.device, fresh=False)
+        g_refl = empty((B, 3, H, W), self.x.device) if want_refl else None
+        _chk(lib.upr_t_enhance_bwd(_p(self.e), _p(self.refl), _p(g_enh), _fp(g_o.t), _p(g_refl), B, H, W, st),
+             "enhance_bwd")
+        self._head_bwd(g_o)
+        return g_refl
+
+    def _head_fwd(self, x):
+        """scale1/2/3 -> concat -> fusion -> output_layer (model.py:415-440): the
+        pre-sigmoid output [B,H,W,3] (Act)."""
+        lib, st = L.lib(), _stream()
+        B, _, H, W = x.shape
+        dev = x.device
         # pyramid (model.py:415-432): bilinear 0.5 / 0.25, max-pool 2 / 4
         xv = nchw_view(x)
         pyr = []
@@ -1450,15 +1494,8 @@ class UPRetinexTrainGraph:
         fused.stale32 = bool(ok16 and wm == 2)
         self.fused = fused
         self.fz = self.fusion.fwd(fused)
-        o = self.outc.fwd(self.fz)
-        self.e = empty((B, H, W, 3), dev)
-        refl = empty((B, 3, H, W), dev)
-        enh = empty((B, 3, H, W), dev)
-        _chk(lib.upr_t_retinex_fwd(_p(x), _p(illu), _fp(o.t), _p(self.e), _p(refl), _p(enh), B, H, W, st),
-             "retinex")
-        self.refl, self.enh = refl, enh
         self.f_hw = [(f2.H, f2.W), (f3.H, f3.W)]
-        return enh, refl, illu
+        return self.outc.fwd(self.fz)
 
     def backward(self, g_enh, g_refl=None, g_illu=None):
         """Accumulates every parameter gradient into the model's .grad views
@@ -1471,6 +1508,15 @@ class UPRetinexTrainGraph:
         g_r = Act.new(B, H, W, 1, dev, fresh=False)
         _chk(lib.upr_t_retinex_bwd(_p(x), _p(self.illu), _p(self.e), _p(self.refl), _p(g_enh), _p(g_refl),
                                    _p(g_illu), _fp(g_o.t), _fp(g_r.t), B, H, W, st), "retinex_bwd")
+        self._head_bwd(g_o)
+        self.ie.bwd(g_r)
+
+    def _head_bwd(self, g_o):
+        """Backward of _head_fwd from dL/d(output_layer output) (Act [B,H,W,3])."""
+        lib, st = L.lib(), _stream()
+        x = self.x
+        B, _, H, W = x.shape
+        dev = x.device
         g_fz = Act.new(B, H, W, 32, dev)
         self.outc.bwd(self.fz, g_o, g_fz)
         g_fused = Act.new(B, H, W, 96, dev)
@@ -1491,4 +1537,3 @@ class UPRetinexTrainGraph:
                 sc.bwd_relu_stem(None, g_s, s_act, x_view=(nchw_view(x), B, H, W))
             else:
                 sc.bwd_relu_stem(xin, g_s, s_act)
-        self.ie.bwd(g_r)

@@ -4,7 +4,8 @@ HIP kernels and checked against the oracle:
 * MultiScaleUP_Retinex.retinex_decompose (models/model.py:405-413) and its
   autograd (x and illumination gradients);
 * MultiScaleUP_Retinex.multi_scale_enhance (models/model.py:415-443) with a
-  caller-given reflectance (UPR_MODEL_HEAD_ONLY handle);
+  caller-given reflectance (UPR_MODEL_HEAD_ONLY handle), and its gradients
+  (reflectance + head parameters) against autograd through the oracle;
 * calculate_texture_complexity (losses/loss.py:523-583), both methods, any C;
 * ResidualIENet in training mode on its own (models/model.py:277-360);
 * TotalLoss refuses an img_low that requires grad (no silent missing gradient).
@@ -74,12 +75,11 @@ def test_multi_scale_enhance_matches_forward_and_oracle(pre, aspp):
     err = (e3.cpu() - ref).abs().max().item()
     print(f"multi_scale_enhance pre={pre} aspp={aspp}: max|d| {err:.2e}")
     assert err <= 1e-4
-    # an input that requires grad is refused in eval mode as in training mode
-    # (no silently detached result); without grad inputs the eval result has no history
-    rg = r.to(DEV).requires_grad_(True)
+    # an x that requires grad is refused in eval mode as in training mode (no
+    # silently detached result); without grad inputs the eval result has no history
     for train in (False, True):
-        with pytest.raises(NotImplementedError, match="gradients"):
-            model.train(train).multi_scale_enhance(x.to(DEV), rg, None)
+        with pytest.raises(NotImplementedError, match="w.r.t. x"):
+            model.train(train).multi_scale_enhance(x.to(DEV).requires_grad_(True), r.to(DEV), None)
     e4 = model.eval().multi_scale_enhance(x.to(DEV), r.to(DEV), None)
     assert not e4.requires_grad and torch.equal(e4, e3)
     # float16 model
@@ -88,6 +88,47 @@ def test_multi_scale_enhance_matches_forward_and_oracle(pre, aspp):
         e16 = m16.multi_scale_enhance(x.half().to(DEV), r.half().to(DEV), None)
     assert e16.dtype == torch.float16
     assert (e16.float().cpu() - ref).abs().max().item() <= 1e-2
+
+
+@pytest.mark.parametrize("train", [False, True])
+def test_multi_scale_enhance_gradients(train):
+    """multi_scale_enhance on its own is differentiable as the reference's
+    (models/model.py:415-443): dL/d reflectance and the head parameters'
+    gradients (scale1/2/3, fusion, output_layer) against autograd through the
+    fp64 oracle (oracle/net.py multi_scale_enhance); fp32 engine, max|d| <=
+    1e-4 * max|ref| + 1e-7 (measured: 1e-6 * max|ref| at worst)."""
+    model = _model(False, True, seed=5)
+    sd = {k: v.clone().double() for k, v in model.state_dict().items()}
+    model = model.to(DEV).train(train)
+    gen = torch.Generator().manual_seed(6)
+    x = torch.rand(2, 3, 64, 48, generator=gen)
+    r = torch.rand(2, 3, 64, 48, generator=gen) * 2.0
+    g = torch.randn(2, 3, 64, 48, generator=gen)
+    rd = r.to(DEV).requires_grad_(True)
+    model.zero_grad(set_to_none=True)
+    enh = model.multi_scale_enhance(x.to(DEV), rd, None)
+    assert enh.requires_grad and enh.dtype == torch.float32
+    (enh * g.to(DEV)).sum().backward()
+    head = [k for k, _ in model.named_parameters() if not k.startswith("ie_net.")]
+    for k in head:
+        sd[k].requires_grad_(True)
+    r64 = r.double().requires_grad_(True)
+    ref = onet.multi_scale_enhance(sd, x.double(), r64)
+    (ref * g.double()).sum().backward()
+    assert _maxrel(enh, ref) <= 1e-5
+    worst = []
+    for name, a, b in [("reflectance", rd.grad, r64.grad)] + \
+            [(k, dict(model.named_parameters())[k].grad, sd[k].grad) for k in head]:
+        assert a is not None, name
+        err = (a.detach().double().cpu() - b).abs().max().item()
+        tol = 1e-4 * b.abs().max().item() + 1e-7
+        worst.append((err / max(tol, 1e-30), name))
+        assert err <= tol, f"{name}: max|d| {err:.3e} > {tol:.3e}"
+    print("multi_scale_enhance grads: worst err/tol %.3f (%s)" % max(worst))
+    # the IENet parameters get no gradient from the head alone
+    for k, p in model.named_parameters():
+        if k.startswith("ie_net.") and p.grad is not None:
+            assert float(p.grad.abs().max()) == 0.0, k
 
 
 @pytest.mark.parametrize("method", ["tv", "edge_density"])
