@@ -642,40 +642,87 @@ __device__ __forceinline__ float ms_feat(const float (&P)[3][PH][PW], int R, int
   return fsum;
 }
 
-// the features of the 4 pixels (R, C .. C + 3) (C 16-byte aligned), summed in
-// fp64 as ms_feat's per-pixel floats: interior quads read 16-byte rows (center,
-// above, below) and the two side neighbours -- 5 LDS reads per channel for 4
-// pixels instead of 5 per pixel; quads at an image border take ms_feat
-template <int PH, int PW>
-__device__ __forceinline__ double ms_feat4(const float (&P)[3][PH][PW], int R, int C, int y, int x, int hs, int ws) {
-  if (x < 1 || x + 4 > ws - 1 || y < 1 || y > hs - 2) {
-    double a = 0.0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (x + k < ws) a += (double)ms_feat(P, R, C + k, y, x + k, hs, ws);
-    return a;
-  }
+// the features of the 4 pixels (R, C .. C + 3) (C 16-byte aligned) of image
+// row y, columns x .. x + 3, summed in fp64 as ms_feat's per-pixel floats
+// (same expression, same order: bit-identical to ms_feat on every pixel).
+// Every lane of the wave calls it (DPP below): lanes whose quad lies outside
+// the hs x ws image contribute 0, as do the pixels of a quad past ws.  A
+// lane's quads sit along a DPP row of 16 lanes: the left / right neighbour
+// columns come from the adjacent lanes' quads (row_shr / row_shl by 1) and
+// only a row's first / last lane (first / last) reads them from LDS -- the
+// stride-4 single-float LDS reads were 4-way bank conflicts on every lane.
+// Image borders: a missing neighbour is replaced by the centre pixel and the
+// difference is not halved (torch.gradient's one-sided edge difference).
+__device__ __forceinline__ float dpp_from_left(float v) {  // lane i <- lane i - 1 within its row of 16
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x111, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float dpp_from_right(float v) {  // lane i <- lane i + 1 within its row of 16
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x101, 0xF, 0xF, false));
+}
+
+// EDGE false: the caller's block holds no image border (block-uniform), so
+// none of the border selects are needed
+template <bool EDGE, int PH, int PW>
+__device__ __forceinline__ double ms_quad(const float (&P)[3][PH][PW], int R, int C, int y, int x, int hs, int ws,
+                                          bool first, bool last) {
+  const bool top = EDGE && y == 0, bot = EDGE && y >= hs - 1;  // (hs < 2: both)
+  const float sy = top || bot ? 1.f : 0.5f;
   float fs[4] = {0.f, 0.f, 0.f, 0.f}, c3[3][4];
 #pragma unroll
   for (int ch = 0; ch < 3; ++ch) {
     const float4 ce = *(const float4*)&P[ch][R][C];
-    const float4 up = *(const float4*)&P[ch][R - 1][C];
-    const float4 dn = *(const float4*)&P[ch][R + 1][C];
-    const float l = P[ch][R][C - 1], r = P[ch][R][C + 4];
+    float4 up = *(const float4*)&P[ch][R - 1][C];
+    float4 dn = *(const float4*)&P[ch][R + 1][C];
+    float l = dpp_from_left(ce.w), r = dpp_from_right(ce.x);
+    if (first) l = P[ch][R][C - 1];
+    if (last) r = P[ch][R][C + 4];
+    if (top) up = ce;
+    if (bot) dn = ce;
     const float v[6] = {l, ce.x, ce.y, ce.z, ce.w, r};
     const float u[4] = {up.x, up.y, up.z, up.w}, d[4] = {dn.x, dn.y, dn.z, dn.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const float gx = (v[k + 2] - v[k]) / 2.f;
-      const float gy = (d[k] - u[k]) / 2.f;
+      const bool lft = EDGE && x + k == 0, rgt = EDGE && x + k >= ws - 1;
+      const float a = lft ? v[k + 1] : v[k], b = rgt ? v[k + 1] : v[k + 2];
+      const float gx = (b - a) * (lft || rgt ? 1.f : 0.5f);
+      const float gy = (d[k] - u[k]) * sy;
       fs[k] += v[k + 1] + __builtin_amdgcn_sqrtf(gx * gx + gy * gy);
       c3[ch][k] = v[k + 1];
     }
   }
   double a = 0.0;
+  if (!EDGE || y < hs) {
 #pragma unroll
-  for (int k = 0; k < 4; ++k) a += (double)(fs[k] + (0.299f * c3[0][k] + 0.587f * c3[1][k] + 0.114f * c3[2][k]));
+    for (int k = 0; k < 4; ++k)
+      if (!EDGE || x + k < ws) a += (double)(fs[k] + (0.299f * c3[0][k] + 0.587f * c3[1][k] + 0.114f * c3[2][k]));
+  }
   return a;
+}
+
+// the block's feature quads: 512 of the full tile (2 per thread), 128 half
+// (threads 0-127), 32 quarter (128-159)
+template <bool E>
+__device__ __forceinline__ void ms_tile_quads(const float (&full)[3][M3_RH][M3_RW], const float (&s1)[3][M3_H1][M3_P1],
+                                              const float (&s2)[3][M3_H2][M3_P2], int t, int ty0, int tx0, int H,
+                                              int W, double& a0, double& a1, double& a2) {
+  a0 = 0.0;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int i = t + 256 * k, r = i >> 4, q = i & 15;
+    a0 += ms_quad<E>(full, r + M3_HALO, 4 * q + M3_HALO, ty0 + r, tx0 + 4 * q, H, W, q == 0, q == 15);
+  }
+  // (one value selected afterwards: assigning a1 / a2 inside the branches
+  // became a dynamically indexed scratch pair)
+  double ah = 0.0;
+  if (t < 128) {  // (waves 0, 1: whole)
+    const int r = t >> 3, q = t & 7;
+    ah = ms_quad<E>(s1, r + 1, 4 * q + 4, ty0 / 2 + r, tx0 / 2 + 4 * q, H / 2, W / 2, q == 0, q == 7);
+  } else if (t < 160) {  // (lanes 0-31 of wave 2: two whole DPP rows)
+    const int r = (t - 128) >> 2, q = (t - 128) & 3;
+    ah = ms_quad<E>(s2, r + 1, 4 * q + 4, ty0 / 4 + r, tx0 / 4 + 4 * q, H / 4, W / 4, q == 0, q == 3);
+  }
+  a1 = t < 128 ? ah : 0.0;
+  a2 = t < 128 ? 0.0 : ah;
 }
 
 __device__ __forceinline__ double ms_factor(const double* sums, int b, double n0, double n1, double n2);
@@ -703,68 +750,74 @@ __global__ __launch_bounds__(256) void ms_sums3_kernel(const T* __restrict__ x, 
   // flight per thread: one HBM round trip per block, not one per quad).  (A
   // persistent form loading tile j + 1 under tile j's work measured no faster:
   // 0.074 vs 0.071 ms)
-  constexpr int QPR = M3_RW / 4, QPC = M3_RH * QPR, NLD = (3 * QPC + 255) / 256;
-  float v[NLD][4];
+  // thread (lr, lq) = quad lq of region rows lr + 14 k (k < 3 covers the 40
+  // rows), all three channels: the 9 loads' offsets are compile-time steps
+  // from one base (the per-quad division / modulo of a flat index was a fifth
+  // of this pass's VALU work)
+  constexpr int QPR = M3_RW / 4, LR = 256 / QPR, NK = (M3_RH + LR - 1) / LR;
+  const int lr = t / QPR, lq = t - lr * QPR;
+  const bool lact = t < LR * QPR;
+  const int xs = tx0 - M3_HALO + 4 * lq, ys0 = ty0 - M3_HALO + lr;
+  const bool xok = lact && (unsigned)xs < (unsigned)W;
+  float v[3][NK][4];
 #pragma unroll
-  for (int k = 0; k < NLD; ++k) {
-    const int i = t + 256 * k;
-    const int ch = i / QPC, rq = i - ch * QPC, r = rq / QPR, q = rq - r * QPR;
-    const int ys = ty0 - M3_HALO + r, xs = tx0 - M3_HALO + 4 * q;
-    v[k][0] = v[k][1] = v[k][2] = v[k][3] = 0.f;
-    if (i < 3 * QPC && (unsigned)ys < (unsigned)H && (unsigned)xs < (unsigned)W)
-      Vec4<T>::load(img + ch * HW + (size_t)ys * W + xs, v[k]);
+  for (int k = 0; k < NK; ++k) {
+    const int ys = ys0 + LR * k;
+    const bool ok = xok && lr + LR * k < M3_RH && (unsigned)ys < (unsigned)H;
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      v[ch][k][0] = v[ch][k][1] = v[ch][k][2] = v[ch][k][3] = 0.f;
+      if (ok) Vec4<T>::load(img + ch * HW + (size_t)ys * W + xs, v[ch][k]);
+    }
   }
 #pragma unroll
-  for (int k = 0; k < NLD; ++k) {
-    const int i = t + 256 * k;
-    const int ch = i / QPC, rq = i - ch * QPC, r = rq / QPR, q = rq - r * QPR;
-    if (i < 3 * QPC) *(float4*)&full[ch][r][4 * q] = make_float4(v[k][0], v[k][1], v[k][2], v[k][3]);
+  for (int k = 0; k < NK; ++k) {
+    if (lact && lr + LR * k < M3_RH) {
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch)
+        *(float4*)&full[ch][lr + LR * k][4 * lq] = make_float4(v[ch][k][0], v[ch][k][1], v[ch][k][2], v[ch][k][3]);
+    }
   }
   __syncthreads();
   const int h1 = H / 2, w1 = W / 2, h2 = H / 4, w2 = W / 4;
   // half / quarter samples with their 1-sample halos (LDS rows of sample r:
   // 2r + 2, 2r + 3 / 4r + 1, 4r + 2 of the region, by the halo of 4); sample
-  // column c at plane column c + 3
-  for (int i = t; i < M3_H1 * M3_W1 + M3_H2 * M3_W2; i += 256) {
-    if (i < M3_H1 * M3_W1) {
-      const int r = i / M3_W1, c = i - r * M3_W1;
-      const int ys = ty0 / 2 - 1 + r, xs = tx0 / 2 - 1 + c;
-      if ((unsigned)ys < (unsigned)h1 && (unsigned)xs < (unsigned)w1) {
+  // column c at plane column c + 3.  Half: thread (r0, c) = (t / 34, t % 34)
+  // takes rows r0 + 7 j (j < 3); quarter: threads 238.. and a second pass
+  {
+    constexpr int R1 = 256 / M3_W1;  // 7 half rows per pass
+    const int r0 = t / M3_W1, c = t - r0 * M3_W1;
+    const int xs1 = tx0 / 2 - 1 + c;
+    if (t < R1 * M3_W1 && (unsigned)xs1 < (unsigned)w1) {
 #pragma unroll
-        for (int ch = 0; ch < 3; ++ch)
-          s1[ch][r][c + 3] = blend_half(full[ch][2 * r + 2][2 * c + 2], full[ch][2 * r + 2][2 * c + 3],
-                                        full[ch][2 * r + 3][2 * c + 2], full[ch][2 * r + 3][2 * c + 3]);
-      }
-    } else {
-      const int j = i - M3_H1 * M3_W1;
-      const int r = j / M3_W2, c = j - r * M3_W2;
-      const int ys = ty0 / 4 - 1 + r, xs = tx0 / 4 - 1 + c;
-      if ((unsigned)ys < (unsigned)h2 && (unsigned)xs < (unsigned)w2) {
+      for (int j = 0; j < (M3_H1 + R1 - 1) / R1; ++j) {
+        const int r = r0 + R1 * j, ys = ty0 / 2 - 1 + r;
+        if (r < M3_H1 && (unsigned)ys < (unsigned)h1) {
 #pragma unroll
-        for (int ch = 0; ch < 3; ++ch)
-          s2[ch][r][c + 3] = blend_half(full[ch][4 * r + 1][4 * c + 1], full[ch][4 * r + 1][4 * c + 2],
-                                        full[ch][4 * r + 2][4 * c + 1], full[ch][4 * r + 2][4 * c + 2]);
+          for (int ch = 0; ch < 3; ++ch)
+            s1[ch][r][c + 3] = blend_half(full[ch][2 * r + 2][2 * c + 2], full[ch][2 * r + 2][2 * c + 3],
+                                          full[ch][2 * r + 3][2 * c + 2], full[ch][2 * r + 3][2 * c + 3]);
+        }
       }
+    }
+    // quarter: 10 x 18 samples over threads 0..179
+    const int r2 = t / M3_W2, c2 = t - r2 * M3_W2;
+    const int ys2 = ty0 / 4 - 1 + r2, xs2 = tx0 / 4 - 1 + c2;
+    if (t < M3_H2 * M3_W2 && (unsigned)ys2 < (unsigned)h2 && (unsigned)xs2 < (unsigned)w2) {
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch)
+        s2[ch][r2][c2 + 3] = blend_half(full[ch][4 * r2 + 1][4 * c2 + 1], full[ch][4 * r2 + 1][4 * c2 + 2],
+                                        full[ch][4 * r2 + 2][4 * c2 + 1], full[ch][4 * r2 + 2][4 * c2 + 2]);
     }
   }
   __syncthreads();
-  // quads: 512 of the full tile (2 per thread), 128 half (threads 0-127), 32 quarter (128-159)
-  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int i = t + 256 * k, r = i >> 4, q = i & 15;
-    const int y = ty0 + r, xx = tx0 + 4 * q;
-    if (y < H && xx < W) a0 += ms_feat4(full, r + M3_HALO, 4 * q + M3_HALO, y, xx, H, W);
-  }
-  if (t < 128) {
-    const int r = t >> 3, q = t & 7;
-    const int y = ty0 / 2 + r, xx = tx0 / 2 + 4 * q;
-    if (y < h1 && xx < w1) a1 += ms_feat4(s1, r + 1, 4 * q + 4, y, xx, h1, w1);
-  } else if (t < 160) {
-    const int r = (t - 128) >> 2, q = (t - 128) & 3;
-    const int y = ty0 / 4 + r, xx = tx0 / 4 + 4 * q;
-    if (y < h2 && xx < w2) a2 += ms_feat4(s2, r + 1, 4 * q + 4, y, xx, h2, w2);
-  }
+  double a0, a1, a2;
+  // a tile touching no image border (at any of the three scales: the half /
+  // quarter tiles' borders are the full tile's) takes the select-free form
+  if (ty0 == 0 || tx0 == 0 || ty0 + M3_TH >= H || tx0 + M3_TW >= W)
+    ms_tile_quads<true>(full, s1, s2, t, ty0, tx0, H, W, a0, a1, a2);
+  else
+    ms_tile_quads<false>(full, s1, s2, t, ty0, tx0, H, W, a0, a1, a2);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     a0 += __shfl_xor(a0, o, 64);
