@@ -212,20 +212,32 @@ __device__ __forceinline__ void rgb2lab_lds(const uint16_t* gam, const uint16_t*
   Bb = sat_u8(descale(200 * (fY - fZ) + 128 * (1 << 15), 15));
 }
 
-// Lab2RGBinteger on LDS copies of the Y / inverse-gamma tables
-__device__ __forceinline__ void lab2rgb_lds(const uint16_t* yf, const uint16_t* ig, const int* c, int L, int A, int Bb,
-                                            int& R, int& G, int& B) {
+// Lab2RGBinteger on LDS copies of the Y / inverse-gamma tables; igf holds the
+// inverse-gamma byte already divided by 255 (__fdiv_rn(ig, 255): the output's
+// /255, one lookup instead of two), yf2 the (y, ify) pair of L as one word
+__device__ __forceinline__ int ab_to_xz_dev(int v) {
+  // lab_tables.h ab_to_xz: the cube branch has v > 3390 > 0, so its signed
+  // divisions by 2^14 are shifts (unsigned: no sign fix-ups)
   const int BASE = 1 << 14;
-  const int y = yf[L * 2], ify = yf[L * 2 + 1];
+  if (v <= 3390) return v * 108 / 841 - BASE * 16 / 116 * 108 / 841;
+  const unsigned u = (unsigned)v;
+  return (int)((((u * u) >> 14) * u) >> 14);
+}
+
+__device__ __forceinline__ void lab2rgb_lds(const uint32_t* yf2, const float* igf, const int* c, int L, int A, int Bb,
+                                            float& R, float& G, float& B) {
+  const int BASE = 1 << 14;
+  const uint32_t yw = yf2[L];
+  const int y = (int)(yw & 0xffffu), ify = (int)(yw >> 16);
   const int adiv = ((5 * A * 53687 + (1 << 7)) >> 13) - 128 * BASE / 500;
   const int bdiv = ((Bb * 41943 + (1 << 4)) >> 9) - 128 * BASE / 200 + 1;
-  const int x = ab_to_xz(ify + adiv);
-  const int z = ab_to_xz(ify - bdiv);
+  const int x = ab_to_xz_dev(ify + adiv);
+  const int z = ab_to_xz_dev(ify - bdiv);
   int r = descale(c[0] * x + c[1] * y + c[2] * z, 14);
   int g = descale(c[3] * x + c[4] * y + c[5] * z, 14);
   int b = descale(c[6] * x + c[7] * y + c[8] * z, 14);
   r = max(0, min(4095, r)); g = max(0, min(4095, g)); b = max(0, min(4095, b));
-  R = ig[r]; G = ig[g]; B = ig[b];
+  R = igf[r]; G = igf[g]; B = igf[b];
 }
 
 // SRC 0: T RGB planes [B,3,H,W] -> L / A / B planes; SRC 1: u8 plane [B,H,W] (src = L)
@@ -314,6 +326,8 @@ __global__ __launch_bounds__(256) void clahe_hist_kernel(const void* __restrict_
     if (col >= TWV) { col -= TWV; ++row; }
   }
   __syncthreads();
+  // (16 sub-histograms, 4 per wave by lane % 4 on padded rows, measured
+  // slower: 27.1 -> 30.4 us, profiles/r5_ms_sums3_v2.txt)
   const int h = hist[0][t] + hist[1][t] + hist[2][t] + hist[3][t];
   const size_t tb = (size_t)b * g.tilesX * g.tilesY + tile;
   if (g.S > 1) {
@@ -341,10 +355,9 @@ __global__ __launch_bounds__(256) void clahe_apply_kernel(const uint8_t* __restr
                                                           const DevLab* __restrict__ tab, void* __restrict__ out,
                                                           ClaheArgs g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
-  __shared__ float inv255[256];            // __fdiv_rn(i, 255): the /255 of the output, looked up
-  uint16_t* yf = (uint16_t*)sm;            // 512
-  uint16_t* ig = yf + 512;                 // 4096
-  uint8_t* lrows = (uint8_t*)(ig + 4096);  // <= 3 tile rows of LUTs
+  float* igf = (float*)sm;                  // 4096: __fdiv_rn(invgamma_b[i], 255)
+  uint32_t* yf2 = (uint32_t*)(igf + 4096);  // 256: (y, ify) of L
+  uint8_t* lrows = (uint8_t*)(yf2 + 256);   // <= 3 tile rows of LUTs
   const int t = threadIdx.x;
   const int b = blockIdx.y;
   const int H = g.H, W = g.W;
@@ -361,9 +374,8 @@ __global__ __launch_bounds__(256) void clahe_apply_kernel(const uint8_t* __restr
   for (int i = t * 16; i < lbytes; i += 256 * 16) *(uint4*)(lrows + i) = *(const uint4*)(lsrc + i);
   int c[9];
   if constexpr (DST == 0) {
-    for (int i = t; i < 512; i += 256) yf[i] = tab->yf_b[i];
-    for (int i = t; i < 4096; i += 256) ig[i] = tab->invgamma_b[i];
-    inv255[t] = __fdiv_rn((float)t, 255.f);
+    yf2[t] = (uint32_t)tab->yf_b[2 * t] | (uint32_t)tab->yf_b[2 * t + 1] << 16;
+    for (int i = t; i < 4096; i += 256) igf[i] = __fdiv_rn((float)tab->invgamma_b[i], 255.f);
 #pragma unroll
     for (int k = 0; k < 9; ++k) c[k] = tab->xyz2rgb[k];
   }
@@ -433,13 +445,7 @@ __global__ __launch_bounds__(256) void clahe_apply_kernel(const uint8_t* __restr
     } else {
       float R[V], G[V], Bo[V];
 #pragma unroll
-      for (int k = 0; k < V; ++k) {
-        int r8, g8, b8;
-        lab2rgb_lds(yf, ig, c, lc[k], Av[k], Bv[k], r8, g8, b8);
-        R[k] = inv255[r8];
-        G[k] = inv255[g8];
-        Bo[k] = inv255[b8];
-      }
+      for (int k = 0; k < V; ++k) lab2rgb_lds(yf2, igf, c, lc[k], Av[k], Bv[k], R[k], G[k], Bo[k]);
       T* o = (T*)out + (size_t)b * 3 * HW + (size_t)y * W + col * V;
       if constexpr (V == 4) {
         Vec4<T>::store(o, R);
@@ -940,7 +946,7 @@ static ClaheArgs clahe_args(int B, int H, int W, float clipLimit, int tilesX, in
   return g;
 }
 
-static size_t clahe_apply_lds(const ClaheArgs& g) { return (512 + 4096) * 2 + (size_t)3 * g.tilesX * 256; }
+static size_t clahe_apply_lds(const ClaheArgs& g) { return 4096 * 4 + 256 * 4 + (size_t)3 * g.tilesX * 256; }
 
 // the three launches; src: T RGB planes (SRC 0) or a u8 plane (SRC 1, then L = src)
 template <int SRC, typename T>
