@@ -1,4 +1,5 @@
 # retinex tail A/B on one box: kernel stats of the fp16 preact+ASPP and fp32 forwards, 4-pixel form vs UPR_TAIL4=0
+# (the UPR_TAIL4 switch and the 4-pixel kernel were removed after this A/B: profiles/r5_retinex_tail_ab.txt)
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 out=gpurun_out/${CK:-r5tailab}
 mkdir -p $out
