@@ -295,15 +295,107 @@ __global__ __launch_bounds__(256) void conv_s2dg_kernel(ConvOp op, int ngroups) 
   }
 }
 
-// the 3x3 stride-2 input gradient above (op: dy as a 1-segment 3x3 op over
-// Hin x Win with the flipped filter, out32 family at 2 Hin x 2 Win); 64 -> 32
-// channels only (the filter must fit the registers)
+// The same phase decomposition for wider convs (enc2.conv1: 128 -> 64 and
+// enc3.conv1: 256 -> 128 input gradients; their filters do not fit the
+// registers): a block owns an NC-channel slice of the output (grid.y), its
+// flipped filter slice sits in LDS as per-lane 16-byte fragments
+// [tap][nt][ks][lane], and a wave walks 16-pixel groups of dy rows, loading
+// the four shifted runs of one 32-channel chunk at a time and issuing every
+// phase's taps on it (accumulators of all four phases live together).  One
+// fragment read per MFMA; dy is read once per slice.  (Those shapes zero-
+// upsampled dy and ran the stride-1 conv over it: 4x the MFMAs and the
+// upsampled tensor's traffic, 17x the shape's bound.)
+template <int KC, int NC>
+__global__ __launch_bounds__(256, 2) void conv_s2dg_lds_kernel(ConvOp op, int ngroups) {
+  constexpr int KS = KC / 32, NT = NC / 16, NFRAG = 9 * NT * KS;
+  extern __shared__ __attribute__((aligned(16))) unsigned char s2smem[];
+  pwh8* wl = (pwh8*)s2smem;  // [9][NT][KS][64]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int fr = lane & 15, fg = lane >> 4;
+  const ConvSeg& sg = op.seg[0];
+  const half_t* src = (const half_t*)sg.src;
+  const int Hin = sg.Hin, Win = sg.Win, HWin = Hin * Win;
+  const int nbase = blockIdx.y * NC;
+  for (int f = threadIdx.x; f < NFRAG * 64; f += 256) {
+    const int ln = f & 63, rest = f >> 6;
+    const int ks = rest % KS, nt = (rest / KS) % NT, t = rest / (KS * NT);
+    wl[f] = *(const pwh8*)((const half_t*)op.W + (size_t)(nbase + nt * 16 + (ln & 15)) * op.Kpad + t * KC + ks * 32 +
+                           (ln >> 4) * 8);
+  }
+  __syncthreads();
+  const int stride = gridDim.x * 4;
+  for (int g = blockIdx.x * 4 + wave; g < ngroups; g += stride) {
+    const int q0 = g * 16;
+    const int b = q0 / HWin, rem = q0 - b * HWin, i = rem / Win, j = rem - i * Win + fr;
+    pwf4 acc[4][NT];
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[ph][nt] = pwf4{0.f, 0.f, 0.f, 0.f};
+    // (two chunks per pass: a fully unrolled chunk loop hoisted every chunk's loads and spilled)
+#pragma unroll 2
+    for (int ks = 0; ks < KS; ++ks) {
+      pwh8 x[4];  // (di, dj) = (0,0), (0,1), (1,0), (1,1)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int ii = i + (s >> 1), jj = j + (s & 1);
+        const bool in = ii < Hin && jj < Win;
+        x[s] = in ? *(const pwh8*)(src + ((size_t)(b * Hin + ii) * Win + jj) * sg.cs + ks * 32 + fg * 8) : pwh8{};
+      }
+#pragma unroll
+      for (int ph = 0; ph < 4; ++ph) {
+        const int py = ph >> 1, px = ph & 1;
+#pragma unroll
+        for (int a = 0; a < 1 + py; ++a) {
+          const int ty = py ? 2 * a : 1;
+#pragma unroll
+          for (int c = 0; c < 1 + px; ++c) {
+            const int tx = px ? 2 * c : 1;
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+              acc[ph][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[(((ty * 3 + tx) * NT + nt) * KS + ks) * 64 + lane],
+                                                                   x[a * 2 + c], acc[ph][nt], 0, 0, 0);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) {
+      const int py = ph >> 1, px = ph & 1;
+      const size_t m = (size_t)(b * 2 * Hin + 2 * i + py) * (2 * Win) + 2 * j + px;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int n = nbase + nt * 16 + fg * 4;
+        pwf4 t;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) t[r] = (float)(half_t)acc[ph][nt][r];
+        if (op.res32) t += *(const pwf4*)(op.res32 + m * op.res32_cs + n);
+        if (op.mask16) {
+          const pwh4 mk = *(const pwh4*)((const half_t*)op.mask16 + m * op.mask16_cs + n);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) t[r] = (float)mk[r] > 0.f ? t[r] : 0.f;
+        }
+        if (!op.skip32) *(pwf4*)(op.out32 + m * op.out32_cs + op.out32_coff + n) = t;
+        if (op.out32_h16)
+          *(pwh4*)((half_t*)op.out32_h16 + m * op.out32_h16_cs + n) =
+              pwh4{(half_t)t[0], (half_t)t[1], (half_t)t[2], (half_t)t[3]};
+      }
+    }
+  }
+}
+
+// the 3x3 stride-2 input gradients above (op: dy as a 1-segment 3x3 op over
+// Hin x Win with the flipped filter, out32 family at 2 Hin x 2 Win): 64 -> 32
+// with the filter in registers, 128 -> 64 and 256 -> 128 with LDS filter slices
 int launch_conv_s2dg(const ConvOp& op, hipStream_t st, bool probe) {
   const ConvSeg& s = op.seg[0];
   if (op.nseg != 1 || op.store != kStoreNHWC || !op.out32 || op.bias || op.relu || op.res1 || op.res2 || op.pool ||
       op.img_bias || op.scale || op.out2)
     return kErrUnsupported;
-  if (s.kh != 3 || s.kw != 3 || s.C != 64 || op.N != 32 || s.kbase != 0 || s.pre != kPreNone) return kErrUnsupported;
+  // (C, N): 64 -> 32 register-filter kernel; 128 -> 64 and 256 -> 128 LDS-filter kernel
+  const int form = s.C == 64 && op.N == 32 ? 1 : s.C == 128 && op.N == 64 ? 2 : s.C == 256 && op.N == 128 ? 3 : 0;
+  if (s.kh != 3 || s.kw != 3 || !form || s.kbase != 0 || s.pre != kPreNone) return kErrUnsupported;
   if (s.cs % 8 || (uintptr_t)s.src % 16 || op.Kpad % 8 || (uintptr_t)op.W % 16 || s.Win % 16) return kErrUnsupported;
   if ((uintptr_t)op.out32 % 16 || op.out32_cs % 4 || op.out32_coff % 4) return kErrUnsupported;
   if (op.res32 && ((uintptr_t)op.res32 % 16 || op.res32_cs % 4)) return kErrUnsupported;
@@ -320,7 +412,26 @@ int launch_conv_s2dg(const ConvOp& op, hipStream_t st, bool probe) {
   }
   int grid = std::min(cus * 2, (ngroups + 3) / 4);
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL((conv_s2dg_kernel<64, 32>), dim3(grid), dim3(256), 0, st, op, ngroups);
+  if (form == 1) {
+    hipLaunchKernelGGL((conv_s2dg_kernel<64, 32>), dim3(grid), dim3(256), 0, st, op, ngroups);
+  } else {
+    // LDS filter slices (73.7 KB each: two blocks per CU); the slices split the CUs
+    auto go = [&](auto kern, int nc, int kc) {
+      const size_t lds = (size_t)9 * nc * kc * 2;
+      static bool attr[4] = {false, false, false, false};
+      if (!attr[form]) {
+        const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return (int)e;
+        attr[form] = true;
+      }
+      const int slices = op.N / nc;
+      const int gx = std::max(1, std::min((cus * 2 + slices - 1) / slices, (ngroups + 3) / 4));
+      hipLaunchKernelGGL(kern, dim3(gx, slices), dim3(256), lds, st, op, ngroups);
+      return 0;
+    };
+    const int rc = form == 2 ? go(conv_s2dg_lds_kernel<128, 32>, 32, 128) : go(conv_s2dg_lds_kernel<256, 16>, 16, 256);
+    if (rc != 0) return rc;
+  }
   return (int)hipGetLastError();
 }
 

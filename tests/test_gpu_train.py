@@ -610,16 +610,19 @@ def test_dgrad_1x1_stride2_scatter(cin, cout):
                                  None, 0, 0, gx.data_ptr(), cin, 0, 8, x16.data_ptr(), 0, y16.data_ptr(), 0, st) != 0
 
 
+@pytest.mark.parametrize("cin,cout", [(32, 64), (64, 128), (128, 256)])
 @pytest.mark.parametrize("acc,keep16", [(False, False), (True, False), (False, True)])
-def test_dgrad_3x3_stride2_phases(acc, keep16):
-    """enc1.conv1's input gradient (3x3 stride 2 pad 1, 32 -> 64, model.py:100-178)
-    from dy itself (upr_t_conv_mfma16 store | 16: the four output phases as small
-    convs, no zero-upsampled operand) vs torch's conv2d_input on the fp16-rounded
-    operands: overwrite, accumulate into an existing gradient, and the fp16-only
-    form (store | 2 | 4: y16 = (half) dx, dx itself not written)."""
+def test_dgrad_3x3_stride2_phases(acc, keep16, cin, cout):
+    """The encoders' stride-2 input gradients (3x3 stride 2 pad 1; enc1 / enc2 /
+    enc3.conv1: 32 -> 64, 64 -> 128, 128 -> 256, model.py:100-178) from dy itself
+    (upr_t_conv_mfma16 store | 16: the four output phases as small convs, no
+    zero-upsampled operand; register filter for the first, LDS filter slices
+    for the others) vs torch's conv2d_input on the fp16-rounded operands:
+    overwrite, accumulate into an existing gradient, and the fp16-only form
+    (store | 2 | 4: y16 = (half) dx, dx itself not written)."""
     from upr import _lib as L
-    gen = torch.Generator().manual_seed(11 + int(acc) + 2 * int(keep16))
-    cin, cout, B, Ho, Wo = 32, 64, 2, 16, 48
+    gen = torch.Generator().manual_seed(11 + int(acc) + 2 * int(keep16) + cin)
+    B, Ho, Wo = 2, 16, 48
     w = torch.randn(cout, cin, 3, 3, generator=gen) * 0.1
     dy = torch.randn(B, cout, Ho, Wo, generator=gen)
     base = torch.randn(B, 2 * Ho, 2 * Wo, cin, generator=gen)
