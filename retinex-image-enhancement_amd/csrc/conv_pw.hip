@@ -412,6 +412,8 @@ int launch_conv_s2dg(const ConvOp& op, hipStream_t st, bool probe) {
   }
   int grid = std::min(cus * 2, (ngroups + 3) / 4);
   if (grid < 1) grid = 1;
+  // (64 -> 32 as an LDS-filter slice measured slower than the register-filter kernel: 141.6 vs
+  // 133.3 us, profiles/r5_s2dgrad_lds_ab.txt)
   if (form == 1) {
     hipLaunchKernelGGL((conv_s2dg_kernel<64, 32>), dim3(grid), dim3(256), 0, st, op, ngroups);
   } else {
