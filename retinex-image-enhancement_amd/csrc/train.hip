@@ -3378,21 +3378,36 @@ __global__ __launch_bounds__(256) void maxpool_gather4_kernel(const unsigned* __
   const int iy = r % H, b = r / H;
   float* dp = O16 ? nullptr : dx + b * xsb + iy * xsh + ix * xsw + c;
   float4 acc = !O16 && accumulate ? *(const float4*)dp : make_float4(0.f, 0.f, 0.f, 0.f);
+  // every window's code word and gradient run is loaded first (independent
+  // loads, one round trip each; a window outside the output reads nothing and
+  // gets the no-hit code 0xffffffff), then the hits are added in the same
+  // window order as before (the 3x3 pool's code -> dy -> next window chain
+  // was 18 dependent round trips per thread: 1.6 TB/s at 512^2)
+  unsigned wv[K * K];
+  float4 gv[K * K];
 #pragma unroll
   for (int t = 0; t < K; ++t) {
     const int ky = K - 1 - t, ny = iy + P - ky;  // oy * S
-    if (ny < 0 || ny % S != 0 || ny / S >= Ho) continue;
-    const int oy = ny / S;
+    const bool oky = ny >= 0 && ny % S == 0 && ny / S < Ho;
+    const int oy = oky ? ny / S : 0;
 #pragma unroll
     for (int u = 0; u < K; ++u) {
       const int kx = K - 1 - u, nx = ix + P - kx;
-      if (nx < 0 || nx % S != 0 || nx / S >= Wo) continue;
-      const int ox = nx / S;
-      const unsigned w = code[((b * Ho + oy) * Wo + ox) * CV + cv];
+      const bool ok = oky && nx >= 0 && nx % S == 0 && nx / S < Wo;
+      const int ox = ok ? nx / S : 0;
+      wv[t * K + u] = ok ? code[((b * Ho + oy) * Wo + ox) * CV + cv] : 0xffffffffu;
+      gv[t * K + u] = ok ? *(const float4*)(dy + b * dsb + oy * dsh + ox * dsw + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < K; ++t) {
+    const int ky = K - 1 - t;
+#pragma unroll
+    for (int u = 0; u < K; ++u) {
+      const int kx = K - 1 - u;
       const unsigned want = (unsigned)(ky * K + kx) * 0x01010101u;
-      const unsigned hit = w ^ want;  // a zero byte marks a window whose max sits here
-      if (((hit - 0x01010101u) & ~hit & 0x80808080u) == 0) continue;
-      const float4 g = *(const float4*)(dy + b * dsb + oy * dsh + ox * dsw + c);
+      const unsigned hit = wv[t * K + u] ^ want;  // a zero byte marks a window whose max sits here
+      const float4 g = gv[t * K + u];
       if ((hit & 0xffu) == 0) acc.x += g.x;
       if ((hit & 0xff00u) == 0) acc.y += g.y;
       if ((hit & 0xff0000u) == 0) acc.z += g.z;
