@@ -1659,9 +1659,14 @@ __global__ __launch_bounds__(256) void fam_ca_bwd32_kernel(const float* __restri
   const int p0 = blockIdx.x * per, p1 = min(HW, p0 + per);
   const float4 cav = *(const float4*)(ca + (size_t)b * 32 + q * 4);
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  // (each pixel's four operand loads are issued together, before its argmax
+  // shuffles: 99.9 -> 93.7 us per call on the training step)
   for (int p = p0 + pl; p < p1; p += 32) {
     const size_t i = (size_t)b * HW + p;
     const float4 v = *(const float4*)(o2 + i * 32 + q * 4);
+    const float4 gv = *(const float4*)(g_o2 + i * 32 + q * 4);
+    const float4 ov = *(const float4*)(o + i * 32 + q * 4);
+    const float gm0 = g_m[i * 2] / 32.f, gm1 = g_m[i * 2 + 1];
     float mv = v.x;
     int mi = q * 4;
     argmax_pick(mv, mi, v.y, q * 4 + 1);
@@ -1673,9 +1678,6 @@ __global__ __launch_bounds__(256) void fam_ca_bwd32_kernel(const float* __restri
       const int i2 = __shfl_xor(mi, off);
       argmax_pick(mv, mi, v2, i2);
     }
-    const float gm0 = g_m[i * 2] / 32.f, gm1 = g_m[i * 2 + 1];
-    const float4 gv = *(const float4*)(g_o2 + i * 32 + q * 4);
-    const float4 ov = *(const float4*)(o + i * 32 + q * 4);
     const int c0 = q * 4;
     const float t0 = gv.x + gm0 + (mi == c0 ? gm1 : 0.f), t1 = gv.y + gm0 + (mi == c0 + 1 ? gm1 : 0.f);
     const float t2 = gv.z + gm0 + (mi == c0 + 2 ? gm1 : 0.f), t3 = gv.w + gm0 + (mi == c0 + 3 ? gm1 : 0.f);
