@@ -337,6 +337,7 @@ int upr_t_maxpool_bwd_code16(const unsigned char* code, const UprView* dy, int B
 /* upr_t_maxpool_code reading the input's compact fp16 copy x16 ([B][H][W][C];
  * the autocast VGG activations exist in fp16 only): 3x3/1/1 and 2x2/2/0 with
  * C % 4 == 0, else UPR_ERR_UNSUPPORTED. */
+/* upr_t_maxpool16_code: y->data NULL writes the fp16 copy y16 only (the pooled values are fp16 values). */
 int upr_t_maxpool16_code(const void* x16, int B, int H, int W, int C, int k, int s, int p, const UprView* y, int Ho,
                          int Wo, unsigned char* code, void* y16, void* stream);
 /* upr_t_copy / upr_t_bilinear also writing the fp16 copy of the result at
@@ -458,6 +459,9 @@ int upr_t_loss_pixel_p(const float* low, const float* enh, const float* illu, co
 /* Perceptual MSE level (F.mse_loss): acc (fp64) += sum (a-b)^2 / n; with
  * g != NULL, g = scale*2*(a-b) (scale = weight/n). */
 int upr_t_mse(const float* a, const float* b, size_t n, double* acc, float* g, float scale, void* stream);
+/* The same over two fp16 tensors (n % 4 == 0, 8-byte aligned; g 16-byte aligned or NULL), else
+ * UPR_ERR_UNSUPPORTED: the frozen VGG's fp16-only features under autocast. */
+int upr_t_mse16(const void* a16, const void* b16, size_t n, double* acc, float* g, float scale, void* stream);
 /* (x NCHW - mean) / std -> NHWC [B,H,W,3]; bwd: g_x (NCHW) += g_y / std. */
 int upr_t_vgg_norm(const float* x, float* y, int B, int H, int W, void* stream);
 int upr_t_vgg_norm_bwd(const float* g_y, float* g_x, int B, int H, int W, void* stream);

@@ -3416,7 +3416,7 @@ __global__ __launch_bounds__(256) void maxpool4_kernel(const TI* __restrict__ x,
       }
     }
   }
-  *(float4*)(y + b * ysb + oy * ysh + ox * ysw + c) = make_float4(m[0], m[1], m[2], m[3]);
+  if (y) *(float4*)(y + b * ysb + oy * ysh + ox * ysw + c) = make_float4(m[0], m[1], m[2], m[3]);
   if (y16) {  // compact [b][oy][ox][C] fp16 copy: element index 4 i
     typedef _Float16 h4 __attribute__((ext_vector_type(4)));
     *(h4*)(y16 + (size_t)i * 4) = h4{(half_t)m[0], (half_t)m[1], (half_t)m[2], (half_t)m[3]};
@@ -3579,6 +3579,7 @@ int upr_t_maxpool_code(const UprView* x, int B, int H, int W, int C, int k, int 
 int upr_t_maxpool16_code(const void* x16, int B, int H, int W, int C, int k, int s, int p, const UprView* y, int Ho,
                          int Wo, unsigned char* code, void* y16, void* stream) {
   if (!x16 || !y || k <= 0 || s <= 0 || k * k > 255) return UPR_ERR_ARG;
+  if (!y->data && !y16) return UPR_ERR_ARG;  // y->data NULL: the fp16 copy only (its values are exact)
   const long long n = (long long)B * Ho * Wo * C;
   if (n == 0) return UPR_OK;
   const int kind = pool_fast_kind(k, s, p);
@@ -3986,6 +3987,38 @@ int upr_t_loss_total(float* terms, float w_exp, float w_col, float w_spa, float 
   if (!terms) return UPR_ERR_ARG;
   hipLaunchKernelGGL(loss_total_kernel, dim3(1), dim3(64), 0, ST(stream), terms, w_exp, w_col, w_spa, w_dec, w_per,
                      w_freq);
+  LAUNCH_CHECK();
+}
+
+// the same over two fp16 tensors (the frozen VGG's features under autocast,
+// which exist in fp16 only: the reference's mse_loss promotes them to fp32),
+// 4 elements per thread
+__global__ __launch_bounds__(256) void mse16_kernel(const half_t* __restrict__ a, const half_t* __restrict__ b,
+                                                    long long n4, long long n, double* acc, float* g, float scale) {
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+  double v[1] = {0.0};
+  GSTRIDE(i, n4) {
+    const h4 x = *(const h4*)(a + 4 * i), y = *(const h4*)(b + 4 * i);
+    float d[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      d[k] = (float)x[k] - (float)y[k];
+      v[0] += (double)d[k] * d[k];
+    }
+    if (g) *(float4*)(g + 4 * i) = make_float4(scale * 2.f * d[0], scale * 2.f * d[1], scale * 2.f * d[2], scale * 2.f * d[3]);
+  }
+  v[0] /= (double)n;
+  double* dst[1] = {acc};
+  block_sum_atomic<1>(v, dst);
+}
+
+int upr_t_mse16(const void* a16, const void* b16, size_t n, double* acc, float* g, float scale, void* stream) {
+  if (!a16 || !b16 || !acc) return UPR_ERR_ARG;
+  if (n % 4 || ((uintptr_t)a16 | (uintptr_t)b16) % 8 || (uintptr_t)g % 16) return UPR_ERR_UNSUPPORTED;
+  if (n == 0) return UPR_OK;
+  const long long n4 = (long long)(n / 4);
+  hipLaunchKernelGGL(mse16_kernel, dim3(grid_for(n4, 256, 4096)), dim3(256), 0, ST(stream), (const half_t*)a16,
+                     (const half_t*)b16, n4, (long long)n, acc, g, scale);
   LAUNCH_CHECK();
 }
 

@@ -198,6 +198,7 @@ SIGNATURES.update({
     "upr_t_loss_pixel_p": (_i, [_p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p, _i, _f, _f, _f, _f, _f, _i, _p, _p]),
     "upr_t_loss_pixel": (_i, [_p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p, _i, _f, _f, _f, _f, _f, _i, _p]),
     "upr_t_mse": (_i, [_p, _p, c_size_t, _p, _p, _f, _p]),
+    "upr_t_mse16": (_i, [_p, _p, c_size_t, _p, _p, _f, _p]),
     "upr_t_vgg_norm": (_i, [_p, _p, _i, _i, _i, _p]),
     "upr_t_vgg_norm_bwd": (_i, [_p, _p, _i, _i, _i, _p]),
     "upr_t_freq": (_i, [_p, _p, _i, _i, _i, _p, _p, _f, _p]),

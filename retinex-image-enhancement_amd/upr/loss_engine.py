@@ -93,7 +93,7 @@ class VGGPerceptual:
                     trace.append(("conv", i, inp, h))
             p = Act.new(h.B, h.H // 2, h.W // 2, h.C, h.t.device, fresh=False)
             code = torch.empty(p.B * p.H * p.W * p.C, dtype=torch.uint8, device=h.t.device) if keep else None
-            maxpool_into(h, p, 2, 2, 0, code)
+            maxpool_into(h, p, 2, 2, 0, code, only16=True)
             if keep:
                 trace.append(("pool", code, h, p))
             h = p
@@ -240,8 +240,13 @@ class TotalLossEngine:
         for a, b in zip(fe, fl):
             n = a.t.numel()
             g = Act.new(a.B, a.H, a.W, a.C, dev, fresh=False) if grads else None
-            _chk(lib.upr_t_mse(_fp(a.t), _fp(b.t), n, _p(acc[1:2]), _fp(g.t) if g else None,
-                               ctypes.c_float(w["perceptual"] / n), st), "mse")
+            if a.stale32 or b.stale32:  # fp16-only features (autocast): the MSE reads the fp16 copies
+                rc = lib.upr_t_mse16(_p(a.t16), _p(b.t16), n, _p(acc[1:2]), _fp(g.t) if g else None,
+                                     ctypes.c_float(w["perceptual"] / n), st)
+            else:
+                rc = lib.upr_t_mse(_fp(a.t), _fp(b.t), n, _p(acc[1:2]), _fp(g.t) if g else None,
+                                   ctypes.c_float(w["perceptual"] / n), st)
+            _chk(rc, "mse")
             gfe.append(g)
         _chk(lib.upr_t_scale_acc(_p(acc[1:2]), 1, ctypes.c_float(1.0), _fp(terms, 5), st), "scale")
         if grads:

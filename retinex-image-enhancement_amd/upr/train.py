@@ -915,18 +915,25 @@ def relu_mask(g, y, want16=False, only16=False):
     _chk(L.lib().upr_t_relu_mask(_fp(g.t), g.cs, g.coff, _fp(y.t), y.cs, y.coff, g.M, g.C, _stream()), "relu_mask")
 
 
-def maxpool_into(x, y, k, s, p, code=None):
+def maxpool_into(x, y, k, s, p, code=None, only16=False):
     """nn.MaxPool2d(k, s, p) of Act x into Act y (argmax codes for the backward
-    when `code`); under autocast also y's fp16 copy (y.t16) in the same pass."""
+    when `code`); under autocast also y's fp16 copy (y.t16) in the same pass.
+    only16 (under autocast, from an fp16 input): y is written as its fp16 copy
+    only (y.stale32; the max of fp16 values is an fp16 value, so nothing is
+    rounded) -- the frozen VGG's pools, whose every reader takes fp16."""
     lib, st = L.lib(), _stream()
     if _AMP[0] and y.coff == 0 and y.cs == y.C:
         y16 = _h16(y.M * y.C, y.t.device)
         if x.t16 is not None and x.coff == 0 and x.cs == x.C:
             # the activation's fp16 copy (its only value when x.stale32)
-            rc = lib.upr_t_maxpool16_code(_p(x.t16), x.B, x.H, x.W, x.C, k, s, p, ctypes.byref(y.view()), y.H, y.W,
+            yv = y.view()
+            if only16:
+                yv.data = None
+            rc = lib.upr_t_maxpool16_code(_p(x.t16), x.B, x.H, x.W, x.C, k, s, p, ctypes.byref(yv), y.H, y.W,
                                           _p(code), _p(y16), st)
             if rc == 0:
                 y.t16 = y16
+                y.stale32 = bool(only16)
                 return
             if rc != L.UPR_ERR_UNSUPPORTED:
                 _chk(rc, "maxpool16")
