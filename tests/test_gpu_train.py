@@ -1558,3 +1558,34 @@ def test_bn_stats16_fin_matches_two_step(M, C):
     for a, b in zip(outs[0], outs[1]):
         assert torch.equal(a, b)
     assert int(outs[1][5]) == 8
+
+
+@pytest.mark.parametrize("n", [4096, 8 * 64 * 64 * 256])
+def test_mse16_matches_fp32_mse(n):
+    """upr_t_mse16 (the perceptual MSE over the frozen VGG's fp16-only features
+    under autocast, losses/loss.py:198-211) vs upr_t_mse on the same values
+    widened to fp32 (the pooled features are exact fp16 values): the mean of
+    squares within fp64 summation order, the gradient 2 * scale * d bit-exact."""
+    from upr import _lib as L
+    gen = torch.Generator().manual_seed(n % 97)
+    a = torch.randn(n, generator=gen).half()
+    b = torch.randn(n, generator=gen).half()
+    lib, st = L.lib(), torch.cuda.current_stream().cuda_stream
+    a16, b16 = a.to(DEV), b.to(DEV)
+    a32, b32 = a16.float(), b16.float()
+    acc = torch.zeros(2, dtype=torch.float64, device=DEV)
+    g16 = torch.empty(n, device=DEV)
+    g32 = torch.empty(n, device=DEV)
+    scale = 0.25 / n
+    assert lib.upr_t_mse16(a16.data_ptr(), b16.data_ptr(), n, acc.data_ptr(), g16.data_ptr(), ctypes.c_float(scale),
+                           st) == 0
+    assert lib.upr_t_mse(a32.data_ptr(), b32.data_ptr(), n, acc.data_ptr() + 8, g32.data_ptr(), ctypes.c_float(scale),
+                         st) == 0
+    torch.cuda.synchronize()
+    ref = ((a.double() - b.double()) ** 2).mean().item()
+    assert abs(acc[0].item() - ref) <= 1e-12 * max(ref, 1.0)
+    assert abs(acc[0].item() - acc[1].item()) <= 1e-12 * max(ref, 1.0)
+    assert torch.equal(g16, g32)
+    # unsupported layouts decline instead of computing
+    assert lib.upr_t_mse16(a16.data_ptr(), b16.data_ptr(), n - 1, acc.data_ptr(), None, ctypes.c_float(1.0),
+                           st) == L.UPR_ERR_UNSUPPORTED
