@@ -22,8 +22,11 @@ from enhancers.multi_scale import MultiScaleEnhancer
 from enhancers.content_aware import ContentAwareEnhancer
 from utils.letterbox import letterbox_u8_image
 
-# PNG encoders running beside the GPU (PIL's zlib releases the GIL); 3 files per image
-_WRITERS = 6
+# PNG encoders running beside the GPU (PIL's encoder releases the GIL); 3 files per
+# image, ~90 / ~160 ms of host CPU each for a 512^2 / comparison PNG of a noisy image,
+# so the batch harness is encode-bound: one writer per usable core but two, at most 14
+# (os.cpu_count() is the whole machine on a shared box; UPR_PNG_WRITERS overrides)
+_WRITERS = int(os.environ.get("UPR_PNG_WRITERS", 0)) or min(14, max(2, (os.cpu_count() or 8) - 2))
 VALID_EXTENSIONS = {'.jpg', '.jpeg', '.png', '.bmp', '.tif', '.tiff'}
 
 
