@@ -26,7 +26,15 @@ from utils.letterbox import letterbox_u8_image
 # image, ~90 / ~160 ms of host CPU each for a 512^2 / comparison PNG of a noisy image,
 # so the batch harness is encode-bound: one writer per usable core but two, at most 14
 # (os.cpu_count() is the whole machine on a shared box; UPR_PNG_WRITERS overrides)
-_WRITERS = int(os.environ.get("UPR_PNG_WRITERS", 0)) or min(14, max(2, (os.cpu_count() or 8) - 2))
+def _writer_count():
+    try:
+        n = int(os.environ.get("UPR_PNG_WRITERS", "0"))
+    except ValueError:
+        n = 0
+    return n if n > 0 else min(14, max(2, (os.cpu_count() or 8) - 2))
+
+
+_WRITERS = _writer_count()
 VALID_EXTENSIONS = {'.jpg', '.jpeg', '.png', '.bmp', '.tif', '.tiff'}
 
 
