@@ -825,10 +825,11 @@ static int build_model(UprModel* m, ParamSet& P) {
 // first use: non-blocking, joined through events every forward.  nullptr keeps
 // the whole forward on the caller's stream: UPR_MS_STREAMS=0 (A/B timing;
 // =1 forks fp32 models too, unset forks fp16 models only).
-// The side stream forks right after op 0 (the side ops need only its scale1
-// output); a later fork (before enc3 / the bottleneck) and a capped CU budget
-// for the side stream's ring convs measured no better (profiles/r3_ms_fork_ab.txt,
-// r3_side_cus_ab.txt), as did a low-priority side stream (r3_ms_streams_ab.txt).
+// The side stream forks before the bottleneck (run_forward; round 3 measured
+// no gain from a later fork, round 5's kernels 1.5-1.8%: profiles/r5_ms_fork_ab.txt);
+// a capped CU budget for the side stream's ring convs (r3_side_cus_ab.txt), a
+// low-priority side stream (r3_ms_streams_ab.txt) and CU-partitioned streams
+// (r5_cu_mask_streams_ab.txt) measured no better.
 
 using Side = UprModel::Side;
 static std::shared_ptr<Side> side_of(UprModel* m, hipStream_t st) {
@@ -1042,9 +1043,22 @@ static int run_forward(UprModel* m, const void* x, int B, int H, int W, void* en
     }
   } else {
     // IENet ops [0, fork) -> fork -> side: the multi-scale ops, main: the rest
-    // of the IENet -> join -> tail.  The fork point is right
-    // after op 0 (the side ops need only its scale1 output)
-    const int fk = 1;
+    // of the IENet -> join -> tail
+    // fork before the bottleneck: the side ops (HBM-bound FAM convs) then run
+    // beside the MFMA-bound bottleneck / ASPP convs instead of competing with the
+    // HBM-bound encoder for bandwidth (fp16 preact+ASPP bs 32: 5.47 ms forking
+    // after op 0, 5.37-5.41 before the bottleneck, 5.40-5.43 before enc3, 5.45
+    // before enc2, 5.50 before dec3; profiles/r5_ms_fork_ab.txt).  The side ops
+    // need only op 0's outputs, so any fork point is exact.  UPR_MS_FORK=<op
+    // name prefix> overrides ("-": right after op 0)
+    static const std::string fork_at = [] {
+      const char* e = getenv("UPR_MS_FORK");
+      return std::string(e ? e : "ie_net.bottleneck");
+    }();
+    int fk = 1;
+    if (fork_at != "-")
+      for (int oi = 1; oi < m->side_begin; ++oi)
+        if (m->ops[oi].name.compare(0, fork_at.size(), fork_at) == 0) { fk = oi; break; }
     int rc = kOk;
     m->forks.fetch_add(1, std::memory_order_relaxed);
     for (int oi = 0; oi < fk; ++oi)
