@@ -453,7 +453,7 @@ def forward_leg(args, world, rank, dev, precision, variant, B, S, traffic, cpu_s
     # last step always stays on one stream
     forked = handle.forks()
     two = forked >= args.steps + max(args.warmup - 1, 0)
-    out["executor"] = ("two streams: the multi-scale ops on a side stream forked after the first conv, joined "
+    out["executor"] = ("two streams: the multi-scale ops on a side stream forked before the bottleneck, joined "
                        "before the Retinex tail (DESIGN §3)" if two else "one stream") + \
         f" ({forked} of {args.steps + args.warmup} forwards forked)" + \
         ("; roofline per-launch events from the serialised profiled step" if stats else "")

@@ -823,8 +823,8 @@ static int build_model(UprModel* m, ParamSet& P) {
 // ---------------------------------------------------------------------------
 // The multi-scale side stream of (current device, caller stream), created on
 // first use: non-blocking, joined through events every forward.  nullptr keeps
-// the whole forward on the caller's stream: UPR_MS_STREAMS=0 (A/B timing;
-// =1 forks fp32 models too, unset forks fp16 models only).
+// the whole forward on the caller's stream: UPR_MS_STREAMS=0 (A/B timing and
+// the rocprofv3 kernel summaries).
 // The side stream forks before the bottleneck (run_forward; round 3 measured
 // no gain from a later fork, round 5's kernels 1.5-1.8%: profiles/r5_ms_fork_ab.txt);
 // a capped CU budget for the side stream's ring convs (r3_side_cus_ab.txt), a
@@ -837,10 +837,11 @@ static std::shared_ptr<Side> side_of(UprModel* m, hipStream_t st) {
     const char* e = getenv("UPR_MS_STREAMS");
     return e ? (atoi(e) != 0 ? 1 : 0) : -1;
   }();
-  // default: fp16 models only.  fp32 gains ~1% (every fp32 conv is MFMA-bound,
-  // profiles/r3_ms_streams_ab.txt) and a single stream keeps each kernel's
-  // duration separable in a trace (the headline's rocprofv3 evidence)
-  if (en == 0 || (en < 0 && m->dtype != kF16)) return nullptr;
+  // default: every model forks (fp32 too since round 5: +1.1% with the fork
+  // before the bottleneck, profiles/r5_ms_fork_ab.txt).  Per-kernel durations
+  // for the roofline come from the serialised profiled step, and the rocprofv3
+  // kernel summaries are taken with UPR_MS_STREAMS=0 (tools/gpu/r5_final.sh)
+  if (en == 0) return nullptr;
   // hipStreamPerThread names a different real stream per calling thread: a
   // Side keyed by it would be shared by threads whose fork / join events then
   // interleave, so those forwards stay on the one stream (upr.h).  The null

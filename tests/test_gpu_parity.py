@@ -471,15 +471,14 @@ def test_two_streams_distinct_handles():
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
 def test_multiscale_side_stream_matches_serial(dtype):
     """The executor runs the multi-scale ops (scale pyramid, scale2/3 first
-    convs, the three EnhancedFAM blocks) on a side stream forked after the fused
-    first conv and joined before the Retinex tail (csrc/model.hip side_of); a
+    convs, the three EnhancedFAM blocks) on a side stream forked before the
+    bottleneck and joined before the Retinex tail (csrc/model.hip side_of); a
     profiled forward (upr_model_profile) keeps every op on the caller's stream.
     Both orders give bit-identical outputs, on the default stream and on a
     non-default caller stream, for repeated forwards of different batches
-    (a missing fork / join edge would read a half-written buffer).  fp16
-    models fork by default; fp32 ones only under UPR_MS_STREAMS=1
-    (tools/gpu/env_ab.sh runs this file under its B env), else this is the
-    serial order twice."""
+    (a missing fork / join edge would read a half-written buffer).  Every
+    model forks by default (fp32 too since round 5); under UPR_MS_STREAMS=0
+    this is the serial order twice."""
     m = make_model(True, True).to(DEV)
     if dtype == torch.float16:
         m = m.half()
@@ -493,11 +492,11 @@ def test_multiscale_side_stream_matches_serial(dtype):
         handle.profile(False)
         n0 = handle.forks()
         forked = [[t.clone() for t in m(x)] for x in xs]
-        # fp16 models fork on torch's default (null) stream too (unless
+        # models fork on torch's default (null) stream too (unless
         # UPR_MS_STREAMS=0), not only on an explicit caller stream
         import os
         env = os.environ.get("UPR_MS_STREAMS")
-        want = (dtype == torch.float16) if env is None else (int(env) != 0)
+        want = True if env is None else (int(env) != 0)
         assert handle.forks() - n0 == (len(xs) if want else 0)
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())

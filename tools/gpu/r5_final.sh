@@ -9,7 +9,7 @@ rc=$?; tail -2 $out/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || exit $?
 timeout -k 10 500 python bench.py --detail $out/bench_detail.json > $out/bench_default.json 2> $out/bench_default.err || exit $?
 wc -c $out/bench_default.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/rp32 -o k --output-format csv -- python3 bench.py --steps 10 --warmup 3 --cpu-seconds 0 --no-traffic --no-nested --detail "" > $out/rp32.log 2>&1 || exit $?
+UPR_MS_STREAMS=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/rp32 -o k --output-format csv -- python3 bench.py --steps 10 --warmup 3 --cpu-seconds 0 --no-traffic --no-nested --detail "" > $out/rp32.log 2>&1 || exit $?
 UPR_MS_STREAMS=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/rp16 -o k --output-format csv -- python3 bench.py --steps 10 --warmup 3 --cpu-seconds 0 --no-traffic --no-nested --precision fp16 --variant preact_aspp --detail "" > $out/rp16.log 2>&1 || exit $?
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $out/rpe -o k --output-format csv -- python3 bench.py --enhance --steps 20 --warmup 3 --no-traffic --cpu-seconds 0 --detail "" > $out/rpe.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/rpt -o k --output-format csv -- python3 bench.py --train --amp --steps 4 --warmup 1 --cpu-seconds 0 --detail "" > $out/rpt.log 2>&1 || exit $?
