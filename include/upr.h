@@ -15,12 +15,14 @@
  *   - return 0 on success, a hipError_t value (> 0) passed through, or a
  *     negative UPR_ERR_* code; upr_status_string() describes either.
  * Thread safety: distinct models / streams may be used concurrently; one model
- * handle must not be used on two streams at once.  A forward of an fp16 model
- * forks its multi-scale head onto a side stream of the library's own, keyed
- * by (device, caller stream); the pseudo-handles that name a different real
- * stream per thread (NULL and hipStreamPerThread) never fork: such forwards
- * run on the one stream, so two threads passing the same pseudo-handle never
- * share a side stream.
+ * handle must not be used on two streams at once.  A forward (fp32 or fp16;
+ * UPR_MS_STREAMS=0 turns it off) forks its multi-scale head onto a side stream
+ * of the library's own, keyed by (device, caller stream), with fork / join
+ * events of that side.  NULL is treated as the one legacy stream: it forks
+ * too, and two threads forwarding on NULL share one side stream and its
+ * events, so a handle -- or two handles -- must not be used from two threads
+ * on NULL at once.  hipStreamPerThread (a different real stream per thread)
+ * never forks: such forwards run on the one stream.
  */
 #ifndef UPR_H_
 #define UPR_H_

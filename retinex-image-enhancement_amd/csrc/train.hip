@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstring>
 #include <mutex>
+#include <thread>
 
 #include "upr_common.h"
 #include "../../include/upr.h"
@@ -107,29 +108,55 @@ void* scratch(int slot, size_t bytes, hipStream_t st, bool* fresh) {
     hipStream_t st;
     void* p[kSlotCount];
     size_t n[kSlotCount];
+    std::thread::id owner;     // the one thread that used the entry (unless shared)
+    bool shared;               // used by more than one thread: never reclaimed
+    unsigned long long tick;   // last use (LRU)
   };
   static std::mutex mu;
   static Entry tab[kScratchStreams];
   static int used = 0;
+  static unsigned long long clock = 0;
   if (fresh) *fresh = false;
   if (slot < 0 || slot >= kSlotCount) return nullptr;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  const std::thread::id me = std::this_thread::get_id();
   std::lock_guard<std::mutex> lock(mu);
   Entry* e = nullptr;
   for (int i = 0; i < used; ++i)
     if (tab[i].dev == dev && tab[i].st == st) e = &tab[i];
   if (!e) {
-    // full: an error, not an eviction.  Another thread may hold a pointer of
-    // any entry whose kernel it has not launched yet, so no entry can be freed
-    // safely here (a device synchronise does not cover a launch still to come,
-    // and it fails while any stream of the device is being captured)
-    if (used >= kScratchStreams) return nullptr;
-    e = &tab[used++];
-    memset(e, 0, sizeof(*e));
+    if (used < kScratchStreams) {
+      e = &tab[used++];
+    } else {
+      // full: reclaim the least recently used entry that only THIS thread
+      // ever used.  Its buffers went out only in this thread's earlier calls,
+      // which returned after enqueueing their launches, so once the device is
+      // idle nobody reads them (another thread's entries may be mid-call:
+      // their pointers can still be waiting for a launch, so they are never
+      // taken).  The device synchronise is not allowed while the caller's
+      // stream is being captured: then the call fails as before.
+      Entry* v = nullptr;
+      for (int i = 0; i < used; ++i)
+        if (!tab[i].shared && tab[i].owner == me && tab[i].dev == dev && (!v || tab[i].tick < v->tick)) v = &tab[i];
+      hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+      if (!v || hipStreamIsCapturing(st, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) {
+        (void)hipGetLastError();
+        return nullptr;
+      }
+      if (hipDeviceSynchronize() != hipSuccess) return nullptr;
+      for (int k = 0; k < kSlotCount; ++k)
+        if (v->p[k]) (void)hipFree(v->p[k]);
+      e = v;
+    }
+    *e = Entry{};
     e->dev = dev;
     e->st = st;
+    e->owner = me;
+  } else if (e->owner != me) {
+    e->shared = true;
   }
+  e->tick = ++clock;
   if (bytes == 0) bytes = 16;
   if (e->n[slot] < bytes) {
     if (e->p[slot]) {

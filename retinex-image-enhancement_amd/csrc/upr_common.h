@@ -127,6 +127,9 @@ int launch_conv_s2dg(const ConvOp& op, hipStream_t stream, bool probe = false);
 int launch_conv_pw(const ConvOp& op, hipStream_t stream, bool probe = false);
 
 int launch_conv(const ConvOp& op, int dtype, hipStream_t stream);
+// fp16 3x3 convs over 256 channels at W 64 on two 80 KiB blocks per CU
+// (conv_hw2.hip); kErrUnsupported for the shapes it does not take
+int launch_conv_hw2(const ConvOp& op, hipStream_t stream);
 
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
@@ -166,9 +169,12 @@ inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 // call on this stack (13 of 36 ms per training step went to them) and
 // stalled the launch queue.  Growth (warm-up only) synchronises the stream
 // before freeing the smaller buffer.  Returns nullptr when out of memory.
-// At most kScratchStreams (device, stream) pairs hold buffers; a new pair
-// past that gets nullptr (the caller's entry point returns an error): an
-// entry is never freed while the process runs, so no thread's pointer dangles.
+// At most kScratchStreams (device, stream) pairs hold buffers; a new pair past
+// that reclaims the least recently used entry that only the calling thread
+// ever used (after a device synchronise: that thread's earlier calls have all
+// enqueued their launches), and gets nullptr (the caller's entry point returns
+// an error) only when every entry is another thread's or shared, or while its
+// stream is being captured.
 constexpr int kScratchStreams = 64;
 enum ScratchSlot { kSlotSlab = 0, kSlotCast, kSlotTmp, kSlotCode, kSlotRows, kSlotPart, kSlotMs, kSlotCount };
 // fresh (optional): set true when the returned buffer was (re)allocated by this call

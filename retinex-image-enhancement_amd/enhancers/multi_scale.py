@@ -1,9 +1,11 @@
 """MultiScaleEnhancer (drop-in for reference enhancers/multi_scale.py).
 
 The scalar adjustment factor 1 + 0.1 * sum_i w_i * mean(features_i) is
-computed on the device per image (one reduction kernel per scale, fp64
-partials); the reference syncs three times through .item() (:313-314) and
-means over the whole batch — it only ever runs B = 1.
+computed on the device per image in one pass over the image for all three
+scales (ms_sums3_kernel: fp64 per-tile partials, added in tile order by
+ms_fin_kernel, which writes the factor); the reference syncs three times
+through .item() (:313-314) and means over the whole batch — it only ever runs
+B = 1.
 """
 import torch
 

@@ -226,9 +226,12 @@ class MultiScaleUP_Retinex(_HipGraphMixin, nn.Module):
         (reference :415-443; `illu` is not read there either).  The head has
         no BatchNorm or Dropout, so train and eval mode compute the same values.
         With grad enabled and a reflectance that requires grad (or the model in
-        training mode) the call is differentiable as the reference's is: the
-        head's training graph (upr.autograd._HeadStep, fp32) returns dL/d
-        reflectance and accumulates the head parameters' gradients.  Otherwise
+        training mode with parameters that require grad) the call is
+        differentiable as the reference's is: the head's training graph
+        (upr.autograd._HeadStep; float32, H and W multiples of 16) returns
+        dL/d reflectance and accumulates the head parameters' gradients.  A
+        reflectance that requires grad outside those shapes is refused; in
+        training mode alone such a call warns and returns the inference value.  Otherwise
         it runs on the inference kernels (UPR_MODEL_HEAD_ONLY handle) and the
         result records no history.  x gets no gradient (as in forward()): an
         x that requires grad is refused rather than silently detached."""
@@ -238,9 +241,27 @@ class MultiScaleUP_Retinex(_HipGraphMixin, nn.Module):
         if torch.is_grad_enabled() and x.requires_grad:
             raise NotImplementedError("multi_scale_enhance: no gradient w.r.t. x (the HIP head differentiates "
                                       "w.r.t. the reflectance and the parameters); pass x.detach()")
-        if torch.is_grad_enabled() and (reflectance.requires_grad or self.training):
-            from upr.autograd import head_train_forward
-            return head_train_forward(self, x, reflectance)
+        if torch.is_grad_enabled() and (reflectance.requires_grad or
+                                        (self.training and any(p.requires_grad for p in self.parameters()))):
+            B, C, H, W = x.shape
+            ok = (x.dtype == torch.float32 and reflectance.dtype == torch.float32 and H % 16 == 0 and W % 16 == 0
+                  and tuple(reflectance.shape) == (B, 3, H, W))
+            if ok:
+                from upr.autograd import head_train_forward
+                return head_train_forward(self, x, reflectance)
+            if reflectance.requires_grad:
+                raise ValueError(f"multi_scale_enhance: the differentiable head takes float32 x / reflectance "
+                                 f"[B,3,H,W] with H, W multiples of 16 (got {tuple(x.shape)} {x.dtype}, "
+                                 f"{tuple(reflectance.shape)} {reflectance.dtype}); detach the reflectance for "
+                                 f"a value without gradients")
+            # training mode, only the parameters would take gradients, and the
+            # training graph does not run this shape / dtype: the value from the
+            # inference kernels, without history (as before the head was
+            # differentiable), and a warning that no gradient is recorded
+            import warnings
+            warnings.warn(f"multi_scale_enhance: {tuple(x.shape)} {x.dtype} is outside the differentiable head "
+                          f"(float32, H, W multiples of 16); returning a value without parameter gradients",
+                          RuntimeWarning, stacklevel=2)
         key = ("head", x.device, x.dtype)
         sig = self._signature()
         cache = self.__dict__.setdefault("_upr_cache", {})

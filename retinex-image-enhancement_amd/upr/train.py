@@ -875,7 +875,9 @@ class BN:
             # the mask comes from the stored output here: with a post-ReLU
             # residual that output is relu(bn(x)) + skip, not the ReLU's own
             # output, and the mask would be wrong wherever skip > 0 >= bn(x)
-            assert not self.has_res, "unfused ReLU backward of relu(bn(x)) + skip: mask needs the pre-residual value"
+            if self.has_res:
+                raise NotImplementedError("unfused ReLU backward of relu(bn(x)) + skip: the mask needs the "
+                                          "pre-residual value (the fused BatchNorm backward takes this layer)")
             relu_mask(g, self.out_act)
         zero(self.acc[:2 * self.C])
         _chk(lib.upr_t_bn_bwd_reduce(_fp(g.t), g.cs, g.coff, x.ptr(), x.cs, 0, _p(self.mean), _p(self.invstd), x.M,

@@ -16,7 +16,8 @@ def test_letterbox_geometry_identity():
 
 
 def test_product_taps_match_oracle_taps():
-    for dst, src in ((85, 200), (128, 300), (60, 30), (13, 30), (30, 30)):
+    for dst, src in ((85, 200), (128, 300), (60, 30), (13, 30), (30, 30), (640, 1920), (384, 1080), (1000, 7),
+                     (7, 1000), (333, 334)):
         t = linear_taps(dst, src)
         o = oracle_taps(dst, src)
         for i in range(4):
