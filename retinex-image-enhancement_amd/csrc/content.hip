@@ -10,6 +10,7 @@
 // OpenCV's RowFilter / SymmColumnFilter and torch's CPU elementwise ops.
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 
 #include "upr_common.h"
 
@@ -99,6 +100,193 @@ __global__ __launch_bounds__(256) void ca_gauss_cols(const double* __restrict__ 
   if (threadIdx.x == 0) {
     part[((size_t)b * nblk + blockIdx.x) * 2] = smn[0];
     part[((size_t)b * nblk + blockIdx.x) * 2 + 1] = smx[0];
+  }
+}
+
+// Fused saliency pass (round 6): gray -> |Laplacian| -> 15-tap Gaussian rows
+// -> 15-tap Gaussian columns for a 32 x 64 output tile in one block, every
+// intermediate in LDS: the tile's gray region (tile + 8 on each side, image
+// coordinates reflected 101) is computed from the image once, the Laplacian
+// over the tile + 7 (a reflected region position's Laplacian equals the
+// Laplacian at the reflected position: the stencil is symmetric), then the
+// row and column passes in the order and fp64 arithmetic of ca_gauss_rows /
+// ca_gauss_cols (bit-identical outputs).  HBM: the image once (12 B/px, the
+// halo from L2) and the fp64 map once (8 B/px), against 52 B/px for the
+// three-kernel form.  Per-block fp64 min / max partials as ca_gauss_cols.
+constexpr int CA_TH = 32, CA_TW = 64, CA_R = 7;
+constexpr int CA_GH = CA_TH + 2 * CA_R + 2, CA_GW = CA_TW + 2 * CA_R + 2;  // 48 x 80 gray region
+constexpr int CA_LH = CA_TH + 2 * CA_R, CA_LW = CA_TW + 2 * CA_R;          // 46 x 78 Laplacian region
+
+template <typename T>
+__device__ __forceinline__ void ld4(const T* p, float (&v)[4]);
+template <>
+__device__ __forceinline__ void ld4<float>(const float* p, float (&v)[4]) {
+  const float4 q = *(const float4*)p;
+  v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+}
+template <>
+__device__ __forceinline__ void ld4<half_t>(const half_t* p, float (&v)[4]) {
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+  const h4 q = *(const h4*)p;
+  v[0] = (float)q[0]; v[1] = (float)q[1]; v[2] = (float)q[2]; v[3] = (float)q[3];
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void ca_sal_fused_kernel(const T* __restrict__ x, double* __restrict__ sal, int H,
+                                                           int W, int tiles_x, GaussK g, double* __restrict__ part,
+                                                           int nblk) {
+  // the gray region and the row-pass output are never live together: one buffer
+  __shared__ __attribute__((aligned(16))) double rowg[CA_LH][CA_TW];  // 23.5 KiB (gray: 15 KiB of it)
+  __shared__ double lap[CA_LH][CA_LW];                                 // 28 KiB
+  int(*gray)[CA_GW] = (int(*)[CA_GW])&rowg[0][0];
+  const int t = threadIdx.x;
+  const int b = blockIdx.y;
+  const int ty0 = (blockIdx.x / tiles_x) * CA_TH, tx0 = (blockIdx.x % tiles_x) * CA_TW;
+  const size_t HW = (size_t)H * W;
+  const T* img = x + (size_t)b * 3 * HW;
+  const int gy0 = ty0 - CA_R - 1, gx0 = tx0 - CA_R - 1;
+  // (1) gray of the region; interior tiles load 4-pixel quads (gx0 is 8-aligned)
+  if (gy0 >= 0 && gx0 >= 0 && gy0 + CA_GH <= H && gx0 + CA_GW <= W && (W & 3) == 0) {
+    constexpr int QPR = CA_GW / 4, NQ = CA_GH * QPR;
+    for (int q = t; q < NQ; q += 256) {
+      const int ry = q / QPR, rq = q - ry * QPR;
+      const size_t o = (size_t)(gy0 + ry) * W + gx0 + 4 * rq;
+      float r[4], gg[4], bb[4];
+      ld4<T>(img + o, r);
+      ld4<T>(img + HW + o, gg);
+      ld4<T>(img + 2 * HW + o, bb);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        gray[ry][4 * rq + k] = (quant_u8c(bb[k]) * 1868 + quant_u8c(gg[k]) * 9617 + quant_u8c(r[k]) * 4899 + (1 << 13)) >> 14;
+    }
+  } else {
+    for (int i = t; i < CA_GH * CA_GW; i += 256) {
+      const int ry = i / CA_GW, rx = i - ry * CA_GW;
+      gray[ry][rx] = gray_at(img, H, W, refl101(gy0 + ry, H), refl101(gx0 + rx, W));
+    }
+  }
+  __syncthreads();
+  // (2) |Laplacian| over the tile + 7
+  for (int i = t; i < CA_LH * CA_LW; i += 256) {
+    const int ly = i / CA_LW, lx = i - ly * CA_LW;
+    const int c = gray[ly + 1][lx + 1];
+    lap[ly][lx] = fabs((double)(gray[ly][lx + 1] + gray[ly + 1][lx] - 4 * c + gray[ly + 1][lx + 2] + gray[ly + 2][lx + 1]));
+  }
+  __syncthreads();
+  // (3) rows: s = k0*S[x-7] + k1*S[x-6] + ... (ca_gauss_rows' order)
+  const int col = t & 63, r0 = t >> 6;
+  for (int ly = r0; ly < CA_LH; ly += 4) {
+    double acc = g.k[0] * lap[ly][col];
+#pragma unroll
+    for (int k = 1; k < 15; ++k) acc += g.k[k] * lap[ly][col + k];
+    rowg[ly][col] = acc;
+  }
+  __syncthreads();
+  // (4) columns: s = ky[7]*S[y] + 0.0; s += ky[7+k]*(S[y+k] + S[y-k])
+  double mn = DBL_MAX, mx = -DBL_MAX;
+  const int xx = tx0 + col;
+#pragma unroll
+  for (int j = 0; j < CA_TH / 4; ++j) {
+    const int yy = r0 + 4 * j, y = ty0 + yy;
+    double acc = g.k[7] * rowg[yy + CA_R][col] + 0.0;
+#pragma unroll
+    for (int k = 1; k <= 7; ++k) acc += g.k[7 + k] * (rowg[yy + CA_R + k][col] + rowg[yy + CA_R - k][col]);
+    if (y < H && xx < W) {
+      sal[(size_t)b * HW + (size_t)y * W + xx] = acc;
+      mn = fmin(mn, acc);
+      mx = fmax(mx, acc);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mn = fmin(mn, __shfl_xor(mn, o, 64));
+    mx = fmax(mx, __shfl_xor(mx, o, 64));
+  }
+  __shared__ double red[2][4];
+  if ((t & 63) == 0) { red[0][t >> 6] = mn; red[1][t >> 6] = mx; }
+  __syncthreads();
+  if (t == 0) {
+    part[((size_t)b * nblk + blockIdx.x) * 2] = fmin(fmin(red[0][0], red[0][1]), fmin(red[0][2], red[0][3]));
+    part[((size_t)b * nblk + blockIdx.x) * 2 + 1] = fmax(fmax(red[1][0], red[1][1]), fmax(red[1][2], red[1][3]));
+  }
+}
+
+// ca_att_kernel over 4 pixels per thread (HW % 4 == 0): 16-byte loads / stores
+template <typename T>
+__global__ __launch_bounds__(256) void ca_att4_kernel(const T* __restrict__ x, const double* __restrict__ sal,
+                                                      const double* __restrict__ mm, float* __restrict__ sal_out,
+                                                      float* __restrict__ att, float* __restrict__ part, int HW4,
+                                                      int nblk) {
+  const int b = blockIdx.y;
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  float mn = FLT_MAX, mx = -FLT_MAX;
+  if (q < HW4) {
+    const size_t HW = (size_t)HW4 * 4, p = (size_t)q * 4;
+    const double smin = mm[2 * b], smax = mm[2 * b + 1];
+    const double2 s01 = *(const double2*)(sal + b * HW + p), s23 = *(const double2*)(sal + b * HW + p + 2);
+    const double sv[4] = {s01.x, s01.y, s23.x, s23.y};
+    const T* img = x + (size_t)b * 3 * HW;
+    float r[4], gg[4], bb[4], so[4], a[4];
+    ld4<T>(img + p, r);
+    ld4<T>(img + HW + p, gg);
+    ld4<T>(img + 2 * HW + p, bb);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      so[k] = (float)((sv[k] - smin) / (smax - smin + 1e-8));
+      const float lum = 0.299f * r[k] + 0.587f * gg[k] + 0.114f * bb[k];
+      a[k] = so[k] * (1.0f / (lum + 0.1f));
+      mn = fminf(mn, a[k]);
+      mx = fmaxf(mx, a[k]);
+    }
+    if (sal_out) *(float4*)(sal_out + b * HW + p) = make_float4(so[0], so[1], so[2], so[3]);
+    *(float4*)(att + b * HW + p) = make_float4(a[0], a[1], a[2], a[3]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mn = fminf(mn, __shfl_xor(mn, o, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  }
+  __shared__ float red[2][4];
+  if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = mn; red[1][threadIdx.x >> 6] = mx; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[((size_t)b * nblk + blockIdx.x) * 2] = fminf(fminf(red[0][0], red[0][1]), fminf(red[0][2], red[0][3]));
+    part[((size_t)b * nblk + blockIdx.x) * 2 + 1] = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
+  }
+}
+
+// ca_apply_kernel over 4 pixels per thread (HW % 4 == 0)
+template <typename T>
+__global__ __launch_bounds__(256) void ca_apply4_kernel(const float* __restrict__ att, const float* __restrict__ mm,
+                                                        float* __restrict__ att_out, const T* __restrict__ enh,
+                                                        T* __restrict__ out, int HW4) {
+  const int b = blockIdx.y;
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= HW4) return;
+  const size_t HW = (size_t)HW4 * 4, p = (size_t)q * 4;
+  const float mn = mm[2 * b], mx = mm[2 * b + 1];
+  const float4 av = *(const float4*)(att + b * HW + p);
+  const float a[4] = {(av.x - mn) / (mx - mn + 1e-8f), (av.y - mn) / (mx - mn + 1e-8f), (av.z - mn) / (mx - mn + 1e-8f),
+                      (av.w - mn) / (mx - mn + 1e-8f)};
+  if (att_out) *(float4*)(att_out + b * HW + p) = make_float4(a[0], a[1], a[2], a[3]);
+  if (enh && out) {
+    float f[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) f[k] = 1.0f + 0.2f * a[k];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const size_t o = ((size_t)b * 3 + c) * HW + p;
+      float v[4];
+      ld4<T>(enh + o, v);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = fminf(fmaxf(v[k] * f[k], 0.f), 1.f);
+      if constexpr (sizeof(T) == 4) {
+        *(float4*)((float*)out + o) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        *(h4*)((half_t*)out + o) = h4{(half_t)v[0], (half_t)v[1], (half_t)v[2], (half_t)v[3]};
+      }
+    }
   }
 }
 
@@ -219,6 +407,34 @@ int launch_content_aware(const void* x, const void* enh, void* out, float* sal_o
   sum = 1. / sum;
   for (int i = 0; i < 15; ++i) g.k[i] *= sum;
   const size_t n = (size_t)B * HW;
+  // UPR_CA_FUSED=0: the three-kernel saliency form and the scalar passes (A/B)
+  static const bool fused = [] { const char* e = getenv("UPR_CA_FUSED"); return !e || atoi(e) != 0; }();
+  if (fused && HW % 4 == 0) {
+    // one fused saliency pass (tiles of 32 x 64) + the 4-pixel attention / apply passes
+    const int tiles_x = (W + CA_TW - 1) / CA_TW, tiles = tiles_x * ((H + CA_TH - 1) / CA_TH);
+    const int HW4 = (int)(HW / 4), nb4 = (HW4 + 255) / 256;
+    if (dtype == kF16)
+      hipLaunchKernelGGL((ca_sal_fused_kernel<half_t>), dim3(tiles, B), dim3(256), 0, st, (const half_t*)x, lap, H, W,
+                         tiles_x, g, part64, tiles);
+    else
+      hipLaunchKernelGGL((ca_sal_fused_kernel<float>), dim3(tiles, B), dim3(256), 0, st, (const float*)x, lap, H, W,
+                         tiles_x, g, part64, tiles);
+    hipLaunchKernelGGL((reduce_minmax<double>), dim3(B), dim3(256), 0, st, part64, mm64, tiles);
+    if (dtype == kF16)
+      hipLaunchKernelGGL((ca_att4_kernel<half_t>), dim3(nb4, B), dim3(256), 0, st, (const half_t*)x, lap, mm64,
+                         sal_out, att, part32, HW4, nb4);
+    else
+      hipLaunchKernelGGL((ca_att4_kernel<float>), dim3(nb4, B), dim3(256), 0, st, (const float*)x, lap, mm64, sal_out,
+                         att, part32, HW4, nb4);
+    hipLaunchKernelGGL((reduce_minmax<float>), dim3(B), dim3(256), 0, st, part32, mm32, nb4);
+    if (dtype == kF16)
+      hipLaunchKernelGGL((ca_apply4_kernel<half_t>), dim3(nb4, B), dim3(256), 0, st, att, mm32, att_out,
+                         (const half_t*)enh, (half_t*)out, HW4);
+    else
+      hipLaunchKernelGGL((ca_apply4_kernel<float>), dim3(nb4, B), dim3(256), 0, st, att, mm32, att_out,
+                         (const float*)enh, (float*)out, HW4);
+    return (int)hipGetLastError();
+  }
   if (dtype == kF16)
     hipLaunchKernelGGL((ca_lap_kernel<half_t>), dim3(gd(n)), dim3(256), 0, st, (const half_t*)x, lap, B, H, W);
   else

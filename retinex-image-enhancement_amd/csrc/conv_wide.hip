@@ -1569,6 +1569,14 @@ static int launch_hwide4_k(const ConvOp& op, hipStream_t st) {
 template <int BN, int W, int NCH>
 static int launch_hwide4(const ConvOp& op, hipStream_t st) {
   if (hw4_ds_ok(op)) {
+    if constexpr (BN == 256 && W == 64 && NCH == 4) {
+      // UPR_HW4_ABL: timing ablations of the bottleneck form (garbage results; profiles/r6_hw4_abl*)
+      static const int abl = [] { const char* e = getenv("UPR_HW4_ABL"); return e ? atoi(e) : 0; }();
+      if (!op.res1 && !op.res2 && abl == 1) return launch_hwide4_k<BN, W, NCH, 1, true, false, 4, 0, false, false, true>(op, st);
+      if (!op.res1 && !op.res2 && abl == 4) return launch_hwide4_k<BN, W, NCH, 4, true, false, 4, 0, false, false, true>(op, st);
+      if (!op.res1 && !op.res2 && abl == 5) return launch_hwide4_k<BN, W, NCH, 5, true, false, 4, 0, false, false, true>(op, st);
+      if (!op.res1 && !op.res2 && abl == 7) return launch_hwide4_k<BN, W, NCH, 7, true, false, 4, 0, false, false, true>(op, st);
+    }
     if (!op.res1 && !op.res2) return launch_hwide4_k<BN, W, NCH, 0, true, false, 4, 0, false, false, true>(op, st);
     return launch_hwide4_k<BN, W, NCH, 0, true>(op, st);
   }
@@ -1660,8 +1668,6 @@ static int hw4_s2_route(const ConvOp& op, hipStream_t st) {
 }
 
 static int halo_route(const ConvOp& op, hipStream_t st) {
-  // the bottleneck / ASPP-branch 3x3 convs: two blocks per CU (conv_hw2.hip)
-  if (const int rc = launch_conv_hw2(op, st); rc != kErrUnsupported) return rc;
   if (const int nsc = hw4_sc_ok(op)) {
     if (nsc == 1) return launch_hwide4_k<128, 128, 2, 0, true, false, 4, 1>(op, st);
     static const bool off = [] { const char* e = getenv("UPR_HW4_SC2"); return e && atoi(e) == 0; }();

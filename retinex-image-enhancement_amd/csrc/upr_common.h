@@ -127,9 +127,6 @@ int launch_conv_s2dg(const ConvOp& op, hipStream_t stream, bool probe = false);
 int launch_conv_pw(const ConvOp& op, hipStream_t stream, bool probe = false);
 
 int launch_conv(const ConvOp& op, int dtype, hipStream_t stream);
-// fp16 3x3 convs over 256 channels at W 64 on two 80 KiB blocks per CU
-// (conv_hw2.hip); kErrUnsupported for the shapes it does not take
-int launch_conv_hw2(const ConvOp& op, hipStream_t stream);
 
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 

@@ -89,6 +89,33 @@ def test_content_aware_enhancer():
     assert md(out, ref) <= 1e-3
 
 
+@pytest.mark.parametrize("B,H,W,dtype", [
+    (2, 96, 200, torch.float32),    # partial 32 x 64 tiles, every tile on an image border (reflected gray region)
+    (1, 160, 256, torch.float32),   # interior tiles (the 4-pixel quad loads of the fused saliency pass)
+    (2, 72, 132, torch.float16),    # fp16 storage
+    (1, 30, 50, torch.float32),     # smaller than one tile
+    (1, 31, 49, torch.float32),     # H * W odd: the three-kernel scalar form
+])
+def test_content_aware_maps_shapes(B, H, W, dtype):
+    """upr_content_aware saliency / attention / output per image vs the oracle
+    (oracle/enhancers.py, image by image): the fused 32 x 64-tile saliency pass
+    (gray -> |Laplacian| -> Gaussian rows -> columns in LDS) and the 4-pixel
+    attention / apply passes, or the scalar three-kernel form when H * W % 4."""
+    from upr import runtime
+    g = torch.Generator().manual_seed(H * W + B)
+    x = (torch.rand(B, 3, H, W, generator=g) * 0.6).to(dtype)
+    enh = torch.rand(B, 3, H, W, generator=g).to(dtype)
+    out, sal, att = runtime.content_aware(x.to(DEV), enh.to(DEV), saliency=True, attention=True)
+    torch.cuda.synchronize()
+    for b in range(B):
+        xb = x[b:b + 1].float()
+        assert md(sal[b], oenh.saliency_map(xb)[0, 0]) <= 1e-6, b
+        ab = oenh.attention_map(xb)[0, 0]
+        assert md(att[b], ab) <= 1e-5, b
+        ref = torch.clamp(enh[b].float() * (1.0 + 0.2 * ab), 0, 1)
+        assert md(out[b].float(), ref) <= (1e-5 if dtype == torch.float32 else 1e-3), b
+
+
 def test_enhance_harness_writes_outputs(tmp_path, golden):
     """enhance_single_image / enhance_batch_images on a real image crop (G4)."""
     from enhancers.simple_enhance import enhance_single_image, enhance_batch_images

@@ -59,14 +59,18 @@ def main():
     ms = timed(lambda: runtime.content_aware(x, enh), args.iters)
     px = B * S * S
     alg = 36.0 * px
-    # bytes the seven passes move: lap (x 12 in, 8 out), gauss rows (8 / 8), gauss cols (8 / 8),
-    # att (x 12 + lap 8 in, att 4 out), apply (att 4 + enh 12 in, 12 out); partials negligible
-    passes = (12 + 8) + (8 + 8) + (8 + 8) + (12 + 8 + 4) + (4 + 12 + 12)
+    # bytes the passes move (partials negligible); the three-kernel form: lap (x 12 in, 8 out), gauss rows
+    # (8 / 8), gauss cols (8 / 8), att (x 12 + lap 8 in, att 4 out), apply (att 4 + enh 12 in, 12 out)
+    fused = os.environ.get("UPR_CA_FUSED", "1") != "0" and (S * S) % 4 == 0
+    # fused: saliency (x 12 in, fp64 map 8 out), att (map 8 + x 12 in, att 4 out), apply (att 4 + enh 12 in, 12 out)
+    passes = (12 + 8) + (8 + 12 + 4) + (4 + 12 + 12) if fused else \
+        (12 + 8) + (8 + 8) + (8 + 8) + (12 + 8 + 4) + (4 + 12 + 12)
     print(json.dumps({"what": "content_aware", "batch": B, "size": S, "ms_per_call": ms, "images_per_s": B / ms * 1e3,
                       "alg_bytes": alg, "achieved_GBs": alg / ms / 1e6, "frac_hbm": alg / ms / 1e6 / PEAK_HBM_GBS,
                       "pass_bytes_per_px": passes, "pass_GBs": passes * px / ms / 1e6,
-                      "kernels": "ca_lap, ca_gauss_rows, ca_gauss_cols, reduce_minmax<double>, ca_att, "
-                                 "reduce_minmax<float>, ca_apply"}))
+                      "kernels": ("ca_sal_fused, reduce_minmax<double>, ca_att4, reduce_minmax<float>, ca_apply4"
+                                  if fused else "ca_lap, ca_gauss_rows, ca_gauss_cols, reduce_minmax<double>, ca_att, "
+                                                "reduce_minmax<float>, ca_apply")}))
     # letterbox: 1920 x 1080 u8 frames -> 640 (the reference default new_shape), auto padding
     import numpy as np
     frames = [np.random.default_rng(k).integers(0, 256, (1080, 1920, 3), dtype=np.uint8) for k in range(4)]
