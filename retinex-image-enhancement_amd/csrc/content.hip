@@ -145,24 +145,52 @@ __global__ __launch_bounds__(256) void ca_sal_fused_kernel(const T* __restrict__
   const size_t HW = (size_t)H * W;
   const T* img = x + (size_t)b * 3 * HW;
   const int gy0 = ty0 - CA_R - 1, gx0 = tx0 - CA_R - 1;
-  // (1) gray of the region; interior tiles load 4-pixel quads (gx0 is 8-aligned)
+  // (1) gray of the region; interior tiles load 4-pixel quads (gx0 is 8-aligned).
+  // Every load of a thread is issued before the first gray is formed (one HBM
+  // round trip per block: a runtime-trip-count loop waited for each quad's
+  // loads in turn and made this pass latency-bound)
   if (gy0 >= 0 && gx0 >= 0 && gy0 + CA_GH <= H && gx0 + CA_GW <= W && (W & 3) == 0) {
-    constexpr int QPR = CA_GW / 4, NQ = CA_GH * QPR;
-    for (int q = t; q < NQ; q += 256) {
+    constexpr int QPR = CA_GW / 4, NQ = CA_GH * QPR, NI = (NQ + 255) / 256;
+    float r[NI][4], gg[NI][4], bb[NI][4];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int q = t + 256 * i < NQ ? t + 256 * i : NQ - 1;
       const int ry = q / QPR, rq = q - ry * QPR;
       const size_t o = (size_t)(gy0 + ry) * W + gx0 + 4 * rq;
-      float r[4], gg[4], bb[4];
-      ld4<T>(img + o, r);
-      ld4<T>(img + HW + o, gg);
-      ld4<T>(img + 2 * HW + o, bb);
+      ld4<T>(img + o, r[i]);
+      ld4<T>(img + HW + o, gg[i]);
+      ld4<T>(img + 2 * HW + o, bb[i]);
+    }
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        gray[ry][4 * rq + k] = (quant_u8c(bb[k]) * 1868 + quant_u8c(gg[k]) * 9617 + quant_u8c(r[k]) * 4899 + (1 << 13)) >> 14;
+    for (int i = 0; i < NI; ++i) {
+      const int q = t + 256 * i;
+      if (q < NQ) {
+        const int ry = q / QPR, rq = q - ry * QPR;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          gray[ry][4 * rq + k] =
+              (quant_u8c(bb[i][k]) * 1868 + quant_u8c(gg[i][k]) * 9617 + quant_u8c(r[i][k]) * 4899 + (1 << 13)) >> 14;
+      }
     }
   } else {
-    for (int i = t; i < CA_GH * CA_GW; i += 256) {
+    constexpr int NP = CA_GH * CA_GW, NI = (NP + 255) / 256;
+    float r[NI], gg[NI], bb[NI];
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+      const int i = t + 256 * k < NP ? t + 256 * k : NP - 1;
       const int ry = i / CA_GW, rx = i - ry * CA_GW;
-      gray[ry][rx] = gray_at(img, H, W, refl101(gy0 + ry, H), refl101(gx0 + rx, W));
+      const size_t o = (size_t)refl101(gy0 + ry, H) * W + refl101(gx0 + rx, W);
+      r[k] = ldf(img, o);
+      gg[k] = ldf(img, HW + o);
+      bb[k] = ldf(img, 2 * HW + o);
+    }
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+      const int i = t + 256 * k;
+      if (i < NP) {
+        const int ry = i / CA_GW, rx = i - ry * CA_GW;
+        gray[ry][rx] = (quant_u8c(bb[k]) * 1868 + quant_u8c(gg[k]) * 9617 + quant_u8c(r[k]) * 4899 + (1 << 13)) >> 14;
+      }
     }
   }
   __syncthreads();
@@ -173,28 +201,43 @@ __global__ __launch_bounds__(256) void ca_sal_fused_kernel(const T* __restrict__
     lap[ly][lx] = fabs((double)(gray[ly][lx + 1] + gray[ly + 1][lx] - 4 * c + gray[ly + 1][lx + 2] + gray[ly + 2][lx + 1]));
   }
   __syncthreads();
-  // (3) rows: s = k0*S[x-7] + k1*S[x-6] + ... (ca_gauss_rows' order)
-  const int col = t & 63, r0 = t >> 6;
-  for (int ly = r0; ly < CA_LH; ly += 4) {
-    double acc = g.k[0] * lap[ly][col];
+  // (3) rows: s = k0*S[x-7] + k1*S[x-6] + ... (ca_gauss_rows' order); a thread
+  // takes 4 consecutive outputs of a row from one 18-value window in registers
+  // (15 LDS reads per output were the pass's limit)
+  for (int sgi = t; sgi < CA_LH * (CA_TW / 4); sgi += 256) {
+    const int ly = sgi / (CA_TW / 4), x0 = (sgi % (CA_TW / 4)) * 4;
+    double w[18];
 #pragma unroll
-    for (int k = 1; k < 15; ++k) acc += g.k[k] * lap[ly][col + k];
-    rowg[ly][col] = acc;
+    for (int i = 0; i < 18; ++i) w[i] = lap[ly][x0 + i];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      double acc = g.k[0] * w[o];
+#pragma unroll
+      for (int k = 1; k < 15; ++k) acc += g.k[k] * w[o + k];
+      rowg[ly][x0 + o] = acc;
+    }
   }
   __syncthreads();
-  // (4) columns: s = ky[7]*S[y] + 0.0; s += ky[7+k]*(S[y+k] + S[y-k])
+  // (4) columns: s = ky[7]*S[y] + 0.0; s += ky[7+k]*(S[y+k] + S[y-k]); a thread
+  // takes 8 consecutive outputs of one column from a 22-value window
   double mn = DBL_MAX, mx = -DBL_MAX;
-  const int xx = tx0 + col;
+  {
+    const int col = t & 63, yb = (t >> 6) * 8;
+    const int xx = tx0 + col;
+    double w[22];
 #pragma unroll
-  for (int j = 0; j < CA_TH / 4; ++j) {
-    const int yy = r0 + 4 * j, y = ty0 + yy;
-    double acc = g.k[7] * rowg[yy + CA_R][col] + 0.0;
+    for (int i = 0; i < 22; ++i) w[i] = rowg[yb + i][col];
 #pragma unroll
-    for (int k = 1; k <= 7; ++k) acc += g.k[7 + k] * (rowg[yy + CA_R + k][col] + rowg[yy + CA_R - k][col]);
-    if (y < H && xx < W) {
-      sal[(size_t)b * HW + (size_t)y * W + xx] = acc;
-      mn = fmin(mn, acc);
-      mx = fmax(mx, acc);
+    for (int o = 0; o < 8; ++o) {
+      const int y = ty0 + yb + o;
+      double acc = g.k[7] * w[o + CA_R] + 0.0;
+#pragma unroll
+      for (int k = 1; k <= 7; ++k) acc += g.k[7 + k] * (w[o + CA_R + k] + w[o + CA_R - k]);
+      if (y < H && xx < W) {
+        sal[(size_t)b * HW + (size_t)y * W + xx] = acc;
+        mn = fmin(mn, acc);
+        mx = fmax(mx, acc);
+      }
     }
   }
 #pragma unroll

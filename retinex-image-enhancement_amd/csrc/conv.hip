@@ -18,6 +18,7 @@
 // across MFMA k-slots is the same for A and B, so the sum is unchanged.
 #include <cstdlib>
 #include <cstring>
+#include <cstdio>
 
 #include "upr_common.h"
 
@@ -393,16 +394,28 @@ int launch_conv_t2(const ConvOp& op, int dtype, hipStream_t st);
 
 int launch_preact_f16(const void* x, const float* sc, const float* sh, void* o, size_t npix, int C, hipStream_t st);
 
+// UPR_TRACE_ROUTE=1: one stderr line per fp16 conv call naming the kernel family
+// it fell to and its shape (tools: which training convs still take a fallback)
+static void trace_route(const char* fam, const ConvOp& op) {
+  static const bool on = [] { const char* e = getenv("UPR_TRACE_ROUTE"); return e && atoi(e) != 0; }();
+  if (!on) return;
+  const ConvSeg& s = op.seg[0];
+  fprintf(stderr, "upr_route %s nseg %d B %d Cin %d Hin %d Win %d -> N %d Ho %d Wo %d k %dx%d s %d p %d d %d pre %d "
+                  "out32 %d res %d relu %d\n", fam, op.nseg, op.B, s.C, s.Hin, s.Win, op.N, op.Ho, op.Wo, s.kh, s.kw,
+          s.stride, s.pad, s.dil, s.pre, op.out32 != nullptr, op.res1 != nullptr || op.res2 != nullptr, op.relu);
+}
+
 int launch_conv_out32(const ConvOp& op, hipStream_t stream) {
   if (!op.out32 || op.out || op.out2 || op.pool || op.store == kStoreHeadIllu) return kErrArg;
   if (op.nseg < 1 || op.nseg > 4 || op.B <= 0 || op.Ho <= 0 || op.Wo <= 0) return kErrArg;
   // narrow 1x1 GEMMs stream (conv_pw.hip); the stride-2 scatter form exists only there
   int rc = launch_conv_pw(op, stream);
-  if (rc != kErrUnsupported || op.out_s2) return rc;
+  if (rc != kErrUnsupported || op.out_s2) return trace_route("pw", op), rc;
   rc = launch_conv_wide(op, stream);
-  if (rc != kErrUnsupported) return rc;
+  if (rc != kErrUnsupported) return trace_route("wide", op), rc;
   rc = launch_conv_ring(op, stream);
-  if (rc != kErrUnsupported) return rc;
+  if (rc != kErrUnsupported) return trace_route("ring", op), rc;
+  trace_route("halo", op);
   return launch_conv_halo(op, kF16, stream);
 }
 
@@ -430,11 +443,11 @@ int launch_conv(const ConvOp& op, int dtype, hipStream_t stream) {
   {
     if (dtype == kF16) {
       int rc = launch_conv_t2(op, dtype, stream);
-      if (rc != kErrUnsupported) return rc;
+      if (rc != kErrUnsupported) return trace_route("t2", op), rc;
       rc = launch_conv_wide(op, stream);
-      if (rc != kErrUnsupported) return rc;
+      if (rc != kErrUnsupported) return trace_route("wide", op), rc;
       rc = launch_conv_ring(op, stream);
-      if (rc != kErrUnsupported) return rc;
+      if (rc != kErrUnsupported) return trace_route("ring", op), rc;
     } else {
       // 32 -> 64 3x3 without a residual (EnhancedFAM branch34_conv1): the fp32
       // ring with its filter in registers first (measured 2.80 -> 2.53 ms at
@@ -448,8 +461,9 @@ int launch_conv(const ConvOp& op, int dtype, hipStream_t stream) {
       if (rc != kErrUnsupported) return rc;
     }
     const int rc = launch_conv_halo(op, dtype, stream);
-    if (rc != kErrUnsupported) return rc;
+    if (rc != kErrUnsupported) return trace_route("halo", op), rc;
   }
+  trace_route("igemm", op);
   return dtype == kF16 ? launch_t<half_t>(op, stream) : launch_t<float>(op, stream);
 }
 

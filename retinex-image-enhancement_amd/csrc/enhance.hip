@@ -10,6 +10,8 @@
 //  gray_hist      8-bit BGR2GRAY histogram (calculate_brightness_features :45-66)
 //  ms_sums        multi-scale feature sums (enhancers/multi_scale.py:17-60, :87-94)
 //  scale_clamp    clamp(enh * factor[b], 0, 1)  (multi_scale.py:97-98)
+#include <utility>
+
 #include "upr_common.h"
 #include "lab_tables.h"
 
@@ -837,6 +839,261 @@ __global__ __launch_bounds__(256) void ms_sums3_kernel(const T* __restrict__ x, 
   if (t < 3) part[((size_t)b * gridDim.x + tin) * 3 + t] = red[0][t] + red[1][t] + red[2][t] + red[3][t];
 }
 
+// Register-streaming form of the one-pass multi-scale sums (round 6): one
+// WAVE owns a strip of 256 full-resolution columns (a 4-pixel quad per lane)
+// of a band of MSR_BH rows and walks the band's rows top to bottom (plus 3
+// halo rows above and below), all three scales from registers -- no LDS, no
+// barriers.  Row j's quads arrive MSR_PF rows ahead of their use; full-row
+// features take the rows above / below from the register window and the
+// left / right neighbour columns from the adjacent lanes (DPP wave_shr:1 /
+// wave_shl:1), lane 0 / 63 from a quad of the neighbouring strip that only they
+// load.  Half samples (rows 2h, 2h + 1, columns 2c, 2c + 1) and quarter samples
+// (rows 4q + 1, 4q + 2, columns 4c + 1, 4c + 2) are blended in registers as rows
+// complete and take their neighbours the same way.  Per pixel the arithmetic
+// is ms_quad's (bit-identical features); the wave's three fp64 sums go to its
+// partial slot, ms_fin_kernel adds an image's slots in order.  (The tiled
+// ms_sums3_kernel staged a 40 x 72 region, its half / quarter planes and ran
+// three barrier-separated phases per block: 44 us for 32 x 512^2.)
+constexpr int MSR_BH = 16, MSR_PF = 2, MSR_NR = MSR_BH + 6;
+
+template <typename F, int... S>
+__device__ __forceinline__ void ms_steps(F&& f, std::integer_sequence<int, S...>) {
+  (f(std::integral_constant<int, S>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void ms_sfor(F&& f) {  // f(0) .. f(N - 1), each index a compile-time constant
+  ms_steps(f, std::make_integer_sequence<int, N>{});
+}
+
+__device__ __forceinline__ float wave_from_left(float v, float edge) {  // lane i <- lane i - 1; lane 0 <- edge
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(edge), __float_as_int(v), 0x138, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_from_right(float v, float edge) {  // lane i <- lane i + 1; lane 63 <- edge
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(edge), __float_as_int(v), 0x130, 0xF, 0xF, false));
+}
+
+// features of N consecutive pixels of one row (c[ch][k], neighbours l / r of
+// the first / last, rows u / d above / below), ms_quad's expression per pixel
+// a value select (an lvalue ?: between array elements became a pointer phi
+// that kept the arrays in scratch)
+__device__ __forceinline__ float fsel(bool p, float a, float b) { return p ? a : b; }
+
+template <int N>
+__device__ __forceinline__ double ms_row_feat(const float (&c)[3][N], const float (&u)[3][N], const float (&d)[3][N],
+                                              const float (&l)[3], const float (&r)[3], int y, int x, int hs, int ws) {
+  // y is wave-uniform: rows off the image contribute nothing, and only the
+  // image's first / last row takes the one-sided vertical difference (a
+  // uniform branch); horizontally (W % 4 == 0, aligned quads) only a run's
+  // first pixel can sit on column 0 and only its last on column ws - 1, and a
+  // run lies wholly inside or outside the image
+  if (y < 0 || y >= hs) return 0.0;
+  const bool top = y == 0, bot = y >= hs - 1;
+  float fs[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) fs[k] = 0.f;
+  auto body = [&](auto VB_) {
+    constexpr bool VB = decltype(VB_)::value;  // vertical border row
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      ms_sfor<N>([&](auto K_) {
+        constexpr int k = decltype(K_)::value;
+        float vl, vr;
+        if constexpr (k == 0) vl = l[ch]; else vl = c[ch][k - 1];
+        if constexpr (k == N - 1) vr = r[ch]; else vr = c[ch][k + 1];
+        const float v = c[ch][k];
+        float gx;
+        if constexpr (k == 0 || k == N - 1) {
+          const bool lft = k == 0 && x == 0, rgt = k == N - 1 && x + k >= ws - 1;
+          const float a = fsel(lft, v, vl), b = fsel(rgt, v, vr);
+          gx = (b - a) * fsel(lft || rgt, 1.f, 0.5f);
+        } else {
+          gx = (vr - vl) * 0.5f;
+        }
+        float gy;
+        if constexpr (VB) {
+          const float uu = fsel(top, v, u[ch][k]), dd = fsel(bot, v, d[ch][k]);
+          gy = (dd - uu) * fsel(top || bot, 1.f, 0.5f);
+        } else {
+          gy = (d[ch][k] - u[ch][k]) * 0.5f;
+        }
+        fs[k] += v + __builtin_amdgcn_sqrtf(gx * gx + gy * gy);
+      });
+    }
+  };
+  if (top || bot) body(std::true_type{});
+  else body(std::false_type{});
+  double a = 0.0;
+  if (x < ws) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) a += (double)(fs[k] + (0.299f * c[0][k] + 0.587f * c[1][k] + 0.114f * c[2][k]));
+  }
+  return a;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256, 2) void ms_rows_kernel(const T* __restrict__ x, double* __restrict__ part, int B,
+                                                      int H, int W, int strips, int nwav) {
+  const int lane = threadIdx.x & 63;
+  // waves in XCD-contiguous order over (image, wave): blocks i, i + 8, ... share
+  // an XCD and take neighbouring bands, whose halo rows then hit that L2
+  const int nb = gridDim.x, bid = blockIdx.x;
+  const int q8 = nb >> 3, r8 = nb & 7, xcd = bid & 7, k8 = bid >> 3;
+  const int blk = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + k8;
+  // global wave = image * nwav + wave; readfirstlane: everything derived from
+  // it is wave-uniform (SGPRs), or every buffer load became a waterfall loop
+  const int gw = blk * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int b = gw / nwav, wv = gw - b * nwav;
+  if (b >= B) return;  // (the last block's spare waves)
+  const int band = wv / strips, strip = wv - band * strips;
+  const int y0 = band * MSR_BH, xs = strip * 256, xq = xs + 4 * lane;
+  const int hs1 = H / 2, ws1 = W / 2, hs2 = H / 4, ws2 = W / 4;
+  const size_t HW = (size_t)H * W;
+  const T* img = x + (size_t)b * 3 * HW;
+  const bool qin = xq < W;
+  // the neighbouring strip's quad of the edge lanes: lane 0 cols xs - 4 .. xs - 1, lane 63 xs + 256 .. + 259
+  const int xe = lane == 0 ? xs - 4 : xs + 256;  // (fp32 reads 3 columns from xe + 1 / xe on lane 0 / 63)
+  const bool ein = (lane == 0 || lane == 63) && xe >= 0 && xe < W;
+  // row j of the window = image row y0 - 3 + j; V: the lane's quad, E: the edge quad's
+  // three columns that the neighbours use (lane 0: xs - 3, xs - 2, xs - 1; lane 63: xs + 256 .. + 258)
+  float V[MSR_NR][3][4], E[MSR_NR][3][3];
+  // loads are unconditional, from clamped (always valid) addresses, and zeroed
+  // by a select after the fact: a load under a divergent branch came with a
+  // vmcnt(0) at the branch's merge, serialising every row's loads.  They are
+  // buffer loads: a per-lane 32-bit column offset fixed for the wave + a
+  // wave-uniform row offset (64-bit per-lane addresses for every row of the
+  // unrolled walk took 264 registers)
+  // the buffer's range is the image: a lane whose quad lies off the image (and
+  // every lane but 0 / 63 for the edge load) reads at an offset past it, which
+  // returns zeros without a memory access
+  const int ib = 3 * (int)HW * (int)sizeof(T);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)img, 0, ib, 0x00020000);
+  constexpr int kOff = 0x40000000;
+  const int vq = qin ? xq * (int)sizeof(T) : kOff;
+  const int ve = ein ? (sizeof(T) == 4 && lane == 0 ? xe + 1 : xe) * (int)sizeof(T) : kOff;
+  auto bld = [&](int voff, int soff, float (&v)[4]) {
+    if constexpr (sizeof(T) == 4) {
+      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0);
+      v[0] = __uint_as_float(q[0]); v[1] = __uint_as_float(q[1]); v[2] = __uint_as_float(q[2]); v[3] = __uint_as_float(q[3]);
+    } else {
+      typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+      typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+      const u32x2 q = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0);
+      const h4 hv = __builtin_bit_cast(h4, q);
+      v[0] = (float)hv[0]; v[1] = (float)hv[1]; v[2] = (float)hv[2]; v[3] = (float)hv[3];
+    }
+  };
+  auto load_row = [&](auto J_) {
+    constexpr int j = decltype(J_)::value;
+    const int y = y0 - 3 + j;
+    const bool yin = y >= 0 && y < H;  // (wave-uniform)
+    // rows off the image: every lane's offset out of range (the range check is
+    // on the per-lane offset; the row's soffset stays a valid one)
+    const int ro = yin ? y * W : 0;
+    const int vqr = yin ? vq : kOff, ver = yin ? ve : kOff;
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      float v[4];
+      const int so = (ch * (int)HW + ro) * (int)sizeof(T);
+      bld(vqr, so, v);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) V[j][ch][k] = v[k];
+      if constexpr (sizeof(T) == 4) {
+        // the three edge columns straight from one 12-byte load (lane 0: xs - 3 ..; lane 63: xs + 256 ..)
+        typedef unsigned u32x3 __attribute__((ext_vector_type(3)));
+        const u32x3 q = __builtin_amdgcn_raw_buffer_load_b96(rs, ver, so, 0);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) E[j][ch][k] = __uint_as_float(q[k]);
+      } else {
+        float e[4];
+        bld(ver, so, e);
+        const bool l0 = lane == 0;
+        E[j][ch][0] = fsel(l0, e[1], e[0]);
+        E[j][ch][1] = fsel(l0, e[2], e[1]);
+        E[j][ch][2] = fsel(l0, e[3], e[2]);
+      }
+    }
+  };
+  // half samples: sample row k (k = 0 .. MSR_BH / 2 + 1) = half row y0 / 2 - 1 + k from window rows 1 + 2k, 2 + 2k;
+  // quarter sample row k (k = 0 .. MSR_BH / 4 + 1) = quarter row y0 / 4 - 1 + k from window rows 4k, 4k + 1
+  float S1[MSR_BH / 2 + 2][3][2], S1e[MSR_BH / 2 + 2][3];  // the lane's 2 half pixels, the edge lane's neighbour
+  float S2[MSR_BH / 4 + 2][3], S2e[MSR_BH / 4 + 2][3];
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+  ms_sfor<MSR_PF + 1>([&](auto J_) { load_row(J_); });
+  ms_sfor<MSR_NR>([&](auto J_) {
+    constexpr int j = decltype(J_)::value;
+    // (a compiler-only fence per row: without it every row's loads were hoisted
+    // to the top -- 316 registers, one wave per SIMD)
+    asm volatile("" ::: "memory");
+    if constexpr (j + MSR_PF + 1 < MSR_NR) load_row(std::integral_constant<int, j + MSR_PF + 1>{});
+    // full features of window row j - 1 (image rows y0 .. y0 + MSR_BH - 1: j - 1 in 3 .. MSR_BH + 2)
+    if constexpr (j - 1 >= 3 && j - 1 < MSR_BH + 3) {
+      constexpr int m = j - 1;
+      float l[3], r[3];
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {
+        l[ch] = wave_from_left(V[m][ch][3], E[m][ch][2]);
+        r[ch] = wave_from_right(V[m][ch][0], E[m][ch][0]);
+      }
+      a0 += ms_row_feat<4>(V[m], V[m - 1], V[m + 1], l, r, y0 - 3 + m, xq, H, W);
+    }
+    // half sample row k once window row 2 + 2k is in
+    if constexpr (j >= 2 && j % 2 == 0) {
+      constexpr int k = (j - 2) / 2;
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {
+        S1[k][ch][0] = blend_half(V[j - 1][ch][0], V[j - 1][ch][1], V[j][ch][0], V[j][ch][1]);
+        S1[k][ch][1] = blend_half(V[j - 1][ch][2], V[j - 1][ch][3], V[j][ch][2], V[j][ch][3]);
+        const bool l0 = lane == 0;  // (value selects: a ?: of two blend calls became pointer phis into scratch)
+        S1e[k][ch] = blend_half(fsel(l0, E[j - 1][ch][1], E[j - 1][ch][0]), fsel(l0, E[j - 1][ch][2], E[j - 1][ch][1]),
+                                fsel(l0, E[j][ch][1], E[j][ch][0]), fsel(l0, E[j][ch][2], E[j][ch][1]));
+      }
+      // half features of sample row k - 1 (half rows y0 / 2 .. y0 / 2 + MSR_BH / 2 - 1: k - 1 in 1 .. MSR_BH / 2)
+      if constexpr (k - 1 >= 1 && k - 1 <= MSR_BH / 2) {
+        constexpr int m = k - 1;
+        float l[3], r[3];
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+          l[ch] = wave_from_left(S1[m][ch][1], S1e[m][ch]);
+          r[ch] = wave_from_right(S1[m][ch][0], S1e[m][ch]);
+        }
+        a1 += ms_row_feat<2>(S1[m], S1[m - 1], S1[m + 1], l, r, y0 / 2 - 1 + m, xq / 2, hs1, ws1);
+      }
+    }
+    // quarter sample row k once window row 4k + 1 is in
+    if constexpr (j % 4 == 1) {
+      constexpr int k = (j - 1) / 4;
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {
+        S2[k][ch] = blend_half(V[j - 1][ch][1], V[j - 1][ch][2], V[j][ch][1], V[j][ch][2]);
+        const bool l0 = lane == 0;
+        S2e[k][ch] = blend_half(fsel(l0, E[j - 1][ch][0], E[j - 1][ch][1]), fsel(l0, E[j - 1][ch][1], E[j - 1][ch][2]),
+                                fsel(l0, E[j][ch][0], E[j][ch][1]), fsel(l0, E[j][ch][1], E[j][ch][2]));
+      }
+      if constexpr (k - 1 >= 1 && k - 1 <= MSR_BH / 4) {
+        constexpr int m = k - 1;
+        float l[3], r[3], c1[3][1], u1[3][1], d1[3][1];
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+          l[ch] = wave_from_left(S2[m][ch], S2e[m][ch]);
+          r[ch] = wave_from_right(S2[m][ch], S2e[m][ch]);
+          c1[ch][0] = S2[m][ch];
+          u1[ch][0] = S2[m - 1][ch];
+          d1[ch][0] = S2[m + 1][ch];
+        }
+        a2 += ms_row_feat<1>(c1, u1, d1, l, r, y0 / 4 - 1 + m, xq / 4, hs2, ws2);
+      }
+    }
+  });
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a0 += __shfl_xor(a0, o, 64);
+    a1 += __shfl_xor(a1, o, 64);
+    a2 += __shfl_xor(a2, o, 64);
+  }
+  if (lane < 3) part[((size_t)b * nwav + wv) * 3 + lane] = lane == 0 ? a0 : lane == 1 ? a1 : a2;
+}
+
 // per image: the tile partials of ms_sums3_kernel added in a fixed order (one
 // block per image; deterministic fp64), then sums and the factor
 __global__ __launch_bounds__(256) void ms_fin_kernel(const double* __restrict__ part, int nblk, double* __restrict__ sums,
@@ -1057,7 +1314,23 @@ int launch_multiscale(const void* x, const void* enh, void* out, double* sums, d
     fac = (double*)scratch(kSlotTmp, sizeof(double) * B, st);
     if (!fac) return (int)hipErrorOutOfMemory;
   }
-  if (H % 4 == 0 && W % 4 == 0 && (uintptr_t)x % (dtype == kF16 ? 8 : 16) == 0) {
+  // UPR_MS_ROWS=0: the tiled single pass (ms_sums3_kernel) instead of the register-streaming one (A/B)
+  static const bool rows = [] { const char* e = getenv("UPR_MS_ROWS"); return !e || atoi(e) != 0; }();
+  if (rows && H % 4 == 0 && W % 4 == 0 && (uintptr_t)x % (dtype == kF16 ? 8 : 16) == 0) {
+    const int strips = (W + 255) / 256, nwav = strips * ((H + MSR_BH - 1) / MSR_BH);
+    double* part = (double*)scratch(kSlotMs, (size_t)B * nwav * 3 * sizeof(double), st);
+    if (!part) return (int)hipErrorOutOfMemory;
+    const int nblk = (B * nwav + 3) / 4;
+    if (dtype == kF16)
+      hipLaunchKernelGGL((ms_rows_kernel<half_t>), dim3(nblk), dim3(256), 0, st, (const half_t*)x, part, B, H, W,
+                         strips, nwav);
+    else
+      hipLaunchKernelGGL((ms_rows_kernel<float>), dim3(nblk), dim3(256), 0, st, (const float*)x, part, B, H, W, strips,
+                         nwav);
+    UPR_CHECK_HIP(hipGetLastError());
+    hipLaunchKernelGGL(ms_fin_kernel, dim3(B), dim3(256), 0, st, (const double*)part, nwav, sums, fac, n0, n1, n2);
+    UPR_CHECK_HIP(hipGetLastError());
+  } else if (H % 4 == 0 && W % 4 == 0 && (uintptr_t)x % (dtype == kF16 ? 8 : 16) == 0) {
     // single pass (ms_sums3_kernel): per-tile partials in a scratch slot,
     // added in order by ms_fin_kernel.  (A streamed form -- 64-column strips
     // walked in 4-row bands through LDS row rings, one band of prefetch --

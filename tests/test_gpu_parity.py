@@ -355,8 +355,8 @@ def test_multiscale_kernel(golden):
     (32, 512, 512, torch.float32),  # the bench's enhance leg (images 0 and 31 checked)
 ])
 def test_multiscale_single_pass(B, H, W, dtype):
-    """upr_multiscale's one-pass kernel (ms_sums3_kernel: all three scales from
-    one read, per-tile partials added in order by ms_fin_kernel) vs the
+    """upr_multiscale's one-pass kernel (ms_rows_kernel: all three scales from
+    one read, per-wave partials added in order by ms_fin_kernel) vs the
     oracle's per-image factor (multi_scale.py:62-100), called three times in a
     row (the three results must be bit-identical)."""
     from upr import runtime
@@ -374,6 +374,33 @@ def test_multiscale_single_pass(B, H, W, dtype):
         assert abs(f0[b].item() - fac[j]) < 1e-6, (b, f0[b].item(), fac[j])
         ref = torch.clamp(enh[b].float() * fac[j], 0, 1)
         assert maxdiff(out0[b].float(), ref) <= (1e-6 if dtype == torch.float32 else 1e-3)
+
+
+@pytest.mark.parametrize("B,H,W,dtype", [
+    (1, 64, 520, torch.float32),    # three 256-column strips, the last one 8 pixels wide
+    (2, 36, 300, torch.float32),    # partial 16-row band, partial strip
+    (2, 100, 136, torch.float32),
+    (1, 48, 256, torch.float16),
+    (1, 16, 1024, torch.float32),   # one band, four strips: every strip edge interior
+])
+def test_multiscale_sums_vs_feature_maps(B, H, W, dtype):
+    """The per-scale feature sums of upr_multiscale's one-pass kernel
+    (ms_rows_kernel: 256-column strips walked row by row in registers, the
+    strip-edge neighbours from the edge lanes' extra quads) against the fp64
+    sums of the oracle's seven feature maps per scale (multi_scale.py:17-60):
+    per pixel the features agree to the gradient magnitude's square root
+    (hardware, <= 1 ulp), so the sums to 1e-6 relative -- a wrong neighbour
+    column at one strip edge moves them by ~1e-5."""
+    from upr import runtime
+    x = torch.rand(B, 3, H, W, generator=torch.Generator().manual_seed(H + W)).to(dtype)
+    _, _, sums = runtime.multiscale(x.to(DEV))
+    torch.cuda.synchronize()
+    for b in range(B):
+        feats = oenh.multiscale_features(x[b:b + 1].float())
+        for i, f in enumerate(feats):
+            ref = f.double().sum().item()
+            got = sums[b, i].item()
+            assert abs(got - ref) <= 1e-6 * abs(ref), (b, i, got, ref)
 
 
 # ---------------------------------------------------------------------------
