@@ -80,13 +80,14 @@ enum RingMode : int { kRingConv = 0, kRingHead = 1, kRingFam = 2, kRingS2 = 3 };
 // kRingWide: 64-pixel strips (4 pixel groups per wave row): twice the MFMAs per
 // step for the same per-step barrier / DMA / cursor work (32 -> 32 convs)
 // kRingOut2: the epilogue also writes relu(fma(o, pre2_scale, pre2_shift)) (ConvOp::out2)
-// kRingOut32: fp32 output (ConvOp::out32, no res32) instead of the fp16 store
+// kRingOut32: fp32 output (ConvOp::out32) instead of the fp16 store; kRingR32:
+// + ConvOp::res32 (an accumulated fp32 input gradient) in that epilogue
 // fp32 ring only: kRingDil2 = the segment is a 3x3 dilation-2 conv (2-pixel halo ring);
 // kRingResPre = the residual is ConvOp::res1 (added before the ReLU) instead of
 // res2 (after it); kRingPool = per-image channel sums of the output into ConvOp::pool
 enum RingFlags : int {
   kRingRes = 1, kRingRelu = 2, kRingSc = 4, kRingOcc3 = 8, kRingWide = 16, kRingOut2 = 32, kRingOut32 = 64,
-  kRingDil2 = 128, kRingResPre = 256, kRingPool = 512, kRingXPool = 1024,
+  kRingDil2 = 128, kRingResPre = 256, kRingPool = 512, kRingXPool = 1024, kRingR32 = 2048,
   // timing ablations only (results garbage; UPR_RING_ABL, tools/convbench.py):
   // no ring DMA after the first two steps / no MFMAs / no output stores
   kRingAblDma = 4096, kRingAblMma = 8192, kRingAblSt = 16384
@@ -237,6 +238,8 @@ struct RingCfg {
   static constexpr int G = RA::G + (FAM ? RB::G : 0);              // ring DMA per step (waves 0-3)
   static constexpr bool OUT2 = (FL & kRingOut2) != 0;
   static constexpr bool OUT32 = (FL & kRingOut32) != 0;
+  static constexpr bool R32 = (FL & kRingR32) != 0;
+  static_assert(!R32 || OUT32, "res32 with the fp32 output");
   static_assert(!OUT32 || (!RES && !SC && !OUT2 && MODE != kRingHead && MODE != kRingFam), "fp32 output: plain convs");
   // stores per wave per step: one 16-byte store per fragment pair (ring_ch),
   // two with OUT2; OUT32 issues one or two more (its fp32 halves / fp16 copy,
@@ -731,18 +734,31 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, RingCfg<MODE, C, NB, FL
             o = __builtin_bit_cast(f16x8_r, w);
           }
           if constexpr (K::OUT32) {
-            if (op.mask16 && ovalid[g]) {
-              const half_t* mk = (const half_t*)op.mask16 + prow * op.mask16_cs +
-                                 (size_t)((g0 + g) * 16 + fr) * op.mask16_cs + fg * 8 + p * 32;
-              const f16x8_r mv = *(const f16x8_r*)mk;
-#pragma unroll
-              for (int i = 0; i < 8; ++i) o[i] = (float)mv[i] > 0.f ? o[i] : (half_t)0.f;
-            }
+            // (float)(fp16 result) + res32, zeroed where mask16 <= 0 (the order
+            // of direct_epilogue); the fp16 copy is the fp32 value stored
             f32x4_r o32a, o32b;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               o32a[i] = (float)o[i];
               o32b[i] = (float)o[4 + i];
+            }
+            if constexpr (K::R32) {
+              if (ovalid[g]) {
+                const float* r32 =
+                    op.res32 + prow * op.res32_cs + (size_t)((g0 + g) * 16 + fr) * op.res32_cs + fg * 8 + p * 32;
+                o32a += *(const f32x4_r*)r32;
+                o32b += *(const f32x4_r*)(r32 + 4);
+              }
+            }
+            if (op.mask16 && ovalid[g]) {
+              const half_t* mk = (const half_t*)op.mask16 + prow * op.mask16_cs +
+                                 (size_t)((g0 + g) * 16 + fr) * op.mask16_cs + fg * 8 + p * 32;
+              const f16x8_r mv = *(const f16x8_r*)mk;
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                o32a[i] = (float)mv[i] > 0.f ? o32a[i] : 0.f;
+                o32b[i] = (float)mv[4 + i] > 0.f ? o32b[i] : 0.f;
+              }
             }
             float* d32 = ovalid[g] ? op.out32 + prow * op.out32_cs + op.out32_coff +
                                          (size_t)((g0 + g) * 16 + fr) * op.out32_cs + fg * 8
@@ -751,11 +767,17 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, RingCfg<MODE, C, NB, FL
               *(f32x4_r*)(d32 + p * 32) = o32a;
               *(f32x4_r*)(d32 + p * 32 + 4) = o32b;
             }
-            if (op.out32_h16) {  // compact fp16 copy: o itself (no res32 on the ring)
+            if (op.out32_h16) {
+              f16x8_r h;
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                h[i] = (half_t)o32a[i];
+                h[4 + i] = (half_t)o32b[i];
+              }
               half_t* d16 = ovalid[g] ? (half_t*)op.out32_h16 + prow * op.out32_h16_cs +
                                             (size_t)((g0 + g) * 16 + fr) * op.out32_h16_cs + fg * 8
                                       : (half_t*)(g_ring_sink + tid * 16);
-              *(uint4*)(d16 + p * 32) = __builtin_bit_cast(uint4, o);
+              *(uint4*)(d16 + p * 32) = __builtin_bit_cast(uint4, h);
             }
           } else {
             *(uint4*)(dg + p * 32) = __builtin_bit_cast(uint4, o);
@@ -803,26 +825,32 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, RingCfg<MODE, C, NB, FL
               if (ovalid[g]) pool[nt][i] += (float)o[i];
           }
           if constexpr (K::OUT32) {
+            f32x4_r o32;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o32[i] = (float)o[i];
+            if constexpr (K::R32) {
+              if (ovalid[g])
+                o32 += *(const f32x4_r*)(op.res32 + prow * op.res32_cs + (size_t)((g0 + g) * 16 + fr) * op.res32_cs +
+                                         fg * 4 + nt * 16);
+            }
             if (op.mask16 && ovalid[g]) {
               const half_t* mk = (const half_t*)op.mask16 + prow * op.mask16_cs +
                                  (size_t)((g0 + g) * 16 + fr) * op.mask16_cs + fg * 4 + nt * 16;
               const uint2 mw = *(const uint2*)mk;
               const f16x4_r mv = __builtin_bit_cast(f16x4_r, mw);
 #pragma unroll
-              for (int i = 0; i < 4; ++i) o[i] = (float)mv[i] > 0.f ? o[i] : (half_t)0.f;
+              for (int i = 0; i < 4; ++i) o32[i] = (float)mv[i] > 0.f ? o32[i] : 0.f;
             }
-            f32x4_r o32;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) o32[i] = (float)o[i];
             float* d32 = ovalid[g] ? op.out32 + prow * op.out32_cs + op.out32_coff +
                                          (size_t)((g0 + g) * 16 + fr) * op.out32_cs + fg * 4
                                    : g_ring_sink32 + tid * 64;
             if (!op.skip32) *(f32x4_r*)(d32 + nt * 16) = o32;
-            if (op.out32_h16) {  // compact fp16 copy: o itself (no res32 on the ring)
+            if (op.out32_h16) {
+              const f16x4_r h = {(half_t)o32[0], (half_t)o32[1], (half_t)o32[2], (half_t)o32[3]};
               half_t* d16 = ovalid[g] ? (half_t*)op.out32_h16 + prow * op.out32_h16_cs +
                                             (size_t)((g0 + g) * 16 + fr) * op.out32_h16_cs + fg * 4
                                       : (half_t*)(g_ring_sink + tid * 16);
-              *(uint2*)(d16 + nt * 16) = __builtin_bit_cast(uint2, o);
+              *(uint2*)(d16 + nt * 16) = __builtin_bit_cast(uint2, h);
             }
           } else {
             *(uint2*)(dg + nt * 16) = __builtin_bit_cast(uint2, o);
@@ -1368,8 +1396,10 @@ int launch_conv_ring(const ConvOp& op, hipStream_t st) {
   if (op.Ho < 4 || op.Wo < 16) return kErrUnsupported;
   if (op.out2 && op.nseg != 2) return kErrUnsupported;  // fused PreAct output: enc1.conv2 program only
   if (op.out32) {
-    // fp32 output (training autocast convs): plain single-segment programs without residuals
-    if (op.res32 || op.res1 || op.res2 || op.out2 || op.nseg != 1 || op.store != kStoreNHWC) return kErrUnsupported;
+    // fp32 output (training autocast convs): plain single-segment programs without
+    // fp16 residuals; an fp32 res32 (an accumulated input gradient) is added in the epilogue
+    if (op.res1 || op.res2 || op.out2 || op.nseg != 1 || op.store != kStoreNHWC) return kErrUnsupported;
+    if (op.res32 && ((uintptr_t)op.res32 % 16 || op.res32_cs % 4)) return kErrUnsupported;
     if (op.img_bias || op.pool || op.scale || op.Kpad % 8 || (uintptr_t)op.out32 % 16 || op.out32_cs % 4 ||
         op.out32_coff % 4)
       return kErrUnsupported;
@@ -1380,6 +1410,11 @@ int launch_conv_ring(const ConvOp& op, hipStream_t st) {
       return ring_relu<kRingS2, 32, 64, kRingOut32>(op, st);
     }
     if (s.stride != 1 || s.Hin != op.Ho || s.Win != op.Wo) return kErrUnsupported;
+    if (op.res32) {
+      // (32-pixel strips: the 64-pixel program with the res32 loads spilled)
+      if (s.C == 32 && op.N == 32) return ring_relu<kRingConv, 32, 32, kRingOut32 | kRingR32>(op, st);
+      return kErrUnsupported;
+    }
     if (s.C == 32 && op.N == 32)
       return op.Wo >= 48 ? ring_relu<kRingConv, 32, 32, kRingWide | kRingOut32>(op, st)
                                         : ring_relu<kRingConv, 32, 32, kRingOut32>(op, st);

@@ -569,6 +569,38 @@ def test_conv_mfma16_1x1_streaming(cin, cout, bias, relu, resid):
         assert torch.equal(y.half().float().view(-1), y16.float())
 
 
+@pytest.mark.parametrize("dil,H,W", [(1, 48, 64), (1, 20, 40), (2, 48, 64)])
+def test_conv_mfma16_3x3_accumulated(dil, H, W):
+    """upr_t_conv_mfma16 on a 32 -> 32 3x3 conv whose fp32 output accumulates
+    into an existing gradient (res == y: the EnhancedFAM branch input
+    gradients, model.py:23-51): dilation 1 on the row ring's fp32 program with
+    the res32 epilogue (round 6; the generic halo kernel before), dilation 2 on
+    the halo kernel; vs fp64 on the fp16-rounded operands, (half)(conv) + res."""
+    import torch.nn.functional as F
+    from upr import _lib as L
+    gen = torch.Generator().manual_seed(dil * 100 + H)
+    B, C = 2, 32
+    x = torch.randn(B, C, H, W, generator=gen)
+    w = torch.randn(C, C, 3, 3, generator=gen) * 0.05
+    r = torch.randn(B, C, H, W, generator=gen)
+    ref = F.conv2d(x.half().double(), w.half().double(), padding=dil, dilation=dil)
+    ref = (ref.float().half().float() + r).permute(0, 2, 3, 1)
+    lib, st = L.lib(), torch.cuda.current_stream().cuda_stream
+    wd = w.to(DEV)
+    wt = torch.empty(w.numel(), device=DEV)
+    assert lib.upr_t_pack_weight(wd.data_ptr(), wt.data_ptr(), C, C, 3, 3, 0, st) == 0  # [Co][(ky, kx, ci)]
+    wt16 = wt.half()
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    y = r.permute(0, 2, 3, 1).contiguous().to(DEV)
+    x16 = torch.empty(B * H * W * C, dtype=torch.float16, device=DEV)
+    y16 = torch.empty(B * H * W * C, dtype=torch.float16, device=DEV)
+    rc = lib.upr_t_conv_mfma16(xd.data_ptr(), B, H, W, C, C, 0, wt16.data_ptr(), None, C, 3, 3, 1, dil, dil,
+                               y.data_ptr(), C, 0, y.data_ptr(), C, 0, 0, x16.data_ptr(), 0, y16.data_ptr(), 0, st)
+    assert rc == 0, rc
+    torch.cuda.synchronize()
+    _close(y, ref, 1e-3, "3x3 accumulated fp32 out")
+
+
 @pytest.mark.parametrize("cin,cout", [(32, 64), (64, 128)])
 def test_dgrad_1x1_stride2_scatter(cin, cout):
     """The projecting shortcut's input gradient (1x1 stride 2, model.py:119-122)
