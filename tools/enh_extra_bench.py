@@ -68,7 +68,7 @@ def main():
     print(json.dumps({"what": "content_aware", "batch": B, "size": S, "ms_per_call": ms, "images_per_s": B / ms * 1e3,
                       "alg_bytes": alg, "achieved_GBs": alg / ms / 1e6, "frac_hbm": alg / ms / 1e6 / PEAK_HBM_GBS,
                       "pass_bytes_per_px": passes, "pass_GBs": passes * px / ms / 1e6,
-                      "kernels": ("ca_sal_fused, reduce_minmax<double>, ca_att4, reduce_minmax<float>, ca_apply4"
+                      "kernels": ("ca_sal_fused, ca_att4, ca_apply4 (each reducing its producer's min / max partials)"
                                   if fused else "ca_lap, ca_gauss_rows, ca_gauss_cols, reduce_minmax<double>, ca_att, "
                                                 "reduce_minmax<float>, ca_apply")}))
     # letterbox: 1920 x 1080 u8 frames -> 640 (the reference default new_shape), auto padding
