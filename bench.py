@@ -204,7 +204,7 @@ def parity_vs_cpu(sd, pre, aspp, x, outs, precision):
 # every kernel launch_conv dispatches to (the bench's conv family = the executor's GEMM ops)
 CONV_KERNELS = ("conv_halo_kernel", "conv_igemm_kernel", "conv_wide_kernel", "conv_wide32_kernel",
                 "conv_ring_kernel", "conv_ring32_kernel", "conv_hwide_kernel", "conv_hwide3_kernel",
-                "conv_hwide4_kernel", "conv_hw2_kernel", "conv_t2_kernel", "conv_t2_f32_kernel")
+                "conv_hwide4_kernel", "conv_t2_kernel", "conv_t2_f32_kernel")
 
 
 def pmc_traffic(precision, variant, batch, size, extra=(), kernels=CONV_KERNELS):
@@ -641,7 +641,7 @@ def train_leg(args, world, rank, dev, B, S, amp, steps, warmup, variant):
 # ----------------------------------------------------------------------------
 # the CLAHE-in-Lab pipeline's kernels (one upr_clahe_enhance call) and the multi-scale ones
 CLAHE_KERNELS = ("clahe_hist_kernel", "clahe_lut_kernel", "clahe_apply_kernel")
-MS_KERNELS = ("ms_sums3_kernel", "ms_sums_kernel", "ms_factor_kernel", "scale_clamp_kernel")
+MS_KERNELS = ("ms_rows_kernel", "ms_sums3_kernel", "ms_fin_kernel", "scale_clamp_kernel")
 
 
 _ENH_DATA = {}
