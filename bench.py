@@ -754,8 +754,9 @@ def enhance_leg(args, world, rank, dev, B, S, traffic, cpu_res):
             "multiscale": {"avg_call_ms": ms_ms, "alg_bytes": ms_bytes,
                            "achieved_GBs": ms_bytes / (ms_ms * 1e-3) / 1e9,
                            "frac": ms_bytes / (ms_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
-                           "kernel": "upr_multiscale: ms_sums3 (all three scales from one read, fp64 per-tile "
-                                     "partials) + ms_fin (adds them in tile order, writes the factor) + scale_clamp",
+                           "kernel": "upr_multiscale: ms_rows (all three scales from one register-streamed read, "
+                                     "fp64 per-wave partials) + ms_fin (adds them in order, writes the factor) + "
+                                     "scale_clamp",
                            "alg_bytes_note": "12 B/px: the fp32 image read once for the three scales' sums + 24 B/px "
                                              "clamp (read enh, write out)"},
         },
