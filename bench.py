@@ -641,7 +641,8 @@ def train_leg(args, world, rank, dev, B, S, amp, steps, warmup, variant):
 # ----------------------------------------------------------------------------
 # the CLAHE-in-Lab pipeline's kernels (one upr_clahe_enhance call) and the multi-scale ones
 CLAHE_KERNELS = ("clahe_hist_kernel", "clahe_lut_kernel", "clahe_apply_kernel")
-MS_KERNELS = ("ms_rows_kernel", "ms_sums3_kernel", "ms_fin_kernel", "scale_clamp_kernel")
+MS_KERNELS = ("ms_rows1_kernel", "ms_rows_kernel", "ms_sums3_kernel", "ms_fin1_kernel", "ms_fin_kernel",
+              "scale_clamp_kernel")
 
 
 _ENH_DATA = {}
@@ -754,9 +755,9 @@ def enhance_leg(args, world, rank, dev, B, S, traffic, cpu_res):
             "multiscale": {"avg_call_ms": ms_ms, "alg_bytes": ms_bytes,
                            "achieved_GBs": ms_bytes / (ms_ms * 1e-3) / 1e9,
                            "frac": ms_bytes / (ms_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
-                           "kernel": "upr_multiscale: ms_rows (all three scales from one register-streamed read, "
-                                     "fp64 per-wave partials) + ms_fin (adds them in order, writes the factor) + "
-                                     "scale_clamp",
+                           "kernel": "upr_multiscale: ms_rows1 (one colour plane per wave, all three scales from one "
+                                     "register-streamed read, fp64 per-wave partials) + ms_fin1 (adds them in order, "
+                                     "writes the sums and the factor) + scale_clamp",
                            "alg_bytes_note": "12 B/px: the fp32 image read once for the three scales' sums + 24 B/px "
                                              "clamp (read enh, write out)"},
         },

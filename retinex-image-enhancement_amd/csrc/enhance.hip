@@ -1094,6 +1094,224 @@ __global__ __launch_bounds__(256, 2) void ms_rows_kernel(const T* __restrict__ x
   if (lane < 3) part[((size_t)b * nwav + wv) * 3 + lane] = lane == 0 ? a0 : lane == 1 ? a1 : a2;
 }
 
+// One CHANNEL per wave (round 6, the default): the register-streaming walk of
+// ms_rows_kernel over one colour plane.  SQ counters on ms_rows_kernel
+// (profiles/r6_ms_rows_sq_counters.txt) showed its waves issue-stalled (47% of
+// their cycles waiting on dependent VALU results, 27% issuing) at two waves
+// per SIMD (256 VGPRs: three planes' windows and loads in flight): with one
+// plane a wave needs a third of the registers, and four-plus waves per SIMD
+// hide each other's dependency chains.  The 7 features of a pixel are summed
+// as sum over channels of (v + |grad v|) plus the luminance, and the
+// luminance's sum is linear in the planes: 0.299f * sum r + 0.587f * sum g +
+// 0.114f * sum b (the sampled half / quarter planes are linear blends too).
+// So a wave keeps, per scale, the sum of v + |grad v| and the sum of v over
+// its pixels (fp32 over a lane's run of a row, fp64 across rows and lanes),
+// and ms_fin1_kernel combines an image's 3 planes in a fixed order.  The
+// rounding differs from ms_rows_kernel's per-pixel fp32 sum of the 7 terms
+// at the 1e-7 relative level (the sums test holds 1e-6 vs the oracle's maps).
+template <int N>
+__device__ __forceinline__ void ms_row_feat1(const float (&c)[N], const float (&u)[N], const float (&d)[N], float l,
+                                             float r, int y, int x, int hs, int ws, double& af, double& av) {
+  if (y < 0 || y >= hs) return;  // (wave-uniform)
+  const bool top = y == 0, bot = y >= hs - 1;
+  float fs = 0.f, vs = 0.f;
+  auto body = [&](auto VB_) {
+    constexpr bool VB = decltype(VB_)::value;  // vertical border row
+    ms_sfor<N>([&](auto K_) {
+      constexpr int k = decltype(K_)::value;
+      float vl, vr;
+      if constexpr (k == 0) vl = l; else vl = c[k - 1];
+      if constexpr (k == N - 1) vr = r; else vr = c[k + 1];
+      const float v = c[k];
+      float gx;
+      if constexpr (k == 0 || k == N - 1) {
+        const bool lft = k == 0 && x == 0, rgt = k == N - 1 && x + k >= ws - 1;
+        const float a = fsel(lft, v, vl), b = fsel(rgt, v, vr);
+        gx = (b - a) * fsel(lft || rgt, 1.f, 0.5f);
+      } else {
+        gx = (vr - vl) * 0.5f;
+      }
+      float gy;
+      if constexpr (VB) {
+        const float uu = fsel(top, v, u[k]), dd = fsel(bot, v, d[k]);
+        gy = (dd - uu) * fsel(top || bot, 1.f, 0.5f);
+      } else {
+        gy = (d[k] - u[k]) * 0.5f;
+      }
+      fs += v + __builtin_amdgcn_sqrtf(gx * gx + gy * gy);
+      vs += v;
+    });
+  };
+  if (top || bot) body(std::true_type{});
+  else body(std::false_type{});
+  if (x < ws) {
+    af += (double)fs;
+    av += (double)vs;
+  }
+}
+
+template <typename T, int BH>
+__global__ __launch_bounds__(256, 4) void ms_rows1_kernel(const T* __restrict__ x, double* __restrict__ part, int B,
+                                                       int H, int W, int strips, int nwav) {
+  constexpr int NR = BH + 6;
+  static_assert(BH % 4 == 0, "bands of whole quarter rows");
+  const int lane = threadIdx.x & 63;
+  const int nb = gridDim.x, bid = blockIdx.x;
+  const int q8 = nb >> 3, r8 = nb & 7, xcd = bid & 7, k8 = bid >> 3;
+  const int blk = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + k8;
+  // global wave = (image * 3 + channel) * nwav + wave (readfirstlane: wave-uniform)
+  const int gw = blk * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int bc = gw / nwav, wv = gw - bc * nwav;
+  if (bc >= 3 * B) return;  // (the last block's spare waves)
+  const int band = wv / strips, strip = wv - band * strips;
+  const int y0 = band * BH, xs = strip * 256, xq = xs + 4 * lane;
+  const int hs1 = H / 2, ws1 = W / 2, hs2 = H / 4, ws2 = W / 4;
+  const size_t HW = (size_t)H * W;
+  const T* plane = x + (size_t)bc * HW;
+  const bool qin = xq < W;
+  const int xe = lane == 0 ? xs - 4 : xs + 256;
+  const bool ein = (lane == 0 || lane == 63) && xe >= 0 && xe < W;
+  float V[NR][4], E[NR][3];
+  // buffer over the plane: off-image lanes read zeros without a memory access
+  // (ms_rows_kernel's scheme, one plane)
+  const int ib = (int)HW * (int)sizeof(T);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)plane, 0, ib, 0x00020000);
+  constexpr int kOff = 0x40000000;
+  const int vq = qin ? xq * (int)sizeof(T) : kOff;
+  const int ve = ein ? (sizeof(T) == 4 && lane == 0 ? xe + 1 : xe) * (int)sizeof(T) : kOff;
+  auto load_row = [&](auto J_) {
+    constexpr int j = decltype(J_)::value;
+    const int y = y0 - 3 + j;
+    const bool yin = y >= 0 && y < H;  // (wave-uniform)
+    const int so = (yin ? y * W : 0) * (int)sizeof(T);
+    const int vqr = yin ? vq : kOff, ver = yin ? ve : kOff;
+    if constexpr (sizeof(T) == 4) {
+      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+      typedef unsigned u32x3 __attribute__((ext_vector_type(3)));
+      const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rs, vqr, so, 0);
+      const u32x3 e = __builtin_amdgcn_raw_buffer_load_b96(rs, ver, so, 0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) V[j][k] = __uint_as_float(q[k]);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) E[j][k] = __uint_as_float(e[k]);
+    } else {
+      typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+      typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+      const h4 hv = __builtin_bit_cast(h4, __builtin_amdgcn_raw_buffer_load_b64(rs, vqr, so, 0));
+      const h4 he = __builtin_bit_cast(h4, __builtin_amdgcn_raw_buffer_load_b64(rs, ver, so, 0));
+#pragma unroll
+      for (int k = 0; k < 4; ++k) V[j][k] = (float)hv[k];
+      const bool l0 = lane == 0;
+      E[j][0] = fsel(l0, (float)he[1], (float)he[0]);
+      E[j][1] = fsel(l0, (float)he[2], (float)he[1]);
+      E[j][2] = fsel(l0, (float)he[3], (float)he[2]);
+    }
+  };
+  float S1[BH / 2 + 2][2], S1e[BH / 2 + 2];
+  float S2[BH / 4 + 2], S2e[BH / 4 + 2];
+  double f0 = 0.0, v0 = 0.0, f1 = 0.0, v1 = 0.0, f2 = 0.0, v2 = 0.0;
+  ms_sfor<MSR_PF + 1>([&](auto J_) { load_row(J_); });
+  ms_sfor<NR>([&](auto J_) {
+    constexpr int j = decltype(J_)::value;
+    asm volatile("" ::: "memory");
+    if constexpr (j + MSR_PF + 1 < NR) load_row(std::integral_constant<int, j + MSR_PF + 1>{});
+    if constexpr (j - 1 >= 3 && j - 1 < BH + 3) {
+      constexpr int m = j - 1;
+      const float l = wave_from_left(V[m][3], E[m][2]), r = wave_from_right(V[m][0], E[m][0]);
+      ms_row_feat1<4>(V[m], V[m - 1], V[m + 1], l, r, y0 - 3 + m, xq, H, W, f0, v0);
+    }
+    if constexpr (j >= 2 && j % 2 == 0) {
+      constexpr int k = (j - 2) / 2;
+      S1[k][0] = blend_half(V[j - 1][0], V[j - 1][1], V[j][0], V[j][1]);
+      S1[k][1] = blend_half(V[j - 1][2], V[j - 1][3], V[j][2], V[j][3]);
+      const bool l0 = lane == 0;
+      S1e[k] = blend_half(fsel(l0, E[j - 1][1], E[j - 1][0]), fsel(l0, E[j - 1][2], E[j - 1][1]),
+                          fsel(l0, E[j][1], E[j][0]), fsel(l0, E[j][2], E[j][1]));
+      if constexpr (k - 1 >= 1 && k - 1 <= BH / 2) {
+        constexpr int m = k - 1;
+        const float l = wave_from_left(S1[m][1], S1e[m]), r = wave_from_right(S1[m][0], S1e[m]);
+        ms_row_feat1<2>(S1[m], S1[m - 1], S1[m + 1], l, r, y0 / 2 - 1 + m, xq / 2, hs1, ws1, f1, v1);
+      }
+    }
+    if constexpr (j % 4 == 1) {
+      constexpr int k = (j - 1) / 4;
+      S2[k] = blend_half(V[j - 1][1], V[j - 1][2], V[j][1], V[j][2]);
+      const bool l0 = lane == 0;
+      S2e[k] = blend_half(fsel(l0, E[j - 1][0], E[j - 1][1]), fsel(l0, E[j - 1][1], E[j - 1][2]),
+                          fsel(l0, E[j][0], E[j][1]), fsel(l0, E[j][1], E[j][2]));
+      if constexpr (k - 1 >= 1 && k - 1 <= BH / 4) {
+        constexpr int m = k - 1;
+        const float l = wave_from_left(S2[m], S2e[m]), r = wave_from_right(S2[m], S2e[m]);
+        const float c1[1] = {S2[m]}, u1[1] = {S2[m - 1]}, d1[1] = {S2[m + 1]};
+        ms_row_feat1<1>(c1, u1, d1, l, r, y0 / 4 - 1 + m, xq / 4, hs2, ws2, f2, v2);
+      }
+    }
+  });
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    f0 += __shfl_xor(f0, o, 64);
+    v0 += __shfl_xor(v0, o, 64);
+    f1 += __shfl_xor(f1, o, 64);
+    v1 += __shfl_xor(v1, o, 64);
+    f2 += __shfl_xor(f2, o, 64);
+    v2 += __shfl_xor(v2, o, 64);
+  }
+  // slot (image, channel, wave): the 3 scales' (sum of v + |grad|, sum of v)
+  if (lane < 6) {
+    const double o = lane == 0 ? f0 : lane == 1 ? v0 : lane == 2 ? f1 : lane == 3 ? v1 : lane == 4 ? f2 : v2;
+    part[(size_t)gw * 6 + lane] = o;
+  }
+}
+
+__device__ __forceinline__ double ms_factor(const double* sums, int b, double n0, double n1, double n2);
+
+// per image: the (channel, wave) slots of ms_rows1_kernel added in a fixed
+// order -- thread t takes waves t, t + 256, ... of every (channel, scale,
+// kind), a fixed tree over the block -- then sum_s = sum_ch F[ch][s] +
+// 0.299f * V[r][s] + 0.587f * V[g][s] + 0.114f * V[b][s] (the luminance
+// weights as the fp32 constants the per-pixel form multiplies by)
+__global__ __launch_bounds__(256) void ms_fin1_kernel(const double* __restrict__ part, int nwav,
+                                                      double* __restrict__ sums, double* __restrict__ factor, double n0,
+                                                      double n1, double n2) {
+  __shared__ double red[18][4];
+  const int b = blockIdx.x, t = threadIdx.x;
+  double a[18];
+#pragma unroll
+  for (int k = 0; k < 18; ++k) a[k] = 0.0;
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch)
+    for (int i = t; i < nwav; i += 256) {
+      const double* p = part + (((size_t)b * 3 + ch) * nwav + i) * 6;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) a[ch * 6 + k] += p[k];
+    }
+  // fixed xor tree within each wave, then the 4 wave sums in order
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int k = 0; k < 18; ++k) a[k] += __shfl_xor(a[k], o, 64);
+  if ((t & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < 18; ++k) red[k][t >> 6] = a[k];
+  __syncthreads();
+  if (t == 0) {
+#pragma unroll
+    for (int k = 0; k < 18; ++k) red[k][0] = ((red[k][0] + red[k][1]) + red[k][2]) + red[k][3];
+    const double wl[3] = {(double)0.299f, (double)0.587f, (double)0.114f};
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      double f = 0.0, l = 0.0;
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {
+        f += red[ch * 6 + 2 * s][0];
+        l += wl[ch] * red[ch * 6 + 2 * s + 1][0];
+      }
+      sums[b * 3 + s] = f + l;
+    }
+    if (factor) factor[b] = ms_factor(sums, b, n0, n1, n2);
+  }
+}
+
 // per image: the tile partials of ms_sums3_kernel added in a fixed order (one
 // block per image; deterministic fp64), then sums and the factor
 __global__ __launch_bounds__(256) void ms_fin_kernel(const double* __restrict__ part, int nblk, double* __restrict__ sums,
@@ -1314,9 +1532,25 @@ int launch_multiscale(const void* x, const void* enh, void* out, double* sums, d
     fac = (double*)scratch(kSlotTmp, sizeof(double) * B, st);
     if (!fac) return (int)hipErrorOutOfMemory;
   }
-  // UPR_MS_ROWS=0: the tiled single pass (ms_sums3_kernel) instead of the register-streaming one (A/B)
-  static const bool rows = [] { const char* e = getenv("UPR_MS_ROWS"); return !e || atoi(e) != 0; }();
-  if (rows && H % 4 == 0 && W % 4 == 0 && (uintptr_t)x % (dtype == kF16 ? 8 : 16) == 0) {
+  // UPR_MS_ROWS=0: the tiled single pass (ms_sums3_kernel); 1: the three-plane
+  // register-streaming walk (ms_rows_kernel); default 2: one plane per wave (A/B)
+  static const int rows = [] { const char* e = getenv("UPR_MS_ROWS"); return e ? atoi(e) : 2; }();
+  if (rows == 2 && H % 4 == 0 && W % 4 == 0 && (uintptr_t)x % (dtype == kF16 ? 8 : 16) == 0) {
+    const int strips = (W + 255) / 256, nwav = strips * ((H + MSR_BH - 1) / MSR_BH);
+    double* part = (double*)scratch(kSlotMs, (size_t)B * 3 * nwav * 6 * sizeof(double), st);
+    if (!part) return (int)hipErrorOutOfMemory;
+    // (bands of 20 / 24 / 32 rows measured the same within noise, profiles/r6_ms_rows1_ab.txt)
+    const int nblk = (B * 3 * nwav + 3) / 4;
+    if (dtype == kF16)
+      hipLaunchKernelGGL((ms_rows1_kernel<half_t, MSR_BH>), dim3(nblk), dim3(256), 0, st, (const half_t*)x, part, B,
+                         H, W, strips, nwav);
+    else
+      hipLaunchKernelGGL((ms_rows1_kernel<float, MSR_BH>), dim3(nblk), dim3(256), 0, st, (const float*)x, part, B, H,
+                         W, strips, nwav);
+    UPR_CHECK_HIP(hipGetLastError());
+    hipLaunchKernelGGL(ms_fin1_kernel, dim3(B), dim3(256), 0, st, (const double*)part, nwav, sums, fac, n0, n1, n2);
+    UPR_CHECK_HIP(hipGetLastError());
+  } else if (rows == 1 && H % 4 == 0 && W % 4 == 0 && (uintptr_t)x % (dtype == kF16 ? 8 : 16) == 0) {
     const int strips = (W + 255) / 256, nwav = strips * ((H + MSR_BH - 1) / MSR_BH);
     double* part = (double*)scratch(kSlotMs, (size_t)B * nwav * 3 * sizeof(double), st);
     if (!part) return (int)hipErrorOutOfMemory;

@@ -90,17 +90,19 @@ def test_content_aware_enhancer():
 
 
 @pytest.mark.parametrize("B,H,W,dtype", [
-    (2, 96, 200, torch.float32),    # partial 32 x 64 tiles, every tile on an image border (reflected gray region)
-    (1, 160, 256, torch.float32),   # interior tiles (the 4-pixel quad loads of the fused saliency pass)
+    (2, 96, 200, torch.float32),    # partial 64 x 64 tiles, every tile on an image border (reflected gray region)
+    (1, 160, 256, torch.float32),   # an interior tile (the 4-pixel quad loads of the fused saliency pass)
+    (1, 272, 328, torch.float32),   # several interior tiles, partial last tile row / column
     (2, 72, 132, torch.float16),    # fp16 storage
     (1, 30, 50, torch.float32),     # smaller than one tile
     (1, 31, 49, torch.float32),     # H * W odd: the three-kernel scalar form
 ])
 def test_content_aware_maps_shapes(B, H, W, dtype):
     """upr_content_aware saliency / attention / output per image vs the oracle
-    (oracle/enhancers.py, image by image): the fused 32 x 64-tile saliency pass
+    (oracle/enhancers.py, image by image): the fused 64 x 64-tile saliency pass
     (gray -> |Laplacian| -> Gaussian rows -> columns in LDS) and the 4-pixel
-    attention / apply passes, or the scalar three-kernel form when H * W % 4."""
+    attention / apply passes (each reducing its producer's per-block min / max
+    partials), or the scalar three-kernel form when H * W % 4."""
     from upr import runtime
     g = torch.Generator().manual_seed(H * W + B)
     x = (torch.rand(B, 3, H, W, generator=g) * 0.6).to(dtype)

@@ -355,8 +355,9 @@ def test_multiscale_kernel(golden):
     (32, 512, 512, torch.float32),  # the bench's enhance leg (images 0 and 31 checked)
 ])
 def test_multiscale_single_pass(B, H, W, dtype):
-    """upr_multiscale's one-pass kernel (ms_rows_kernel: all three scales from
-    one read, per-wave partials added in order by ms_fin_kernel) vs the
+    """upr_multiscale's one-pass kernel (ms_rows1_kernel: all three scales from
+    one read of each colour plane, per-wave partials added in order by
+    ms_fin1_kernel) vs the
     oracle's per-image factor (multi_scale.py:62-100), called three times in a
     row (the three results must be bit-identical)."""
     from upr import runtime
@@ -385,8 +386,9 @@ def test_multiscale_single_pass(B, H, W, dtype):
 ])
 def test_multiscale_sums_vs_feature_maps(B, H, W, dtype):
     """The per-scale feature sums of upr_multiscale's one-pass kernel
-    (ms_rows_kernel: 256-column strips walked row by row in registers, the
-    strip-edge neighbours from the edge lanes' extra quads) against the fp64
+    (ms_rows1_kernel: one colour plane's 256-column strip walked row by row
+    in registers per wave, the strip-edge neighbours from the edge lanes'
+    extra quads; the luminance sum formed from the planes' sums) against the fp64
     sums of the oracle's seven feature maps per scale (multi_scale.py:17-60):
     per pixel the features agree to the gradient magnitude's square root
     (hardware, <= 1 ulp), so the sums to 1e-6 relative -- a wrong neighbour
