@@ -20,6 +20,7 @@ find $out/rp32 -name "*kernel_stats.csv" -exec cp {} $out/fp32_plain_kernel_stat
 find $out/rpe -name "*kernel_stats.csv" -exec cp {} $out/enhance_kernel_stats.csv \; ; find $out/rpt -name "*kernel_stats.csv" -exec cp {} $out/train_kernel_stats.csv \; ; find $out/rpt -name "*kernel_trace.csv" -exec cp {} $out/train_kernel_trace.csv \;
 find $out/rpc -name "*kernel_stats.csv" -exec cp {} $out/ca_kernel_stats.csv \;
 rm -rf $out/rp32 $out/rp16 $out/rpe $out/rpt $out/rpc
+timeout -k 10 300 python bench.py --precision fp16 --variant preact_aspp --no-nested --breakdown --cpu-seconds 0 --no-traffic --detail "" > $out/fp16_layers.json 2> $out/fp16_layers.txt || exit $?
 for s in 256 512; do
   timeout -k 10 300 python tools/harness_bench.py --n 32 --size $s > $out/harness_$s.json 2> $out/harness_$s.err || exit $?
   echo "harness $s $(cat $out/harness_$s.json)"
