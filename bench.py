@@ -681,6 +681,19 @@ def cpu_enhance_baseline(n, size):
                       f"median of {CPU_REPS}"}
 
 
+def _under_profiler():
+    """True under rocprofv3 (its preloaded library initialises the GPU before
+    main()): the child-process legs -- PMC passes, the forked CPU enhancer
+    pool -- are then skipped, since a fork or exec from a GPU-initialised
+    process is not allowed; their results are reported as absent."""
+    return any(k.startswith("ROCPROF") for k in os.environ)
+
+
+_CPU_SKIPPED = {"value": None, "unit": "images/s", "cores": 0, "kind": "port",
+                "sample": "skipped: run under rocprofv3, whose preloaded library initialised the GPU before "
+                          "main() (no forked CPU pool from a GPU-initialised process)"}
+
+
 def cpu_enhance_child(n, size):
     """Run cpu_enhance_baseline in a child process (before this process
     initialises the GPU); None on failure."""
@@ -898,10 +911,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.enhance:
         trE = cpuE = None
-        if world == 1 and not args.no_traffic and not any(k.startswith("ROCPROF") for k in os.environ):
+        if world == 1 and not args.no_traffic and not _under_profiler():
             trE = pmc_traffic("fp32", "plain", args.batch, args.size, ["--enhance"], CLAHE_KERNELS)
         if world == 1 and args.cpu_seconds > 0:
-            cpuE = cpu_enhance_child(args.batch, args.size)
+            cpuE = cpu_enhance_child(args.batch, args.size) if not _under_profiler() else _CPU_SKIPPED
         world, rank, dev = dist_setup(args)
         out = enhance_leg(args, world, rank, dev, args.batch, args.size, trE, cpuE)
         if rank == 0:
@@ -920,14 +933,15 @@ def main():
         return
     nested = not args.no_nested and not (args.precision == "fp16" and args.variant == "preact_aspp")
     traffic = traffic16 = trafficE = cpuE = None
-    if world == 1 and not args.no_traffic and not any(k.startswith("ROCPROF") for k in os.environ):
+    if world == 1 and not args.no_traffic and not _under_profiler():
         # child processes, before this process initialises the GPU
         traffic = pmc_traffic(args.precision, args.variant, args.batch, args.size)
         if nested:
             traffic16 = pmc_traffic("fp16", "preact_aspp", args.batch, args.size)
             trafficE = pmc_traffic("fp32", "plain", args.batch, args.size, ["--enhance"], CLAHE_KERNELS)
     if world == 1 and nested and args.cpu_seconds > 0:
-        cpuE = cpu_enhance_child(args.batch, args.size)  # a process pool: forked before any GPU context exists
+        # a process pool: forked before any GPU context exists (not possible under a profiler)
+        cpuE = cpu_enhance_child(args.batch, args.size) if not _under_profiler() else _CPU_SKIPPED
     world, rank, dev = dist_setup(args)
     B, S = args.batch, args.size
     out = forward_leg(args, world, rank, dev, args.precision, args.variant, B, S, traffic,
