@@ -336,7 +336,7 @@ class Conv:
                                        res.ptr() if res is not None else None, res.cs if res is not None else 0,
                                        int(relu), _fp(out.t), out.cs, out.coff,
                                        store | (2 if keep16 and res is None else 0) |
-                                       (4 if only16 and keep16 and res is None and out16 is None else 0),
+                                       (4 if only16 and keep16 and res is None else 0),
                                        x16p, int(ready), y16p, y16cs, _stream()), "conv_mfma16")
         if out16 is not None:
             out.t16 = None
@@ -364,7 +364,9 @@ class Conv:
         out.fresh = False
         out.t16 = None  # any fp16 copy of an earlier content is stale now
         out.stale32 = False
-        self.only16 = bool(only16 and _AMP[0] and res is None and out.coff == 0 and out.cs == out.C)
+        # (a channel slice of a concat qualifies when its fp16 copy goes to the concat's copy, out16)
+        self.only16 = bool(only16 and _AMP[0] and res is None and
+                           ((out.coff == 0 and out.cs == out.C) or out16 is not None))
         self.amp = _AMP[0] and self.mfma and x_view is None
         # autocast 3 -> 32 / 64 3x3 convs: input gradient on MFMA from an fp16 dy (upr_t_conv_dgrad_c3_16)
         self.dgrad16_c3 = _AMP[0] and self.Cin == 3 and self.Cout in (32, 64) and \
@@ -1230,20 +1232,28 @@ class FAMT:
         # under autocast the four branch convs also write the concat's fp16 copy (the fusion conv's operand)
         cat16 = _h16(B * H * W * 4 * C, dev) if _AMP[0] else None
         o16 = (lambda k: (cat16, k * C, 4 * C)) if cat16 is not None else (lambda k: None)
-        self.b1.fwd(x, out=cat.slice(0, C), out16=o16(0))
+        # fp16-only stores: the concat's fp32 slices are read by nothing when the fusion
+        # conv's weight gradient runs on the fp16 GEMM (it reads cat16), and t3 / t4 by
+        # nothing when branch3 / branch4's second conv's weight gradient does (the ReLU
+        # backward masks with their fp16 copies); the engine asserts on any fp32 read
+        # of a stale activation
+        cat16_only = cat16 is not None and self.fu.wgrad16_ok(W)
+        self.b1.fwd(x, out=cat.slice(0, C), out16=o16(0), only16=cat16_only)
         ok16 = self.b1.wrote16
         self.mp = Act.new(B, H, W, x.C, dev, fresh=False)
         self.mp_code = torch.empty(B * H * W * x.C, dtype=torch.uint8, device=dev)  # argmax codes for the backward
         maxpool_into(x, self.mp, 3, 1, 1, self.mp_code)
-        self.b2.fwd(self.mp, out=cat.slice(C, C), out16=o16(1))
+        self.b2.fwd(self.mp, out=cat.slice(C, C), out16=o16(1), only16=cat16_only)
         ok16 = ok16 and self.b2.wrote16
-        self.t3 = self.b3a.fwd(x, relu=True)
-        self.b3b.fwd(self.t3, out=cat.slice(2 * C, C), out16=o16(2))
+        self.t3 = self.b3a.fwd(x, relu=True, only16=self.b3b.wgrad16_ok(W))
+        self.b3b.fwd(self.t3, out=cat.slice(2 * C, C), out16=o16(2), only16=cat16_only)
         ok16 = ok16 and self.b3b.wrote16
-        self.t4 = self.b4a.fwd(x, relu=True)
-        self.b4b.fwd(self.t4, out=cat.slice(3 * C, C), out16=o16(3))
+        self.t4 = self.b4a.fwd(x, relu=True, only16=self.b4b.wgrad16_ok(W))
+        self.b4b.fwd(self.t4, out=cat.slice(3 * C, C), out16=o16(3), only16=cat16_only)
         ok16 = ok16 and self.b4b.wrote16
+        assert ok16 or not cat16_only, "fp16-only concat slices without the concat's fp16 copy"
         cat.t16 = cat16 if ok16 else None
+        cat.stale32 = bool(ok16 and cat16_only)
         self.o = self.fu.fwd(cat, relu=True)
         self.pool = Act.new(B, 1, 1, C, dev, fresh=False)
         _chk(lib.upr_t_pixel_sum(_fp(self.o.t), B, HW, C, C, 0, ctypes.c_float(1.0 / HW), _fp(self.pool.t), 0, st),
