@@ -490,7 +490,9 @@ class Conv:
         conv whose input needs no gradient (the image stems), the ReLU backward of
         its output y fused into the small-channel weight-gradient kernel (gy is
         left unmasked: this is its only reader)."""
-        if not self.frozen and not (self.mfma and x_view is None) and not gy.stale32 and not y.stale32:
+        # (y.stale32 -- the stem output stored fp16-only -- still takes the stem kernel,
+        # whose mask reads y's fp16 copy; the generic direct kernel reads y in fp32)
+        if not self.frozen and not (self.mfma and x_view is None) and not gy.stale32:
             lib, st = L.lib(), _stream()
             if x_view is not None:
                 xv, B, H, W = x_view
@@ -507,16 +509,18 @@ class Conv:
                     return
                 if rc != L.UPR_ERR_UNSUPPORTED:
                     _chk(rc, "conv_stem_wgrad_relu16")
-            with _timed("direct", "wgrad", self.flops(B, gy.H, gy.W), (self.Cin, self.Cout, self.kh, self.s, H, W)):
-                rc = lib.upr_t_conv_direct_wgrad_relu(ctypes.byref(xv), ctypes.byref(gy.view()),
-                                                      ctypes.byref(y.view()), B, H, W, self.Cin, gy.H, gy.W,
-                                                      self.Cout, self.kh, self.kw, self.s, self.p, self.d,
-                                                      _p(self.m.weight.grad),
-                                                      _p(self.bias.grad) if self.bias is not None else None, st)
-            if rc == 0:
-                return
-            if rc != L.UPR_ERR_UNSUPPORTED:
-                _chk(rc, "conv_direct_wgrad_relu")
+            if not y.stale32:
+                with _timed("direct", "wgrad", self.flops(B, gy.H, gy.W),
+                            (self.Cin, self.Cout, self.kh, self.s, H, W)):
+                    rc = lib.upr_t_conv_direct_wgrad_relu(ctypes.byref(xv), ctypes.byref(gy.view()),
+                                                          ctypes.byref(y.view()), B, H, W, self.Cin, gy.H, gy.W,
+                                                          self.Cout, self.kh, self.kw, self.s, self.p, self.d,
+                                                          _p(self.m.weight.grad),
+                                                          _p(self.bias.grad) if self.bias is not None else None, st)
+                if rc == 0:
+                    return
+                if rc != L.UPR_ERR_UNSUPPORTED:
+                    _chk(rc, "conv_direct_wgrad_relu")
         relu_mask(gy, y)
         self.bwd(x, gy, None, x_view=x_view)
 
@@ -1220,6 +1224,13 @@ class FAMT:
     def convs(self):
         return [self.b1, self.b2, self.b3a, self.b3b, self.b4a, self.b4b, self.fu, self.ca1, self.ca2, self.sa]
 
+    def takes16_input(self, W):
+        """Under autocast, every reader of this module's input x of width W takes its
+        fp16 copy: branch1 / branch3 / branch4's first convs (forward on x.t16, weight
+        gradients on the fp16 GEMM) and the 3x3 max-pool (fp16 path); the input may
+        then be stored fp16-only."""
+        return all(c.wgrad16_ok(W) for c in (self.b1, self.b3a, self.b4a))
+
     def fwd(self, x):
         dev = x.t.device
         lib, st = L.lib(), _stream()
@@ -1242,7 +1253,9 @@ class FAMT:
         ok16 = self.b1.wrote16
         self.mp = Act.new(B, H, W, x.C, dev, fresh=False)
         self.mp_code = torch.empty(B * H * W * x.C, dtype=torch.uint8, device=dev)  # argmax codes for the backward
-        maxpool_into(x, self.mp, 3, 1, 1, self.mp_code)
+        # mp's readers: branch2's conv (forward: its fp16 copy; weight gradient: the fp16
+        # GEMM when wgrad16_ok) -- the backward of the pool itself takes the argmax codes
+        maxpool_into(x, self.mp, 3, 1, 1, self.mp_code, only16=self.b2.wgrad16_ok(W))
         self.b2.fwd(self.mp, out=cat.slice(C, C), out16=o16(1), only16=cat16_only)
         ok16 = ok16 and self.b2.wrote16
         self.t3 = self.b3a.fwd(x, relu=True, only16=self.b3b.wgrad16_ok(W))
@@ -1478,10 +1491,12 @@ class UPRetinexTrainGraph:
                                    H // f // k, W // f // k, st), "maxpool")
             pyr.append(xp)
         self.pyr = pyr
+        # the scale stems' outputs fp16-only where every reader takes fp16 (FAMT.takes16_input;
+        # the stems' own ReLU backward masks with the fp16 copy)
         self.s1 = self.s1c.fwd(None, relu=True, x_view=(xv, B, H, W),
-                               out=Act.new(B, H, W, 32, dev, fresh=False))
+                               out=Act.new(B, H, W, 32, dev, fresh=False), only16=self.s1f.takes16_input(W))
         f1 = self.s1f.fwd(self.s1)
-        self.s2 = self.s2c.fwd(pyr[0], relu=True)
+        self.s2 = self.s2c.fwd(pyr[0], relu=True, only16=self.s2f.takes16_input(pyr[0].W))
         f2 = self.s2f.fwd(self.s2)
         self.s3 = self.s3c.fwd(pyr[1], relu=True)
         f3 = self.s3f.fwd(self.s3)
