@@ -758,6 +758,18 @@ __global__ __launch_bounds__(kRedThreads) void chan_part_kernel(const TA* __rest
       }
     };
     int r = r0 + rg;
+    // one-operand modes (the forward statistics): 8 rows' loads in flight per
+    // thread (4 left the 512^2 statistics passes latency-bound at ~3 TB/s),
+    // then the 4-row batches, then single rows
+    if (!gx) {
+      for (; r + 7 * R < r1; r += 8 * R) {
+        float4 av[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) av[k] = ld4f(ap + (size_t)(r + k * R) * a_cs);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) row(av[k], av[k]);
+      }
+    }
     for (; r + 3 * R < r1; r += 4 * R) {
       float4 av[4], xv[4];
 #pragma unroll
