@@ -160,16 +160,6 @@ __global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(const float* __r
     const float* p = slab + (size_t)co * ldn + k;
     const size_t step = (size_t)Cout * ldn;
     int sp = j;
-    // batches of 16 slabs (four iterations of the 4-slab loop below, the same
-    // order into s[0..3]): 16 loads in flight per row instead of 4 -- the
-    // reduce is latency-bound, one memory round trip per batch
-    for (; sp + 240 < splits; sp += 256) {
-      f32x4_w2 v[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = *(const f32x4_w2*)(p + (size_t)(sp + 16 * u) * step);
-#pragma unroll
-      for (int u = 0; u < 16; ++u) s[u & 3] += v[u];
-    }
     for (; sp + 48 < splits; sp += 64) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) s[u] += *(const f32x4_w2*)(p + (size_t)(sp + 16 * u) * step);
