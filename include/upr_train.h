@@ -249,6 +249,13 @@ int upr_t_bn_stats16_fin(const void* x16, int M, int C, double* acc, float momen
 int upr_t_bn_apply16h(const void* x16, int M, int C, const float* mean, const float* invstd, const float* gamma,
                       const float* beta, const float* res, int res_cs, int res_coff, int res_post, int relu, float* y,
                       int y_cs, int y_coff, void* y16, int skip32, void* stream);
+/* upr_t_bn_apply16h with y16 a channel slice of a wider fp16 copy: y16 points
+ * at the slice's first channel, y16_cs is the copy's channel stride (0: the
+ * compact [M][C] form).  The ASPP concat under autocast (its fusion conv reads
+ * the concat's fp16 copy). */
+int upr_t_bn_apply16h_cs(const void* x16, int M, int C, const float* mean, const float* invstd, const float* gamma,
+                         const float* beta, const float* res, int res_cs, int res_coff, int res_post, int relu,
+                         float* y, int y_cs, int y_coff, void* y16, int y16_cs, int skip32, void* stream);
 /* g16 (nullable): g read from the input-gradient conv's fp16 output instead
  * (compact [M][C]; g / g_cs / g_coff then unused). */
 int upr_t_bn_bwd_fused16(const float* g, const void* g16, int g_cs, int g_coff, const void* x16, const float* mean,
@@ -365,6 +372,10 @@ int upr_t_pixel_sum(const float* x, int B, int HW, int C, int cs, int coff, floa
 /* y[b][p][c] (+)= v[b][c] * scale  (broadcast of a per-image vector). */
 int upr_t_broadcast(const float* v, int B, int HW, int C, float scale, float* y, int y_cs, int y_coff, int accumulate,
                     void* stream);
+/* y16[b][p][y_coff + c] = (half)(v[b][c] * scale): the fp16 form (a channel
+ * slice of an fp16 copy, channel stride y_cs). */
+int upr_t_broadcast16(const float* v, int B, int HW, int C, float scale, void* y16, int y_cs, int y_coff,
+                      void* stream);
 
 /* ---- EnhancedFAM attention (model.py:47-59, 84-97) ---------------------- */
 /* o2 = o*ca[b][c]; m[b][p] = (mean_c o2, max_c o2).  o [B,HW,C] contiguous. */

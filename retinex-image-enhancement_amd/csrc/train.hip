@@ -908,8 +908,10 @@ __global__ __launch_bounds__(256) void bn_apply4_kernel(const TX* __restrict__ x
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, const float* res, int res_cs,
                                                         int res_coff, int res_post, int relu, float* y, int y_cs,
-                                                        int y_coff, half_t* __restrict__ y16, int skip32 = 0) {
+                                                        int y_coff, half_t* __restrict__ y16, int skip32 = 0,
+                                                        int y16_cs = 0) {
   const int C4 = C / 4;
+  const int ycs16 = y16_cs > 0 ? y16_cs : C;  // y16: compact [M][C], or a channel slice of a wider copy
   if (256 % C4 == 0) {
     // this thread's 4 channels are fixed (the grid stride is a multiple of C4):
     // per-channel parameters once, row index by addition -- no div / mod per
@@ -934,7 +936,7 @@ __global__ __launch_bounds__(256) void bn_apply4_kernel(const TX* __restrict__ x
       if (!skip32) *(float4*)(y + (size_t)m * y_cs + y_coff + c) = make_float4(o[0], o[1], o[2], o[3]);
       if (y16) {
         typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-        *(h4*)(y16 + (size_t)m * C + c) = h4{(half_t)o[0], (half_t)o[1], (half_t)o[2], (half_t)o[3]};
+        *(h4*)(y16 + (size_t)m * ycs16 + c) = h4{(half_t)o[0], (half_t)o[1], (half_t)o[2], (half_t)o[3]};
       }
     }
     return;
@@ -958,7 +960,7 @@ __global__ __launch_bounds__(256) void bn_apply4_kernel(const TX* __restrict__ x
     if (!skip32) *(float4*)(y + m * y_cs + y_coff + c) = make_float4(o[0], o[1], o[2], o[3]);
     if (y16) {
       typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-      *(h4*)(y16 + m * C + c) = h4{(half_t)o[0], (half_t)o[1], (half_t)o[2], (half_t)o[3]};
+      *(h4*)(y16 + m * ycs16 + c) = h4{(half_t)o[0], (half_t)o[1], (half_t)o[2], (half_t)o[3]};
     }
   }
 }
@@ -1508,6 +1510,22 @@ __global__ __launch_bounds__(256) void pixel_sum_fin_kernel(const float* __restr
   }
   for (; k < chunks; ++k) t += p[(size_t)k * C];
   out[j] = (accumulate ? out[j] : 0.f) + t * scale;
+}
+
+// the fp16 form: y16[b][p][coff + c] = (half)(v[b][c] * scale), 4 channels per thread
+__global__ void broadcast16_kernel(const float* __restrict__ v, int B, int HW, int C, float scale,
+                                   half_t* __restrict__ y16, int y_cs, int y_coff) {
+  const int C4 = C / 4;
+  const long long n = (long long)B * HW * C4;
+  GSTRIDE(i, n) {
+    const int c = (int)(i % C4) * 4;
+    const long long m = i / C4;
+    const int b = (int)(m / HW);
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    const float* s = v + (size_t)b * C + c;
+    *(h4*)(y16 + m * y_cs + y_coff + c) =
+        h4{(half_t)(s[0] * scale), (half_t)(s[1] * scale), (half_t)(s[2] * scale), (half_t)(s[3] * scale)};
+  }
 }
 
 __global__ void broadcast_kernel(const float* __restrict__ v, int B, int HW, int C, float scale, float* y, int y_cs,
@@ -3138,20 +3156,28 @@ int upr_t_bn_stats16_fin(const void* x16, int M, int C, double* acc, float momen
   LAUNCH_CHECK();
 }
 
-int upr_t_bn_apply16h(const void* x16, int M, int C, const float* mean, const float* invstd, const float* gamma,
-                      const float* beta, const float* res, int res_cs, int res_coff, int res_post, int relu, float* y,
-                      int y_cs, int y_coff, void* y16, int skip32, void* stream) {
+int upr_t_bn_apply16h_cs(const void* x16, int M, int C, const float* mean, const float* invstd, const float* gamma,
+                         const float* beta, const float* res, int res_cs, int res_coff, int res_post, int relu,
+                         float* y, int y_cs, int y_coff, void* y16, int y16_cs, int skip32, void* stream) {
   if (!x16 || !y || !mean || !invstd || !gamma || !beta || M <= 0 || C <= 0) return UPR_ERR_ARG;
   if (skip32 && !y16) return UPR_ERR_ARG;
+  if (y16_cs < 0 || (y16_cs > 0 && y16_cs < C)) return UPR_ERR_ARG;
   const auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
   if (C % 4 || (uintptr_t)x16 % 8 || y_cs % 4 || y_coff % 4 || !a16(y) ||
-      (res && (res_cs % 4 || res_coff % 4 || !a16(res))) || ((uintptr_t)y16 & 7))
+      (res && (res_cs % 4 || res_coff % 4 || !a16(res))) || ((uintptr_t)y16 & 7) || y16_cs % 4)
     return UPR_ERR_UNSUPPORTED;
   const long long n4 = (long long)M * (C / 4);
   hipLaunchKernelGGL(bn_apply4_kernel<half_t>, dim3(grid_for(n4)), dim3(256), 0, ST(stream), (const half_t*)x16, M, C,
                      C, 0, mean, invstd, gamma, beta, res, res_cs, res_coff, res_post, relu, y, y_cs, y_coff,
-                     (half_t*)y16, skip32);
+                     (half_t*)y16, skip32, y16_cs);
   LAUNCH_CHECK();
+}
+
+int upr_t_bn_apply16h(const void* x16, int M, int C, const float* mean, const float* invstd, const float* gamma,
+                      const float* beta, const float* res, int res_cs, int res_coff, int res_post, int relu, float* y,
+                      int y_cs, int y_coff, void* y16, int skip32, void* stream) {
+  return upr_t_bn_apply16h_cs(x16, M, C, mean, invstd, gamma, beta, res, res_cs, res_coff, res_post, relu, y, y_cs,
+                              y_coff, y16, 0, skip32, stream);
 }
 
 int upr_t_bn_bwd_fused16(const float* g, const void* g16, int g_cs, int g_coff, const void* x16, const float* mean,
@@ -3804,6 +3830,16 @@ int upr_t_broadcast(const float* v, int B, int HW, int C, float scale, float* y,
   const long long n = (long long)B * HW * C;
   hipLaunchKernelGGL(broadcast_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), v, B, HW, C, scale, y, y_cs,
                      y_coff, accumulate);
+  LAUNCH_CHECK();
+}
+
+int upr_t_broadcast16(const float* v, int B, int HW, int C, float scale, void* y16, int y_cs, int y_coff,
+                      void* stream) {
+  if (!v || !y16 || B <= 0 || HW <= 0 || C <= 0 || y_cs < y_coff + C) return UPR_ERR_ARG;
+  if (C % 4 || y_cs % 4 || y_coff % 4 || (uintptr_t)y16 % 8) return UPR_ERR_UNSUPPORTED;
+  const long long n = (long long)B * HW * (C / 4);
+  hipLaunchKernelGGL(broadcast16_kernel, dim3(grid_for(n)), dim3(256), 0, ST(stream), v, B, HW, C, scale,
+                     (half_t*)y16, y_cs, y_coff);
   LAUNCH_CHECK();
 }
 

@@ -156,6 +156,7 @@ SIGNATURES.update({
     "upr_t_bn_stats16": (_i, [_p, _i, _i, _p, _p]),
     "upr_t_bn_stats16_fin": (_i, [_p, _i, _i, _p, _f, _f, _p, _p, _p, _p, _p, _p]),
     "upr_t_bn_apply16h": (_i, [_p, _i, _i, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _i, _i, _p, _i, _p]),
+    "upr_t_bn_apply16h_cs": (_i, [_p, _i, _i, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _i, _i, _p, _i, _i, _p]),
     "upr_t_bn_bwd_fused16": (_i, [_p, _p, _i, _i, _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _i, _i, _i, _i,
                                   _p, _i, _p]),
     "upr_t_chan_sum16": (_i, [_p, _i, _i, _p, _i, _p, _p]),
@@ -181,6 +182,7 @@ SIGNATURES.update({
     "upr_t_bilinear_bwd": (_i, [_vp, _i, _i, _i, _i, _i, _i, _vp, _p]),
     "upr_t_pixel_sum": (_i, [_p, _i, _i, _i, _i, _i, _f, _p, _i, _p]),
     "upr_t_broadcast": (_i, [_p, _i, _i, _i, _f, _p, _i, _i, _i, _p]),
+    "upr_t_broadcast16": (_i, [_p, _i, _i, _i, _f, _p, _i, _i, _p]),
     "upr_t_fam_ca_apply": (_i, [_p, _p, _i, _i, _i, _p, _p, _p]),
     "upr_t_fam_sa_apply": (_i, [_p, _p, _i, _i, _i, _p, _p, _p]),
     "upr_t_fam_sa_bwd": (_i, [_p, _p, _p, _i, _i, _i, _p, _p, _p]),

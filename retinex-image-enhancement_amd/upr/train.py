@@ -65,6 +65,13 @@ def empty(shape, dev):
 _AMP = [False]
 
 
+# fp16-only activation stores (the FAM / ASPP concats, FAM branch and pool
+# outputs, scale stems) where no reader needs the fp32 value; False writes the
+# fp32 values too (the gradients must not change: tests/test_gpu_train.py
+# test_amp_fp16_only_stores_bitwise)
+FP16_ONLY_STORES = [True]
+
+
 def autocast_active():
     """True inside torch.autocast('cuda') (any half dtype: the kernels compute fp16)."""
     try:
@@ -780,10 +787,14 @@ class BN:
         # per-channel sums + the two-stage reduction's partial slots (upr_t_reduce_acc_doubles)
         self.acc = torch.empty((L.lib().upr_t_reduce_acc_doubles(self.C),), dtype=torch.float64, device=dev)
 
-    def fwd(self, x, relu=False, out=None, res=None, res_post=False, only16=False):
+    def fwd(self, x, relu=False, out=None, res=None, res_post=False, only16=False, out16=None):
         """only16: under autocast every reader of the output takes its fp16 copy (convs
         whose weight gradients run on the fp16-operand GEMM): the fp32 output is not
-        written (out.stale32)."""
+        written (out.stale32).  out16 = (fp16 tensor, channel offset, channel stride):
+        `out` is a channel slice of a concat whose fp16 copy the caller assembles; the
+        slice's fp16 values go there (and with only16 its fp32 values are not written);
+        self.wrote16 tells whether they did."""
+        self.wrote16 = False
         lib, st = L.lib(), _stream()
         m = self.m
         # under autocast x is an fp16 conv's output: its fp16 copy holds the same values
@@ -809,6 +820,26 @@ class BN:
                                          _p(self.mean), _p(self.invstd), st), "bn_eval_stats")
         if out is None:
             out = Act.new(x.B, x.H, x.W, self.C, x.t.device, fresh=False)
+        if out16 is not None and _AMP[0] and x16 is not None and res is None:
+            # a concat slice: fp16 values into the caller's copy (no fallback: the fp16
+            # input path always exists here, and a half-written copy must not be claimed)
+            t16, c16, cs16 = out16
+            skip32 = int(bool(only16))
+            _chk(lib.upr_t_bn_apply16h_cs(_p(x16), x.M, self.C, _p(self.mean), _p(self.invstd), _p(m.weight),
+                                          _p(m.bias), None, 0, 0, 0, int(relu), _fp(out.t), out.cs, out.coff,
+                                          ctypes.c_void_p(t16.data_ptr() + 2 * c16), cs16, skip32, st),
+                 "bn_apply16h_cs")
+            self.wrote16 = True
+            out.t16 = None
+            # (the slice object; the caller marks the concat.  An unfused backward that
+            # would mask with this output refuses a stale one, below in bwd)
+            out.stale32 = bool(skip32)
+            self.x = x
+            self.out_act = out
+            self.batch_stats = bool(m.training)
+            self.relu_only = bool(relu)
+            self.has_res = False
+            return out
         # under autocast the consumer is an fp16 conv: write its fp16 input copy here
         y16 = _h16(out.M * self.C, out.t.device) if _AMP[0] and out.coff == 0 and out.cs == self.C else None
         rc = L.UPR_ERR_UNSUPPORTED
@@ -884,6 +915,9 @@ class BN:
             if self.has_res:
                 raise NotImplementedError("unfused ReLU backward of relu(bn(x)) + skip: the mask needs the "
                                           "pre-residual value (the fused BatchNorm backward takes this layer)")
+            if self.out_act.stale32:
+                raise NotImplementedError("unfused ReLU backward of an fp16-only BatchNorm output: the mask "
+                                          "needs the fp32 value (the fused BatchNorm backward takes this layer)")
             relu_mask(g, self.out_act)
         zero(self.acc[:2 * self.C])
         _chk(lib.upr_t_bn_bwd_reduce(_fp(g.t), g.cs, g.coff, x.ptr(), x.cs, 0, _p(self.mean), _p(self.invstd), x.M,
@@ -1119,16 +1153,31 @@ class ASPPT:
         self.x = x
         cat = Act.new(x.B, x.H, x.W, C * nb, dev, fresh=False)
         self.cat = cat
-        self.b1.fwd(self.c1.fwd(x, only16=True), relu=True, out=cat.slice(0, C))
-        for i, (cv, bn) in enumerate(self.br):
-            bn.fwd(cv.fwd(x, only16=True), relu=True, out=cat.slice(C * (i + 1), C))
+        # under autocast the branch BatchNorms and the global broadcast also write the
+        # concat's fp16 copy (the fusion conv's operand); only that copy when the fusion
+        # conv's weight gradient reads it too (the branch BatchNorm backwards recompute
+        # their ReLU masks from their inputs: nothing else reads the concat)
+        cat16 = _h16(cat.M * C * nb, dev) if _AMP[0] else None
+        only = FP16_ONLY_STORES[0] and cat16 is not None and self.fc.wgrad16_ok(x.W)
+        o16 = (lambda k: (cat16, C * k, C * nb)) if cat16 is not None else (lambda k: None)
+        ok16 = cat16 is not None
+        for i, (cv, bn) in enumerate([(self.c1, self.b1)] + self.br):
+            bn.fwd(cv.fwd(x, only16=True), relu=True, out=cat.slice(C * i, C), out16=o16(i), only16=only)
+            ok16 = ok16 and bn.wrote16
+        assert ok16 or not only, "fp16-only ASPP concat slices without the concat's fp16 copy"
         # global branch: mean -> 1x1 -> BN (over the batch) -> ReLU -> broadcast
         self.gm = Act.new(x.B, 1, 1, x.C, dev, fresh=False)
         _chk(L.lib().upr_t_pixel_sum(x.ptr(), x.B, x.H * x.W, x.C, x.cs, 0, ctypes.c_float(1.0 / (x.H * x.W)),
                                      _fp(self.gm.t), 0, _stream()), "gap")
         self.gp = self.gb.fwd(self.gc.fwd(self.gm), relu=True)
-        _chk(L.lib().upr_t_broadcast(_fp(self.gp.t), x.B, x.H * x.W, C, ctypes.c_float(1.0), _fp(cat.t), cat.cs,
-                                     C * (nb - 1), 0, _stream()), "broadcast")
+        if not only:
+            _chk(L.lib().upr_t_broadcast(_fp(self.gp.t), x.B, x.H * x.W, C, ctypes.c_float(1.0), _fp(cat.t), cat.cs,
+                                         C * (nb - 1), 0, _stream()), "broadcast")
+        if ok16:
+            _chk(L.lib().upr_t_broadcast16(_fp(self.gp.t), x.B, x.H * x.W, C, ctypes.c_float(1.0), _p(cat16),
+                                           C * nb, C * (nb - 1), _stream()), "broadcast16")
+        cat.t16 = cat16 if ok16 else None
+        cat.stale32 = bool(only)
         self.a = self.fb.fwd(self.fc.fwd(cat, only16=True), relu=True)
         self.dropped = self.training  # the backward applies the mask only when this forward drew one
         if not self.dropped:
@@ -1229,7 +1278,7 @@ class FAMT:
         fp16 copy: branch1 / branch3 / branch4's first convs (forward on x.t16, weight
         gradients on the fp16 GEMM) and the 3x3 max-pool (fp16 path); the input may
         then be stored fp16-only."""
-        return all(c.wgrad16_ok(W) for c in (self.b1, self.b3a, self.b4a))
+        return FP16_ONLY_STORES[0] and all(c.wgrad16_ok(W) for c in (self.b1, self.b3a, self.b4a))
 
     def fwd(self, x):
         dev = x.t.device
@@ -1248,20 +1297,20 @@ class FAMT:
         # nothing when branch3 / branch4's second conv's weight gradient does (the ReLU
         # backward masks with their fp16 copies); the engine asserts on any fp32 read
         # of a stale activation
-        cat16_only = cat16 is not None and self.fu.wgrad16_ok(W)
+        cat16_only = FP16_ONLY_STORES[0] and cat16 is not None and self.fu.wgrad16_ok(W)
         self.b1.fwd(x, out=cat.slice(0, C), out16=o16(0), only16=cat16_only)
         ok16 = self.b1.wrote16
         self.mp = Act.new(B, H, W, x.C, dev, fresh=False)
         self.mp_code = torch.empty(B * H * W * x.C, dtype=torch.uint8, device=dev)  # argmax codes for the backward
         # mp's readers: branch2's conv (forward: its fp16 copy; weight gradient: the fp16
         # GEMM when wgrad16_ok) -- the backward of the pool itself takes the argmax codes
-        maxpool_into(x, self.mp, 3, 1, 1, self.mp_code, only16=self.b2.wgrad16_ok(W))
+        maxpool_into(x, self.mp, 3, 1, 1, self.mp_code, only16=FP16_ONLY_STORES[0] and self.b2.wgrad16_ok(W))
         self.b2.fwd(self.mp, out=cat.slice(C, C), out16=o16(1), only16=cat16_only)
         ok16 = ok16 and self.b2.wrote16
-        self.t3 = self.b3a.fwd(x, relu=True, only16=self.b3b.wgrad16_ok(W))
+        self.t3 = self.b3a.fwd(x, relu=True, only16=FP16_ONLY_STORES[0] and self.b3b.wgrad16_ok(W))
         self.b3b.fwd(self.t3, out=cat.slice(2 * C, C), out16=o16(2), only16=cat16_only)
         ok16 = ok16 and self.b3b.wrote16
-        self.t4 = self.b4a.fwd(x, relu=True, only16=self.b4b.wgrad16_ok(W))
+        self.t4 = self.b4a.fwd(x, relu=True, only16=FP16_ONLY_STORES[0] and self.b4b.wgrad16_ok(W))
         self.b4b.fwd(self.t4, out=cat.slice(3 * C, C), out16=o16(3), only16=cat16_only)
         ok16 = ok16 and self.b4b.wrote16
         assert ok16 or not cat16_only, "fp16-only concat slices without the concat's fp16 copy"

@@ -1617,3 +1617,42 @@ def test_mse16_matches_fp32_mse(n):
     # unsupported layouts decline instead of computing
     assert lib.upr_t_mse16(a16.data_ptr(), b16.data_ptr(), n - 1, acc.data_ptr(), None, ctypes.c_float(1.0),
                            st) == L.UPR_ERR_UNSUPPORTED
+
+
+def test_amp_fp16_only_stores_bitwise():
+    """The autocast step's fp16-only activation stores (upr/train.py
+    FP16_ONLY_STORES: the EnhancedFAM and ASPP concats, the FAM branch / pool
+    outputs, the scale stems) only skip fp32 values nothing reads: the
+    parameter gradients and loss terms of a preact+ASPP step at 512^2 (every
+    store form active: widths multiples of 64 at the FAM and the ASPP) are
+    bit-identical with the stores on and off."""
+    from losses.loss import TotalLoss
+    from upr import train as T
+
+    def step(only):
+        T.FP16_ONLY_STORES[0] = only
+        try:
+            torch.manual_seed(11)
+            model = _model(True, True, seed=3).to(DEV).train()
+            crit = TotalLoss(use_freq_loss=True).to(DEV)
+            x = (torch.rand(2, 3, 512, 512, generator=torch.Generator().manual_seed(6)) * 0.6).to(DEV)
+            with torch.autocast("cuda", dtype=torch.float16):
+                enh, refl, illu = model(x)
+                total, d = crit(x, enh, illu, refl)
+            total.backward()
+            torch.cuda.synchronize()
+            g = model.__dict__["_upr_train"]["graph"]
+            asp = [b for b in g.ie.mid if type(b).__name__ == "ASPPT"][0]
+            stale = (asp.cat.stale32, g.s1f.cat.stale32)
+            grads = {n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None}
+            return float(total), grads, stale
+        finally:
+            T.FP16_ONLY_STORES[0] = True
+
+    l1, g1, st1 = step(True)
+    l0, g0, st0 = step(False)
+    assert st1 == (True, True) and st0 == (False, False), (st1, st0)
+    assert l1 == l0
+    assert g1.keys() == g0.keys() and len(g1) > 0
+    for n in g1:
+        assert torch.equal(g1[n], g0[n]), n
