@@ -16,6 +16,8 @@ Parameters and their gradients live in ONE flat fp32 buffer each
 (`FlatParams`), so clip_grad_norm_ and Adam are single launches.
 """
 import ctypes
+import os
+import sys
 
 import torch
 
@@ -69,6 +71,7 @@ _AMP = [False]
 # outputs, scale stems) where no reader needs the fp32 value; False writes the
 # fp32 values too (the gradients must not change: tests/test_gpu_train.py
 # test_amp_fp16_only_stores_bitwise)
+_TRACE_CAST = os.environ.get("UPR_TRACE_CAST", "0") == "1"
 FP16_ONLY_STORES = [True]
 
 
@@ -329,6 +332,8 @@ class Conv:
         ready = x16 is not None
         if not ready:
             x16 = _h16(B * H * W * C, dev)
+            if _TRACE_CAST:  # UPR_TRACE_CAST=1: name the convs whose fp16 operand is cast here
+                print(f"upr_cast conv {C}->{N} k{kh} s{s} {H}x{W} B{B}", file=sys.stderr)
         # x16_strided: x16 is the shared fp16 copy of the concat x is a slice of (channel stride cs)
         x16p = ctypes.c_void_p(x16.data_ptr() + 2 * coff) if x16_strided else _p(x16)
         if x16_strided:
