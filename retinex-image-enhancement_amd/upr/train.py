@@ -333,7 +333,9 @@ class Conv:
         if not ready:
             x16 = _h16(B * H * W * C, dev)
             if _TRACE_CAST:  # UPR_TRACE_CAST=1: name the convs whose fp16 operand is cast here
-                print(f"upr_cast conv {C}->{N} k{kh} s{s} {H}x{W} B{B}", file=sys.stderr)
+                import traceback
+                where = " < ".join(f"{f.name}:{f.lineno}" for f in traceback.extract_stack()[-5:-1][::-1])
+                print(f"upr_cast conv {C}->{N} k{kh} s{s} {H}x{W} B{B} at {where}", file=sys.stderr)
         # x16_strided: x16 is the shared fp16 copy of the concat x is a slice of (channel stride cs)
         x16p = ctypes.c_void_p(x16.data_ptr() + 2 * coff) if x16_strided else _p(x16)
         if x16_strided:
