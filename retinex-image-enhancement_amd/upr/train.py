@@ -1444,7 +1444,9 @@ class IENetT:
             return Act.new(a.B, a.H, a.W, a.C, dev)
         g_h = like(self.h)
         self.h2.bwd(self.h, g_r, g_h)
-        relu_mask(g_h, self.h)
+        # under autocast the masked gradient's fp16 copy (h0's input-gradient / weight-
+        # gradient operand) comes out of the mask pass, not a separate cast
+        relu_mask(g_h, self.h, want16=self.h0.amp and self.h0.mfma)
         g_d1 = like(self.d1)
         self.h0.bwd(self.d1, g_h, g_d1)
         g_x1, g_x2, g_x3 = like(self.x1), like(self.x2), like(self.x3)
